@@ -1,0 +1,174 @@
+/*
+ * sgn_hip.h -- C ABI of libsgn_hip.so, the MI355X (gfx950) implementation of
+ * the SG-NeRF / Point-NeRF per-ray rendering hot path:
+ *
+ *     neural-point grid  ->  ray march + shading-sample selection + layered kNN
+ *     ->  per-neighbour aggregator MLP (MFMA)  ->  colour MLP  ->  alpha composite
+ *
+ * Every pointer named d_* is a DEVICE pointer owned by the caller (torch
+ * tensors on the Python side); the library never allocates on the per-frame
+ * path (sgn_query / sgn_aggregate / sgn_composite).  Only sgn_grid_build
+ * allocates (once per point-cloud version) and sgn_grid_free releases.
+ * Every call takes an explicit hipStream_t and is asynchronous w.r.t. the host
+ * unless stated.  Return value: 0 on success, < 0 on error; sgn_last_error()
+ * gives a message for the calling thread.
+ *
+ * Reference interfaces replaced (file:line in Quyans/SG-NeRF):
+ *   sgn_grid_build   <- lighting_fast_querier.build_occ_vox
+ *                       models/neural_points/query_point_indices_worldcoords.py:706-778
+ *                       (claim_occ :265, map_coor2occ :328, fill_occ2pnts :365)
+ *                       -- hoisted out of the per-chunk call (:797) and cached.
+ *   sgn_query        <- lighting_fast_querier.query_grid_point_index :782-954
+ *                       (mask_raypos :413, get_shadingloc :439,
+ *                        query_neigh_along_ray_layered[_semantic_guidance] :594 / :489)
+ *   sgn_aggregate    <- NeuralPoints.forward gather  neural_points.py:942-988
+ *                       + PointAggregator.forward / viewmlp
+ *                       models/aggregators/point_aggregators.py:868-959 / :561-786
+ *   sgn_composite    <- NeuralPointsRayMarching.forward ray_dist + ray_march + fill_invalid
+ *                       models/neural_points_volumetric_model.py:569-631, :158-195
+ *                       models/rendering/diff_ray_marching.py:509-555
+ */
+#ifndef SGN_HIP_H
+#define SGN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
+typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
+
+#define SGN_ABI_VERSION 1
+
+/* ---- grid ------------------------------------------------------------- */
+
+typedef struct {
+    float shift[3];      /* ranges[:3] after padding, fp32          (worldcoords.py:79,793) */
+    float vs[3];         /* scaled voxel size = fl32(vsize*vscale)   (:73) */
+    int32_t dims[3];     /* scaled_vdim                              (:86) */
+    int32_t kernel[3];   /* kernel_size: layered kNN search extent   (:635) */
+    int32_t query[3];    /* query_size: occupancy-flag neighbourhood (:797) */
+    int32_t max_o;       /* max occupied voxels                      (:307) */
+    int32_t P;           /* max points per voxel                     (:398) */
+    int32_t fix_occ0;    /* 0 = reproduce `voxel_idx > 0` (:395); 1 = fixed */
+    uint64_t seed;       /* reservoir seed (reference: wall clock)   (:314,:402) */
+} sgn_grid_params;
+
+typedef struct {
+    int64_t n_points;    /* points given to the build */
+    int64_t n_claimed;   /* occupied voxels (= reference occ_idx, may exceed max_o) */
+    int64_t n_slots;     /* min(n_claimed, max_o) */
+    int64_t n_listed;    /* points kept in per-voxel lists (sum of min(P, count)) */
+    int64_t volume;      /* dims[0]*dims[1]*dims[2] */
+    int64_t device_bytes;
+} sgn_grid_info;
+
+/* Builds the grid.  Synchronises `stream` twice (sizes read back). */
+int sgn_grid_build(const float *d_points, int64_t n_points, const sgn_grid_params *params,
+                   sgn_stream_t stream, sgn_grid **out_grid);
+int sgn_grid_free(sgn_grid *grid);
+int sgn_grid_get_info(const sgn_grid *grid, sgn_grid_info *out);
+/* Writes the reference's own grid structures (for parity tests):
+ * coor_occ/coor_2_occ int32[volume], occ_numpnts int32[max_o], occ_2_pnts int32[max_o*P]. */
+int sgn_grid_export(const sgn_grid *grid, int32_t *d_coor_occ, int32_t *d_coor_2_occ,
+                    int32_t *d_occ_numpnts, int32_t *d_occ_2_pnts, sgn_stream_t stream);
+
+/* ---- query ------------------------------------------------------------ */
+
+typedef struct {
+    int32_t SR;          /* max shading samples per ray  (<= 128) */
+    int32_t K;           /* neighbours per sample        (<= 16)  */
+    int32_t D;           /* candidate depths per ray (z_depth_dim) */
+    int32_t per_ray_t;   /* 0: t_table is [D]; 1: t_table is [R, D] (jittered training rays) */
+    float r2;            /* np.float32(radius_limit ** 2); 0 disables the radius test */
+    int32_t dense_out;   /* 0: pidx indexed by sample; 1: by ray*SR+slot (reference layout) */
+    int32_t semantic;    /* 1: semantic-guidance filter (:489-591) */
+    uint64_t seconds;    /* wall-clock value the semantic filter reads (:553) */
+} sgn_query_params;
+
+/* Sample-major outputs of one query call (all device, caller-allocated,
+ * capacity R*SR samples unless noted):
+ *   ray_ns    int32[R]        selected shading samples per ray (<= SR)
+ *   ray_soff  int32[R]        exclusive prefix sum of ray_ns (first sample id of the ray)
+ *   samp_ray  int32[S]        ray of each sample
+ *   samp_d    int32[S]        candidate depth index of each sample
+ *   samp_locw float[S*3]      sample position (world)
+ *   samp_nnb  int32[S]        valid neighbours of the sample (0..K)
+ *   pidx      int32[S*K] or [R*SR*K] (dense_out; caller pre-fills -1)
+ *   work      int32[S]        ids of samples with samp_nnb > 0 (unordered)
+ *   counters  int32[4]        [0] = S (total samples), [1] = work items
+ */
+typedef struct {
+    int32_t *ray_ns, *ray_soff, *samp_ray, *samp_d, *samp_nnb, *pidx, *work, *counters;
+    float *samp_locw;
+} sgn_query_out;
+
+size_t sgn_query_workspace_bytes(int64_t R);
+int sgn_query(const sgn_grid *grid, const sgn_query_params *qp, const float *d_campos,
+              const float *d_raydir, int64_t R, const float *d_t_table,
+              const int32_t *d_point_labels, const int32_t *d_ray_labels,
+              const sgn_query_out *out, void *d_workspace, size_t workspace_bytes,
+              sgn_stream_t stream);
+
+/* ---- aggregator (per-neighbour MLP + K-blend, colour MLP) -------------- */
+
+/* Size in bytes of the packed fp16 weight blob for the ScanNet-layout viewmlp
+ * (block1 284->256->256, block3 263->256->256, alpha 256->1, colour 280->128x3->3). */
+size_t sgn_mlp_packed_bytes(void);
+/* Packs fp32 nn.Linear weights (row-major [out][in]) + biases into the
+ * MFMA fragment-major fp16 layout.  Host pointers in, device pointer out
+ * (synchronous copy). Order of `w`/`b`: block1.0, block1.2, block3.0,
+ * block3.2, alpha_branch.0, color_branch.0, .2, .4, .6 (9 layers). */
+int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed,
+                 sgn_stream_t stream);
+
+typedef struct {
+    /* point tables, row = neural point index */
+    const float *xyz;        /* [N,3]  */
+    const float *embedding;  /* [N,32] */
+    const float *color;      /* [N,3]  */
+    const float *dir;        /* [N,3]  */
+    const float *conf;       /* [N]    */
+    int64_t n_points;
+    /* camera */
+    const float *campos;     /* [3] */
+    const float *camrotc2w;  /* [3,3] row-major */
+    const float *raydir;     /* [R,3] */
+} sgn_point_tables;
+
+/* out_feat: float4[S] = [alpha_s, r, g, b] for every sample id (samples with
+ * no valid neighbour are written as zeros); also writes out_blend (optional,
+ * may be NULL) float[S*K] = normalised weight * conf (reference `weight*conf_coefficient`). */
+size_t sgn_aggregate_workspace_bytes(int64_t S);
+int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
+                  int32_t K, const void *d_packed_mlp, float *d_out_feat, float *d_out_blend,
+                  void *d_workspace, size_t workspace_bytes, sgn_stream_t stream);
+
+/* ---- composite --------------------------------------------------------- */
+
+typedef struct {
+    int32_t SR;
+    float vsize_z;        /* vsize[2] (0.008): last-interval / replacement distance */
+    int32_t raydist_mode_unit;
+    float bg[3];          /* bg_color (tone map off) */
+} sgn_composite_params;
+
+/* Per ray: out_rgb float[R*3] (bg for invalid rays), out_mask int8[R]
+ * (reference ray_mask after masked_valid_ray), out_bgT float[R] (background
+ * transmission; 1 for invalid rays), out_opacity float[R*SR] (may be NULL). */
+int sgn_composite(const sgn_composite_params *cp, const float *d_campos, const float *d_camrotc2w,
+                  const float *d_raydir, int64_t R, const float *d_t_table, int32_t per_ray_t,
+                  int32_t D, const sgn_query_out *q, const float *d_feat, float *d_out_rgb,
+                  int8_t *d_out_mask, float *d_out_bgT, float *d_out_opacity, sgn_stream_t stream);
+
+/* ---- misc -------------------------------------------------------------- */
+int sgn_abi_version(void);
+const char *sgn_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGN_HIP_H */

@@ -1,0 +1,116 @@
+"""ctypes binding of libsgn_hip.so (C ABI: include/sgn_hip.h).
+
+This is the only place the HIP library is loaded.  There is no fallback: if the
+library is missing or a call fails, an exception is raised.  Pointers passed in
+are raw device addresses of torch tensors (``tensor.data_ptr()``) and the
+stream is ``torch.cuda.current_stream().cuda_stream``.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
+ABI_VERSION = 1
+
+c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
+                                         ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
+
+
+class GridParams(ctypes.Structure):
+    _fields_ = [("shift", c_f32 * 3), ("vs", c_f32 * 3), ("dims", c_i32 * 3),
+                ("kernel", c_i32 * 3), ("query", c_i32 * 3), ("max_o", c_i32), ("P", c_i32),
+                ("fix_occ0", c_i32), ("seed", c_u64)]
+
+
+class GridInfo(ctypes.Structure):
+    _fields_ = [("n_points", c_i64), ("n_claimed", c_i64), ("n_slots", c_i64),
+                ("n_listed", c_i64), ("volume", c_i64), ("device_bytes", c_i64)]
+
+
+class QueryParams(ctypes.Structure):
+    _fields_ = [("SR", c_i32), ("K", c_i32), ("D", c_i32), ("per_ray_t", c_i32), ("r2", c_f32),
+                ("dense_out", c_i32), ("semantic", c_i32), ("seconds", c_u64)]
+
+
+class QueryOut(ctypes.Structure):
+    _fields_ = [("ray_ns", c_vp), ("ray_soff", c_vp), ("samp_ray", c_vp), ("samp_d", c_vp),
+                ("samp_nnb", c_vp), ("pidx", c_vp), ("work", c_vp), ("counters", c_vp),
+                ("samp_locw", c_vp)]
+
+
+class PointTables(ctypes.Structure):
+    _fields_ = [("xyz", c_vp), ("embedding", c_vp), ("color", c_vp), ("dir", c_vp),
+                ("conf", c_vp), ("n_points", c_i64), ("campos", c_vp), ("camrotc2w", c_vp),
+                ("raydir", c_vp)]
+
+
+class CompositeParams(ctypes.Structure):
+    _fields_ = [("SR", c_i32), ("vsize_z", c_f32), ("raydist_mode_unit", c_i32), ("bg", c_f32 * 3)]
+
+
+# name -> (restype, argtypes); every symbol include/sgn_hip.h declares.
+SIGNATURES = {
+    "sgn_abi_version": (c_i32, []),
+    "sgn_last_error": (ctypes.c_char_p, []),
+    "sgn_grid_build": (c_i32, [c_vp, c_i64, ctypes.POINTER(GridParams), c_vp, ctypes.POINTER(c_vp)]),
+    "sgn_grid_free": (c_i32, [c_vp]),
+    "sgn_grid_get_info": (c_i32, [c_vp, ctypes.POINTER(GridInfo)]),
+    "sgn_grid_export": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_query_workspace_bytes": (c_sz, [c_i64]),
+    "sgn_query": (c_i32, [c_vp, ctypes.POINTER(QueryParams), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                          ctypes.POINTER(QueryOut), c_vp, c_sz, c_vp]),
+    "sgn_mlp_packed_bytes": (c_sz, []),
+    "sgn_mlp_pack": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
+    "sgn_aggregate_workspace_bytes": (c_sz, [c_i64]),
+    "sgn_aggregate": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,
+                              c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
+                              c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+}
+
+
+class SgnError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle.  Raises if the .so is absent."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise SgnError(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback for the hot path)")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        v = h.sgn_abi_version()
+        if v != ABI_VERSION:
+            raise SgnError(f"libsgn_hip.so ABI {v} != expected {ABI_VERSION}")
+        _LIB = h
+    return _LIB
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().sgn_last_error()
+        raise SgnError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t):
+    """Device address of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,287 @@
+// query.hip -- ray march, shading-sample selection and layered kNN.
+//
+// Replaces lighting_fast_querier.query_grid_point_index
+// (models/neural_points/query_point_indices_worldcoords.py:782-954):
+//   mask_raypos (:413-437) + ray compaction / cumsum slot rule (:833-844) +
+//   get_shadingloc (:439-461)                    -> k_march (one thread per ray)
+//   query_neigh_along_ray_layered (:594-681) and the semantic-guidance variant
+//   (:489-591)                                   -> k_knn (one thread per sample)
+//
+// Differences in structure (not in results):
+//   * the [R, D, 3] candidate positions (3.07 GB at 800x800x400) are never
+//     materialised: position d is recomputed as campos + raydir * t[d] with the
+//     reference's two roundings;
+//   * the march stops at the SR-th flagged candidate (later candidates can
+//     never receive a slot: slot = cumsum - 1 <= SR - 1);
+//   * samples are stored sample-major (prefix sum over rays) so the kNN runs
+//     one thread per real sample instead of R*SR threads;
+//   * a voxel's candidate points are one contiguous float4 run (grid.hip).
+#include <hipcub/hipcub.hpp>
+
+#include "sgn_common.h"
+
+namespace sgn {
+namespace {
+
+constexpr int TPB = 256;
+
+// ---- march -----------------------------------------------------------------
+// Candidate d of ray r is flagged when its voxel is inside the grid and
+// coor_occ == 1 (vox != -2).  The first SR flagged candidates become slots.
+template <bool PER_RAY_T>
+__global__ __launch_bounds__(TPB) void k_march(GridView g, const float *__restrict__ campos,
+                                               const float *__restrict__ raydir, int64_t R,
+                                               const float *__restrict__ t_table, int D, int SR,
+                                               int32_t *__restrict__ ray_ns,
+                                               int16_t *__restrict__ ray_slot_d) {
+    int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    const float cx = campos[0], cy = campos[1], cz = campos[2];
+    const float dx = raydir[r * 3 + 0], dy = raydir[r * 3 + 1], dz = raydir[r * 3 + 2];
+    const float *tt = PER_RAY_T ? t_table + r * (int64_t)D : t_table;
+    const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+    int cnt = 0;
+    constexpr int U = 8;  // candidates whose grid words are in flight together
+    for (int d0 = 0; d0 < D && cnt < SR; d0 += U) {
+        int32_t word[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int d = d0 + u;
+            word[u] = VOX_UNFLAGGED;
+            if (d < D) {
+                float t = tt[d];
+                int ix = vox_coord(ray_coord(cx, dx, t), g.shift[0], g.vs[0]);
+                int iy = vox_coord(ray_coord(cy, dy, t), g.shift[1], g.vs[1]);
+                int iz = vox_coord(ray_coord(cz, dz, t), g.shift[2], g.vs[2]);
+                if (ix >= 0 && ix < g.dims[0] && iy >= 0 && iy < g.dims[1] && iz >= 0 && iz < g.dims[2])
+                    word[u] = g.vox[(int64_t)ix * plane + (int64_t)iy * g.dims[2] + iz];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (word[u] != VOX_UNFLAGGED && cnt < SR) {
+                ray_slot_d[r * SR + cnt] = (int16_t)(d0 + u);
+                ++cnt;
+            }
+        }
+    }
+    ray_ns[r] = cnt;
+}
+
+__global__ void k_sample_total(const int32_t *__restrict__ soff, const int32_t *__restrict__ ns,
+                               int64_t R, int32_t *__restrict__ counters) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        counters[0] = R > 0 ? soff[R - 1] + ns[R - 1] : 0;
+        counters[1] = 0;
+    }
+}
+
+__global__ __launch_bounds__(TPB) void k_emit_samples(const int32_t *__restrict__ ray_ns,
+                                                      const int32_t *__restrict__ ray_soff,
+                                                      const int16_t *__restrict__ ray_slot_d, int64_t R,
+                                                      int SR, int32_t *__restrict__ samp_ray,
+                                                      int32_t *__restrict__ samp_d) {
+    int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    int n = ray_ns[r], o = ray_soff[r];
+    for (int j = 0; j < n; ++j) {
+        samp_ray[o + j] = (int32_t)r;
+        samp_d[o + j] = ray_slot_d[r * SR + j];
+    }
+}
+
+// ---- layered kNN -------------------------------------------------------------
+template <int K>
+struct KBuf {
+    int32_t id[K];
+    float d2[K];
+    int kid, far_ind;
+    float far2;
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < K; ++i) { id[i] = -1; d2[i] = 0.f; }
+        kid = 0; far_ind = 0; far2 = 0.f;
+    }
+    // :653-672, register-resident, static indices only
+    __device__ __forceinline__ void push(int32_t pidx, float xyz2) {
+        if (kid < K) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i == kid) { id[i] = pidx; d2[i] = xyz2; }
+            if (xyz2 > far2) { far2 = xyz2; far_ind = kid; }
+            ++kid;
+        } else {
+            ++kid;
+            if (xyz2 < far2) {
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    if (i == far_ind) { id[i] = pidx; d2[i] = xyz2; }
+                float f = xyz2;
+                int fi = far_ind;
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    if (d2[i] > f) { f = d2[i]; fi = i; }
+                far2 = f;
+                far_ind = fi;
+            }
+        }
+    }
+};
+
+template <int K, bool SEMANTIC>
+__global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict__ campos,
+                                             const float *__restrict__ raydir,
+                                             const float *__restrict__ t_table, int D, int per_ray_t,
+                                             int SR, float r2, int dense_out,
+                                             const int32_t *__restrict__ point_labels,
+                                             const int32_t *__restrict__ ray_labels, uint32_t sec_mod10,
+                                             const int32_t *__restrict__ ray_soff,
+                                             const int32_t *__restrict__ samp_ray,
+                                             const int32_t *__restrict__ samp_d,
+                                             int32_t *__restrict__ counters, float *__restrict__ samp_locw,
+                                             int32_t *__restrict__ samp_nnb, int32_t *__restrict__ pidx_out,
+                                             int32_t *__restrict__ work) {
+    const int64_t S = counters[0];
+    const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = samp_ray[s];
+        const int32_t d = samp_d[s];
+        const float t = per_ray_t ? t_table[(int64_t)r * D + d] : t_table[d];
+        const float ctr_x = ray_coord(campos[0], raydir[(int64_t)r * 3 + 0], t);
+        const float ctr_y = ray_coord(campos[1], raydir[(int64_t)r * 3 + 1], t);
+        const float ctr_z = ray_coord(campos[2], raydir[(int64_t)r * 3 + 2], t);
+        const int fx = vox_coord(ctr_x, g.shift[0], g.vs[0]);
+        const int fy = vox_coord(ctr_y, g.shift[1], g.vs[1]);
+        const int fz = vox_coord(ctr_z, g.shift[2], g.vs[2]);
+        int center_label = 0;
+        if (SEMANTIC) center_label = ray_labels[r];
+        KBuf<K> kb;
+        kb.init();
+        const int nlayer = (g.kernel0 + 1) / 2;
+        for (int layer = 0; layer < nlayer; ++layer) {
+            const int x0 = max(-fx, -layer), x1 = min(g.dims[0] - fx, layer + 1);
+            const int y0 = max(-fy, -layer), y1 = min(g.dims[1] - fy, layer + 1);
+            const int z0 = max(-fz, -layer), z1 = min(g.dims[2] - fz, layer + 1);
+            for (int x = x0; x < x1; ++x)
+                for (int y = y0; y < y1; ++y)
+                    for (int z = z0; z < z1; ++z) {
+                        if (max(abs(z), max(abs(x), abs(y))) != layer) continue;
+                        const int32_t occ =
+                            g.vox[(int64_t)(fx + x) * plane + (int64_t)(fy + y) * g.dims[2] + (fz + z)];
+                        if (occ < 0) continue;
+                        const int32_t st = g.start[occ], n = g.cnt[occ];
+                        for (int q = 0; q < n; ++q) {
+                            const float4 pt = g.pts[st + q];
+                            const int32_t pid = __float_as_int(pt.w);
+                            if (SEMANTIC) {
+                                // :548-553 with label_prob == 0 (int tensor read as float, :916)
+                                int lv = point_labels[pid];
+                                bool pass = center_label == lv || lv == 0 || center_label == 0 || sec_mod10 <= 1u;
+                                if (!pass) continue;
+                            }
+                            const float xv = __fsub_rn(pt.x, ctr_x);
+                            const float yv = __fsub_rn(pt.y, ctr_y);
+                            const float zv = __fsub_rn(pt.z, ctr_z);
+                            const float xyz2 = __fmaf_rn(zv, zv, __fmaf_rn(yv, yv, __fmul_rn(xv, xv)));
+                            if (r2 == 0.0f || xyz2 <= r2) kb.push(pid, xyz2);
+                        }
+                    }
+            if (kb.kid >= K) break;
+        }
+        const int64_t ob = dense_out ? ((int64_t)r * SR + (s - ray_soff[r])) * K : s * K;
+#pragma unroll
+        for (int i = 0; i < K; ++i) pidx_out[ob + i] = kb.id[i];
+        const int nnb = kb.kid < K ? kb.kid : K;
+        samp_nnb[s] = nnb;
+        samp_locw[s * 3 + 0] = ctr_x;
+        samp_locw[s * 3 + 1] = ctr_y;
+        samp_locw[s * 3 + 2] = ctr_z;
+        if (nnb > 0) {
+            int32_t w = atomicAdd(counters + 1, 1);
+            work[w] = (int32_t)s;
+        }
+    }
+}
+
+size_t scan_temp_bytes(int64_t R) {
+    size_t tb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int32_t *)nullptr, (int32_t *)nullptr,
+                                           (int)(R > 0 ? R : 1), (hipStream_t)0);
+    return tb;
+}
+
+template <int K>
+void launch_knn(dim3 grid, hipStream_t st, bool semantic, GridView g, const float *campos,
+                const float *raydir, const float *t, int D, int per_ray_t, int SR, float r2,
+                int dense, const int32_t *pl, const int32_t *rl, uint32_t sec,
+                const sgn_query_out *o) {
+    if (semantic)
+        hipLaunchKernelGGL((k_knn<K, true>), grid, dim3(TPB), 0, st, g, campos, raydir, t, D, per_ray_t, SR,
+                           r2, dense, pl, rl, sec, o->ray_soff, o->samp_ray, o->samp_d, o->counters,
+                           o->samp_locw, o->samp_nnb, o->pidx, o->work);
+    else
+        hipLaunchKernelGGL((k_knn<K, false>), grid, dim3(TPB), 0, st, g, campos, raydir, t, D, per_ray_t, SR,
+                           r2, dense, pl, rl, sec, o->ray_soff, o->samp_ray, o->samp_d, o->counters,
+                           o->samp_locw, o->samp_nnb, o->pidx, o->work);
+}
+
+}  // namespace
+}  // namespace sgn
+
+extern "C" {
+
+size_t sgn_query_workspace_bytes(int64_t R) {
+    // [R*SR_MAX int16 slot->depth table] is carved by the caller? no: kept here.
+    size_t scan = sgn::scan_temp_bytes(R);
+    size_t slots = (size_t)(R > 0 ? R : 1) * 128 * sizeof(int16_t);
+    return ((scan + 255) / 256) * 256 + slots;
+}
+
+int sgn_query(const sgn_grid *grid, const sgn_query_params *qp, const float *d_campos,
+              const float *d_raydir, int64_t R, const float *d_t_table, const int32_t *d_point_labels,
+              const int32_t *d_ray_labels, const sgn_query_out *o, void *d_workspace,
+              size_t workspace_bytes, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(grid && qp && o, "null grid/params/out");
+    SGN_REQUIRE(qp->SR > 0 && qp->SR <= 128, "SR must be in [1, 128]");
+    SGN_REQUIRE(qp->K == 1 || qp->K == 4 || qp->K == 8 || qp->K == 16, "K must be 1, 4, 8 or 16");
+    SGN_REQUIRE(qp->D > 0 && qp->D <= 32767, "D must be in [1, 32767]");
+    SGN_REQUIRE(!qp->semantic || (d_point_labels && d_ray_labels), "semantic query needs labels");
+    SGN_REQUIRE(R >= 0 && R * (int64_t)qp->SR < (int64_t)INT32_MAX, "R*SR must fit int32");
+    SGN_REQUIRE(workspace_bytes >= sgn_query_workspace_bytes(R), "workspace too small");
+    hipStream_t st = as_stream(stream);
+    if (R == 0) {
+        SGN_CHECK_HIP(hipMemsetAsync(o->counters, 0, 4 * sizeof(int32_t), st));
+        return 0;
+    }
+    size_t scan = scan_temp_bytes(R);
+    char *ws = (char *)d_workspace;
+    int16_t *slot_d = (int16_t *)(ws + ((scan + 255) / 256) * 256);
+    GridView g = grid->view();
+    dim3 rg((unsigned)((R + TPB - 1) / TPB));
+    if (qp->per_ray_t)
+        hipLaunchKernelGGL((k_march<true>), rg, dim3(TPB), 0, st, g, d_campos, d_raydir, R, d_t_table,
+                           qp->D, qp->SR, o->ray_ns, slot_d);
+    else
+        hipLaunchKernelGGL((k_march<false>), rg, dim3(TPB), 0, st, g, d_campos, d_raydir, R, d_t_table,
+                           qp->D, qp->SR, o->ray_ns, slot_d);
+    SGN_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ws, scan, o->ray_ns, o->ray_soff, (int)R, st));
+    hipLaunchKernelGGL(k_sample_total, dim3(1), dim3(64), 0, st, o->ray_soff, o->ray_ns, R, o->counters);
+    hipLaunchKernelGGL(k_emit_samples, rg, dim3(TPB), 0, st, o->ray_ns, o->ray_soff, slot_d, R, qp->SR,
+                       o->samp_ray, o->samp_d);
+    int64_t cap = R * qp->SR;
+    int64_t kb = (cap + TPB - 1) / TPB;
+    dim3 kg((unsigned)(kb < 16384 ? kb : 16384));
+    uint32_t sec = (uint32_t)(qp->seconds % 10);
+    switch (qp->K) {
+        case 1: launch_knn<1>(kg, st, qp->semantic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
+        case 4: launch_knn<4>(kg, st, qp->semantic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
+        case 8: launch_knn<8>(kg, st, qp->semantic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
+        default: launch_knn<16>(kg, st, qp->semantic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
+    }
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

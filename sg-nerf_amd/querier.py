@@ -1,0 +1,253 @@
+"""HIP neural-point querier: drop-in for the reference's world-coordinate
+`lighting_fast_querier` (models/neural_points/query_point_indices_worldcoords.py:47-954).
+
+Two levels:
+  * `HipGrid` -- the cached device grid (sgn_grid_build), rebuilt only when the
+    point cloud changes (the reference rebuilds it per ray chunk, :797).
+  * `LightningFastQuerier.query_points(...)` -- same arguments and 7-tuple
+    result as the reference (:95-122), dense [1, R'', SR, K] layout.
+  * `LightningFastQuerier.query_samples(...)` -- the sample-major result the
+    fused renderer consumes (no [R, SR, K] materialisation, no host sync).
+"""
+import ctypes
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from .hyper import grid_hyperparameters, point_extent
+from .opts import HotPathOpts
+from .raygen import depth_table, shared_depth_table
+
+
+class HipGrid:
+    """Owns one sgn_grid (device memory is released on close/GC)."""
+
+    def __init__(self, xyz, opts: HotPathOpts, hyper=None, stream=None):
+        assert xyz.is_cuda and xyz.dtype == torch.float32
+        self.device = xyz.device
+        self.opts = opts
+        pts = xyz.reshape(-1, 3).contiguous()
+        if hyper is None:
+            hyper = grid_hyperparameters(opts, *point_extent(pts))
+        self.hyper = hyper
+        p = _lib.GridParams()
+        for a in range(3):
+            p.shift[a] = float(hyper.shift[a])
+            p.vs[a] = float(hyper.scaled_vsize[a])
+            p.dims[a] = int(hyper.scaled_vdim[a])
+            p.kernel[a] = int(opts.kernel_size[a])
+            p.query[a] = int(opts.query_size[a])
+        p.max_o, p.P, p.fix_occ0, p.seed = int(opts.max_o), int(opts.P), int(opts.fix_occ0), int(opts.reservoir_seed)
+        self.params = p
+        self.handle = ctypes.c_void_p()
+        L = _lib.lib()
+        with torch.cuda.device(self.device):
+            _lib.check(L.sgn_grid_build(_lib.ptr(pts), pts.shape[0], ctypes.byref(p),
+                                        stream or _lib.stream_handle(), ctypes.byref(self.handle)),
+                       "sgn_grid_build")
+        self.n_points = pts.shape[0]
+        self._keep = pts  # points must outlive nothing (grid holds its own copy); kept for checks
+
+    def info(self):
+        inf = _lib.GridInfo()
+        _lib.check(_lib.lib().sgn_grid_get_info(self.handle, ctypes.byref(inf)), "sgn_grid_get_info")
+        return {k: getattr(inf, k) for k, _ in inf._fields_}
+
+    def export(self):
+        """Reference-format grid tensors (coor_occ, coor_2_occ, occ_numpnts, occ_2_pnts)."""
+        d = [int(x) for x in self.hyper.scaled_vdim]
+        opts = self.opts
+        coor_occ = torch.empty(d, dtype=torch.int32, device=self.device)
+        coor_2_occ = torch.empty(d, dtype=torch.int32, device=self.device)
+        numpnts = torch.empty(opts.max_o, dtype=torch.int32, device=self.device)
+        lists = torch.empty(opts.max_o * opts.P, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().sgn_grid_export(self.handle, _lib.ptr(coor_occ), _lib.ptr(coor_2_occ),
+                                                  _lib.ptr(numpnts), _lib.ptr(lists), _lib.stream_handle()),
+                       "sgn_grid_export")
+        return coor_occ, coor_2_occ, numpnts, lists.view(opts.max_o, opts.P)
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            _lib.lib().sgn_grid_free(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class QueryResult:
+    """Sample-major query output (device tensors, capacity R*SR)."""
+    R: int
+    SR: int
+    K: int
+    ray_ns: torch.Tensor
+    ray_soff: torch.Tensor
+    samp_ray: torch.Tensor
+    samp_d: torch.Tensor
+    samp_nnb: torch.Tensor
+    pidx: torch.Tensor
+    work: torch.Tensor
+    counters: torch.Tensor
+    samp_locw: torch.Tensor
+    t_table: torch.Tensor
+    per_ray_t: int
+
+    def abi(self):
+        o = _lib.QueryOut()
+        for name in ("ray_ns", "ray_soff", "samp_ray", "samp_d", "samp_nnb", "pidx", "work", "counters",
+                     "samp_locw"):
+            setattr(o, name, getattr(self, name).data_ptr())
+        return o
+
+    def n_samples(self):
+        return int(self.counters[0].item())
+
+
+class QueryWorkspace:
+    """Reusable device buffers for one ray-batch size (no per-call allocation)."""
+
+    def __init__(self, R, SR, K, device, dense=False):
+        self.R, self.SR, self.K, self.device, self.dense = R, SR, K, device, dense
+        cap = max(R * SR, 1)
+        i32 = dict(dtype=torch.int32, device=device)
+        self.ray_ns = torch.empty(max(R, 1), **i32)
+        self.ray_soff = torch.empty(max(R, 1), **i32)
+        self.samp_ray = torch.empty(cap, **i32)
+        self.samp_d = torch.empty(cap, **i32)
+        self.samp_nnb = torch.empty(cap, **i32)
+        self.pidx = torch.empty(cap * K, **i32)
+        self.work = torch.empty(cap, **i32)
+        self.counters = torch.zeros(4, **i32)
+        self.samp_locw = torch.empty(cap * 3, dtype=torch.float32, device=device)
+        nbytes = int(_lib.lib().sgn_query_workspace_bytes(R))
+        self.scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+
+    def fits(self, R, SR, K, dense):
+        return R <= self.R and SR <= self.SR and K == self.K and dense == self.dense
+
+
+def run_query(grid: HipGrid, opts: HotPathOpts, campos, raydir, t_table, per_ray_t, ws: QueryWorkspace,
+              dense=False, point_labels=None, ray_labels=None, seconds=None):
+    """Launch sgn_query on the current stream; returns a QueryResult (views into ws)."""
+    R = raydir.shape[0]
+    qp = _lib.QueryParams()
+    qp.SR, qp.K, qp.D, qp.per_ray_t = int(opts.SR), int(opts.K), int(t_table.shape[-1]), int(per_ray_t)
+    qp.r2 = float(grid.hyper.r2)
+    qp.dense_out = int(dense)
+    qp.semantic = int(point_labels is not None)
+    qp.seconds = int(time.time() if seconds is None else seconds)
+    if dense:
+        ws.pidx[: R * opts.SR * opts.K].fill_(-1)
+    res = QueryResult(R, opts.SR, opts.K, ws.ray_ns, ws.ray_soff, ws.samp_ray, ws.samp_d, ws.samp_nnb,
+                      ws.pidx, ws.work, ws.counters, ws.samp_locw, t_table, int(per_ray_t))
+    o = res.abi()
+    _lib.check(_lib.lib().sgn_query(grid.handle, ctypes.byref(qp), _lib.ptr(campos), _lib.ptr(raydir), R,
+                                    _lib.ptr(t_table), _lib.ptr(point_labels), _lib.ptr(ray_labels),
+                                    ctypes.byref(o), _lib.ptr(ws.scratch), ws.scratch.numel(),
+                                    _lib.stream_handle()), "sgn_query")
+    return res
+
+
+class LightningFastQuerier:
+    """Reference-compatible querier (lighting_fast_querier, worldcoords.py:47)."""
+
+    def __init__(self, device, opt):
+        self.device = torch.device(device)
+        self.opt = opt
+        self.opts = opt if isinstance(opt, HotPathOpts) else HotPathOpts.from_opt(opt)
+        self.inverse = getattr(opt, "inverse", 0)
+        self._grid = None
+        self._grid_key = None
+        self._ws = None
+
+    # -- grid cache ---------------------------------------------------------------
+    def grid_for(self, point_xyz_w_tensor, version=None):
+        """Build (or reuse) the grid of this point cloud.  `version` lets callers
+        that know when points change skip the identity check."""
+        key = (point_xyz_w_tensor.data_ptr(), tuple(point_xyz_w_tensor.shape),
+               point_xyz_w_tensor._version if version is None else version)
+        if self._grid is None or self._grid_key != key:
+            if self._grid is not None:
+                self._grid.close()
+            self._grid = HipGrid(point_xyz_w_tensor.detach(), self.opts)
+            self._grid_key = key
+        return self._grid
+
+    def _workspace(self, R, dense):
+        o = self.opts
+        if self._ws is None or not self._ws.fits(R, o.SR, o.K, dense):
+            self._ws = QueryWorkspace(R, o.SR, o.K, self.device, dense)
+        return self._ws
+
+    def depth_table(self, near, far, R):
+        o = self.opts
+        if o.is_train > 0:
+            return depth_table(near, far, o.z_depth_dim, jitter=0.3, R=R, device=self.device), 1
+        return shared_depth_table(near, far, o.z_depth_dim, self.device), 0
+
+    # -- sample-major fast path ------------------------------------------------------
+    def query_samples(self, point_xyz_w_tensor, campos, raydir, near, far, point_labels=None,
+                      ray_labels=None, seconds=None):
+        grid = self.grid_for(point_xyz_w_tensor)
+        R = raydir.shape[0]
+        t, per_ray = self.depth_table(near, far, R)
+        return run_query(grid, self.opts, campos.reshape(3).contiguous(), raydir.reshape(-1, 3).contiguous(),
+                         t, per_ray, self._workspace(R, False), False, point_labels, ray_labels, seconds)
+
+    # -- reference signature ---------------------------------------------------------
+    def query_points(self, pixel_idx_tensor, point_xyz_pers_tensor, point_xyz_w_tensor, actual_numpoints_tensor,
+                     h, w, intrinsic, near_depth, far_depth, ray_dirs_tensor, cam_pos_tensor, cam_rot_tensor,
+                     pixel_label_tensor=None, points_label_tensor=None, points_label_prob_tensor=None,
+                     ray_label_tensor=None):
+        """Returns (sample_pidx [1,R'',SR,K] int32, sample_loc [1,R'',SR,3] (pers),
+        sample_loc_w [1,R'',SR,3], sample_ray_dirs [1,R'',SR,3], ray_mask int8 [1,R],
+        vsize np[3], ranges np[6]) exactly as worldcoords.py:122."""
+        o = self.opts
+        near_depth, far_depth = np.asarray(near_depth).item(), np.asarray(far_depth).item()
+        pts_w = point_xyz_w_tensor.reshape(-1, 3)
+        grid = self.grid_for(pts_w)
+        raydir = ray_dirs_tensor.reshape(-1, 3).contiguous()
+        R = raydir.shape[0]
+        t, per_ray = self.depth_table(near_depth, far_depth, R)
+        semantic = o.semantic_guidance == 1 and points_label_tensor is not None
+        pl = points_label_tensor.reshape(-1).to(torch.int32).contiguous() if semantic else None
+        rl = ray_label_tensor.reshape(-1).to(torch.int32).contiguous() if semantic else None
+        ws = self._workspace(R, True)
+        res = run_query(grid, o, cam_pos_tensor.reshape(3).contiguous(), raydir, t, per_ray, ws, True, pl, rl)
+        SR, K = o.SR, o.K
+        pidx = ws.pidx[: R * SR * K].view(R, SR, K)
+        # dense sample_loc_w: slots >= ray_ns stay 0 (sample_loc_tensor zeros, :835)
+        loc_w = torch.zeros(R, SR, 3, dtype=torch.float32, device=self.device)
+        S = res.n_samples()
+        if S > 0:
+            sr = res.samp_ray[:S].long()
+            slot = torch.arange(S, device=self.device) - res.ray_soff[sr].long()
+            loc_w[sr, slot] = res.samp_locw[: S * 3].view(S, 3)
+        ray_mask = ws.ray_ns[:R] > 0
+        valid_ray = torch.any((pidx >= 0).view(R, -1), dim=-1)  # masked_valid_ray (:944)
+        ray_mask = ray_mask & valid_ray
+        keep = torch.nonzero(ray_mask).view(-1)
+        sample_pidx = pidx[keep][None].contiguous()
+        sample_loc_w = loc_w[keep][None].contiguous()
+        sample_ray_dirs = raydir[keep][None, :, None, :].expand(-1, -1, SR, -1).contiguous()
+        sample_loc = self.w2pers(sample_loc_w, cam_rot_tensor, cam_pos_tensor)
+        return (sample_pidx, sample_loc, sample_loc_w, sample_ray_dirs, ray_mask.to(torch.int8)[None],
+                grid.hyper.vsize, grid.hyper.ranges)
+
+    @staticmethod
+    def w2pers(point_xyz_w, camrotc2w, campos):
+        """worldcoords.py:125-132 (torch, used on the compatibility path only)."""
+        xyz_w_shift = point_xyz_w - campos[:, None, :]
+        xyz_c = torch.sum(xyz_w_shift[..., None, :] * torch.transpose(camrotc2w, 1, 2)[:, None, None, ...], dim=-1)
+        z_pers = xyz_c[..., 2]
+        x_pers = xyz_c[..., 0] / xyz_c[..., 2]
+        y_pers = xyz_c[..., 1] / xyz_c[..., 2]
+        return torch.stack([x_pers, y_pers, z_pers], dim=-1)

@@ -1,0 +1,213 @@
+"""Generates tests/golden/*.npz by RUNNING the reference's own importable code
+from /root/reference (this container only; run with `python -B` so no bytecode
+is written into the reference):
+
+  * models.aggregators.point_aggregators.PointAggregator  (viewmlp forward)
+  * models.rendering.diff_ray_marching.near_far_linear_ray_generation, ray_march
+  * models.rendering.diff_render_func.alpha_blend / radiance_render
+  * models.helpers.networks.positional_encoding
+
+The neighbour query feeding the aggregator cannot run here (pycuda,
+worldcoords.py:5-9); its inputs come from the C restatement (oracle/), so the
+indices in these fixtures are oracle-generated ("parity unpinned" for the
+query stage), while every floating-point output is the reference's own.
+Glue that lives in non-importable reference modules is restated here with
+citations: the NeuralPoints gather (neural_points.py:838-850, :956-967), the
+querier's w2pers (worldcoords.py:125-132) and ray_dist
+(neural_points_volumetric_model.py:569-577).
+
+Usage:  python -B tests/golden/make_golden.py
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+
+
+def reference_opt():
+    from models.aggregators.point_aggregators import PointAggregator
+    parser = argparse.ArgumentParser()
+    PointAggregator.modify_commandline_options(parser, True)
+    opt = parser.parse_args([])
+    scannet = dict(
+        act_type="LeakyReLU", point_hyper_dim=256, point_features_dim=32, num_pos_freqs=10,
+        num_viewdir_freqs=4, which_agg_model="viewmlp", agg_distance_kernel="linear", agg_dist_pers=20,
+        agg_intrp_order=2, agg_weight_norm=1, agg_axis_weight=None, agg_feat_xyz_mode="None",
+        agg_alpha_xyz_mode="None", agg_color_xyz_mode="None", apply_pnt_mask=1, shading_feature_mlp_layer0=1,
+        shading_feature_mlp_layer1=2, shading_feature_mlp_layer2=0, shading_feature_mlp_layer2_bpnet=0,
+        shading_feature_mlp_layer3=2, shading_alpha_mlp_layer=1, shading_color_mlp_layer=4,
+        shading_feature_num=256, dist_xyz_freq=5, num_feat_freqs=3, dist_xyz_deno=0.0, point_color_mode="1",
+        point_dir_mode="1", point_conf_mode="1", act_super=1, view_ori=0, shading_color_channel_num=3,
+        sparse_loss_weight=0.0, zero_one_loss_items=["conf_coefficient"], prob=0, weight_xyz_freq=2,
+        weight_feat_dim=8, predict_semantic=0)
+    for k, v in scannet.items():
+        setattr(opt, k, v)
+    return opt
+
+
+def w2pers_points(point_xyz, camrotc2w, campos):
+    # neural_points.py:838-850
+    point_xyz_shift = point_xyz[None, ...] - campos[:, None, :]
+    xyz = torch.sum(camrotc2w[:, None, :, :] * point_xyz_shift[:, :, :, None], dim=-2)
+    xper = xyz[:, :, 0] / xyz[:, :, 2]
+    yper = xyz[:, :, 1] / xyz[:, :, 2]
+    return torch.stack([xper, yper, xyz[:, :, 2]], dim=-1)
+
+
+def w2pers_samples(point_xyz_w, camrotc2w, campos):
+    # worldcoords.py:125-132
+    xyz_w_shift = point_xyz_w - campos[:, None, :]
+    xyz_c = torch.sum(xyz_w_shift[..., None, :] * torch.transpose(camrotc2w, 1, 2)[:, None, None, ...], dim=-1)
+    z_pers = xyz_c[..., 2]
+    x_pers = xyz_c[..., 0] / xyz_c[..., 2]
+    y_pers = xyz_c[..., 1] / xyz_c[..., 2]
+    return torch.stack([x_pers, y_pers, z_pers], dim=-1)
+
+
+def make_case(name, pc, view, o, agg, refmods, pc_name=None):
+    import oracle_query as oq
+    from sgnerf_amd.hyper import grid_hyperparameters
+    near_far_linear_ray_generation, ray_march, alpha_blend, radiance_render = refmods
+    hy = grid_hyperparameters(o, torch.from_numpy(pc.xyz.min(0)), torch.from_numpy(pc.xyz.max(0)))
+    campos = torch.from_numpy(view.campos)[None]
+    rot = torch.from_numpy(view.camrotc2w)[None]
+    raydir = torch.from_numpy(view.raydir)[None]
+    R = raydir.shape[1]
+    # reference ray generation (test mode, jitter 0): pins the depth table and raypos
+    raypos, _, _, mid = near_far_linear_ray_generation(campos, raydir, o.z_depth_dim, near=view.near,
+                                                       far=view.far, jitter=0.0)
+    t_ref = mid[0, 0].contiguous()
+    assert torch.equal(mid[0], t_ref[None].expand(R, -1)), "test-mode depths must be ray independent"
+    # neighbour query (C restatement)
+    og = oq.OracleGrid(pc.xyz, hy, o)
+    q = og.query(view.campos, view.raydir, t_ref.numpy())
+    sample_pidx, sample_loc_w, ray_mask = oq.reference_layout(q)
+    # the oracle's sample positions must be the reference's raypos, bit for bit
+    for r in range(R):
+        for s in range(q["ray_ns"][r]):
+            assert np.array_equal(q["loc_w"][r, s], raypos[0, r, q["ray_d"][r, s]].numpy())
+    sample_pidx = torch.from_numpy(sample_pidx)[None].long()
+    sample_loc_w = torch.from_numpy(sample_loc_w)[None]
+    keep = torch.from_numpy(ray_mask.astype(bool))
+    B, Rv, SR, K = sample_pidx.shape
+    # NeuralPoints.forward gather, neural_points.py:956-967
+    xyz = torch.from_numpy(pc.xyz)
+    emb = torch.from_numpy(pc.embedding)[None]
+    color = torch.from_numpy(pc.color)[None]
+    pdir = torch.from_numpy(pc.dir)[None]
+    conf = torch.from_numpy(pc.conf)[None]
+    pers = w2pers_points(xyz, rot, campos)
+    mask = sample_pidx >= 0
+    flat = torch.clamp(sample_pidx, min=0).view(-1)
+    sampled_embedding = torch.index_select(torch.cat([xyz[None, ...], pers, emb], dim=-1), 1, flat).view(B, Rv, SR, K, 38)
+    sampled_color = torch.index_select(color, 1, flat).view(B, Rv, SR, K, 3)
+    sampled_dir = torch.index_select(pdir, 1, flat).view(B, Rv, SR, K, 3)
+    sampled_conf = torch.index_select(conf, 1, flat).view(B, Rv, SR, K, 1)
+    Rw2c = torch.eye(3)
+    sample_loc = w2pers_samples(sample_loc_w, rot, campos)
+    sample_ray_dirs = raydir[0][keep][None, :, None, :].expand(-1, -1, SR, -1).contiguous()
+    vsize = np.asarray(o.vsize)
+    with torch.no_grad():
+        decoded, ray_valid, weight, conf_coef = agg(
+            sampled_color, None, Rw2c, sampled_dir, sampled_conf, sampled_embedding[..., 6:],
+            sampled_embedding[..., 3:6], sampled_embedding[..., :3], mask, sample_loc, sample_loc_w,
+            sample_ray_dirs, vsize, 0)
+        # ray_dist, neural_points_volumetric_model.py:569-577
+        ray_dist = torch.cummax(sample_loc[..., 2], dim=-1)[0]
+        ray_dist = torch.cat([ray_dist[..., 1:] - ray_dist[..., :-1],
+                              torch.full((ray_dist.shape[0], ray_dist.shape[1], 1), vsize[2])], dim=-1)
+        m = ray_dist < 1e-8
+        m = torch.logical_or(m, ray_dist > 2 * vsize[2])  # raydist_mode_unit = 1
+        m = m.to(torch.float32)
+        ray_dist = ray_dist * (1.0 - m) + m * vsize[2]
+        ray_dist *= ray_valid.float()
+        bg = torch.ones(1, 3)
+        ray_color, point_color, opacity, acc_t, blend_w, bg_t, _ = ray_march(
+            ray_dist, ray_valid, decoded, radiance_render, alpha_blend, bg)
+    full = torch.ones(R, 3)  # fill_invalid: white background (tonemap off), :179-181
+    full[keep] = ray_color[0]
+    pc_name = pc_name or name
+    return {
+        f"{pc_name}/xyz": pc.xyz, f"{pc_name}/embedding": pc.embedding, f"{pc_name}/color": pc.color,
+        f"{pc_name}/dir": pc.dir, f"{pc_name}/conf": pc.conf, f"{name}/points": np.array(pc_name),
+        f"{name}/campos": view.campos, f"{name}/camrotc2w": view.camrotc2w, f"{name}/raydir": view.raydir,
+        f"{name}/near_far": np.array([view.near, view.far], np.float32),
+        f"{name}/SR": np.int32(o.SR), f"{name}/K": np.int32(o.K),
+        f"{name}/t_table": t_ref.numpy(),
+        f"{name}/raypos_rays0_3": raypos[0, :4].numpy(),
+        f"{name}/sample_pidx": sample_pidx[0].numpy().astype(np.int32),
+        f"{name}/sample_loc_w": sample_loc_w[0].numpy(),
+        f"{name}/sample_loc": sample_loc[0].numpy(),
+        f"{name}/ray_mask": ray_mask,
+        f"{name}/decoded": decoded[0].numpy(), f"{name}/ray_valid": ray_valid[0].numpy(),
+        f"{name}/weight": weight[0].numpy(), f"{name}/conf_coefficient": conf_coef[0].numpy(),
+        f"{name}/ray_dist": ray_dist[0].numpy(), f"{name}/opacity": opacity[0].numpy(),
+        f"{name}/bg_transmission": bg_t[0, :, 0].numpy(), f"{name}/ray_color": ray_color[0].numpy(),
+        f"{name}/full_color": full.numpy(),
+    }
+
+
+def main():
+    assert os.path.isdir(REF), "the golden generator runs only where /root/reference exists"
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from models.aggregators.point_aggregators import PointAggregator
+    from models.helpers.networks import positional_encoding
+    from models.rendering.diff_ray_marching import near_far_linear_ray_generation, ray_march
+    from models.rendering.diff_render_func import alpha_blend, radiance_render
+    import sgnerf_amd  # noqa: F401
+    from sgnerf_amd import scene
+    from sgnerf_amd.opts import HotPathOpts
+
+    torch.manual_seed(0)
+    opt = reference_opt()
+    agg = PointAggregator(opt).eval()
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for n, p in agg.named_parameters():
+            if n.endswith("bias"):
+                p.copy_(torch.randn(p.shape, generator=g) * 0.01)
+    out = {f"mlp/{k}": v.detach().numpy() for k, v in agg.state_dict().items()}
+    refmods = (near_far_linear_ray_generation, ray_march, alpha_blend, radiance_render)
+
+    # case "patch": a 0.6 m wall patch + a small box, seen from 0.8 m
+    rng = np.random.default_rng(11)
+    n = 9000
+    xyz = np.stack([rng.uniform(1.7, 2.3, n), np.full(n, 3.0), rng.uniform(1.2, 1.8, n)], 1)
+    xyz[: n // 4, 1] = rng.uniform(2.8, 3.0, n // 4)  # some depth structure
+    xyz += rng.normal(0, 0.002, xyz.shape)
+    pc = scene.PointCloud(xyz.astype(np.float32), *scene._attributes(rng, n))
+    view = scene.room_view(16, 16, yaw=90.0, pitch=0.0, campos=(2.0, 2.2, 1.5), focal=40.0)
+    out.update(make_case("patch", pc, view, HotPathOpts(SR=24), agg, refmods))
+    out.update(make_case("patch64", pc, view, HotPathOpts(SR=64, K=8), agg, refmods, pc_name="patch"))
+    # case "dense": every early candidate flagged with >= K neighbours
+    rng = np.random.default_rng(12)
+    n = 5000
+    xyz = np.stack([rng.uniform(1.9, 2.1, n), rng.uniform(2.85, 3.05, n), rng.uniform(1.4, 1.6, n)], 1)
+    pc = scene.PointCloud(xyz.astype(np.float32), *scene._attributes(rng, n))
+    view = scene.room_view(8, 8, yaw=90.0, pitch=0.0, campos=(2.0, 2.2, 1.5), focal=60.0)
+    out.update(make_case("dense", pc, view, HotPathOpts(SR=32), agg, refmods))
+
+    # positional_encoding known answers (networks.py:175-192)
+    x = torch.linspace(-2.0, 2.0, 24).view(4, 6)
+    out["pe/x"] = x.numpy()
+    out["pe/f3"] = positional_encoding(x, 3).numpy()
+    out["pe/f4_ori"] = positional_encoding(x[:, :3], 4, ori=True).numpy()
+    path = os.path.join(HERE, "reference_aggregator.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path) / 1e6, "MB")
+    for k in ("patch", "patch64", "dense"):
+        print(k, "rays", out[f"{k}/raydir"].shape[0], "valid rays", int(out[f"{k}/ray_mask"].sum()),
+              "valid samples", int(out[f"{k}/ray_valid"].sum()), "valid nb", int((out[f"{k}/sample_pidx"] >= 0).sum()))
+
+
+if __name__ == "__main__":
+    main()

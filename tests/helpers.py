@@ -1,0 +1,42 @@
+"""Shared test helpers: seeded scenes, options, hyper-parameters."""
+import numpy as np
+import torch
+
+import sgnerf_amd  # noqa: F401
+from sgnerf_amd import raygen, scene
+from sgnerf_amd.hyper import grid_hyperparameters
+from sgnerf_amd.opts import HotPathOpts
+
+
+def small_room(n=200_000, seed=0):
+    return scene.synth_room(n, seed=seed)
+
+
+def hyper_for(pc, opts):
+    return grid_hyperparameters(opts, torch.from_numpy(pc.xyz.min(0)), torch.from_numpy(pc.xyz.max(0)))
+
+
+def make_view(h=48, w=64, yaw=30.0, pitch=-10.0, **kw):
+    return scene.room_view(h, w, yaw=yaw, pitch=pitch, **kw)
+
+
+def t_table(opts, near=0.1, far=8.0):
+    return raygen.depth_table(near, far, opts.z_depth_dim)
+
+
+def opts(**kw):
+    return HotPathOpts(**kw)
+
+
+def assert_equal_arrays(a, b, what):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, f"{what}: shape {a.shape} vs {b.shape}"
+    if a.dtype.kind == "f":
+        ok = np.array_equal(a.view(np.int32), b.astype(a.dtype).view(np.int32))
+    else:
+        ok = np.array_equal(a, b)
+    if not ok:
+        diff = np.nonzero((a != b).reshape(-1))[0]
+        raise AssertionError(f"{what}: {diff.size} mismatches, first at {diff[:10]}: "
+                             f"{a.reshape(-1)[diff[:5]]} vs {b.reshape(-1)[diff[:5]]}")
