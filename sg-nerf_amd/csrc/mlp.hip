@@ -1,0 +1,475 @@
+// mlp.hip -- fused neural-point aggregator on MFMA (gfx950, fp16 in / fp32 accumulate).
+//
+// Replaces NeuralPoints.forward's gather (neural_points.py:942-988) and
+// PointAggregator.forward + viewmlp (point_aggregators.py:868-959, :561-786) for the
+// ScanNet configuration (agg_dist_pers 20, linear kernel, agg_intrp_order 2).
+//
+// k_agg_rows: one wave owns a 32-row column tile = 4 shading samples x K=8 neighbours.
+//   prologue : gather point records by index, pers transform, 6-d dists, inverse-distance
+//              weights normalised over the 8 rows of a sample (lane butterflies), conf
+//              clamp, positional encodings -> 18 fp16 B fragments (288 channels)
+//   block1   : 284->256->256, block3: 263->256->256 as MFMA chains; each layer's
+//              accumulator tile is converted in place into the next layer's B operand
+//              (no LDS, no transpose; the k permutation lives in the packed weights)
+//   alpha    : per-row dot with the alpha weights, softplus(x - 1), K-blend
+//   K-blend  : f_s = sum_k w_k h_k over the sample's 8 lanes -> fp16 feature rows
+// k_color: one wave = 32 samples: [f_s | PE(viewdir)] -> 128 -> 128 -> 128 -> 3, sigmoid.
+//
+// A fragments (weights) are read straight from global memory (L2-resident, 672 KB);
+// activations never leave registers between layers.
+#include <vector>
+
+#include "mlp_layout.h"
+#include "sgn_common.h"
+
+namespace sgn {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+using namespace mlp;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Weight blob access through a buffer descriptor: one VGPR of per-lane offset plus a
+// compile-time SGPR/immediate offset per fragment (flat 64-bit addresses per fragment
+// would be hoisted out of the sample loop and spill).
+struct WBlob {
+    __amdgpu_buffer_rsrc_t rsrc;
+    __device__ __forceinline__ h8 frag(uint32_t byte_off, int lane) const {
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * 16, byte_off, 0));
+    }
+    // 4 fp32 of an accumulator-order vector: element (t*2 + h)*16 + 4g of f32 section offset `f`
+    __device__ __forceinline__ f32x4 acc4(uint32_t f, int t, int g, int h) const {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rsrc, h * 64, (uint32_t)(OFF_F32 + (f + t * 32 + 4 * g) * 4), 0));
+    }
+    __device__ __forceinline__ float scalar(uint32_t f) const {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, 0, (uint32_t)(OFF_F32 + f * 4), 0));
+    }
+};
+
+__device__ __forceinline__ WBlob make_blob(const void *p) {
+    WBlob b;
+    b.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)TOTAL_BYTES, 0x00020000);
+    return b;
+}
+
+__device__ __forceinline__ f32x16 mfma32(h8 a, h8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : x * 0.01f; }
+__device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float sum8(float x) {  // over lanes j^1, j^2, j^4 (one sample)
+    x += __shfl_xor(x, 1);
+    x += __shfl_xor(x, 2);
+    x += __shfl_xor(x, 4);
+    return x;
+}
+
+struct Cam {
+    float cx, cy, cz;
+    float r[9];  // camrotc2w row-major
+    // w2pers (neural_points.py:845-850): c_j = sum_i R[i][j] * (p_i - campos_i)
+    __device__ __forceinline__ void pers(float x, float y, float z, float &px, float &py, float &pz) const {
+        float sx = __fsub_rn(x, cx), sy = __fsub_rn(y, cy), sz = __fsub_rn(z, cz);
+        float c0 = __fadd_rn(__fadd_rn(__fmul_rn(r[0], sx), __fmul_rn(r[3], sy)), __fmul_rn(r[6], sz));
+        float c1 = __fadd_rn(__fadd_rn(__fmul_rn(r[1], sx), __fmul_rn(r[4], sy)), __fmul_rn(r[7], sz));
+        float c2 = __fadd_rn(__fadd_rn(__fmul_rn(r[2], sx), __fmul_rn(r[5], sy)), __fmul_rn(r[8], sz));
+        px = __fdiv_rn(c0, c2);
+        py = __fdiv_rn(c1, c2);
+        pz = c2;
+    }
+};
+
+__device__ __forceinline__ Cam load_cam(const float *campos, const float *rot) {
+    Cam c;
+    c.cx = campos[0]; c.cy = campos[1]; c.cz = campos[2];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) c.r[i] = rot[i];
+    return c;
+}
+
+// One dense layer, output chained into the next layer's B fragments (16 k-steps).
+// KS k-steps of input: the first min(KS, NIN) from `in`, step NIN (if KS > NIN) from `extra`.
+template <int KS, int NIN, int NT = 8>
+__device__ __forceinline__ void layer_chain(const WBlob &wb, uint32_t woff, uint32_t boff,
+                                            const h8 (&in)[NIN], h8 extra, h8 (&out)[2 * NT], int lane) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+            acc = mfma32(wb.frag(woff + (uint32_t)(t * KS + k) * FRAG, lane), k < NIN ? in[k] : extra, acc);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 b = wb.acc4(boff, t, g, h);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                int r = 4 * g + c;
+                out[2 * t + (r >> 3)][r & 7] = (_Float16)lrelu(acc[r] + b[c]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep one tile's weight loads in flight, not eight
+    }
+}
+
+struct AggArgs {
+    // point tables
+    const float *xyz, *emb, *color, *dir, *conf;
+    const float *campos, *rot, *raydir;
+    // query
+    const int32_t *counters, *work, *samp_ray, *pidx;
+    const float *samp_locw;
+    // weights
+    const void *blob;
+    // outputs
+    float *feat;      // float4 per sample id: .x alpha written here
+    float *blend;     // [S*8] weight * conf (optional)
+    _Float16 *fs;     // [chunk][256] blended features (natural unit order)
+    int32_t item0, n_items;  // work-list chunk
+};
+
+constexpr int AGG_TPB = 256;
+
+__global__ __launch_bounds__(AGG_TPB, 1) void k_agg_rows(AggArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, j = lane & 31, q = j >> 3, kk = j & 7;
+    const int nwork = a.counters[1];
+    const int end = min(nwork, a.item0 + a.n_items);
+    const int wave = blockIdx.x * (AGG_TPB / 64) + (threadIdx.x >> 6);
+    const int nwaves = gridDim.x * (AGG_TPB / 64);
+    const Cam cam = load_cam(a.campos, a.rot);
+    const WBlob wb = make_blob(a.blob);
+    for (int base = a.item0 + wave * 4; base < end; base += nwaves * 4) {
+        const int item = base + q;
+        const bool sval = item < end;
+        const int s = sval ? a.work[item] : 0;
+        const int pid = sval ? a.pidx[(int64_t)s * 8 + kk] : -1;
+        const bool m = pid >= 0;
+        // ---- gather ---------------------------------------------------------
+        const float lx = a.samp_locw[(int64_t)s * 3 + 0], ly = a.samp_locw[(int64_t)s * 3 + 1],
+                    lz = a.samp_locw[(int64_t)s * 3 + 2];
+        const int ray = a.samp_ray[s];
+        const float vx = a.raydir[(int64_t)ray * 3 + 0], vy = a.raydir[(int64_t)ray * 3 + 1],
+                    vz = a.raydir[(int64_t)ray * 3 + 2];
+        float px = 0.f, py = 0.f, pz = 0.f, cf = 0.f;
+        float col[3] = {0.f, 0.f, 0.f}, pdr[3] = {0.f, 0.f, 0.f};
+        float feat[16];
+        if (m) {
+            px = a.xyz[(int64_t)pid * 3 + 0]; py = a.xyz[(int64_t)pid * 3 + 1]; pz = a.xyz[(int64_t)pid * 3 + 2];
+            const f32x4 *e4 = (const f32x4 *)(a.emb + (int64_t)pid * 32 + 16 * h);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 v = e4[g];
+                feat[4 * g + 0] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { col[c] = a.color[(int64_t)pid * 3 + c]; pdr[c] = a.dir[(int64_t)pid * 3 + c]; }
+            cf = a.conf[pid];
+        } else {
+#pragma unroll
+            for (int c = 0; c < 16; ++c) feat[c] = 0.f;
+        }
+        // ---- dists (point_aggregators.py:917-925) ---------------------------
+        const float dwx = __fsub_rn(px, lx), dwy = __fsub_rn(py, ly), dwz = __fsub_rn(pz, lz);
+        float dist[3] = {m ? dwx : 0.f, m ? dwy : 0.f, m ? dwz : 0.f};
+        if (h == 1) {
+            float xp = 0.f, yp = 0.f, zp = 0.f, xl, yl, zl;
+            if (m) cam.pers(px, py, pz, xp, yp, zp);
+            cam.pers(lx, ly, lz, xl, yl, zl);
+            dist[0] = m ? __fsub_rn(__fmul_rn(xp, zp), __fmul_rn(xl, zl)) : 0.f;
+            dist[1] = m ? __fsub_rn(__fmul_rn(yp, zp), __fmul_rn(yl, zl)) : 0.f;
+            dist[2] = m ? __fsub_rn(zp, zl) : 0.f;
+        }
+        // ---- weights: linear kernel + normalisation + conf (:494-502, :946-953)
+        float w = 0.f;
+        if (m) {
+            float n2 = __fadd_rn(__fadd_rn(__fmul_rn(dwx, dwx), __fmul_rn(dwy, dwy)), __fmul_rn(dwz, dwz));
+            w = 1.f / fmaxf(sqrtf(n2), 1e-6f);
+        }
+        const float wsum = sum8(w);
+        w = w / fmaxf(wsum, 1e-8f);
+        w = w * fminf(fmaxf(cf, 1e-4f), 1.f);
+        if (a.blend && sval && h == 0) a.blend[(int64_t)s * 8 + kk] = w;
+        // ---- layer-0 input fragments (mlp_layout.h channel order) ------------
+        h8 x0[KS_L0];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) x0[c >> 3][c & 7] = (_Float16)feat[c];
+#pragma unroll
+        for (int d = 0; d < 16; ++d) {
+#pragma unroll
+            for (int f = 0; f < 3; ++f) {
+                float sv, cv;
+                sincosf(feat[d] * (float)(1 << f), &sv, &cv);
+                const int c = 16 + 6 * d + 2 * f;
+                x0[c >> 3][c & 7] = (_Float16)sv;
+                x0[(c + 1) >> 3][(c + 1) & 7] = (_Float16)cv;
+            }
+        }
+#pragma unroll
+        for (int dd = 0; dd < 3; ++dd) {
+#pragma unroll
+            for (int f = 0; f < 5; ++f) {
+                float sv, cv;
+                sincosf(dist[dd] * (float)(1 << f), &sv, &cv);
+                const int c = 112 + 10 * dd + 2 * f;
+                x0[c >> 3][c & 7] = (_Float16)sv;
+                x0[(c + 1) >> 3][(c + 1) & 7] = (_Float16)cv;
+            }
+        }
+        x0[17][6] = (_Float16)0.f;
+        x0[17][7] = (_Float16)0.f;
+        // ---- block1 ------------------------------------------------------------
+        const h8 zero8 = {};
+        h8 a1[16];
+        layer_chain<KS_L0, KS_L0>(wb, OFF_W0, F_B0, x0, zero8, a1, lane);
+        h8 a2[16];
+        layer_chain<KS_HID, 16>(wb, OFF_W1, F_B1, a1, zero8, a2, lane);
+        // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane-half 0 only
+        h8 ext;
+        {
+            h8 e = {};
+            if (h == 0 && m) {
+                e[0] = (_Float16)col[0]; e[1] = (_Float16)col[1]; e[2] = (_Float16)col[2];
+                e[3] = (_Float16)__fsub_rn(pdr[0], vx);
+                e[4] = (_Float16)__fsub_rn(pdr[1], vy);
+                e[5] = (_Float16)__fsub_rn(pdr[2], vz);
+                e[6] = (_Float16)__fadd_rn(__fadd_rn(__fmul_rn(pdr[0], vx), __fmul_rn(pdr[1], vy)), __fmul_rn(pdr[2], vz));
+            }
+            ext = e;
+        }
+        h8 a3[16];
+        layer_chain<KS_L2, 16>(wb, OFF_W2, F_B2, a2, ext, a3, lane);
+        // ---- block3 second layer + alpha + K-blend ------------------------------
+        float apart = 0.f;
+        _Float16 *fsrow = a.fs + (int64_t)(item - a.item0) * HID;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            f32x16 acc = {};
+#pragma unroll
+            for (int k = 0; k < KS_HID; ++k)
+                acc = mfma32(wb.frag(OFF_W3 + (uint32_t)(t * KS_HID + k) * FRAG, lane), a3[k], acc);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 b = wb.acc4(F_B3, t, g, h), wa = wb.acc4(F_WA, t, g, h);
+                float v[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    v[c] = lrelu(acc[4 * g + c] + b[c]);
+                    apart = fmaf(wa[c], v[c], apart);
+                    v[c] = sum8(w * v[c]);
+                }
+                // lane kk == g of the sample stores units 32t + 8g + 4h + (0..3)
+                if (sval && kk == g) {
+                    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+                    h4 o = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+                    *(h4 *)(fsrow + 32 * t + 8 * g + 4 * h) = o;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        float araw = apart + __shfl_xor(apart, 32);
+        float alpha_row = softplus(araw + wb.scalar(F_BA) - 1.f);
+        float alpha_s = sum8(w * alpha_row);
+        if (sval && kk == 0 && h == 0) a.feat[(int64_t)s * 4 + 0] = alpha_s;
+    }
+}
+
+struct ColorArgs {
+    const int32_t *counters, *work, *samp_ray;
+    const float *raydir;
+    const void *blob;
+    const _Float16 *fs;
+    float *feat;
+    int32_t item0, n_items;
+};
+
+__global__ __launch_bounds__(AGG_TPB, 2) void k_color(ColorArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, j = lane & 31;
+    const int nwork = a.counters[1];
+    const int end = min(nwork, a.item0 + a.n_items);
+    const int wave = blockIdx.x * (AGG_TPB / 64) + (threadIdx.x >> 6);
+    const int nwaves = gridDim.x * (AGG_TPB / 64);
+    const WBlob wb = make_blob(a.blob);
+    for (int base = a.item0 + wave * 32; base < end; base += nwaves * 32) {
+        const int item = base + j;
+        const bool sval = item < end;
+        const int s = sval ? a.work[item] : 0;
+        const int ray = a.samp_ray[s];
+        h8 x[KS_C0];
+        const h8 *row = (const h8 *)(a.fs + (int64_t)(sval ? item - a.item0 : 0) * HID);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = row[2 * k + h];
+        // PE(viewdir) ori=True, channels [3:] (point_aggregators.py:579-585, networks.py:175-192)
+        float v[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1], a.raydir[(int64_t)ray * 3 + 2]};
+        float pe[24];
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                float sv, cv;
+                sincosf(v[d] * (float)(1 << f), &sv, &cv);
+                pe[d * 4 + f] = sv;
+                pe[12 + d * 4 + f] = cv;
+            }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            x[16][e] = (_Float16)(h ? pe[8 + e] : pe[e]);
+            x[17][e] = (_Float16)(h ? 0.f : pe[16 + e]);
+        }
+        h8 y1[KS_CH], y2[KS_CH];
+        const h8 zero8 = {};
+        layer_chain<KS_C0, KS_C0, T_CHID>(wb, OFF_C0, F_CB0, x, zero8, y1, lane);
+        layer_chain<KS_CH, KS_CH, T_CHID>(wb, OFF_C1, F_CB1, y1, zero8, y2, lane);
+        float o[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < T_CHID; ++t) {
+            f32x16 acc = {};
+#pragma unroll
+            for (int k = 0; k < KS_CH; ++k)
+                acc = mfma32(wb.frag(OFF_C2 + (uint32_t)(t * KS_CH + k) * FRAG, lane), y2[k], acc);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 b = wb.acc4(F_CB2, t, g, h);
+                f32x4 w0 = wb.acc4(F_WC3, t, g, h), w1 = wb.acc4(F_WC3 + 128, t, g, h),
+                      w2 = wb.acc4(F_WC3 + 256, t, g, h);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    float hv = lrelu(acc[4 * g + c] + b[c]);
+                    o[0] = fmaf(w0[c], hv, o[0]);
+                    o[1] = fmaf(w1[c], hv, o[1]);
+                    o[2] = fmaf(w2[c], hv, o[2]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float z = o[c] + __shfl_xor(o[c], 32) + wb.scalar(F_BC3 + c);
+            o[c] = (1.f / (1.f + expf(-z))) * (1.f + 2.f * 0.001f) - 0.001f;
+        }
+        if (sval && h == 0) {
+            a.feat[(int64_t)s * 4 + 1] = o[0];
+            a.feat[(int64_t)s * 4 + 2] = o[1];
+            a.feat[(int64_t)s * 4 + 3] = o[2];
+        }
+    }
+}
+
+// ---- host-side packing ---------------------------------------------------------
+
+// column of the reference weight matrix feeding B position p of k-step ks (-1: zero)
+int col_l0(int ks, int p) { return l0_ref_col(p >> 3, 8 * ks + (p & 7)); }
+int col_chain(int ks, int p) { return 16 * ks + perm_acc(p); }
+int col_l2(int ks, int p) { return ks < 16 ? col_chain(ks, p) : (p < 7 ? 256 + p : -1); }
+int col_c0(int ks, int p) { return ks < 16 ? 16 * ks + p : (16 * (ks - 16) + p < 24 ? 256 + 16 * (ks - 16) + p : -1); }
+
+template <typename ColFn>
+void pack_frags(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles, int KS, ColFn col) {
+    for (int t = 0; t < n_tiles; ++t)
+        for (int ks = 0; ks < KS; ++ks)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                    int row = 32 * t + (lane & 31);
+                    int c = col(ks, 8 * (lane >> 5) + e);
+                    float v = (row < n_out && c >= 0 && c < n_in) ? W[(size_t)row * n_in + c] : 0.f;
+                    dst[(((size_t)t * KS + ks) * 64 + lane) * 8 + e] = (_Float16)v;
+                }
+}
+
+void pack_acc_order(float *dst, const float *v, int n_tiles) {
+    for (int t = 0; t < n_tiles; ++t)
+        for (int h = 0; h < 2; ++h)
+            for (int r = 0; r < 16; ++r) dst[(t * 2 + h) * 16 + r] = v[32 * t + acc_unit(r, h)];
+}
+
+}  // namespace
+}  // namespace sgn
+
+extern "C" {
+
+size_t sgn_mlp_packed_bytes(void) { return sgn::mlp::TOTAL_BYTES; }
+
+int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    SGN_REQUIRE(w && b && d_packed, "null argument");
+    std::vector<uint8_t> blob(TOTAL_BYTES, 0);
+    auto frag = [&](size_t off) { return (_Float16 *)(blob.data() + off); };
+    pack_frags(frag(OFF_W0), w[0], 256, 284, T_HID, KS_L0, col_l0);
+    pack_frags(frag(OFF_W1), w[1], 256, 256, T_HID, KS_HID, col_chain);
+    pack_frags(frag(OFF_W2), w[2], 256, 263, T_HID, KS_L2, col_l2);
+    pack_frags(frag(OFF_W3), w[3], 256, 256, T_HID, KS_HID, col_chain);
+    pack_frags(frag(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, col_c0);
+    pack_frags(frag(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, col_chain);
+    pack_frags(frag(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, col_chain);
+    float *F = (float *)(blob.data() + OFF_F32);
+    pack_acc_order(F + F_B0, b[0], T_HID);
+    pack_acc_order(F + F_B1, b[1], T_HID);
+    pack_acc_order(F + F_B2, b[2], T_HID);
+    pack_acc_order(F + F_B3, b[3], T_HID);
+    pack_acc_order(F + F_CB0, b[5], T_CHID);
+    pack_acc_order(F + F_CB1, b[6], T_CHID);
+    pack_acc_order(F + F_CB2, b[7], T_CHID);
+    pack_acc_order(F + F_WA, w[4], T_HID);
+    F[F_BA] = b[4][0];
+    for (int c = 0; c < 3; ++c) {
+        pack_acc_order(F + F_WC3 + c * 128, w[8] + c * 128, T_CHID);
+        F[F_BC3 + c] = b[8][c];
+    }
+    hipStream_t st = as_stream(stream);
+    SGN_CHECK_HIP(hipMemcpyAsync(d_packed, blob.data(), TOTAL_BYTES, hipMemcpyHostToDevice, st));
+    SGN_CHECK_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+size_t sgn_aggregate_workspace_bytes(int64_t S) {
+    // blended-feature rows for one chunk of work items (fp16, 512 B each)
+    int64_t chunk = S < (1 << 21) ? S : (1 << 21);
+    if (chunk < 1) chunk = 1;
+    return (size_t)chunk * sgn::mlp::HID * sizeof(_Float16);
+}
+
+int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                  const void *d_packed, float *d_out_feat, float *d_out_blend, void *d_workspace,
+                  size_t workspace_bytes, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace, "null argument");
+    SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
+    hipStream_t st = as_stream(stream);
+    int64_t chunk = (int64_t)(workspace_bytes / (HID * sizeof(_Float16)));
+    SGN_REQUIRE(chunk >= 32, "aggregate workspace too small");
+    if (chunk > (1 << 21)) chunk = 1 << 21;
+    const uint8_t *P = (const uint8_t *)d_packed;
+    AggArgs a;
+    a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
+    a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
+    a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
+    a.samp_locw = q->samp_locw;
+    a.blob = P;
+    a.feat = d_out_feat; a.blend = d_out_blend; a.fs = (_Float16 *)d_workspace;
+    ColorArgs c;
+    c.counters = q->counters; c.work = q->work; c.samp_ray = q->samp_ray; c.raydir = pt->raydir;
+    c.blob = P; c.fs = a.fs; c.feat = d_out_feat;
+    for (int64_t i0 = 0; i0 < S_capacity; i0 += chunk) {
+        int64_t n = S_capacity - i0 < chunk ? S_capacity - i0 : chunk;
+        a.item0 = c.item0 = (int32_t)i0;
+        a.n_items = c.n_items = (int32_t)n;
+        int64_t wg = (n + 15) / 16;  // 4 samples per wave, 4 waves per block
+        dim3 g1((unsigned)(wg < 2048 ? wg : 2048));
+        hipLaunchKernelGGL(k_agg_rows, g1, dim3(AGG_TPB), 0, st, a);
+        int64_t wg2 = (n + 127) / 128;  // 32 samples per wave
+        dim3 g2((unsigned)(wg2 < 2048 ? wg2 : 2048));
+        hipLaunchKernelGGL(k_color, g2, dim3(AGG_TPB), 0, st, c);
+    }
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+"""Fused frame renderer: query -> MFMA aggregator -> composite, all on one stream,
+no host synchronisation and no [R, SR, K, C] intermediates.
+
+This is the product path behind NeuralPointsRayMarching.forward (ray_marching.py)
+and bench.py.  Buffers are sized once per (R, SR) and reused.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .opts import HotPathOpts
+from .querier import LightningFastQuerier
+from .weights import pack_mlp
+
+
+@dataclass
+class RenderOut:
+    rgb: torch.Tensor        # [R,3] fill_invalid'ed colour (bg for invalid rays)
+    ray_mask: torch.Tensor   # [R] int8, reference ray_mask after masked_valid_ray
+    bg_transmission: torch.Tensor  # [R] coarse_is_background (1 for invalid rays)
+    opacity: torch.Tensor    # [R,SR] coarse_point_opacity (0 for invalid rays / empty slots)
+    query: object            # QueryResult (sample-major, device)
+    feat: torch.Tensor       # [S_cap,4] per-sample (alpha, r, g, b)
+    blend: torch.Tensor      # [S_cap,8] weight * conf_coefficient
+
+
+class PointTables:
+    """Device-resident neural point cloud (contiguous fp32 tables)."""
+
+    def __init__(self, xyz, embedding, color, dir, conf, device):
+        def t(x, cols):
+            x = torch.as_tensor(x).reshape(-1, cols)
+            return x.to(device=device, dtype=torch.float32).contiguous()
+        self.xyz = t(xyz, 3)
+        self.embedding = t(embedding, 32)
+        self.color = t(color, 3)
+        self.dir = t(dir, 3)
+        self.conf = t(conf, 1)
+        self.n = self.xyz.shape[0]
+
+    @classmethod
+    def from_cloud(cls, pc, device):
+        return cls(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, device)
+
+
+class HipRenderer:
+    def __init__(self, points: PointTables, mlp_state, opts: HotPathOpts, device):
+        self.device = torch.device(device)
+        self.opts = opts.check_supported()
+        self.points = points
+        self.querier = LightningFastQuerier(self.device, opts)
+        self.packed = pack_mlp(mlp_state, self.device)
+        self._cap = None
+
+    def set_mlp(self, mlp_state):
+        self.packed = pack_mlp(mlp_state, self.device)
+
+    def _buffers(self, R):
+        SR = self.opts.SR
+        if self._cap is None or self._cap[0] < R:
+            cap = max(R * SR, 1)
+            dev = self.device
+            self.feat = torch.empty(cap, 4, dtype=torch.float32, device=dev)
+            self.blend = torch.empty(cap, 8, dtype=torch.float32, device=dev)
+            nb = int(_lib.lib().sgn_aggregate_workspace_bytes(cap))
+            self.agg_ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+            self.rgb = torch.empty(max(R, 1), 3, dtype=torch.float32, device=dev)
+            self.mask = torch.empty(max(R, 1), dtype=torch.int8, device=dev)
+            self.bgT = torch.empty(max(R, 1), dtype=torch.float32, device=dev)
+            self.opacity = torch.empty(max(R, 1), SR, dtype=torch.float32, device=dev)
+            self._cap = (R, cap)
+
+    def render(self, campos, camrotc2w, raydir, near, far, want_opacity=True, want_blend=False):
+        o = self.opts
+        campos = campos.reshape(3).to(self.device, torch.float32).contiguous()
+        rot = camrotc2w.reshape(3, 3).to(self.device, torch.float32).contiguous()
+        raydir = raydir.reshape(-1, 3).to(self.device, torch.float32).contiguous()
+        R = raydir.shape[0]
+        self._buffers(R)
+        q = self.querier.query_samples(self.points.xyz, campos, raydir, near, far)
+        L = _lib.lib()
+        st = _lib.stream_handle()
+        pt = _lib.PointTables()
+        pt.xyz, pt.embedding, pt.color = self.points.xyz.data_ptr(), self.points.embedding.data_ptr(), self.points.color.data_ptr()
+        pt.dir, pt.conf, pt.n_points = self.points.dir.data_ptr(), self.points.conf.data_ptr(), self.points.n
+        pt.campos, pt.camrotc2w, pt.raydir = campos.data_ptr(), rot.data_ptr(), raydir.data_ptr()
+        qo = q.abi()
+        cap = R * o.SR
+        _lib.check(L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), cap, o.K, _lib.ptr(self.packed),
+                                   _lib.ptr(self.feat), _lib.ptr(self.blend) if want_blend else None,
+                                   _lib.ptr(self.agg_ws), self.agg_ws.numel(), st), "sgn_aggregate")
+        cp = _lib.CompositeParams()
+        cp.SR, cp.vsize_z, cp.raydist_mode_unit = o.SR, float(o.vsize[2]), o.raydist_mode_unit
+        bg = (1.0, 1.0, 1.0) if o.bg_color == "white" else (0.0, 0.0, 0.0)
+        for i in range(3):
+            cp.bg[i] = bg[i]
+        _lib.check(L.sgn_composite(ctypes.byref(cp), _lib.ptr(campos), _lib.ptr(rot), _lib.ptr(raydir), R,
+                                   _lib.ptr(q.t_table), q.per_ray_t, q.t_table.shape[-1], ctypes.byref(qo),
+                                   _lib.ptr(self.feat), _lib.ptr(self.rgb), _lib.ptr(self.mask), _lib.ptr(self.bgT),
+                                   _lib.ptr(self.opacity) if want_opacity else None, st), "sgn_composite")
+        return RenderOut(self.rgb[:R], self.mask[:R], self.bgT[:R], self.opacity[:R], q, self.feat, self.blend)

@@ -1,0 +1,83 @@
+"""Aggregator MLP parameters: reference-layout init and MFMA packing.
+
+Parameter names and shapes follow PointAggregator.viewmlp_init
+(models/aggregators/point_aggregators.py:312-421) at the ScanNet config, i.e. the
+keys of `aggregator.*` in `{iter}_net_ray_marching.pth`.  Initialisation follows
+init_seq (models/helpers/networks.py:120-172): xavier-uniform with the LeakyReLU(0.01)
+gain for layers followed by an activation, gain 1 for the last layer, zero bias.
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+
+# (name, out, in, followed_by_activation)
+LAYERS = [
+    ("block1.0", 256, 284, True),
+    ("block1.2", 256, 256, True),
+    ("block3.0", 256, 263, True),
+    ("block3.2", 256, 256, True),
+    ("alpha_branch.0", 1, 256, False),
+    ("color_branch.0", 128, 280, True),
+    ("color_branch.2", 128, 128, True),
+    ("color_branch.4", 128, 128, True),
+    ("color_branch.6", 3, 128, False),
+]
+N_PARAMS = sum(o * i + o for _, o, i, _ in LAYERS)  # 341,764
+
+
+def init_mlp(seed=0, bias_std=0.0):
+    """Reference-style init (init_seq).  bias_std > 0 perturbs biases (fixtures)."""
+    g = torch.Generator().manual_seed(seed)
+    leaky_gain = math.sqrt(2.0 / (1 + 0.01 ** 2))  # nn.init.calculate_gain('leaky_relu', 0.01)
+    state = {}
+    for name, o, i, act in LAYERS:
+        gain = leaky_gain if act else 1.0
+        std = gain * math.sqrt(2.0 / (i + o))
+        a = std * math.sqrt(3.0)
+        state[name + ".weight"] = (torch.rand((o, i), generator=g) * 2 - 1) * a
+        b = torch.zeros(o)
+        if bias_std > 0:
+            b = torch.randn(o, generator=g) * bias_std
+        state[name + ".bias"] = b
+    return state
+
+
+def strip_prefix(state, prefix="aggregator."):
+    """Accepts a full net_ray_marching state dict (keys `aggregator.*`, `module.aggregator.*`)."""
+    out = {}
+    for k, v in state.items():
+        for p in ("module." + prefix, prefix, ""):
+            if k.startswith(p) and k[len(p):] in {n + s for n, *_ in LAYERS for s in (".weight", ".bias")}:
+                out[k[len(p):]] = v
+                break
+    missing = [n + s for n, *_ in LAYERS for s in (".weight", ".bias") if n + s not in out]
+    if missing:
+        raise KeyError(f"aggregator parameters missing: {missing}")
+    return out
+
+
+def check_shapes(state):
+    for name, o, i, _ in LAYERS:
+        w, b = state[name + ".weight"], state[name + ".bias"]
+        if tuple(w.shape) != (o, i) or tuple(b.shape) != (o,):
+            raise ValueError(f"{name}: expected weight {(o, i)} bias {(o,)}, got {tuple(w.shape)} {tuple(b.shape)}")
+
+
+def pack_mlp(state, device):
+    """fp32 state -> packed fp16 MFMA fragment blob on `device` (uint8 tensor)."""
+    state = strip_prefix(state)
+    check_shapes(state)
+    L = _lib.lib()
+    nbytes = int(L.sgn_mlp_packed_bytes())
+    out = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    ws = [np.ascontiguousarray(state[n + ".weight"].detach().cpu().float().numpy()) for n, *_ in LAYERS]
+    bs = [np.ascontiguousarray(state[n + ".bias"].detach().cpu().float().numpy()) for n, *_ in LAYERS]
+    wp = (ctypes.c_void_p * len(LAYERS))(*[w.ctypes.data for w in ws])
+    bp = (ctypes.c_void_p * len(LAYERS))(*[b.ctypes.data for b in bs])
+    with torch.cuda.device(device):
+        _lib.check(L.sgn_mlp_pack(wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack")
+    return out

@@ -1,0 +1,70 @@
+"""CPU: the oracle (and the host-side restatements) against the golden vectors
+produced by the imported reference code (tests/golden/make_golden.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import agg_ref
+import oracle_query as oq
+from helpers import assert_equal_arrays
+from sgnerf_amd import raygen
+from sgnerf_amd.hyper import grid_hyperparameters
+from sgnerf_amd.opts import HotPathOpts
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_aggregator.npz")
+CASES = ["patch", "patch64", "dense"]
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD, allow_pickle=False)
+
+
+def case(gold, name):
+    pcn = str(gold[f"{name}/points"])
+    pts = {k: torch.from_numpy(gold[f"{pcn}/{k}"]) for k in ("xyz", "embedding", "color", "dir", "conf")}
+    mlp = {k[len("mlp/"):]: torch.from_numpy(gold[k]) for k in gold.files if k.startswith("mlp/")}
+    return pts, mlp
+
+
+def test_positional_encoding_golden(gold):
+    x = torch.from_numpy(gold["pe/x"])
+    assert_equal_arrays(agg_ref.positional_encoding(x, 3).numpy(), gold["pe/f3"], "PE f=3")
+    assert_equal_arrays(agg_ref.positional_encoding(x[:, :3], 4, ori=True).numpy(), gold["pe/f4_ori"], "PE ori f=4")
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_depth_table_and_raypos_golden(gold, name):
+    near, far = gold[f"{name}/near_far"]
+    t = raygen.depth_table(float(near), float(far), 400)
+    assert_equal_arrays(t.numpy(), gold[f"{name}/t_table"], "depth table")
+    campos = gold[f"{name}/campos"]
+    raydir = gold[f"{name}/raydir"]
+    # raypos = campos + raydir * t with two fp32 roundings (diff_ray_marching.py:387)
+    pos = campos[None, None, :] + (raydir[:4, None, :] * t.numpy()[None, :, None]).astype(np.float32)
+    assert_equal_arrays(pos.astype(np.float32), gold[f"{name}/raypos_rays0_3"], "raypos")
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_render_matches_reference(gold, name):
+    pts, mlp = case(gold, name)
+    SR, K = int(gold[f"{name}/SR"]), int(gold[f"{name}/K"])
+    o = HotPathOpts(SR=SR, K=K)
+    xyz = gold[f"{str(gold[f'{name}/points'])}/xyz"]
+    hy = grid_hyperparameters(o, torch.from_numpy(xyz.min(0)), torch.from_numpy(xyz.max(0)))
+    og = oq.OracleGrid(xyz, hy, o)
+    campos, rot, raydir = (torch.from_numpy(gold[f"{name}/{k}"]) for k in ("campos", "camrotc2w", "raydir"))
+    q = og.query(gold[f"{name}/campos"], gold[f"{name}/raydir"], gold[f"{name}/t_table"])
+    sp, sl, rm = oq.reference_layout(q)
+    assert_equal_arrays(sp, gold[f"{name}/sample_pidx"], "sample_pidx (oracle determinism)")
+    assert_equal_arrays(rm, gold[f"{name}/ray_mask"], "ray_mask")
+    with torch.no_grad():
+        full, ray_mask, fd, opacity, bg_t = agg_ref.render(pts, mlp, campos, rot, raydir, q, SR)
+    keep = ray_mask.numpy()
+    dec = gold[f"{name}/decoded"]
+    np.testing.assert_allclose(fd[keep].numpy(), dec, atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(opacity[keep].numpy(), gold[f"{name}/opacity"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(bg_t[keep].numpy(), gold[f"{name}/bg_transmission"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(full.numpy(), gold[f"{name}/full_color"], atol=2e-6, rtol=1e-5)
