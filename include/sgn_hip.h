@@ -143,9 +143,10 @@ typedef struct {
  * no valid neighbour are written as zeros); also writes out_blend (optional,
  * may be NULL) float[S*K] = normalised weight * conf (reference `weight*conf_coefficient`). */
 size_t sgn_aggregate_workspace_bytes(int64_t S);
+/* stages: bit 0 = per-neighbour MLP + K-blend (writes alpha), bit 1 = colour MLP (rgb). */
 int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
                   int32_t K, const void *d_packed_mlp, float *d_out_feat, float *d_out_blend,
-                  void *d_workspace, size_t workspace_bytes, sgn_stream_t stream);
+                  void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream);
 
 /* ---- composite --------------------------------------------------------- */
 

@@ -64,7 +64,7 @@ SIGNATURES = {
     "sgn_mlp_pack": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
     "sgn_aggregate_workspace_bytes": (c_sz, [c_i64]),
     "sgn_aggregate": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,
-                              c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+                              c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
                               c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }

@@ -429,15 +429,15 @@ int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, s
 }
 
 size_t sgn_aggregate_workspace_bytes(int64_t S) {
-    // blended-feature rows for one chunk of work items (fp16, 512 B each)
-    int64_t chunk = S < (1 << 21) ? S : (1 << 21);
-    if (chunk < 1) chunk = 1;
-    return (size_t)chunk * sgn::mlp::HID * sizeof(_Float16);
+    // blended-feature rows of every possible work item (fp16, 512 B each): one launch per
+    // stage; a smaller workspace is accepted and processed in chunks.
+    if (S < 32) S = 32;
+    return (size_t)S * sgn::mlp::HID * sizeof(_Float16);
 }
 
 int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
                   const void *d_packed, float *d_out_feat, float *d_out_blend, void *d_workspace,
-                  size_t workspace_bytes, sgn_stream_t stream) {
+                  size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
     using namespace sgn;
     using namespace sgn::mlp;
     SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace, "null argument");
@@ -445,7 +445,6 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
     hipStream_t st = as_stream(stream);
     int64_t chunk = (int64_t)(workspace_bytes / (HID * sizeof(_Float16)));
     SGN_REQUIRE(chunk >= 32, "aggregate workspace too small");
-    if (chunk > (1 << 21)) chunk = 1 << 21;
     const uint8_t *P = (const uint8_t *)d_packed;
     AggArgs a;
     a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
@@ -463,10 +462,10 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
         a.n_items = c.n_items = (int32_t)n;
         int64_t wg = (n + 15) / 16;  // 4 samples per wave, 4 waves per block
         dim3 g1((unsigned)(wg < 2048 ? wg : 2048));
-        hipLaunchKernelGGL(k_agg_rows, g1, dim3(AGG_TPB), 0, st, a);
+        if (stages & 1) hipLaunchKernelGGL(k_agg_rows, g1, dim3(AGG_TPB), 0, st, a);
         int64_t wg2 = (n + 127) / 128;  // 32 samples per wave
         dim3 g2((unsigned)(wg2 < 2048 ? wg2 : 2048));
-        hipLaunchKernelGGL(k_color, g2, dim3(AGG_TPB), 0, st, c);
+        if (stages & 2) hipLaunchKernelGGL(k_color, g2, dim3(AGG_TPB), 0, st, c);
     }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;

@@ -72,13 +72,17 @@ class HipRenderer:
             self.opacity = torch.empty(max(R, 1), SR, dtype=torch.float32, device=dev)
             self._cap = (R, cap)
 
-    def render(self, campos, camrotc2w, raydir, near, far, want_opacity=True, want_blend=False):
+    def render(self, campos, camrotc2w, raydir, near, far, want_opacity=True, want_blend=False, marks=None):
+        """One frame.  `marks(name)` (optional) is called between stages on the host thread
+        (bench.py records HIP events on the current stream there)."""
         o = self.opts
+        mark = marks or (lambda name: None)
         campos = campos.reshape(3).to(self.device, torch.float32).contiguous()
         rot = camrotc2w.reshape(3, 3).to(self.device, torch.float32).contiguous()
         raydir = raydir.reshape(-1, 3).to(self.device, torch.float32).contiguous()
         R = raydir.shape[0]
         self._buffers(R)
+        mark("query")
         q = self.querier.query_samples(self.points.xyz, campos, raydir, near, far)
         L = _lib.lib()
         st = _lib.stream_handle()
@@ -88,9 +92,12 @@ class HipRenderer:
         pt.campos, pt.camrotc2w, pt.raydir = campos.data_ptr(), rot.data_ptr(), raydir.data_ptr()
         qo = q.abi()
         cap = R * o.SR
-        _lib.check(L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), cap, o.K, _lib.ptr(self.packed),
-                                   _lib.ptr(self.feat), _lib.ptr(self.blend) if want_blend else None,
-                                   _lib.ptr(self.agg_ws), self.agg_ws.numel(), st), "sgn_aggregate")
+        for stage, name in ((1, "agg_rows"), (2, "agg_color")):
+            mark(name)
+            _lib.check(L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), cap, o.K, _lib.ptr(self.packed),
+                                       _lib.ptr(self.feat), _lib.ptr(self.blend) if want_blend else None,
+                                       _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate")
+        mark("composite")
         cp = _lib.CompositeParams()
         cp.SR, cp.vsize_z, cp.raydist_mode_unit = o.SR, float(o.vsize[2]), o.raydist_mode_unit
         bg = (1.0, 1.0, 1.0) if o.bg_color == "white" else (0.0, 0.0, 0.0)
@@ -100,4 +107,8 @@ class HipRenderer:
                                    _lib.ptr(q.t_table), q.per_ray_t, q.t_table.shape[-1], ctypes.byref(qo),
                                    _lib.ptr(self.feat), _lib.ptr(self.rgb), _lib.ptr(self.mask), _lib.ptr(self.bgT),
                                    _lib.ptr(self.opacity) if want_opacity else None, st), "sgn_composite")
+        mark("end")
         return RenderOut(self.rgb[:R], self.mask[:R], self.bgT[:R], self.opacity[:R], q, self.feat, self.blend)
+
+    def grid_info(self):
+        return self.querier.grid_for(self.points.xyz).info()
