@@ -17,6 +17,7 @@
 //
 // A fragments (weights) are read straight from global memory (L2-resident, 672 KB);
 // activations never leave registers between layers.
+#include <utility>
 #include <vector>
 
 #include "mlp_layout.h"
@@ -62,13 +63,6 @@ __device__ __forceinline__ f32x16 mfma32(h8 a, h8 b, f32x16 c) {
 }
 __device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : x * 0.01f; }
 __device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
-__device__ __forceinline__ float sum8(float x) {  // over lanes j^1, j^2, j^4 (one sample)
-    x += __shfl_xor(x, 1);
-    x += __shfl_xor(x, 2);
-    x += __shfl_xor(x, 4);
-    return x;
-}
-
 struct Cam {
     float cx, cy, cz;
     float r[9];  // camrotc2w row-major
@@ -135,150 +129,352 @@ struct AggArgs {
 
 constexpr int AGG_TPB = 256;
 
-__global__ __launch_bounds__(AGG_TPB, 1) void k_agg_rows(AggArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, j = lane & 31, q = j >> 3, kk = j & 7;
-    const int nwork = a.counters[1];
-    const int end = min(nwork, a.item0 + a.n_items);
-    const int wave = blockIdx.x * (AGG_TPB / 64) + (threadIdx.x >> 6);
-    const int nwaves = gridDim.x * (AGG_TPB / 64);
-    const Cam cam = load_cam(a.campos, a.rot);
-    const WBlob wb = make_blob(a.blob);
-    for (int base = a.item0 + wave * 4; base < end; base += nwaves * 4) {
-        const int item = base + q;
-        const bool sval = item < end;
-        const int s = sval ? a.work[item] : 0;
-        const int pid = sval ? a.pidx[(int64_t)s * 8 + kk] : -1;
-        const bool m = pid >= 0;
-        // ---- gather ---------------------------------------------------------
-        const float lx = a.samp_locw[(int64_t)s * 3 + 0], ly = a.samp_locw[(int64_t)s * 3 + 1],
-                    lz = a.samp_locw[(int64_t)s * 3 + 2];
-        const int ray = a.samp_ray[s];
-        const float vx = a.raydir[(int64_t)ray * 3 + 0], vy = a.raydir[(int64_t)ray * 3 + 1],
-                    vz = a.raydir[(int64_t)ray * 3 + 2];
-        float px = 0.f, py = 0.f, pz = 0.f, cf = 0.f;
-        float col[3] = {0.f, 0.f, 0.f}, pdr[3] = {0.f, 0.f, 0.f};
-        float feat[16];
-        if (m) {
-            px = a.xyz[(int64_t)pid * 3 + 0]; py = a.xyz[(int64_t)pid * 3 + 1]; pz = a.xyz[(int64_t)pid * 3 + 2];
-            const f32x4 *e4 = (const f32x4 *)(a.emb + (int64_t)pid * 32 + 16 * h);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                f32x4 v = e4[g];
-                feat[4 * g + 0] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
-            }
-#pragma unroll
-            for (int c = 0; c < 3; ++c) { col[c] = a.color[(int64_t)pid * 3 + c]; pdr[c] = a.dir[(int64_t)pid * 3 + c]; }
-            cf = a.conf[pid];
-        } else {
-#pragma unroll
-            for (int c = 0; c < 16; ++c) feat[c] = 0.f;
-        }
-        // ---- dists (point_aggregators.py:917-925) ---------------------------
-        const float dwx = __fsub_rn(px, lx), dwy = __fsub_rn(py, ly), dwz = __fsub_rn(pz, lz);
-        float dist[3] = {m ? dwx : 0.f, m ? dwy : 0.f, m ? dwz : 0.f};
-        if (h == 1) {
-            float xp = 0.f, yp = 0.f, zp = 0.f, xl, yl, zl;
-            if (m) cam.pers(px, py, pz, xp, yp, zp);
-            cam.pers(lx, ly, lz, xl, yl, zl);
-            dist[0] = m ? __fsub_rn(__fmul_rn(xp, zp), __fmul_rn(xl, zl)) : 0.f;
-            dist[1] = m ? __fsub_rn(__fmul_rn(yp, zp), __fmul_rn(yl, zl)) : 0.f;
-            dist[2] = m ? __fsub_rn(zp, zl) : 0.f;
-        }
-        // ---- weights: linear kernel + normalisation + conf (:494-502, :946-953)
-        float w = 0.f;
-        if (m) {
-            float n2 = __fadd_rn(__fadd_rn(__fmul_rn(dwx, dwx), __fmul_rn(dwy, dwy)), __fmul_rn(dwz, dwz));
-            w = 1.f / fmaxf(sqrtf(n2), 1e-6f);
-        }
-        const float wsum = sum8(w);
-        w = w / fmaxf(wsum, 1e-8f);
-        w = w * fminf(fmaxf(cf, 1e-4f), 1.f);
-        if (a.blend && sval && h == 0) a.blend[(int64_t)s * 8 + kk] = w;
-        // ---- layer-0 input fragments (mlp_layout.h channel order) ------------
-        h8 x0[KS_L0];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) x0[c >> 3][c & 7] = (_Float16)feat[c];
-#pragma unroll
-        for (int d = 0; d < 16; ++d) {
-#pragma unroll
-            for (int f = 0; f < 3; ++f) {
-                float sv, cv;
-                sincosf(feat[d] * (float)(1 << f), &sv, &cv);
-                const int c = 16 + 6 * d + 2 * f;
-                x0[c >> 3][c & 7] = (_Float16)sv;
-                x0[(c + 1) >> 3][(c + 1) & 7] = (_Float16)cv;
-            }
-        }
-#pragma unroll
-        for (int dd = 0; dd < 3; ++dd) {
-#pragma unroll
-            for (int f = 0; f < 5; ++f) {
-                float sv, cv;
-                sincosf(dist[dd] * (float)(1 << f), &sv, &cv);
-                const int c = 112 + 10 * dd + 2 * f;
-                x0[c >> 3][c & 7] = (_Float16)sv;
-                x0[(c + 1) >> 3][(c + 1) & 7] = (_Float16)cv;
-            }
-        }
-        x0[17][6] = (_Float16)0.f;
-        x0[17][7] = (_Float16)0.f;
-        // ---- block1 ------------------------------------------------------------
-        const h8 zero8 = {};
-        h8 a1[16];
-        layer_chain<KS_L0, KS_L0>(wb, OFF_W0, F_B0, x0, zero8, a1, lane);
-        h8 a2[16];
-        layer_chain<KS_HID, 16>(wb, OFF_W1, F_B1, a1, zero8, a2, lane);
-        // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane-half 0 only
-        h8 ext;
-        {
-            h8 e = {};
-            if (h == 0 && m) {
-                e[0] = (_Float16)col[0]; e[1] = (_Float16)col[1]; e[2] = (_Float16)col[2];
-                e[3] = (_Float16)__fsub_rn(pdr[0], vx);
-                e[4] = (_Float16)__fsub_rn(pdr[1], vy);
-                e[5] = (_Float16)__fsub_rn(pdr[2], vz);
-                e[6] = (_Float16)__fadd_rn(__fadd_rn(__fmul_rn(pdr[0], vx), __fmul_rn(pdr[1], vy)), __fmul_rn(pdr[2], vz));
-            }
-            ext = e;
-        }
-        h8 a3[16];
-        layer_chain<KS_L2, 16>(wb, OFF_W2, F_B2, a2, ext, a3, lane);
-        // ---- block3 second layer + alpha + K-blend ------------------------------
-        float apart = 0.f;
-        _Float16 *fsrow = a.fs + (int64_t)(item - a.item0) * HID;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            f32x16 acc = {};
-#pragma unroll
-            for (int k = 0; k < KS_HID; ++k)
-                acc = mfma32(wb.frag(OFF_W3 + (uint32_t)(t * KS_HID + k) * FRAG, lane), a3[k], acc);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                f32x4 b = wb.acc4(F_B3, t, g, h), wa = wb.acc4(F_WA, t, g, h);
-                float v[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    v[c] = lrelu(acc[4 * g + c] + b[c]);
-                    apart = fmaf(wa[c], v[c], apart);
-                    v[c] = sum8(w * v[c]);
-                }
-                // lane kk == g of the sample stores units 32t + 8g + 4h + (0..3)
-                if (sval && kk == g) {
-                    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-                    h4 o = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
-                    *(h4 *)(fsrow + 32 * t + 8 * g + 4 * h) = o;
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        float araw = apart + __shfl_xor(apart, 32);
-        float alpha_row = softplus(araw + wb.scalar(F_BA) - 1.f);
-        float alpha_s = sum8(w * alpha_row);
-        if (sval && kk == 0 && h == 0) a.feat[(int64_t)s * 4 + 0] = alpha_s;
+// ---- workgroup-shared weight stream, k-outer ---------------------------------------
+// A workgroup = 8 waves (2 per SIMD) = 32 samples x 8 neighbours = 256 rows, 32 rows per
+// wave.  Per layer each wave keeps all eight 32x32 output tiles as MFMA accumulators
+// (128 AGPRs) and walks the input k-steps in order, so an input fragment dies as soon as it
+// has been multiplied into the 8 tiles: layer-0 fragments are even generated just in time
+// (positional encodings computed per k-step, interleaved with the MFMAs of the partner wave).
+// Block1/block3 weights (536 fragments of 1 KiB, packed [layer][k-step][tile]) stream through
+// a 2-slot LDS ring, one chunk = KC k-steps x 8 tiles; chunk c+1 is fetched global->VGPR at
+// the start of chunk c and stored to the other slot after chunk c's MFMAs (one barrier per
+// chunk).  Every fragment fetched into LDS feeds 8 waves.
+constexpr int ROWS_TPB = 512;
+constexpr int WG_WAVES = ROWS_TPB / 64;
+constexpr int WG_SAMPLES = WG_WAVES * 4;  // 32
+constexpr int TP = 4;                      // output tiles per pass (2 passes per layer)
+constexpr int KC = 4;                      // k-steps per chunk
+constexpr int CHUNK_FRAGS = KC * TP;
+constexpr int SLOT_BYTES = CHUNK_FRAGS * (int)FRAG;
+constexpr int PF_N = CHUNK_FRAGS / WG_WAVES;  // prefetch fragments per wave per chunk
+constexpr int LDS_F32_OFF = 2 * SLOT_BYTES;
+constexpr int LDS_BYTES = LDS_F32_OFF + (int)N_F32 * 4;
+static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the waves");
+
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// DPP butterflies: lanes j^1, j^2 (quad_perm), then the mirrored quad of the 8-lane half-row
+__device__ __forceinline__ float dpp_sum8(float x) {
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, true));
+    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x141, 0xF, 0xF, true));
+    return x;
+}
+
+__device__ __forceinline__ h8 pack8(float a0, float a1, float a2, float a3, float a4, float a5, float a6,
+                                    float a7) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 p0 = {(_Float16)a0, (_Float16)a1}, p1 = {(_Float16)a2, (_Float16)a3};
+    const h2 p2 = {(_Float16)a4, (_Float16)a5}, p3 = {(_Float16)a6, (_Float16)a7};
+    const u32x4 u = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1),
+                     __builtin_bit_cast(uint32_t, p2), __builtin_bit_cast(uint32_t, p3)};
+    return __builtin_bit_cast(h8, u);
+}
+
+// sin/cos for the positional encodings: hardware v_sin/v_cos on the argument reduced to
+// [-0.5, 0.5] revolutions (abs error ~1e-6, far below the fp16 rounding of the result)
+__device__ __forceinline__ float pe_sin(float x) {
+    float r = x * 0.15915494309189535f;
+    r = r - rintf(r);
+    return __builtin_amdgcn_sinf(r);
+}
+__device__ __forceinline__ float pe_cos(float x) {
+    float r = x * 0.15915494309189535f;
+    r = r - rintf(r);
+    return __builtin_amdgcn_cosf(r);
+}
+
+// value of layer-0 channel C (0..143) of a lane-half (mlp_layout.h order)
+template <int C>
+__device__ __forceinline__ float l0_channel(const float (&feat)[16], const float (&dist)[3]) {
+    if constexpr (C < 16) {
+        return feat[C];
+    } else if constexpr (C < 112) {
+        constexpr int m = C - 16, d = m / 6, f = (m % 6) / 2, sc = m % 2;
+        const float x = feat[d] * (float)(1 << f);
+        return sc ? pe_cos(x) : pe_sin(x);
+    } else if constexpr (C < 142) {
+        constexpr int m = C - 112, dd = m / 10, f = (m % 10) / 2, sc = m % 2;
+        const float x = dist[dd] * (float)(1 << f);
+        return sc ? pe_cos(x) : pe_sin(x);
+    } else {
+        return 0.f;
     }
 }
 
+template <int K0>
+__device__ __forceinline__ h8 l0_step(const float (&feat)[16], const float (&dist)[3]) {
+    return pack8(l0_channel<8 * K0 + 0>(feat, dist), l0_channel<8 * K0 + 1>(feat, dist),
+                 l0_channel<8 * K0 + 2>(feat, dist), l0_channel<8 * K0 + 3>(feat, dist),
+                 l0_channel<8 * K0 + 4>(feat, dist), l0_channel<8 * K0 + 5>(feat, dist),
+                 l0_channel<8 * K0 + 6>(feat, dist), l0_channel<8 * K0 + 7>(feat, dist));
+}
+
+__host__ __device__ constexpr int layer_ks(int L) { return L == 0 ? KS_L0 : L == 2 ? KS_L2 : KS_HID; }
+__host__ __device__ constexpr int layer_nch(int L) { return (layer_ks(L) + KC - 1) / KC; }
+__host__ __device__ constexpr size_t layer_off(int L) {
+    return L == 0 ? OFF_W0 : L == 1 ? OFF_W1 : L == 2 ? OFF_W2 : OFF_W3;
+}
+__host__ __device__ constexpr int chunk_nk(int L, int c) {
+    return (layer_ks(L) - c * KC) < KC ? (layer_ks(L) - c * KC) : KC;
+}
+// stream position: layer L, pass P (tiles 4P..4P+3), chunk C (k-steps C*KC..) -> blob offset
+__host__ __device__ constexpr uint32_t chunk_off(int L, int P, int C) {
+    return (uint32_t)(layer_off(L) + ((size_t)P * layer_ks(L) * TP + (size_t)C * KC * TP) * FRAG);
+}
+
+// fetch chunk (L, P, C) fragments of this wave: i = w + WG_WAVES*j (clamped into the chunk).
+// `lz` is an opaque zero that keeps the per-chunk offsets from being hoisted into SGPRs.
+template <int L, int P, int C>
+__device__ __forceinline__ void pf_load(const WBlob &wb, int w, int lane, int lz, u32x4 (&pf)[PF_N]) {
+    constexpr int nf = chunk_nk(L, C) * TP;
+#pragma unroll
+    for (int j = 0; j < PF_N; ++j) {
+        const int i = min(w + WG_WAVES * j, nf - 1);
+        pf[j] = __builtin_amdgcn_raw_buffer_load_b128(wb.rsrc, lane * 16 + i * (int)FRAG,
+                                                      chunk_off(L, P, C) + (uint32_t)lz, 0);
+    }
+}
+template <int L, int C>
+__device__ __forceinline__ void pf_commit(char *slot, int w, int lane, const u32x4 (&pf)[PF_N]) {
+    constexpr int nf = chunk_nk(L, C) * TP;
+#pragma unroll
+    for (int j = 0; j < PF_N; ++j) {
+        const int i = w + WG_WAVES * j;
+        if (nf == CHUNK_FRAGS || i < nf) *(u32x4 *)(slot + i * (int)FRAG + lane * 16) = pf[j];
+    }
+}
+// the chunk after (L, P, C) in the stream (wraps to the next work tile's layer 0)
+template <int L, int P, int C>
+__device__ __forceinline__ void pf_load_next(const WBlob &wb, int w, int lane, int lz, u32x4 (&pf)[PF_N]) {
+    if constexpr (C + 1 < layer_nch(L)) pf_load<L, P, C + 1>(wb, w, lane, lz, pf);
+    else if constexpr (P == 0) pf_load<L, 1, 0>(wb, w, lane, lz, pf);
+    else if constexpr (L < 3) pf_load<L + 1, 0, 0>(wb, w, lane, lz, pf);
+    else pf_load<0, 0, 0>(wb, w, lane, lz, pf);
+}
+template <int L, int P, int C>
+__device__ __forceinline__ void pf_commit_next(char *slot, int w, int lane, const u32x4 (&pf)[PF_N]) {
+    if constexpr (C + 1 < layer_nch(L)) pf_commit<L, C + 1>(slot, w, lane, pf);
+    else if constexpr (P == 0) pf_commit<L, 0>(slot, w, lane, pf);
+    else if constexpr (L < 3) pf_commit<L + 1, 0>(slot, w, lane, pf);
+    else pf_commit<0, 0>(slot, w, lane, pf);
+}
+
+// One pass of a layer, k-outer: acc[t] += W[4P+t][k] * in(k) for every k-step, chunk by chunk.
+template <int L, int P, class InFn>
+__device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
+                                         f32x16 (&acc)[TP], InFn &&in) {
+#pragma unroll
+    for (int t = 0; t < TP; ++t) acc[t] = f32x16{};
+    static_for<layer_nch(L)>([&](auto cc) {
+        constexpr int C = decltype(cc)::value;
+        __syncthreads();
+        u32x4 pf[PF_N];
+        pf_load_next<L, P, C>(wb, w, lane, lz, pf);
+        const char *sl = lds + slot * SLOT_BYTES;
+        static_for<chunk_nk(L, C)>([&](auto kk) {
+            constexpr int KK = decltype(kk)::value;
+            const h8 B = in(std::integral_constant<int, C * KC + KK>{});
+#pragma unroll
+            for (int t = 0; t < TP; ++t) {
+                const h8 A = *(const h8 *)(sl + (KK * TP + t) * (int)FRAG + lane * 16);
+                acc[t] = mfma32(A, B, acc[t]);
+            }
+        });
+        slot ^= 1;
+        pf_commit_next<L, P, C>(lds + slot * SLOT_BYTES, w, lane, pf);
+        __builtin_amdgcn_sched_barrier(0);
+    });
+}
+
+// bias + LeakyReLU + fp16 pack: pass P accumulators -> next-layer fragments 8P..8P+7
+template <int P>
+__device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], const float *Fl, size_t fb, int h,
+                                          h8 (&out)[16]) {
+#pragma unroll
+    for (int tt = 0; tt < TP; ++tt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int t = TP * P + tt;
+            const f32x4 b0 = *(const f32x4 *)(Fl + fb + (t * 2 + h) * 16 + 8 * s2);
+            const f32x4 b1 = *(const f32x4 *)(Fl + fb + (t * 2 + h) * 16 + 8 * s2 + 4);
+            const int r = 8 * s2;
+            out[2 * t + s2] = pack8(lrelu(acc[tt][r + 0] + b0[0]), lrelu(acc[tt][r + 1] + b0[1]),
+                                    lrelu(acc[tt][r + 2] + b0[2]), lrelu(acc[tt][r + 3] + b0[3]),
+                                    lrelu(acc[tt][r + 4] + b1[0]), lrelu(acc[tt][r + 5] + b1[1]),
+                                    lrelu(acc[tt][r + 6] + b1[2]), lrelu(acc[tt][r + 7] + b1[3]));
+        }
+}
+
+struct RowIn {
+    int s;       // sample id
+    bool sval;   // work item exists
+    float wgt;   // normalised weight * conf of this row
+};
+
+// Gather + pers + dists + weights of this lane's row; raw features for the
+// just-in-time layer-0 encodings, block3's extra channels.
+__device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, int item, int end, int lane,
+                                            float (&feat)[16], float (&dist)[3], h8 &ext) {
+    const int h = lane >> 5, kk = lane & 7;
+    RowIn ri;
+    ri.sval = item < end;
+    ri.s = ri.sval ? a.work[item] : 0;
+    const int s = ri.s;
+    const int pid = ri.sval ? a.pidx[(int64_t)s * 8 + kk] : -1;
+    const bool m = pid >= 0;
+    const float lx = a.samp_locw[(int64_t)s * 3 + 0], ly = a.samp_locw[(int64_t)s * 3 + 1],
+                lz = a.samp_locw[(int64_t)s * 3 + 2];
+    const int ray = a.samp_ray[s];
+    const float vx = a.raydir[(int64_t)ray * 3 + 0], vy = a.raydir[(int64_t)ray * 3 + 1],
+                vz = a.raydir[(int64_t)ray * 3 + 2];
+    float px = 0.f, py = 0.f, pz = 0.f, cf = 0.f;
+    float col[3] = {0.f, 0.f, 0.f}, pdr[3] = {0.f, 0.f, 0.f};
+    if (m) {
+        px = a.xyz[(int64_t)pid * 3 + 0]; py = a.xyz[(int64_t)pid * 3 + 1]; pz = a.xyz[(int64_t)pid * 3 + 2];
+        const f32x4 *e4 = (const f32x4 *)(a.emb + (int64_t)pid * 32 + 16 * h);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            f32x4 v = e4[g];
+            feat[4 * g + 0] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { col[c] = a.color[(int64_t)pid * 3 + c]; pdr[c] = a.dir[(int64_t)pid * 3 + c]; }
+        cf = a.conf[pid];
+    } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) feat[c] = 0.f;
+    }
+    // dists (point_aggregators.py:917-925): half 0 world offsets, half 1 pers-space terms
+    const float dwx = __fsub_rn(px, lx), dwy = __fsub_rn(py, ly), dwz = __fsub_rn(pz, lz);
+    dist[0] = m ? dwx : 0.f; dist[1] = m ? dwy : 0.f; dist[2] = m ? dwz : 0.f;
+    if (h == 1) {
+        float xp = 0.f, yp = 0.f, zp = 0.f, xl, yl, zl;
+        if (m) cam.pers(px, py, pz, xp, yp, zp);
+        cam.pers(lx, ly, lz, xl, yl, zl);
+        dist[0] = m ? __fsub_rn(__fmul_rn(xp, zp), __fmul_rn(xl, zl)) : 0.f;
+        dist[1] = m ? __fsub_rn(__fmul_rn(yp, zp), __fmul_rn(yl, zl)) : 0.f;
+        dist[2] = m ? __fsub_rn(zp, zl) : 0.f;
+    }
+    // linear kernel weights, normalised over the sample's 8 rows, times clamped conf
+    float w = 0.f;
+    if (m) {
+        float n2 = __fadd_rn(__fadd_rn(__fmul_rn(dwx, dwx), __fmul_rn(dwy, dwy)), __fmul_rn(dwz, dwz));
+        w = 1.f / fmaxf(sqrtf(n2), 1e-6f);
+    }
+    const float wsum = dpp_sum8(w);
+    w = w / fmaxf(wsum, 1e-8f);
+    ri.wgt = w * fminf(fmaxf(cf, 1e-4f), 1.f);
+    if (a.blend && ri.sval && h == 0) a.blend[(int64_t)s * 8 + kk] = ri.wgt;
+    // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane-half 0 only
+    h8 e = {};
+    if (h == 0 && m) {
+        e = pack8(col[0], col[1], col[2], __fsub_rn(pdr[0], vx), __fsub_rn(pdr[1], vy), __fsub_rn(pdr[2], vz),
+                  __fadd_rn(__fadd_rn(__fmul_rn(pdr[0], vx), __fmul_rn(pdr[1], vy)), __fmul_rn(pdr[2], vz)), 0.f);
+    }
+    ext = e;
+    return ri;
+}
+
+__global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, kk = lane & 7, q = (lane & 31) >> 3;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwork = a.counters[1];
+    const int end = min(nwork, a.item0 + a.n_items);
+    const Cam cam = load_cam(a.campos, a.rot);
+    const WBlob wb = make_blob(a.blob);
+    {   // fp32 parameters (biases, alpha weights) -> LDS once
+        const float *src = (const float *)((const char *)a.blob + OFF_F32);
+        float *dst = (float *)(lds + LDS_F32_OFF);
+        for (int i = threadIdx.x; i < (int)N_F32; i += ROWS_TPB) dst[i] = src[i];
+    }
+    int slot = 0;
+    {
+        u32x4 pf[PF_N];
+        pf_load<0, 0, 0>(wb, w, lane, 0, pf);
+        pf_commit<0, 0>(lds, w, lane, pf);
+    }
+    for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
+        // opaque zero per iteration: keeps LDS parameter reads and weight offsets inside the loop
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        char *ldsi = lds + lz;
+        const float *Fl = (const float *)(ldsi + LDS_F32_OFF);
+        const int item = base + w * 4 + q;
+        float feat[16], dist[3];
+        h8 ext;
+        const RowIn ri = gather_row(a, cam, item, end, lane, feat, dist, ext);
+        f32x16 acc[TP];
+        h8 actA[16], actB[16];
+        auto l0in = [&](auto k) { return l0_step<decltype(k)::value>(feat, dist); };
+        // block1.0: 284 -> 256 (inputs generated per k-step)
+        run_pass<0, 0>(wb, ldsi, slot, w, lane, lz, acc, l0in);
+        chain_out<0>(acc, Fl, F_B0, h, actA);
+        run_pass<0, 1>(wb, ldsi, slot, w, lane, lz, acc, l0in);
+        chain_out<1>(acc, Fl, F_B0, h, actA);
+        // block1.2: 256 -> 256
+        auto inA = [&](auto k) { return actA[decltype(k)::value]; };
+        run_pass<1, 0>(wb, ldsi, slot, w, lane, lz, acc, inA);
+        chain_out<0>(acc, Fl, F_B1, h, actB);
+        run_pass<1, 1>(wb, ldsi, slot, w, lane, lz, acc, inA);
+        chain_out<1>(acc, Fl, F_B1, h, actB);
+        // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256
+        auto inB = [&](auto k) {
+            constexpr int K = decltype(k)::value;
+            if constexpr (K < 16) return actB[K]; else return ext;
+        };
+        run_pass<2, 0>(wb, ldsi, slot, w, lane, lz, acc, inB);
+        chain_out<0>(acc, Fl, F_B2, h, actA);
+        run_pass<2, 1>(wb, ldsi, slot, w, lane, lz, acc, inB);
+        chain_out<1>(acc, Fl, F_B2, h, actA);
+        // block3.2: 256 -> 256, then alpha + K-blend, one pass of 4 output tiles at a time
+        float apart = 0.f;
+        _Float16 *fsrow = a.fs + (int64_t)(item - a.item0) * HID;
+        auto l3_epilogue = [&](auto pp) {
+            constexpr int P = decltype(pp)::value;
+#pragma unroll
+            for (int tt = 0; tt < TP; ++tt) {
+                const int t = TP * P + tt;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 b = *(const f32x4 *)(Fl + F_B3 + (t * 2 + h) * 16 + 4 * g);
+                    const f32x4 wa = *(const f32x4 *)(Fl + F_WA + (t * 2 + h) * 16 + 4 * g);
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[e] = lrelu(acc[tt][4 * g + e] + b[e]);
+                        apart = fmaf(wa[e], v[e], apart);
+                        v[e] = dpp_sum8(ri.wgt * v[e]);
+                    }
+                    // lane kk == g of the sample stores units 32t + 8g + 4h + (0..3)
+                    if (ri.sval && kk == g) {
+                        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+                        h4 o = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+                        *(h4 *)(fsrow + 32 * t + 8 * g + 4 * h) = o;
+                    }
+                }
+            }
+        };
+        auto inA3 = [&](auto k) { return actA[decltype(k)::value]; };
+        run_pass<3, 0>(wb, ldsi, slot, w, lane, lz, acc, inA3);
+        l3_epilogue(std::integral_constant<int, 0>{});
+        run_pass<3, 1>(wb, ldsi, slot, w, lane, lz, acc, inA3);
+        l3_epilogue(std::integral_constant<int, 1>{});
+        const float araw = apart + __shfl_xor(apart, 32);
+        const float alpha_row = softplus(araw + Fl[F_BA] - 1.f);
+        const float alpha_s = dpp_sum8(ri.wgt * alpha_row);
+        if (ri.sval && kk == 0 && h == 0) a.feat[(int64_t)ri.s * 4 + 0] = alpha_s;
+    }
+}
 struct ColorArgs {
     const int32_t *counters, *work, *samp_ray;
     const float *raydir;
@@ -369,8 +565,10 @@ int col_chain(int ks, int p) { return 16 * ks + perm_acc(p); }
 int col_l2(int ks, int p) { return ks < 16 ? col_chain(ks, p) : (p < 7 ? 256 + p : -1); }
 int col_c0(int ks, int p) { return ks < 16 ? 16 * ks + p : (16 * (ks - 16) + p < 24 ? 256 + 16 * (ks - 16) + p : -1); }
 
+// kouter: fragment (t, ks) at index ks*n_tiles + t (block1/block3 stream order), else t*KS + ks
 template <typename ColFn>
-void pack_frags(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles, int KS, ColFn col) {
+void pack_frags(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles, int KS, ColFn col,
+                bool kouter) {
     for (int t = 0; t < n_tiles; ++t)
         for (int ks = 0; ks < KS; ++ks)
             for (int lane = 0; lane < 64; ++lane)
@@ -378,7 +576,9 @@ void pack_frags(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles,
                     int row = 32 * t + (lane & 31);
                     int c = col(ks, 8 * (lane >> 5) + e);
                     float v = (row < n_out && c >= 0 && c < n_in) ? W[(size_t)row * n_in + c] : 0.f;
-                    dst[(((size_t)t * KS + ks) * 64 + lane) * 8 + e] = (_Float16)v;
+                    // kouter: [pass = t/4][ks][t%4] (k-outer stream of k_agg_rows)
+                    size_t f = kouter ? ((size_t)(t / 4) * KS + ks) * 4 + (t % 4) : (size_t)t * KS + ks;
+                    dst[(f * 64 + lane) * 8 + e] = (_Float16)v;
                 }
 }
 
@@ -401,13 +601,13 @@ int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, s
     SGN_REQUIRE(w && b && d_packed, "null argument");
     std::vector<uint8_t> blob(TOTAL_BYTES, 0);
     auto frag = [&](size_t off) { return (_Float16 *)(blob.data() + off); };
-    pack_frags(frag(OFF_W0), w[0], 256, 284, T_HID, KS_L0, col_l0);
-    pack_frags(frag(OFF_W1), w[1], 256, 256, T_HID, KS_HID, col_chain);
-    pack_frags(frag(OFF_W2), w[2], 256, 263, T_HID, KS_L2, col_l2);
-    pack_frags(frag(OFF_W3), w[3], 256, 256, T_HID, KS_HID, col_chain);
-    pack_frags(frag(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, col_c0);
-    pack_frags(frag(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, col_chain);
-    pack_frags(frag(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, col_chain);
+    pack_frags(frag(OFF_W0), w[0], 256, 284, T_HID, KS_L0, col_l0, true);
+    pack_frags(frag(OFF_W1), w[1], 256, 256, T_HID, KS_HID, col_chain, true);
+    pack_frags(frag(OFF_W2), w[2], 256, 263, T_HID, KS_L2, col_l2, true);
+    pack_frags(frag(OFF_W3), w[3], 256, 256, T_HID, KS_HID, col_chain, true);
+    pack_frags(frag(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, col_c0, false);
+    pack_frags(frag(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, col_chain, false);
+    pack_frags(frag(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, col_chain, false);
     float *F = (float *)(blob.data() + OFF_F32);
     pack_acc_order(F + F_B0, b[0], T_HID);
     pack_acc_order(F + F_B1, b[1], T_HID);
@@ -460,9 +660,9 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
         int64_t n = S_capacity - i0 < chunk ? S_capacity - i0 : chunk;
         a.item0 = c.item0 = (int32_t)i0;
         a.n_items = c.n_items = (int32_t)n;
-        int64_t wg = (n + 15) / 16;  // 4 samples per wave, 4 waves per block
-        dim3 g1((unsigned)(wg < 2048 ? wg : 2048));
-        if (stages & 1) hipLaunchKernelGGL(k_agg_rows, g1, dim3(AGG_TPB), 0, st, a);
+        int64_t wg = (n + WG_SAMPLES - 1) / WG_SAMPLES;  // persistent: one workgroup per CU
+        dim3 g1((unsigned)(wg < 256 ? wg : 256));
+        if (stages & 1) hipLaunchKernelGGL(k_agg_rows, g1, dim3(ROWS_TPB), 0, st, a);
         int64_t wg2 = (n + 127) / 128;  // 32 samples per wave
         dim3 g2((unsigned)(wg2 < 2048 ? wg2 : 2048));
         if (stages & 2) hipLaunchKernelGGL(k_color, g2, dim3(AGG_TPB), 0, st, c);
