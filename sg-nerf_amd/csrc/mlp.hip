@@ -142,12 +142,18 @@ constexpr int AGG_TPB = 256;
 constexpr int ROWS_TPB = 512;
 constexpr int WG_WAVES = ROWS_TPB / 64;
 constexpr int WG_SAMPLES = WG_WAVES * 4;  // 32
-constexpr int TP = 4;                      // output tiles per pass (2 passes per layer)
-constexpr int KC = 4;                      // k-steps per chunk
-constexpr int CHUNK_FRAGS = KC * TP;
+constexpr int CHUNK_FRAGS = 16;            // fragments per LDS chunk (k-steps x tiles of a pass)
+// output tiles per pass: layer 0 runs all 8 tiles in one pass (its inputs are generated on
+// the fly and never stored), the chained layers run two passes of 4 (their input fragments
+// stay in registers, the accumulators of 8 tiles would not fit beside them)
+__host__ __device__ constexpr int layer_tp(int L) { return L == 0 ? 8 : 4; }
+__host__ __device__ constexpr int layer_np(int L) { return 8 / layer_tp(L); }
+__host__ __device__ constexpr int layer_kc(int L) { return CHUNK_FRAGS / layer_tp(L); }
 constexpr int SLOT_BYTES = CHUNK_FRAGS * (int)FRAG;
-constexpr int PF_N = CHUNK_FRAGS / WG_WAVES;  // prefetch fragments per wave per chunk
-constexpr int LDS_F32_OFF = 2 * SLOT_BYTES;
+constexpr int PF_N = CHUNK_FRAGS / WG_WAVES;  // LDS-DMA instructions per wave per chunk
+constexpr int DIST = 2;                       // chunks in flight ahead of the one being consumed
+constexpr int NSLOT = DIST + 1;               // ring slots (the DMA target was read one chunk ago)
+constexpr int LDS_F32_OFF = NSLOT * SLOT_BYTES;
 constexpr int LDS_BYTES = LDS_F32_OFF + (int)N_F32 * 4;
 static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the waves");
 
@@ -191,6 +197,22 @@ __device__ __forceinline__ float pe_cos(float x) {
     return __builtin_amdgcn_cosf(r);
 }
 
+// sin/cos of x * 2^F from one hardware sin/cos of x and F double-angle steps
+// (sin 2a = 2 sin a cos a, cos 2a = (cos a - sin a)(cos a + sin a)); identical
+// sub-expressions of the channels of one k-step are CSE'd by the compiler.
+template <int F>
+__device__ __forceinline__ void sincos_pow2(float x, float &s, float &c) {
+    if constexpr (F == 0) {
+        s = pe_sin(x);
+        c = pe_cos(x);
+    } else {
+        float s0, c0;
+        sincos_pow2<F - 1>(x, s0, c0);
+        s = 2.f * s0 * c0;
+        c = (c0 - s0) * (c0 + s0);
+    }
+}
+
 // value of layer-0 channel C (0..143) of a lane-half (mlp_layout.h order)
 template <int C>
 __device__ __forceinline__ float l0_channel(const float (&feat)[16], const float (&dist)[3]) {
@@ -198,12 +220,14 @@ __device__ __forceinline__ float l0_channel(const float (&feat)[16], const float
         return feat[C];
     } else if constexpr (C < 112) {
         constexpr int m = C - 16, d = m / 6, f = (m % 6) / 2, sc = m % 2;
-        const float x = feat[d] * (float)(1 << f);
-        return sc ? pe_cos(x) : pe_sin(x);
+        float sv, cv;
+        sincos_pow2<f>(feat[d], sv, cv);
+        return sc ? cv : sv;
     } else if constexpr (C < 142) {
         constexpr int m = C - 112, dd = m / 10, f = (m % 10) / 2, sc = m % 2;
-        const float x = dist[dd] * (float)(1 << f);
-        return sc ? pe_cos(x) : pe_sin(x);
+        float sv, cv;
+        sincos_pow2<f>(dist[dd], sv, cv);
+        return sc ? cv : sv;
     } else {
         return 0.f;
     }
@@ -218,66 +242,86 @@ __device__ __forceinline__ h8 l0_step(const float (&feat)[16], const float (&dis
 }
 
 __host__ __device__ constexpr int layer_ks(int L) { return L == 0 ? KS_L0 : L == 2 ? KS_L2 : KS_HID; }
-__host__ __device__ constexpr int layer_nch(int L) { return (layer_ks(L) + KC - 1) / KC; }
+__host__ __device__ constexpr int layer_nch(int L) { return (layer_ks(L) + layer_kc(L) - 1) / layer_kc(L); }
 __host__ __device__ constexpr size_t layer_off(int L) {
     return L == 0 ? OFF_W0 : L == 1 ? OFF_W1 : L == 2 ? OFF_W2 : OFF_W3;
 }
 __host__ __device__ constexpr int chunk_nk(int L, int c) {
-    return (layer_ks(L) - c * KC) < KC ? (layer_ks(L) - c * KC) : KC;
+    return (layer_ks(L) - c * layer_kc(L)) < layer_kc(L) ? (layer_ks(L) - c * layer_kc(L)) : layer_kc(L);
 }
-// stream position: layer L, pass P (tiles 4P..4P+3), chunk C (k-steps C*KC..) -> blob offset
+// stream position: layer L, pass P (tiles TP*P..), chunk C (k-steps C*KC..) -> blob offset
 __host__ __device__ constexpr uint32_t chunk_off(int L, int P, int C) {
-    return (uint32_t)(layer_off(L) + ((size_t)P * layer_ks(L) * TP + (size_t)C * KC * TP) * FRAG);
+    return (uint32_t)(layer_off(L) + ((size_t)P * layer_ks(L) * layer_tp(L) +
+                                      (size_t)C * layer_kc(L) * layer_tp(L)) * FRAG);
 }
 
-// fetch chunk (L, P, C) fragments of this wave: i = w + WG_WAVES*j (clamped into the chunk).
-// `lz` is an opaque zero that keeps the per-chunk offsets from being hoisted into SGPRs.
-template <int L, int P, int C>
-__device__ __forceinline__ void pf_load(const WBlob &wb, int w, int lane, int lz, u32x4 (&pf)[PF_N]) {
-    constexpr int nf = chunk_nk(L, C) * TP;
-#pragma unroll
-    for (int j = 0; j < PF_N; ++j) {
-        const int i = min(w + WG_WAVES * j, nf - 1);
-        pf[j] = __builtin_amdgcn_raw_buffer_load_b128(wb.rsrc, lane * 16 + i * (int)FRAG,
-                                                      chunk_off(L, P, C) + (uint32_t)lz, 0);
-    }
+// ---- chunk stream ---------------------------------------------------------------
+// Per work tile the stream is: layer 0 (1 pass x 9 chunks), layers 1..3 (2 passes each).
+__host__ __device__ constexpr int pass_chunks(int L) { return layer_nch(L); }
+__host__ __device__ constexpr int layer_chunks(int L) { return layer_np(L) * layer_nch(L); }
+__host__ __device__ constexpr int chunk_base(int L) {
+    return L == 0 ? 0 : chunk_base(L - 1) + layer_chunks(L - 1);
 }
-template <int L, int C>
-__device__ __forceinline__ void pf_commit(char *slot, int w, int lane, const u32x4 (&pf)[PF_N]) {
-    constexpr int nf = chunk_nk(L, C) * TP;
+constexpr int NCHUNK = chunk_base(3) + layer_chunks(3);
+__host__ __device__ constexpr int chunk_index(int L, int P, int C) { return chunk_base(L) + P * pass_chunks(L) + C; }
+__host__ __device__ constexpr int chunk_L(int n) {
+    return n < chunk_base(1) ? 0 : n < chunk_base(2) ? 1 : n < chunk_base(3) ? 2 : 3;
+}
+__host__ __device__ constexpr int chunk_P(int n) { return (n - chunk_base(chunk_L(n))) / pass_chunks(chunk_L(n)); }
+__host__ __device__ constexpr int chunk_C(int n) { return (n - chunk_base(chunk_L(n))) % pass_chunks(chunk_L(n)); }
+
+// Issue the LDS-DMA of stream chunk N into LDS slot `dst`: each wave moves fragments
+// w + WG_WAVES*j (1 KiB, lane-linear) with buffer_load ... lds; indices past the chunk
+// re-load its last fragment into unused slot space so every wave issues exactly PF_N
+// DMAs per chunk (the counted vmcnt below relies on it).
+template <int N>
+__device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
+    constexpr int L = chunk_L(N), P = chunk_P(N), C = chunk_C(N);
+    constexpr int nf = chunk_nk(L, C) * layer_tp(L);
 #pragma unroll
     for (int j = 0; j < PF_N; ++j) {
         const int i = w + WG_WAVES * j;
-        if (nf == CHUNK_FRAGS || i < nf) *(u32x4 *)(slot + i * (int)FRAG + lane * 16) = pf[j];
+        const int src = min(i, nf - 1);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            wb.rsrc, (__attribute__((address_space(3))) void *)(dst + i * (int)FRAG), 16,
+            lane * 16 + src * (int)FRAG, chunk_off(L, P, C) + (uint32_t)lz, 0, 0);
     }
 }
-// the chunk after (L, P, C) in the stream (wraps to the next work tile's layer 0)
-template <int L, int P, int C>
-__device__ __forceinline__ void pf_load_next(const WBlob &wb, int w, int lane, int lz, u32x4 (&pf)[PF_N]) {
-    if constexpr (C + 1 < layer_nch(L)) pf_load<L, P, C + 1>(wb, w, lane, lz, pf);
-    else if constexpr (P == 0) pf_load<L, 1, 0>(wb, w, lane, lz, pf);
-    else if constexpr (L < 3) pf_load<L + 1, 0, 0>(wb, w, lane, lz, pf);
-    else pf_load<0, 0, 0>(wb, w, lane, lz, pf);
-}
-template <int L, int P, int C>
-__device__ __forceinline__ void pf_commit_next(char *slot, int w, int lane, const u32x4 (&pf)[PF_N]) {
-    if constexpr (C + 1 < layer_nch(L)) pf_commit<L, C + 1>(slot, w, lane, pf);
-    else if constexpr (P == 0) pf_commit<L, 0>(slot, w, lane, pf);
-    else if constexpr (L < 3) pf_commit<L + 1, 0>(slot, w, lane, pf);
-    else pf_commit<0, 0>(slot, w, lane, pf);
+
+// Chunk boundary: wait for this wave's DMAs of the chunk about to be read (all but the
+// DIST-1 younger chunks' PF_N each), drain LDS reads, barrier; then start the DMA that is
+// DIST chunks ahead into the slot read one chunk ago.
+template <int N>
+__device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz) {
+    static_assert((DIST - 1) * PF_N == 2, "vmcnt immediate below assumes 2 younger DMAs");
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int tgt = slot + DIST;
+    tgt = tgt >= NSLOT ? tgt - NSLOT : tgt;
+    dma_chunk<(N + DIST) % NCHUNK>(wb, lds + tgt * SLOT_BYTES, w, lane, lz);
 }
 
-// One pass of a layer, k-outer: acc[t] += W[4P+t][k] * in(k) for every k-step, chunk by chunk.
+__device__ __forceinline__ float lrelu_max(float x) {
+    return __builtin_amdgcn_fmed3f(x, 0.01f * x, __builtin_inff());
+}
+
+// One pass of a layer, k-outer: acc[t] = bias + sum_k W[TP*P+t][k] * in(k), chunk by chunk.
 template <int L, int P, class InFn>
 __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
-                                         f32x16 (&acc)[TP], InFn &&in) {
+                                         const float *Fl, size_t fb, f32x16 (&acc)[layer_tp(L)], InFn &&in) {
+    constexpr int TP = layer_tp(L), KC = layer_kc(L);
+    const int h = lane >> 5;
 #pragma unroll
-    for (int t = 0; t < TP; ++t) acc[t] = f32x16{};
+    for (int tt = 0; tt < TP; ++tt) {  // accumulators start at the bias (acc order, LDS)
+        const f32x4 *b = (const f32x4 *)(Fl + fb + ((TP * P + tt) * 2 + h) * 16);
+        const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+        acc[tt] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                         b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+    }
     static_for<layer_nch(L)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
-        __syncthreads();
-        u32x4 pf[PF_N];
-        pf_load_next<L, P, C>(wb, w, lane, lz, pf);
+        chunk_enter<chunk_index(L, P, C)>(wb, lds, slot, w, lane, lz);
         const char *sl = lds + slot * SLOT_BYTES;
         static_for<chunk_nk(L, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
@@ -288,28 +332,22 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
                 acc[t] = mfma32(A, B, acc[t]);
             }
         });
-        slot ^= 1;
-        pf_commit_next<L, P, C>(lds + slot * SLOT_BYTES, w, lane, pf);
+        slot = slot + 1 == NSLOT ? 0 : slot + 1;
         __builtin_amdgcn_sched_barrier(0);
     });
 }
 
-// bias + LeakyReLU + fp16 pack: pass P accumulators -> next-layer fragments 8P..8P+7
-template <int P>
-__device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], const float *Fl, size_t fb, int h,
-                                          h8 (&out)[16]) {
+// LeakyReLU + fp16 pack: pass accumulators (bias included) -> next-layer fragments
+template <int TP, int P>
+__device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]) {
 #pragma unroll
     for (int tt = 0; tt < TP; ++tt)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-            const int t = TP * P + tt;
-            const f32x4 b0 = *(const f32x4 *)(Fl + fb + (t * 2 + h) * 16 + 8 * s2);
-            const f32x4 b1 = *(const f32x4 *)(Fl + fb + (t * 2 + h) * 16 + 8 * s2 + 4);
-            const int r = 8 * s2;
-            out[2 * t + s2] = pack8(lrelu(acc[tt][r + 0] + b0[0]), lrelu(acc[tt][r + 1] + b0[1]),
-                                    lrelu(acc[tt][r + 2] + b0[2]), lrelu(acc[tt][r + 3] + b0[3]),
-                                    lrelu(acc[tt][r + 4] + b1[0]), lrelu(acc[tt][r + 5] + b1[1]),
-                                    lrelu(acc[tt][r + 6] + b1[2]), lrelu(acc[tt][r + 7] + b1[3]));
+            const int t = TP * P + tt, r = 8 * s2;
+            out[2 * t + s2] = pack8(lrelu_max(acc[tt][r + 0]), lrelu_max(acc[tt][r + 1]), lrelu_max(acc[tt][r + 2]),
+                                    lrelu_max(acc[tt][r + 3]), lrelu_max(acc[tt][r + 4]), lrelu_max(acc[tt][r + 5]),
+                                    lrelu_max(acc[tt][r + 6]), lrelu_max(acc[tt][r + 7]));
         }
 }
 
@@ -392,17 +430,20 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     const int end = min(nwork, a.item0 + a.n_items);
     const Cam cam = load_cam(a.campos, a.rot);
     const WBlob wb = make_blob(a.blob);
+    const __amdgpu_buffer_rsrc_t fs_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.fs, (short)0, 0x7fffffff, 0x00020000);
     {   // fp32 parameters (biases, alpha weights) -> LDS once
         const float *src = (const float *)((const char *)a.blob + OFF_F32);
         float *dst = (float *)(lds + LDS_F32_OFF);
         for (int i = threadIdx.x; i < (int)N_F32; i += ROWS_TPB) dst[i] = src[i];
     }
+    __syncthreads();  // parameters visible before the first tile's bias reads
     int slot = 0;
-    {
-        u32x4 pf[PF_N];
-        pf_load<0, 0, 0>(wb, w, lane, 0, pf);
-        pf_commit<0, 0>(lds, w, lane, pf);
-    }
+    // stream prologue: chunks 0..DIST-1 in flight (chunk_enter<n> issues chunk n+DIST)
+    static_for<DIST>([&](auto nn) {
+        constexpr int N0 = decltype(nn)::value;
+        dma_chunk<N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
+    });
     for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
         // opaque zero per iteration: keeps LDS parameter reads and weight offsets inside the loop
         int lz = 0;
@@ -413,67 +454,70 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         float feat[16], dist[3];
         h8 ext;
         const RowIn ri = gather_row(a, cam, item, end, lane, feat, dist, ext);
-        f32x16 acc[TP];
         h8 actA[16], actB[16];
-        auto l0in = [&](auto k) { return l0_step<decltype(k)::value>(feat, dist); };
-        // block1.0: 284 -> 256 (inputs generated per k-step)
-        run_pass<0, 0>(wb, ldsi, slot, w, lane, lz, acc, l0in);
-        chain_out<0>(acc, Fl, F_B0, h, actA);
-        run_pass<0, 1>(wb, ldsi, slot, w, lane, lz, acc, l0in);
-        chain_out<1>(acc, Fl, F_B0, h, actA);
+        {   // block1.0: 284 -> 256, one pass over 8 tiles, inputs generated per k-step
+            f32x16 acc0[8];
+            run_pass<0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0,
+                           [&](auto k) { return l0_step<decltype(k)::value>(feat, dist); });
+            chain_out<8, 0>(acc0, actA);
+        }
+        f32x16 acc[4];
         // block1.2: 256 -> 256
         auto inA = [&](auto k) { return actA[decltype(k)::value]; };
-        run_pass<1, 0>(wb, ldsi, slot, w, lane, lz, acc, inA);
-        chain_out<0>(acc, Fl, F_B1, h, actB);
-        run_pass<1, 1>(wb, ldsi, slot, w, lane, lz, acc, inA);
-        chain_out<1>(acc, Fl, F_B1, h, actB);
+        run_pass<1, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
+        chain_out<4, 0>(acc, actB);
+        run_pass<1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
+        chain_out<4, 1>(acc, actB);
         // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256
         auto inB = [&](auto k) {
             constexpr int K = decltype(k)::value;
             if constexpr (K < 16) return actB[K]; else return ext;
         };
-        run_pass<2, 0>(wb, ldsi, slot, w, lane, lz, acc, inB);
-        chain_out<0>(acc, Fl, F_B2, h, actA);
-        run_pass<2, 1>(wb, ldsi, slot, w, lane, lz, acc, inB);
-        chain_out<1>(acc, Fl, F_B2, h, actA);
+        run_pass<2, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, inB);
+        chain_out<4, 0>(acc, actA);
+        run_pass<2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, inB);
+        chain_out<4, 1>(acc, actA);
         // block3.2: 256 -> 256, then alpha + K-blend, one pass of 4 output tiles at a time
         float apart = 0.f;
-        _Float16 *fsrow = a.fs + (int64_t)(item - a.item0) * HID;
+        const int fs_row = (item - a.item0) * HID * 2;  // byte offset of this row's blended features
         auto l3_epilogue = [&](auto pp) {
-            constexpr int P = decltype(pp)::value;
+            constexpr int P = decltype(pp)::value, TP = 4;
 #pragma unroll
             for (int tt = 0; tt < TP; ++tt) {
                 const int t = TP * P + tt;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const f32x4 b = *(const f32x4 *)(Fl + F_B3 + (t * 2 + h) * 16 + 4 * g);
                     const f32x4 wa = *(const f32x4 *)(Fl + F_WA + (t * 2 + h) * 16 + 4 * g);
                     float v[4];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        v[e] = lrelu(acc[tt][4 * g + e] + b[e]);
+                        v[e] = lrelu_max(acc[tt][4 * g + e]);
                         apart = fmaf(wa[e], v[e], apart);
                         v[e] = dpp_sum8(ri.wgt * v[e]);
                     }
                     // lane kk == g of the sample stores units 32t + 8g + 4h + (0..3)
                     if (ri.sval && kk == g) {
-                        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-                        h4 o = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
-                        *(h4 *)(fsrow + 32 * t + 8 * g + 4 * h) = o;
+                        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+                        const h2 o0 = {(_Float16)v[0], (_Float16)v[1]}, o1 = {(_Float16)v[2], (_Float16)v[3]};
+                        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                        const u32x2 o = {__builtin_bit_cast(uint32_t, o0), __builtin_bit_cast(uint32_t, o1)};
+                        __builtin_amdgcn_raw_buffer_store_b64(o, fs_rsrc, fs_row + (32 * t + 8 * g + 4 * h) * 2, 0, 0);
                     }
                 }
             }
         };
         auto inA3 = [&](auto k) { return actA[decltype(k)::value]; };
-        run_pass<3, 0>(wb, ldsi, slot, w, lane, lz, acc, inA3);
+        run_pass<3, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 0>{});
-        run_pass<3, 1>(wb, ldsi, slot, w, lane, lz, acc, inA3);
+        run_pass<3, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 1>{});
         const float araw = apart + __shfl_xor(apart, 32);
         const float alpha_row = softplus(araw + Fl[F_BA] - 1.f);
         const float alpha_s = dpp_sum8(ri.wgt * alpha_row);
         if (ri.sval && kk == 0 && h == 0) a.feat[(int64_t)ri.s * 4 + 0] = alpha_s;
     }
+    // the stream ran DIST chunks ahead: let those LDS-DMAs land before the workgroup retires
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 struct ColorArgs {
     const int32_t *counters, *work, *samp_ray;
@@ -568,7 +612,7 @@ int col_c0(int ks, int p) { return ks < 16 ? 16 * ks + p : (16 * (ks - 16) + p <
 // kouter: fragment (t, ks) at index ks*n_tiles + t (block1/block3 stream order), else t*KS + ks
 template <typename ColFn>
 void pack_frags(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles, int KS, ColFn col,
-                bool kouter) {
+                int kouter) {
     for (int t = 0; t < n_tiles; ++t)
         for (int ks = 0; ks < KS; ++ks)
             for (int lane = 0; lane < 64; ++lane)
@@ -576,8 +620,9 @@ void pack_frags(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles,
                     int row = 32 * t + (lane & 31);
                     int c = col(ks, 8 * (lane >> 5) + e);
                     float v = (row < n_out && c >= 0 && c < n_in) ? W[(size_t)row * n_in + c] : 0.f;
-                    // kouter: [pass = t/4][ks][t%4] (k-outer stream of k_agg_rows)
-                    size_t f = kouter ? ((size_t)(t / 4) * KS + ks) * 4 + (t % 4) : (size_t)t * KS + ks;
+                    // kouter > 0: [pass = t/kouter][ks][t%kouter] (k-outer stream of k_agg_rows)
+                    size_t f = kouter ? ((size_t)(t / kouter) * KS + ks) * kouter + (t % kouter)
+                                      : (size_t)t * KS + ks;
                     dst[(f * 64 + lane) * 8 + e] = (_Float16)v;
                 }
 }
@@ -601,13 +646,13 @@ int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, s
     SGN_REQUIRE(w && b && d_packed, "null argument");
     std::vector<uint8_t> blob(TOTAL_BYTES, 0);
     auto frag = [&](size_t off) { return (_Float16 *)(blob.data() + off); };
-    pack_frags(frag(OFF_W0), w[0], 256, 284, T_HID, KS_L0, col_l0, true);
-    pack_frags(frag(OFF_W1), w[1], 256, 256, T_HID, KS_HID, col_chain, true);
-    pack_frags(frag(OFF_W2), w[2], 256, 263, T_HID, KS_L2, col_l2, true);
-    pack_frags(frag(OFF_W3), w[3], 256, 256, T_HID, KS_HID, col_chain, true);
-    pack_frags(frag(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, col_c0, false);
-    pack_frags(frag(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, col_chain, false);
-    pack_frags(frag(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, col_chain, false);
+    pack_frags(frag(OFF_W0), w[0], 256, 284, T_HID, KS_L0, col_l0, layer_tp(0));
+    pack_frags(frag(OFF_W1), w[1], 256, 256, T_HID, KS_HID, col_chain, layer_tp(1));
+    pack_frags(frag(OFF_W2), w[2], 256, 263, T_HID, KS_L2, col_l2, layer_tp(2));
+    pack_frags(frag(OFF_W3), w[3], 256, 256, T_HID, KS_HID, col_chain, layer_tp(3));
+    pack_frags(frag(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, col_c0, 0);
+    pack_frags(frag(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, col_chain, 0);
+    pack_frags(frag(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, col_chain, 0);
     float *F = (float *)(blob.data() + OFF_F32);
     pack_acc_order(F + F_B0, b[0], T_HID);
     pack_acc_order(F + F_B1, b[1], T_HID);
