@@ -293,8 +293,11 @@ __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int
 // DIST chunks ahead into the slot read one chunk ago.
 template <int N>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz) {
-    static_assert((DIST - 1) * PF_N == 2, "vmcnt immediate below assumes 2 younger DMAs");
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    constexpr int younger = (DIST - 1) * PF_N;  // DMAs issued after this chunk's
+    static_assert(younger == 2 || younger == 4 || younger == 6, "add the vmcnt immediate");
+    if constexpr (younger == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     int tgt = slot + DIST;
@@ -302,9 +305,9 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
     dma_chunk<(N + DIST) % NCHUNK>(wb, lds + tgt * SLOT_BYTES, w, lane, lz);
 }
 
-__device__ __forceinline__ float lrelu_max(float x) {
-    return __builtin_amdgcn_fmed3f(x, 0.01f * x, __builtin_inff());
-}
+// LeakyReLU(0.01) = 0.505 x + 0.495 |x|: one v_mul with an |x| source modifier + one v_fma
+// (no compare/select, no NaN canonicalisation); within 1 ulp of max(x, 0.01x)
+__device__ __forceinline__ float lrelu_max(float x) { return __builtin_fmaf(0.505f, x, 0.495f * __builtin_fabsf(x)); }
 
 // One pass of a layer, k-outer: acc[t] = bias + sum_k W[TP*P+t][k] * in(k), chunk by chunk.
 template <int L, int P, class InFn>

@@ -15,7 +15,7 @@ for grp in \
   "FETCH_SIZE TCC_HIT_sum" \
   "WRITE_SIZE TCC_MISS_sum" ; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_agg_rows|k_knn|k_march|k_color|k_composite" \
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-k_agg_rows|k_knn|k_march|k_color|k_composite}" \
       -d "$OUT/p$i" -o pmc --output-format csv -- python bench.py $ARGS > "$OUT/p$i.log" 2>&1
 done
 echo PMC_DONE
