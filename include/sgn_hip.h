@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 1
+#define SGN_ABI_VERSION 2
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -136,17 +136,26 @@ typedef struct {
     /* camera */
     const float *campos;     /* [3] */
     const float *camrotc2w;  /* [3,3] row-major */
-    const float *raydir;     /* [R,3] */
+    const float *raydir;     /* [rows of samp_ray's index space, 3]: per-ray view directions */
+    /* optional precomputed camera-space ("pers") coordinates -- the compatibility path
+     * (PointAggregator.forward on pre-gathered tensors) receives them from the caller;
+     * NULL = compute from xyz and the camera (neural_points.py:838-850).  campos and
+     * camrotc2w must still be valid pointers (unused values when pers is given). */
+    const float *pers;       /* [N,3] or NULL */
+    const float *samp_pers;  /* [S,3] or NULL (with pers) */
 } sgn_point_tables;
 
-/* out_feat: float4[S] = [alpha_s, r, g, b] for every sample id (samples with
- * no valid neighbour are written as zeros); also writes out_blend (optional,
- * may be NULL) float[S*K] = normalised weight * conf (reference `weight*conf_coefficient`). */
+/* out_feat: float4[S] = [alpha_s, r, g, b] for every work-list sample (samples
+ * without a valid neighbour are not written; the composite ignores them).
+ * Optional (NULL to skip): out_blend float[S*K] = normalised weight * conf
+ * (the reference's `weight * conf_coefficient`), out_wnorm float[S*K] = normalised
+ * weight alone (the reference's `weight` output, point_aggregators.py:946-958). */
 size_t sgn_aggregate_workspace_bytes(int64_t S);
 /* stages: bit 0 = per-neighbour MLP + K-blend (writes alpha), bit 1 = colour MLP (rgb). */
 int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
                   int32_t K, const void *d_packed_mlp, float *d_out_feat, float *d_out_blend,
-                  void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream);
+                  float *d_out_wnorm, void *d_workspace, size_t workspace_bytes, int32_t stages,
+                  sgn_stream_t stream);
 
 /* ---- composite --------------------------------------------------------- */
 
@@ -159,11 +168,20 @@ typedef struct {
 
 /* Per ray: out_rgb float[R*3] (bg for invalid rays), out_mask int8[R]
  * (reference ray_mask after masked_valid_ray), out_bgT float[R] (background
- * transmission; 1 for invalid rays), out_opacity float[R*SR] (may be NULL). */
+ * transmission; 1 for invalid rays), out_opacity / out_blendw float[R*SR]
+ * (opacity and alpha-blend weight per slot; may be NULL). */
 int sgn_composite(const sgn_composite_params *cp, const float *d_campos, const float *d_camrotc2w,
                   const float *d_raydir, int64_t R, const float *d_t_table, int32_t per_ray_t,
                   int32_t D, const sgn_query_out *q, const float *d_feat, float *d_out_rgb,
-                  int8_t *d_out_mask, float *d_out_bgT, float *d_out_opacity, sgn_stream_t stream);
+                  int8_t *d_out_mask, float *d_out_bgT, float *d_out_opacity, float *d_out_blendw,
+                  sgn_stream_t stream);
+
+/* ray_march on dense [R, SR] inputs (diff_ray_marching.py:509-555, alpha blend +
+ * radiance render): ray_dist/valid/feat(float4) in, rgb[R*3] (+ bg*T if bg != NULL,
+ * host pointer to 3 floats), opacity/acc_transmission/blend_weight[R*SR], bg T[R]. */
+int sgn_ray_march_dense(const float *d_ray_dist, const uint8_t *d_valid, const float *d_feat, int64_t R,
+                        int32_t SR, const float *bg, float *d_rgb, float *d_opacity, float *d_acc_t,
+                        float *d_blendw, float *d_bgT, sgn_stream_t stream);
 
 /* ---- misc -------------------------------------------------------------- */
 int sgn_abi_version(void);

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -42,7 +42,7 @@ class QueryOut(ctypes.Structure):
 class PointTables(ctypes.Structure):
     _fields_ = [("xyz", c_vp), ("embedding", c_vp), ("color", c_vp), ("dir", c_vp),
                 ("conf", c_vp), ("n_points", c_i64), ("campos", c_vp), ("camrotc2w", c_vp),
-                ("raydir", c_vp)]
+                ("raydir", c_vp), ("pers", c_vp), ("samp_pers", c_vp)]
 
 
 class CompositeParams(ctypes.Structure):
@@ -64,9 +64,11 @@ SIGNATURES = {
     "sgn_mlp_pack": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
     "sgn_aggregate_workspace_bytes": (c_sz, [c_i64]),
     "sgn_aggregate": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,
-                              c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
+                              c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
-                              c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                              c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_ray_march_dense": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.POINTER(c_f32), c_vp, c_vp, c_vp,
+                                    c_vp, c_vp, c_vp]),
 }
 
 

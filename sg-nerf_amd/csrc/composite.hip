@@ -22,7 +22,7 @@ struct CompArgs {
     int64_t R;
     int SR, unit;
     float vz, bg0, bg1, bg2;
-    float *out_rgb, *out_bgT, *out_opacity;
+    float *out_rgb, *out_bgT, *out_opacity, *out_blendw;
     int8_t *out_mask;
 };
 
@@ -55,6 +55,7 @@ __global__ __launch_bounds__(256) void k_composite(CompArgs a) {
             cg += pf.z * wgt;
             cb += pf.w * wgt;
         }
+        if (a.out_blendw) a.out_blendw[r * a.SR + slot] = wgt;
         T = T * (1.f - o + 1e-10f);
         if (a.out_opacity) a.out_opacity[r * a.SR + slot] = o;
     };
@@ -83,13 +84,68 @@ __global__ __launch_bounds__(256) void k_composite(CompArgs a) {
     if (a.out_bgT) a.out_bgT[r] = any_valid ? T : 1.f;
 }
 
+// ---- dense ray_march (compatibility sub-boundary, diff_ray_marching.py:509-555) ----------
+struct MarchArgs {
+    const float *ray_dist, *feat;
+    const uint8_t *valid;
+    int64_t R;
+    int SR;
+    float bg0, bg1, bg2;
+    int has_bg;
+    float *rgb, *opacity, *acc_t, *blendw, *bgT;
+};
+
+__global__ __launch_bounds__(256) void k_ray_march_dense(MarchArgs a) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= a.R) return;
+    float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
+    for (int s = 0; s < a.SR; ++s) {
+        const int64_t i = r * a.SR + s;
+        const float v = a.valid[i] ? 1.f : 0.f;
+        const float4 f = *(const float4 *)(a.feat + i * 4);
+        const float sigma = f.x * v;
+        const float o = 1.f - expf(-sigma * a.ray_dist[i]);
+        const float wgt = o * T;
+        cr += f.y * wgt;
+        cg += f.z * wgt;
+        cb += f.w * wgt;
+        a.opacity[i] = o;
+        a.acc_t[i] = T;
+        a.blendw[i] = wgt;
+        T = T * (1.f - o + 1e-10f);
+    }
+    a.bgT[r] = T;
+    a.rgb[r * 3 + 0] = cr + (a.has_bg ? a.bg0 * T : 0.f);
+    a.rgb[r * 3 + 1] = cg + (a.has_bg ? a.bg1 * T : 0.f);
+    a.rgb[r * 3 + 2] = cb + (a.has_bg ? a.bg2 * T : 0.f);
+}
+
 }  // namespace
 }  // namespace sgn
+
+extern "C" int sgn_ray_march_dense(const float *d_ray_dist, const uint8_t *d_valid, const float *d_feat,
+                                   int64_t R, int32_t SR, const float *bg, float *d_rgb, float *d_opacity,
+                                   float *d_acc_t, float *d_blendw, float *d_bgT, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(d_ray_dist && d_valid && d_feat && d_rgb && d_opacity && d_acc_t && d_blendw && d_bgT,
+                "null argument");
+    SGN_REQUIRE(SR > 0, "SR must be positive");
+    if (R == 0) return 0;
+    MarchArgs a;
+    a.ray_dist = d_ray_dist; a.valid = d_valid; a.feat = d_feat; a.R = R; a.SR = SR;
+    a.has_bg = bg != nullptr;
+    a.bg0 = bg ? bg[0] : 0.f; a.bg1 = bg ? bg[1] : 0.f; a.bg2 = bg ? bg[2] : 0.f;
+    a.rgb = d_rgb; a.opacity = d_opacity; a.acc_t = d_acc_t; a.blendw = d_blendw; a.bgT = d_bgT;
+    hipLaunchKernelGGL(k_ray_march_dense, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
 
 extern "C" int sgn_composite(const sgn_composite_params *cp, const float *d_campos, const float *d_camrotc2w,
                              const float *d_raydir, int64_t R, const float *d_t_table, int32_t per_ray_t,
                              int32_t D, const sgn_query_out *q, const float *d_feat, float *d_out_rgb,
-                             int8_t *d_out_mask, float *d_out_bgT, float *d_out_opacity, sgn_stream_t stream) {
+                             int8_t *d_out_mask, float *d_out_bgT, float *d_out_opacity, float *d_out_blendw,
+                             sgn_stream_t stream) {
     using namespace sgn;
     (void)d_t_table; (void)per_ray_t; (void)D;
     SGN_REQUIRE(cp && q && d_feat && d_out_rgb && d_out_mask, "null argument");
@@ -102,6 +158,7 @@ extern "C" int sgn_composite(const sgn_composite_params *cp, const float *d_camp
     a.R = R; a.SR = cp->SR; a.unit = cp->raydist_mode_unit; a.vz = cp->vsize_z;
     a.bg0 = cp->bg[0]; a.bg1 = cp->bg[1]; a.bg2 = cp->bg[2];
     a.out_rgb = d_out_rgb; a.out_bgT = d_out_bgT; a.out_opacity = d_out_opacity; a.out_mask = d_out_mask;
+    a.out_blendw = d_out_blendw;
     hipLaunchKernelGGL(k_composite, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;

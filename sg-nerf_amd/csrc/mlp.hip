@@ -115,6 +115,7 @@ struct AggArgs {
     // point tables
     const float *xyz, *emb, *color, *dir, *conf;
     const float *campos, *rot, *raydir;
+    const float *pers, *samp_pers;  // optional precomputed pers coordinates
     // query
     const int32_t *counters, *work, *samp_ray, *pidx;
     const float *samp_locw;
@@ -123,6 +124,7 @@ struct AggArgs {
     // outputs
     float *feat;      // float4 per sample id: .x alpha written here
     float *blend;     // [S*8] weight * conf (optional)
+    float *wnorm;     // [S*8] normalised weight (optional)
     _Float16 *fs;     // [chunk][256] blended features (natural unit order)
     int32_t item0, n_items;  // work-list chunk
 };
@@ -398,8 +400,13 @@ __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, in
     dist[0] = m ? dwx : 0.f; dist[1] = m ? dwy : 0.f; dist[2] = m ? dwz : 0.f;
     if (h == 1) {
         float xp = 0.f, yp = 0.f, zp = 0.f, xl, yl, zl;
-        if (m) cam.pers(px, py, pz, xp, yp, zp);
-        cam.pers(lx, ly, lz, xl, yl, zl);
+        if (a.pers) {
+            if (m) { xp = a.pers[(int64_t)pid * 3]; yp = a.pers[(int64_t)pid * 3 + 1]; zp = a.pers[(int64_t)pid * 3 + 2]; }
+            xl = a.samp_pers[(int64_t)s * 3]; yl = a.samp_pers[(int64_t)s * 3 + 1]; zl = a.samp_pers[(int64_t)s * 3 + 2];
+        } else {
+            if (m) cam.pers(px, py, pz, xp, yp, zp);
+            cam.pers(lx, ly, lz, xl, yl, zl);
+        }
         dist[0] = m ? __fsub_rn(__fmul_rn(xp, zp), __fmul_rn(xl, zl)) : 0.f;
         dist[1] = m ? __fsub_rn(__fmul_rn(yp, zp), __fmul_rn(yl, zl)) : 0.f;
         dist[2] = m ? __fsub_rn(zp, zl) : 0.f;
@@ -414,6 +421,7 @@ __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, in
     w = w / fmaxf(wsum, 1e-8f);
     ri.wgt = w * fminf(fmaxf(cf, 1e-4f), 1.f);
     if (a.blend && ri.sval && h == 0) a.blend[(int64_t)s * 8 + kk] = ri.wgt;
+    if (a.wnorm && ri.sval && h == 1) a.wnorm[(int64_t)s * 8 + kk] = w;
     // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane-half 0 only
     h8 e = {};
     if (h == 0 && m) {
@@ -684,8 +692,8 @@ size_t sgn_aggregate_workspace_bytes(int64_t S) {
 }
 
 int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
-                  const void *d_packed, float *d_out_feat, float *d_out_blend, void *d_workspace,
-                  size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
+                  const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
+                  void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
     using namespace sgn;
     using namespace sgn::mlp;
     SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace, "null argument");
@@ -697,10 +705,13 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
     AggArgs a;
     a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
     a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
+    a.pers = pt->pers; a.samp_pers = pt->samp_pers;
+    SGN_REQUIRE((pt->pers == nullptr) == (pt->samp_pers == nullptr), "pers and samp_pers go together");
+    SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir, "camera (campos, camrotc2w, raydir) required");
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
     a.blob = P;
-    a.feat = d_out_feat; a.blend = d_out_blend; a.fs = (_Float16 *)d_workspace;
+    a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
     ColorArgs c;
     c.counters = q->counters; c.work = q->work; c.samp_ray = q->samp_ray; c.raydir = pt->raydir;
     c.blob = P; c.fs = a.fs; c.feat = d_out_feat;

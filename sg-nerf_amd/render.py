@@ -12,7 +12,7 @@ import torch
 from . import _lib
 from .opts import HotPathOpts
 from .querier import LightningFastQuerier
-from .weights import pack_mlp
+from .weights import pack_mlp, strip_prefix
 
 
 @dataclass
@@ -23,7 +23,9 @@ class RenderOut:
     opacity: torch.Tensor    # [R,SR] coarse_point_opacity (0 for invalid rays / empty slots)
     query: object            # QueryResult (sample-major, device)
     feat: torch.Tensor       # [S_cap,4] per-sample (alpha, r, g, b)
-    blend: torch.Tensor      # [S_cap,8] weight * conf_coefficient
+    blend: torch.Tensor      # [S_cap,8] weight * conf_coefficient (when want_blend)
+    wnorm: torch.Tensor = None    # [S_cap,8] normalised weight (when want_weights)
+    blendw: torch.Tensor = None   # [R,SR] alpha-blend weight o*T (when want_weights)
 
 
 class PointTables:
@@ -51,11 +53,13 @@ class HipRenderer:
         self.opts = opts.check_supported()
         self.points = points
         self.querier = LightningFastQuerier(self.device, opts)
-        self.packed = pack_mlp(mlp_state, self.device)
+        self.set_mlp(mlp_state)
         self._cap = None
 
     def set_mlp(self, mlp_state):
-        self.packed = pack_mlp(mlp_state, self.device)
+        self.mlp_state = {k: torch.as_tensor(v).detach().to("cpu", torch.float32)
+                          for k, v in strip_prefix(mlp_state).items()}
+        self.packed = pack_mlp(self.mlp_state, self.device)
 
     def _buffers(self, R):
         SR = self.opts.SR
@@ -70,11 +74,16 @@ class HipRenderer:
             self.mask = torch.empty(max(R, 1), dtype=torch.int8, device=dev)
             self.bgT = torch.empty(max(R, 1), dtype=torch.float32, device=dev)
             self.opacity = torch.empty(max(R, 1), SR, dtype=torch.float32, device=dev)
+            self.wnorm = None
+            self.blendw = None
             self._cap = (R, cap)
 
-    def render(self, campos, camrotc2w, raydir, near, far, want_opacity=True, want_blend=False, marks=None):
+    def render(self, campos, camrotc2w, raydir, near, far, want_opacity=True, want_blend=False, marks=None,
+               bg=None, want_weights=False):
         """One frame.  `marks(name)` (optional) is called between stages on the host thread
-        (bench.py records HIP events on the current stream there)."""
+        (bench.py records HIP events on the current stream there).  `bg`: 3 floats
+        overriding opts.bg_color.  `want_weights`: also produce the normalised neighbour
+        weights and the per-slot alpha-blend weights (reference `weight`, `blend_weight`)."""
         o = self.opts
         mark = marks or (lambda name: None)
         campos = campos.reshape(3).to(self.device, torch.float32).contiguous()
@@ -82,6 +91,11 @@ class HipRenderer:
         raydir = raydir.reshape(-1, 3).to(self.device, torch.float32).contiguous()
         R = raydir.shape[0]
         self._buffers(R)
+        if want_weights and self.wnorm is None:
+            self.wnorm = torch.empty(self._cap[1], 8, dtype=torch.float32, device=self.device)
+            self.blendw = torch.empty(max(self._cap[0], 1), o.SR, dtype=torch.float32, device=self.device)
+        if want_weights:
+            self.wnorm.zero_()
         mark("query")
         q = self.querier.query_samples(self.points.xyz, campos, raydir, near, far)
         L = _lib.lib()
@@ -96,19 +110,23 @@ class HipRenderer:
             mark(name)
             _lib.check(L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), cap, o.K, _lib.ptr(self.packed),
                                        _lib.ptr(self.feat), _lib.ptr(self.blend) if want_blend else None,
+                                       _lib.ptr(self.wnorm) if want_weights and stage == 1 else None,
                                        _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate")
         mark("composite")
         cp = _lib.CompositeParams()
         cp.SR, cp.vsize_z, cp.raydist_mode_unit = o.SR, float(o.vsize[2]), o.raydist_mode_unit
-        bg = (1.0, 1.0, 1.0) if o.bg_color == "white" else (0.0, 0.0, 0.0)
+        if bg is None:
+            bg = (1.0, 1.0, 1.0) if o.bg_color == "white" else (0.0, 0.0, 0.0)
         for i in range(3):
             cp.bg[i] = bg[i]
         _lib.check(L.sgn_composite(ctypes.byref(cp), _lib.ptr(campos), _lib.ptr(rot), _lib.ptr(raydir), R,
                                    _lib.ptr(q.t_table), q.per_ray_t, q.t_table.shape[-1], ctypes.byref(qo),
                                    _lib.ptr(self.feat), _lib.ptr(self.rgb), _lib.ptr(self.mask), _lib.ptr(self.bgT),
-                                   _lib.ptr(self.opacity) if want_opacity else None, st), "sgn_composite")
+                                   _lib.ptr(self.opacity) if want_opacity else None,
+                                   _lib.ptr(self.blendw) if want_weights else None, st), "sgn_composite")
         mark("end")
-        return RenderOut(self.rgb[:R], self.mask[:R], self.bgT[:R], self.opacity[:R], q, self.feat, self.blend)
+        return RenderOut(self.rgb[:R], self.mask[:R], self.bgT[:R], self.opacity[:R], q, self.feat, self.blend,
+                         self.wnorm if want_weights else None, self.blendw[:R] if want_weights else None)
 
     def grid_info(self):
         return self.querier.grid_for(self.points.xyz).info()

@@ -25,3 +25,25 @@ def run_smoke():
     assert np.array_equal(pidx, ref["pidx"]), "smoke: neighbour indices differ from the oracle"
     assert (pidx >= 0).sum() > 0
     print(f"smoke OK: {R} rays, {int((pidx >= 0).sum())} neighbour indices bit-exact")
+
+    # full hot path through the reference operator API (query -> MFMA aggregator ->
+    # composite) against the oracle's torch restatement
+    import agg_ref
+    from sgnerf_amd.ray_marching import NeuralPoints, NeuralPointsRayMarching
+    from sgnerf_amd.weights import init_mlp
+    mlp = init_mlp(0, bias_std=0.01)
+    mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 100.0
+    net = NeuralPointsRayMarching(NeuralPoints.from_cloud(pc, dev), mlp, o, dev)
+    d = lambda a: torch.from_numpy(a).to(dev)[None]  # noqa: E731
+    out = net.render({"campos": d(view.campos), "raydir": d(view.raydir), "camrotc2w": d(view.camrotc2w),
+                      "near": 0.1, "far": 8.0})
+    qs = oq.OracleGrid(pc.xyz, hy, o).query(view.campos, view.raydir, t.numpy())
+    tp = {k: torch.from_numpy(getattr(pc, k)) for k in ("xyz", "embedding", "color", "dir", "conf")}
+    with torch.no_grad():
+        full, mask, _, _, _ = agg_ref.render(tp, mlp, torch.from_numpy(view.campos), torch.from_numpy(view.camrotc2w),
+                                             torch.from_numpy(view.raydir), qs, o.SR)
+    rgb = out["coarse_raycolor"][0].cpu()
+    assert torch.equal(out["ray_mask"][0].cpu().bool(), mask), "smoke: ray_mask differs from the oracle"
+    err = float((rgb - full).abs().max())
+    assert err <= 1e-3, f"smoke: rgb differs from the oracle by {err:.3e}"
+    print(f"smoke OK: rendered {R} rays, {int(mask.sum())} valid, max |rgb - oracle| = {err:.2e}")

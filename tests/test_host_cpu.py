@@ -1,0 +1,161 @@
+"""CPU tests of the host side: the C ABI surface (library loads, exports every symbol
+include/sgn_hip.h declares, validates its arguments before touching the GPU), the
+option/hyper-parameter logic, weight handling and the reference bookkeeping
+(fill_invalid, ray-slot densification) that runs in torch around the kernels."""
+import argparse
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from sgnerf_amd import _lib, raygen
+from sgnerf_amd.hyper import grid_hyperparameters
+from sgnerf_amd.opts import HotPathOpts
+from sgnerf_amd.ray_marching import _dense_from_samples, fill_invalid
+from sgnerf_amd.weights import LAYERS, N_PARAMS, check_shapes, init_mlp, strip_prefix
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "sgn_hip.h")
+
+
+def _header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \t\*]*?\b(sgn_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = _header_functions()
+    for n in ("sgn_grid_build", "sgn_grid_free", "sgn_query", "sgn_aggregate", "sgn_composite",
+              "sgn_ray_march_dense", "sgn_mlp_pack", "sgn_abi_version", "sgn_last_error"):
+        assert n in names
+    assert set(names) == set(_lib.SIGNATURES), "ctypes SIGNATURES must bind exactly what the header declares"
+
+
+def test_library_loads_and_exports_every_symbol():
+    L = _lib.lib()
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    for n in _header_functions():
+        assert hasattr(raw, n), f"libsgn_hip.so does not export {n}"
+    v = int(re.search(r"#define SGN_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert L.sgn_abi_version() == v == _lib.ABI_VERSION
+
+
+def test_sizing_functions():
+    L = _lib.lib()
+    assert L.sgn_mlp_packed_bytes() > 2 * N_PARAMS  # fp16 fragments (+ padding) + fp32 params
+    assert L.sgn_query_workspace_bytes(2000) >= L.sgn_query_workspace_bytes(1000) > 0
+    assert L.sgn_aggregate_workspace_bytes(10_000) >= 10_000 * 256 * 2
+
+
+def test_argument_errors_are_reported_without_gpu():
+    """Parameter validation runs before any HIP call: bad arguments give rc < 0 and a message."""
+    L = _lib.lib()
+    fake = ctypes.c_void_p(16)
+    pt, qo = _lib.PointTables(), _lib.QueryOut()
+    for f in ("xyz", "embedding", "color", "dir", "conf", "campos", "camrotc2w", "raydir"):
+        setattr(pt, f, 16)
+    rc = L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), 64, 4, fake, fake, None, None, fake, 1 << 20, 3, None)
+    assert rc != 0 and b"K = 8" in L.sgn_last_error()
+    with pytest.raises(_lib.SgnError, match="K = 8"):
+        _lib.check(rc, "sgn_aggregate")
+    cp = _lib.CompositeParams()
+    cp.SR = 0
+    rc = L.sgn_composite(ctypes.byref(cp), fake, fake, fake, 4, fake, 0, 400, ctypes.byref(qo), fake, fake, fake,
+                         fake, None, None, None)
+    assert rc != 0 and b"SR" in L.sgn_last_error()
+    rc = L.sgn_ray_march_dense(None, None, None, 4, 8, None, None, None, None, None, None, None)
+    assert rc != 0 and b"null" in L.sgn_last_error()
+    rc = L.sgn_grid_build(None, 10, None, None, ctypes.byref(ctypes.c_void_p()))
+    assert rc != 0
+
+
+# ---- options ------------------------------------------------------------------------
+def test_opts_from_reference_namespace():
+    ns = argparse.Namespace(SR=24, K=8, vsize=[0.008, 0.008, 0.008], kernel_size=[3, 3, 3], query_size=[0, 0, 0],
+                            z_depth_dim=400, bg_color="white", unrelated_flag=7)
+    o = HotPathOpts.from_opt(ns)
+    assert o.vsize == (0.008, 0.008, 0.008) and o.query_size == (3, 3, 3)  # neural_points.py:425
+    assert o.check_supported() is o
+    with pytest.raises(NotImplementedError, match="block2_bpnet"):
+        HotPathOpts(shading_feature_mlp_layer2_bpnet=1).check_supported()
+    with pytest.raises(NotImplementedError, match="agg_dist_pers"):
+        HotPathOpts(agg_dist_pers=10).check_supported()
+
+
+def test_grid_hyperparameters_scannet():
+    o = HotPathOpts()
+    mn = torch.tensor([0.0, 0.0, 0.0])
+    mx = torch.tensor([4.0, 4.0, 3.0])
+    h = grid_hyperparameters(o, mn, mx)
+    assert h.scaled_vsize.dtype == np.float32 and np.all(h.scaled_vsize == np.float32(0.016))
+    assert h.radius_limit == np.float32(0.032) and h.r2 == np.float32(np.float32(0.032) ** 2)
+    pad = np.float32(0.016 * 3 / 2)
+    np.testing.assert_array_equal(h.shift, (mn.numpy() - pad).astype(np.float32))
+    # ceil((max - min) / vsize / vscale) in float64 (worldcoords.py:85-86)
+    ext = (mx + float(pad)) - (mn - float(pad))
+    want = np.ceil(ext.numpy() / np.array(o.vsize) / np.array(o.vscale)).astype(np.int32)
+    np.testing.assert_array_equal(h.scaled_vdim, want)
+    assert h.volume == int(np.prod(want.astype(np.int64)))
+
+
+def test_depth_table_linear_and_jittered():
+    t = raygen.depth_table(0.1, 8.0, 400)
+    assert t.shape == (400,) and t.dtype == torch.float32
+    assert torch.all(t[1:] > t[:-1]) and 0.1 < float(t[0]) < float(t[-1]) < 8.0
+    g = torch.Generator().manual_seed(3)
+    tj = raygen.depth_table(0.1, 8.0, 400, jitter=0.3, R=5, generator=g)
+    assert tj.shape == (5, 400)
+    assert torch.all(tj[:, 1:] > tj[:, :-1])
+
+
+# ---- weights -------------------------------------------------------------------------
+def test_init_mlp_matches_reference_architecture():
+    st = init_mlp(0, bias_std=0.01)
+    assert sum(v.numel() for v in st.values()) == N_PARAMS == 341_764
+    check_shapes(st)
+    assert len(LAYERS) == 9
+    full = {"module.aggregator." + k: v for k, v in st.items()}
+    full["neural_points.xyz"] = torch.zeros(3, 3)
+    assert set(strip_prefix(full)) == set(st)
+    bad = dict(st)
+    bad["block1.0.weight"] = torch.zeros(256, 283)
+    with pytest.raises(ValueError):
+        check_shapes(bad)
+
+
+# ---- reference bookkeeping around the kernels ------------------------------------------
+def test_fill_invalid_expands_compacted_outputs():
+    R, SR = 6, 4
+    ray_mask = torch.tensor([[0, 1, 1, 0, 1, 0]], dtype=torch.int8)
+    n = 3
+    out = {"ray_mask": ray_mask,
+           "coarse_is_background": torch.full((1, n, 1), 0.25),
+           "coarse_raycolor": torch.arange(n * 3, dtype=torch.float32).view(1, n, 3),
+           "coarse_point_opacity": torch.full((1, n, SR), 0.5),
+           "queried_shading": torch.zeros(1, n, 3)}
+    res = fill_invalid(out, {"bg_color": torch.tensor([[0.2, 0.3, 0.4]])})
+    keep = ray_mask[0].bool()
+    assert res["coarse_raycolor"].shape == (1, R, 3)
+    torch.testing.assert_close(res["coarse_raycolor"][0, keep], torch.arange(9, dtype=torch.float32).view(3, 3))
+    torch.testing.assert_close(res["coarse_raycolor"][0, ~keep], torch.tensor([[0.2, 0.3, 0.4]] * 3))
+    assert torch.all(res["coarse_is_background"][0, ~keep] == 1) and torch.all(res["coarse_is_background"][0, keep] == 0.25)
+    torch.testing.assert_close(res["coarse_mask"], 1 - res["coarse_is_background"])
+    assert torch.all(res["coarse_point_opacity"][0, ~keep] == 0)
+    assert torch.all(res["queried_shading"][0, ~keep] == 1) and torch.all(res["queried_shading"][0, keep] == 0)
+
+
+def test_dense_from_samples():
+    class Q:
+        ray_ns = torch.tensor([2, 0, 3], dtype=torch.int32)
+        ray_soff = torch.tensor([0, 2, 2], dtype=torch.int32)
+    vals = torch.arange(5 * 2, dtype=torch.float32).view(5, 2)
+    d = _dense_from_samples(Q, vals, 3, 4, -1.0)
+    assert d.shape == (3, 4, 2)
+    torch.testing.assert_close(d[0, :2], vals[0:2])
+    assert torch.all(d[0, 2:] == -1) and torch.all(d[1] == -1)
+    torch.testing.assert_close(d[2, :3], vals[2:5])
+    assert torch.all(d[2, 3] == -1)
