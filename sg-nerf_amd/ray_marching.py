@@ -191,19 +191,20 @@ class NeuralPointsRayMarching:
         return weight, out.blendw[:R, :, None], conf_coef
 
     def render(self, inputs):
-        """Expanded outputs (what fill_invalid(forward(inputs)) gives), no host sync."""
+        """Expanded outputs (what fill_invalid(forward(inputs)) gives), no host sync.
+        Fresh tensors, as the reference returns (the renderer's buffers are reused)."""
         out, R = self._render(inputs, self.return_weights)
         res = {
-            "coarse_raycolor": out.rgb[None],
-            "coarse_point_opacity": out.opacity[None],
-            "coarse_is_background": out.bg_transmission[None, :, None],
+            "coarse_raycolor": out.rgb[None].clone(),
+            "coarse_point_opacity": out.opacity[None].clone(),
+            "coarse_is_background": out.bg_transmission[None, :, None].clone(),
             "queried_shading": (1 - out.ray_mask.float())[None, :, None].expand(1, R, 3).contiguous(),
-            "ray_mask": out.ray_mask[None],
+            "ray_mask": out.ray_mask[None].clone(),
         }
         res["coarse_mask"] = 1 - res["coarse_is_background"]
         if self.return_weights:
             w, bw, cc = self._weights(out, R)
-            res["weight"], res["blend_weight"], res["conf_coefficient"] = w[None], bw[None], cc[None]
+            res["weight"], res["blend_weight"], res["conf_coefficient"] = w[None], bw[None].clone(), cc[None]
         return res
 
     def forward(self, inputs, **kargs):
@@ -215,7 +216,7 @@ class NeuralPointsRayMarching:
             "coarse_point_opacity": out.opacity[keep][None],
             "queried_shading": torch.zeros(1, keep.numel(), 3, dtype=torch.float32, device=self.device),
             "coarse_is_background": out.bg_transmission[keep][None, :, None],
-            "ray_mask": out.ray_mask[None],
+            "ray_mask": out.ray_mask[None].clone(),
         }
         if self.return_weights:
             w, bw, cc = self._weights(out, R)
