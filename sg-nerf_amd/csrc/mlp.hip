@@ -312,17 +312,24 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
 __device__ __forceinline__ float lrelu_max(float x) { return __builtin_fmaf(0.505f, x, 0.495f * __builtin_fabsf(x)); }
 
 // One pass of a layer, k-outer: acc[t] = bias + sum_k W[TP*P+t][k] * in(k), chunk by chunk.
-template <int L, int P, class InFn>
+// TRANS: the activations are the A operand and the weights the B operand, so the
+// accumulators hold D^T (lane = output unit, registers = rows) and start at zero (the bias
+// is added in the epilogue, where it is one value per lane).
+template <int L, int P, bool TRANS = false, class InFn>
 __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
                                          const float *Fl, size_t fb, f32x16 (&acc)[layer_tp(L)], InFn &&in) {
     constexpr int TP = layer_tp(L), KC = layer_kc(L);
     const int h = lane >> 5;
 #pragma unroll
-    for (int tt = 0; tt < TP; ++tt) {  // accumulators start at the bias (acc order, LDS)
-        const f32x4 *b = (const f32x4 *)(Fl + fb + ((TP * P + tt) * 2 + h) * 16);
-        const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
-        acc[tt] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
-                         b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+    for (int tt = 0; tt < TP; ++tt) {
+        if constexpr (TRANS) {
+            acc[tt] = f32x16{};
+        } else {  // accumulators start at the bias (acc order, LDS)
+            const f32x4 *b = (const f32x4 *)(Fl + fb + ((TP * P + tt) * 2 + h) * 16);
+            const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+            acc[tt] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                             b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+        }
     }
     static_for<layer_nch(L)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
@@ -334,12 +341,22 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
 #pragma unroll
             for (int t = 0; t < TP; ++t) {
                 const h8 A = *(const h8 *)(sl + (KK * TP + t) * (int)FRAG + lane * 16);
-                acc[t] = mfma32(A, B, acc[t]);
+                acc[t] = TRANS ? mfma32(B, A, acc[t]) : mfma32(A, B, acc[t]);
             }
         });
         slot = slot + 1 == NSLOT ? 0 : slot + 1;
         __builtin_amdgcn_sched_barrier(0);
     });
+}
+
+// fp16 pack + LeakyReLU on the packed halves: v_cvt_pk_f16_f32, v_pk_mul_f16, v_pk_max_f16
+// (1.5 instructions per value; lrelu(fp16(x)) differs from fp16(lrelu(x)) only by the
+// rounding of 0.01x on negative inputs)
+__device__ __forceinline__ uint32_t lrelu_pk(float x0, float x1) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 v = {(_Float16)x0, (_Float16)x1};
+    const h2 sl = v * h2{(_Float16)0.01f, (_Float16)0.01f};
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, sl));
 }
 
 // LeakyReLU + fp16 pack: pass accumulators (bias included) -> next-layer fragments
@@ -350,9 +367,15 @@ __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
             const int t = TP * P + tt, r = 8 * s2;
+#if SGN_LRELU_F32
             out[2 * t + s2] = pack8(lrelu_max(acc[tt][r + 0]), lrelu_max(acc[tt][r + 1]), lrelu_max(acc[tt][r + 2]),
                                     lrelu_max(acc[tt][r + 3]), lrelu_max(acc[tt][r + 4]), lrelu_max(acc[tt][r + 5]),
                                     lrelu_max(acc[tt][r + 6]), lrelu_max(acc[tt][r + 7]));
+#else
+            const u32x4 u = {lrelu_pk(acc[tt][r + 0], acc[tt][r + 1]), lrelu_pk(acc[tt][r + 2], acc[tt][r + 3]),
+                             lrelu_pk(acc[tt][r + 4], acc[tt][r + 5]), lrelu_pk(acc[tt][r + 6], acc[tt][r + 7])};
+            out[2 * t + s2] = __builtin_bit_cast(h8, u);
+#endif
         }
 }
 
@@ -488,42 +511,85 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         chain_out<4, 0>(acc, actA);
         run_pass<2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, inB);
         chain_out<4, 1>(acc, actA);
-        // block3.2: 256 -> 256, then alpha + K-blend, one pass of 4 output tiles at a time
-        float apart = 0.f;
-        const int fs_row = (item - a.item0) * HID * 2;  // byte offset of this row's blended features
+        // block3.2: 256 -> 256, transposed (lane = output unit j = lane & 31 of tile t,
+        // register i = row (i & 3) + 8 (i >> 2) + 4h, i.e. sample i >> 2), so the K-blend
+        // and the alpha dot product are per-lane FMAs over registers
+        float wv[16];      // K-blend weight of the row in register i
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            wv[i] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
+                                                  ((i & 3) + 8 * (i >> 2) + 4 * h) * 4, __builtin_bit_cast(int, ri.wgt)));
+        float apart[16];   // alpha logit partial of row i over this lane's units
+#pragma unroll
+        for (int i = 0; i < 16; ++i) apart[i] = 0.f;
+        const int j = lane & 31;
         auto l3_epilogue = [&](auto pp) {
             constexpr int P = decltype(pp)::value, TP = 4;
 #pragma unroll
             for (int tt = 0; tt < TP; ++tt) {
                 const int t = TP * P + tt;
+                const float bu = Fl[F_B3 + 32 * t + j], wau = Fl[F_WA + 32 * t + j];
+                float fg[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x4 wa = *(const f32x4 *)(Fl + F_WA + (t * 2 + h) * 16 + 4 * g);
-                    float v[4];
+                for (int i = 0; i < 16; ++i) {
+                    const float y = acc[tt][i] + bu;
+                    const float hv = fmaxf(y, 0.01f * y);
+                    apart[i] = fmaf(wau, hv, apart[i]);
+                    fg[i >> 2] = fmaf(wv[i], hv, fg[i >> 2]);
+                }
+                // halves hold rows 4h..4h+3 of each sample: lanes 0-31 <- samples 0 / 2,
+                // lanes 32-63 <- samples 1 / 3 (v_permlane32_swap)
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        v[e] = lrelu_max(acc[tt][4 * g + e]);
-                        apart = fmaf(wa[e], v[e], apart);
-                        v[e] = dpp_sum8(ri.wgt * v[e]);
-                    }
-                    // lane kk == g of the sample stores units 32t + 8g + 4h + (0..3)
-                    if (ri.sval && kk == g) {
-                        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-                        const h2 o0 = {(_Float16)v[0], (_Float16)v[1]}, o1 = {(_Float16)v[2], (_Float16)v[3]};
-                        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                        const u32x2 o = {__builtin_bit_cast(uint32_t, o0), __builtin_bit_cast(uint32_t, o1)};
-                        __builtin_amdgcn_raw_buffer_store_b64(o, fs_rsrc, fs_row + (32 * t + 8 * g + 4 * h) * 2, 0, 0);
+                for (int k2 = 0; k2 < 2; ++k2) {
+                    const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, fg[2 * k2]),
+                                                                     __builtin_bit_cast(uint32_t, fg[2 * k2 + 1]),
+                                                                     false, false);
+                    const float tot = __builtin_bit_cast(float, sw[0]) + __builtin_bit_cast(float, sw[1]);
+                    const int g = h + 2 * k2, it = base + w * 4 + g;
+                    if (it < end) {
+                        const _Float16 hv16 = (_Float16)tot;
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, hv16), fs_rsrc,
+                                                              ((it - a.item0) * HID + 32 * t + j) * 2, 0, 0);
                     }
                 }
             }
         };
         auto inA3 = [&](auto k) { return actA[decltype(k)::value]; };
-        run_pass<3, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
+        run_pass<3, 0, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 0>{});
-        run_pass<3, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
+        run_pass<3, 1, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 1>{});
-        const float araw = apart + __shfl_xor(apart, 32);
-        const float alpha_row = softplus(araw + Fl[F_BA] - 1.f);
+        // alpha: reduce the 16 row partials over the 32 lanes (units) of each half,
+        // reduce-scatter style; lane j ends with row index i = 8 b1 + 4 b2 + 2 b3 + b4 (b = bits of j)
+        float bq[8];
+#pragma unroll
+        for (int p2 = 0; p2 < 8; ++p2) {  // lanes j, j^16 (v_permlane16_swap)
+            const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, apart[2 * p2]),
+                                                             __builtin_bit_cast(uint32_t, apart[2 * p2 + 1]), false,
+                                                             false);
+            bq[p2] = __builtin_bit_cast(float, sw[0]) + __builtin_bit_cast(float, sw[1]);
+        }
+        auto rs_step = [&](float lo, float hi, bool upper, auto ctrl) {
+            const float keep = upper ? hi : lo, send = upper ? lo : hi;
+            return keep + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send),
+                                                                             decltype(ctrl)::value, 0xF, 0xF, true));
+        };
+        float cq[4], dq[2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)  // lanes j, j^8 (row_ror:8)
+            cq[u] = rs_step(bq[2 * u], bq[2 * u + 1], (j & 8) != 0, std::integral_constant<int, 0x128>{});
+#pragma unroll
+        for (int v = 0; v < 2; ++v)  // lanes j, 7-j within 8 (row_half_mirror)
+            dq[v] = rs_step(cq[2 * v], cq[2 * v + 1], (j & 4) != 0, std::integral_constant<int, 0x141>{});
+        float eq = rs_step(dq[0], dq[1], (j & 2) != 0, std::integral_constant<int, 0x4E>{});  // j, j^2
+        eq += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, eq), 0xB1, 0xF, 0xF, true));
+        const float alpha_val = softplus(eq + Fl[F_BA] - 1.f);
+        // back to lane = row: row r lives in half (r >> 2) & 1 at register i = (r & 3) + 4 (r >> 3)
+        const int ri_ = (j & 3) + 4 * (j >> 3);
+        const int src = 32 * ((j >> 2) & 1) + 2 * ((ri_ >> 3) & 1) + 4 * ((ri_ >> 2) & 1) + 8 * ((ri_ >> 1) & 1) +
+                        16 * (ri_ & 1);
+        const float alpha_row =
+            __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src * 4, __builtin_bit_cast(int, alpha_val)));
         const float alpha_s = dpp_sum8(ri.wgt * alpha_row);
         if (ri.sval && kk == 0 && h == 0) a.feat[(int64_t)ri.s * 4 + 0] = alpha_s;
     }
@@ -668,11 +734,11 @@ int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, s
     pack_acc_order(F + F_B0, b[0], T_HID);
     pack_acc_order(F + F_B1, b[1], T_HID);
     pack_acc_order(F + F_B2, b[2], T_HID);
-    pack_acc_order(F + F_B3, b[3], T_HID);
+    for (int u = 0; u < HID; ++u) F[F_B3 + u] = b[3][u];  // natural order: block3.2 runs transposed
     pack_acc_order(F + F_CB0, b[5], T_CHID);
     pack_acc_order(F + F_CB1, b[6], T_CHID);
     pack_acc_order(F + F_CB2, b[7], T_CHID);
-    pack_acc_order(F + F_WA, w[4], T_HID);
+    for (int u = 0; u < HID; ++u) F[F_WA + u] = w[4][u];
     F[F_BA] = b[4][0];
     for (int c = 0; c < 3; ++c) {
         pack_acc_order(F + F_WC3 + c * 128, w[8] + c * 128, T_CHID);
