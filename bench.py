@@ -73,15 +73,37 @@ def cpu_baseline(pc, mlp, o, view, stride=4):
     og = oq.OracleGrid(pc.xyz, hy, o)
     t = depth_table(view.near, view.far, o.z_depth_dim).numpy()
     pts = {k: torch.from_numpy(getattr(pc, k)) for k in ("xyz", "embedding", "color", "dir", "conf")}
-    t0 = time.perf_counter()
-    q = og.query(view.campos, raydir, t)
-    with torch.no_grad():
-        agg_ref.render(pts, mlp, torch.from_numpy(view.campos), torch.from_numpy(view.camrotc2w),
-                       torch.from_numpy(raydir), q, o.SR)
-    dt = time.perf_counter() - t0
-    return {"value": len(idx) / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
+
+    def run(rd):
+        t0 = time.perf_counter()
+        q = og.query(view.campos, rd, t)
+        with torch.no_grad():
+            agg_ref.render(pts, mlp, torch.from_numpy(view.campos), torch.from_numpy(view.camrotc2w),
+                           torch.from_numpy(rd), q, o.SR)
+        return time.perf_counter() - t0
+
+    dt = run(raydir)
+    threads = torch.get_num_threads()
+    # single-thread rate on a quarter of the sample (OpenMP query + torch both pinned to 1)
+    sub = raydir[::4]
+    torch.set_num_threads(1)
+    oq.lib().sgnref_set_threads(1)
+    dt1 = run(sub)
+    torch.set_num_threads(threads)
+    oq.lib().sgnref_set_threads(threads)
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": len(idx) / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+            "value_1thread": len(sub) / dt1, "cpu_model": cpu,
             "sample": f"{len(idx)} rays ({view.h // stride}x{view.w // stride} strided subset of frame 0, SR={o.SR}), "
-                      f"{dt:.2f} s; C query (OpenMP) + torch-CPU aggregator/composite"}
+                      f"{dt:.2f} s on {threads} threads; 1-thread: {len(sub)} rays in {dt1:.2f} s; "
+                      f"C query (OpenMP) + torch-CPU aggregator/composite"}
 
 
 def main():

@@ -42,6 +42,8 @@ def lib():
         L.sgnref_query.restype = None
         L.sgnref_query.argtypes = [P(Params), vp, vp, vp, vp, vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int,
                                    ctypes.c_int, vp, vp, vp, vp, vp, vp, ctypes.c_uint64]
+        L.sgnref_set_threads.restype = None
+        L.sgnref_set_threads.argtypes = [ctypes.c_int]
         L.sgnref_knn_one.restype = ctypes.c_int
         L.sgnref_knn_one.argtypes = [P(Params), vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_uint64]
         _L = L

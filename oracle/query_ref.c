@@ -49,6 +49,19 @@
 
 #include "query_ref.h"
 
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* thread count of the OpenMP query loop (bench.py's 1-thread CPU baseline) */
+void sgnref_set_threads(int n) {
+#ifdef _OPENMP
+    omp_set_num_threads(n > 0 ? n : 1);
+#else
+    (void)n;
+#endif
+}
+
 static inline uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;

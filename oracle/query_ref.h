@@ -18,6 +18,7 @@ typedef struct {
     int fix_occ0;     /* 0 = reproduce `voxel_idx > 0` (:395)             */
 } sgnref_params;
 
+void sgnref_set_threads(int n);
 float sgnref_uniform(uint64_t seed, uint64_t stream, uint64_t i);
 int64_t sgnref_grid_volume(const sgnref_params *p);
 int64_t sgnref_grid_build(const float *pts, int64_t n, const sgnref_params *p, int32_t *coor_occ,

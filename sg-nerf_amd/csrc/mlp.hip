@@ -307,6 +307,17 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
     dma_chunk<(N + DIST) % NCHUNK>(wb, lds + tgt * SLOT_BYTES, w, lane, lz);
 }
 
+// v_permlane{16,32}_swap as inline asm: this compiler's lowering of the two-result
+// builtins returns the first result twice (seen in the ISA: v_add v48, v48, v48 after the
+// swap).  x, y are swapped in place: permlane32: x.hi <-> y.lo; permlane16: odd rows of x
+// <-> even rows of y.  The s_nops cover the VALU-write -> permlane-read hazard.
+__device__ __forceinline__ void permlane32_swap(float &x, float &y) {
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void permlane16_swap(float &x, float &y) {
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+}
+
 // LeakyReLU(0.01) = 0.505 x + 0.495 |x|: one v_mul with an |x| source modifier + one v_fma
 // (no compare/select, no NaN canonicalisation); within 1 ulp of max(x, 0.01x)
 __device__ __forceinline__ float lrelu_max(float x) { return __builtin_fmaf(0.505f, x, 0.495f * __builtin_fabsf(x)); }
@@ -541,10 +552,9 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
                 // lanes 32-63 <- samples 1 / 3 (v_permlane32_swap)
 #pragma unroll
                 for (int k2 = 0; k2 < 2; ++k2) {
-                    const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, fg[2 * k2]),
-                                                                     __builtin_bit_cast(uint32_t, fg[2 * k2 + 1]),
-                                                                     false, false);
-                    const float tot = __builtin_bit_cast(float, sw[0]) + __builtin_bit_cast(float, sw[1]);
+                    float x = fg[2 * k2], y = fg[2 * k2 + 1];
+                    permlane32_swap(x, y);
+                    const float tot = x + y;
                     const int g = h + 2 * k2, it = base + w * 4 + g;
                     if (it < end) {
                         const _Float16 hv16 = (_Float16)tot;
@@ -564,10 +574,9 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         float bq[8];
 #pragma unroll
         for (int p2 = 0; p2 < 8; ++p2) {  // lanes j, j^16 (v_permlane16_swap)
-            const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, apart[2 * p2]),
-                                                             __builtin_bit_cast(uint32_t, apart[2 * p2 + 1]), false,
-                                                             false);
-            bq[p2] = __builtin_bit_cast(float, sw[0]) + __builtin_bit_cast(float, sw[1]);
+            float x = apart[2 * p2], y = apart[2 * p2 + 1];
+            permlane16_swap(x, y);
+            bq[p2] = x + y;
         }
         auto rs_step = [&](float lo, float hi, bool upper, auto ctrl) {
             const float keep = upper ? hi : lo, send = upper ? lo : hi;

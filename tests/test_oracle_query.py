@@ -133,7 +133,7 @@ def test_march_first_sr_flagged_candidates():
 def test_gpu_matches_known_answers(fix):
     from sgnerf_amd.querier import HipGrid, QueryWorkspace, run_query
     dev = "cuda:0"
-    o = _opts(fix_occ0=fix, reservoir_seed=1)
+    o = _opts(fix_occ0=fix, reservoir_seed=1, K=4)  # the GPU kNN is instantiated for K = 1, 4, 8, 16
     hy = types.SimpleNamespace(shift=np.zeros(3, np.float32), scaled_vsize=np.ones(3, np.float32),
                                scaled_vdim=np.array([6, 6, 6], np.int32), r2=np.float32(0.0), volume=216)
     g = HipGrid(torch.from_numpy(PTS).to(dev), o, hyper=hy)
