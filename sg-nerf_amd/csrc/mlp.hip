@@ -33,6 +33,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 using namespace mlp;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Weight blob access through a buffer descriptor: one VGPR of per-lane offset plus a
 // compile-time SGPR/immediate offset per fragment (flat 64-bit addresses per fragment
@@ -144,7 +145,10 @@ constexpr int AGG_TPB = 256;
 constexpr int ROWS_TPB = 512;
 constexpr int WG_WAVES = ROWS_TPB / 64;
 constexpr int WG_SAMPLES = WG_WAVES * 4;  // 32
-constexpr int CHUNK_FRAGS = 16;            // fragments per LDS chunk (k-steps x tiles of a pass)
+#ifndef SGN_CHUNK_FRAGS
+#define SGN_CHUNK_FRAGS 32
+#endif
+constexpr int CHUNK_FRAGS = SGN_CHUNK_FRAGS;  // fragments per LDS chunk (k-steps x tiles of a pass)
 // output tiles per pass: layer 0 runs all 8 tiles in one pass (its inputs are generated on
 // the fly and never stored), the chained layers run two passes of 4 (their input fragments
 // stay in registers, the accumulators of 8 tiles would not fit beside them)
@@ -530,9 +534,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         for (int i = 0; i < 16; ++i)
             wv[i] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
                                                   ((i & 3) + 8 * (i >> 2) + 4 * h) * 4, __builtin_bit_cast(int, ri.wgt)));
-        float apart[16];   // alpha logit partial of row i over this lane's units
-#pragma unroll
-        for (int i = 0; i < 16; ++i) apart[i] = 0.f;
+        f32x2 ap2[8] = {};  // alpha logit partials of rows (2p, 2p+1) over this lane's units
         const int j = lane & 31;
         auto l3_epilogue = [&](auto pp) {
             constexpr int P = decltype(pp)::value, TP = 4;
@@ -540,14 +542,19 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
             for (int tt = 0; tt < TP; ++tt) {
                 const int t = TP * P + tt;
                 const float bu = Fl[F_B3 + 32 * t + j], wau = Fl[F_WA + 32 * t + j];
-                float fg[4] = {0.f, 0.f, 0.f, 0.f};
+                // register pairs (i, i+1) as packed fp32 (v_pk_add/mul/fma_f32)
+                f32x2 fg2[4] = {};
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float y = acc[tt][i] + bu;
-                    const float hv = fmaxf(y, 0.01f * y);
-                    apart[i] = fmaf(wau, hv, apart[i]);
-                    fg[i >> 2] = fmaf(wv[i], hv, fg[i >> 2]);
+                for (int i = 0; i < 16; i += 2) {
+                    const f32x2 y = f32x2{acc[tt][i], acc[tt][i + 1]} + f32x2{bu, bu};
+                    const f32x2 z = y * f32x2{0.01f, 0.01f};
+                    const f32x2 hv = {fmaxf(y[0], z[0]), fmaxf(y[1], z[1])};
+                    ap2[i >> 1] = __builtin_elementwise_fma(f32x2{wau, wau}, hv, ap2[i >> 1]);
+                    fg2[i >> 2] = __builtin_elementwise_fma(f32x2{wv[i], wv[i + 1]}, hv, fg2[i >> 2]);
                 }
+                float fg[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) fg[g] = fg2[g][0] + fg2[g][1];
                 // halves hold rows 4h..4h+3 of each sample: lanes 0-31 <- samples 0 / 2,
                 // lanes 32-63 <- samples 1 / 3 (v_permlane32_swap)
 #pragma unroll
@@ -574,7 +581,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         float bq[8];
 #pragma unroll
         for (int p2 = 0; p2 < 8; ++p2) {  // lanes j, j^16 (v_permlane16_swap)
-            float x = apart[2 * p2], y = apart[2 * p2 + 1];
+            float x = ap2[p2][0], y = ap2[p2][1];
             permlane16_swap(x, y);
             bq[p2] = x + y;
         }
