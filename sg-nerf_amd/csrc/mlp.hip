@@ -149,6 +149,13 @@ constexpr int WG_SAMPLES = WG_WAVES * 4;  // 32
 #define SGN_CHUNK_FRAGS 32
 #endif
 constexpr int CHUNK_FRAGS = SGN_CHUNK_FRAGS;  // fragments per LDS chunk (k-steps x tiles of a pass)
+#ifndef SGN_FRAG_PD
+#define SGN_FRAG_PD 4
+#endif
+#ifndef SGN_SCHED_PIN
+#define SGN_SCHED_PIN 0
+#endif
+constexpr int FRAG_PD = SGN_FRAG_PD;  // weight fragments in flight per wave (LDS -> VGPR queue)
 // output tiles per pass: layer 0 runs all 8 tiles in one pass (its inputs are generated on
 // the fly and never stored), the chained layers run two passes of 4 (their input fragments
 // stay in registers, the accumulators of 8 tiles would not fit beside them)
@@ -350,14 +357,25 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
         constexpr int C = decltype(cc)::value;
         chunk_enter<chunk_index(L, P, C)>(wb, lds, slot, w, lane, lz);
         const char *sl = lds + slot * SLOT_BYTES;
+        // weight fragments through a register queue PD deep, so LDS latency overlaps PD MFMAs
+        constexpr int NF = chunk_nk(L, C) * TP, PD = NF < FRAG_PD ? NF : FRAG_PD;
+        auto frag = [&](int f) { return *(const h8 *)(sl + f * (int)FRAG + lane * 16); };
+        h8 fr[PD];
+#pragma unroll
+        for (int f = 0; f < PD; ++f) fr[f] = frag(f);
         static_for<chunk_nk(L, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
             const h8 B = in(std::integral_constant<int, C * KC + KK>{});
-#pragma unroll
-            for (int t = 0; t < TP; ++t) {
-                const h8 A = *(const h8 *)(sl + (KK * TP + t) * (int)FRAG + lane * 16);
+            static_for<TP>([&](auto tt) {
+                constexpr int t = decltype(tt)::value, F = KK * TP + t;
+                const h8 A = fr[F % PD];
+                if constexpr (F + PD < NF) fr[F % PD] = frag(F + PD);
                 acc[t] = TRANS ? mfma32(B, A, acc[t]) : mfma32(A, B, acc[t]);
-            }
+#if SGN_SCHED_PIN
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // then one LDS read
+#endif
+            });
         });
         slot = slot + 1 == NSLOT ? 0 : slot + 1;
         __builtin_amdgcn_sched_barrier(0);
@@ -409,7 +427,11 @@ __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, in
     ri.sval = item < end;
     ri.s = ri.sval ? a.work[item] : 0;
     const int s = ri.s;
+#ifdef SGN_DEBUG_FAST_GATHER  // timing experiment only: no dependent index load, L2-resident records
+    const int pid = ri.sval ? ((item * 8 + kk) & 1023) : -1;
+#else
     const int pid = ri.sval ? a.pidx[(int64_t)s * 8 + kk] : -1;
+#endif
     const bool m = pid >= 0;
     const float lx = a.samp_locw[(int64_t)s * 3 + 0], ly = a.samp_locw[(int64_t)s * 3 + 1],
                 lz = a.samp_locw[(int64_t)s * 3 + 2];
