@@ -163,9 +163,21 @@ __host__ __device__ constexpr int layer_tp(int L) { return L == 0 ? 8 : 4; }
 __host__ __device__ constexpr int layer_np(int L) { return 8 / layer_tp(L); }
 __host__ __device__ constexpr int layer_kc(int L) { return CHUNK_FRAGS / layer_tp(L); }
 constexpr int SLOT_BYTES = CHUNK_FRAGS * (int)FRAG;
-constexpr int PF_N = CHUNK_FRAGS / WG_WAVES;  // LDS-DMA instructions per wave per chunk
-constexpr int DIST = 2;                       // chunks in flight ahead of the one being consumed
-constexpr int NSLOT = DIST + 1;               // ring slots (the DMA target was read one chunk ago)
+// LAG > 0: waves WG_WAVES/2.. (followers, one per SIMD) run LAG chunks behind waves 0..
+// (leaders, one per SIMD), so on every SIMD one wave's VALU epilogue overlaps the other's
+// MFMAs instead of both stalling the matrix pipe at once.  The leaders issue every LDS-DMA;
+// the ring keeps LAG extra slots for the followers.
+#ifndef SGN_LAG
+#define SGN_LAG 0
+#endif
+constexpr int LAG = SGN_LAG;
+constexpr int N_DMA_WAVES = LAG ? WG_WAVES / 2 : WG_WAVES;
+constexpr int PF_N = CHUNK_FRAGS / N_DMA_WAVES;  // LDS-DMA instructions per issuing wave per chunk
+#ifndef SGN_DIST
+#define SGN_DIST 2
+#endif
+constexpr int DIST = SGN_DIST;                // chunks in flight ahead of the one being consumed
+constexpr int NSLOT = DIST + LAG + 1;         // ring slots (the DMA target was read LAG+1 chunks ago)
 constexpr int LDS_F32_OFF = NSLOT * SLOT_BYTES;
 constexpr int LDS_BYTES = LDS_F32_OFF + (int)N_F32 * 4;
 static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the waves");
@@ -248,6 +260,10 @@ __device__ __forceinline__ float l0_channel(const float (&feat)[16], const float
 
 template <int K0>
 __device__ __forceinline__ h8 l0_step(const float (&feat)[16], const float (&dist)[3]) {
+#ifdef SGN_ABLATE_PE  // timing experiment only: raw features instead of encodings (wrong results)
+    return pack8(feat[(8 * K0) & 15], feat[(8 * K0 + 1) & 15], feat[(8 * K0 + 2) & 15], feat[(8 * K0 + 3) & 15],
+                 feat[(8 * K0 + 4) & 15], feat[(8 * K0 + 5) & 15], dist[K0 % 3], feat[(8 * K0 + 7) & 15]);
+#endif
     return pack8(l0_channel<8 * K0 + 0>(feat, dist), l0_channel<8 * K0 + 1>(feat, dist),
                  l0_channel<8 * K0 + 2>(feat, dist), l0_channel<8 * K0 + 3>(feat, dist),
                  l0_channel<8 * K0 + 4>(feat, dist), l0_channel<8 * K0 + 5>(feat, dist),
@@ -293,11 +309,11 @@ __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int
     constexpr int nf = chunk_nk(L, C) * layer_tp(L);
 #pragma unroll
     for (int j = 0; j < PF_N; ++j) {
-        const int i = w + WG_WAVES * j;
+        const int i = w + N_DMA_WAVES * j;
         const int src = min(i, nf - 1);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             wb.rsrc, (__attribute__((address_space(3))) void *)(dst + i * (int)FRAG), 16,
-            lane * 16 + src * (int)FRAG, chunk_off(L, P, C) + (uint32_t)lz, 0, 0);
+            lane * 16, chunk_off(L, P, C) + (uint32_t)(src * (int)FRAG + lz), 0, 0);
     }
 }
 
@@ -306,16 +322,24 @@ __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int
 // DIST chunks ahead into the slot read one chunk ago.
 template <int N>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz) {
+#ifdef SGN_ABLATE_STREAM  // timing experiment only: no weight stream, no barriers (wrong results)
+    return;
+#endif
     constexpr int younger = (DIST - 1) * PF_N;  // DMAs issued after this chunk's
-    static_assert(younger == 2 || younger == 4 || younger == 6, "add the vmcnt immediate");
-    if constexpr (younger == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    static_assert(younger == 0 || younger == 4 || younger == 8, "add the vmcnt immediate");
+    const bool issuer = !LAG || w < N_DMA_WAVES;  // wave-uniform
+    if (issuer) {
+        if constexpr (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if constexpr (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    int tgt = slot + DIST;
-    tgt = tgt >= NSLOT ? tgt - NSLOT : tgt;
-    dma_chunk<(N + DIST) % NCHUNK>(wb, lds + tgt * SLOT_BYTES, w, lane, lz);
+    if (issuer) {
+        int tgt = slot + DIST;
+        tgt = tgt >= NSLOT ? tgt - NSLOT : tgt;
+        dma_chunk<(N + DIST) % NCHUNK>(wb, lds + tgt * SLOT_BYTES, w, lane, lz);
+    }
 }
 
 // v_permlane{16,32}_swap as inline asm: this compiler's lowering of the two-result
@@ -400,7 +424,10 @@ __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
             const int t = TP * P + tt, r = 8 * s2;
-#if SGN_LRELU_F32
+#if defined(SGN_ABLATE_ACT)  // timing experiment only: no activation (wrong results)
+            out[2 * t + s2] = pack8(acc[tt][r + 0], acc[tt][r + 1], acc[tt][r + 2], acc[tt][r + 3], acc[tt][r + 4],
+                                    acc[tt][r + 5], acc[tt][r + 6], acc[tt][r + 7]);
+#elif SGN_LRELU_F32
             out[2 * t + s2] = pack8(lrelu_max(acc[tt][r + 0]), lrelu_max(acc[tt][r + 1]), lrelu_max(acc[tt][r + 2]),
                                     lrelu_max(acc[tt][r + 3]), lrelu_max(acc[tt][r + 4]), lrelu_max(acc[tt][r + 5]),
                                     lrelu_max(acc[tt][r + 6]), lrelu_max(acc[tt][r + 7]));
@@ -511,10 +538,15 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     __syncthreads();  // parameters visible before the first tile's bias reads
     int slot = 0;
     // stream prologue: chunks 0..DIST-1 in flight (chunk_enter<n> issues chunk n+DIST)
-    static_for<DIST>([&](auto nn) {
-        constexpr int N0 = decltype(nn)::value;
-        dma_chunk<N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
-    });
+    if (!LAG || w < N_DMA_WAVES) {
+        static_for<DIST>([&](auto nn) {
+            constexpr int N0 = decltype(nn)::value;
+            dma_chunk<N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
+        });
+    } else {
+        // followers start LAG chunk intervals late (the leaders add LAG barriers at the end)
+        for (int i = 0; i < LAG; ++i) __builtin_amdgcn_s_barrier();
+    }
     for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
         // opaque zero per iteration: keeps LDS parameter reads and weight offsets inside the loop
         int lz = 0;
@@ -631,6 +663,8 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         const float alpha_s = dpp_sum8(ri.wgt * alpha_row);
         if (ri.sval && kk == 0 && h == 0) a.feat[(int64_t)ri.s * 4 + 0] = alpha_s;
     }
+    if (LAG && w < N_DMA_WAVES)
+        for (int i = 0; i < LAG; ++i) __builtin_amdgcn_s_barrier();  // match the followers' late start
     // the stream ran DIST chunks ahead: let those LDS-DMAs land before the workgroup retires
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
