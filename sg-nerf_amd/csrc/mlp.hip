@@ -677,15 +677,70 @@ struct ColorArgs {
     int32_t item0, n_items;
 };
 
-__global__ __launch_bounds__(AGG_TPB, 2) void k_color(ColorArgs a) {
+// Colour MLP, one 512-thread workgroup per CU: the 136 colour fragments (C0..C2, 136 KiB)
+// and the colour fp32 parameters are copied into LDS once (LDS-DMA), then every wave runs
+// 32 samples at a time: [f_s | PE(viewdir)] -> 128 -> 128 -> 128 (MFMA, A from LDS) -> 3.
+constexpr int COL_TPB = 512;
+constexpr int COL_FRAGS = T_CHID * (KS_C0 + 2 * KS_CH);  // 136
+constexpr int COL_F32 = (int)(N_F32 - F_CB0);             // colour biases + output layer
+constexpr int COL_LDS = COL_FRAGS * (int)FRAG + COL_F32 * 4;
+static_assert(COL_FRAGS % (COL_TPB / 64) == 0, "colour fragments split evenly over the waves");
+static_assert(OFF_C1 == OFF_C0 + (size_t)T_CHID * KS_C0 * FRAG && OFF_C2 == OFF_C1 + (size_t)T_CHID * KS_CH * FRAG,
+              "colour layers are contiguous");
+
+template <int KS, int NIN>
+__device__ __forceinline__ void color_layer(const char *wl, const float *bl, const h8 (&in)[NIN], h8 (&out)[8],
+                                            int lane) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < T_CHID; ++t) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+            acc = mfma32(*(const h8 *)(wl + (t * KS + k) * (int)FRAG + lane * 16), in[k], acc);
+        const float *b = bl + (t * 2 + h) * 16;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int r = 8 * s2;
+            const u32x4 u = {lrelu_pk(acc[r + 0] + b[r + 0], acc[r + 1] + b[r + 1]),
+                             lrelu_pk(acc[r + 2] + b[r + 2], acc[r + 3] + b[r + 3]),
+                             lrelu_pk(acc[r + 4] + b[r + 4], acc[r + 5] + b[r + 5]),
+                             lrelu_pk(acc[r + 6] + b[r + 6], acc[r + 7] + b[r + 7])};
+            out[2 * t + s2] = __builtin_bit_cast(h8, u);
+        }
+    }
+}
+
+__global__ __launch_bounds__(COL_TPB, 1) void k_color(ColorArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[COL_LDS];
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, j = lane & 31;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nwork = a.counters[1];
     const int end = min(nwork, a.item0 + a.n_items);
-    const int wave = blockIdx.x * (AGG_TPB / 64) + (threadIdx.x >> 6);
-    const int nwaves = gridDim.x * (AGG_TPB / 64);
     const WBlob wb = make_blob(a.blob);
+#pragma unroll
+    for (int i = 0; i < COL_FRAGS / (COL_TPB / 64); ++i) {  // colour fragments -> LDS
+        const int f = w + (COL_TPB / 64) * i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            wb.rsrc, (__attribute__((address_space(3))) void *)(lds + f * (int)FRAG), 16, lane * 16,
+            (uint32_t)(OFF_C0 + (size_t)f * FRAG), 0, 0);
+    }
+    {   // f32 section from F_CB0
+        float *dst = (float *)(lds + COL_FRAGS * (int)FRAG);
+        const float *src = (const float *)((const char *)a.blob + OFF_F32) + F_CB0;
+        for (int i = threadIdx.x; i < COL_F32; i += COL_TPB) dst[i] = src[i];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int wave = blockIdx.x * (COL_TPB / 64) + w;
+    const int nwaves = gridDim.x * (COL_TPB / 64);
     for (int base = a.item0 + wave * 32; base < end; base += nwaves * 32) {
+        // opaque zero: keeps the (loop-invariant) LDS fragment reads inside the loop
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        const char *W0 = lds + lz, *W1 = W0 + T_CHID * KS_C0 * (int)FRAG, *W2 = W1 + T_CHID * KS_CH * (int)FRAG;
+        const float *Fc = (const float *)(lds + lz + COL_FRAGS * (int)FRAG);
         const int item = base + j;
         const bool sval = item < end;
         const int s = sval ? a.work[item] : 0;
@@ -694,52 +749,52 @@ __global__ __launch_bounds__(AGG_TPB, 2) void k_color(ColorArgs a) {
         const h8 *row = (const h8 *)(a.fs + (int64_t)(sval ? item - a.item0 : 0) * HID);
 #pragma unroll
         for (int k = 0; k < 16; ++k) x[k] = row[2 * k + h];
-        // PE(viewdir) ori=True, channels [3:] (point_aggregators.py:579-585, networks.py:175-192)
-        float v[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1], a.raydir[(int64_t)ray * 3 + 2]};
+        // PE(viewdir) ori=True, channels [3:] (point_aggregators.py:579-585, networks.py:175-192):
+        // pe[d*4+f] = sin(v_d 2^f), pe[12+d*4+f] = cos(v_d 2^f)
+        const float v[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1], a.raydir[(int64_t)ray * 3 + 2]};
         float pe[24];
 #pragma unroll
-        for (int d = 0; d < 3; ++d)
+        for (int d = 0; d < 3; ++d) {
+            float s0, c0;
+            sincos_pow2<0>(v[d], s0, c0);
+            pe[d * 4] = s0;
+            pe[12 + d * 4] = c0;
 #pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                float sv, cv;
-                sincosf(v[d] * (float)(1 << f), &sv, &cv);
-                pe[d * 4 + f] = sv;
-                pe[12 + d * 4 + f] = cv;
+            for (int f = 1; f < 4; ++f) {
+                const float s1 = 2.f * s0 * c0, c1 = (c0 - s0) * (c0 + s0);
+                s0 = s1;
+                c0 = c1;
+                pe[d * 4 + f] = s0;
+                pe[12 + d * 4 + f] = c0;
             }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            x[16][e] = (_Float16)(h ? pe[8 + e] : pe[e]);
-            x[17][e] = (_Float16)(h ? 0.f : pe[16 + e]);
         }
+        x[16] = h ? pack8(pe[8], pe[9], pe[10], pe[11], pe[12], pe[13], pe[14], pe[15])
+                  : pack8(pe[0], pe[1], pe[2], pe[3], pe[4], pe[5], pe[6], pe[7]);
+        x[17] = h ? h8{} : pack8(pe[16], pe[17], pe[18], pe[19], pe[20], pe[21], pe[22], pe[23]);
         h8 y1[KS_CH], y2[KS_CH];
-        const h8 zero8 = {};
-        layer_chain<KS_C0, KS_C0, T_CHID>(wb, OFF_C0, F_CB0, x, zero8, y1, lane);
-        layer_chain<KS_CH, KS_CH, T_CHID>(wb, OFF_C1, F_CB1, y1, zero8, y2, lane);
+        color_layer<KS_C0, KS_C0>(W0, Fc + (F_CB0 - F_CB0), x, y1, lane);
+        color_layer<KS_CH, KS_CH>(W1, Fc + (F_CB1 - F_CB0), y1, y2, lane);
         float o[3] = {0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < T_CHID; ++t) {
             f32x16 acc = {};
 #pragma unroll
             for (int k = 0; k < KS_CH; ++k)
-                acc = mfma32(wb.frag(OFF_C2 + (uint32_t)(t * KS_CH + k) * FRAG, lane), y2[k], acc);
+                acc = mfma32(*(const h8 *)(W2 + (t * KS_CH + k) * (int)FRAG + lane * 16), y2[k], acc);
+            const float *b = Fc + (F_CB2 - F_CB0) + (t * 2 + h) * 16;
+            const float *w0 = Fc + (F_WC3 - F_CB0) + (t * 2 + h) * 16;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                f32x4 b = wb.acc4(F_CB2, t, g, h);
-                f32x4 w0 = wb.acc4(F_WC3, t, g, h), w1 = wb.acc4(F_WC3 + 128, t, g, h),
-                      w2 = wb.acc4(F_WC3 + 256, t, g, h);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    float hv = lrelu(acc[4 * g + c] + b[c]);
-                    o[0] = fmaf(w0[c], hv, o[0]);
-                    o[1] = fmaf(w1[c], hv, o[1]);
-                    o[2] = fmaf(w2[c], hv, o[2]);
-                }
+            for (int r = 0; r < 16; ++r) {
+                const float y = acc[r] + b[r];
+                const float hv = fmaxf(y, 0.01f * y);
+                o[0] = fmaf(w0[r], hv, o[0]);
+                o[1] = fmaf(w0[128 + r], hv, o[1]);
+                o[2] = fmaf(w0[256 + r], hv, o[2]);
             }
-            __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            float z = o[c] + __shfl_xor(o[c], 32) + wb.scalar(F_BC3 + c);
+            const float z = o[c] + __shfl_xor(o[c], 32) + Fc[F_BC3 - F_CB0 + c];
             o[c] = (1.f / (1.f + expf(-z))) * (1.f + 2.f * 0.001f) - 0.001f;
         }
         if (sval && h == 0) {
@@ -860,9 +915,9 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
         int64_t wg = (n + WG_SAMPLES - 1) / WG_SAMPLES;  // persistent: one workgroup per CU
         dim3 g1((unsigned)(wg < 256 ? wg : 256));
         if (stages & 1) hipLaunchKernelGGL(k_agg_rows, g1, dim3(ROWS_TPB), 0, st, a);
-        int64_t wg2 = (n + 127) / 128;  // 32 samples per wave
-        dim3 g2((unsigned)(wg2 < 2048 ? wg2 : 2048));
-        if (stages & 2) hipLaunchKernelGGL(k_color, g2, dim3(AGG_TPB), 0, st, c);
+        int64_t wg2 = (n + 32 * (COL_TPB / 64) - 1) / (32 * (COL_TPB / 64));  // 32 samples per wave
+        dim3 g2((unsigned)(wg2 < 256 ? wg2 : 256));  // persistent: colour weights loaded once per CU
+        if (stages & 2) hipLaunchKernelGGL(k_color, g2, dim3(COL_TPB), 0, st, c);
     }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
