@@ -150,10 +150,10 @@ constexpr int WG_SAMPLES = WG_WAVES * 4;  // 32
 #endif
 constexpr int CHUNK_FRAGS = SGN_CHUNK_FRAGS;  // fragments per LDS chunk (k-steps x tiles of a pass)
 #ifndef SGN_FRAG_PD
-#define SGN_FRAG_PD 4
+#define SGN_FRAG_PD 3
 #endif
 #ifndef SGN_SCHED_PIN
-#define SGN_SCHED_PIN 0
+#define SGN_SCHED_PIN 1
 #endif
 constexpr int FRAG_PD = SGN_FRAG_PD;  // weight fragments in flight per wave (LDS -> VGPR queue)
 // output tiles per pass: layer 0 runs all 8 tiles in one pass (its inputs are generated on
@@ -387,6 +387,9 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
         h8 fr[PD];
 #pragma unroll
         for (int f = 0; f < PD; ++f) fr[f] = frag(f);
+#if SGN_SCHED_PIN
+        __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);  // PD LDS reads in flight first
+#endif
         static_for<chunk_nk(L, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
             const h8 B = in(std::integral_constant<int, C * KC + KK>{});
