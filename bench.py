@@ -51,7 +51,63 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--train", action="store_true",
+                    help="BASELINE config 5: training steps on 4096 random rays per rank (backward + DP all-reduce)")
+    ap.add_argument("--train-rays", type=int, default=4096)
     return ap.parse_args()
+
+
+def train_main(args, world, rank, dev, dist):
+    """Config 5: one training step = 4096 random rays of a random spiral pose per rank, HIP query,
+    device autograd through aggregator + composite, bucketed RCCL all-reduce, two Adam groups."""
+    from sgnerf_amd.train import PointParams, Trainer
+    o = HotPathOpts(SR=24, is_train=1)
+    pc = scene.synth_room(args.points, seed=0)
+    mlp = init_mlp(0, bias_std=0.01)
+    mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
+    points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, dev)
+    tr = Trainer(points, mlp, o, dev)
+    g = torch.Generator().manual_seed(1 + rank)
+    n_steps = args.warmup + args.steps
+    batches = []
+    for i in range(n_steps):
+        v = pose_view(int(torch.randint(0, 120, (1,), generator=g)), args.h, args.w)
+        idx = torch.randint(0, args.h * args.w, (args.train_rays,), generator=g)
+        gt = torch.rand(args.train_rays, 3, generator=g)
+        batches.append(tuple(x.to(dev) for x in (torch.from_numpy(v.campos), torch.from_numpy(v.camrotc2w),
+                                                   torch.from_numpy(v.raydir)[idx], gt)))
+    tr.querier = None
+    for i in range(args.warmup):
+        c, r_, d, gt = batches[i]
+        tr.step(c, r_, d, 0.1, 8.0, gt)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = []
+    for i in range(args.warmup, n_steps):
+        c, r_, d, gt = batches[i]
+        parts, _, _ = tr.step(c, r_, d, 0.1, 8.0, gt)
+        losses.append(parts["total"])
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if dist:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(el.item())
+    rays = args.train_rays * args.steps * world
+    res = {"metric": "training rays/sec, 4096-ray batches with backward, DP (BASELINE config 5)",
+           "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "config": {"workload": f"synth-room, {args.train_rays} random rays per rank per step, SR=24, K=8, "
+                                  f"{args.points} neural points, HIP query + device autograd + RCCL all-reduce",
+                      "parallelism": f"dp{world}"},
+           "final_loss": float(torch.stack(losses).mean().item())}
+    if rank == 0:
+        print(json.dumps(res))
 
 
 def pose_view(i, h, w, n_poses=120):
@@ -118,6 +174,11 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.train:
+        train_main(args, world, rank, dev, dist)
+        if dist:
+            torch.distributed.destroy_process_group()
+        return
     o = HotPathOpts(SR=args.sr)
     pc = scene.synth_room(args.points, seed=0)
     mlp = init_mlp(0, bias_std=0.01)
@@ -174,15 +235,20 @@ def main():
     stage_ms = {n: float(np.mean([ev[n].elapsed_time(ev[order[j + 1]]) for ev in events]))
                 for j, n in enumerate(stage_names)}
     # occupancy / algorithmic work of the timed frames (deterministic re-render, untimed)
-    n_nb, n_smp, n_samples = [], [], []
+    n_nb, n_smp, n_samples, q_bytes = [], [], [], []
     for i in range(args.warmup, n_frames):
         out = frame(i)
         q = out.query
         S = q.n_samples()
-        W = int(q.counters[1].item())
+        cnt = q.counters.tolist()
+        W = cnt[1]
         n_samples.append(S)
         n_smp.append(W)
         n_nb.append(int(q.samp_nnb[:S].sum().item()))
+        # query-stage algorithmic bytes (no reuse credit): march: ray direction + per-ray
+        # outputs; kNN: voxel words + 16-B candidate records read, per-sample inputs and outputs
+        q_bytes.append(R * (12 + 4 + 4 + 2 * args.sr) + 4 * cnt[2] + 16 * cnt[3] + S * (4 + 4 + 12 + 12 + 4 + 4 * 8)
+                       + 4 * W)
     torch.cuda.synchronize()
     rows_flop = FLOP_PER_NB * float(np.mean(n_nb))
     achieved = rows_flop / (stage_ms["agg_rows"] * 1e-3) / 1e12
@@ -221,6 +287,12 @@ def main():
             "bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / PEAK_F16_TFLOPS, "traffic": traffic,
             "flop_per_launch": rows_flop, "avg_launch_ms": stage_ms["agg_rows"],
+        },
+        "roofline_query": {
+            "kernel": "query stage (k_march + scan + k_emit_samples + k_knn)", "bound": "hbm",
+            "achieved": float(np.mean(q_bytes)) / (stage_ms["query"] * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": float(np.mean(q_bytes)) / (stage_ms["query"] * 1e-3) / 1e9 / PEAK_HBM_GBS,
+            "bytes_per_frame": float(np.mean(q_bytes)),
         },
         "stages_ms": stage_ms,
         "grid_build_ms": grid_ms,

@@ -99,7 +99,8 @@ typedef struct {
  *   samp_nnb  int32[S]        valid neighbours of the sample (0..K)
  *   pidx      int32[S*K] or [R*SR*K] (dense_out; caller pre-fills -1)
  *   work      int32[S]        ids of samples with samp_nnb > 0 (unordered)
- *   counters  int32[4]        [0] = S (total samples), [1] = work items
+ *   counters  int32[4]        [0] = S (total samples), [1] = work items, [2] voxel words and
+ *                             [3] candidate points the kNN read (algorithmic-traffic counters)
  */
 typedef struct {
     int32_t *ray_ns, *ray_soff, *samp_ray, *samp_d, *samp_nnb, *pidx, *work, *counters;

@@ -158,6 +158,7 @@ __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict
         if (SEMANTIC) center_label = ray_labels[r];
         KBuf<K> kb;
         kb.init();
+        int n_vox = 0, n_cand = 0;  // algorithmic-traffic counters (bench roofline)
         const int nlayer = (g.kernel0 + 1) / 2;
         for (int layer = 0; layer < nlayer; ++layer) {
             const int x0 = max(-fx, -layer), x1 = min(g.dims[0] - fx, layer + 1);
@@ -169,8 +170,10 @@ __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict
                         if (max(abs(z), max(abs(x), abs(y))) != layer) continue;
                         const int32_t occ =
                             g.vox[(int64_t)(fx + x) * plane + (int64_t)(fy + y) * g.dims[2] + (fz + z)];
+                        ++n_vox;
                         if (occ < 0) continue;
                         const int32_t st = g.start[occ], n = g.cnt[occ];
+                        n_cand += n;
                         for (int q = 0; q < n; ++q) {
                             const float4 pt = g.pts[st + q];
                             const int32_t pid = __float_as_int(pt.w);
@@ -201,6 +204,8 @@ __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict
             int32_t w = atomicAdd(counters + 1, 1);
             work[w] = (int32_t)s;
         }
+        atomicAdd(counters + 2, n_vox);
+        atomicAdd(counters + 3, n_cand);
     }
 }
 

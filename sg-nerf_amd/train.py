@@ -1,0 +1,283 @@
+"""Training step of the per-ray path, first version.
+
+One step on a batch of rays, as the reference's `optimize_parameters` does it
+(models/base_rendering_model.py:534-664, models/mvs_points_volumetric_model.py:47-141):
+
+  query        HIP (`sgn_query`, bit-exact vs the oracle): shading samples + neighbour
+               indices; no gradient flows through it (the reference's is pycuda, also
+               non-differentiable)
+  aggregator   NeuralPoints gather + PointAggregator / viewmlp (point_aggregators.py:868-959,
+               :561-786) as differentiable torch ops on the device: the GEMMs run on the ROCm
+               BLAS libraries, gradients reach the MLP and the per-point parameters
+               (points_embeding, points_color, points_dir, points_conf) through the gather;
+               conf goes through the straight-through clamp (:863-865)
+  composite    ray_dist + ray_march (neural_points_volumetric_model.py:569-631,
+               diff_ray_marching.py:509-555)
+  losses       ray-masked colour MSE (`ray_masked_coarse_raycolor`, weight 1) + zero-one on
+               `conf_coefficient` (weight 1e-4, zero_epsilon 1e-3), ScanNet opt.txt:33-34,202-204
+  update       data-parallel: gradients all-reduced (mean) over ranks in flat buckets
+               (RCCL over xGMI; gloo in the CPU tests), then two Adam groups
+               (net lr 5e-4, points plr 2e-3, betas (0.9, 0.999)) with the reference's
+               iter_exponential_decay schedule (lr * 0.1 ** (step / 1e6))
+
+The forward used for rendering stays the fused HIP kernels; this module is the
+differentiable restatement needed for gradients until the HIP backward lands.  `loss_from_query`
+takes a query result (sample-major) so the same code runs on CPU with the oracle's query in
+the parity tests.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .opts import HotPathOpts
+from .weights import LAYERS, strip_prefix
+
+
+def _pe(x, freqs, ori=False):
+    """positional_encoding (networks.py:175-192)."""
+    bands = (2.0 ** torch.arange(freqs, device=x.device, dtype=x.dtype))
+    p = (x[..., None] * bands).reshape(x.shape[:-1] + (freqs * x.shape[-1],))
+    if ori:
+        return torch.cat([x, torch.sin(p), torch.cos(p)], dim=-1)
+    return torch.stack([torch.sin(p), torch.cos(p)], dim=-1).reshape(p.shape[:-1] + (p.shape[-1] * 2,))
+
+
+class ViewMLP(nn.Module):
+    """The ScanNet viewmlp parameters under the reference names (block1.0.weight, ...)."""
+
+    def __init__(self, state):
+        super().__init__()
+        state = strip_prefix(state)
+        self.lin = nn.ModuleDict()
+        for name, o, i, _ in LAYERS:
+            m = nn.Linear(i, o)
+            with torch.no_grad():
+                m.weight.copy_(torch.as_tensor(state[name + ".weight"]))
+                m.bias.copy_(torch.as_tensor(state[name + ".bias"]))
+            self.lin[name.replace(".", "_")] = m
+
+    def f(self, name, x):
+        return self.lin[name.replace(".", "_")](x)
+
+    def state(self):
+        out = {}
+        for name, *_ in LAYERS:
+            m = self.lin[name.replace(".", "_")]
+            out[name + ".weight"] = m.weight.detach()
+            out[name + ".bias"] = m.bias.detach()
+        return out
+
+
+class PointParams(nn.Module):
+    """Trainable neural-point parameters (neural_points.py:370-414 names)."""
+
+    def __init__(self, xyz, embedding, color, dir, conf, device):
+        super().__init__()
+        f = dict(dtype=torch.float32, device=device)
+        self.register_buffer("xyz", torch.as_tensor(xyz).to(**f).reshape(-1, 3).contiguous())
+        n = self.xyz.shape[0]
+        self.points_embeding = nn.Parameter(torch.as_tensor(embedding).to(**f).reshape(n, -1).clone())
+        self.points_color = nn.Parameter(torch.as_tensor(color).to(**f).reshape(n, 3).clone())
+        self.points_dir = nn.Parameter(torch.as_tensor(dir).to(**f).reshape(n, 3).clone())
+        self.points_conf = nn.Parameter(torch.as_tensor(conf).to(**f).reshape(n, 1).clone())
+
+
+def _w2pers(p, rot, campos):
+    c = (p - campos) @ rot  # c_j = sum_i R[i][j] (p_i - campos_i)  (neural_points.py:845-850)
+    return torch.stack([c[..., 0] / c[..., 2], c[..., 1] / c[..., 2], c[..., 2]], dim=-1)
+
+
+def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, samp_locw, pidx):
+    """Differentiable PointAggregator.forward on sample-major neighbours.
+    Returns feat [S,4] (alpha, r, g, b; zeros for samples without neighbours), conf_coefficient
+    [S,K] (straight-through clamp) and the neighbour mask [S,K]."""
+    S, K = pidx.shape
+    mask = pidx >= 0
+    flat = torch.clamp(pidx, min=0).reshape(-1).long()
+    xyz = points.xyz[flat].view(S, K, 3)
+    pers = _w2pers(xyz, rot, campos)
+    loc = _w2pers(samp_locw, rot, campos)
+    dists = torch.cat([xyz - samp_locw[:, None, :],
+                       torch.stack([pers[..., 0] * pers[..., 2] - loc[:, None, 0] * loc[:, None, 2],
+                                    pers[..., 1] * pers[..., 2] - loc[:, None, 1] * loc[:, None, 2],
+                                    pers[..., 2] - loc[:, None, 2]], dim=-1)], dim=-1)
+    weight = mask / torch.clamp(torch.norm(dists[..., :3], dim=-1), min=1e-6)        # :494-502
+    weight = weight / torch.clamp(torch.sum(weight, dim=-1, keepdim=True), min=1e-8)  # :946-947
+    conf = points.points_conf[flat].view(S, K)
+    conf_coef = conf - (conf - torch.clamp(conf, 1e-4, 1.0)).detach()                # :863-865
+    w = weight * conf_coef
+    valid = mask.any(-1)
+    v = raydir[samp_ray.long()]
+    vpe = _pe(v, 4, ori=True)
+    ori_v, vpe = vpe[..., :3], vpe[..., 3:]
+    m = mask.reshape(-1)
+    emb = points.points_embeding[flat][m]
+    x = torch.cat([emb, _pe(emb, 3), _pe(dists.reshape(-1, 6)[m], 5)], dim=-1)
+    lr_ = lambda t: F.leaky_relu(t, 0.01)  # noqa: E731
+    h = lr_(mlp.f("block1.2", lr_(mlp.f("block1.0", x))))
+    sd = points.points_dir[flat][m]
+    ov = ori_v[:, None, :].expand(S, K, 3).reshape(-1, 3)[m]
+    h = torch.cat([h, points.points_color[flat][m], sd - ov, torch.sum(sd * ov, dim=-1, keepdim=True)], dim=-1)
+    h = lr_(mlp.f("block3.2", lr_(mlp.f("block3.0", h))))
+    alpha = F.softplus(mlp.f("alpha_branch.0", h) - 1)
+    hk = torch.zeros(S * K, h.shape[-1], device=h.device, dtype=h.dtype).masked_scatter(m[:, None], h)
+    ak = torch.zeros(S * K, 1, device=h.device, dtype=h.dtype).masked_scatter(m[:, None], alpha)
+    fs = torch.sum(hk.view(S, K, -1) * w[..., None], dim=1)
+    a_s = torch.sum(ak.view(S, K, 1) * w[..., None], dim=1)
+    c = torch.cat([fs, vpe], dim=-1)
+    c = lr_(mlp.f("color_branch.0", c))
+    c = lr_(mlp.f("color_branch.2", c))
+    c = lr_(mlp.f("color_branch.4", c))
+    c = torch.sigmoid(mlp.f("color_branch.6", c)) * (1 + 2 * 0.001) - 0.001
+    feat = torch.cat([a_s, c], dim=-1) * valid[:, None]
+    return feat, conf_coef, mask
+
+
+def loss_from_query(points, mlp, q, campos, rot, raydir, gt, opts: HotPathOpts, bg=(1.0, 1.0, 1.0),
+                    zero_one_weight=1e-4, zero_eps=1e-3):
+    """Reference losses for one batch given a sample-major query result q (dict of tensors:
+    ray_ns [R], ray_soff [R], samp_ray [S], samp_locw [S,3], pidx [S,K]).
+    Returns (total loss, dict of parts, rendered colour [R,3], ray_mask [R])."""
+    R = raydir.shape[0]
+    SR = opts.SR
+    campos = campos.reshape(1, 3)
+    rot = rot.reshape(3, 3)
+    feat, conf_coef, mask = aggregate(points, mlp, campos, rot, raydir, q["samp_ray"], q["samp_locw"], q["pidx"])
+    nnb = mask.sum(-1)
+    S = q["samp_ray"].shape[0]
+    dev = raydir.device
+    sr = q["samp_ray"].long()
+    slot = torch.arange(S, device=dev) - q["ray_soff"].long()[sr]
+    fd = torch.zeros(R, SR, 4, device=dev).index_put((sr, slot), feat)
+    vd = torch.zeros(R, SR, dtype=torch.bool, device=dev).index_put((sr, slot), nnb > 0)
+    ld = torch.zeros(R, SR, 3, device=dev).index_put((sr, slot), q["samp_locw"])
+    z = _w2pers(ld, rot, campos)[..., 2]
+    cm = torch.cummax(z, dim=-1)[0]
+    rd = torch.cat([cm[:, 1:] - cm[:, :-1], torch.full((R, 1), float(opts.vsize[2]), device=dev)], dim=-1)
+    msk = rd < 1e-8
+    if opts.raydist_mode_unit:
+        msk = msk | (rd > 2 * float(opts.vsize[2]))
+    msk = msk.float()
+    rd = (rd * (1 - msk) + msk * float(opts.vsize[2])) * vd.float()
+    sigma = fd[..., 0] * vd.float()
+    o = 1 - torch.exp(-sigma * rd)
+    acc = torch.cumprod(1 - o + 1e-10, dim=-1)
+    bg_t = acc[:, -1:]
+    acc = torch.cat([torch.ones(R, 1, device=dev), acc[:, :-1]], dim=-1)
+    bgv = torch.tensor(bg, dtype=torch.float32, device=dev)
+    color = torch.sum(fd[..., 1:4] * (o * acc)[..., None], dim=1) + bgv * bg_t
+    ray_mask = vd.any(-1)
+    full = torch.where(ray_mask[:, None], color, bgv.expand(R, 3))
+    # ray_masked_coarse_raycolor (weight 1), ray_miss / coarse (weight 0): each adds 1e-6 (:560)
+    if bool(ray_mask.any()):
+        l_col = F.mse_loss(full[ray_mask], gt[ray_mask])
+    else:
+        l_col = torch.zeros((), device=dev)
+    # zero_one_loss on conf_coefficient (:607-614) over the reference's dense [R'', SR, K] tensor
+    # (point_aggregators.py:951-958): every (slot, k) of a valid ray, where empty slots and masked
+    # neighbours read conf at the clamped index 0 (neural_points.py:956-967)
+    K = q["pidx"].shape[1]
+    pd = torch.full((R, SR, K), -1, dtype=torch.long, device=dev).index_put((sr, slot), q["pidx"].long())
+    pd = pd[ray_mask]
+    cd = points.points_conf[torch.clamp(pd, min=0).reshape(-1)].view(pd.shape)
+    cc = cd - (cd - torch.clamp(cd, 1e-4, 1.0)).detach()
+    val = torch.clamp(cc, zero_eps, 1 - zero_eps)
+    l_zo = torch.mean(torch.log(val) + torch.log(1 - val)) if cc.numel() else torch.zeros((), device=dev)
+    total = l_col + 3e-6 + zero_one_weight * l_zo
+    return total, {"ray_masked_coarse_raycolor": l_col.detach(), "conf_coefficient": l_zo.detach()}, full, ray_mask
+
+
+class Trainer:
+    """One data-parallel training step per call (config 5: 4096 random rays per rank)."""
+
+    def __init__(self, points: PointParams, mlp_state, opts: HotPathOpts, device, lr=5e-4, plr=2e-3,
+                 lr_decay_exp=0.1, lr_decay_iters=1_000_000, bucket_mb=64, querier=None):
+        self.device = torch.device(device)
+        self.opts = opts
+        self.points = points
+        self.mlp = ViewMLP(mlp_state).to(self.device)
+        self.net_params = list(self.mlp.parameters())
+        self.point_params = [points.points_embeding, points.points_color, points.points_dir, points.points_conf]
+        self.opt_net = torch.optim.Adam(self.net_params, lr=lr, betas=(0.9, 0.999))
+        self.opt_pts = torch.optim.Adam(self.point_params, lr=plr, betas=(0.9, 0.999))
+        self.base_lr = (lr, plr)
+        self.decay = (lr_decay_exp, lr_decay_iters)
+        self.step_count = 0
+        self.bucket_elems = bucket_mb * (1 << 20) // 4
+        self.querier = querier
+
+    def _query(self, campos, raydir, near, far):
+        """HIP query -> sample-major dict (indices carry no gradient)."""
+        if self.querier is None:
+            from .querier import LightningFastQuerier
+            self.querier = LightningFastQuerier(self.device, self.opts)
+        res = self.querier.query_samples(self.points.xyz, campos, raydir, near, far)
+        S = res.n_samples()
+        return {"ray_ns": res.ray_ns[: raydir.shape[0]].long(), "ray_soff": res.ray_soff[: raydir.shape[0]].long(),
+                "samp_ray": res.samp_ray[:S].long(), "samp_locw": res.samp_locw[: S * 3].view(S, 3).clone(),
+                "pidx": res.pidx[: S * self.opts.K].view(S, self.opts.K).long()}
+
+    def allreduce_grads(self, params):
+        """Mean of the gradients over ranks, in flat buckets (one collective per bucket)."""
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        n = dist.get_world_size()
+        grads = [p.grad for p in params if p.grad is not None]
+        i = 0
+        while i < len(grads):
+            bucket, size = [], 0
+            while i < len(grads) and (not bucket or size + grads[i].numel() <= self.bucket_elems):
+                bucket.append(grads[i])
+                size += grads[i].numel()
+                i += 1
+            flat = torch.cat([g.reshape(-1) for g in bucket])
+            dist.all_reduce(flat)
+            flat /= n
+            off = 0
+            for g in bucket:
+                g.copy_(flat[off:off + g.numel()].view_as(g))
+                off += g.numel()
+
+    def _set_lr(self):
+        exp, iters = self.decay
+        f = exp ** (self.step_count / iters)  # iter_exponential_decay (helpers/networks.py get_scheduler)
+        for opt, base in ((self.opt_net, self.base_lr[0]), (self.opt_pts, self.base_lr[1])):
+            for g in opt.param_groups:
+                g["lr"] = base * f
+
+    def backward(self, campos, rot, raydir, near, far, gt, q=None):
+        """Forward + backward + gradient all-reduce (no parameter update)."""
+        if q is None:
+            q = self._query(campos.reshape(3).contiguous(), raydir.reshape(-1, 3).contiguous(), near, far)
+        self.opt_net.zero_grad(set_to_none=True)
+        self.opt_pts.zero_grad(set_to_none=True)
+        total, parts, full, ray_mask = loss_from_query(self.points, self.mlp, q, campos, rot, raydir, gt, self.opts)
+        total.backward()
+        for p in self.point_params + self.net_params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        self.allreduce_grads(self.net_params + self.point_params)
+        parts["total"] = total.detach()
+        return parts, full.detach(), ray_mask
+
+    def apply(self):
+        self._set_lr()
+        self.opt_net.step()
+        self.opt_pts.step()
+        self.step_count += 1
+
+    def step(self, campos, rot, raydir, near, far, gt, q=None):
+        """One optimisation step; returns the loss parts (detached) and the rendered colour."""
+        out = self.backward(campos, rot, raydir, near, far, gt, q)
+        self.apply()
+        return out
+
+    def mlp_state(self):
+        return self.mlp.state()
+
+
+def psnr(mse):
+    return -10.0 * math.log10(max(float(mse), 1e-12))
