@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 2
+#define SGN_ABI_VERSION 3
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -87,6 +87,7 @@ typedef struct {
     int32_t dense_out;   /* 0: pidx indexed by sample; 1: by ray*SR+slot (reference layout) */
     int32_t semantic;    /* 1: semantic-guidance filter (:489-591) */
     uint64_t seconds;    /* wall-clock value the semantic filter reads (:553) */
+    int32_t count_traffic; /* 1: fill counters[2..3] (bench byte model; slower kNN) */
 } sgn_query_params;
 
 /* Sample-major outputs of one query call (all device, caller-allocated,
@@ -99,8 +100,8 @@ typedef struct {
  *   samp_nnb  int32[S]        valid neighbours of the sample (0..K)
  *   pidx      int32[S*K] or [R*SR*K] (dense_out; caller pre-fills -1)
  *   work      int32[S]        ids of samples with samp_nnb > 0 (unordered)
- *   counters  int32[4]        [0] = S (total samples), [1] = work items, [2] voxel words and
- *                             [3] candidate points the kNN read (algorithmic-traffic counters)
+ *   counters  int32[4]        [0] = S (total samples), [1] = work items; with count_traffic:
+ *                             [2] voxel words and [3] (uint32) candidate points the kNN read
  */
 typedef struct {
     int32_t *ray_ns, *ray_soff, *samp_ray, *samp_d, *samp_nnb, *pidx, *work, *counters;
@@ -157,6 +158,27 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
                   int32_t K, const void *d_packed_mlp, float *d_out_feat, float *d_out_blend,
                   float *d_out_wnorm, void *d_workspace, size_t workspace_bytes, int32_t stages,
                   sgn_stream_t stream);
+
+/* ---- SG-NeRF variant: block2_bpnet (shading_feature_mlp_layer2_bpnet) ---
+ * Replaces PointAggregator.block2_bpnet (models/aggregators/point_aggregators.py:345-354,
+ * applied at :629-636) and the BPNet-embedding gather of NeuralPoints.forward
+ * (models/neural_points/neural_points.py:970-972): Linear(256 + bpnet_dim -> 256) + LReLU
+ * on [block1 output | bpnet_points_embedding[pidx]] between block1 and block3.
+ * Supported: bpnet_layers 0 (= the base functions above), or 1 with bpnet_dim 96
+ * (predict_semantic = 1, semantic_guidance = 1) or 0 (predict_semantic = 0).
+ * Weight order: the 9 base layers, then block2_bpnet.0 ([256][256 + bpnet_dim]). */
+size_t sgn_mlp_packed_bytes_sg(int32_t bpnet_layers, int32_t bpnet_dim); /* 0: unsupported */
+int sgn_mlp_pack_sg(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w,
+                    const float *const *b, void *d_packed, sgn_stream_t stream);
+/* bpnet_points_embedding f32[N, 96] -> fp16 [N, 96] (the table sgn_aggregate_sg gathers;
+ * the reference holds it detached, neural_points.py:662). 16-byte aligned pointers. */
+int sgn_bpnet_pack(const float *d_embedding, int64_t n_points, int32_t bpnet_dim, void *d_out_f16,
+                   sgn_stream_t stream);
+int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpnet_f16,
+                     const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
+                     int32_t K, const void *d_packed_mlp, float *d_out_feat, float *d_out_blend,
+                     float *d_out_wnorm, void *d_workspace, size_t workspace_bytes,
+                     int32_t stages, sgn_stream_t stream);
 
 /* ---- composite --------------------------------------------------------- */
 

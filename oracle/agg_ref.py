@@ -7,6 +7,7 @@ Follows, operation for operation:
   PointAggregator.forward (agg_dist_pers=20, linear kernel, weight norm, conf clamp)
                                            models/aggregators/point_aggregators.py:868-959, :494-502, :863-865
   viewmlp (agg_intrp_order=2)              models/aggregators/point_aggregators.py:561-786
+    + SG block2_bpnet                        models/aggregators/point_aggregators.py:345-354, :629-636
   positional_encoding                      models/helpers/networks.py:175-192
   ray_dist                                 models/neural_points_volumetric_model.py:569-577
   ray_march + alpha_blend + radiance       models/rendering/diff_ray_marching.py:509-555,
@@ -56,7 +57,8 @@ def _lrelu(x):
 
 
 def aggregate(points, mlp, campos, rot, raydir, samp_ray, samp_locw, pidx):
-    """points: dict xyz[N,3], embedding[N,32], color[N,3], dir[N,3], conf[N,1] (fp32 tensors);
+    """points: dict xyz[N,3], embedding[N,32], color[N,3], dir[N,3], conf[N,1] (fp32 tensors),
+    optional bpnet[N,96] (SG);
     mlp: reference state_dict names (aggregator.* prefix stripped);
     campos [3], rot [3,3], raydir [R,3]; per sample: samp_ray [S], samp_locw [S,3], pidx [S,K].
     Returns feat [S,4] = (alpha, r, g, b) (zeros for samples without neighbours) and
@@ -97,6 +99,12 @@ def aggregate(points, mlp, campos, rot, raydir, samp_ray, samp_locw, pidx):
     f = torch.cat([f, positional_encoding(f, 3)], dim=-1)
     f = torch.cat([f, d6], dim=-1)
     f = _lrelu(_lin(mlp, "block1.2", _lrelu(_lin(mlp, "block1.0", f))))
+    if "block2_bpnet.0.weight" in mlp:
+        # SG block2_bpnet (point_aggregators.py:629-636): [h | gathered BPNet embedding] when the
+        # embedding is given (semantic_guidance, neural_points.py:970-972), then Linear + LReLU
+        if points.get("bpnet") is not None:
+            f = torch.cat([f, points["bpnet"][flat].view(S * K, -1)[m]], dim=-1)
+        f = _lrelu(_lin(mlp, "block2_bpnet.0", f))
     sd = pdir.reshape(-1, 3)[m]
     ov = ori_v[:, None, :].repeat(1, K, 1).reshape(-1, 3)[m]
     f = torch.cat([f, color.reshape(-1, 3)[m], sd - ov, torch.sum(sd * ov, dim=-1, keepdim=True)], dim=-1)

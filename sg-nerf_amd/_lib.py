@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -30,7 +30,8 @@ class GridInfo(ctypes.Structure):
 
 class QueryParams(ctypes.Structure):
     _fields_ = [("SR", c_i32), ("K", c_i32), ("D", c_i32), ("per_ray_t", c_i32), ("r2", c_f32),
-                ("dense_out", c_i32), ("semantic", c_i32), ("seconds", c_u64)]
+                ("dense_out", c_i32), ("semantic", c_i32), ("seconds", c_u64),
+                ("count_traffic", c_i32)]
 
 
 class QueryOut(ctypes.Structure):
@@ -65,6 +66,11 @@ SIGNATURES = {
     "sgn_aggregate_workspace_bytes": (c_sz, [c_i64]),
     "sgn_aggregate": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,
                               c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
+    "sgn_mlp_packed_bytes_sg": (c_sz, [c_i32, c_i32]),
+    "sgn_mlp_pack_sg": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
+    "sgn_bpnet_pack": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "sgn_aggregate_sg": (c_i32, [c_i32, c_i32, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64,
+                                 c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
                               c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_ray_march_dense": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.POINTER(c_f32), c_vp, c_vp, c_vp,

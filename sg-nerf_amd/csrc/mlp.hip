@@ -53,9 +53,9 @@ struct WBlob {
     }
 };
 
-__device__ __forceinline__ WBlob make_blob(const void *p) {
+__device__ __forceinline__ WBlob make_blob(const void *p, size_t bytes = TOTAL_BYTES) {
     WBlob b;
-    b.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)TOTAL_BYTES, 0x00020000);
+    b.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
     return b;
 }
 
@@ -122,6 +122,8 @@ struct AggArgs {
     const float *samp_locw;
     // weights
     const void *blob;
+    size_t blob_bytes;
+    const _Float16 *bpnet;  // [N, bpnet_dim] fp16 (SG variant with predict_semantic = 1), else null
     // outputs
     float *feat;      // float4 per sample id: .x alpha written here
     float *blend;     // [S*8] weight * conf (optional)
@@ -179,7 +181,7 @@ constexpr int PF_N = CHUNK_FRAGS / N_DMA_WAVES;  // LDS-DMA instructions per iss
 constexpr int DIST = SGN_DIST;                // chunks in flight ahead of the one being consumed
 constexpr int NSLOT = DIST + LAG + 1;         // ring slots (the DMA target was read LAG+1 chunks ago)
 constexpr int LDS_F32_OFF = NSLOT * SLOT_BYTES;
-constexpr int LDS_BYTES = LDS_F32_OFF + (int)N_F32 * 4;
+constexpr int LDS_BYTES = LDS_F32_OFF + (int)(N_F32 + HID) * 4;  // + block2_bpnet bias (SG)
 static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the waves");
 
 template <class F, int... I>
@@ -270,57 +272,80 @@ __device__ __forceinline__ h8 l0_step(const float (&feat)[16], const float (&dis
                  l0_channel<8 * K0 + 6>(feat, dist), l0_channel<8 * K0 + 7>(feat, dist));
 }
 
-__host__ __device__ constexpr int layer_ks(int L) { return L == 0 ? KS_L0 : L == 2 ? KS_L2 : KS_HID; }
-__host__ __device__ constexpr int layer_nch(int L) { return (layer_ks(L) + layer_kc(L) - 1) / layer_kc(L); }
-__host__ __device__ constexpr size_t layer_off(int L) {
-    return L == 0 ? OFF_W0 : L == 1 ? OFF_W1 : L == 2 ? OFF_W2 : OFF_W3;
+// Layers of the row stream: 0 block1.0, 1 block1.2, 2 block3.0, 3 block3.2, 4 block2_bpnet.0
+// (SG variant only).  KSB = k-steps of block2_bpnet.0 (0: variant absent).  Stream order:
+// 0, 1, [4], 2, 3.
+__host__ __device__ constexpr int layer_ks(int KSB, int L) {
+    return L == 0 ? KS_L0 : L == 2 ? KS_L2 : L == 4 ? KSB : KS_HID;
 }
-__host__ __device__ constexpr int chunk_nk(int L, int c) {
-    return (layer_ks(L) - c * layer_kc(L)) < layer_kc(L) ? (layer_ks(L) - c * layer_kc(L)) : layer_kc(L);
+__host__ __device__ constexpr int layer_nch(int KSB, int L) {
+    return (layer_ks(KSB, L) + layer_kc(L) - 1) / layer_kc(L);
+}
+__host__ __device__ constexpr size_t layer_off(int L) {
+    return L == 0 ? OFF_W0 : L == 1 ? OFF_W1 : L == 2 ? OFF_W2 : L == 3 ? OFF_W3 : OFF_WB;
+}
+__host__ __device__ constexpr int chunk_nk(int KSB, int L, int c) {
+    return (layer_ks(KSB, L) - c * layer_kc(L)) < layer_kc(L) ? (layer_ks(KSB, L) - c * layer_kc(L)) : layer_kc(L);
 }
 // stream position: layer L, pass P (tiles TP*P..), chunk C (k-steps C*KC..) -> blob offset
-__host__ __device__ constexpr uint32_t chunk_off(int L, int P, int C) {
-    return (uint32_t)(layer_off(L) + ((size_t)P * layer_ks(L) * layer_tp(L) +
+__host__ __device__ constexpr uint32_t chunk_off(int KSB, int L, int P, int C) {
+    return (uint32_t)(layer_off(L) + ((size_t)P * layer_ks(KSB, L) * layer_tp(L) +
                                       (size_t)C * layer_kc(L) * layer_tp(L)) * FRAG);
 }
 
 // ---- chunk stream ---------------------------------------------------------------
-// Per work tile the stream is: layer 0 (1 pass x 9 chunks), layers 1..3 (2 passes each).
-__host__ __device__ constexpr int pass_chunks(int L) { return layer_nch(L); }
-__host__ __device__ constexpr int layer_chunks(int L) { return layer_np(L) * layer_nch(L); }
-__host__ __device__ constexpr int chunk_base(int L) {
-    return L == 0 ? 0 : chunk_base(L - 1) + layer_chunks(L - 1);
+// Per work tile the stream is: layer 0 (1 pass x 9 chunks), then the chained layers
+// (2 passes each) in stream order.
+__host__ __device__ constexpr int n_stream(int KSB) { return KSB ? 5 : 4; }
+__host__ __device__ constexpr int stream_layer(int KSB, int i) { return KSB ? (i < 2 ? i : i == 2 ? 4 : i - 1) : i; }
+__host__ __device__ constexpr int stream_pos(int KSB, int L) { return KSB ? (L < 2 ? L : L == 4 ? 2 : L + 1) : L; }
+__host__ __device__ constexpr int pass_chunks(int KSB, int L) { return layer_nch(KSB, L); }
+__host__ __device__ constexpr int layer_chunks(int KSB, int L) { return layer_np(L) * layer_nch(KSB, L); }
+__host__ __device__ constexpr int pos_base(int KSB, int i) {
+    return i == 0 ? 0 : pos_base(KSB, i - 1) + layer_chunks(KSB, stream_layer(KSB, i - 1));
 }
-constexpr int NCHUNK = chunk_base(3) + layer_chunks(3);
-__host__ __device__ constexpr int chunk_index(int L, int P, int C) { return chunk_base(L) + P * pass_chunks(L) + C; }
-__host__ __device__ constexpr int chunk_L(int n) {
-    return n < chunk_base(1) ? 0 : n < chunk_base(2) ? 1 : n < chunk_base(3) ? 2 : 3;
+__host__ __device__ constexpr int chunk_base(int KSB, int L) { return pos_base(KSB, stream_pos(KSB, L)); }
+__host__ __device__ constexpr int n_chunks(int KSB) { return pos_base(KSB, n_stream(KSB)); }
+__host__ __device__ constexpr int chunk_index(int KSB, int L, int P, int C) {
+    return chunk_base(KSB, L) + P * pass_chunks(KSB, L) + C;
 }
-__host__ __device__ constexpr int chunk_P(int n) { return (n - chunk_base(chunk_L(n))) / pass_chunks(chunk_L(n)); }
-__host__ __device__ constexpr int chunk_C(int n) { return (n - chunk_base(chunk_L(n))) % pass_chunks(chunk_L(n)); }
+__host__ __device__ constexpr int chunk_pos(int KSB, int n, int i = 0) {
+    return (i + 1 >= n_stream(KSB) || n < pos_base(KSB, i + 1)) ? i : chunk_pos(KSB, n, i + 1);
+}
+__host__ __device__ constexpr int chunk_L(int KSB, int n) { return stream_layer(KSB, chunk_pos(KSB, n)); }
+__host__ __device__ constexpr int chunk_P(int KSB, int n) {
+    return (n - chunk_base(KSB, chunk_L(KSB, n))) / pass_chunks(KSB, chunk_L(KSB, n));
+}
+__host__ __device__ constexpr int chunk_C(int KSB, int n) {
+    return (n - chunk_base(KSB, chunk_L(KSB, n))) % pass_chunks(KSB, chunk_L(KSB, n));
+}
+static_assert(CHUNK_FRAGS != 32 || n_chunks(0) == 5 + 2 * (2 + 3 + 2), "base stream");
+static_assert(CHUNK_FRAGS != 32 || (chunk_L(ks_bp(BP_DIM), 9) == 4 && chunk_L(ks_bp(BP_DIM), 8) == 1 &&
+                                     chunk_L(ks_bp(BP_DIM), 15) == 2 && n_chunks(ks_bp(BP_DIM)) == 25),
+              "SG stream order");
 
 // Issue the LDS-DMA of stream chunk N into LDS slot `dst`: each wave moves fragments
 // w + WG_WAVES*j (1 KiB, lane-linear) with buffer_load ... lds; indices past the chunk
 // re-load its last fragment into unused slot space so every wave issues exactly PF_N
 // DMAs per chunk (the counted vmcnt below relies on it).
-template <int N>
+template <int KSB, int N>
 __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
-    constexpr int L = chunk_L(N), P = chunk_P(N), C = chunk_C(N);
-    constexpr int nf = chunk_nk(L, C) * layer_tp(L);
+    constexpr int L = chunk_L(KSB, N), P = chunk_P(KSB, N), C = chunk_C(KSB, N);
+    constexpr int nf = chunk_nk(KSB, L, C) * layer_tp(L);
 #pragma unroll
     for (int j = 0; j < PF_N; ++j) {
         const int i = w + N_DMA_WAVES * j;
         const int src = min(i, nf - 1);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             wb.rsrc, (__attribute__((address_space(3))) void *)(dst + i * (int)FRAG), 16,
-            lane * 16, chunk_off(L, P, C) + (uint32_t)(src * (int)FRAG + lz), 0, 0);
+            lane * 16, chunk_off(KSB, L, P, C) + (uint32_t)(src * (int)FRAG + lz), 0, 0);
     }
 }
 
 // Chunk boundary: wait for this wave's DMAs of the chunk about to be read (all but the
 // DIST-1 younger chunks' PF_N each), drain LDS reads, barrier; then start the DMA that is
 // DIST chunks ahead into the slot read one chunk ago.
-template <int N>
+template <int KSB, int N>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz) {
 #ifdef SGN_ABLATE_STREAM  // timing experiment only: no weight stream, no barriers (wrong results)
     return;
@@ -338,7 +363,7 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
     if (issuer) {
         int tgt = slot + DIST;
         tgt = tgt >= NSLOT ? tgt - NSLOT : tgt;
-        dma_chunk<(N + DIST) % NCHUNK>(wb, lds + tgt * SLOT_BYTES, w, lane, lz);
+        dma_chunk<KSB, (N + DIST) % n_chunks(KSB)>(wb, lds + tgt * SLOT_BYTES, w, lane, lz);
     }
 }
 
@@ -361,7 +386,7 @@ __device__ __forceinline__ float lrelu_max(float x) { return __builtin_fmaf(0.50
 // TRANS: the activations are the A operand and the weights the B operand, so the
 // accumulators hold D^T (lane = output unit, registers = rows) and start at zero (the bias
 // is added in the epilogue, where it is one value per lane).
-template <int L, int P, bool TRANS = false, class InFn>
+template <int KSB, int L, int P, bool TRANS = false, class InFn>
 __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
                                          const float *Fl, size_t fb, f32x16 (&acc)[layer_tp(L)], InFn &&in) {
     constexpr int TP = layer_tp(L), KC = layer_kc(L);
@@ -377,12 +402,12 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
                              b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
         }
     }
-    static_for<layer_nch(L)>([&](auto cc) {
+    static_for<layer_nch(KSB, L)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
-        chunk_enter<chunk_index(L, P, C)>(wb, lds, slot, w, lane, lz);
+        chunk_enter<KSB, chunk_index(KSB, L, P, C)>(wb, lds, slot, w, lane, lz);
         const char *sl = lds + slot * SLOT_BYTES;
         // weight fragments through a register queue PD deep, so LDS latency overlaps PD MFMAs
-        constexpr int NF = chunk_nk(L, C) * TP, PD = NF < FRAG_PD ? NF : FRAG_PD;
+        constexpr int NF = chunk_nk(KSB, L, C) * TP, PD = NF < FRAG_PD ? NF : FRAG_PD;
         auto frag = [&](int f) { return *(const h8 *)(sl + f * (int)FRAG + lane * 16); };
         h8 fr[PD];
 #pragma unroll
@@ -390,7 +415,7 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
 #if SGN_SCHED_PIN
         __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);  // PD LDS reads in flight first
 #endif
-        static_for<chunk_nk(L, C)>([&](auto kk) {
+        static_for<chunk_nk(KSB, L, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
             const h8 B = in(std::integral_constant<int, C * KC + KK>{});
             static_for<TP>([&](auto tt) {
@@ -442,10 +467,16 @@ __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]
         }
 }
 
+template <bool C, class T>
+__device__ __forceinline__ T &pick(T &a, T &b) {
+    if constexpr (C) return a; else return b;
+}
+
 struct RowIn {
     int s;       // sample id
     bool sval;   // work item exists
     float wgt;   // normalised weight * conf of this row
+    int pid;     // neighbour point index (-1: masked)
 };
 
 // Gather + pers + dists + weights of this lane's row; raw features for the
@@ -463,6 +494,7 @@ __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, in
     const int pid = ri.sval ? a.pidx[(int64_t)s * 8 + kk] : -1;
 #endif
     const bool m = pid >= 0;
+    ri.pid = pid;
     const float lx = a.samp_locw[(int64_t)s * 3 + 0], ly = a.samp_locw[(int64_t)s * 3 + 1],
                 lz = a.samp_locw[(int64_t)s * 3 + 2];
     const int ray = a.samp_ray[s];
@@ -522,21 +554,29 @@ __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, in
     return ri;
 }
 
+template <int KSB>
 __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    constexpr int NBP = KSB > KS_HID ? KSB - KS_HID : 0;  // BPNet k-steps (SG, predict_semantic = 1)
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES + WG_WAVES * NBP * (int)FRAG];
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, kk = lane & 7, q = (lane & 31) >> 3;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nwork = a.counters[1];
     const int end = min(nwork, a.item0 + a.n_items);
     const Cam cam = load_cam(a.campos, a.rot);
-    const WBlob wb = make_blob(a.blob);
+    const WBlob wb = make_blob(a.blob, a.blob_bytes);
+    const __amdgpu_buffer_rsrc_t bp_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.bpnet, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t fs_rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.fs, (short)0, 0x7fffffff, 0x00020000);
     {   // fp32 parameters (biases, alpha weights) -> LDS once
         const float *src = (const float *)((const char *)a.blob + OFF_F32);
         float *dst = (float *)(lds + LDS_F32_OFF);
         for (int i = threadIdx.x; i < (int)N_F32; i += ROWS_TPB) dst[i] = src[i];
+        if constexpr (KSB > 0) {  // block2_bpnet.0 bias (acc order) after the base section
+            const float *bb = (const float *)((const char *)a.blob + off_bb(KSB));
+            for (int i = threadIdx.x; i < HID; i += ROWS_TPB) dst[F_BB + i] = bb[i];
+        }
     }
     __syncthreads();  // parameters visible before the first tile's bias reads
     int slot = 0;
@@ -544,7 +584,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     if (!LAG || w < N_DMA_WAVES) {
         static_for<DIST>([&](auto nn) {
             constexpr int N0 = decltype(nn)::value;
-            dma_chunk<N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
+            dma_chunk<KSB, N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
         });
     } else {
         // followers start LAG chunk intervals late (the leaders add LAG barriers at the end)
@@ -560,29 +600,54 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         float feat[16], dist[3];
         h8 ext;
         const RowIn ri = gather_row(a, cam, item, end, lane, feat, dist, ext);
+        // SG: this row's BPNet embedding -> the wave's LDS area as ready-made B fragments
+        // (LDS-DMA, one 1-KiB fragment per k-step; lane (row, half h) <- channels 16j+8h..+7).
+        // Its vmcnt is covered by the chunk waits before block2_bpnet (older than those DMAs).
+        char *bpl = ldsi + LDS_BYTES + w * NBP * (int)FRAG;
+        if constexpr (KSB > KS_HID) {
+            const uint32_t rb = (uint32_t)(ri.pid < 0 ? 0 : ri.pid) * (NBP * 32) + 16 * h;
+#pragma unroll
+            for (int j = 0; j < NBP; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    bp_rsrc, (__attribute__((address_space(3))) void *)(bpl + j * (int)FRAG), 16, rb + 32 * j, 0, 0, 0);
+        }
         h8 actA[16], actB[16];
         {   // block1.0: 284 -> 256, one pass over 8 tiles, inputs generated per k-step
             f32x16 acc0[8];
-            run_pass<0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0,
-                           [&](auto k) { return l0_step<decltype(k)::value>(feat, dist); });
+            run_pass<KSB, 0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0,
+                                [&](auto k) { return l0_step<decltype(k)::value>(feat, dist); });
             chain_out<8, 0>(acc0, actA);
         }
         f32x16 acc[4];
         // block1.2: 256 -> 256
         auto inA = [&](auto k) { return actA[decltype(k)::value]; };
-        run_pass<1, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
+        run_pass<KSB, 1, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
         chain_out<4, 0>(acc, actB);
-        run_pass<1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
+        run_pass<KSB, 1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
         chain_out<4, 1>(acc, actB);
-        // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256
-        auto inB = [&](auto k) {
+        if constexpr (KSB > 0) {
+            // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256 (point_aggregators.py:629-636)
+            auto inBP = [&](auto k) {
+                constexpr int K = decltype(k)::value;
+                if constexpr (K < 16) return actB[K];
+                else return *(const h8 *)(bpl + (K - 16) * (int)FRAG + lane * 16);
+            };
+            run_pass<KSB, 4, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
+            chain_out<4, 0>(acc, actA);
+            run_pass<KSB, 4, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
+            chain_out<4, 1>(acc, actA);
+        }
+        // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input in actB, or actA after block2_bpnet)
+        auto &in3 = pick<(KSB > 0)>(actA, actB);
+        auto &out3 = pick<(KSB > 0)>(actB, actA);
+        auto in3f = [&](auto k) {
             constexpr int K = decltype(k)::value;
-            if constexpr (K < 16) return actB[K]; else return ext;
+            if constexpr (K < 16) return in3[K]; else return ext;
         };
-        run_pass<2, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, inB);
-        chain_out<4, 0>(acc, actA);
-        run_pass<2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, inB);
-        chain_out<4, 1>(acc, actA);
+        run_pass<KSB, 2, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
+        chain_out<4, 0>(acc, out3);
+        run_pass<KSB, 2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
+        chain_out<4, 1>(acc, out3);
         // block3.2: 256 -> 256, transposed (lane = output unit j = lane & 31 of tile t,
         // register i = row (i & 3) + 8 (i >> 2) + 4h, i.e. sample i >> 2), so the K-blend
         // and the alpha dot product are per-lane FMAs over registers
@@ -628,10 +693,10 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
                 }
             }
         };
-        auto inA3 = [&](auto k) { return actA[decltype(k)::value]; };
-        run_pass<3, 0, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
+        auto inA3 = [&](auto k) { return out3[decltype(k)::value]; };
+        run_pass<KSB, 3, 0, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 0>{});
-        run_pass<3, 1, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
+        run_pass<KSB, 3, 1, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 1>{});
         // alpha: reduce the 16 row partials over the 32 lanes (units) of each half,
         // reduce-scatter style; lane j ends with row index i = 8 b1 + 4 b2 + 2 b3 + b4 (b = bits of j)
@@ -808,12 +873,26 @@ __global__ __launch_bounds__(COL_TPB, 1) void k_color(ColorArgs a) {
     }
 }
 
+// fp32 -> fp16 point table (BPNet embedding of the SG variant): 4 values per thread
+__global__ __launch_bounds__(256) void k_to_f16(const float *__restrict__ src, _Float16 *__restrict__ dst, int64_t n) {
+    for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
+        if (i + 4 <= n) {
+            const f32x4 v = *(const f32x4 *)(src + i);
+            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+            *(h4 *)(dst + i) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        } else {
+            for (int64_t k = i; k < n; ++k) dst[k] = (_Float16)src[k];
+        }
+    }
+}
+
 // ---- host-side packing ---------------------------------------------------------
 
 // column of the reference weight matrix feeding B position p of k-step ks (-1: zero)
 int col_l0(int ks, int p) { return l0_ref_col(p >> 3, 8 * ks + (p & 7)); }
 int col_chain(int ks, int p) { return 16 * ks + perm_acc(p); }
 int col_l2(int ks, int p) { return ks < 16 ? col_chain(ks, p) : (p < 7 ? 256 + p : -1); }
+int col_bp(int ks, int p) { return ks < 16 ? col_chain(ks, p) : 256 + 16 * (ks - 16) + p; }
 int col_c0(int ks, int p) { return ks < 16 ? 16 * ks + p : (16 * (ks - 16) + p < 24 ? 256 + 16 * (ks - 16) + p : -1); }
 
 // kouter: fragment (t, ks) at index ks*n_tiles + t (block1/block3 stream order), else t*KS + ks
@@ -847,11 +926,25 @@ extern "C" {
 
 size_t sgn_mlp_packed_bytes(void) { return sgn::mlp::TOTAL_BYTES; }
 
-int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, sgn_stream_t stream) {
+static int mlp_variant_ksb(int32_t bpnet_layers, int32_t bpnet_dim) {
+    if (bpnet_layers == 0) return 0;
+    if (bpnet_layers == 1 && (bpnet_dim == 0 || bpnet_dim == sgn::mlp::BP_DIM)) return sgn::mlp::ks_bp(bpnet_dim);
+    return -1;
+}
+
+size_t sgn_mlp_packed_bytes_sg(int32_t bpnet_layers, int32_t bpnet_dim) {
+    const int ksb = mlp_variant_ksb(bpnet_layers, bpnet_dim);
+    return ksb < 0 ? 0 : sgn::mlp::total_bytes_sg(ksb);
+}
+
+int sgn_mlp_pack_sg(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,
+                    void *d_packed, sgn_stream_t stream) {
     using namespace sgn;
     using namespace sgn::mlp;
     SGN_REQUIRE(w && b && d_packed, "null argument");
-    std::vector<uint8_t> blob(TOTAL_BYTES, 0);
+    const int ksb = mlp_variant_ksb(bpnet_layers, bpnet_dim);
+    SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    std::vector<uint8_t> blob(total_bytes_sg(ksb), 0);
     auto frag = [&](size_t off) { return (_Float16 *)(blob.data() + off); };
     pack_frags(frag(OFF_W0), w[0], 256, 284, T_HID, KS_L0, col_l0, layer_tp(0));
     pack_frags(frag(OFF_W1), w[1], 256, 256, T_HID, KS_HID, col_chain, layer_tp(1));
@@ -874,10 +967,19 @@ int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, s
         pack_acc_order(F + F_WC3 + c * 128, w[8] + c * 128, T_CHID);
         F[F_BC3 + c] = b[8][c];
     }
+    if (ksb > 0) {  // block2_bpnet.0 = w[9] [256, 256 + bpnet_dim], b[9] [256]
+        SGN_REQUIRE(w[9] && b[9], "block2_bpnet.0 weights missing");
+        pack_frags(frag(OFF_WB), w[9], 256, 256 + bpnet_dim, T_HID, ksb, col_bp, layer_tp(4));
+        pack_acc_order((float *)(blob.data() + off_bb(ksb)), b[9], T_HID);
+    }
     hipStream_t st = as_stream(stream);
-    SGN_CHECK_HIP(hipMemcpyAsync(d_packed, blob.data(), TOTAL_BYTES, hipMemcpyHostToDevice, st));
+    SGN_CHECK_HIP(hipMemcpyAsync(d_packed, blob.data(), blob.size(), hipMemcpyHostToDevice, st));
     SGN_CHECK_HIP(hipStreamSynchronize(st));
     return 0;
+}
+
+int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, sgn_stream_t stream) {
+    return sgn_mlp_pack_sg(0, 0, w, b, d_packed, stream);
 }
 
 size_t sgn_aggregate_workspace_bytes(int64_t S) {
@@ -887,12 +989,16 @@ size_t sgn_aggregate_workspace_bytes(int64_t S) {
     return (size_t)S * sgn::mlp::HID * sizeof(_Float16);
 }
 
-int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
-                  const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
-                  void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
+int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpnet_f16,
+                     const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                     const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
+                     void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
     using namespace sgn;
     using namespace sgn::mlp;
     SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace, "null argument");
+    const int ksb = mlp_variant_ksb(bpnet_layers, bpnet_dim);
+    SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    SGN_REQUIRE(ksb <= KS_HID || d_bpnet_f16, "bpnet_dim > 0 needs the fp16 BPNet point embedding");
     SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
     hipStream_t st = as_stream(stream);
     int64_t chunk = (int64_t)(workspace_bytes / (HID * sizeof(_Float16)));
@@ -907,6 +1013,8 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
     a.blob = P;
+    a.blob_bytes = total_bytes_sg(ksb);
+    a.bpnet = (const _Float16 *)d_bpnet_f16;
     a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
     ColorArgs c;
     c.counters = q->counters; c.work = q->work; c.samp_ray = q->samp_ray; c.raydir = pt->raydir;
@@ -917,13 +1025,39 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
         a.n_items = c.n_items = (int32_t)n;
         int64_t wg = (n + WG_SAMPLES - 1) / WG_SAMPLES;  // persistent: one workgroup per CU
         dim3 g1((unsigned)(wg < 256 ? wg : 256));
-        if (stages & 1) hipLaunchKernelGGL(k_agg_rows, g1, dim3(ROWS_TPB), 0, st, a);
+        if (stages & 1) {
+            if (ksb == 0) hipLaunchKernelGGL(k_agg_rows<0>, g1, dim3(ROWS_TPB), 0, st, a);
+            else if (ksb == KS_HID) hipLaunchKernelGGL(k_agg_rows<KS_HID>, g1, dim3(ROWS_TPB), 0, st, a);
+            else hipLaunchKernelGGL(k_agg_rows<ks_bp(BP_DIM)>, g1, dim3(ROWS_TPB), 0, st, a);
+        }
         int64_t wg2 = (n + 32 * (COL_TPB / 64) - 1) / (32 * (COL_TPB / 64));  // 32 samples per wave
         dim3 g2((unsigned)(wg2 < 256 ? wg2 : 256));  // persistent: colour weights loaded once per CU
         if (stages & 2) hipLaunchKernelGGL(k_color, g2, dim3(COL_TPB), 0, st, c);
     }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
+}
+
+int sgn_bpnet_pack(const float *d_embedding, int64_t n_points, int32_t bpnet_dim, void *d_out_f16,
+                   sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(n_points >= 0 && bpnet_dim == mlp::BP_DIM, "bpnet_dim must be 96");
+    SGN_REQUIRE(n_points == 0 || (d_embedding && d_out_f16), "null argument");
+    SGN_REQUIRE(((uintptr_t)d_embedding & 15) == 0 && ((uintptr_t)d_out_f16 & 15) == 0, "16-byte alignment required");
+    const int64_t n = n_points * bpnet_dim;
+    if (n == 0) return 0;
+    int64_t blocks = (n / 4 + 255) / 256;
+    hipLaunchKernelGGL(k_to_f16, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, as_stream(stream),
+                       d_embedding, (_Float16 *)d_out_f16, n);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                  const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
+                  void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
+    return sgn_aggregate_sg(0, 0, nullptr, pt, q, S_capacity, K, d_packed, d_out_feat, d_out_blend, d_out_wnorm,
+                            d_workspace, workspace_bytes, stages, stream);
 }
 
 }  // extern "C"

@@ -49,6 +49,19 @@ constexpr size_t F_BC3 = 2052;                                         // colour
 constexpr size_t N_F32 = 2056;
 constexpr size_t TOTAL_BYTES = OFF_F32 + N_F32 * 4;
 
+// SG-NeRF extension (shading_feature_mlp_layer2_bpnet = 1, point_aggregators.py:345-354,
+// :629-636): block2_bpnet.0 = Linear(256 + bpnet_dim -> 256) + LReLU between block1 and
+// block3, appended after the base blob so the base layout is unchanged.
+//   k-steps 0..15: the chained block1 output (perm_acc order); 16..: the gathered per-point
+//   BPNet embedding, channel 16 j + 8 h + e at k-step 16 + j, lane-half h, element e
+//   (= natural [N, bpnet_dim] order, so the fp16 point table needs no permutation).
+constexpr int BP_DIM = 96;                           // predict_semantic = 1 (:346)
+__host__ __device__ constexpr int ks_bp(int bpnet_dim) { return KS_HID + (bpnet_dim + 15) / 16; }
+constexpr size_t OFF_WB = TOTAL_BYTES;                // block2_bpnet.0 fragments (k-outer stream order)
+__host__ __device__ constexpr size_t off_bb(int ksb) { return OFF_WB + (size_t)T_HID * ksb * FRAG; }  // bias, acc order
+__host__ __device__ constexpr size_t total_bytes_sg(int ksb) { return ksb ? off_bb(ksb) + HID * 4 : TOTAL_BYTES; }
+constexpr size_t F_BB = N_F32;                        // bias slot after the base fp32 section (LDS copy)
+
 // unit of the 32-wide tile held by accumulator register r of lane-half h
 __host__ __device__ constexpr int acc_unit(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 // B-operand position p (0..15, p = 8h + e) of a k-step fed from accumulator registers

@@ -73,6 +73,8 @@ __global__ void k_sample_total(const int32_t *__restrict__ soff, const int32_t *
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         counters[0] = R > 0 ? soff[R - 1] + ns[R - 1] : 0;
         counters[1] = 0;
+        counters[2] = 0;
+        counters[3] = 0;
     }
 }
 
@@ -128,7 +130,7 @@ struct KBuf {
     }
 };
 
-template <int K, bool SEMANTIC>
+template <int K, bool SEMANTIC, bool COUNT>
 __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict__ campos,
                                              const float *__restrict__ raydir,
                                              const float *__restrict__ t_table, int D, int per_ray_t,
@@ -143,6 +145,7 @@ __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict
                                              int32_t *__restrict__ work) {
     const int64_t S = counters[0];
     const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+    int n_vox = 0, n_cand = 0;  // algorithmic-traffic counters (bench roofline), one atomic per wave
     for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
          s += (int64_t)gridDim.x * blockDim.x) {
         const int32_t r = samp_ray[s];
@@ -158,7 +161,6 @@ __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict
         if (SEMANTIC) center_label = ray_labels[r];
         KBuf<K> kb;
         kb.init();
-        int n_vox = 0, n_cand = 0;  // algorithmic-traffic counters (bench roofline)
         const int nlayer = (g.kernel0 + 1) / 2;
         for (int layer = 0; layer < nlayer; ++layer) {
             const int x0 = max(-fx, -layer), x1 = min(g.dims[0] - fx, layer + 1);
@@ -170,10 +172,10 @@ __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict
                         if (max(abs(z), max(abs(x), abs(y))) != layer) continue;
                         const int32_t occ =
                             g.vox[(int64_t)(fx + x) * plane + (int64_t)(fy + y) * g.dims[2] + (fz + z)];
-                        ++n_vox;
+                        if (COUNT) ++n_vox;
                         if (occ < 0) continue;
                         const int32_t st = g.start[occ], n = g.cnt[occ];
-                        n_cand += n;
+                        if (COUNT) n_cand += n;
                         for (int q = 0; q < n; ++q) {
                             const float4 pt = g.pts[st + q];
                             const int32_t pid = __float_as_int(pt.w);
@@ -204,8 +206,17 @@ __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict
             int32_t w = atomicAdd(counters + 1, 1);
             work[w] = (int32_t)s;
         }
-        atomicAdd(counters + 2, n_vox);
-        atomicAdd(counters + 3, n_cand);
+    }
+    if constexpr (COUNT) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            n_vox += __shfl_xor(n_vox, o);
+            n_cand += __shfl_xor(n_cand, o);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(counters + 2, n_vox);
+            atomicAdd((uint32_t *)counters + 3, (uint32_t)n_cand);
+        }
     }
 }
 
@@ -217,18 +228,14 @@ size_t scan_temp_bytes(int64_t R) {
 }
 
 template <int K>
-void launch_knn(dim3 grid, hipStream_t st, bool semantic, GridView g, const float *campos,
+void launch_knn(dim3 grid, hipStream_t st, bool semantic, bool count, GridView g, const float *campos,
                 const float *raydir, const float *t, int D, int per_ray_t, int SR, float r2,
                 int dense, const int32_t *pl, const int32_t *rl, uint32_t sec,
                 const sgn_query_out *o) {
-    if (semantic)
-        hipLaunchKernelGGL((k_knn<K, true>), grid, dim3(TPB), 0, st, g, campos, raydir, t, D, per_ray_t, SR,
-                           r2, dense, pl, rl, sec, o->ray_soff, o->samp_ray, o->samp_d, o->counters,
-                           o->samp_locw, o->samp_nnb, o->pidx, o->work);
-    else
-        hipLaunchKernelGGL((k_knn<K, false>), grid, dim3(TPB), 0, st, g, campos, raydir, t, D, per_ray_t, SR,
-                           r2, dense, pl, rl, sec, o->ray_soff, o->samp_ray, o->samp_d, o->counters,
-                           o->samp_locw, o->samp_nnb, o->pidx, o->work);
+    auto kern = semantic ? (count ? k_knn<K, true, true> : k_knn<K, true, false>)
+                         : (count ? k_knn<K, false, true> : k_knn<K, false, false>);
+    hipLaunchKernelGGL(kern, grid, dim3(TPB), 0, st, g, campos, raydir, t, D, per_ray_t, SR, r2, dense, pl, rl, sec,
+                       o->ray_soff, o->samp_ray, o->samp_d, o->counters, o->samp_locw, o->samp_nnb, o->pidx, o->work);
 }
 
 }  // namespace
@@ -280,10 +287,10 @@ int sgn_query(const sgn_grid *grid, const sgn_query_params *qp, const float *d_c
     dim3 kg((unsigned)(kb < 16384 ? kb : 16384));
     uint32_t sec = (uint32_t)(qp->seconds % 10);
     switch (qp->K) {
-        case 1: launch_knn<1>(kg, st, qp->semantic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
-        case 4: launch_knn<4>(kg, st, qp->semantic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
-        case 8: launch_knn<8>(kg, st, qp->semantic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
-        default: launch_knn<16>(kg, st, qp->semantic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
+        case 1: launch_knn<1>(kg, st, qp->semantic, qp->count_traffic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
+        case 4: launch_knn<4>(kg, st, qp->semantic, qp->count_traffic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
+        case 8: launch_knn<8>(kg, st, qp->semantic, qp->count_traffic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
+        default: launch_knn<16>(kg, st, qp->semantic, qp->count_traffic, g, d_campos, d_raydir, d_t_table, qp->D, qp->per_ray_t, qp->SR, qp->r2, qp->dense_out, d_point_labels, d_ray_labels, sec, o); break;
     }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;

@@ -30,6 +30,7 @@ class HotPathOpts:
     inverse: int = 0
     wcoord_query: int = 1
     semantic_guidance: int = 0
+    predict_semantic: int = 0  # 1: BPNet embedding (96) feeds block2_bpnet (point_aggregators.py:346)
     near_plane: float = 0.1
     far_plane: float = 8.0
     # aggregator (point_aggregators.py)
@@ -73,6 +74,13 @@ class HotPathOpts:
     reservoir_seed: int = 0    # replaces the reference's wall-clock curand seed (:314, :402)
     is_train: int = 0
 
+    @property
+    def bpnet_variant(self):
+        """(bpnet_layers, bpnet_dim) of the aggregator (SG block2_bpnet, point_aggregators.py:345-354)."""
+        if self.shading_feature_mlp_layer2_bpnet == 0:
+            return 0, 0
+        return 1, (96 if self.predict_semantic == 1 else 0)
+
     @classmethod
     def from_opt(cls, opt, **overrides):
         """Take every known field from a reference-style Namespace."""
@@ -102,8 +110,14 @@ class HotPathOpts:
         if (self.shading_feature_mlp_layer1, self.shading_feature_mlp_layer2, self.shading_feature_mlp_layer3,
                 self.shading_alpha_mlp_layer, self.shading_color_mlp_layer) != (2, 0, 2, 1, 4):
             bad.append("viewmlp layer counts must be (2, 0, 2, 1, 4)")
-        if self.shading_feature_mlp_layer2_bpnet != 0:
-            bad.append("block2_bpnet (SG semantic embedding) is not implemented yet")
+        if self.shading_feature_mlp_layer2_bpnet not in (0, 1):
+            bad.append("block2_bpnet: at most one layer (shading_feature_mlp_layer2_bpnet 0 or 1)")
+        elif self.shading_feature_mlp_layer2_bpnet == 1 and bool(self.predict_semantic) != bool(self.semantic_guidance):
+            # the reference concatenates the gathered embedding iff semantic_guidance (neural_points.py:971,
+            # point_aggregators.py:631-635) but sizes the layer by predict_semantic (:346): other pairs crash there
+            bad.append("block2_bpnet needs predict_semantic == semantic_guidance")
+        if self.shading_feature_mlp_layer2_bpnet == 0 and self.predict_semantic not in (0, 1):
+            bad.append("predict_semantic must be 0 or 1")
         if self.act_type != "LeakyReLU" or self.act_super != 1 or self.view_ori != 0:
             bad.append("activations must be LeakyReLU + act_super=1, view_ori=0")
         if self.agg_feat_xyz_mode != "None" or self.agg_alpha_xyz_mode != "None" or self.agg_color_xyz_mode != "None":

@@ -135,8 +135,9 @@ class QueryWorkspace:
 
 
 def run_query(grid: HipGrid, opts: HotPathOpts, campos, raydir, t_table, per_ray_t, ws: QueryWorkspace,
-              dense=False, point_labels=None, ray_labels=None, seconds=None):
-    """Launch sgn_query on the current stream; returns a QueryResult (views into ws)."""
+              dense=False, point_labels=None, ray_labels=None, seconds=None, count_traffic=False):
+    """Launch sgn_query on the current stream; returns a QueryResult (views into ws).
+    count_traffic: also fill counters[2..3] (bench byte model; slows the kNN)."""
     R = raydir.shape[0]
     qp = _lib.QueryParams()
     qp.SR, qp.K, qp.D, qp.per_ray_t = int(opts.SR), int(opts.K), int(t_table.shape[-1]), int(per_ray_t)
@@ -144,6 +145,7 @@ def run_query(grid: HipGrid, opts: HotPathOpts, campos, raydir, t_table, per_ray
     qp.dense_out = int(dense)
     qp.semantic = int(point_labels is not None)
     qp.seconds = int(time.time() if seconds is None else seconds)
+    qp.count_traffic = int(bool(count_traffic))
     if dense:
         ws.pidx[: R * opts.SR * opts.K].fill_(-1)
     res = QueryResult(R, opts.SR, opts.K, ws.ray_ns, ws.ray_soff, ws.samp_ray, ws.samp_d, ws.samp_nnb,
@@ -195,12 +197,13 @@ class LightningFastQuerier:
 
     # -- sample-major fast path ------------------------------------------------------
     def query_samples(self, point_xyz_w_tensor, campos, raydir, near, far, point_labels=None,
-                      ray_labels=None, seconds=None):
+                      ray_labels=None, seconds=None, count_traffic=False):
         grid = self.grid_for(point_xyz_w_tensor)
         R = raydir.shape[0]
         t, per_ray = self.depth_table(near, far, R)
         return run_query(grid, self.opts, campos.reshape(3).contiguous(), raydir.reshape(-1, 3).contiguous(),
-                         t, per_ray, self._workspace(R, False), False, point_labels, ray_labels, seconds)
+                         t, per_ray, self._workspace(R, False), False, point_labels, ray_labels, seconds,
+                         count_traffic)
 
     # -- reference signature ---------------------------------------------------------
     def query_points(self, pixel_idx_tensor, point_xyz_pers_tensor, point_xyz_w_tensor, actual_numpoints_tensor,

@@ -25,7 +25,7 @@ import torch
 from . import _lib
 from .opts import HotPathOpts
 from .render import HipRenderer, PointTables
-from .weights import pack_mlp, strip_prefix
+from .weights import mlp_variant, pack_mlp, strip_prefix
 
 
 def _bg_tuple(bg_color, opts):
@@ -64,8 +64,20 @@ class NeuralPoints:
         self.points_conf = torch.as_tensor(points_conf).to(**f).reshape(1, n, 1)
         self.Rw2c = torch.eye(3, **f)
         self.device = dev
+        # SG-NeRF semantic attributes (neural_points.py:653-665), set by set_bpnet_feats
+        self.bpnet_points_embedding = None  # [1,N,96], detached
+        self.points_label = None            # [N,1]
+        self.points_label_prob = None
         self._tables = None
         self._key = None
+
+    def set_bpnet_feats(self, points_label_prob, points_label, bpnet_points_embedding):
+        """neural_points.py:653-665: per-point BPNet labels and (first call only) embedding."""
+        self.points_label_prob = points_label_prob
+        self.points_label = None if points_label is None else torch.as_tensor(points_label).to(self.device).reshape(-1, 1)
+        if bpnet_points_embedding is not None and self.bpnet_points_embedding is None:
+            self.bpnet_points_embedding = torch.as_tensor(bpnet_points_embedding).detach().to(
+                self.device, torch.float32).reshape(1, self.xyz.shape[0], -1)
 
     @classmethod
     def from_state_dict(cls, sd, device="cuda", prefix="neural_points."):
@@ -83,6 +95,8 @@ class NeuralPoints:
 
     def _version_key(self):
         ts = (self.xyz, self.points_embeding, self.points_color, self.points_dir, self.points_conf)
+        if self.bpnet_points_embedding is not None:
+            ts = ts + (self.bpnet_points_embedding,)
         return tuple((t.data_ptr(), tuple(t.shape), t._version) for t in ts)
 
     def tables(self):
@@ -91,7 +105,7 @@ class NeuralPoints:
             if self.points_embeding.shape[-1] != 32:
                 raise NotImplementedError("the MFMA aggregator is built for point_features_dim = 32")
             self._tables = PointTables(self.xyz, self.points_embeding, self.points_color, self.points_dir,
-                                       self.points_conf, self.device)
+                                       self.points_conf, self.device, self.bpnet_points_embedding)
             self._key = key
         return self._tables
 
@@ -176,8 +190,15 @@ class NeuralPointsRayMarching:
         near = _scalar(inputs["near"]) if "near" in inputs else self.opts.near_plane
         far = _scalar(inputs["far"]) if "far" in inputs else self.opts.far_plane
         bg = _bg_tuple(inputs.get("bg_color"), self.opts)
+        pl = rl = None
+        if self.opts.semantic_guidance == 1:  # neural_points.py:771-785: labels of the points and of the rays
+            if self.neural_points.points_label is None or inputs.get("pixel_label") is None:
+                raise ValueError("semantic_guidance = 1 needs neural_points.points_label and inputs['pixel_label']")
+            pl = self.neural_points.points_label.reshape(-1).to(self.device, torch.int32).contiguous()
+            rl = torch.as_tensor(inputs["pixel_label"]).reshape(-1).to(self.device, torch.int32).contiguous()
         return self.renderer.render(campos, rot, raydir, near, far, want_opacity=True, want_blend=False,
-                                    bg=bg, want_weights=want_weights), raydir.shape[0]
+                                    bg=bg, want_weights=want_weights, point_labels=pl, ray_labels=rl,
+                                    seconds=inputs.get("seconds")), raydir.shape[0]
 
     def _weights(self, out, R):
         """weight [R,SR,K], blend_weight [R,SR,1], conf_coefficient [R,SR,K] (dense ray slots)."""
@@ -240,7 +261,9 @@ class PointAggregator:
         self.opts = opt if isinstance(opt, HotPathOpts) else (HotPathOpts.from_opt(opt) if opt is not None
                                                                else HotPathOpts())
         self.device = torch.device(device)
-        self.packed = pack_mlp(strip_prefix(aggregator_state), self.device)
+        state = strip_prefix(aggregator_state)
+        self.variant = mlp_variant(state)
+        self.packed = pack_mlp(state, self.device)
 
     def forward(self, sampled_color, sampled_label_embedding, sampled_Rw2c, sampled_dir, sampled_conf,
                 sampled_embedding, sampled_xyz_pers, sampled_xyz, sample_pnt_mask, sample_loc, sample_loc_w,
@@ -277,6 +300,15 @@ class PointAggregator:
         pt.dir, pt.conf, pt.n_points = pdir.data_ptr(), conf.data_ptr(), S * K
         pt.campos, pt.camrotc2w, pt.raydir = zero3.data_ptr(), eye.data_ptr(), vdir.data_ptr()
         pt.pers, pt.samp_pers = pers.data_ptr(), loc.data_ptr()
+        nl, dim = self.variant
+        bp = None
+        if dim:  # point_aggregators.py:631-635: [h | sampled_label_embedding] into block2_bpnet
+            if sampled_label_embedding is None:
+                raise ValueError("block2_bpnet with predict_semantic = 1 needs sampled_label_embedding")
+            bp = torch.empty(S * K, 96, dtype=torch.float16, device=dev)
+            lab = f(sampled_label_embedding, 96)
+            _lib.check(_lib.lib().sgn_bpnet_pack(_lib.ptr(lab), S * K, 96, _lib.ptr(bp), _lib.stream_handle()),
+                       "sgn_bpnet_pack")
         qo = _lib.QueryOut()
         qo.ray_ns = qo.ray_soff = qo.samp_d = nnb.data_ptr()
         qo.samp_ray, qo.samp_nnb, qo.pidx = samp_ray.data_ptr(), nnb.data_ptr(), pidx.data_ptr()
@@ -285,9 +317,9 @@ class PointAggregator:
         wnorm = torch.zeros(S, K, dtype=torch.float32, device=dev)
         L = _lib.lib()
         ws = torch.empty(int(L.sgn_aggregate_workspace_bytes(S)), dtype=torch.uint8, device=dev)
-        _lib.check(L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), S, K, _lib.ptr(self.packed), _lib.ptr(feat),
-                                   None, _lib.ptr(wnorm), _lib.ptr(ws), ws.numel(), 3, _lib.stream_handle()),
-                   "sgn_aggregate")
+        _lib.check(L.sgn_aggregate_sg(nl, dim, _lib.ptr(bp), ctypes.byref(pt), ctypes.byref(qo), S, K,
+                                      _lib.ptr(self.packed), _lib.ptr(feat), None, _lib.ptr(wnorm), _lib.ptr(ws),
+                                      ws.numel(), 3, _lib.stream_handle()), "sgn_aggregate_sg")
         # point_aggregators.py:951-953 (forward value of the straight-through clamp)
         conf_coef = torch.clamp(sampled_conf.to(dev)[..., 0], 1e-4, 1.0)
         return feat.view(shp + (4,)), ray_valid.view(shp), wnorm.view(shp + (K,)), conf_coef

@@ -12,7 +12,7 @@ import torch
 from . import _lib
 from .opts import HotPathOpts
 from .querier import LightningFastQuerier
-from .weights import pack_mlp, strip_prefix
+from .weights import mlp_variant, pack_mlp, strip_prefix
 
 
 @dataclass
@@ -31,7 +31,7 @@ class RenderOut:
 class PointTables:
     """Device-resident neural point cloud (contiguous fp32 tables)."""
 
-    def __init__(self, xyz, embedding, color, dir, conf, device):
+    def __init__(self, xyz, embedding, color, dir, conf, device, bpnet=None):
         def t(x, cols):
             x = torch.as_tensor(x).reshape(-1, cols)
             return x.to(device=device, dtype=torch.float32).contiguous()
@@ -41,10 +41,24 @@ class PointTables:
         self.dir = t(dir, 3)
         self.conf = t(conf, 1)
         self.n = self.xyz.shape[0]
+        self.bpnet16 = None
+        if bpnet is not None:
+            self.set_bpnet(bpnet)
+
+    def set_bpnet(self, bpnet):
+        """SG: bpnet_points_embedding [N, 96] (neural_points.py:653-665, detached there too)
+        -> the fp16 table the aggregator gathers (sgn_bpnet_pack)."""
+        b = torch.as_tensor(bpnet).reshape(-1, 96).to(device=self.xyz.device, dtype=torch.float32).contiguous()
+        if b.shape[0] != self.n:
+            raise ValueError(f"bpnet embedding has {b.shape[0]} rows for {self.n} points")
+        self.bpnet16 = torch.empty(self.n, 96, dtype=torch.float16, device=self.xyz.device)
+        with torch.cuda.device(self.xyz.device):
+            _lib.check(_lib.lib().sgn_bpnet_pack(_lib.ptr(b), self.n, 96, _lib.ptr(self.bpnet16),
+                                                 _lib.stream_handle()), "sgn_bpnet_pack")
 
     @classmethod
     def from_cloud(cls, pc, device):
-        return cls(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, device)
+        return cls(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, device, getattr(pc, "bpnet", None))
 
 
 class HipRenderer:
@@ -59,6 +73,10 @@ class HipRenderer:
     def set_mlp(self, mlp_state):
         self.mlp_state = {k: torch.as_tensor(v).detach().to("cpu", torch.float32)
                           for k, v in strip_prefix(mlp_state).items()}
+        self.variant = mlp_variant(self.mlp_state)
+        if self.variant != self.opts.bpnet_variant:
+            raise ValueError(f"aggregator weights are block2_bpnet variant {self.variant}, options say "
+                             f"{self.opts.bpnet_variant} (shading_feature_mlp_layer2_bpnet / predict_semantic)")
         self.packed = pack_mlp(self.mlp_state, self.device)
 
     def _buffers(self, R):
@@ -79,11 +97,14 @@ class HipRenderer:
             self._cap = (R, cap)
 
     def render(self, campos, camrotc2w, raydir, near, far, want_opacity=True, want_blend=False, marks=None,
-               bg=None, want_weights=False):
+               bg=None, want_weights=False, point_labels=None, ray_labels=None, seconds=None,
+               count_traffic=False):
         """One frame.  `marks(name)` (optional) is called between stages on the host thread
         (bench.py records HIP events on the current stream there).  `bg`: 3 floats
         overriding opts.bg_color.  `want_weights`: also produce the normalised neighbour
-        weights and the per-slot alpha-blend weights (reference `weight`, `blend_weight`)."""
+        weights and the per-slot alpha-blend weights (reference `weight`, `blend_weight`).
+        `point_labels` [N] / `ray_labels` [R] int32 (+ `seconds`): the SG semantic-guided kNN
+        (semantic_guidance = 1, worldcoords.py:839-938)."""
         o = self.opts
         mark = marks or (lambda name: None)
         campos = campos.reshape(3).to(self.device, torch.float32).contiguous()
@@ -97,7 +118,10 @@ class HipRenderer:
         if want_weights:
             self.wnorm.zero_()
         mark("query")
-        q = self.querier.query_samples(self.points.xyz, campos, raydir, near, far)
+        if o.semantic_guidance == 1 and (point_labels is None or ray_labels is None):
+            raise ValueError("semantic_guidance = 1 needs point_labels and ray_labels")
+        q = self.querier.query_samples(self.points.xyz, campos, raydir, near, far, point_labels, ray_labels, seconds,
+                                       count_traffic)
         L = _lib.lib()
         st = _lib.stream_handle()
         pt = _lib.PointTables()
@@ -106,12 +130,17 @@ class HipRenderer:
         pt.campos, pt.camrotc2w, pt.raydir = campos.data_ptr(), rot.data_ptr(), raydir.data_ptr()
         qo = q.abi()
         cap = R * o.SR
+        nl, dim = self.variant
+        if dim and self.points.bpnet16 is None:
+            raise ValueError("block2_bpnet with predict_semantic = 1 needs the points' BPNet embedding (set_bpnet)")
+        bp = _lib.ptr(self.points.bpnet16) if dim else None
         for stage, name in ((1, "agg_rows"), (2, "agg_color")):
             mark(name)
-            _lib.check(L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), cap, o.K, _lib.ptr(self.packed),
-                                       _lib.ptr(self.feat), _lib.ptr(self.blend) if want_blend else None,
-                                       _lib.ptr(self.wnorm) if want_weights and stage == 1 else None,
-                                       _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate")
+            _lib.check(L.sgn_aggregate_sg(nl, dim, bp, ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
+                                          _lib.ptr(self.packed), _lib.ptr(self.feat),
+                                          _lib.ptr(self.blend) if want_blend else None,
+                                          _lib.ptr(self.wnorm) if want_weights and stage == 1 else None,
+                                          _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate_sg")
         mark("composite")
         cp = _lib.CompositeParams()
         cp.SR, cp.vsize_z, cp.raydist_mode_unit = o.SR, float(o.vsize[2]), o.raydist_mode_unit

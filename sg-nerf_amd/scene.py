@@ -23,10 +23,28 @@ class PointCloud:
     color: np.ndarray      # float32 [N,3]
     dir: np.ndarray        # float32 [N,3]
     conf: np.ndarray       # float32 [N,1]
+    bpnet: np.ndarray = None   # float32 [N,96] SG BPNet point embedding (optional)
+    labels: np.ndarray = None  # int32 [N] SG point labels (optional)
 
     @property
     def n(self):
         return self.xyz.shape[0]
+
+
+def with_semantics(pc, seed=0, n_classes=20, bpnet_dim=96, cell=None):
+    """Synthetic stand-ins for the BPNet outputs the SG variant consumes (set_bpnet_feats,
+    neural_points.py:653-665): a 96-d per-point embedding and labels 0..n_classes-1.
+    cell=None: labels random per point; cell=c: one label per c-metre cube (spatially
+    coherent, as a segmentation is)."""
+    rng = np.random.default_rng(seed)
+    emb = (rng.standard_normal((pc.n, bpnet_dim)) * 0.5).astype(np.float32)
+    if cell is None:
+        lab = rng.integers(0, n_classes, pc.n).astype(np.int32)
+    else:
+        c = np.floor(pc.xyz / cell).astype(np.int64)
+        h = (c[:, 0] * 73856093) ^ (c[:, 1] * 19349663) ^ (c[:, 2] * 83492791)
+        lab = (np.abs(h) % n_classes).astype(np.int32)
+    return PointCloud(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, emb, lab)
 
 
 def _attributes(rng, n, feat_dim=32):

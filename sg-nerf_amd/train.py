@@ -106,7 +106,7 @@ def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, 
                                     pers[..., 2] - loc[:, None, 2]], dim=-1)], dim=-1)
     weight = mask / torch.clamp(torch.norm(dists[..., :3], dim=-1), min=1e-6)        # :494-502
     weight = weight / torch.clamp(torch.sum(weight, dim=-1, keepdim=True), min=1e-8)  # :946-947
-    conf = points.points_conf[flat].view(S, K)
+    conf = torch.index_select(points.points_conf, 0, flat).view(S, K)
     conf_coef = conf - (conf - torch.clamp(conf, 1e-4, 1.0)).detach()                # :863-865
     w = weight * conf_coef
     valid = mask.any(-1)
@@ -114,13 +114,14 @@ def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, 
     vpe = _pe(v, 4, ori=True)
     ori_v, vpe = vpe[..., :3], vpe[..., 3:]
     m = mask.reshape(-1)
-    emb = points.points_embeding[flat][m]
+    fm = flat[m]  # index_select: its backward is an index_add (atomics), not a sort-based index_put
+    emb = torch.index_select(points.points_embeding, 0, fm)
     x = torch.cat([emb, _pe(emb, 3), _pe(dists.reshape(-1, 6)[m], 5)], dim=-1)
     lr_ = lambda t: F.leaky_relu(t, 0.01)  # noqa: E731
     h = lr_(mlp.f("block1.2", lr_(mlp.f("block1.0", x))))
-    sd = points.points_dir[flat][m]
+    sd = torch.index_select(points.points_dir, 0, fm)
     ov = ori_v[:, None, :].expand(S, K, 3).reshape(-1, 3)[m]
-    h = torch.cat([h, points.points_color[flat][m], sd - ov, torch.sum(sd * ov, dim=-1, keepdim=True)], dim=-1)
+    h = torch.cat([h, torch.index_select(points.points_color, 0, fm), sd - ov, torch.sum(sd * ov, dim=-1, keepdim=True)], dim=-1)
     h = lr_(mlp.f("block3.2", lr_(mlp.f("block3.0", h))))
     alpha = F.softplus(mlp.f("alpha_branch.0", h) - 1)
     hk = torch.zeros(S * K, h.shape[-1], device=h.device, dtype=h.dtype).masked_scatter(m[:, None], h)
@@ -182,7 +183,7 @@ def loss_from_query(points, mlp, q, campos, rot, raydir, gt, opts: HotPathOpts, 
     K = q["pidx"].shape[1]
     pd = torch.full((R, SR, K), -1, dtype=torch.long, device=dev).index_put((sr, slot), q["pidx"].long())
     pd = pd[ray_mask]
-    cd = points.points_conf[torch.clamp(pd, min=0).reshape(-1)].view(pd.shape)
+    cd = torch.index_select(points.points_conf, 0, torch.clamp(pd, min=0).reshape(-1)).view(pd.shape)
     cc = cd - (cd - torch.clamp(cd, 1e-4, 1.0)).detach()
     val = torch.clamp(cc, zero_eps, 1 - zero_eps)
     l_zo = torch.mean(torch.log(val) + torch.log(1 - val)) if cc.numel() else torch.zeros((), device=dev)

@@ -16,7 +16,8 @@ citations: the NeuralPoints gather (neural_points.py:838-850, :956-967), the
 querier's w2pers (worldcoords.py:125-132) and ray_dist
 (neural_points_volumetric_model.py:569-577).
 
-Usage:  python -B tests/golden/make_golden.py
+Usage:  python -B tests/golden/make_golden.py         (reference_aggregator.npz)
+        python -B tests/golden/make_golden.py --sg    (reference_sg.npz, SG block2_bpnet variant)
 """
 import argparse
 import os
@@ -30,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 
 
-def reference_opt():
+def reference_opt(**extra):
     from models.aggregators.point_aggregators import PointAggregator
     parser = argparse.ArgumentParser()
     PointAggregator.modify_commandline_options(parser, True)
@@ -46,6 +47,7 @@ def reference_opt():
         point_dir_mode="1", point_conf_mode="1", act_super=1, view_ori=0, shading_color_channel_num=3,
         sparse_loss_weight=0.0, zero_one_loss_items=["conf_coefficient"], prob=0, weight_xyz_freq=2,
         weight_feat_dim=8, predict_semantic=0)
+    scannet.update(extra)
     for k, v in scannet.items():
         setattr(opt, k, v)
     return opt
@@ -70,7 +72,7 @@ def w2pers_samples(point_xyz_w, camrotc2w, campos):
     return torch.stack([x_pers, y_pers, z_pers], dim=-1)
 
 
-def make_case(name, pc, view, o, agg, refmods, pc_name=None):
+def make_case(name, pc, view, o, agg, refmods, pc_name=None, bpnet=None):
     import oracle_query as oq
     from sgnerf_amd.hyper import grid_hyperparameters
     near_far_linear_ray_generation, ray_march, alpha_blend, radiance_render = refmods
@@ -109,13 +111,17 @@ def make_case(name, pc, view, o, agg, refmods, pc_name=None):
     sampled_color = torch.index_select(color, 1, flat).view(B, Rv, SR, K, 3)
     sampled_dir = torch.index_select(pdir, 1, flat).view(B, Rv, SR, K, 3)
     sampled_conf = torch.index_select(conf, 1, flat).view(B, Rv, SR, K, 1)
+    # SG: neural_points.py:970-972 (gathered only with semantic_guidance)
+    sampled_label = None
+    if bpnet is not None:
+        sampled_label = torch.index_select(torch.from_numpy(bpnet)[None], 1, flat).view(B, Rv, SR, K, bpnet.shape[1])
     Rw2c = torch.eye(3)
     sample_loc = w2pers_samples(sample_loc_w, rot, campos)
     sample_ray_dirs = raydir[0][keep][None, :, None, :].expand(-1, -1, SR, -1).contiguous()
     vsize = np.asarray(o.vsize)
     with torch.no_grad():
         decoded, ray_valid, weight, conf_coef = agg(
-            sampled_color, None, Rw2c, sampled_dir, sampled_conf, sampled_embedding[..., 6:],
+            sampled_color, sampled_label, Rw2c, sampled_dir, sampled_conf, sampled_embedding[..., 6:],
             sampled_embedding[..., 3:6], sampled_embedding[..., :3], mask, sample_loc, sample_loc_w,
             sample_ray_dirs, vsize, 0)
         # ray_dist, neural_points_volumetric_model.py:569-577
@@ -151,6 +157,50 @@ def make_case(name, pc, view, o, agg, refmods, pc_name=None):
         f"{name}/bg_transmission": bg_t[0, :, 0].numpy(), f"{name}/ray_color": ray_color[0].numpy(),
         f"{name}/full_color": full.numpy(),
     }
+
+
+def seeded_aggregator(PointAggregator, seed_torch, seed_bias, **extra):
+    torch.manual_seed(seed_torch)
+    agg = PointAggregator(reference_opt(**extra)).eval()
+    g = torch.Generator().manual_seed(seed_bias)
+    with torch.no_grad():
+        for n, p in agg.named_parameters():
+            if n.endswith("bias"):
+                p.copy_(torch.randn(p.shape, generator=g) * 0.01)
+    return agg
+
+
+def main_sg():
+    """tests/golden/reference_sg.npz: the SG-NeRF aggregator variant (block2_bpnet,
+    point_aggregators.py:345-354, :629-636) run by the imported reference, for
+    predict_semantic 1 (Linear 352->256 on [h | BPNet embedding]) and 0 (Linear 256->256)."""
+    from models.aggregators.point_aggregators import PointAggregator
+    from models.rendering.diff_ray_marching import near_far_linear_ray_generation, ray_march
+    from models.rendering.diff_render_func import alpha_blend, radiance_render
+    import sgnerf_amd  # noqa: F401
+    from sgnerf_amd import scene
+    from sgnerf_amd.opts import HotPathOpts
+    refmods = (near_far_linear_ray_generation, ray_march, alpha_blend, radiance_render)
+    out = {}
+    rng = np.random.default_rng(21)
+    n = 9000
+    xyz = np.stack([rng.uniform(1.7, 2.3, n), np.full(n, 3.0), rng.uniform(1.2, 1.8, n)], 1)
+    xyz[: n // 4, 1] = rng.uniform(2.8, 3.0, n // 4)
+    xyz += rng.normal(0, 0.002, xyz.shape)
+    pc = scene.with_semantics(scene.PointCloud(xyz.astype(np.float32), *scene._attributes(rng, n)), seed=22)
+    view = scene.room_view(16, 16, yaw=90.0, pitch=0.0, campos=(2.0, 2.2, 1.5), focal=40.0)
+    for name, ps in (("sg96", 1), ("sg0", 0)):
+        agg = seeded_aggregator(PointAggregator, 3 + ps, 4 + ps, shading_feature_mlp_layer2_bpnet=1,
+                                predict_semantic=ps)
+        out.update({f"mlp_{name}/{k}": v.detach().numpy() for k, v in agg.state_dict().items()})
+        o = HotPathOpts(SR=24, shading_feature_mlp_layer2_bpnet=1, predict_semantic=ps, semantic_guidance=ps)
+        out.update(make_case(name, pc, view, o, agg, refmods, pc_name="sgpatch", bpnet=pc.bpnet if ps else None))
+    out["sgpatch/bpnet"] = pc.bpnet
+    path = os.path.join(HERE, "reference_sg.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path) / 1e6, "MB")
+    for k in ("sg96", "sg0"):
+        print(k, "valid rays", int(out[f"{k}/ray_mask"].sum()), "valid nb", int((out[f"{k}/sample_pidx"] >= 0).sum()))
 
 
 def main():
@@ -210,4 +260,12 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--sg" in sys.argv:
+        assert os.path.isdir(REF), "the golden generator runs only where /root/reference exists"
+        sys.dont_write_bytecode = True
+        sys.path.insert(0, REF)
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        main_sg()
+    else:
+        main()

@@ -179,3 +179,51 @@ def test_render_vid_frames_match_single_renders(tmp_path):
         assert torch.equal(one, frames[i])
     n = render_vid.write_frames(frames, 24, 32, str(tmp_path))
     assert n == 3 and (tmp_path / "frame_0002.png").exists()
+
+
+# ---- SG-NeRF block2_bpnet variant through the reference API mirrors -----------------
+GOLD_SG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_sg.npz")
+
+
+def _load_sg(name):
+    g = np.load(GOLD_SG, allow_pickle=False)
+    pts = {k: g[f"sgpatch/{k}"] for k in ("xyz", "embedding", "color", "dir", "conf", "bpnet")}
+    pre = f"mlp_{name}/"
+    mlp = {k[len(pre):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(pre)}
+    case = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(name + "/")}
+    return pts, mlp, case
+
+
+@pytest.mark.parametrize("name", ["sg96", "sg0"])
+def test_point_aggregator_sg_matches_reference(name):
+    pts, mlp, case = _load_sg(name)
+    ps = 1 if name == "sg96" else 0
+    o = HotPathOpts(SR=int(case["SR"]), shading_feature_mlp_layer2_bpnet=1, predict_semantic=ps, semantic_guidance=ps)
+    agg = PointAggregator(mlp, o, DEV)
+    args = _gathered(pts, case)
+    if ps:  # neural_points.py:970-972
+        pidx = case["sample_pidx"]
+        R, SR, K = pidx.shape
+        lab = pts["bpnet"][np.clip(pidx, 0, None).reshape(-1)].reshape(R, SR, K, 96)
+        args["sampled_label_embedding"] = torch.from_numpy(np.ascontiguousarray(lab))[None].to(DEV)
+    dec, valid, weight, conf = agg(**args)
+    np.testing.assert_array_equal(valid[0].cpu().numpy(), case["ray_valid"])
+    err = np.abs(dec[0].cpu().numpy() - case["decoded"]).max()
+    print(f"{name}: PointAggregator (SG) max |decoded - reference| = {err:.3e}")
+    assert err <= FEAT_TOL
+
+
+def test_ray_marching_forward_sg_matches_reference():
+    pts, mlp, case = _load_sg("sg96")
+    o = HotPathOpts(SR=int(case["SR"]), shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1)
+    npnts = NeuralPoints(pts["xyz"], pts["embedding"], pts["color"], pts["dir"], pts["conf"], DEV)
+    n = pts["xyz"].shape[0]
+    npnts.set_bpnet_feats(None, torch.zeros(n, dtype=torch.int32), torch.from_numpy(pts["bpnet"]))
+    rm = NeuralPointsRayMarching(npnts, mlp, o, DEV)
+    inp = _inputs(case)
+    inp["pixel_label"] = torch.zeros(1, case["raydir"].shape[0], 1, dtype=torch.int32, device=DEV)
+    out = fill_invalid(rm.forward(inp), inp)
+    err = np.abs(out["coarse_raycolor"][0].cpu().numpy() - case["full_color"]).max()
+    print(f"sg96: NeuralPointsRayMarching max |rgb - reference| = {err:.3e}")
+    assert err <= RGB_TOL
+    np.testing.assert_array_equal(out["ray_mask"][0].cpu().numpy(), case["ray_mask"])

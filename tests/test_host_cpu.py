@@ -81,7 +81,7 @@ def test_opts_from_reference_namespace():
     assert o.vsize == (0.008, 0.008, 0.008) and o.query_size == (3, 3, 3)  # neural_points.py:425
     assert o.check_supported() is o
     with pytest.raises(NotImplementedError, match="block2_bpnet"):
-        HotPathOpts(shading_feature_mlp_layer2_bpnet=1).check_supported()
+        HotPathOpts(shading_feature_mlp_layer2_bpnet=3).check_supported()
     with pytest.raises(NotImplementedError, match="agg_dist_pers"):
         HotPathOpts(agg_dist_pers=10).check_supported()
 
@@ -159,3 +159,35 @@ def test_dense_from_samples():
     assert torch.all(d[0, 2:] == -1) and torch.all(d[1] == -1)
     torch.testing.assert_close(d[2, :3], vals[2:5])
     assert torch.all(d[2, 3] == -1)
+
+
+def test_sg_variant_options_and_weights():
+    import pytest as _pt
+    from sgnerf_amd.opts import HotPathOpts
+    from sgnerf_amd.weights import init_mlp, mlp_variant, layers_for
+    assert HotPathOpts().bpnet_variant == (0, 0)
+    o = HotPathOpts(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1).check_supported()
+    assert o.bpnet_variant == (1, 96)
+    assert HotPathOpts(shading_feature_mlp_layer2_bpnet=1).check_supported().bpnet_variant == (1, 0)
+    with _pt.raises(NotImplementedError):
+        HotPathOpts(shading_feature_mlp_layer2_bpnet=2).check_supported()
+    with _pt.raises(NotImplementedError):  # reference would crash (352-wide layer fed 256)
+        HotPathOpts(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=0).check_supported()
+    s = init_mlp(0, bpnet_layers=1, bpnet_dim=96)
+    assert tuple(s["block2_bpnet.0.weight"].shape) == (256, 352)
+    assert mlp_variant(s) == (1, 96) and mlp_variant(init_mlp(0)) == (0, 0)
+    # base draws unchanged by the extra layer
+    b = init_mlp(0)
+    assert all(torch.equal(b[k], s[k]) for k in b)
+    assert len(layers_for(1, 0)) == 10
+
+
+def test_sg_abi_sizes():
+    from sgnerf_amd import _lib
+    L = _lib.lib()
+    base = int(L.sgn_mlp_packed_bytes())
+    assert int(L.sgn_mlp_packed_bytes_sg(0, 0)) == base
+    assert int(L.sgn_mlp_packed_bytes_sg(1, 96)) == base + 8 * 22 * 1024 + 1024
+    assert int(L.sgn_mlp_packed_bytes_sg(1, 0)) == base + 8 * 16 * 1024 + 1024
+    assert int(L.sgn_mlp_packed_bytes_sg(2, 96)) == 0
+    assert int(L.sgn_mlp_packed_bytes_sg(1, 32)) == 0

@@ -68,3 +68,35 @@ def test_oracle_render_matches_reference(gold, name):
     np.testing.assert_allclose(opacity[keep].numpy(), gold[f"{name}/opacity"], atol=2e-6, rtol=1e-5)
     np.testing.assert_allclose(bg_t[keep].numpy(), gold[f"{name}/bg_transmission"], atol=2e-6, rtol=1e-5)
     np.testing.assert_allclose(full.numpy(), gold[f"{name}/full_color"], atol=2e-6, rtol=1e-5)
+
+
+# ---- SG-NeRF block2_bpnet variant (tests/golden/reference_sg.npz) -------------------
+GOLD_SG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_sg.npz")
+
+
+def sg_case(g, name):
+    pts = {k: torch.from_numpy(g[f"sgpatch/{k}"]) for k in ("xyz", "embedding", "color", "dir", "conf")}
+    if name == "sg96":
+        pts["bpnet"] = torch.from_numpy(g["sgpatch/bpnet"])
+    pre = f"mlp_{name}/"
+    mlp = {k[len(pre):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(pre)}
+    return pts, mlp
+
+
+@pytest.mark.parametrize("name", ["sg96", "sg0"])
+def test_oracle_sg_block2_bpnet_matches_reference(name):
+    g = np.load(GOLD_SG, allow_pickle=False)
+    pts, mlp = sg_case(g, name)
+    assert mlp["block2_bpnet.0.weight"].shape[1] == (352 if name == "sg96" else 256)
+    o = HotPathOpts(SR=int(g[f"{name}/SR"]))
+    xyz = g["sgpatch/xyz"]
+    hy = grid_hyperparameters(o, torch.from_numpy(xyz.min(0)), torch.from_numpy(xyz.max(0)))
+    q = oq.OracleGrid(xyz, hy, o).query(g[f"{name}/campos"], g[f"{name}/raydir"], g[f"{name}/t_table"])
+    sp, _, rm = oq.reference_layout(q)
+    assert_equal_arrays(sp, g[f"{name}/sample_pidx"], "sample_pidx")
+    campos, rot, raydir = (torch.from_numpy(g[f"{name}/{k}"]) for k in ("campos", "camrotc2w", "raydir"))
+    with torch.no_grad():
+        full, ray_mask, fd, opacity, bg_t = agg_ref.render(pts, mlp, campos, rot, raydir, q, o.SR)
+    keep = ray_mask.numpy()
+    np.testing.assert_allclose(fd[keep].numpy(), g[f"{name}/decoded"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(full.numpy(), g[f"{name}/full_color"], atol=2e-6, rtol=1e-5)

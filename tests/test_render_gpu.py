@@ -93,3 +93,76 @@ def test_render_matches_oracle_room(SR, seed, yaw, alpha_bias):
     print(f"room SR={SR}: max |rgb - oracle| = {err:.3e}, valid rays {int(mask.sum())}/{mask.numel()}")
     assert err <= RGB_TOL
     assert int(mask.sum()) > 0.5 * mask.numel()
+
+
+# ---- SG-NeRF block2_bpnet variant -------------------------------------------------------
+GOLD_SG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_sg.npz")
+
+
+@pytest.mark.parametrize("name", ["sg96", "sg0"])
+def test_render_sg_matches_reference_golden(name):
+    """block2_bpnet (point_aggregators.py:345-354, :629-636) in the fused kernel vs the
+    reference's own SG aggregator.  Labels are all 0, which passes the semantic filter
+    (worldcoords.py:548-553), so the query equals the golden's plain query."""
+    g = np.load(GOLD_SG, allow_pickle=False)
+    ps = 1 if name == "sg96" else 0
+    mlp = {k[len(f"mlp_{name}/"):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(f"mlp_{name}/")}
+    pts = PointTables(*(g[f"sgpatch/{k}"] for k in ("xyz", "embedding", "color", "dir", "conf")), DEV,
+                      bpnet=g["sgpatch/bpnet"] if ps else None)
+    o = HotPathOpts(SR=int(g[f"{name}/SR"]), shading_feature_mlp_layer2_bpnet=1, predict_semantic=ps,
+                    semantic_guidance=ps)
+    near, far = (float(x) for x in g[f"{name}/near_far"])
+    raydir = torch.from_numpy(g[f"{name}/raydir"])
+    R = raydir.shape[0]
+    r = HipRenderer(pts, mlp, o, DEV)
+    kw = {}
+    if ps:
+        kw = dict(point_labels=torch.zeros(pts.n, dtype=torch.int32, device=DEV),
+                  ray_labels=torch.zeros(R, dtype=torch.int32, device=DEV), seconds=5)
+    out = r.render(torch.from_numpy(g[f"{name}/campos"]), torch.from_numpy(g[f"{name}/camrotc2w"]), raydir,
+                   near, far, **kw)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.ray_mask.cpu().numpy(), g[f"{name}/ray_mask"])
+    err = np.abs(out.rgb.cpu().numpy() - g[f"{name}/full_color"]).max()
+    print(f"{name}: max |rgb - reference| = {err:.3e}")
+    assert err <= RGB_TOL
+    q = out.query
+    S = q.n_samples()
+    sr = q.samp_ray[:S].cpu().numpy()
+    slot = np.arange(S) - q.ray_soff[:R].cpu().numpy()[sr]
+    valid = q.samp_nnb[:S].cpu().numpy() > 0
+    dense = np.zeros((R, o.SR, 4), np.float32)
+    dense[sr[valid], slot[valid]] = out.feat[:S].cpu().numpy()[valid]
+    keep = g[f"{name}/ray_mask"].astype(bool)
+    ferr = np.abs(dense[keep] - g[f"{name}/decoded"]).max()
+    print(f"{name}: max |decoded - reference| = {ferr:.3e}")
+    assert ferr <= FEAT_TOL
+
+
+def test_render_sg_semantic_matches_oracle_room():
+    """SG end to end on a room: semantic-guided kNN with real labels + block2_bpnet(352)."""
+    pc = scene.with_semantics(small_room(300_000, seed=5), seed=6, n_classes=4)
+    o = HotPathOpts(SR=32, shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1)
+    mlp = init_mlp(5, bias_std=0.01, bpnet_layers=1, bpnet_dim=96)
+    mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 150.0
+    view = make_view(48, 64, yaw=75.0, pitch=-6.0)
+    R = view.raydir.shape[0]
+    ray_labels = np.random.default_rng(7).integers(0, 4, R).astype(np.int32)
+    secs = 12  # seconds % 10 = 2 > 1: the label filter is active (worldcoords.py:553)
+    r = HipRenderer(PointTables(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV, bpnet=pc.bpnet), mlp, o, DEV)
+    out = r.render(torch.from_numpy(view.campos), torch.from_numpy(view.camrotc2w), torch.from_numpy(view.raydir),
+                   view.near, view.far, point_labels=torch.from_numpy(pc.labels).to(DEV),
+                   ray_labels=torch.from_numpy(ray_labels).to(DEV), seconds=secs)
+    torch.cuda.synchronize()
+    hy = hyper_for(pc, o)
+    q = oq.OracleGrid(pc.xyz, hy, o).query(view.campos, view.raydir, r.querier.depth_table(0.1, 8.0, 0)[0].cpu().numpy(),
+                                           point_labels=pc.labels, ray_labels=ray_labels, seconds=secs)
+    tp = {k: torch.from_numpy(getattr(pc, k)) for k in ("xyz", "embedding", "color", "dir", "conf", "bpnet")}
+    with torch.no_grad():
+        full, mask, fd, opacity, bg_t = agg_ref.render(tp, mlp, torch.from_numpy(view.campos),
+                                                       torch.from_numpy(view.camrotc2w), torch.from_numpy(view.raydir), q, o.SR)
+    np.testing.assert_array_equal(out.ray_mask.cpu().numpy().astype(bool), mask.numpy())
+    err = np.abs(out.rgb.cpu().numpy() - full.numpy()).max()
+    print(f"SG room: max |rgb - oracle| = {err:.3e}, valid rays {int(mask.sum())}/{mask.numel()}")
+    assert err <= RGB_TOL
+    assert int(mask.sum()) > 0.5 * mask.numel()
