@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="BASELINE config 5: training steps on 4096 random rays per rank (backward + DP all-reduce)")
     ap.add_argument("--train-rays", type=int, default=4096)
+    ap.add_argument("--train-torch", action="store_true",
+                    help="config 5 on the torch-autograd restatement (train.Trainer) instead of the HIP backward")
     ap.add_argument("--sg", action="store_true",
                     help="SG-NeRF variant: semantic-guided kNN + block2_bpnet (352->256) on the config-2 frame")
     return ap.parse_args()
@@ -63,12 +65,13 @@ def train_main(args, world, rank, dev, dist):
     """Config 5: one training step = 4096 random rays of a random spiral pose per rank, HIP query,
     device autograd through aggregator + composite, bucketed RCCL all-reduce, two Adam groups."""
     from sgnerf_amd.train import PointParams, Trainer
+    from sgnerf_amd.train_hip import HipTrainer
     o = HotPathOpts(SR=24, is_train=1)
     pc = scene.synth_room(args.points, seed=0)
     mlp = init_mlp(0, bias_std=0.01)
     mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
     points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, dev)
-    tr = Trainer(points, mlp, o, dev)
+    tr = (Trainer if args.train_torch else HipTrainer)(points, mlp, o, dev)
     g = torch.Generator().manual_seed(1 + rank)
     n_steps = args.warmup + args.steps
     batches = []
@@ -103,9 +106,12 @@ def train_main(args, world, rank, dev, dist):
     res = {"metric": "training rays/sec, 4096-ray batches with backward, DP (BASELINE config 5)",
            "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "vs_baseline": None, "dtype": "f32" if args.train_torch else "f16", "data": "synthetic",
            "config": {"workload": f"synth-room, {args.train_rays} random rays per rank per step, SR=24, K=8, "
-                                  f"{args.points} neural points, HIP query + device autograd + RCCL all-reduce",
+                                  f"{args.points} neural points, HIP query + "
+                                  + ("torch autograd" if args.train_torch else
+                                     "HIP MFMA row-MLP forward/backward + torch colour/composite autograd")
+                                  + " + RCCL all-reduce",
                       "parallelism": f"dp{world}"},
            "final_loss": float(torch.stack(losses).mean().item())}
     if rank == 0:

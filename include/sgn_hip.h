@@ -180,6 +180,53 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
                      float *d_out_wnorm, void *d_workspace, size_t workspace_bytes,
                      int32_t stages, sgn_stream_t stream);
 
+/* ---- training: forward with saved activations + backward ---
+ * Gradients of PointAggregator.forward / viewmlp (point_aggregators.py:868-959, :561-786)
+ * and of the NeuralPoints gather (neural_points.py:942-988) -- the reference gets them from
+ * torch autograd in optimize_parameters (base_rendering_model.py:534-664).  Base ScanNet
+ * layout only (no block2_bpnet). Rows: row = 8 * item + k (item = work-list position). */
+typedef struct {
+    void *x0;   /* fp16 [rows][288] block1.0 inputs           */
+    void *h1;   /* fp16 [rows][256] block1.2 inputs           */
+    void *h2;   /* fp16 [rows][272] block3.0 inputs (| ext)   */
+    void *h3;   /* fp16 [rows][256] block3.2 inputs           */
+} sgn_agg_saved;
+typedef struct {
+    void *d4, *d3, *d2, *d1;  /* fp16 [rows][256] scaled d loss / d pre-activation of block3.2,
+                                 block3.0, block1.2, block1.0 outputs (sgn_train_colmap 0 order) */
+    void *h4;                 /* fp16 [rows][256] block3.2 outputs (same order) */
+    float *dza;               /* [rows] scaled d loss / d alpha-branch logit */
+} sgn_agg_deltas;
+typedef struct {
+    float *embedding, *color, *dir, *conf;  /* [N,32] [N,3] [N,3] [N]: accumulated (+=), unscaled */
+} sgn_point_grads;
+
+/* Stage 1 of sgn_aggregate in one launch (items [0, S_capacity)), saving per-row layer
+ * inputs.  d_fs: fp16 [S_capacity][256] blended features (the colour MLP's input). */
+int sgn_aggregate_train_fwd(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
+                            int32_t K, const void *d_packed_mlp, float *d_out_feat, void *d_fs,
+                            const sgn_agg_saved *saved, sgn_stream_t stream);
+/* Transposed-weight blob of block1.0, block1.2, block3.0, block3.2 (w[0..3] as in
+ * sgn_mlp_pack), host in, device out (synchronous). */
+size_t sgn_train_tblob_bytes(void);
+int sgn_train_pack_t(const float *const *w, void *d_tblob, sgn_stream_t stream);
+/* Index maps for packing ON THE DEVICE from a flat fp32 parameter vector (the 9 base layers
+ * in sgn_mlp_pack order, each weight row-major then its bias): out[i] = flat index + 1, 0 =
+ * zero.  sgn_mlp_pack_index: which 0 = fp16 fragment part (n = OFF_F32 / 2 elements),
+ * 1 = fp32 section (n = 2056); sgn_train_pack_index: transposed blob (n = tblob_bytes / 2). */
+int sgn_mlp_pack_index(int32_t which, int32_t *out, int64_t n);
+int sgn_train_pack_index(int32_t *out, int64_t n);
+/* Column maps of the saved/delta tiles to reference indices (-1 = padding):
+ * which 0: [256] chain order -> unit, 1: [288] -> block1.0 input, 2: [272] -> block3.0 input. */
+int sgn_train_colmap(int32_t which, int32_t *out, int32_t n);
+/* Backward for n_items work items: d_dfs f32 [n_items][256], d_dalpha f32 [n_items] (d loss
+ * w.r.t. the blended features / alpha), d_scale: device scalar loss scale. */
+int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, int32_t n_items,
+                           const void *d_packed_mlp, const void *d_tblob, const sgn_agg_saved *saved,
+                           const float *d_dfs, const float *d_dalpha, const float *d_scale,
+                           const sgn_agg_deltas *deltas, const sgn_point_grads *grads,
+                           sgn_stream_t stream);
+
 /* ---- composite --------------------------------------------------------- */
 
 typedef struct {

@@ -46,6 +46,18 @@ class PointTables(ctypes.Structure):
                 ("raydir", c_vp), ("pers", c_vp), ("samp_pers", c_vp)]
 
 
+class AggSaved(ctypes.Structure):
+    _fields_ = [("x0", c_vp), ("h1", c_vp), ("h2", c_vp), ("h3", c_vp)]
+
+
+class AggDeltas(ctypes.Structure):
+    _fields_ = [("d4", c_vp), ("d3", c_vp), ("d2", c_vp), ("d1", c_vp), ("h4", c_vp), ("dza", c_vp)]
+
+
+class PointGrads(ctypes.Structure):
+    _fields_ = [("embedding", c_vp), ("color", c_vp), ("dir", c_vp), ("conf", c_vp)]
+
+
 class CompositeParams(ctypes.Structure):
     _fields_ = [("SR", c_i32), ("vsize_z", c_f32), ("raydist_mode_unit", c_i32), ("bg", c_f32 * 3)]
 
@@ -71,6 +83,16 @@ SIGNATURES = {
     "sgn_bpnet_pack": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "sgn_aggregate_sg": (c_i32, [c_i32, c_i32, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64,
                                  c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
+    "sgn_aggregate_train_fwd": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32, c_vp,
+                                        c_vp, c_vp, ctypes.POINTER(AggSaved), c_vp]),
+    "sgn_train_tblob_bytes": (c_sz, []),
+    "sgn_train_pack_t": (c_i32, [ctypes.POINTER(c_vp), c_vp, c_vp]),
+    "sgn_mlp_pack_index": (c_i32, [c_i32, ctypes.POINTER(c_i32), c_i64]),
+    "sgn_train_pack_index": (c_i32, [ctypes.POINTER(c_i32), c_i64]),
+    "sgn_train_colmap": (c_i32, [c_i32, ctypes.POINTER(c_i32), c_i32]),
+    "sgn_aggregate_backward": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp,
+                                       ctypes.POINTER(AggSaved), c_vp, c_vp, c_vp, ctypes.POINTER(AggDeltas),
+                                       ctypes.POINTER(PointGrads), c_vp]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
                               c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_ray_march_dense": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.POINTER(c_f32), c_vp, c_vp, c_vp,

@@ -1,0 +1,414 @@
+// agg_train.hip -- training backward of the fused neural-point aggregator.
+//
+// Gradients of PointAggregator.forward / viewmlp (models/aggregators/point_aggregators.py:
+// 868-959, :561-786) and of the NeuralPoints gather (models/neural_points/neural_points.py:
+// 942-988) w.r.t. the per-point parameters (points_embeding, points_color, points_dir,
+// points_conf through the straight-through clamp :863-865), given d loss / d f_s (the
+// blended 256-d features) and d loss / d alpha_s from the colour MLP + ray march (those
+// are per-sample and small; the host differentiates them).
+//
+// Forward (mlp.hip, k_agg_rows<0, true>) saved per row: block1.0 inputs x0, block1.2
+// inputs h1, block3.0 inputs [h2 | ext], block3.2 inputs h3 (fp16, fragment column order).
+//
+// k_agg_bwd, one wave per 32-row tile (4 samples x 8 neighbours), everything on MFMA
+// v_mfma_f32_32x32x16_f16:
+//   recompute z4 = W3 h3 + b3 (h4 = LReLU(z4)), the alpha logit za = wa . h4 + ba
+//   d za  = w * d alpha_s * sigmoid(za - 1)                     (softplus(za - 1), :298-304)
+//   d w   = <h4, d f_s> + alpha * d alpha_s                      (K-blend, :743-770)
+//   delta4 = (w d f_s + d za wa) * LReLU'(z4)
+//   delta3 = (W3^T delta4) * LReLU'(h3), delta2 = (W2^T delta3)[:256] * LReLU'(h2), ext grads
+//   delta1 = (W1^T delta2) * LReLU'(h1), d x0 = W0^T delta1 -> d feat through PE(feat)
+// The accumulator of one product is converted in registers into the B operand of the next
+// (the k permutation lives in the transposed weight blob, as in the forward).  Weight
+// gradients dW_l = delta_l^T x_l are plain GEMMs over the saved [rows][C] tiles (host side,
+// hipBLASLt); the deltas are written for them.  Gradients are computed with a loss scale
+// (device scalar) so fp16 deltas keep their precision; point gradients leave unscaled.
+#include <vector>
+
+#include "agg_device.h"
+
+namespace sgn {
+namespace {
+
+using namespace mlp;
+
+// transposed-weight blob: fragment (row tile t, k-step ks) of layer L at OFF_T[L] + (t*16 + ks)*FRAG;
+// rows = the layer's input units, k = its output units in chain order (16 k-steps)
+constexpr int TT0 = 9, TT1 = 8, TT2 = 9, TT3 = 8;  // row tiles (inputs 288 / 256 / 263 / 256)
+constexpr size_t OFF_T3 = 0;
+constexpr size_t OFF_T2 = OFF_T3 + (size_t)TT3 * 16 * FRAG;
+constexpr size_t OFF_T1 = OFF_T2 + (size_t)TT2 * 16 * FRAG;
+constexpr size_t OFF_T0 = OFF_T1 + (size_t)TT1 * 16 * FRAG;
+constexpr size_t T_BYTES = OFF_T0 + (size_t)TT0 * 16 * FRAG;
+
+struct BwdArgs {
+    AggArgs a;                 // point tables, query, forward blob (gather + W3 recompute)
+    const void *tblob;         // transposed weights
+    const _Float16 *sh1, *sh2, *sh3;
+    const float *dfs;          // [n_items][256] d loss / d f_s (natural unit order)
+    const float *dalpha;       // [n_items]      d loss / d alpha_s
+    const float *scale;        // device scalar loss scale
+    _Float16 *d4, *d3, *d2, *d1;  // [rows][256] scaled deltas, chain column order
+    _Float16 *h4;              // [rows][256] block3.2 outputs, chain column order
+    float *dza;                // [rows] scaled d alpha-logit
+    float *g_emb, *g_color, *g_dir, *g_conf;  // [N,32] [N,3] [N,3] [N] (atomic add, unscaled)
+    int32_t n_items;
+};
+
+__device__ __forceinline__ h8 load_frag(const _Float16 *base, int C, int64_t row0, int s, int lane, bool ok) {
+    if (!ok) return h8{};
+    return *(const h8 *)(base + (row0 + (lane & 31)) * C + s * 16 + (lane >> 5) * 8);
+}
+
+// delta (fp32 accumulator registers 8 s2 .. 8 s2 + 7) * LReLU'(h) with h the saved fp16 fragment
+__device__ __forceinline__ h8 mask_frag(const f32x16 &acc, int s2, h8 hv) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float d = acc[8 * s2 + e];
+        v[e] = (float)hv[e] > 0.f ? d : 0.01f * d;
+    }
+    return pack8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+}
+
+__device__ __forceinline__ h8 plain_frag(const f32x16 &acc, int s2) {
+    const int r = 8 * s2;
+    return pack8(acc[r], acc[r + 1], acc[r + 2], acc[r + 3], acc[r + 4], acc[r + 5], acc[r + 6], acc[r + 7]);
+}
+
+// acc[t] = sum_ks T[t0 + t][ks] * in[ks] for NT row tiles of a transposed layer
+template <int NT>
+__device__ __forceinline__ void tmul(const WBlob &tb, size_t off, int t0, const h8 (&in)[16], f32x16 (&acc)[NT],
+                                     int lane) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            acc[t] = mfma32(tb.frag((uint32_t)(off + ((size_t)(t0 + t) * 16 + ks) * FRAG), lane), in[ks], acc[t]);
+}
+
+// d feat[c] contribution of layer-0 local channel C (mlp_layout.h l0 order): PE(feat) chain rule
+template <int C>
+__device__ __forceinline__ void l0_backward(float d, const float (&feat)[16], float (&df)[16]) {
+    if constexpr (C < 16) {
+        df[C] += d;
+    } else if constexpr (C < 112) {
+        constexpr int m = C - 16, dd = m / 6, f = (m % 6) / 2, sc = m % 2;
+        float sv, cv;
+        sincos_pow2<f>(feat[dd], sv, cv);
+        df[dd] += sc ? -d * sv * (float)(1 << f) : d * cv * (float)(1 << f);
+    }
+    // C >= 112: PE(dists) -> point xyz / sample positions (not trained)
+}
+
+__global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
+    const AggArgs &a = b.a;
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, j = lane & 31, q = j >> 3;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Cam cam = load_cam(a.campos, a.rot);
+    const WBlob wb = make_blob(a.blob);
+    const WBlob tb = make_blob(b.tblob, T_BYTES);
+    const float *F = (const float *)((const char *)a.blob + OFF_F32);
+    const float scale = *b.scale, inv = 1.f / scale;
+    const int end = b.n_items;
+    for (int base = (blockIdx.x * 4 + w) * 4; base < end; base += gridDim.x * 16) {
+        const int item = base + q;
+        const int64_t row0 = (int64_t)base * 8;
+        float feat[16], dist[3];
+        h8 ext;
+        const RowIn ri = gather_row(a, cam, item, end, lane, feat, dist, ext);
+        const bool ok = ri.sval;
+        const int it = ok ? item : 0;
+        // ---- recompute block3.2: z4 = W3 h3 + b3 ------------------------------------------
+        f32x16 acc[8];
+        {
+            h8 x3[16];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) x3[s] = load_frag(b.sh3, 256, row0, s, lane, ok);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    acc[t] = mfma32(wb.frag((uint32_t)(OFF_W3 + ((size_t)((t >> 2) * KS_HID + ks) * 4 + (t & 3)) * FRAG), lane),
+                                    x3[ks], acc[t]);
+        }
+        // ---- pass 1: h4, alpha logit, <h4, d f_s> ------------------------------------------
+        const float *dfs = b.dfs + (int64_t)it * HID;
+        float za = 0.f, dwv = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int u0 = 32 * t + 8 * g + 4 * h;
+                const f32x4 df4 = *(const f32x4 *)(dfs + u0);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int r = 4 * g + c, u = u0 + c;
+                    const float z = acc[t][r] + F[F_B3 + u];
+                    const float hv = z > 0.f ? z : 0.01f * z;
+                    acc[t][r] = hv;
+                    za = fmaf(F[F_WA + u], hv, za);
+                    dwv = fmaf(hv, df4[c], dwv);
+                }
+            }
+        za += __shfl_xor(za, 32) + F[F_BA];
+        dwv = (dwv + __shfl_xor(dwv, 32)) * scale;
+        const float x1 = za - 1.f;
+        const float alpha_row = softplus(x1);
+        const float sig = 1.f / (1.f + expf(-x1));
+        const float das = ok ? b.dalpha[it] * scale : 0.f;
+        const float wgt = ri.wgt;  // 0 for masked neighbours and padding rows
+        const float dz = wgt * das * sig;
+        const float dwgt = dwv + alpha_row * das;  // scaled d loss / d (weight * conf) of this row
+        // ---- pass 2: delta4 = (w d f_s + dz wa) * LReLU'(z4); save h4 / delta4 ---------------
+        h8 dl[16];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            f32x16 dv;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int u0 = 32 * t + 8 * g + 4 * h;
+                const f32x4 df4 = *(const f32x4 *)(dfs + u0);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int r = 4 * g + c, u = u0 + c;
+                    const float hv = acc[t][r];
+                    const float d = fmaf(wgt * scale, df4[c], dz * F[F_WA + u]);
+                    dv[r] = hv > 0.f ? d : 0.01f * d;
+                }
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                dl[2 * t + s2] = plain_frag(dv, s2);
+                save_frag(b.h4, 256, row0, 2 * t + s2, plain_frag(acc[t], s2), lane, ok);
+                save_frag(b.d4, 256, row0, 2 * t + s2, dl[2 * t + s2], lane, ok);
+            }
+        }
+        if (ok && h == 0) b.dza[row0 + j] = dz;
+        // ---- block3.2 backward: delta3 = (W3^T delta4) * LReLU'(h3) ----------------------
+        h8 dn[16];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            f32x16 ac[4];
+            tmul<4>(tb, OFF_T3, 4 * p, dl, ac, lane);
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int k = 2 * (4 * p + tt) + s2;
+                    dn[k] = mask_frag(ac[tt], s2, load_frag(b.sh3, 256, row0, k, lane, ok));
+                    save_frag(b.d3, 256, row0, k, dn[k], lane, ok);
+                }
+        }
+        // ---- block3.0 backward: delta2 = (W2^T delta3)[:256] * LReLU'(h2); ext grads -------
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            f32x16 ac[4];
+            tmul<4>(tb, OFF_T2, 4 * p, dn, ac, lane);
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int k = 2 * (4 * p + tt) + s2;
+                    dl[k] = mask_frag(ac[tt], s2, load_frag(b.sh2, KS_L2 * 16, row0, k, lane, ok));
+                    save_frag(b.d2, 256, row0, k, dl[k], lane, ok);
+                }
+        }
+        {
+            f32x16 ae[1];
+            tmul<1>(tb, OFF_T2, 8, dn, ae, lane);
+            // tile 8 = inputs 256..262: half 0 regs 0..3 -> colour 0..2, (dir - v)_0;
+            // half 1 regs 0..2 -> (dir - v)_1, (dir - v)_2, <dir, v>   (:639-652)
+            const float o0 = __shfl_xor(ae[0][0], 32), o1 = __shfl_xor(ae[0][1], 32), o2 = __shfl_xor(ae[0][2], 32);
+            if (ok && ri.pid >= 0 && h == 0) {
+                const int ray = a.samp_ray[ri.s];
+                const float v[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1],
+                                    a.raydir[(int64_t)ray * 3 + 2]};
+                const float ddiff[3] = {ae[0][3], o0, o1};
+                const int64_t pb = (int64_t)ri.pid * 3;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    atomicAdd(b.g_color + pb + c, ae[0][c] * inv);
+                    atomicAdd(b.g_dir + pb + c, fmaf(o2, v[c], ddiff[c]) * inv);
+                }
+                atomicAdd(b.g_conf + ri.pid, dwgt * ri.wn * inv);  // straight-through clamp (:863-865)
+            }
+        }
+        // ---- block1.2 backward: delta1 = (W1^T delta2) * LReLU'(h1) ----------------------
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            f32x16 ac[4];
+            tmul<4>(tb, OFF_T1, 4 * p, dl, ac, lane);
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int k = 2 * (4 * p + tt) + s2;
+                    dn[k] = mask_frag(ac[tt], s2, load_frag(b.sh1, 256, row0, k, lane, ok));
+                    save_frag(b.d1, 256, row0, k, dn[k], lane, ok);
+                }
+        }
+        // ---- block1.0 backward: d x0 = W0^T delta1 -> d feat through PE(feat) --------------
+        float dfe[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dfe[c] = 0.f;
+        static_for<3>([&](auto pp) {
+            constexpr int P = decltype(pp)::value;
+            f32x16 ac[3];
+            tmul<3>(tb, OFF_T0, 3 * P, dn, ac, lane);
+            static_for<3>([&](auto ttc) {
+                constexpr int T = 3 * P + decltype(ttc)::value;
+                static_for<16>([&](auto rr) {
+                    constexpr int R = decltype(rr)::value;
+                    l0_backward<16 * T + R>(ac[T - 3 * P][R], feat, dfe);
+                });
+            });
+        });
+        if (ok && ri.pid >= 0) {
+            float *ge = b.g_emb + (int64_t)ri.pid * 32 + 16 * h;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) atomicAdd(ge + c, dfe[c] * inv);
+        }
+    }
+}
+
+// ---- host-side packing of the transposed blob -------------------------------------------
+
+// M: [n_rows][n_cols] row-major fp32; fragment (t, ks), lane, e <- M[rowfn(32 t + (lane & 31))][colfn(ks, 8 (lane >> 5) + e)]
+template <typename T, typename RowFn, typename ColFn>
+void pack_t(T *dst, const float *M, int n_rows, int n_cols, int n_tiles, RowFn rowfn, ColFn colfn) {
+    for (int t = 0; t < n_tiles; ++t)
+        for (int ks = 0; ks < 16; ++ks)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                    const int r = rowfn(32 * t + (lane & 31));
+                    const int c = colfn(ks, 8 * (lane >> 5) + e);
+                    const float v = (r >= 0 && r < n_rows && c >= 0 && c < n_cols) ? M[(size_t)r * n_cols + c] : 0.f;
+                    dst[(((size_t)t * 16 + ks) * 64 + lane) * 8 + e] = (T)v;
+                }
+}
+
+std::vector<float> transpose(const float *W, int n_out, int n_in) {
+    std::vector<float> T((size_t)n_out * n_in);
+    for (int o = 0; o < n_out; ++o)
+        for (int i = 0; i < n_in; ++i) T[(size_t)i * n_out + o] = W[(size_t)o * n_in + i];
+    return T;
+}
+
+int chain_col(int ks, int p) { return 16 * ks + perm_acc(p); }
+// layer-0 transposed rows: tile position 32 t + jj holds local channel 16 t + r of lane-half hh,
+// (hh, r) = ((jj >> 2) & 1, (jj & 3) + 4 (jj >> 3)) -- the inverse of acc_unit
+int t0_row(int pos) {
+    const int t = pos >> 5, jj = pos & 31;
+    return l0_ref_col((jj >> 2) & 1, 16 * t + (jj & 3) + 4 * (jj >> 3));
+}
+
+template <typename T>
+void pack_tblob(const float *const *w, T *e) {
+    const auto idr = [](int r) { return r; };
+    std::vector<float> t3 = transpose(w[3], 256, 256), t2 = transpose(w[2], 256, 263), t1 = transpose(w[1], 256, 256),
+                       t0 = transpose(w[0], 256, 284);
+    pack_t(e + OFF_T3 / 2, t3.data(), 256, 256, TT3, idr, chain_col);
+    pack_t(e + OFF_T2 / 2, t2.data(), 263, 256, TT2, idr, chain_col);
+    pack_t(e + OFF_T1 / 2, t1.data(), 256, 256, TT1, idr, chain_col);
+    pack_t(e + OFF_T0 / 2, t0.data(), 284, 256, TT0, t0_row, chain_col);
+}
+
+}  // namespace
+}  // namespace sgn
+
+extern "C" {
+
+size_t sgn_train_tblob_bytes(void) { return sgn::T_BYTES; }
+
+/* Index map of the transposed blob over the flat parameter vector (as sgn_mlp_pack_index):
+ * n = sgn_train_tblob_bytes() / 2 elements, value = flat index + 1, 0 = zero. */
+int sgn_train_pack_index(int32_t *out, int64_t n) {
+    using namespace sgn;
+    SGN_REQUIRE(out && n == (int64_t)(T_BYTES / 2), "sgn_train_pack_index: bad size");
+    // flat offsets of block1.0 / block1.2 / block3.0 / block3.2 weights (LAYERS order: w, b per layer)
+    const int64_t o0 = 0, o1 = o0 + 256 * 284 + 256, o2 = o1 + 256 * 256 + 256, o3 = o2 + 256 * 263 + 256;
+    const int64_t offs[4] = {o0, o1, o2, o3};
+    const int sz[4] = {256 * 284, 256 * 256, 256 * 263, 256 * 256};
+    std::vector<std::vector<float>> wi(4);
+    std::vector<const float *> wp(4);
+    for (int L = 0; L < 4; ++L) {
+        wi[L].resize(sz[L]);
+        for (int i = 0; i < sz[L]; ++i) wi[L][i] = (float)(offs[L] + i + 1);
+        wp[L] = wi[L].data();
+    }
+    std::vector<float> e(T_BYTES / 2, 0.f);
+    pack_tblob(wp.data(), e.data());
+    for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)e[(size_t)i];
+    return 0;
+}
+
+int sgn_train_pack_t(const float *const *w, void *d_tblob, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    SGN_REQUIRE(w && w[0] && w[1] && w[2] && w[3], "null weights");
+    std::vector<uint8_t> blob(T_BYTES, 0);
+    pack_tblob(w, (_Float16 *)blob.data());
+    hipStream_t st = as_stream(stream);
+    SGN_CHECK_HIP(hipMemcpyAsync(d_tblob, blob.data(), T_BYTES, hipMemcpyHostToDevice, st));
+    SGN_CHECK_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+/* Column maps of the saved / delta tiles -> reference indices (-1 = padding):
+ * which 0: chain columns (256) -> unit; 1: block1.0 inputs (288) -> block1.0 input column;
+ * 2: block3.0 inputs (272) -> block3.0 input column. */
+int sgn_train_colmap(int32_t which, int32_t *out, int32_t n) {
+    using namespace sgn::mlp;
+    const int want = which == 0 ? 256 : which == 1 ? KS_L0 * 16 : which == 2 ? KS_L2 * 16 : -1;
+    SGN_REQUIRE(want > 0 && out && n == want, "sgn_train_colmap: bad map id or size");
+    for (int p = 0; p < n; ++p) {
+        const int ks = p >> 4, hh = (p >> 3) & 1, e = p & 7;
+        if (which == 1) out[p] = l0_ref_col(hh, 8 * ks + e);
+        else if (ks < 16) out[p] = 16 * ks + perm_acc(p & 15);
+        else out[p] = (hh == 0 && e < 7) ? 256 + e : -1;
+    }
+    return 0;
+}
+
+int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, int32_t n_items,
+                           const void *d_packed, const void *d_tblob, const sgn_agg_saved *saved,
+                           const float *d_dfs, const float *d_dalpha, const float *d_scale,
+                           const sgn_agg_deltas *deltas, const sgn_point_grads *grads, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(pt && q && d_packed && d_tblob && saved && deltas && grads && d_scale, "null argument");
+    SGN_REQUIRE(n_items >= 0, "n_items < 0");
+    SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
+    if (n_items == 0) return 0;
+    SGN_REQUIRE(d_dfs && d_dalpha && saved->h1 && saved->h2 && saved->h3, "null saved/input tensors");
+    SGN_REQUIRE(deltas->d1 && deltas->d2 && deltas->d3 && deltas->d4 && deltas->h4 && deltas->dza, "null delta outputs");
+    SGN_REQUIRE(grads->embedding && grads->color && grads->dir && grads->conf, "null gradient outputs");
+    BwdArgs b{};
+    AggArgs &a = b.a;
+    a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
+    a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
+    a.pers = nullptr; a.samp_pers = nullptr;
+    a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
+    a.samp_locw = q->samp_locw;
+    a.blob = d_packed; a.blob_bytes = mlp::TOTAL_BYTES;
+    a.blend = nullptr; a.wnorm = nullptr;
+    b.tblob = d_tblob;
+    b.sh1 = (const _Float16 *)saved->h1; b.sh2 = (const _Float16 *)saved->h2; b.sh3 = (const _Float16 *)saved->h3;
+    b.dfs = d_dfs; b.dalpha = d_dalpha; b.scale = d_scale;
+    b.d4 = (_Float16 *)deltas->d4; b.d3 = (_Float16 *)deltas->d3; b.d2 = (_Float16 *)deltas->d2;
+    b.d1 = (_Float16 *)deltas->d1; b.h4 = (_Float16 *)deltas->h4; b.dza = deltas->dza;
+    b.g_emb = grads->embedding; b.g_color = grads->color; b.g_dir = grads->dir; b.g_conf = grads->conf;
+    b.n_items = n_items;
+    const int64_t waves = ((int64_t)n_items + 3) / 4;
+    const int64_t blocks = (waves + 3) / 4;
+    hipLaunchKernelGGL(k_agg_bwd, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, as_stream(stream), b);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

@@ -20,72 +20,10 @@
 #include <utility>
 #include <vector>
 
-#include "mlp_layout.h"
-#include "sgn_common.h"
+#include "agg_device.h"
 
 namespace sgn {
 namespace {
-
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-using namespace mlp;
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// Weight blob access through a buffer descriptor: one VGPR of per-lane offset plus a
-// compile-time SGPR/immediate offset per fragment (flat 64-bit addresses per fragment
-// would be hoisted out of the sample loop and spill).
-struct WBlob {
-    __amdgpu_buffer_rsrc_t rsrc;
-    __device__ __forceinline__ h8 frag(uint32_t byte_off, int lane) const {
-        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * 16, byte_off, 0));
-    }
-    // 4 fp32 of an accumulator-order vector: element (t*2 + h)*16 + 4g of f32 section offset `f`
-    __device__ __forceinline__ f32x4 acc4(uint32_t f, int t, int g, int h) const {
-        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rsrc, h * 64, (uint32_t)(OFF_F32 + (f + t * 32 + 4 * g) * 4), 0));
-    }
-    __device__ __forceinline__ float scalar(uint32_t f) const {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, 0, (uint32_t)(OFF_F32 + f * 4), 0));
-    }
-};
-
-__device__ __forceinline__ WBlob make_blob(const void *p, size_t bytes = TOTAL_BYTES) {
-    WBlob b;
-    b.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
-    return b;
-}
-
-__device__ __forceinline__ f32x16 mfma32(h8 a, h8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : x * 0.01f; }
-__device__ __forceinline__ float softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
-struct Cam {
-    float cx, cy, cz;
-    float r[9];  // camrotc2w row-major
-    // w2pers (neural_points.py:845-850): c_j = sum_i R[i][j] * (p_i - campos_i)
-    __device__ __forceinline__ void pers(float x, float y, float z, float &px, float &py, float &pz) const {
-        float sx = __fsub_rn(x, cx), sy = __fsub_rn(y, cy), sz = __fsub_rn(z, cz);
-        float c0 = __fadd_rn(__fadd_rn(__fmul_rn(r[0], sx), __fmul_rn(r[3], sy)), __fmul_rn(r[6], sz));
-        float c1 = __fadd_rn(__fadd_rn(__fmul_rn(r[1], sx), __fmul_rn(r[4], sy)), __fmul_rn(r[7], sz));
-        float c2 = __fadd_rn(__fadd_rn(__fmul_rn(r[2], sx), __fmul_rn(r[5], sy)), __fmul_rn(r[8], sz));
-        px = __fdiv_rn(c0, c2);
-        py = __fdiv_rn(c1, c2);
-        pz = c2;
-    }
-};
-
-__device__ __forceinline__ Cam load_cam(const float *campos, const float *rot) {
-    Cam c;
-    c.cx = campos[0]; c.cy = campos[1]; c.cz = campos[2];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) c.r[i] = rot[i];
-    return c;
-}
 
 // One dense layer, output chained into the next layer's B fragments (16 k-steps).
 // KS k-steps of input: the first min(KS, NIN) from `in`, step NIN (if KS > NIN) from `extra`.
@@ -112,25 +50,6 @@ __device__ __forceinline__ void layer_chain(const WBlob &wb, uint32_t woff, uint
     }
 }
 
-struct AggArgs {
-    // point tables
-    const float *xyz, *emb, *color, *dir, *conf;
-    const float *campos, *rot, *raydir;
-    const float *pers, *samp_pers;  // optional precomputed pers coordinates
-    // query
-    const int32_t *counters, *work, *samp_ray, *pidx;
-    const float *samp_locw;
-    // weights
-    const void *blob;
-    size_t blob_bytes;
-    const _Float16 *bpnet;  // [N, bpnet_dim] fp16 (SG variant with predict_semantic = 1), else null
-    // outputs
-    float *feat;      // float4 per sample id: .x alpha written here
-    float *blend;     // [S*8] weight * conf (optional)
-    float *wnorm;     // [S*8] normalised weight (optional)
-    _Float16 *fs;     // [chunk][256] blended features (natural unit order)
-    int32_t item0, n_items;  // work-list chunk
-};
 
 constexpr int AGG_TPB = 256;
 
@@ -184,93 +103,6 @@ constexpr int LDS_F32_OFF = NSLOT * SLOT_BYTES;
 constexpr int LDS_BYTES = LDS_F32_OFF + (int)(N_F32 + HID) * 4;  // + block2_bpnet bias (SG)
 static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the waves");
 
-template <class F, int... I>
-__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void static_for(F &&f) {
-    static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// DPP butterflies: lanes j^1, j^2 (quad_perm), then the mirrored quad of the 8-lane half-row
-__device__ __forceinline__ float dpp_sum8(float x) {
-    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, true));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, true));
-    x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x141, 0xF, 0xF, true));
-    return x;
-}
-
-__device__ __forceinline__ h8 pack8(float a0, float a1, float a2, float a3, float a4, float a5, float a6,
-                                    float a7) {
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    const h2 p0 = {(_Float16)a0, (_Float16)a1}, p1 = {(_Float16)a2, (_Float16)a3};
-    const h2 p2 = {(_Float16)a4, (_Float16)a5}, p3 = {(_Float16)a6, (_Float16)a7};
-    const u32x4 u = {__builtin_bit_cast(uint32_t, p0), __builtin_bit_cast(uint32_t, p1),
-                     __builtin_bit_cast(uint32_t, p2), __builtin_bit_cast(uint32_t, p3)};
-    return __builtin_bit_cast(h8, u);
-}
-
-// sin/cos for the positional encodings: hardware v_sin/v_cos on the argument reduced to
-// [-0.5, 0.5] revolutions (abs error ~1e-6, far below the fp16 rounding of the result)
-__device__ __forceinline__ float pe_sin(float x) {
-    float r = x * 0.15915494309189535f;
-    r = r - rintf(r);
-    return __builtin_amdgcn_sinf(r);
-}
-__device__ __forceinline__ float pe_cos(float x) {
-    float r = x * 0.15915494309189535f;
-    r = r - rintf(r);
-    return __builtin_amdgcn_cosf(r);
-}
-
-// sin/cos of x * 2^F from one hardware sin/cos of x and F double-angle steps
-// (sin 2a = 2 sin a cos a, cos 2a = (cos a - sin a)(cos a + sin a)); identical
-// sub-expressions of the channels of one k-step are CSE'd by the compiler.
-template <int F>
-__device__ __forceinline__ void sincos_pow2(float x, float &s, float &c) {
-    if constexpr (F == 0) {
-        s = pe_sin(x);
-        c = pe_cos(x);
-    } else {
-        float s0, c0;
-        sincos_pow2<F - 1>(x, s0, c0);
-        s = 2.f * s0 * c0;
-        c = (c0 - s0) * (c0 + s0);
-    }
-}
-
-// value of layer-0 channel C (0..143) of a lane-half (mlp_layout.h order)
-template <int C>
-__device__ __forceinline__ float l0_channel(const float (&feat)[16], const float (&dist)[3]) {
-    if constexpr (C < 16) {
-        return feat[C];
-    } else if constexpr (C < 112) {
-        constexpr int m = C - 16, d = m / 6, f = (m % 6) / 2, sc = m % 2;
-        float sv, cv;
-        sincos_pow2<f>(feat[d], sv, cv);
-        return sc ? cv : sv;
-    } else if constexpr (C < 142) {
-        constexpr int m = C - 112, dd = m / 10, f = (m % 10) / 2, sc = m % 2;
-        float sv, cv;
-        sincos_pow2<f>(dist[dd], sv, cv);
-        return sc ? cv : sv;
-    } else {
-        return 0.f;
-    }
-}
-
-template <int K0>
-__device__ __forceinline__ h8 l0_step(const float (&feat)[16], const float (&dist)[3]) {
-#ifdef SGN_ABLATE_PE  // timing experiment only: raw features instead of encodings (wrong results)
-    return pack8(feat[(8 * K0) & 15], feat[(8 * K0 + 1) & 15], feat[(8 * K0 + 2) & 15], feat[(8 * K0 + 3) & 15],
-                 feat[(8 * K0 + 4) & 15], feat[(8 * K0 + 5) & 15], dist[K0 % 3], feat[(8 * K0 + 7) & 15]);
-#endif
-    return pack8(l0_channel<8 * K0 + 0>(feat, dist), l0_channel<8 * K0 + 1>(feat, dist),
-                 l0_channel<8 * K0 + 2>(feat, dist), l0_channel<8 * K0 + 3>(feat, dist),
-                 l0_channel<8 * K0 + 4>(feat, dist), l0_channel<8 * K0 + 5>(feat, dist),
-                 l0_channel<8 * K0 + 6>(feat, dist), l0_channel<8 * K0 + 7>(feat, dist));
-}
 
 // Layers of the row stream: 0 block1.0, 1 block1.2, 2 block3.0, 3 block3.2, 4 block2_bpnet.0
 // (SG variant only).  KSB = k-steps of block2_bpnet.0 (0: variant absent).  Stream order:
@@ -367,21 +199,6 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
     }
 }
 
-// v_permlane{16,32}_swap as inline asm: this compiler's lowering of the two-result
-// builtins returns the first result twice (seen in the ISA: v_add v48, v48, v48 after the
-// swap).  x, y are swapped in place: permlane32: x.hi <-> y.lo; permlane16: odd rows of x
-// <-> even rows of y.  The s_nops cover the VALU-write -> permlane-read hazard.
-__device__ __forceinline__ void permlane32_swap(float &x, float &y) {
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
-}
-__device__ __forceinline__ void permlane16_swap(float &x, float &y) {
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
-}
-
-// LeakyReLU(0.01) = 0.505 x + 0.495 |x|: one v_mul with an |x| source modifier + one v_fma
-// (no compare/select, no NaN canonicalisation); within 1 ulp of max(x, 0.01x)
-__device__ __forceinline__ float lrelu_max(float x) { return __builtin_fmaf(0.505f, x, 0.495f * __builtin_fabsf(x)); }
-
 // One pass of a layer, k-outer: acc[t] = bias + sum_k W[TP*P+t][k] * in(k), chunk by chunk.
 // TRANS: the activations are the A operand and the weights the B operand, so the
 // accumulators hold D^T (lane = output unit, registers = rows) and start at zero (the bias
@@ -434,16 +251,6 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
     });
 }
 
-// fp16 pack + LeakyReLU on the packed halves: v_cvt_pk_f16_f32, v_pk_mul_f16, v_pk_max_f16
-// (1.5 instructions per value; lrelu(fp16(x)) differs from fp16(lrelu(x)) only by the
-// rounding of 0.01x on negative inputs)
-__device__ __forceinline__ uint32_t lrelu_pk(float x0, float x1) {
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    const h2 v = {(_Float16)x0, (_Float16)x1};
-    const h2 sl = v * h2{(_Float16)0.01f, (_Float16)0.01f};
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, sl));
-}
-
 // LeakyReLU + fp16 pack: pass accumulators (bias included) -> next-layer fragments
 template <int TP, int P>
 __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]) {
@@ -467,94 +274,7 @@ __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]
         }
 }
 
-template <bool C, class T>
-__device__ __forceinline__ T &pick(T &a, T &b) {
-    if constexpr (C) return a; else return b;
-}
-
-struct RowIn {
-    int s;       // sample id
-    bool sval;   // work item exists
-    float wgt;   // normalised weight * conf of this row
-    int pid;     // neighbour point index (-1: masked)
-};
-
-// Gather + pers + dists + weights of this lane's row; raw features for the
-// just-in-time layer-0 encodings, block3's extra channels.
-__device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, int item, int end, int lane,
-                                            float (&feat)[16], float (&dist)[3], h8 &ext) {
-    const int h = lane >> 5, kk = lane & 7;
-    RowIn ri;
-    ri.sval = item < end;
-    ri.s = ri.sval ? a.work[item] : 0;
-    const int s = ri.s;
-#ifdef SGN_DEBUG_FAST_GATHER  // timing experiment only: no dependent index load, L2-resident records
-    const int pid = ri.sval ? ((item * 8 + kk) & 1023) : -1;
-#else
-    const int pid = ri.sval ? a.pidx[(int64_t)s * 8 + kk] : -1;
-#endif
-    const bool m = pid >= 0;
-    ri.pid = pid;
-    const float lx = a.samp_locw[(int64_t)s * 3 + 0], ly = a.samp_locw[(int64_t)s * 3 + 1],
-                lz = a.samp_locw[(int64_t)s * 3 + 2];
-    const int ray = a.samp_ray[s];
-    const float vx = a.raydir[(int64_t)ray * 3 + 0], vy = a.raydir[(int64_t)ray * 3 + 1],
-                vz = a.raydir[(int64_t)ray * 3 + 2];
-    float px = 0.f, py = 0.f, pz = 0.f, cf = 0.f;
-    float col[3] = {0.f, 0.f, 0.f}, pdr[3] = {0.f, 0.f, 0.f};
-    if (m) {
-        px = a.xyz[(int64_t)pid * 3 + 0]; py = a.xyz[(int64_t)pid * 3 + 1]; pz = a.xyz[(int64_t)pid * 3 + 2];
-        const f32x4 *e4 = (const f32x4 *)(a.emb + (int64_t)pid * 32 + 16 * h);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = e4[g];
-            feat[4 * g + 0] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
-        }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) { col[c] = a.color[(int64_t)pid * 3 + c]; pdr[c] = a.dir[(int64_t)pid * 3 + c]; }
-        cf = a.conf[pid];
-    } else {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) feat[c] = 0.f;
-    }
-    // dists (point_aggregators.py:917-925): half 0 world offsets, half 1 pers-space terms
-    const float dwx = __fsub_rn(px, lx), dwy = __fsub_rn(py, ly), dwz = __fsub_rn(pz, lz);
-    dist[0] = m ? dwx : 0.f; dist[1] = m ? dwy : 0.f; dist[2] = m ? dwz : 0.f;
-    if (h == 1) {
-        float xp = 0.f, yp = 0.f, zp = 0.f, xl, yl, zl;
-        if (a.pers) {
-            if (m) { xp = a.pers[(int64_t)pid * 3]; yp = a.pers[(int64_t)pid * 3 + 1]; zp = a.pers[(int64_t)pid * 3 + 2]; }
-            xl = a.samp_pers[(int64_t)s * 3]; yl = a.samp_pers[(int64_t)s * 3 + 1]; zl = a.samp_pers[(int64_t)s * 3 + 2];
-        } else {
-            if (m) cam.pers(px, py, pz, xp, yp, zp);
-            cam.pers(lx, ly, lz, xl, yl, zl);
-        }
-        dist[0] = m ? __fsub_rn(__fmul_rn(xp, zp), __fmul_rn(xl, zl)) : 0.f;
-        dist[1] = m ? __fsub_rn(__fmul_rn(yp, zp), __fmul_rn(yl, zl)) : 0.f;
-        dist[2] = m ? __fsub_rn(zp, zl) : 0.f;
-    }
-    // linear kernel weights, normalised over the sample's 8 rows, times clamped conf
-    float w = 0.f;
-    if (m) {
-        float n2 = __fadd_rn(__fadd_rn(__fmul_rn(dwx, dwx), __fmul_rn(dwy, dwy)), __fmul_rn(dwz, dwz));
-        w = 1.f / fmaxf(sqrtf(n2), 1e-6f);
-    }
-    const float wsum = dpp_sum8(w);
-    w = w / fmaxf(wsum, 1e-8f);
-    ri.wgt = w * fminf(fmaxf(cf, 1e-4f), 1.f);
-    if (a.blend && ri.sval && h == 0) a.blend[(int64_t)s * 8 + kk] = ri.wgt;
-    if (a.wnorm && ri.sval && h == 1) a.wnorm[(int64_t)s * 8 + kk] = w;
-    // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane-half 0 only
-    h8 e = {};
-    if (h == 0 && m) {
-        e = pack8(col[0], col[1], col[2], __fsub_rn(pdr[0], vx), __fsub_rn(pdr[1], vy), __fsub_rn(pdr[2], vz),
-                  __fadd_rn(__fadd_rn(__fmul_rn(pdr[0], vx), __fmul_rn(pdr[1], vy)), __fmul_rn(pdr[2], vz)), 0.f);
-    }
-    ext = e;
-    return ri;
-}
-
-template <int KSB>
+template <int KSB, bool SAVE = false>
 __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     constexpr int NBP = KSB > KS_HID ? KSB - KS_HID : 0;  // BPNet k-steps (SG, predict_semantic = 1)
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES + WG_WAVES * NBP * (int)FRAG];
@@ -600,6 +320,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         float feat[16], dist[3];
         h8 ext;
         const RowIn ri = gather_row(a, cam, item, end, lane, feat, dist, ext);
+        const int64_t srow0 = (int64_t)(base + w * 4 - a.item0) * 8;  // first saved row of this wave (SAVE)
         // SG: this row's BPNet embedding -> the wave's LDS area as ready-made B fragments
         // (LDS-DMA, one 1-KiB fragment per k-step; lane (row, half h) <- channels 16j+8h..+7).
         // Its vmcnt is covered by the chunk waits before block2_bpnet (older than those DMAs).
@@ -614,17 +335,33 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         h8 actA[16], actB[16];
         {   // block1.0: 284 -> 256, one pass over 8 tiles, inputs generated per k-step
             f32x16 acc0[8];
-            run_pass<KSB, 0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0,
-                                [&](auto k) { return l0_step<decltype(k)::value>(feat, dist); });
+            run_pass<KSB, 0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0, [&](auto k) {
+                const h8 v = l0_step<decltype(k)::value>(feat, dist);
+                if constexpr (SAVE) save_frag(a.sx0, KS_L0 * 16, srow0, decltype(k)::value, v, lane, ri.sval);
+                return v;
+            });
             chain_out<8, 0>(acc0, actA);
+            if constexpr (SAVE) {
+#pragma unroll
+                for (int s2 = 0; s2 < 16; ++s2) save_frag(a.sh1, 256, srow0, s2, actA[s2], lane, ri.sval);
+            }
         }
         f32x16 acc[4];
         // block1.2: 256 -> 256
         auto inA = [&](auto k) { return actA[decltype(k)::value]; };
         run_pass<KSB, 1, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
         chain_out<4, 0>(acc, actB);
+        if constexpr (SAVE) {
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
+        }
         run_pass<KSB, 1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
         chain_out<4, 1>(acc, actB);
+        if constexpr (SAVE) {
+#pragma unroll
+            for (int s2 = 8; s2 < 16; ++s2) save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
+            save_frag(a.sh2, KS_L2 * 16, srow0, 16, ext, lane, ri.sval);
+        }
         if constexpr (KSB > 0) {
             // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256 (point_aggregators.py:629-636)
             auto inBP = [&](auto k) {
@@ -648,6 +385,10 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         chain_out<4, 0>(acc, out3);
         run_pass<KSB, 2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
         chain_out<4, 1>(acc, out3);
+        if constexpr (SAVE) {
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) save_frag(a.sh3, 256, srow0, s2, out3[s2], lane, ri.sval);
+        }
         // block3.2: 256 -> 256, transposed (lane = output unit j = lane & 31 of tile t,
         // register i = row (i & 3) + 8 (i >> 2) + 4h, i.e. sample i >> 2), so the K-blend
         // and the alpha dot product are per-lane FMAs over registers
@@ -896,9 +637,8 @@ int col_bp(int ks, int p) { return ks < 16 ? col_chain(ks, p) : 256 + 16 * (ks -
 int col_c0(int ks, int p) { return ks < 16 ? 16 * ks + p : (16 * (ks - 16) + p < 24 ? 256 + 16 * (ks - 16) + p : -1); }
 
 // kouter: fragment (t, ks) at index ks*n_tiles + t (block1/block3 stream order), else t*KS + ks
-template <typename ColFn>
-void pack_frags(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles, int KS, ColFn col,
-                int kouter) {
+template <typename T, typename ColFn>
+void pack_frags(T *dst, const float *W, int n_out, int n_in, int n_tiles, int KS, ColFn col, int kouter) {
     for (int t = 0; t < n_tiles; ++t)
         for (int ks = 0; ks < KS; ++ks)
             for (int lane = 0; lane < 64; ++lane)
@@ -909,7 +649,7 @@ void pack_frags(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles,
                     // kouter > 0: [pass = t/kouter][ks][t%kouter] (k-outer stream of k_agg_rows)
                     size_t f = kouter ? ((size_t)(t / kouter) * KS + ks) * kouter + (t % kouter)
                                       : (size_t)t * KS + ks;
-                    dst[(f * 64 + lane) * 8 + e] = (_Float16)v;
+                    dst[(f * 64 + lane) * 8 + e] = (T)v;
                 }
 }
 
@@ -917,6 +657,37 @@ void pack_acc_order(float *dst, const float *v, int n_tiles) {
     for (int t = 0; t < n_tiles; ++t)
         for (int h = 0; h < 2; ++h)
             for (int r = 0; r < 16; ++r) dst[(t * 2 + h) * 16 + r] = v[32 * t + acc_unit(r, h)];
+}
+
+// The whole blob: fragment part as elements of e16 (element i = byte 2 i), fp32 section F,
+// block2_bpnet bias Fbb (SG).  T16 = _Float16 packs weights; T16 = float packs index maps.
+template <typename T16>
+void pack_blob(int ksb, int bpnet_dim, const float *const *w, const float *const *b, T16 *e16, float *F, float *Fbb) {
+    auto frag = [&](size_t off) { return e16 + off / 2; };
+    pack_frags(frag(OFF_W0), w[0], 256, 284, T_HID, KS_L0, col_l0, layer_tp(0));
+    pack_frags(frag(OFF_W1), w[1], 256, 256, T_HID, KS_HID, col_chain, layer_tp(1));
+    pack_frags(frag(OFF_W2), w[2], 256, 263, T_HID, KS_L2, col_l2, layer_tp(2));
+    pack_frags(frag(OFF_W3), w[3], 256, 256, T_HID, KS_HID, col_chain, layer_tp(3));
+    pack_frags(frag(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, col_c0, 0);
+    pack_frags(frag(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, col_chain, 0);
+    pack_frags(frag(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, col_chain, 0);
+    pack_acc_order(F + F_B0, b[0], T_HID);
+    pack_acc_order(F + F_B1, b[1], T_HID);
+    pack_acc_order(F + F_B2, b[2], T_HID);
+    for (int u = 0; u < HID; ++u) F[F_B3 + u] = b[3][u];  // natural order: block3.2 runs transposed
+    pack_acc_order(F + F_CB0, b[5], T_CHID);
+    pack_acc_order(F + F_CB1, b[6], T_CHID);
+    pack_acc_order(F + F_CB2, b[7], T_CHID);
+    for (int u = 0; u < HID; ++u) F[F_WA + u] = w[4][u];
+    F[F_BA] = b[4][0];
+    for (int c = 0; c < 3; ++c) {
+        pack_acc_order(F + F_WC3 + c * 128, w[8] + c * 128, T_CHID);
+        F[F_BC3 + c] = b[8][c];
+    }
+    if (ksb > 0) {  // block2_bpnet.0 = w[9] [256, 256 + bpnet_dim], b[9] [256]
+        pack_frags(frag(OFF_WB), w[9], 256, 256 + bpnet_dim, T_HID, ksb, col_bp, layer_tp(4));
+        pack_acc_order(Fbb, b[9], T_HID);
+    }
 }
 
 }  // namespace
@@ -944,34 +715,10 @@ int sgn_mlp_pack_sg(int32_t bpnet_layers, int32_t bpnet_dim, const float *const 
     SGN_REQUIRE(w && b && d_packed, "null argument");
     const int ksb = mlp_variant_ksb(bpnet_layers, bpnet_dim);
     SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    if (ksb > 0) SGN_REQUIRE(w[9] && b[9], "block2_bpnet.0 weights missing");
     std::vector<uint8_t> blob(total_bytes_sg(ksb), 0);
-    auto frag = [&](size_t off) { return (_Float16 *)(blob.data() + off); };
-    pack_frags(frag(OFF_W0), w[0], 256, 284, T_HID, KS_L0, col_l0, layer_tp(0));
-    pack_frags(frag(OFF_W1), w[1], 256, 256, T_HID, KS_HID, col_chain, layer_tp(1));
-    pack_frags(frag(OFF_W2), w[2], 256, 263, T_HID, KS_L2, col_l2, layer_tp(2));
-    pack_frags(frag(OFF_W3), w[3], 256, 256, T_HID, KS_HID, col_chain, layer_tp(3));
-    pack_frags(frag(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, col_c0, 0);
-    pack_frags(frag(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, col_chain, 0);
-    pack_frags(frag(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, col_chain, 0);
-    float *F = (float *)(blob.data() + OFF_F32);
-    pack_acc_order(F + F_B0, b[0], T_HID);
-    pack_acc_order(F + F_B1, b[1], T_HID);
-    pack_acc_order(F + F_B2, b[2], T_HID);
-    for (int u = 0; u < HID; ++u) F[F_B3 + u] = b[3][u];  // natural order: block3.2 runs transposed
-    pack_acc_order(F + F_CB0, b[5], T_CHID);
-    pack_acc_order(F + F_CB1, b[6], T_CHID);
-    pack_acc_order(F + F_CB2, b[7], T_CHID);
-    for (int u = 0; u < HID; ++u) F[F_WA + u] = w[4][u];
-    F[F_BA] = b[4][0];
-    for (int c = 0; c < 3; ++c) {
-        pack_acc_order(F + F_WC3 + c * 128, w[8] + c * 128, T_CHID);
-        F[F_BC3 + c] = b[8][c];
-    }
-    if (ksb > 0) {  // block2_bpnet.0 = w[9] [256, 256 + bpnet_dim], b[9] [256]
-        SGN_REQUIRE(w[9] && b[9], "block2_bpnet.0 weights missing");
-        pack_frags(frag(OFF_WB), w[9], 256, 256 + bpnet_dim, T_HID, ksb, col_bp, layer_tp(4));
-        pack_acc_order((float *)(blob.data() + off_bb(ksb)), b[9], T_HID);
-    }
+    pack_blob(ksb, bpnet_dim, w, b, (_Float16 *)blob.data(), (float *)(blob.data() + OFF_F32),
+              ksb > 0 ? (float *)(blob.data() + off_bb(ksb)) : nullptr);
     hipStream_t st = as_stream(stream);
     SGN_CHECK_HIP(hipMemcpyAsync(d_packed, blob.data(), blob.size(), hipMemcpyHostToDevice, st));
     SGN_CHECK_HIP(hipStreamSynchronize(st));
@@ -980,6 +727,36 @@ int sgn_mlp_pack_sg(int32_t bpnet_layers, int32_t bpnet_dim, const float *const 
 
 int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, sgn_stream_t stream) {
     return sgn_mlp_pack_sg(0, 0, w, b, d_packed, stream);
+}
+
+/* Index maps of the base forward blob over the flat parameter vector (LAYERS order, each
+ * layer weight row-major then bias): out[i] = flat index + 1, 0 = zero padding.
+ * which 0: fragment part (OFF_F32 / 2 fp16 elements), 1: fp32 section (N_F32). */
+int sgn_mlp_pack_index(int32_t which, int32_t *out, int64_t n) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    const int64_t want = which == 0 ? (int64_t)(OFF_F32 / 2) : which == 1 ? (int64_t)N_F32 : -1;
+    SGN_REQUIRE(out && n == want, "sgn_mlp_pack_index: bad map id or size");
+    static const int shape[9][2] = {{256, 284}, {256, 256}, {256, 263}, {256, 256}, {1, 256},
+                                    {128, 280}, {128, 128}, {128, 128}, {3, 128}};
+    std::vector<std::vector<float>> wi(9), bi(9);
+    std::vector<const float *> wp(9), bp(9);
+    int64_t off = 0;
+    for (int L = 0; L < 9; ++L) {
+        wi[L].resize((size_t)shape[L][0] * shape[L][1]);
+        for (size_t i = 0; i < wi[L].size(); ++i) wi[L][i] = (float)(off + (int64_t)i + 1);
+        off += (int64_t)wi[L].size();
+        bi[L].resize(shape[L][0]);
+        for (size_t i = 0; i < bi[L].size(); ++i) bi[L][i] = (float)(off + (int64_t)i + 1);
+        off += (int64_t)bi[L].size();
+        wp[L] = wi[L].data();
+        bp[L] = bi[L].data();
+    }
+    std::vector<float> e16(OFF_F32 / 2, 0.f), F(N_F32, 0.f);
+    pack_blob<float>(0, 0, wp.data(), bp.data(), e16.data(), F.data(), nullptr);
+    const std::vector<float> &src = which == 0 ? e16 : F;
+    for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)src[(size_t)i];
+    return 0;
 }
 
 size_t sgn_aggregate_workspace_bytes(int64_t S) {
@@ -1034,6 +811,33 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
         dim3 g2((unsigned)(wg2 < 256 ? wg2 : 256));  // persistent: colour weights loaded once per CU
         if (stages & 2) hipLaunchKernelGGL(k_color, g2, dim3(COL_TPB), 0, st, c);
     }
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_aggregate_train_fwd(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                            const void *d_packed, float *d_out_feat, void *d_fs, const sgn_agg_saved *saved,
+                            sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_fs && saved, "null argument");
+    SGN_REQUIRE(saved->x0 && saved->h1 && saved->h2 && saved->h3, "null saved-activation buffer");
+    SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
+    SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
+    SGN_REQUIRE(S_capacity >= 0 && S_capacity < (1 << 27), "S_capacity out of range");
+    if (S_capacity == 0) return 0;
+    AggArgs a{};
+    a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
+    a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
+    a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
+    a.samp_locw = q->samp_locw;
+    a.blob = d_packed; a.blob_bytes = TOTAL_BYTES;
+    a.feat = d_out_feat; a.fs = (_Float16 *)d_fs;
+    a.item0 = 0; a.n_items = (int32_t)S_capacity;
+    a.sx0 = (_Float16 *)saved->x0; a.sh1 = (_Float16 *)saved->h1; a.sh2 = (_Float16 *)saved->h2;
+    a.sh3 = (_Float16 *)saved->h3;
+    int64_t wg = (S_capacity + WG_SAMPLES - 1) / WG_SAMPLES;
+    hipLaunchKernelGGL((k_agg_rows<0, true>), dim3((unsigned)(wg < 256 ? wg : 256)), dim3(ROWS_TPB), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

@@ -142,18 +142,27 @@ def loss_from_query(points, mlp, q, campos, rot, raydir, gt, opts: HotPathOpts, 
     """Reference losses for one batch given a sample-major query result q (dict of tensors:
     ray_ns [R], ray_soff [R], samp_ray [S], samp_locw [S,3], pidx [S,K]).
     Returns (total loss, dict of parts, rendered colour [R,3], ray_mask [R])."""
+    campos = campos.reshape(1, 3)
+    rot = rot.reshape(3, 3)
+    feat, conf_coef, mask = aggregate(points, mlp, campos, rot, raydir, q["samp_ray"], q["samp_locw"], q["pidx"])
+    return composite_losses(points, q, feat, mask.sum(-1) > 0, campos, rot, raydir, gt, opts, bg, zero_one_weight,
+                            zero_eps)
+
+
+def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotPathOpts, bg=(1.0, 1.0, 1.0),
+                     zero_one_weight=1e-4, zero_eps=1e-3):
+    """ray_dist + ray_march + the reference losses from per-sample features feat [S,4]
+    (alpha, r, g, b) and the per-sample validity (>= 1 neighbour)."""
     R = raydir.shape[0]
     SR = opts.SR
     campos = campos.reshape(1, 3)
     rot = rot.reshape(3, 3)
-    feat, conf_coef, mask = aggregate(points, mlp, campos, rot, raydir, q["samp_ray"], q["samp_locw"], q["pidx"])
-    nnb = mask.sum(-1)
     S = q["samp_ray"].shape[0]
     dev = raydir.device
     sr = q["samp_ray"].long()
     slot = torch.arange(S, device=dev) - q["ray_soff"].long()[sr]
     fd = torch.zeros(R, SR, 4, device=dev).index_put((sr, slot), feat)
-    vd = torch.zeros(R, SR, dtype=torch.bool, device=dev).index_put((sr, slot), nnb > 0)
+    vd = torch.zeros(R, SR, dtype=torch.bool, device=dev).index_put((sr, slot), valid)
     ld = torch.zeros(R, SR, 3, device=dev).index_put((sr, slot), q["samp_locw"])
     z = _w2pers(ld, rot, campos)[..., 2]
     cm = torch.cummax(z, dim=-1)[0]
@@ -191,6 +200,33 @@ def loss_from_query(points, mlp, q, campos, rot, raydir, gt, opts: HotPathOpts, 
     return total, {"ray_masked_coarse_raycolor": l_col.detach(), "conf_coefficient": l_zo.detach()}, full, ray_mask
 
 
+def _allreduce_buckets(grads, bucket_elems):
+    """Mean of the gradients over ranks, in flat buckets (one collective per bucket; a single
+    tensor larger than a bucket is reduced in place)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    n = dist.get_world_size()
+    i = 0
+    while i < len(grads):
+        if grads[i].numel() >= bucket_elems:
+            dist.all_reduce(grads[i])
+            grads[i] /= n
+            i += 1
+            continue
+        bucket, size = [], 0
+        while i < len(grads) and grads[i].numel() < bucket_elems and (not bucket or size + grads[i].numel() <= bucket_elems):
+            bucket.append(grads[i])
+            size += grads[i].numel()
+            i += 1
+        flat = torch.cat([g.reshape(-1) for g in bucket])
+        dist.all_reduce(flat)
+        flat /= n
+        off = 0
+        for g in bucket:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+            off += g.numel()
+
+
 class Trainer:
     """One data-parallel training step per call (config 5: 4096 random rays per rank)."""
 
@@ -222,25 +258,7 @@ class Trainer:
                 "pidx": res.pidx[: S * self.opts.K].view(S, self.opts.K).long()}
 
     def allreduce_grads(self, params):
-        """Mean of the gradients over ranks, in flat buckets (one collective per bucket)."""
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-            return
-        n = dist.get_world_size()
-        grads = [p.grad for p in params if p.grad is not None]
-        i = 0
-        while i < len(grads):
-            bucket, size = [], 0
-            while i < len(grads) and (not bucket or size + grads[i].numel() <= self.bucket_elems):
-                bucket.append(grads[i])
-                size += grads[i].numel()
-                i += 1
-            flat = torch.cat([g.reshape(-1) for g in bucket])
-            dist.all_reduce(flat)
-            flat /= n
-            off = 0
-            for g in bucket:
-                g.copy_(flat[off:off + g.numel()].view_as(g))
-                off += g.numel()
+        _allreduce_buckets([p.grad for p in params if p.grad is not None], self.bucket_elems)
 
     def _set_lr(self):
         exp, iters = self.decay

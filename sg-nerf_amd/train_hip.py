@@ -1,0 +1,308 @@
+"""Training step on the HIP kernels.
+
+The reference trains through torch autograd (`optimize_parameters`,
+models/base_rendering_model.py:534-664; models/mvs_points_volumetric_model.py:47-141).  Here
+the per-neighbour part -- the NeuralPoints gather and the 4-layer per-row MLP + alpha +
+K-blend of PointAggregator (point_aggregators.py:868-959, :561-786), 95 % of the FLOPs --
+runs forward and backward in hand-written MFMA kernels (mlp.hip k_agg_rows<0, true>,
+agg_train.hip k_agg_bwd); the per-sample colour MLP, ray_dist / ray_march and the losses
+are differentiated by torch on the device (they are small, per sample / per ray):
+
+  query        sgn_query (jittered depths, is_train), indices carry no gradient
+  forward      sgn_aggregate_train_fwd: blended features f_s (fp16) and alpha_s per sample,
+               per-row layer inputs saved for the backward
+  colour+loss  torch: colour MLP on [f_s | PE(v)], ray_dist + ray_march, ray-masked MSE +
+               zero-one(conf) (train.composite_losses); backward -> d f_s, d alpha_s, colour grads
+  backward     sgn_aggregate_backward: deltas of the 4 row layers, d alpha-logit, point grads
+               (embedding via PE(feat), colour, dir, conf through the straight-through clamp)
+               with a power-of-two loss scale; dW = delta^T x per layer as fp16 GEMMs with fp32
+               output (hipBLASLt), unpermuted into the flat parameter gradient
+  update       bucketed all-reduce (RCCL) of the flat MLP gradient and the point gradients,
+               two Adam groups (lr 5e-4 / plr 2e-3) with iter_exponential_decay
+
+MLP weights live in ONE flat fp32 parameter (LAYERS order), so the MFMA blobs are re-packed on
+the device every step by index gathers (sgn_mlp_pack_index / sgn_train_pack_index).
+"""
+import ctypes
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .opts import HotPathOpts
+from .train import PointParams, _pe, composite_losses, _allreduce_buckets
+from .weights import LAYERS, strip_prefix
+
+N_F32 = 2056
+
+
+class FlatMLP(nn.Module):
+    """The 9 viewmlp layers in one flat fp32 parameter: per layer weight (row-major) then bias."""
+
+    def __init__(self, state, device):
+        super().__init__()
+        state = strip_prefix(state)
+        parts, self.slices, off = [], {}, 0
+        for name, o, i, _ in LAYERS:
+            parts += [torch.as_tensor(state[name + ".weight"]).float().reshape(-1),
+                      torch.as_tensor(state[name + ".bias"]).float().reshape(-1)]
+            self.slices[name] = (off, o, i)
+            off += o * i + o
+        self.flat = nn.Parameter(torch.cat(parts).to(device))
+
+    def w(self, name, t=None):
+        off, o, i = self.slices[name]
+        return (self.flat if t is None else t)[off:off + o * i].view(o, i)
+
+    def b(self, name, t=None):
+        off, o, i = self.slices[name]
+        return (self.flat if t is None else t)[off + o * i:off + o * i + o]
+
+    def state(self):
+        out = {}
+        for name, *_ in LAYERS:
+            out[name + ".weight"] = self.w(name).detach().clone()
+            out[name + ".bias"] = self.b(name).detach().clone()
+        return out
+
+
+class _Packer:
+    """Device-side re-packing of the forward and transposed MFMA blobs from the flat weights."""
+
+    def __init__(self, device):
+        L = _lib.lib()
+        self.total = int(L.sgn_mlp_packed_bytes())
+        self.off_f32 = self.total - 4 * N_F32
+        self.tbytes = int(L.sgn_train_tblob_bytes())
+        maps = []
+        for which, n in ((0, self.off_f32 // 2), (1, N_F32)):
+            a = (ctypes.c_int32 * n)()
+            _lib.check(L.sgn_mlp_pack_index(which, a, n), "sgn_mlp_pack_index")
+            maps.append(torch.frombuffer(bytearray(a), dtype=torch.int32).long())
+        a = (ctypes.c_int32 * (self.tbytes // 2))()
+        _lib.check(L.sgn_train_pack_index(a, self.tbytes // 2), "sgn_train_pack_index")
+        maps.append(torch.frombuffer(bytearray(a), dtype=torch.int32).long())
+        self.i16, self.i32, self.it = (m.to(device) for m in maps)
+        self.blob = torch.zeros(self.total, dtype=torch.uint8, device=device)
+        self.tblob = torch.zeros(self.tbytes, dtype=torch.uint8, device=device)
+
+    def pack(self, flat):
+        ext = torch.cat([flat.detach().new_zeros(1), flat.detach()])
+        self.blob[:self.off_f32].view(torch.float16).copy_(ext[self.i16])
+        self.blob[self.off_f32:].view(torch.float32).copy_(ext[self.i32])
+        self.tblob.view(torch.float16).copy_(ext[self.it])
+        return self.blob, self.tblob
+
+
+def _colmap(which, n, device):
+    a = (ctypes.c_int32 * n)()
+    _lib.check(_lib.lib().sgn_train_colmap(which, a, n), "sgn_train_colmap")
+    return torch.frombuffer(bytearray(a), dtype=torch.int32).long().to(device)
+
+
+_MM_OUT_DTYPE = None
+
+
+def _mm_f32(a, b):
+    """fp16 x fp16 -> fp32 GEMM (hipBLASLt through torch.mm(out_dtype=)); fp32 GEMM otherwise."""
+    global _MM_OUT_DTYPE
+    if _MM_OUT_DTYPE is None:
+        try:
+            torch.mm(a[:1, :1], b[:1, :1], out_dtype=torch.float32)
+            _MM_OUT_DTYPE = True
+        except Exception:
+            _MM_OUT_DTYPE = False
+    if _MM_OUT_DTYPE:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    return a.float() @ b.float()
+
+
+class HipTrainer:
+    """One data-parallel training step per call on the HIP path (config 5)."""
+
+    def __init__(self, points: PointParams, mlp_state, opts: HotPathOpts, device, lr=5e-4, plr=2e-3,
+                 lr_decay_exp=0.1, lr_decay_iters=1_000_000, bucket_mb=64, querier=None):
+        self.device = torch.device(device)
+        self.opts = opts.check_supported()
+        if opts.bpnet_variant != (0, 0):
+            raise NotImplementedError("the HIP training path is built for the base viewmlp (no block2_bpnet)")
+        self.points = points
+        self.mlp = FlatMLP(mlp_state, self.device)
+        self.point_params = [points.points_embeding, points.points_color, points.points_dir, points.points_conf]
+        self.opt_net = torch.optim.Adam([self.mlp.flat], lr=lr, betas=(0.9, 0.999))
+        self.opt_pts = torch.optim.Adam(self.point_params, lr=plr, betas=(0.9, 0.999))
+        self.base_lr = (lr, plr)
+        self.decay = (lr_decay_exp, lr_decay_iters)
+        self.step_count = 0
+        self.bucket_elems = bucket_mb * (1 << 20) // 4
+        self.querier = querier
+        self.packer = _Packer(self.device)
+        self.map_chain = _colmap(0, 256, self.device)
+        self.map_x0 = _colmap(1, 288, self.device)
+        self.map_h2 = _colmap(2, 272, self.device)
+        self._cap = 0
+
+    # -- buffers -----------------------------------------------------------------------
+    def _buffers(self, n_items, S_cap):
+        dev = self.device
+        if S_cap > getattr(self, "_scap", 0):
+            self.feat = torch.zeros(S_cap, 4, dtype=torch.float32, device=dev)
+            self._scap = S_cap
+        if n_items > self._cap:
+            cap = max(32, ((n_items + 31) // 32) * 32)
+            rows = cap * 8
+            h = dict(dtype=torch.float16, device=dev)
+            self.fs = torch.empty(cap, 256, **h)
+            self.x0 = torch.empty(rows, 288, **h)
+            self.h1 = torch.empty(rows, 256, **h)
+            self.h2 = torch.empty(rows, 272, **h)
+            self.h3 = torch.empty(rows, 256, **h)
+            self.d = [torch.empty(rows, 256, **h) for _ in range(4)]  # d1..d4
+            self.h4 = torch.empty(rows, 256, **h)
+            self.dza = torch.empty(rows, dtype=torch.float32, device=dev)
+            self._cap = cap
+
+    def _query(self, campos, raydir, near, far):
+        if self.querier is None:
+            from .querier import LightningFastQuerier
+            self.querier = LightningFastQuerier(self.device, self.opts)
+        return self.querier.query_samples(self.points.xyz, campos, raydir, near, far)
+
+    def _tables(self, campos, rot, raydir):
+        pt = _lib.PointTables()
+        P = self.points
+        pt.xyz, pt.embedding, pt.color = P.xyz.data_ptr(), P.points_embeding.data_ptr(), P.points_color.data_ptr()
+        pt.dir, pt.conf, pt.n_points = P.points_dir.data_ptr(), P.points_conf.data_ptr(), P.xyz.shape[0]
+        pt.campos, pt.camrotc2w, pt.raydir = campos.data_ptr(), rot.data_ptr(), raydir.data_ptr()
+        return pt
+
+    def _colour(self, fs, v):
+        m = self.mlp
+        vpe = _pe(v, 4, ori=True)[..., 3:]
+        c = torch.cat([fs, vpe], dim=-1)
+        for name in ("color_branch.0", "color_branch.2", "color_branch.4"):
+            c = F.leaky_relu(F.linear(c, m.w(name), m.b(name)), 0.01)
+        c = F.linear(c, m.w("color_branch.6"), m.b("color_branch.6"))
+        return torch.sigmoid(c) * (1 + 2 * 0.001) - 0.001
+
+    # -- one step ------------------------------------------------------------------------
+    def backward(self, campos, rot, raydir, near, far, gt):
+        """Forward + backward + gradient all-reduce (no parameter update).
+        Returns (loss parts, rendered colour [R,3], ray_mask [R])."""
+        o = self.opts
+        dev = self.device
+        campos = campos.reshape(3).to(dev, torch.float32).contiguous()
+        rot = rot.reshape(3, 3).to(dev, torch.float32).contiguous()
+        raydir = raydir.reshape(-1, 3).to(dev, torch.float32).contiguous()
+        R = raydir.shape[0]
+        q = self._query(campos, raydir, near, far)
+        S, n = (int(x) for x in q.counters[:2].tolist())  # one host sync per step
+        self._buffers(n, max(S, 1))
+        blob, tblob = self.packer.pack(self.mlp.flat)
+        L = _lib.lib()
+        st = _lib.stream_handle()
+        pt = self._tables(campos, rot, raydir)
+        qo = q.abi()
+        saved = _lib.AggSaved(self.x0.data_ptr(), self.h1.data_ptr(), self.h2.data_ptr(), self.h3.data_ptr())
+        if n > 0:
+            _lib.check(L.sgn_aggregate_train_fwd(ctypes.byref(pt), ctypes.byref(qo), n, o.K, _lib.ptr(blob),
+                                                 _lib.ptr(self.feat), _lib.ptr(self.fs), ctypes.byref(saved), st),
+                       "sgn_aggregate_train_fwd")
+        for p in self.point_params + [self.mlp.flat]:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            else:
+                p.grad.zero_()
+        # ---- colour MLP + composite + losses (torch autograd, per sample / per ray) ----------
+        samp = q.work[:n].long()
+        fs_t = self.fs[:n].float().requires_grad_(True)
+        alpha_t = self.feat[samp, 0].clone().requires_grad_(True)
+        v = raydir[q.samp_ray[samp].long()]
+        feat_s = torch.cat([alpha_t[:, None], self._colour(fs_t, v)], dim=-1)
+        featS = torch.zeros(S, 4, device=dev).index_put((samp,), feat_s)
+        validS = torch.zeros(S, dtype=torch.bool, device=dev)
+        validS[samp] = True
+        qd = {"ray_ns": q.ray_ns[:R].long(), "ray_soff": q.ray_soff[:R].long(), "samp_ray": q.samp_ray[:S].long(),
+              "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K).long()}
+        total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, campos, rot, raydir, gt, o)
+        total.backward()
+        # ---- HIP backward of the per-row part -----------------------------------------------
+        if n > 0:
+            dfs = fs_t.grad.contiguous()
+            dal = alpha_t.grad.contiguous()
+            m = torch.maximum(dfs.abs().amax(), dal.abs().amax())
+            scale = torch.exp2(-torch.floor(torch.log2(torch.clamp(m, min=1e-30)))).reshape(1).contiguous()
+            deltas = _lib.AggDeltas(self.d[3].data_ptr(), self.d[2].data_ptr(), self.d[1].data_ptr(),
+                                    self.d[0].data_ptr(), self.h4.data_ptr(), self.dza.data_ptr())
+            P = self.points
+            grads = _lib.PointGrads(P.points_embeding.grad.data_ptr(), P.points_color.grad.data_ptr(),
+                                    P.points_dir.grad.data_ptr(), P.points_conf.grad.data_ptr())
+            _lib.check(L.sgn_aggregate_backward(ctypes.byref(pt), ctypes.byref(qo), n, _lib.ptr(blob), _lib.ptr(tblob),
+                                                ctypes.byref(saved), _lib.ptr(dfs), _lib.ptr(dal), _lib.ptr(scale),
+                                                ctypes.byref(deltas), ctypes.byref(grads), st),
+                       "sgn_aggregate_backward")
+            self._weight_grads(n * 8, scale)
+        self.allreduce_grads([self.mlp.flat] + self.point_params)
+        parts["total"] = total.detach()
+        return parts, full.detach(), ray_mask
+
+    def _weight_grads(self, rows, scale):
+        """dW_l = delta_l^T x_l (fp16 GEMM, fp32 out), db_l = sum delta_l, unpermuted."""
+        m = self.mlp
+        g = m.flat.grad
+        inv = 1.0 / scale
+        uc = self.map_chain
+        for name, d, x, xmap in (("block3.2", self.d[3], self.h3, self.map_chain),
+                                 ("block3.0", self.d[2], self.h2, self.map_h2),
+                                 ("block1.2", self.d[1], self.h1, self.map_chain),
+                                 ("block1.0", self.d[0], self.x0, self.map_x0)):
+            dr, xr = d[:rows], x[:rows]
+            G = _mm_f32(dr.t(), xr) * inv
+            ok = xmap >= 0
+            gw = m.w(name, g)
+            gw.index_put_((uc[:, None], xmap[ok][None, :]), G[:, ok], accumulate=True)
+            m.b(name, g).index_put_((uc,), dr.float().sum(0) * inv, accumulate=True)
+        # alpha branch: dWa = dza^T h4, dba = sum dza
+        ga = (self.dza[:rows][None, :] @ self.h4[:rows].float())[0] * inv
+        m.w("alpha_branch.0", g)[0].index_put_((uc,), ga, accumulate=True)
+        m.b("alpha_branch.0", g).add_(self.dza[:rows].sum() * inv)
+
+    def allreduce_grads(self, params):
+        _allreduce_buckets([p.grad for p in params if p.grad is not None], self.bucket_elems)
+
+    def _set_lr(self):
+        exp, iters = self.decay
+        f = exp ** (self.step_count / iters)  # iter_exponential_decay
+        for opt, base in ((self.opt_net, self.base_lr[0]), (self.opt_pts, self.base_lr[1])):
+            for gr in opt.param_groups:
+                gr["lr"] = base * f
+
+    def apply(self):
+        self._set_lr()
+        self.opt_net.step()
+        self.opt_pts.step()
+        self.step_count += 1
+
+    def step(self, campos, rot, raydir, near, far, gt):
+        out = self.backward(campos, rot, raydir, near, far, gt)
+        self.apply()
+        return out
+
+    def mlp_state(self):
+        return self.mlp.state()
+
+
+def grads_named(trainer: HipTrainer):
+    """Gradients under the reference names (for parity tests): MLP layers + point params."""
+    m = trainer.mlp
+    g = m.flat.grad
+    out = {}
+    for name, *_ in LAYERS:
+        out[name + ".weight"] = m.w(name, g).detach().clone()
+        out[name + ".bias"] = m.b(name, g).detach().clone()
+    P = trainer.points
+    for k in ("points_embeding", "points_color", "points_dir", "points_conf"):
+        out[k] = getattr(P, k).grad.detach().clone()
+    return out

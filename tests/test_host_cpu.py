@@ -191,3 +191,35 @@ def test_sg_abi_sizes():
     assert int(L.sgn_mlp_packed_bytes_sg(1, 0)) == base + 8 * 16 * 1024 + 1024
     assert int(L.sgn_mlp_packed_bytes_sg(2, 96)) == 0
     assert int(L.sgn_mlp_packed_bytes_sg(1, 32)) == 0
+
+
+def test_training_pack_index_maps():
+    """Index maps of the device-side re-packing cover every packed parameter exactly as the
+    host packers do (flat LAYERS order)."""
+    from sgnerf_amd.weights import N_PARAMS
+    L = _lib.lib()
+    total = int(L.sgn_mlp_packed_bytes())
+    n16, n32 = (total - 4 * 2056) // 2, 2056
+    a16, a32 = (ctypes.c_int32 * n16)(), (ctypes.c_int32 * n32)()
+    assert L.sgn_mlp_pack_index(0, a16, n16) == 0 and L.sgn_mlp_pack_index(1, a32, n32) == 0
+    m16, m32 = np.frombuffer(a16, np.int32), np.frombuffer(a32, np.int32)
+    # block1/3 + colour hidden weights live in fragments: each exactly once
+    used16 = np.bincount(m16[m16 > 0], minlength=N_PARAMS + 1)
+    assert used16.max() == 1
+    # biases, alpha weights and colour output layer live in the fp32 section
+    used32 = np.bincount(m32[m32 > 0], minlength=N_PARAMS + 1)
+    assert used32.max() == 1
+    assert int((used16 + used32 > 0).sum()) == N_PARAMS  # every parameter packed somewhere
+    nt = int(L.sgn_train_tblob_bytes()) // 2
+    at = (ctypes.c_int32 * nt)()
+    assert L.sgn_train_pack_index(at, nt) == 0
+    mt = np.frombuffer(at, np.int32)
+    ut = np.bincount(mt[mt > 0], minlength=N_PARAMS + 1)
+    assert ut.max() == 1 and int((ut > 0).sum()) == 256 * (284 + 256 + 263 + 256)
+    cm = (ctypes.c_int32 * 256)()
+    assert L.sgn_train_colmap(0, cm, 256) == 0
+    assert sorted(np.frombuffer(cm, np.int32).tolist()) == list(range(256))
+    c1 = (ctypes.c_int32 * 288)()
+    assert L.sgn_train_colmap(1, c1, 288) == 0
+    v1 = np.frombuffer(c1, np.int32)
+    assert sorted(v1[v1 >= 0].tolist()) == list(range(284))
