@@ -191,11 +191,20 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     # neighbours read conf at the clamped index 0 (neural_points.py:956-967)
     K = q["pidx"].shape[1]
     pd = torch.full((R, SR, K), -1, dtype=torch.long, device=dev).index_put((sr, slot), q["pidx"].long())
-    pd = pd[ray_mask]
-    cd = torch.index_select(points.points_conf, 0, torch.clamp(pd, min=0).reshape(-1)).view(pd.shape)
+    # Empty entries all read conf[0]: gather them as one scalar (its gradient is a reduction)
+    # and spread their gather indices, so the index_select backward does not pile every empty
+    # entry's atomic add onto point 0.  Invalid rays are weighted out instead of compacted
+    # (no host sync); the value is the mean over the valid rays' entries, as in the reference.
+    n_pts = points.points_conf.shape[0]
+    ok = pd >= 0
+    spread = (torch.arange(pd.numel(), device=dev) % n_pts).view(pd.shape)
+    cg = torch.index_select(points.points_conf, 0, torch.where(ok, pd, spread).reshape(-1)).view(pd.shape)
+    cd = torch.where(ok, cg, points.points_conf[0, 0])
     cc = cd - (cd - torch.clamp(cd, 1e-4, 1.0)).detach()
     val = torch.clamp(cc, zero_eps, 1 - zero_eps)
-    l_zo = torch.mean(torch.log(val) + torch.log(1 - val)) if cc.numel() else torch.zeros((), device=dev)
+    wr = ray_mask.to(val.dtype)[:, None, None]
+    n_e = wr.sum() * (SR * K)
+    l_zo = torch.sum((torch.log(val) + torch.log(1 - val)) * wr) / torch.clamp(n_e, min=1.0)
     total = l_col + 3e-6 + zero_one_weight * l_zo
     return total, {"ray_masked_coarse_raycolor": l_col.detach(), "conf_coefficient": l_zo.detach()}, full, ray_mask
 

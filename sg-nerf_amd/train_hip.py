@@ -103,6 +103,28 @@ def _colmap(which, n, device):
 
 
 _MM_OUT_DTYPE = None
+_BMM_OUT_DTYPE = None
+
+
+def _gemm_rows_f32(a, b, split):
+    """a^T b over the row dimension: a [rows, M], b [rows, N] fp16 -> [M, N] fp32, as `split`
+    batched GEMMs over row chunks (split-K: a 256 x 288 output alone would occupy ~20 of the
+    256 CUs) summed in fp32.  rows % split == 0."""
+    global _BMM_OUT_DTYPE
+    rows = a.shape[0]
+    if split <= 1:
+        return _mm_f32(a.t(), b)
+    at = a.view(split, rows // split, a.shape[1]).transpose(1, 2)
+    bt = b.view(split, rows // split, b.shape[1])
+    if _BMM_OUT_DTYPE is None:
+        try:
+            torch.bmm(at[:1, :1, :1], bt[:1, :1, :1], out_dtype=torch.float32)
+            _BMM_OUT_DTYPE = True
+        except Exception:
+            _BMM_OUT_DTYPE = False
+    if _BMM_OUT_DTYPE:
+        return torch.bmm(at, bt, out_dtype=torch.float32).sum(0)
+    return torch.bmm(at.float(), bt.float()).sum(0)
 
 
 def _mm_f32(a, b):
@@ -139,10 +161,22 @@ class HipTrainer:
         self.bucket_elems = bucket_mb * (1 << 20) // 4
         self.querier = querier
         self.packer = _Packer(self.device)
+        # stored column p -> reference index; inverses: reference index -> stored column
         self.map_chain = _colmap(0, 256, self.device)
         self.map_x0 = _colmap(1, 288, self.device)
         self.map_h2 = _colmap(2, 272, self.device)
+        self.inv_chain = self._inverse(self.map_chain, 256)
+        self.inv_x0 = self._inverse(self.map_x0, 284)
+        self.inv_h2 = self._inverse(self.map_h2, 263)
         self._cap = 0
+
+    @staticmethod
+    def _inverse(m, n):
+        inv = torch.full((n,), -1, dtype=torch.long, device=m.device)
+        ok = m >= 0
+        inv[m[ok]] = torch.nonzero(ok).reshape(-1)
+        assert bool((inv >= 0).all())
+        return inv
 
     # -- buffers -----------------------------------------------------------------------
     def _buffers(self, n_items, S_cap):
@@ -253,20 +287,24 @@ class HipTrainer:
         m = self.mlp
         g = m.flat.grad
         inv = 1.0 / scale
-        uc = self.map_chain
-        for name, d, x, xmap in (("block3.2", self.d[3], self.h3, self.map_chain),
-                                 ("block3.0", self.d[2], self.h2, self.map_h2),
-                                 ("block1.2", self.d[1], self.h1, self.map_chain),
-                                 ("block1.0", self.d[0], self.x0, self.map_x0)):
-            dr, xr = d[:rows], x[:rows]
-            G = _mm_f32(dr.t(), xr) * inv
-            ok = xmap >= 0
-            gw = m.w(name, g)
-            gw.index_put_((uc[:, None], xmap[ok][None, :]), G[:, ok], accumulate=True)
-            m.b(name, g).index_put_((uc,), dr.float().sum(0) * inv, accumulate=True)
+        iu = self.inv_chain
+        rp = ((rows + 255) // 256) * 256      # rows padded to a multiple of 256 (buffers are)
+        split = max(1, min(32, rp // 8192))
+        while split > 1 and rp % split:
+            split //= 2
+        for t in self.d + [self.x0, self.h1, self.h2, self.h3]:
+            t[rows:rp].zero_()                 # stale tails must not reach the GEMM (0 * NaN)
+        for name, d, x, ix in (("block3.2", self.d[3], self.h3, self.inv_chain),
+                               ("block3.0", self.d[2], self.h2, self.inv_h2),
+                               ("block1.2", self.d[1], self.h1, self.inv_chain),
+                               ("block1.0", self.d[0], self.x0, self.inv_x0)):
+            dr, xr = d[:rp], x[:rp]
+            G = _gemm_rows_f32(dr, xr, split)    # [256 stored][C stored]
+            m.w(name, g).add_(G[iu][:, ix] * inv)        # gathers, no scatter
+            m.b(name, g).add_(torch.sum(dr, 0, dtype=torch.float32)[iu] * inv)
         # alpha branch: dWa = dza^T h4, dba = sum dza
-        ga = (self.dza[:rows][None, :] @ self.h4[:rows].float())[0] * inv
-        m.w("alpha_branch.0", g)[0].index_put_((uc,), ga, accumulate=True)
+        ga = _mm_f32(self.dza[:rows].to(torch.float16)[None, :], self.h4[:rows])[0]
+        m.w("alpha_branch.0", g)[0].add_(ga[iu] * inv)
         m.b("alpha_branch.0", g).add_(self.dza[:rows].sum() * inv)
 
     def allreduce_grads(self, params):
