@@ -34,6 +34,10 @@ from sgnerf_amd.weights import init_mlp  # noqa: E402
 
 METRIC = "rays/sec + ms/frame, 800×800×64 samples, ScanNet scene, 1/2/4/8 GPU"
 FLOP_PER_NB = 2 * (284 * 256 + 256 * 256 + 263 * 256 + 256 * 256 + 256)  # 542,720
+# split block1.0: per row only the 60 PE(dists) inputs of block1.0 remain; the
+# 224 per-point inputs are multiplied once per point and frame by k_point_proj
+FLOP_PER_ROW_SPLIT = FLOP_PER_NB - 2 * 224 * 256                          # 428,032
+FLOP_PER_POINT_PROJ = 2 * 224 * 256                                         # 114,688
 FLOP_PER_SMP = 2 * (280 * 128 + 128 * 128 * 2 + 128 * 3)                 # 137,984
 PEAK_F16_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12  # dense fp16 MFMA, MI355X_MICROARCH.md (~2.5 PF)
 PEAK_HBM_GBS = 8000.0
@@ -260,7 +264,7 @@ def main():
     if dist:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(el.item())
-    stage_names = ["query", "agg_rows", "agg_color", "composite"]
+    stage_names = ["query", "proj", "agg_rows", "agg_color", "composite"]
     order = stage_names + ["end"]
     stage_ms = {n: float(np.mean([ev[n].elapsed_time(ev[order[j + 1]]) for ev in events]))
                 for j, n in enumerate(stage_names)}
@@ -280,8 +284,9 @@ def main():
         q_bytes.append(R * (12 + 4 + 4 + 2 * args.sr) + 4 * cnt[2] + 16 * cnt[3] + S * (4 + 4 + 12 + 12 + 4 + 4 * 8)
                        + 4 * W)
     torch.cuda.synchronize()
-    flop_nb = FLOP_PER_NB + (2 * 352 * 256 if args.sg else 0)  # + block2_bpnet.0 (SG)
+    flop_nb = FLOP_PER_ROW_SPLIT + (2 * 352 * 256 if args.sg else 0)  # + block2_bpnet.0 (SG)
     rows_flop = flop_nb * float(np.mean(n_nb))
+    ref_flop = (FLOP_PER_NB + (2 * 352 * 256 if args.sg else 0)) * float(np.mean(n_nb))
     achieved = rows_flop / (stage_ms["agg_rows"] * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -319,7 +324,8 @@ def main():
                       + "263->256->256 + alpha + K-blend)",
             "bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / PEAK_F16_TFLOPS, "traffic": traffic,
-            "flop_per_launch": rows_flop, "avg_launch_ms": stage_ms["agg_rows"],
+            "flop_per_launch": rows_flop, "flop_per_valid_row": flop_nb, "avg_launch_ms": stage_ms["agg_rows"],
+            "reference_formulation_TFLOPs": ref_flop / (stage_ms["agg_rows"] * 1e-3) / 1e12,
         },
         "roofline_query": {
             "kernel": "query stage (k_march + scan + k_emit_samples + k_knn)", "bound": "hbm/l2 gather",
@@ -330,6 +336,11 @@ def main():
             "effective_GBps_no_reuse_credit": float(np.mean(q_bytes)) / (stage_ms["query"] * 1e-3) / 1e9,
             "hbm_peak_GBps": PEAK_HBM_GBS,
             "bytes_per_frame_no_reuse_credit": float(np.mean(q_bytes)),
+        },
+        "roofline_proj": {
+            "kernel": "k_point_proj (block1.0 point inputs, all points, once per frame)", "bound": "mfma",
+            "achieved": FLOP_PER_POINT_PROJ * args.points / (stage_ms["proj"] * 1e-3) / 1e12, "peak": PEAK_F16_TFLOPS,
+            "unit": "TFLOP/s", "avg_launch_ms": stage_ms["proj"],
         },
         "stages_ms": stage_ms,
         "grid_build_ms": grid_ms,

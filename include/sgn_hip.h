@@ -159,6 +159,19 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
                   float *d_out_wnorm, void *d_workspace, size_t workspace_bytes, int32_t stages,
                   sgn_stream_t stream);
 
+/* ---- split block1.0 (per-point projection) ----------------------------------
+ * block1.0's inputs [feat | PE(feat) | PE(dists)] (point_aggregators.py:594-621) are per
+ * point for the first 224 of 284 channels: sgn_point_project computes
+ * P[p] = W0a [feat_p | PE(feat_p)] + b0 for every point once per frame (fp16,
+ * sgn_point_proj_bytes(N)), and sgn_aggregate_sg(d_point_proj = P) then multiplies only the
+ * 60 PE(dists) channels per (sample, neighbour) row.  Same sums, regrouped. */
+size_t sgn_point_proj_bytes(int64_t n_points);
+int sgn_point_project(const sgn_point_tables *pt, const void *d_packed_mlp, void *d_proj,
+                      sgn_stream_t stream);
+/* Byte offsets inside the packed blob: 0 = fp32 section, 1 = split block1.0 sections,
+ * 2 = end of the base blob (sgn_mlp_packed_bytes). */
+size_t sgn_mlp_section(int32_t which);
+
 /* ---- SG-NeRF variant: block2_bpnet (shading_feature_mlp_layer2_bpnet) ---
  * Replaces PointAggregator.block2_bpnet (models/aggregators/point_aggregators.py:345-354,
  * applied at :629-636) and the BPNet-embedding gather of NeuralPoints.forward
@@ -175,7 +188,7 @@ int sgn_mlp_pack_sg(int32_t bpnet_layers, int32_t bpnet_dim, const float *const 
 int sgn_bpnet_pack(const float *d_embedding, int64_t n_points, int32_t bpnet_dim, void *d_out_f16,
                    sgn_stream_t stream);
 int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpnet_f16,
-                     const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
+                     const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
                      int32_t K, const void *d_packed_mlp, float *d_out_feat, float *d_out_blend,
                      float *d_out_wnorm, void *d_workspace, size_t workspace_bytes,
                      int32_t stages, sgn_stream_t stream);
@@ -214,7 +227,7 @@ int sgn_train_pack_t(const float *const *w, void *d_tblob, sgn_stream_t stream);
  * in sgn_mlp_pack order, each weight row-major then its bias): out[i] = flat index + 1, 0 =
  * zero.  sgn_mlp_pack_index: which 0 = fp16 fragment part (n = OFF_F32 / 2 elements),
  * 1 = fp32 section (n = 2056); sgn_train_pack_index: transposed blob (n = tblob_bytes / 2). */
-int sgn_mlp_pack_index(int32_t which, int32_t *out, int64_t n);
+int sgn_mlp_pack_index(int32_t which, int32_t *out, int64_t n);  /* which 2: split block1.0 sections */
 int sgn_train_pack_index(int32_t *out, int64_t n);
 /* Column maps of the saved/delta tiles to reference indices (-1 = padding):
  * which 0: [256] chain order -> unit, 1: [288] -> block1.0 input, 2: [272] -> block3.0 input. */

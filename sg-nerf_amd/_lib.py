@@ -81,7 +81,10 @@ SIGNATURES = {
     "sgn_mlp_packed_bytes_sg": (c_sz, [c_i32, c_i32]),
     "sgn_mlp_pack_sg": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
     "sgn_bpnet_pack": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
-    "sgn_aggregate_sg": (c_i32, [c_i32, c_i32, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64,
+    "sgn_point_proj_bytes": (c_sz, [c_i64]),
+    "sgn_point_project": (c_i32, [ctypes.POINTER(PointTables), c_vp, c_vp, c_vp]),
+    "sgn_mlp_section": (c_sz, [c_i32]),
+    "sgn_aggregate_sg": (c_i32, [c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64,
                                  c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
     "sgn_aggregate_train_fwd": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32, c_vp,
                                         c_vp, c_vp, ctypes.POINTER(AggSaved), c_vp]),

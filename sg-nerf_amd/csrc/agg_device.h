@@ -92,6 +92,7 @@ struct AggArgs {
     float *blend;     // [S*8] weight * conf (optional)
     float *wnorm;     // [S*8] normalised weight (optional)
     _Float16 *fs;     // [chunk][256] blended features (natural unit order)
+    const _Float16 *proj;  // split block1.0: P[point][2][128] = W0a [feat | PE(feat)] + b0, acc order
     int32_t item0, n_items;  // work-list chunk
     // training forward (save mode): per-row layer inputs, row = 8 * (item - item0) + k,
     // fp16 in fragment column order (mlp_layout.h: column 16 s + 8 h + e of k-step s)
@@ -237,6 +238,7 @@ struct RowIn {
 
 // Gather + pers + dists + weights of this lane's row; raw features for the
 // just-in-time layer-0 encodings, block3's extra channels.
+template <bool FEAT = true>  // FEAT = false: the point features are not needed (split block1.0)
 __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, int item, int end, int lane,
                                             float (&feat)[16], float (&dist)[3], h8 &ext) {
     const int h = lane >> 5, kk = lane & 7;
@@ -260,11 +262,16 @@ __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, in
     float col[3] = {0.f, 0.f, 0.f}, pdr[3] = {0.f, 0.f, 0.f};
     if (m) {
         px = a.xyz[(int64_t)pid * 3 + 0]; py = a.xyz[(int64_t)pid * 3 + 1]; pz = a.xyz[(int64_t)pid * 3 + 2];
-        const f32x4 *e4 = (const f32x4 *)(a.emb + (int64_t)pid * 32 + 16 * h);
+        if constexpr (FEAT) {
+            const f32x4 *e4 = (const f32x4 *)(a.emb + (int64_t)pid * 32 + 16 * h);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 v = e4[g];
-            feat[4 * g + 0] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
+            for (int g = 0; g < 4; ++g) {
+                f32x4 v = e4[g];
+                feat[4 * g + 0] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 16; ++c) feat[c] = 0.f;
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) { col[c] = a.color[(int64_t)pid * 3 + c]; pdr[c] = a.dir[(int64_t)pid * 3 + c]; }

@@ -95,7 +95,7 @@ constexpr int LAG = SGN_LAG;
 constexpr int N_DMA_WAVES = LAG ? WG_WAVES / 2 : WG_WAVES;
 constexpr int PF_N = CHUNK_FRAGS / N_DMA_WAVES;  // LDS-DMA instructions per issuing wave per chunk
 #ifndef SGN_DIST
-#define SGN_DIST 2
+#define SGN_DIST 1  // measured: 1 chunk in flight beats 2 by 12 % (k_agg_rows 13.65 -> 11.97 ms, same box)
 #endif
 constexpr int DIST = SGN_DIST;                // chunks in flight ahead of the one being consumed
 constexpr int NSLOT = DIST + LAG + 1;         // ring slots (the DMA target was read LAG+1 chunks ago)
@@ -105,32 +105,35 @@ static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the wav
 
 
 // Layers of the row stream: 0 block1.0, 1 block1.2, 2 block3.0, 3 block3.2, 4 block2_bpnet.0
-// (SG variant only).  KSB = k-steps of block2_bpnet.0 (0: variant absent).  Stream order:
-// 0, 1, [4], 2, 3.
-__host__ __device__ constexpr int layer_ks(int KSB, int L) {
-    return L == 0 ? KS_L0 : L == 2 ? KS_L2 : L == 4 ? KSB : KS_HID;
+// (SG variant only).  Variant code V = KSB + 256 * SPLIT: KSB = k-steps of block2_bpnet.0
+// (0: variant absent), SPLIT = per-point block1.0 projection (layer 0 = W0b only, 4 k-steps).
+// Stream order: 0, 1, [4], 2, 3.  (The stream helpers below take V in their KSB argument.)
+__host__ __device__ constexpr int vksb(int V) { return V & 255; }
+__host__ __device__ constexpr bool vsplit(int V) { return (V >> 8) != 0; }
+__host__ __device__ constexpr int layer_ks(int V, int L) {
+    return L == 0 ? (vsplit(V) ? KS_L0S : KS_L0) : L == 2 ? KS_L2 : L == 4 ? vksb(V) : KS_HID;
 }
 __host__ __device__ constexpr int layer_nch(int KSB, int L) {
     return (layer_ks(KSB, L) + layer_kc(L) - 1) / layer_kc(L);
 }
-__host__ __device__ constexpr size_t layer_off(int L) {
-    return L == 0 ? OFF_W0 : L == 1 ? OFF_W1 : L == 2 ? OFF_W2 : L == 3 ? OFF_W3 : OFF_WB;
+__host__ __device__ constexpr size_t layer_off(int V, int L) {
+    return L == 0 ? (vsplit(V) ? OFF_W0B : OFF_W0) : L == 1 ? OFF_W1 : L == 2 ? OFF_W2 : L == 3 ? OFF_W3 : OFF_WB;
 }
 __host__ __device__ constexpr int chunk_nk(int KSB, int L, int c) {
     return (layer_ks(KSB, L) - c * layer_kc(L)) < layer_kc(L) ? (layer_ks(KSB, L) - c * layer_kc(L)) : layer_kc(L);
 }
 // stream position: layer L, pass P (tiles TP*P..), chunk C (k-steps C*KC..) -> blob offset
 __host__ __device__ constexpr uint32_t chunk_off(int KSB, int L, int P, int C) {
-    return (uint32_t)(layer_off(L) + ((size_t)P * layer_ks(KSB, L) * layer_tp(L) +
+    return (uint32_t)(layer_off(KSB, L) + ((size_t)P * layer_ks(KSB, L) * layer_tp(L) +
                                       (size_t)C * layer_kc(L) * layer_tp(L)) * FRAG);
 }
 
 // ---- chunk stream ---------------------------------------------------------------
 // Per work tile the stream is: layer 0 (1 pass x 9 chunks), then the chained layers
 // (2 passes each) in stream order.
-__host__ __device__ constexpr int n_stream(int KSB) { return KSB ? 5 : 4; }
-__host__ __device__ constexpr int stream_layer(int KSB, int i) { return KSB ? (i < 2 ? i : i == 2 ? 4 : i - 1) : i; }
-__host__ __device__ constexpr int stream_pos(int KSB, int L) { return KSB ? (L < 2 ? L : L == 4 ? 2 : L + 1) : L; }
+__host__ __device__ constexpr int n_stream(int V) { return vksb(V) ? 5 : 4; }
+__host__ __device__ constexpr int stream_layer(int V, int i) { return vksb(V) ? (i < 2 ? i : i == 2 ? 4 : i - 1) : i; }
+__host__ __device__ constexpr int stream_pos(int V, int L) { return vksb(V) ? (L < 2 ? L : L == 4 ? 2 : L + 1) : L; }
 __host__ __device__ constexpr int pass_chunks(int KSB, int L) { return layer_nch(KSB, L); }
 __host__ __device__ constexpr int layer_chunks(int KSB, int L) { return layer_np(L) * layer_nch(KSB, L); }
 __host__ __device__ constexpr int pos_base(int KSB, int i) {
@@ -155,6 +158,7 @@ static_assert(CHUNK_FRAGS != 32 || n_chunks(0) == 5 + 2 * (2 + 3 + 2), "base str
 static_assert(CHUNK_FRAGS != 32 || (chunk_L(ks_bp(BP_DIM), 9) == 4 && chunk_L(ks_bp(BP_DIM), 8) == 1 &&
                                      chunk_L(ks_bp(BP_DIM), 15) == 2 && n_chunks(ks_bp(BP_DIM)) == 25),
               "SG stream order");
+static_assert(CHUNK_FRAGS != 32 || (n_chunks(256) == 1 + 2 * (2 + 3 + 2) && chunk_L(256, 1) == 1), "split stream");
 
 // Issue the LDS-DMA of stream chunk N into LDS slot `dst`: each wave moves fragments
 // w + WG_WAVES*j (1 KiB, lane-linear) with buffer_load ... lds; indices past the chunk
@@ -203,14 +207,16 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
 // TRANS: the activations are the A operand and the weights the B operand, so the
 // accumulators hold D^T (lane = output unit, registers = rows) and start at zero (the bias
 // is added in the epilogue, where it is one value per lane).
-template <int KSB, int L, int P, bool TRANS = false, class InFn>
+template <int KSB, int L, int P, bool TRANS = false, bool PREINIT = false, class InFn>
 __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
                                          const float *Fl, size_t fb, f32x16 (&acc)[layer_tp(L)], InFn &&in) {
     constexpr int TP = layer_tp(L), KC = layer_kc(L);
     const int h = lane >> 5;
 #pragma unroll
     for (int tt = 0; tt < TP; ++tt) {
-        if constexpr (TRANS) {
+        if constexpr (PREINIT) {
+            // accumulators already hold the per-point partial sums (split block1.0)
+        } else if constexpr (TRANS) {
             acc[tt] = f32x16{};
         } else {  // accumulators start at the bias (acc order, LDS)
             const f32x4 *b = (const f32x4 *)(Fl + fb + ((TP * P + tt) * 2 + h) * 16);
@@ -274,8 +280,11 @@ __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]
         }
 }
 
-template <int KSB, bool SAVE = false>
+template <int V, bool SAVE = false>
 __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
+    constexpr int KSB = vksb(V);
+    constexpr bool SPLIT = vsplit(V);
+    static_assert(!(SPLIT && SAVE), "the training save mode runs the unsplit block1.0");
     constexpr int NBP = KSB > KS_HID ? KSB - KS_HID : 0;  // BPNet k-steps (SG, predict_semantic = 1)
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES + WG_WAVES * NBP * (int)FRAG];
     const int lane = threadIdx.x & 63;
@@ -285,6 +294,11 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     const int end = min(nwork, a.item0 + a.n_items);
     const Cam cam = load_cam(a.campos, a.rot);
     const WBlob wb = make_blob(a.blob, a.blob_bytes);
+#if defined(SGN_PRIO_HI)  // (timing option, measured neutral with DIST = 1) static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+    if (w >= WG_WAVES / 2) __builtin_amdgcn_s_setprio(1);
+#elif defined(SGN_PRIO_LO)
+    if (w < WG_WAVES / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     const __amdgpu_buffer_rsrc_t bp_rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.bpnet, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t fs_rsrc =
@@ -304,7 +318,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     if (!LAG || w < N_DMA_WAVES) {
         static_for<DIST>([&](auto nn) {
             constexpr int N0 = decltype(nn)::value;
-            dma_chunk<KSB, N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
+            dma_chunk<V, N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
         });
     } else {
         // followers start LAG chunk intervals late (the leaders add LAG barriers at the end)
@@ -319,7 +333,8 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         const int item = base + w * 4 + q;
         float feat[16], dist[3];
         h8 ext;
-        const RowIn ri = gather_row(a, cam, item, end, lane, feat, dist, ext);
+        const RowIn ri = gather_row<!SPLIT>(a, cam, item, end, lane, feat, dist, ext);
+
         const int64_t srow0 = (int64_t)(base + w * 4 - a.item0) * 8;  // first saved row of this wave (SAVE)
         // SG: this row's BPNet embedding -> the wave's LDS area as ready-made B fragments
         // (LDS-DMA, one 1-KiB fragment per k-step; lane (row, half h) <- channels 16j+8h..+7).
@@ -335,11 +350,33 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         h8 actA[16], actB[16];
         {   // block1.0: 284 -> 256, one pass over 8 tiles, inputs generated per k-step
             f32x16 acc0[8];
-            run_pass<KSB, 0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0, [&](auto k) {
-                const h8 v = l0_step<decltype(k)::value>(feat, dist);
-                if constexpr (SAVE) save_frag(a.sx0, KS_L0 * 16, srow0, decltype(k)::value, v, lane, ri.sval);
-                return v;
-            });
+            if constexpr (SPLIT) {
+                // accumulators start at P[pid] (this lane-half's 128 values, acc order); only the
+                // PE(dists) channels (local 112..143) remain for the row
+#ifdef SGN_ABLATE_PROJ  // timing experiment only: P of point 0 for every row (wrong results)
+                const h8 *src = (const h8 *)(a.proj + 128 * h);
+#else
+                const h8 *src = (const h8 *)(a.proj + (int64_t)(ri.pid < 0 ? 0 : ri.pid) * HID + 128 * h);
+#endif
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const h8 p0 = src[2 * t], p1 = src[2 * t + 1];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        acc0[t][r] = (float)p0[r];
+                        acc0[t][r + 8] = (float)p1[r];
+                    }
+                }
+                run_pass<V, 0, 0, false, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0, [&](auto k) {
+                    return l0_step<KS_P0 + decltype(k)::value>(feat, dist);
+                });
+            } else {
+                run_pass<V, 0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0, [&](auto k) {
+                    const h8 v = l0_step<decltype(k)::value>(feat, dist);
+                    if constexpr (SAVE) save_frag(a.sx0, KS_L0 * 16, srow0, decltype(k)::value, v, lane, ri.sval);
+                    return v;
+                });
+            }
             chain_out<8, 0>(acc0, actA);
             if constexpr (SAVE) {
 #pragma unroll
@@ -349,13 +386,13 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         f32x16 acc[4];
         // block1.2: 256 -> 256
         auto inA = [&](auto k) { return actA[decltype(k)::value]; };
-        run_pass<KSB, 1, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
+        run_pass<V, 1, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
         chain_out<4, 0>(acc, actB);
         if constexpr (SAVE) {
 #pragma unroll
             for (int s2 = 0; s2 < 8; ++s2) save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
         }
-        run_pass<KSB, 1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
+        run_pass<V, 1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
         chain_out<4, 1>(acc, actB);
         if constexpr (SAVE) {
 #pragma unroll
@@ -369,9 +406,9 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
                 if constexpr (K < 16) return actB[K];
                 else return *(const h8 *)(bpl + (K - 16) * (int)FRAG + lane * 16);
             };
-            run_pass<KSB, 4, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
+            run_pass<V, 4, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
             chain_out<4, 0>(acc, actA);
-            run_pass<KSB, 4, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
+            run_pass<V, 4, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
             chain_out<4, 1>(acc, actA);
         }
         // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input in actB, or actA after block2_bpnet)
@@ -381,9 +418,9 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
             constexpr int K = decltype(k)::value;
             if constexpr (K < 16) return in3[K]; else return ext;
         };
-        run_pass<KSB, 2, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
+        run_pass<V, 2, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
         chain_out<4, 0>(acc, out3);
-        run_pass<KSB, 2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
+        run_pass<V, 2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
         chain_out<4, 1>(acc, out3);
         if constexpr (SAVE) {
 #pragma unroll
@@ -435,9 +472,9 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
             }
         };
         auto inA3 = [&](auto k) { return out3[decltype(k)::value]; };
-        run_pass<KSB, 3, 0, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
+        run_pass<V, 3, 0, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 0>{});
-        run_pass<KSB, 3, 1, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
+        run_pass<V, 3, 1, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 1>{});
         // alpha: reduce the 16 row partials over the 32 lanes (units) of each half,
         // reduce-scatter style; lane j ends with row index i = 8 b1 + 4 b2 + 2 b3 + b4 (b = bits of j)
@@ -614,6 +651,87 @@ __global__ __launch_bounds__(COL_TPB, 1) void k_color(ColorArgs a) {
     }
 }
 
+// ---- per-point block1.0 projection (split block1.0) ---------------------------------
+// P[p] = W0a [feat_p | PE(feat_p)] + b0 for every point (the 224 point-only channels of the
+// 284 block1.0 inputs, mlp_layout.h), fp16 in accumulator order per lane-half: P[p][h][t][r] =
+// unit 32 t + acc_unit(r, h).  One 512-thread workgroup per CU keeps W0a (112 KiB) and b0 in
+// LDS; each wave takes 32 points at a time, lane = point, k-outer over 14 k-steps.
+constexpr int PROJ_TPB = 512;
+constexpr int PROJ_FRAGS = T_HID * KS_P0;  // 112
+constexpr int PROJ_LDS = PROJ_FRAGS * (int)FRAG + HID * 4;
+static_assert(PROJ_FRAGS % (PROJ_TPB / 64) == 0, "projection fragments split evenly over the waves");
+
+struct ProjArgs {
+    const float *emb;
+    int64_t n;
+    const void *blob;
+    _Float16 *proj;
+};
+
+__global__ __launch_bounds__(PROJ_TPB, 1) void k_point_proj(ProjArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[PROJ_LDS];
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const WBlob wb = make_blob(a.blob);
+#pragma unroll
+    for (int i = 0; i < PROJ_FRAGS / (PROJ_TPB / 64); ++i) {  // W0a fragments -> LDS (LDS-DMA)
+        const int f = w + (PROJ_TPB / 64) * i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)(lds + f * (int)FRAG),
+                                                 16, lane * 16, (uint32_t)(OFF_W0A + (size_t)f * FRAG), 0, 0);
+    }
+    {
+        float *dst = (float *)(lds + PROJ_FRAGS * (int)FRAG);
+        const float *src = (const float *)((const char *)a.blob + OFF_F32) + F_B0;
+        for (int i = threadIdx.x; i < HID; i += PROJ_TPB) dst[i] = src[i];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int64_t nt = (a.n + 31) / 32;
+    for (int64_t tile = (int64_t)blockIdx.x * (PROJ_TPB / 64) + w; tile < nt; tile += (int64_t)gridDim.x * (PROJ_TPB / 64)) {
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        const char *W = lds + lz;
+        const float *B = (const float *)(lds + lz + PROJ_FRAGS * (int)FRAG);
+        const int64_t p = tile * 32 + (lane & 31);
+        const bool ok = p < a.n;
+        float feat[16], dist[3] = {0.f, 0.f, 0.f};
+        {
+            const f32x4 *e4 = (const f32x4 *)(a.emb + (ok ? p : 0) * 32 + 16 * h);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 v = e4[g];
+                feat[4 * g] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
+            }
+        }
+        f32x16 acc[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f32x4 *b = (const f32x4 *)(B + (t * 2 + h) * 16);
+            const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+            acc[t] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                            b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+        }
+        static_for<KS_P0>([&](auto kk) {
+            constexpr int KK = decltype(kk)::value;
+            const h8 x = l0_step<KK>(feat, dist);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                acc[t] = mfma32(*(const h8 *)(W + (t * KS_P0 + KK) * (int)FRAG + lane * 16), x, acc[t]);
+        });
+        if (ok) {
+            h8 *dst = (h8 *)(a.proj + p * HID + 128 * h);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int r = 8 * s2;
+                    dst[2 * t + s2] = pack8(acc[t][r], acc[t][r + 1], acc[t][r + 2], acc[t][r + 3], acc[t][r + 4],
+                                            acc[t][r + 5], acc[t][r + 6], acc[t][r + 7]);
+                }
+        }
+    }
+}
+
 // fp32 -> fp16 point table (BPNet embedding of the SG variant): 4 values per thread
 __global__ __launch_bounds__(256) void k_to_f16(const float *__restrict__ src, _Float16 *__restrict__ dst, int64_t n) {
     for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4; i < n; i += (int64_t)gridDim.x * blockDim.x * 4) {
@@ -633,6 +751,8 @@ __global__ __launch_bounds__(256) void k_to_f16(const float *__restrict__ src, _
 int col_l0(int ks, int p) { return l0_ref_col(p >> 3, 8 * ks + (p & 7)); }
 int col_chain(int ks, int p) { return 16 * ks + perm_acc(p); }
 int col_l2(int ks, int p) { return ks < 16 ? col_chain(ks, p) : (p < 7 ? 256 + p : -1); }
+int col_l0b(int ks, int p) { return l0_ref_col(p >> 3, 8 * (KS_P0 + ks) + (p & 7)); }
+int col_l0a(int ks, int p) { return l0_ref_col(p >> 3, 8 * ks + (p & 7)); }
 int col_bp(int ks, int p) { return ks < 16 ? col_chain(ks, p) : 256 + 16 * (ks - 16) + p; }
 int col_c0(int ks, int p) { return ks < 16 ? 16 * ks + p : (16 * (ks - 16) + p < 24 ? 256 + 16 * (ks - 16) + p : -1); }
 
@@ -671,6 +791,8 @@ void pack_blob(int ksb, int bpnet_dim, const float *const *w, const float *const
     pack_frags(frag(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, col_c0, 0);
     pack_frags(frag(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, col_chain, 0);
     pack_frags(frag(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, col_chain, 0);
+    pack_frags(frag(OFF_W0B), w[0], 256, 284, T_HID, KS_L0S, col_l0b, layer_tp(0));  // split block1.0, per row
+    pack_frags(frag(OFF_W0A), w[0], 256, 284, T_HID, KS_P0, col_l0a, 0);             // split block1.0, per point
     pack_acc_order(F + F_B0, b[0], T_HID);
     pack_acc_order(F + F_B1, b[1], T_HID);
     pack_acc_order(F + F_B2, b[2], T_HID);
@@ -696,6 +818,27 @@ void pack_blob(int ksb, int bpnet_dim, const float *const *w, const float *const
 extern "C" {
 
 size_t sgn_mlp_packed_bytes(void) { return sgn::mlp::TOTAL_BYTES; }
+
+size_t sgn_mlp_section(int32_t which) {
+    using namespace sgn::mlp;
+    return which == 0 ? OFF_F32 : which == 1 ? OFF_W0B : which == 2 ? TOTAL_BYTES : 0;
+}
+
+size_t sgn_point_proj_bytes(int64_t n_points) { return (size_t)(n_points > 0 ? n_points : 0) * sgn::mlp::PROJ_BYTES_PER_POINT; }
+
+int sgn_point_project(const sgn_point_tables *pt, const void *d_packed, void *d_proj, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    SGN_REQUIRE(pt && d_packed && d_proj, "null argument");
+    SGN_REQUIRE(pt->n_points >= 0 && (pt->n_points == 0 || pt->embedding), "embedding required");
+    if (pt->n_points == 0) return 0;
+    ProjArgs a{pt->embedding, pt->n_points, d_packed, (_Float16 *)d_proj};
+    const int64_t waves = (pt->n_points + 31) / 32;
+    const int64_t wg = (waves + PROJ_TPB / 64 - 1) / (PROJ_TPB / 64);
+    hipLaunchKernelGGL(k_point_proj, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(PROJ_TPB), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
 
 static int mlp_variant_ksb(int32_t bpnet_layers, int32_t bpnet_dim) {
     if (bpnet_layers == 0) return 0;
@@ -731,11 +874,13 @@ int sgn_mlp_pack(const float *const *w, const float *const *b, void *d_packed, s
 
 /* Index maps of the base forward blob over the flat parameter vector (LAYERS order, each
  * layer weight row-major then bias): out[i] = flat index + 1, 0 = zero padding.
- * which 0: fragment part (OFF_F32 / 2 fp16 elements), 1: fp32 section (N_F32). */
+ * which 0: fragment part (OFF_F32 / 2 fp16 elements), 1: fp32 section (N_F32),
+ * 2: split block1.0 sections [OFF_W0B, TOTAL_BYTES) as fp16 elements. */
 int sgn_mlp_pack_index(int32_t which, int32_t *out, int64_t n) {
     using namespace sgn;
     using namespace sgn::mlp;
-    const int64_t want = which == 0 ? (int64_t)(OFF_F32 / 2) : which == 1 ? (int64_t)N_F32 : -1;
+    const int64_t want = which == 0 ? (int64_t)(OFF_F32 / 2) : which == 1 ? (int64_t)N_F32
+                       : which == 2 ? (int64_t)((TOTAL_BYTES - OFF_W0B) / 2) : -1;
     SGN_REQUIRE(out && n == want, "sgn_mlp_pack_index: bad map id or size");
     static const int shape[9][2] = {{256, 284}, {256, 256}, {256, 263}, {256, 256}, {1, 256},
                                     {128, 280}, {128, 128}, {128, 128}, {3, 128}};
@@ -752,10 +897,10 @@ int sgn_mlp_pack_index(int32_t which, int32_t *out, int64_t n) {
         wp[L] = wi[L].data();
         bp[L] = bi[L].data();
     }
-    std::vector<float> e16(OFF_F32 / 2, 0.f), F(N_F32, 0.f);
+    std::vector<float> e16(TOTAL_BYTES / 2, 0.f), F(N_F32, 0.f);
     pack_blob<float>(0, 0, wp.data(), bp.data(), e16.data(), F.data(), nullptr);
-    const std::vector<float> &src = which == 0 ? e16 : F;
-    for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)src[(size_t)i];
+    const float *src = which == 0 ? e16.data() : which == 1 ? F.data() : e16.data() + OFF_W0B / 2;
+    for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)src[i];
     return 0;
 }
 
@@ -766,7 +911,7 @@ size_t sgn_aggregate_workspace_bytes(int64_t S) {
     return (size_t)S * sgn::mlp::HID * sizeof(_Float16);
 }
 
-int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpnet_f16,
+int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpnet_f16, const void *d_point_proj,
                      const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
                      const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
                      void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
@@ -792,6 +937,7 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
     a.blob = P;
     a.blob_bytes = total_bytes_sg(ksb);
     a.bpnet = (const _Float16 *)d_bpnet_f16;
+    a.proj = (const _Float16 *)d_point_proj;
     a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
     ColorArgs c;
     c.counters = q->counters; c.work = q->work; c.samp_ray = q->samp_ray; c.raydir = pt->raydir;
@@ -803,9 +949,17 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
         int64_t wg = (n + WG_SAMPLES - 1) / WG_SAMPLES;  // persistent: one workgroup per CU
         dim3 g1((unsigned)(wg < 256 ? wg : 256));
         if (stages & 1) {
-            if (ksb == 0) hipLaunchKernelGGL(k_agg_rows<0>, g1, dim3(ROWS_TPB), 0, st, a);
-            else if (ksb == KS_HID) hipLaunchKernelGGL(k_agg_rows<KS_HID>, g1, dim3(ROWS_TPB), 0, st, a);
-            else hipLaunchKernelGGL(k_agg_rows<ks_bp(BP_DIM)>, g1, dim3(ROWS_TPB), 0, st, a);
+            constexpr int SP = 256;  // split block1.0 (per-point projection given)
+#if SGN_LAG || defined(SGN_KB16)  // timing builds with a bigger ring: the SG BPNet LDS staging does not fit
+            constexpr int KB = KS_HID;
+#else
+            constexpr int KB = ks_bp(BP_DIM);
+#endif
+            auto kern = d_point_proj ? (ksb == 0 ? k_agg_rows<SP> : ksb == KS_HID ? k_agg_rows<KS_HID + SP>
+                                                                                : k_agg_rows<KB + SP>)
+                                     : (ksb == 0 ? k_agg_rows<0> : ksb == KS_HID ? k_agg_rows<KS_HID>
+                                                                                : k_agg_rows<KB>);
+            hipLaunchKernelGGL(kern, g1, dim3(ROWS_TPB), 0, st, a);
         }
         int64_t wg2 = (n + 32 * (COL_TPB / 64) - 1) / (32 * (COL_TPB / 64));  // 32 samples per wave
         dim3 g2((unsigned)(wg2 < 256 ? wg2 : 256));  // persistent: colour weights loaded once per CU
@@ -860,7 +1014,7 @@ int sgn_bpnet_pack(const float *d_embedding, int64_t n_points, int32_t bpnet_dim
 int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
                   const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
                   void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
-    return sgn_aggregate_sg(0, 0, nullptr, pt, q, S_capacity, K, d_packed, d_out_feat, d_out_blend, d_out_wnorm,
+    return sgn_aggregate_sg(0, 0, nullptr, nullptr, pt, q, S_capacity, K, d_packed, d_out_feat, d_out_blend, d_out_wnorm,
                             d_workspace, workspace_bytes, stages, stream);
 }
 

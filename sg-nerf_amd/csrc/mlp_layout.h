@@ -47,7 +47,19 @@ constexpr size_t F_BA = 1664;                                          // alpha 
 constexpr size_t F_WC3 = 1668;                                         // colour out [3][128]
 constexpr size_t F_BC3 = 2052;                                         // colour out bias [3]
 constexpr size_t N_F32 = 2056;
-constexpr size_t TOTAL_BYTES = OFF_F32 + N_F32 * 4;
+constexpr size_t BASE_BYTES = OFF_F32 + N_F32 * 4;
+
+// Split block1.0 (inference): its inputs [feat 32 | PE(feat) 192 | PE(dists) 60] are
+// per-point for the first 224 channels, so W0a [feat | PE(feat)] + b0 is applied once per
+// point and frame (k_point_proj -> P[point], fp16) and the per-row layer 0 only multiplies
+// W0b by the 30 PE(dists) channels of each lane-half (4 k-steps), its accumulators starting
+// at P[pid].  Same sums, regrouped; the sections are appended after the base blob.
+constexpr int KS_L0S = 4;        // per-row k-steps: local channels 112..143 of each lane-half
+constexpr int KS_P0 = 14;        // per-point k-steps: local channels 0..111 of each lane-half
+constexpr size_t OFF_W0B = BASE_BYTES;                                   // [1 pass][4 ks][8 tiles]
+constexpr size_t OFF_W0A = OFF_W0B + (size_t)T_HID * KS_L0S * FRAG;      // [tile][14 ks]
+constexpr size_t TOTAL_BYTES = OFF_W0A + (size_t)T_HID * KS_P0 * FRAG;
+constexpr size_t PROJ_BYTES_PER_POINT = HID * 2;  // P[point]: 2 lane-halves x 128 fp16, acc order
 
 // SG-NeRF extension (shading_feature_mlp_layer2_bpnet = 1, point_aggregators.py:345-354,
 // :629-636): block2_bpnet.0 = Linear(256 + bpnet_dim -> 256) + LReLU between block1 and

@@ -317,7 +317,7 @@ class PointAggregator:
         wnorm = torch.zeros(S, K, dtype=torch.float32, device=dev)
         L = _lib.lib()
         ws = torch.empty(int(L.sgn_aggregate_workspace_bytes(S)), dtype=torch.uint8, device=dev)
-        _lib.check(L.sgn_aggregate_sg(nl, dim, _lib.ptr(bp), ctypes.byref(pt), ctypes.byref(qo), S, K,
+        _lib.check(L.sgn_aggregate_sg(nl, dim, _lib.ptr(bp), None, ctypes.byref(pt), ctypes.byref(qo), S, K,
                                       _lib.ptr(self.packed), _lib.ptr(feat), None, _lib.ptr(wnorm), _lib.ptr(ws),
                                       ws.numel(), 3, _lib.stream_handle()), "sgn_aggregate_sg")
         # point_aggregators.py:951-953 (forward value of the straight-through clamp)

@@ -69,6 +69,7 @@ class HipRenderer:
         self.querier = LightningFastQuerier(self.device, opts)
         self.set_mlp(mlp_state)
         self._cap = None
+        self._proj = None
 
     def set_mlp(self, mlp_state):
         self.mlp_state = {k: torch.as_tensor(v).detach().to("cpu", torch.float32)
@@ -134,9 +135,16 @@ class HipRenderer:
         if dim and self.points.bpnet16 is None:
             raise ValueError("block2_bpnet with predict_semantic = 1 needs the points' BPNet embedding (set_bpnet)")
         bp = _lib.ptr(self.points.bpnet16) if dim else None
+        # split block1.0: P[point] = W0a [feat | PE(feat)] + b0 for every point, once per frame
+        mark("proj")
+        nproj = int(L.sgn_point_proj_bytes(self.points.n))
+        if self._proj is None or self._proj.numel() < nproj:
+            self._proj = torch.empty(max(nproj, 16), dtype=torch.uint8, device=self.device)
+        _lib.check(L.sgn_point_project(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
+                   "sgn_point_project")
         for stage, name in ((1, "agg_rows"), (2, "agg_color")):
             mark(name)
-            _lib.check(L.sgn_aggregate_sg(nl, dim, bp, ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
+            _lib.check(L.sgn_aggregate_sg(nl, dim, bp, _lib.ptr(self._proj), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
                                           _lib.ptr(self.packed), _lib.ptr(self.feat),
                                           _lib.ptr(self.blend) if want_blend else None,
                                           _lib.ptr(self.wnorm) if want_weights and stage == 1 else None,

@@ -74,24 +74,26 @@ class _Packer:
     def __init__(self, device):
         L = _lib.lib()
         self.total = int(L.sgn_mlp_packed_bytes())
-        self.off_f32 = self.total - 4 * N_F32
+        self.off_f32 = int(L.sgn_mlp_section(0))
+        self.off_split = int(L.sgn_mlp_section(1))
         self.tbytes = int(L.sgn_train_tblob_bytes())
         maps = []
-        for which, n in ((0, self.off_f32 // 2), (1, N_F32)):
+        for which, n in ((0, self.off_f32 // 2), (1, N_F32), (2, (self.total - self.off_split) // 2)):
             a = (ctypes.c_int32 * n)()
             _lib.check(L.sgn_mlp_pack_index(which, a, n), "sgn_mlp_pack_index")
             maps.append(torch.frombuffer(bytearray(a), dtype=torch.int32).long())
         a = (ctypes.c_int32 * (self.tbytes // 2))()
         _lib.check(L.sgn_train_pack_index(a, self.tbytes // 2), "sgn_train_pack_index")
         maps.append(torch.frombuffer(bytearray(a), dtype=torch.int32).long())
-        self.i16, self.i32, self.it = (m.to(device) for m in maps)
+        self.i16, self.i32, self.isp, self.it = (m.to(device) for m in maps)
         self.blob = torch.zeros(self.total, dtype=torch.uint8, device=device)
         self.tblob = torch.zeros(self.tbytes, dtype=torch.uint8, device=device)
 
     def pack(self, flat):
         ext = torch.cat([flat.detach().new_zeros(1), flat.detach()])
         self.blob[:self.off_f32].view(torch.float16).copy_(ext[self.i16])
-        self.blob[self.off_f32:].view(torch.float32).copy_(ext[self.i32])
+        self.blob[self.off_f32:self.off_f32 + 4 * N_F32].view(torch.float32).copy_(ext[self.i32])
+        self.blob[self.off_split:].view(torch.float16).copy_(ext[self.isp])
         self.tblob.view(torch.float16).copy_(ext[self.it])
         return self.blob, self.tblob
 

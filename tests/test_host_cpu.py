@@ -199,7 +199,7 @@ def test_training_pack_index_maps():
     from sgnerf_amd.weights import N_PARAMS
     L = _lib.lib()
     total = int(L.sgn_mlp_packed_bytes())
-    n16, n32 = (total - 4 * 2056) // 2, 2056
+    n16, n32 = int(L.sgn_mlp_section(0)) // 2, 2056
     a16, a32 = (ctypes.c_int32 * n16)(), (ctypes.c_int32 * n32)()
     assert L.sgn_mlp_pack_index(0, a16, n16) == 0 and L.sgn_mlp_pack_index(1, a32, n32) == 0
     m16, m32 = np.frombuffer(a16, np.int32), np.frombuffer(a32, np.int32)
@@ -210,6 +210,13 @@ def test_training_pack_index_maps():
     used32 = np.bincount(m32[m32 > 0], minlength=N_PARAMS + 1)
     assert used32.max() == 1
     assert int((used16 + used32 > 0).sum()) == N_PARAMS  # every parameter packed somewhere
+    # split block1.0 sections: block1.0's weights once each (W0b: PE(dists) columns, W0a: the rest)
+    nsp = (total - int(L.sgn_mlp_section(1))) // 2
+    asp = (ctypes.c_int32 * nsp)()
+    assert L.sgn_mlp_pack_index(2, asp, nsp) == 0
+    msp = np.frombuffer(asp, np.int32)
+    usp = np.bincount(msp[msp > 0], minlength=N_PARAMS + 1)
+    assert usp.max() == 1 and int((usp > 0).sum()) == 256 * 284 and int(usp[1:256 * 284 + 1].sum()) == 256 * 284
     nt = int(L.sgn_train_tblob_bytes()) // 2
     at = (ctypes.c_int32 * nt)()
     assert L.sgn_train_pack_index(at, nt) == 0
