@@ -238,24 +238,40 @@ struct RowIn {
 
 // Gather + pers + dists + weights of this lane's row; raw features for the
 // just-in-time layer-0 encodings, block3's extra channels.
+// Index chain of a row (work item -> sample -> neighbour point, sample -> ray); k_agg_rows
+// loads it one work tile ahead so the record gather below starts from resident indices.
+struct RowIdx {
+    int s, pid, ray;
+    bool sval;
+};
+
+__device__ __forceinline__ RowIdx row_index(const AggArgs &a, int item, int end, int lane) {
+    RowIdx x;
+    x.sval = item < end;
+    x.s = x.sval ? a.work[item] : 0;
+#ifdef SGN_DEBUG_FAST_GATHER  // timing experiment only: no dependent index load, L2-resident records
+    x.pid = x.sval ? ((item * 8 + (lane & 7)) & 1023) : -1;
+#else
+    x.pid = x.sval ? a.pidx[(int64_t)x.s * 8 + (lane & 7)] : -1;
+#endif
+    x.ray = a.samp_ray[x.s];
+    return x;
+}
+
 template <bool FEAT = true>  // FEAT = false: the point features are not needed (split block1.0)
-__device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, int item, int end, int lane,
+__device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, const RowIdx &ix, int lane,
                                             float (&feat)[16], float (&dist)[3], h8 &ext) {
     const int h = lane >> 5, kk = lane & 7;
     RowIn ri;
-    ri.sval = item < end;
-    ri.s = ri.sval ? a.work[item] : 0;
+    ri.sval = ix.sval;
+    ri.s = ix.s;
     const int s = ri.s;
-#ifdef SGN_DEBUG_FAST_GATHER  // timing experiment only: no dependent index load, L2-resident records
-    const int pid = ri.sval ? ((item * 8 + kk) & 1023) : -1;
-#else
-    const int pid = ri.sval ? a.pidx[(int64_t)s * 8 + kk] : -1;
-#endif
+    const int pid = ix.pid;
     const bool m = pid >= 0;
     ri.pid = pid;
     const float lx = a.samp_locw[(int64_t)s * 3 + 0], ly = a.samp_locw[(int64_t)s * 3 + 1],
                 lz = a.samp_locw[(int64_t)s * 3 + 2];
-    const int ray = a.samp_ray[s];
+    const int ray = ix.ray;
     const float vx = a.raydir[(int64_t)ray * 3 + 0], vy = a.raydir[(int64_t)ray * 3 + 1],
                 vz = a.raydir[(int64_t)ray * 3 + 2];
     float px = 0.f, py = 0.f, pz = 0.f, cf = 0.f;
@@ -316,6 +332,12 @@ __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, in
     }
     ext = e;
     return ri;
+}
+
+template <bool FEAT = true>
+__device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, int item, int end, int lane,
+                                            float (&feat)[16], float (&dist)[3], h8 &ext) {
+    return gather_row<FEAT>(a, cam, row_index(a, item, end, lane), lane, feat, dist, ext);
 }
 
 

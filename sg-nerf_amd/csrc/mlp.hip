@@ -257,6 +257,67 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
     });
 }
 
+// Split block1.0, per row: acc[t] = P[pid][t] + W0b[t] PE(dists) (4 k-steps, one stream chunk).
+// P (fp16, [point][tile t][lane-half h][16], so the two lanes of a row read one 64-B run per
+// load) is loaded at entry; tiles go in pairs, k-outer inside a pair, so P of the later tiles
+// lands while the earlier tiles multiply and only the first pair waits on the gather.
+template <int V>
+__device__ __forceinline__ void run_split_l0(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
+                                             const _Float16 *proj, int pid, const float (&feat)[16],
+                                             const float (&dist)[3], f32x16 (&acc)[8]) {
+    static_assert(layer_nch(V, 0) == 1 && layer_ks(V, 0) == 4, "split layer 0 is one chunk of 4 k-steps");
+    const int h = lane >> 5;
+#ifdef SGN_ABLATE_PROJ  // timing experiment only: P of point 0 for every row (wrong results)
+    const h8 *src = (const h8 *)proj;
+#else
+    const h8 *src = (const h8 *)(proj + (int64_t)(pid < 0 ? 0 : pid) * HID);
+#endif
+    h8 pv[16];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        pv[2 * t] = src[(2 * t + h) * 2];
+        pv[2 * t + 1] = src[(2 * t + h) * 2 + 1];
+    }
+    h8 B[4];
+    static_for<4>([&](auto kk) { B[decltype(kk)::value] = l0_step<KS_P0 + decltype(kk)::value>(feat, dist); });
+    chunk_enter<V, chunk_index(V, 0, 0, 0)>(wb, lds, slot, w, lane, lz);
+    const char *sl = lds + slot * SLOT_BYTES;
+    // stream position n -> fragment (k-step k, tile t): pair p = n / 8, k = (n % 8) / 2, t = 2p + n % 2
+    auto fidx = [](int n) { return ((n & 7) >> 1) * 8 + 2 * (n >> 3) + (n & 1); };
+    auto frag = [&](int f) { return *(const h8 *)(sl + f * (int)FRAG + lane * 16); };
+    constexpr int NF = 32, PD = FRAG_PD;
+    h8 fr[PD];
+#pragma unroll
+    for (int f = 0; f < PD; ++f) fr[f] = frag(fidx(f));
+#if SGN_SCHED_PIN
+    __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
+#endif
+    static_for<4>([&](auto pp) {
+        constexpr int P = decltype(pp)::value;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int t = 2 * P + u;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                acc[t][r] = (float)pv[2 * t][r];
+                acc[t][r + 8] = (float)pv[2 * t + 1][r];
+            }
+        }
+        static_for<8>([&](auto nn) {
+            constexpr int N = 8 * P + decltype(nn)::value, K = (N & 7) >> 1, T = 2 * P + (N & 1);
+            const h8 A = fr[N % PD];
+            if constexpr (N + PD < NF) fr[N % PD] = frag(fidx(N + PD));
+            acc[T] = mfma32(A, B[K], acc[T]);
+#if SGN_SCHED_PIN
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#endif
+        });
+    });
+    slot = slot + 1 == NSLOT ? 0 : slot + 1;
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // LeakyReLU + fp16 pack: pass accumulators (bias included) -> next-layer fragments
 template <int TP, int P>
 __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]) {
@@ -324,6 +385,8 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         // followers start LAG chunk intervals late (the leaders add LAG barriers at the end)
         for (int i = 0; i < LAG; ++i) __builtin_amdgcn_s_barrier();
     }
+    // index chain of this wave's rows, one work tile ahead (issued mid-tile, see block1.2)
+    RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG_SAMPLES + w * 4 + q, end, lane);
     for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
         // opaque zero per iteration: keeps LDS parameter reads and weight offsets inside the loop
         int lz = 0;
@@ -333,7 +396,8 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         const int item = base + w * 4 + q;
         float feat[16], dist[3];
         h8 ext;
-        const RowIn ri = gather_row<!SPLIT>(a, cam, item, end, lane, feat, dist, ext);
+        const RowIn ri = gather_row<!SPLIT>(a, cam, nx, lane, feat, dist, ext);
+        const int nitem = item + gridDim.x * WG_SAMPLES;
 
         const int64_t srow0 = (int64_t)(base + w * 4 - a.item0) * 8;  // first saved row of this wave (SAVE)
         // SG: this row's BPNet embedding -> the wave's LDS area as ready-made B fragments
@@ -351,25 +415,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         {   // block1.0: 284 -> 256, one pass over 8 tiles, inputs generated per k-step
             f32x16 acc0[8];
             if constexpr (SPLIT) {
-                // accumulators start at P[pid] (this lane-half's 128 values, acc order); only the
-                // PE(dists) channels (local 112..143) remain for the row
-#ifdef SGN_ABLATE_PROJ  // timing experiment only: P of point 0 for every row (wrong results)
-                const h8 *src = (const h8 *)(a.proj + 128 * h);
-#else
-                const h8 *src = (const h8 *)(a.proj + (int64_t)(ri.pid < 0 ? 0 : ri.pid) * HID + 128 * h);
-#endif
-#pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const h8 p0 = src[2 * t], p1 = src[2 * t + 1];
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        acc0[t][r] = (float)p0[r];
-                        acc0[t][r + 8] = (float)p1[r];
-                    }
-                }
-                run_pass<V, 0, 0, false, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0, [&](auto k) {
-                    return l0_step<KS_P0 + decltype(k)::value>(feat, dist);
-                });
+                run_split_l0<V>(wb, ldsi, slot, w, lane, lz, a.proj, ri.pid, feat, dist, acc0);
             } else {
                 run_pass<V, 0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0, [&](auto k) {
                     const h8 v = l0_step<decltype(k)::value>(feat, dist);
@@ -387,12 +433,19 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         // block1.2: 256 -> 256
         auto inA = [&](auto k) { return actA[decltype(k)::value]; };
         run_pass<V, 1, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
+        // next tile's work entry: lands by the next chunk boundary (every chunk_enter drains vmcnt)
+        const int s_next = nitem < end ? a.work[nitem] : 0;
         chain_out<4, 0>(acc, actB);
         if constexpr (SAVE) {
 #pragma unroll
             for (int s2 = 0; s2 < 8; ++s2) save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
         }
         run_pass<V, 1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
+        // ... and its neighbour / ray indices, two chunk boundaries later
+        nx.sval = nitem < end;
+        nx.s = s_next;
+        nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
+        nx.ray = a.samp_ray[s_next];
         chain_out<4, 1>(acc, actB);
         if constexpr (SAVE) {
 #pragma unroll
@@ -719,13 +772,13 @@ __global__ __launch_bounds__(PROJ_TPB, 1) void k_point_proj(ProjArgs a) {
                 acc[t] = mfma32(*(const h8 *)(W + (t * KS_P0 + KK) * (int)FRAG + lane * 16), x, acc[t]);
         });
         if (ok) {
-            h8 *dst = (h8 *)(a.proj + p * HID + 128 * h);
+            h8 *dst = (h8 *)(a.proj + p * HID);  // [t][h][16]: see run_split_l0
 #pragma unroll
             for (int t = 0; t < 8; ++t)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const int r = 8 * s2;
-                    dst[2 * t + s2] = pack8(acc[t][r], acc[t][r + 1], acc[t][r + 2], acc[t][r + 3], acc[t][r + 4],
+                    dst[(2 * t + h) * 2 + s2] = pack8(acc[t][r], acc[t][r + 1], acc[t][r + 2], acc[t][r + 3], acc[t][r + 4],
                                             acc[t][r + 5], acc[t][r + 6], acc[t][r + 7]);
                 }
         }
