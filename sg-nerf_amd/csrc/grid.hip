@@ -184,6 +184,13 @@ __global__ void k_counts(const int32_t *__restrict__ seg_start, const int32_t *_
     }
 }
 
+__global__ void k_interleave_sc(const int32_t *__restrict__ start, const int32_t *__restrict__ kept, int64_t n_slots,
+                                int2 *__restrict__ sc) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_slots;
+         j += (int64_t)gridDim.x * blockDim.x)
+        sc[j] = make_int2(start[j], kept[j]);
+}
+
 __global__ void k_emit_points(const uint32_t *__restrict__ skey, const int32_t *__restrict__ sval,
                               int64_t n, uint32_t n_slots, const int32_t *__restrict__ seg_start,
                               const int32_t *__restrict__ resv, const int32_t *__restrict__ occ_start,
@@ -312,7 +319,7 @@ static int grid_build_impl(const float *d_points, int64_t n, const sgn_grid_para
         tmp.get(&seg_start, ns) || tmp.get(&seg_end, ns) || tmp.get(&resv, ns * prm->P))
         return -1;
     if (dalloc(&g->occ_start, ns, &g->device_bytes) || dalloc(&g->occ_kept, ns, &g->device_bytes) ||
-        dalloc(&g->occ_routed, ns, &g->device_bytes))
+        dalloc(&g->occ_routed, ns, &g->device_bytes) || dalloc(&g->occ_sc, ns, &g->device_bytes))
         return -1;
     int end_bit = 1;
     while (end_bit < 32 && ((uint64_t)1 << end_bit) <= (uint64_t)ns) ++end_bit;
@@ -342,6 +349,9 @@ static int grid_build_impl(const float *d_points, int64_t n, const sgn_grid_para
     if (tmp.get((char **)&tstore2, (int64_t)tb2)) return -1;
     if (ns > 0) SGN_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tstore2, tb2, g->occ_kept, g->occ_start, (int)ns, st));
     hipLaunchKernelGGL(k_total, dim3(1), dim3(64), 0, st, g->occ_start, g->occ_kept, ns, d_total + 1);
+    if (ns > 0)
+        hipLaunchKernelGGL(k_interleave_sc, dim3(blocks_for(ns)), dim3(TPB), 0, st, g->occ_start, g->occ_kept, ns,
+                           g->occ_sc);
     int64_t n_listed = 0;
     SGN_CHECK_HIP(hipMemcpyAsync(&n_listed, d_total + 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     SGN_CHECK_HIP(hipStreamSynchronize(st));
@@ -381,6 +391,7 @@ int sgn_grid_free(sgn_grid *g) {
     (void)hipFree(g->occ_kept);
     (void)hipFree(g->occ_routed);
     (void)hipFree(g->cell_pts);
+    (void)hipFree(g->occ_sc);
     delete g;
     return 0;
 }

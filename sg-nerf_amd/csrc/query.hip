@@ -17,6 +17,7 @@
 //     one thread per real sample instead of R*SR threads;
 //   * a voxel's candidate points are one contiguous float4 run (grid.hip).
 #include <hipcub/hipcub.hpp>
+#include <utility>
 
 #include "sgn_common.h"
 
@@ -220,6 +221,106 @@ __global__ __launch_bounds__(TPB) void k_knn(GridView g, const float *__restrict
     }
 }
 
+template <class F, int... I>
+__device__ __forceinline__ void unroll_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void unroll(F &&f) {  // f(integral_constant<0..N-1>), fully unrolled
+    unroll_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---- layered kNN, query_size 3 (ScanNet / NeRF-synthetic configs) ----------------
+// Same visit order and replacement rule as k_knn (layer 0 = the centre voxel, layer 1 = the 26
+// others in x, y, z order; worldcoords.py:636-642), restructured for memory-level parallelism:
+// the 27 grid words are loaded together, then the 27 {start, count} pairs together, so a
+// sample waits on two dependent loads instead of 2 x 27 before its candidate runs; inside a
+// voxel two candidates are in flight.  Out-of-grid neighbours read as empty, exactly like the
+// reference's clipped loop bounds (:628-633).
+template <int K, bool SEMANTIC>
+__global__ __launch_bounds__(TPB) void k_knn27(GridView g, const float *__restrict__ campos,
+                                               const float *__restrict__ raydir,
+                                               const float *__restrict__ t_table, int D, int per_ray_t,
+                                               int SR, float r2, int dense_out,
+                                               const int32_t *__restrict__ point_labels,
+                                               const int32_t *__restrict__ ray_labels, uint32_t sec_mod10,
+                                               const int32_t *__restrict__ ray_soff,
+                                               const int32_t *__restrict__ samp_ray,
+                                               const int32_t *__restrict__ samp_d,
+                                               int32_t *__restrict__ counters, float *__restrict__ samp_locw,
+                                               int32_t *__restrict__ samp_nnb, int32_t *__restrict__ pidx_out,
+                                               int32_t *__restrict__ work) {
+    const int64_t S = counters[0];
+    const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < S;
+         s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t r = samp_ray[s];
+        const int32_t d = samp_d[s];
+        const float t = per_ray_t ? t_table[(int64_t)r * D + d] : t_table[d];
+        const float ctr_x = ray_coord(campos[0], raydir[(int64_t)r * 3 + 0], t);
+        const float ctr_y = ray_coord(campos[1], raydir[(int64_t)r * 3 + 1], t);
+        const float ctr_z = ray_coord(campos[2], raydir[(int64_t)r * 3 + 2], t);
+        const int fx = vox_coord(ctr_x, g.shift[0], g.vs[0]);
+        const int fy = vox_coord(ctr_y, g.shift[1], g.vs[1]);
+        const int fz = vox_coord(ctr_z, g.shift[2], g.vs[2]);
+        int center_label = 0;
+        if (SEMANTIC) center_label = ray_labels[r];
+        int2 sc[27];
+        {
+            int32_t wd[27];
+#pragma unroll
+            for (int v = 0; v < 27; ++v) {
+                const int x = fx + v / 9 - 1, y = fy + (v / 3) % 3 - 1, z = fz + v % 3 - 1;
+                const bool in = (unsigned)x < (unsigned)g.dims[0] && (unsigned)y < (unsigned)g.dims[1] &&
+                                (unsigned)z < (unsigned)g.dims[2];
+                wd[v] = in ? g.vox[(int64_t)x * plane + (int64_t)y * g.dims[2] + z] : -1;
+            }
+#pragma unroll
+            for (int v = 0; v < 27; ++v) sc[v] = wd[v] >= 0 ? g.sc[wd[v]] : make_int2(0, 0);
+        }
+        KBuf<K> kb;
+        kb.init();
+        auto consider = [&](const float4 &pt) {
+            const int32_t pid = __float_as_int(pt.w);
+            if (SEMANTIC) {
+                const int lv = point_labels[pid];
+                if (!(center_label == lv || lv == 0 || center_label == 0 || sec_mod10 <= 1u)) return;
+            }
+            const float xv = __fsub_rn(pt.x, ctr_x);
+            const float yv = __fsub_rn(pt.y, ctr_y);
+            const float zv = __fsub_rn(pt.z, ctr_z);
+            const float xyz2 = __fmaf_rn(zv, zv, __fmaf_rn(yv, yv, __fmul_rn(xv, xv)));
+            if (r2 == 0.0f || xyz2 <= r2) kb.push(pid, xyz2);
+        };
+        auto visit = [&](int2 c) {
+            int q = 0;
+            for (; q + 1 < c.y; q += 2) {
+                const float4 p0 = g.pts[c.x + q], p1 = g.pts[c.x + q + 1];
+                consider(p0);
+                consider(p1);
+            }
+            if (q < c.y) consider(g.pts[c.x + q]);
+        };
+        visit(sc[13]);  // layer 0
+        if (kb.kid < K)
+            unroll<27>([&](auto vv) {
+                if constexpr (decltype(vv)::value != 13) visit(sc[decltype(vv)::value]);
+            });
+        const int64_t ob = dense_out ? ((int64_t)r * SR + (s - ray_soff[r])) * K : s * K;
+#pragma unroll
+        for (int i = 0; i < K; ++i) pidx_out[ob + i] = kb.id[i];
+        const int nnb = kb.kid < K ? kb.kid : K;
+        samp_nnb[s] = nnb;
+        samp_locw[s * 3 + 0] = ctr_x;
+        samp_locw[s * 3 + 1] = ctr_y;
+        samp_locw[s * 3 + 2] = ctr_z;
+        if (nnb > 0) {
+            int32_t w = atomicAdd(counters + 1, 1);
+            work[w] = (int32_t)s;
+        }
+    }
+}
+
 size_t scan_temp_bytes(int64_t R) {
     size_t tb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int32_t *)nullptr, (int32_t *)nullptr,
@@ -232,8 +333,10 @@ void launch_knn(dim3 grid, hipStream_t st, bool semantic, bool count, GridView g
                 const float *raydir, const float *t, int D, int per_ray_t, int SR, float r2,
                 int dense, const int32_t *pl, const int32_t *rl, uint32_t sec,
                 const sgn_query_out *o) {
-    auto kern = semantic ? (count ? k_knn<K, true, true> : k_knn<K, true, false>)
-                         : (count ? k_knn<K, false, true> : k_knn<K, false, false>);
+    // k_knn27 (query_size 3, K <= 8: its K = 16 instance would keep the K-buffer in scratch)
+    const bool k27 = g.kernel0 == 3 && K <= 8 && !count;
+    auto kern = semantic ? (count ? k_knn<K, true, true> : k27 ? k_knn27<K, true> : k_knn<K, true, false>)
+                         : (count ? k_knn<K, false, true> : k27 ? k_knn27<K, false> : k_knn<K, false, false>);
     hipLaunchKernelGGL(kern, grid, dim3(TPB), 0, st, g, campos, raydir, t, D, per_ray_t, SR, r2, dense, pl, rl, sec,
                        o->ray_soff, o->samp_ray, o->samp_d, o->counters, o->samp_locw, o->samp_nnb, o->pidx, o->work);
 }

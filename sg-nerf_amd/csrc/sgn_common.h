@@ -61,6 +61,7 @@ struct GridView {
     const int32_t *start;   // [n_slots] first kept point of the slot in pts
     const int32_t *cnt;     // [n_slots] kept points (min(P, routed))
     const float4 *pts;      // [n_listed] {x, y, z, bits(pidx)}
+    const int2 *sc;         // [n_slots] {start, cnt}: one 8-B load per occupied voxel (k_knn27)
     float shift[3];
     float vs[3];
     int dims[3];
@@ -81,10 +82,11 @@ struct sgn_grid {
     int32_t *occ_kept = nullptr;   // [n_slots] min(P, routed)
     int32_t *occ_routed = nullptr; // [n_slots] routed points (reference occ_numpnts)
     float4 *cell_pts = nullptr;    // [n_listed]
+    int2 *occ_sc = nullptr;        // [n_slots] {occ_start, occ_kept} interleaved
     int64_t device_bytes = 0;
     sgn::GridView view() const {
         sgn::GridView g;
-        g.vox = vox; g.start = occ_start; g.cnt = occ_kept; g.pts = cell_pts;
+        g.vox = vox; g.start = occ_start; g.cnt = occ_kept; g.pts = cell_pts; g.sc = occ_sc;
         for (int a = 0; a < 3; ++a) { g.shift[a] = p.shift[a]; g.vs[a] = p.vs[a]; g.dims[a] = p.dims[a]; }
         g.kernel0 = p.kernel[0];
         return g;
