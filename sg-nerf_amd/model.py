@@ -9,9 +9,16 @@ shim `models/hip_points_volumetric_model.py` a maintainer adds to the reference.
 Checkpoints use the reference layout: `{epoch}_net_ray_marching.pth` holding
 `neural_points.{xyz,points_embeding,points_color,points_dir,points_conf}` and
 `aggregator.*` (models/base_model.py:85-119), loaded with
-torch.load(weights_only=True).  Training (optimize_parameters and friends) is
-SURVEY.md §8 row f1 and raises NotImplementedError until it lands.
+torch.load(weights_only=True).
+
+Training (run/train_ft.py:858-1051): optimize_parameters runs one HipTrainer step
+(train_hip.py: HIP query, MFMA aggregator forward/backward, reference losses, two Adam
+groups lr / plr with iter_exponential_decay, DP all-reduce when torch.distributed is up);
+setup_optimizer / clean_optimizer / init_scheduler / prune_points / grow_points follow
+models/mvs_points_volumetric_model.py:47-141,195-270 and neural_points.py:520-572.  The
+trainable tensors are shared with `neural_points`, so test() renders the current state.
 """
+import dataclasses
 import os
 
 import torch
@@ -19,6 +26,8 @@ import torch
 from .opts import HotPathOpts
 from .ray_marching import NeuralPoints, NeuralPointsRayMarching
 from .weights import strip_prefix
+
+LOSS_NAMES = ["total", "ray_masked_coarse_raycolor", "conf_coefficient"]
 
 
 class HipPointsVolumetricModel:
@@ -45,7 +54,8 @@ class HipPointsVolumetricModel:
             extra["fix_occ0"] = int(opt.sgn_fix_occ0)
         if hasattr(opt, "sgn_reservoir_seed"):
             extra["reservoir_seed"] = int(opt.sgn_reservoir_seed)
-        self.opts = HotPathOpts.from_opt(opt, **extra).check_supported()
+        # rendering (test / probe) runs the test-mode depth table; the trainer jitters (is_train)
+        self.opts = HotPathOpts.from_opt(opt, **extra, is_train=0).check_supported()
         self.model_names = ["ray_marching"]
         self.visual_names = ["coarse_raycolor", "ray_mask", "coarse_is_background"]
         self.loss_names = []
@@ -54,15 +64,17 @@ class HipPointsVolumetricModel:
         self.output = {}
 
     def setup(self, opt, train_len=None):
-        if self.is_train:
-            raise NotImplementedError("training on the HIP path is SURVEY.md §8 row f1 (not built yet)")
         resume = getattr(opt, "resume_iter", None)
         if resume is not None and getattr(opt, "resume_dir", None):
             self.load_networks(resume)
+        if self.is_train and self.neural_points is not None:
+            self.setup_optimizer(opt)
+            self.init_scheduler(int(getattr(opt, "resume_step", 0) or 0), opt)
 
     def set_points(self, xyz, points_embeding, points_conf=None, points_dir=None, points_color=None,
                    aggregator_state=None, Rw2c=None, **unused):
-        """neural_points.py:520-572; also takes the aggregator weights when no checkpoint is loaded."""
+        """neural_points.py:520-572; also takes the aggregator weights when no checkpoint is loaded.
+        In training the optimizers are rebuilt over the new points (mvs_points_volumetric_model.py:191-199)."""
         self.neural_points = NeuralPoints(xyz, points_embeding, points_color, points_dir, points_conf, self.device)
         if aggregator_state is not None or self.net_ray_marching is None:
             if aggregator_state is None:
@@ -70,7 +82,91 @@ class HipPointsVolumetricModel:
             self.net_ray_marching = NeuralPointsRayMarching(self.neural_points, aggregator_state, self.opts,
                                                             self.device)
         else:
+            self._sync_weights()
             self.net_ray_marching.neural_points = self.neural_points
+        if self.is_train:
+            self.setup_optimizer(self.opt)
+
+    # -- training (mvs_points_volumetric_model.py:47-141, base_model.py:138-160) -----------------
+    def setup_optimizer(self, opt):
+        """Two Adam groups, aggregator (lr) and neural points (plr), as the reference builds them."""
+        from .train import PointParams
+        from .train_hip import HipTrainer
+        if self.neural_points is None or self.net_ray_marching is None:
+            raise RuntimeError("setup_optimizer: no neural points / aggregator weights yet")
+        self._sync_weights()
+        npnt = self.neural_points
+        params = PointParams(npnt.xyz, npnt.points_embeding, npnt.points_color, npnt.points_dir, npnt.points_conf,
+                             self.device)
+        g = lambda k, d: float(getattr(opt, k, d) if getattr(opt, k, None) is not None else d)  # noqa: E731
+        self.trainer = HipTrainer(params, self.net_ray_marching.renderer.mlp_state,
+                                  dataclasses.replace(self.opts, is_train=1), self.device,
+                                  lr=g("lr", 5e-4), plr=g("plr", 2e-3), lr_decay_exp=g("lr_decay_exp", 0.1),
+                                  lr_decay_iters=g("lr_decay_iters", 1_000_000))
+        # the renderer reads the trained tensors in place (views; the table cache follows their versions)
+        n = params.xyz.shape[0]
+        npnt.points_embeding = params.points_embeding.detach().view(1, n, -1)
+        npnt.points_color = params.points_color.detach().view(1, n, 3)
+        npnt.points_dir = params.points_dir.detach().view(1, n, 3)
+        npnt.points_conf = params.points_conf.detach().view(1, n, 1)
+        self.optimizers = [self.trainer.opt_net, self.trainer.opt_pts]
+        self.schedulers = []
+        self.loss_names = list(LOSS_NAMES)
+
+    def init_scheduler(self, total_steps, opt):
+        """iter_exponential_decay resumed at total_steps (the reference steps its schedulers that often)."""
+        if getattr(self, "trainer", None) is not None:
+            self.trainer.step_count = int(total_steps)
+            self.trainer._set_lr()
+
+    reset_scheduler = init_scheduler
+
+    def clean_optimizer(self):
+        self._sync_weights()
+        self.trainer = None
+        self.optimizers = []
+
+    def clean_scheduler(self):
+        self.schedulers = []
+
+    def clean_optimizer_scheduler(self):
+        self.clean_optimizer()
+        self.clean_scheduler()
+
+    def reset_optimizer(self, opt):
+        self.clean_optimizer()
+        self.setup_optimizer(opt)
+
+    def _sync_weights(self):
+        """Trained aggregator weights -> the renderer's packed blob (once per change)."""
+        tr = getattr(self, "trainer", None)
+        if tr is not None and getattr(self, "_weights_dirty", False):
+            self.net_ray_marching.set_aggregator_state(tr.mlp_state())
+        self._weights_dirty = False
+
+    def prune_points(self, thresh):
+        """neural_points.py:520-543: keep points with conf >= thresh."""
+        self._sync_weights()
+        p = self.neural_points
+        mask = p.points_conf[0, :, 0] >= thresh
+        self.neural_points = NeuralPoints(p.xyz[mask], p.points_embeding[:, mask], p.points_color[:, mask],
+                                          p.points_dir[:, mask], p.points_conf[:, mask], self.device)
+        self.net_ray_marching.neural_points = self.neural_points
+        return int((~mask).sum())
+
+    def grow_points(self, add_xyz, add_embedding, add_color, add_dir, add_conf, add_label=None, **unused):
+        """neural_points.py:546-572: append points (embedding/colour/dir/conf given as [M, C])."""
+        self._sync_weights()
+        p = self.neural_points
+        f = lambda t, c: torch.as_tensor(t).to(self.device, torch.float32).reshape(1, -1, c)  # noqa: E731
+        self.neural_points = NeuralPoints(
+            torch.cat([p.xyz, f(add_xyz, 3)[0]], 0),
+            torch.cat([p.points_embeding, f(add_embedding, p.points_embeding.shape[-1])], 1),
+            torch.cat([p.points_color, f(add_color, 3)], 1), torch.cat([p.points_dir, f(add_dir, 3)], 1),
+            torch.cat([p.points_conf, f(add_conf, 1)], 1), self.device)
+        self.net_ray_marching.neural_points = self.neural_points
+        if self.is_train and getattr(self, "trainer", None) is not None:
+            self.setup_optimizer(self.opt)
 
     # -- per-batch surface -----------------------------------------------------------------
     def set_input(self, input):
@@ -80,6 +176,7 @@ class HipPointsVolumetricModel:
     def forward(self):
         if self.net_ray_marching is None:
             raise RuntimeError("no neural points / weights: call load_networks() or set_points() first")
+        self._sync_weights()
         self.output = self.net_ray_marching.render(self.input)  # == fill_invalid(forward(input))
         for k in self.visual_names:
             setattr(self, k, self.output[k])
@@ -93,22 +190,47 @@ class HipPointsVolumetricModel:
         return {k: getattr(self, k) for k in self.visual_names}
 
     def get_current_losses(self):
-        return {}
+        return {k: getattr(self, "loss_" + k) for k in self.loss_names if hasattr(self, "loss_" + k)}
 
     def eval(self):
         return self
 
     def train(self):
-        raise NotImplementedError("training on the HIP path is SURVEY.md §8 row f1 (not built yet)")
+        return self
 
-    def optimize_parameters(self, *a, **k):
-        raise NotImplementedError("training on the HIP path is SURVEY.md §8 row f1 (not built yet)")
+    def optimize_parameters(self, backward=True, total_steps=0):
+        """neural_points_volumetric_model.py:320-331: forward, losses, backward, both Adam steps."""
+        if getattr(self, "trainer", None) is None:
+            self.setup_optimizer(self.opt)
+        inp = self.input
+        tr = self.trainer
+        near = inp["near"] if "near" in inp else self.opts.near_plane
+        far = inp["far"] if "far" in inp else self.opts.far_plane
+        near, far = (float(torch.as_tensor(x).reshape(-1)[0]) for x in (near, far))
+        gt = inp["gt_image"].reshape(-1, 3).to(self.device, torch.float32)
+        args = (inp["campos"], inp["camrotc2w"], inp["raydir"], near, far, gt)
+        tr.step_count = int(total_steps)
+        if backward:
+            parts, full, ray_mask = tr.step(*args)
+            self._weights_dirty = True
+        else:
+            parts, full, ray_mask = tr.backward(*args)
+        for k, v in parts.items():
+            setattr(self, "loss_" + k, v)
+        self.output = {"coarse_raycolor": full[None], "ray_mask": ray_mask[None].to(torch.int8)}
+        self.coarse_raycolor = self.output["coarse_raycolor"]
+        self.ray_mask = self.output["ray_mask"]
+        return parts
 
-    def update_learning_rate(self, *a, **k):
-        raise NotImplementedError("training on the HIP path is SURVEY.md §8 row f1 (not built yet)")
+    def update_learning_rate(self, opt=None, total_steps=None, **k):
+        """Schedulers are the trainer's iter_exponential_decay, applied at every step."""
+        if getattr(self, "trainer", None) is not None and total_steps is not None:
+            self.init_scheduler(total_steps + 1, opt)
+        return [g["lr"] for o in getattr(self, "optimizers", []) for g in o.param_groups]
 
     # -- checkpoints (models/base_model.py:85-119) -------------------------------------------
     def state_dict(self):
+        self._sync_weights()
         sd = dict(self.neural_points.state_dict())
         for k, v in self.net_ray_marching.renderer.mlp_state.items():
             sd["aggregator." + k] = v

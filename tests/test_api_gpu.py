@@ -157,8 +157,6 @@ def test_model_plugin_checkpoint_roundtrip(tmp_path):
         assert torch.equal(out1[k], out2[k]), k
     vis = m2.get_current_visuals()
     assert set(vis) >= {"coarse_raycolor", "ray_mask"}
-    with pytest.raises(NotImplementedError):
-        m2.optimize_parameters()
 
 
 def test_render_vid_frames_match_single_renders(tmp_path):

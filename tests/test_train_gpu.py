@@ -87,3 +87,77 @@ def test_hip_training_steps_lower_loss():
     print("losses", losses)
     assert losses[-1] < losses[0]
     assert tr.step_count == 8
+
+
+def test_model_plugin_training_surface(tmp_path):
+    """The plugin's training surface as run/train_ft.py drives it (setup / set_points ->
+    optimize_parameters(total_steps) -> get_current_losses -> update_learning_rate, prune /
+    grow with optimizer rebuilds, test() and checkpoints of the trained state): the first
+    step equals a HipTrainer step on the same batch and jitter seed, the loss falls over a
+    fixed batch, and a checkpoint reloaded into an inference model renders identically."""
+    import argparse
+    import dataclasses
+
+    from sgnerf_amd.model import LOSS_NAMES, HipPointsVolumetricModel
+    pc, view, qd, mlp, gt = _setup(seed=3)
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    opt = argparse.Namespace(SR=24, K=8, gpu_ids=[0], is_train=True, checkpoints_dir=str(tmp_path), name="scene",
+                             lr=5e-4, plr=2e-3, lr_decay_exp=0.1, lr_decay_iters=1_000_000, bg_color="white")
+    m = HipPointsVolumetricModel()
+    m.initialize(opt)
+    m.set_points(pc.xyz, pc.embedding, points_conf=pc.conf, points_dir=pc.dir, points_color=pc.color,
+                 aggregator_state=mlp)
+    m.setup(opt)
+    inputs = {"campos": d(view.campos)[None], "raydir": d(view.raydir)[None], "camrotc2w": d(view.camrotc2w)[None],
+              "near": torch.tensor([[[0.1]]]), "far": torch.tensor([[[8.0]]]), "gt_image": gt[None].to(DEV)}
+    m.set_input(inputs)
+    before = m.test()["coarse_raycolor"].clone()
+    # reference step: HipTrainer on the same batch, same jitter seed
+    tr = HipTrainer(PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV), mlp,
+                    dataclasses.replace(O, is_train=1), DEV)
+    torch.manual_seed(11)
+    parts_ref, _, _ = tr.step(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV))
+    torch.manual_seed(11)
+    m.optimize_parameters(total_steps=0)
+    losses = m.get_current_losses()
+    assert set(losses) == set(LOSS_NAMES)
+    assert float(losses["total"]) == float(parts_ref["total"])
+    lrs = m.update_learning_rate(opt=opt, total_steps=0)
+    assert len(lrs) == 2 and abs(lrs[0] - 5e-4 * 0.1 ** (1 / 1_000_000)) < 1e-12
+    hist = [float(losses["total"])]
+    for step in range(1, 6):
+        m.optimize_parameters(total_steps=step)
+        hist.append(float(m.get_current_losses()["total"]))
+    assert hist[-1] < hist[0], hist
+    # test() renders the trained state, and so does a checkpoint reloaded for inference
+    after = m.test()["coarse_raycolor"].clone()
+    assert not torch.equal(after, before)
+    m.save_networks("latest")
+    opt_test = argparse.Namespace(**{**vars(opt), "is_train": False, "resume_dir": str(tmp_path / "scene")})
+    m2 = HipPointsVolumetricModel()
+    m2.initialize(opt_test)
+    m2.load_networks("latest")
+    m2.set_input(inputs)
+    assert torch.equal(m2.test()["coarse_raycolor"], after)
+    # prune (run/train_ft.py:878-884) and grow (:916-917), each followed by a training step
+    n0 = m.neural_points.xyz.shape[0]
+    thresh = float(torch.quantile(m.neural_points.points_conf.reshape(-1), 0.25))
+    m.clean_optimizer()
+    m.clean_scheduler()
+    n_pruned = m.prune_points(thresh)
+    m.setup_optimizer(opt)
+    m.init_scheduler(6, opt)
+    assert n_pruned > 0 and m.neural_points.xyz.shape[0] == n0 - n_pruned
+    assert bool((m.neural_points.points_conf >= thresh).all())
+    m.optimize_parameters(total_steps=6)
+    assert np.isfinite(float(m.get_current_losses()["total"]))
+    k = 64
+    g = torch.Generator().manual_seed(0)
+    add = [torch.rand(k, c, generator=g) for c in (3, 32, 3, 3, 1)]
+    add[0] = add[0] * 0.1 + torch.from_numpy(pc.xyz[:1])
+    m.clean_optimizer_scheduler()
+    m.grow_points(*add, add_label=None)
+    assert m.neural_points.xyz.shape[0] == n0 - n_pruned + k
+    m.optimize_parameters(total_steps=7)
+    assert np.isfinite(float(m.get_current_losses()["total"]))
+    assert m.test()["coarse_raycolor"].shape == before.shape
