@@ -50,8 +50,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--h", type=int, default=800)
     ap.add_argument("--w", type=int, default=800)
-    ap.add_argument("--sr", type=int, default=64)
-    ap.add_argument("--points", type=int, default=1_200_000)
+    ap.add_argument("--sr", type=int, default=None, help="samples per ray (default 64 room, 128 lego)")
+    ap.add_argument("--points", type=int, default=None, help="neural points (default 1.2M room, 300k lego)")
+    ap.add_argument("--scene", choices=["room", "lego"], default="room",
+                    help="room: BASELINE config 2 (headline); lego: config 4 (NeRF-synthetic camera, SR 128)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -122,6 +124,11 @@ def train_main(args, world, rank, dev, dist):
         print(json.dumps(res))
 
 
+def lego_pose_view(i, h, w, n_poses=120):
+    """Config 4: the render_vid-style orbit of load_blender.py:51-56 (theta 0..360, phi -30, r 4)."""
+    return scene.lego_view(360.0 * (i % n_poses) / n_poses, h, w, focal=1111.1111 * w / 800)
+
+
 def pose_view(i, h, w, n_poses=120):
     yaw, pitch = scene.spiral_yaw_pitch(i % n_poses, n_poses)
     return scene.room_view(h, w, yaw=yaw + 15.0, pitch=pitch - 5.0)
@@ -176,6 +183,11 @@ def cpu_baseline(pc, mlp, o, view, stride=4):
 
 def main():
     args = parse()
+    lego = args.scene == "lego"
+    if args.sr is None:
+        args.sr = 128 if lego else 64
+    if args.points is None:
+        args.points = 300_000 if lego else 1_200_000
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -193,7 +205,7 @@ def main():
         return
     sg = dict(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1) if args.sg else {}
     o = HotPathOpts(SR=args.sr, **sg)
-    pc = scene.synth_room(args.points, seed=0)
+    pc = scene.lego_standin(args.points, seed=0) if lego else scene.synth_room(args.points, seed=0)
     if args.sg:
         pc = scene.with_semantics(pc, seed=1, n_classes=20, cell=0.5)
     mlp = init_mlp(0, bias_std=0.01, bpnet_layers=1 if args.sg else 0, bpnet_dim=96 if args.sg else 0)
@@ -201,7 +213,7 @@ def main():
     r = HipRenderer(PointTables.from_cloud(pc, dev), mlp, o, dev)
     n_frames = args.warmup + args.steps
     poses = [(s * world + rank) for s in range(n_frames)]
-    views = [pose_view(p, args.h, args.w) for p in poses]
+    views = [(lego_pose_view if lego else pose_view)(p, args.h, args.w) for p in poses]
     rays = [torch.from_numpy(v.raydir).to(dev) for v in views]
     cams = [(torch.from_numpy(v.campos).to(dev), torch.from_numpy(v.camrotc2w).to(dev)) for v in views]
     R = args.h * args.w
@@ -219,7 +231,7 @@ def main():
         # first neighbour of each ray's first occupied sample (plain query, untimed); seconds fixed
         pl = torch.from_numpy(pc.labels).to(dev)
         for i in range(n_frames):
-            q = r.querier.query_samples(r.points.xyz, cams[i][0], rays[i], 0.1, 8.0)
+            q = r.querier.query_samples(r.points.xyz, cams[i][0], rays[i], views[i].near, views[i].far)
             S = q.n_samples()
             sr = q.samp_ray[:S].long()
             ok = q.samp_nnb[:S] > 0
@@ -232,7 +244,7 @@ def main():
             sem[i] = dict(point_labels=pl, ray_labels=rl.contiguous(), seconds=12)
 
     def frame(i, marks=None, count=False):
-        out = r.render(cams[i][0], cams[i][1], rays[i], 0.1, 8.0, want_opacity=False, marks=marks,
+        out = r.render(cams[i][0], cams[i][1], rays[i], views[i].near, views[i].far, want_opacity=False, marks=marks,
                        count_traffic=count, **sem[i])
         if gathered is not None:
             torch.distributed.all_gather_into_tensor(gathered, out.rgb)
@@ -312,8 +324,11 @@ def main():
         "dtype": "f16",
         "data": "synthetic",
         "config": {
-            "workload": f"synth-room {args.h}x{args.w} rays x SR={args.sr} samples, D=400, K=8, P=26, "
-                        f"{args.points} neural points (BASELINE config 2, 1 frame per rank per step)"
+            "workload": (f"synth-lego stand-in {args.h}x{args.w} rays x SR={args.sr} samples, D=400, K=8, P=26, "
+                         f"{args.points} neural points, Blender camera orbit, near 2 far 6 (BASELINE config 4, "
+                         f"1 frame per rank per step)") if lego else
+                        (f"synth-room {args.h}x{args.w} rays x SR={args.sr} samples, D=400, K=8, P=26, "
+                         f"{args.points} neural points (BASELINE config 2, 1 frame per rank per step)")
                         + (" + SG-NeRF variant: semantic-guided kNN (20 labels), block2_bpnet 352->256" if args.sg else ""),
             "rays_per_frame": R, "SR": args.sr, "K": 8, "D": 400, "points": args.points,
             "parallelism": f"frame-sharded x{world}" + ("" if gathered is None else " + all-gather of frames"),

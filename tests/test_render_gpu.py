@@ -95,6 +95,34 @@ def test_render_matches_oracle_room(SR, seed, yaw, alpha_bias):
     assert int(mask.sum()) > 0.5 * mask.numel()
 
 
+@pytest.mark.parametrize("theta,alpha_bias", [(30.0, 0.0), (200.0, 150.0)])
+def test_render_matches_oracle_lego(theta, alpha_bias):
+    """BASELINE config 4 at test size: the NeRF-synthetic camera model
+    (get_blender_raydir data_utils.py:41-53, pose_spherical load_blender.py:51-56, near 2,
+    far 6) over the lego stand-in cloud, SR = 128: ray masks bit-exact, RGB within 1e-3."""
+    pc = scene.lego_standin(120_000, seed=4)
+    o = HotPathOpts(SR=128)
+    mlp = init_mlp(4, bias_std=0.01)
+    mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + alpha_bias
+    view = scene.lego_view(theta, h=40, w=40, focal=1111.1111 * 40 / 800)
+    pts = dict(xyz=pc.xyz, embedding=pc.embedding, color=pc.color, dir=pc.dir, conf=pc.conf)
+    r, out = _render(pts, mlp, view, o)
+    hy = hyper_for(pc, o)
+    tt = r.querier.depth_table(view.near, view.far, 0)[0].cpu().numpy()
+    q = oq.OracleGrid(pc.xyz, hy, o).query(view.campos, view.raydir, tt)
+    tp = {k: torch.from_numpy(v) for k, v in pts.items()}
+    with torch.no_grad():
+        full, mask, fd, opacity, bg_t = agg_ref.render(tp, mlp, torch.from_numpy(view.campos),
+                                                       torch.from_numpy(view.camrotc2w), torch.from_numpy(view.raydir), q, 128)
+    np.testing.assert_array_equal(out.ray_mask.cpu().numpy().astype(bool), mask.numpy())
+    err = np.abs(out.rgb.cpu().numpy() - full.numpy()).max()
+    ns = out.query.ray_ns[:view.raydir.shape[0]].cpu().numpy()
+    print(f"lego theta={theta}: max |rgb - oracle| = {err:.3e}, valid rays {int(mask.sum())}/{mask.numel()}, "
+          f"max samples/ray {ns.max()}")
+    assert err <= RGB_TOL
+    assert int(mask.sum()) > 0.2 * mask.numel()
+
+
 # ---- SG-NeRF block2_bpnet variant -------------------------------------------------------
 GOLD_SG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_sg.npz")
 
