@@ -17,6 +17,8 @@
 //
 // A fragments (weights) are read straight from global memory (L2-resident, 672 KB);
 // activations never leave registers between layers.
+#include <cstdio>
+#include <cstdlib>
 #include <utility>
 #include <vector>
 
@@ -92,7 +94,17 @@ constexpr int SLOT_BYTES = CHUNK_FRAGS * (int)FRAG;
 #define SGN_LAG 0
 #endif
 constexpr int LAG = SGN_LAG;
-constexpr int N_DMA_WAVES = LAG ? WG_WAVES / 2 : WG_WAVES;
+// SGN_DMA_HALF: only waves 0..3 issue the weight LDS-DMAs (and wait vmcnt(0) at chunk boundaries);
+// waves 4..7 never wait on memory at a boundary, so they issue the workgroup's mid-tile global
+// stores (their own and, through LDS, those of waves 0..3): a store's ~2.5 us acknowledgement
+// otherwise stalls the issuing wave's next boundary.
+#ifndef SGN_STAGGER
+#define SGN_STAGGER 1
+#endif
+#ifndef SGN_DMA_HALF
+#define SGN_DMA_HALF 0
+#endif
+constexpr int N_DMA_WAVES = (LAG || SGN_DMA_HALF) ? WG_WAVES / 2 : WG_WAVES;
 constexpr int PF_N = CHUNK_FRAGS / N_DMA_WAVES;  // LDS-DMA instructions per issuing wave per chunk
 #ifndef SGN_DIST
 #define SGN_DIST 1  // measured: 1 chunk in flight beats 2 by 12 % (k_agg_rows 13.65 -> 11.97 ms, same box)
@@ -100,8 +112,27 @@ constexpr int PF_N = CHUNK_FRAGS / N_DMA_WAVES;  // LDS-DMA instructions per iss
 constexpr int DIST = SGN_DIST;                // chunks in flight ahead of the one being consumed
 constexpr int NSLOT = DIST + LAG + 1;         // ring slots (the DMA target was read LAG+1 chunks ago)
 constexpr int LDS_F32_OFF = NSLOT * SLOT_BYTES;
-constexpr int LDS_BYTES = LDS_F32_OFF + (int)(N_F32 + HID) * 4;  // + block2_bpnet bias (SG)
+constexpr int STAGE_OFF = LDS_F32_OFF + (int)(N_F32 + HID) * 4;  // + block2_bpnet bias (SG)
+constexpr int STAGE_BYTES = N_DMA_WAVES < WG_WAVES ? WG_WAVES * 1024 : 0;  // block3.2 pass-0 features, per wave
+constexpr int LDS_BYTES = STAGE_OFF + STAGE_BYTES;
 static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the waves");
+#ifdef SGN_TIMING
+// Timing build only: every chunk boundary of the first TDBG_BLOCKS workgroups writes the wave's
+// clock (s_memtime) to g_tdbg[(block * 8 + wave) * TDBG_EV + seq]; seq lives in LDS after the
+// kernel's own bytes (non-SG variants).
+constexpr int TDBG_BLOCKS = 4, TDBG_EV = 512;
+__device__ unsigned long long *g_tdbg;
+#endif
+#ifdef SGN_TIMING
+__device__ __forceinline__ void tmark(char *lds, int w, int lane) {
+    int *seq = (int *)(lds + LDS_BYTES) + w;
+    const int n = *seq;
+    if (lane == 0) {
+        if (blockIdx.x < TDBG_BLOCKS && n < TDBG_EV) g_tdbg[((int64_t)blockIdx.x * 8 + w) * TDBG_EV + n] = clock64();
+        *seq = n + 1;
+    }
+}
+#endif
 
 
 // Layers of the row stream: 0 block1.0, 1 block1.2, 2 block3.0, 3 block3.2, 4 block2_bpnet.0
@@ -188,7 +219,7 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
 #endif
     constexpr int younger = (DIST - 1) * PF_N;  // DMAs issued after this chunk's
     static_assert(younger == 0 || younger == 4 || younger == 8, "add the vmcnt immediate");
-    const bool issuer = !LAG || w < N_DMA_WAVES;  // wave-uniform
+    const bool issuer = w < N_DMA_WAVES;  // wave-uniform
     if (issuer) {
         if constexpr (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else if constexpr (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -196,6 +227,9 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+#ifdef SGN_TIMING
+    tmark(lds, w, lane);
+#endif
     if (issuer) {
         int tgt = slot + DIST;
         tgt = tgt >= NSLOT ? tgt - NSLOT : tgt;
@@ -207,9 +241,18 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
 // TRANS: the activations are the A operand and the weights the B operand, so the
 // accumulators hold D^T (lane = output unit, registers = rows) and start at zero (the bias
 // is added in the epilogue, where it is one value per lane).
-template <int KSB, int L, int P, bool TRANS = false, bool PREINIT = false, class InFn>
+struct NoHook {
+    __device__ void operator()() const {}
+};
+
+// post(): called once, right after the boundary of the pass's chunk HOOK_C -- stores of the previous
+// phase issued there are waited for by the NEXT boundary's vmcnt(0), one chunk of MFMAs later,
+// instead of stalling the boundary that follows them directly.
+template <int KSB, int L, int P, bool TRANS = false, bool PREINIT = false, int HOOK_C = 0, class InFn,
+          class PostFn = NoHook>
 __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
-                                         const float *Fl, size_t fb, f32x16 (&acc)[layer_tp(L)], InFn &&in) {
+                                         const float *Fl, size_t fb, f32x16 (&acc)[layer_tp(L)], InFn &&in,
+                                         PostFn &&post = PostFn{}) {
     constexpr int TP = layer_tp(L), KC = layer_kc(L);
     const int h = lane >> 5;
 #pragma unroll
@@ -228,6 +271,7 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
     static_for<layer_nch(KSB, L)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
         chunk_enter<KSB, chunk_index(KSB, L, P, C)>(wb, lds, slot, w, lane, lz);
+        if constexpr (C == HOOK_C) post();
         const char *sl = lds + slot * SLOT_BYTES;
         // weight fragments through a register queue PD deep, so LDS latency overlaps PD MFMAs
         constexpr int NF = chunk_nk(KSB, L, C) * TP, PD = NF < FRAG_PD ? NF : FRAG_PD;
@@ -261,26 +305,33 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
 // P (fp16, [point][tile t][lane-half h][16], so the two lanes of a row read one 64-B run per
 // load) is loaded at entry; tiles go in pairs, k-outer inside a pair, so P of the later tiles
 // lands while the earlier tiles multiply and only the first pair waits on the gather.
-template <int V>
-__device__ __forceinline__ void run_split_l0(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
-                                             const _Float16 *proj, int pid, const float (&feat)[16],
-                                             const float (&dist)[3], f32x16 (&acc)[8]) {
-    static_assert(layer_nch(V, 0) == 1 && layer_ks(V, 0) == 4, "split layer 0 is one chunk of 4 k-steps");
+// P[pid] of this lane's row -> 16 B fragments in accumulator order (layout: run_split_l0)
+__device__ __forceinline__ void load_proj(const _Float16 *proj, int pid, int lane, h8 (&pv)[16]) {
     const int h = lane >> 5;
 #ifdef SGN_ABLATE_PROJ  // timing experiment only: P of point 0 for every row (wrong results)
     const h8 *src = (const h8 *)proj;
 #else
     const h8 *src = (const h8 *)(proj + (int64_t)(pid < 0 ? 0 : pid) * HID);
 #endif
-    h8 pv[16];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         pv[2 * t] = src[(2 * t + h) * 2];
         pv[2 * t + 1] = src[(2 * t + h) * 2 + 1];
     }
+}
+
+// pv: the rows' P, loaded a tile ahead (k_agg_rows issues it during the previous tile's last
+// chunk): the scattered 16-B P reads cost the vector-memory path ~8k cycles per workgroup
+// tile, which then overlap that chunk's MFMAs instead of stalling this tile's first barrier.
+template <int V, class PostFn>
+__device__ __forceinline__ void run_split_l0(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
+                                             const h8 (&pv)[16], const float (&feat)[16],
+                                             const float (&dist)[3], f32x16 (&acc)[8], PostFn &&post) {
+    static_assert(layer_nch(V, 0) == 1 && layer_ks(V, 0) == 4, "split layer 0 is one chunk of 4 k-steps");
     h8 B[4];
     static_for<4>([&](auto kk) { B[decltype(kk)::value] = l0_step<KS_P0 + decltype(kk)::value>(feat, dist); });
     chunk_enter<V, chunk_index(V, 0, 0, 0)>(wb, lds, slot, w, lane, lz);
+    post();
     const char *sl = lds + slot * SLOT_BYTES;
     // stream position n -> fragment (k-step k, tile t): pair p = n / 8, k = (n % 8) / 2, t = 2p + n % 2
     auto fidx = [](int n) { return ((n & 7) >> 1) * 8 + 2 * (n >> 3) + (n & 1); };
@@ -347,7 +398,12 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     constexpr bool SPLIT = vsplit(V);
     static_assert(!(SPLIT && SAVE), "the training save mode runs the unsplit block1.0");
     constexpr int NBP = KSB > KS_HID ? KSB - KS_HID : 0;  // BPNet k-steps (SG, predict_semantic = 1)
+#ifdef SGN_TIMING
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES + WG_WAVES * NBP * (int)FRAG + 64];
+    if (threadIdx.x < 8) ((int *)(lds + LDS_BYTES))[threadIdx.x] = 0;
+#else
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES + WG_WAVES * NBP * (int)FRAG];
+#endif
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, kk = lane & 7, q = (lane & 31) >> 3;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -376,17 +432,50 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     __syncthreads();  // parameters visible before the first tile's bias reads
     int slot = 0;
     // stream prologue: chunks 0..DIST-1 in flight (chunk_enter<n> issues chunk n+DIST)
-    if (!LAG || w < N_DMA_WAVES) {
+    if (w < N_DMA_WAVES) {
         static_for<DIST>([&](auto nn) {
             constexpr int N0 = decltype(nn)::value;
             dma_chunk<V, N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
         });
-    } else {
+    } else if (LAG) {
         // followers start LAG chunk intervals late (the leaders add LAG barriers at the end)
         for (int i = 0; i < LAG; ++i) __builtin_amdgcn_s_barrier();
     }
+#if SGN_STAGGER
+    // Phase stagger: every workgroup runs identical tiles, so without it all CUs gather their
+    // tiles' point records (~150 KB per CU) in the same microseconds and the chip-wide burst
+    // (~38 MB of random reads) sets the tile-start latency.  Eight start phases, one per
+    // group of CUs on every XCD (workgroups go round-robin over the 8 XCDs), ~1/8 tile apart.
+    for (int i = (blockIdx.x >> 3) & 7; i > 0; --i) __builtin_amdgcn_s_sleep(127);
+#endif
     // index chain of this wave's rows, one work tile ahead (issued mid-tile, see block1.2)
     RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG_SAMPLES + w * 4 + q, end, lane);
+    asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));  // waited for here (once), see block3.0
+    h8 pnext[16];  // split block1.0: the next tile's P rows (see run_split_l0)
+    if constexpr (SPLIT) load_proj(a.proj, nx.pid, lane, pnext);
+    // blended features of a block3.2 pass as fp16 pairs (tile tt, half k2) -> pf[tt]; pass 0's
+    // are stored after block3.2 pass 1's first chunk boundary (see run_pass), pass 1's at once
+    // (the next tile's first boundary waits on its gather loads anyway)
+    const int jl = lane & 31;
+    uint32_t pf0[4], pf1[4];
+    // stores as wave ww; drop = true sends them out of the buffer's range (discarded by the
+    // hardware) so the wave-role choice below needs no branch (a branch here costs ~20 spills)
+    auto flush_fs = [&](const uint32_t (&pv)[4], int pbase, int P, int ww, bool drop = false) {
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+            const int it = pbase + ww * 4 + h + 2 * k2;
+            const uint32_t off = (it < end && !drop) ? (uint32_t)((it - a.item0) * HID + jl) * 2 : 0xFFFF0000u;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)  // tile offset in the instruction's immediate
+#ifndef SGN_ABLATE_FS  // timing experiment only: no blended-feature stores (wrong results)
+                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(pv[tt] >> (16 * k2)), fs_rsrc, off,
+                                                      64 * (4 * P + tt), 0);
+#else
+                (void)off;
+#endif
+        }
+    };
+
     for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
         // opaque zero per iteration: keeps LDS parameter reads and weight offsets inside the loop
         int lz = 0;
@@ -396,7 +485,13 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         const int item = base + w * 4 + q;
         float feat[16], dist[3];
         h8 ext;
+#ifdef SGN_TIMING
+        tmark(ldsi, w, lane);  // tile start (after the loop back-edge)
+#endif
         const RowIn ri = gather_row<!SPLIT>(a, cam, nx, lane, feat, dist, ext);
+#ifdef SGN_TIMING
+        tmark(ldsi, w, lane);  // gather issued (and its uses that the compiler placed before this)
+#endif
         const int nitem = item + gridDim.x * WG_SAMPLES;
 
         const int64_t srow0 = (int64_t)(base + w * 4 - a.item0) * 8;  // first saved row of this wave (SAVE)
@@ -415,7 +510,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         {   // block1.0: 284 -> 256, one pass over 8 tiles, inputs generated per k-step
             f32x16 acc0[8];
             if constexpr (SPLIT) {
-                run_split_l0<V>(wb, ldsi, slot, w, lane, lz, a.proj, ri.pid, feat, dist, acc0);
+                run_split_l0<V>(wb, ldsi, slot, w, lane, lz, pnext, feat, dist, acc0, NoHook{});
             } else {
                 run_pass<V, 0, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B0, acc0, [&](auto k) {
                     const h8 v = l0_step<decltype(k)::value>(feat, dist);
@@ -433,19 +528,14 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         // block1.2: 256 -> 256
         auto inA = [&](auto k) { return actA[decltype(k)::value]; };
         run_pass<V, 1, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
-        // next tile's work entry: lands by the next chunk boundary (every chunk_enter drains vmcnt)
-        const int s_next = nitem < end ? a.work[nitem] : 0;
         chain_out<4, 0>(acc, actB);
         if constexpr (SAVE) {
 #pragma unroll
             for (int s2 = 0; s2 < 8; ++s2) save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
         }
         run_pass<V, 1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
-        // ... and its neighbour / ray indices, two chunk boundaries later
-        nx.sval = nitem < end;
-        nx.s = s_next;
-        nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
-        nx.ray = a.samp_ray[s_next];
+        // next tile's index chain: work entry now, neighbour / ray indices one pass later
+        const int s_next = nitem < end ? a.work[nitem] : 0;
         chain_out<4, 1>(acc, actB);
         if constexpr (SAVE) {
 #pragma unroll
@@ -459,6 +549,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
                 if constexpr (K < 16) return actB[K];
                 else return *(const h8 *)(bpl + (K - 16) * (int)FRAG + lane * 16);
             };
+            if (w >= N_DMA_WAVES) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own BPNet LDS-DMA landed
             run_pass<V, 4, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
             chain_out<4, 0>(acc, actA);
             run_pass<V, 4, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
@@ -472,8 +563,17 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
             if constexpr (K < 16) return in3[K]; else return ext;
         };
         run_pass<V, 2, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
+        nx.sval = nitem < end;
+        nx.s = s_next;
+        nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
+        nx.ray = a.samp_ray[s_next];
         chain_out<4, 0>(acc, out3);
         run_pass<V, 2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
+        // the next tile's indices have landed (this pass's boundaries drained vmcnt); hide their
+        // loads from the compiler's wait tracking, which otherwise -- with more VMEM ops in
+        // between than vmcnt can count -- waits for every younger load (the next tile's P) at
+        // the loop head
+        asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
         chain_out<4, 1>(acc, out3);
         if constexpr (SAVE) {
 #pragma unroll
@@ -510,25 +610,44 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
                 for (int g = 0; g < 4; ++g) fg[g] = fg2[g][0] + fg2[g][1];
                 // halves hold rows 4h..4h+3 of each sample: lanes 0-31 <- samples 0 / 2,
                 // lanes 32-63 <- samples 1 / 3 (v_permlane32_swap)
-#pragma unroll
-                for (int k2 = 0; k2 < 2; ++k2) {
-                    float x = fg[2 * k2], y = fg[2 * k2 + 1];
-                    permlane32_swap(x, y);
-                    const float tot = x + y;
-                    const int g = h + 2 * k2, it = base + w * 4 + g;
-                    if (it < end) {
-                        const _Float16 hv16 = (_Float16)tot;
-                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, hv16), fs_rsrc,
-                                                              ((it - a.item0) * HID + 32 * t + j) * 2, 0, 0);
-                    }
-                }
+                float x0 = fg[0], y0 = fg[1], x1 = fg[2], y1 = fg[3];
+                permlane32_swap(x0, y0);
+                permlane32_swap(x1, y1);
+                typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+                const h2 pk = {(_Float16)(x0 + y0), (_Float16)(x1 + y1)};
+                pick<P == 0>(pf0, pf1)[tt] = __builtin_bit_cast(uint32_t, pk);
+                (void)t;
             }
         };
         auto inA3 = [&](auto k) { return out3[decltype(k)::value]; };
         run_pass<V, 3, 0, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 0>{});
-        run_pass<V, 3, 1, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
+        const bool dma_wave = w < N_DMA_WAVES;
+        if constexpr (STAGE_BYTES > 0) {
+            // pass-0 features: non-DMA waves store their own now; DMA waves leave theirs in LDS for
+            // wave w + 4, which stores them after block3.2 pass 1 (two barriers later)
+            uint32_t *stage = (uint32_t *)(ldsi + STAGE_OFF) + w * 256 + lane;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) stage[tt * 64] = pf0[tt];
+            flush_fs(pf0, base, 0, w, dma_wave);
+        } else {
+            flush_fs(pf0, base, 0, w);
+        }
+        run_pass<V, 3, 1, true, false, layer_nch(V, 3) - 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3, [&]() {
+            if constexpr (SPLIT) load_proj(a.proj, nx.pid, lane, pnext);  // next tile's P (its last chunk)
+        });
+        if constexpr (STAGE_BYTES > 0) {
+            const uint32_t *pstage = (const uint32_t *)(ldsi + STAGE_OFF) + (w ^ N_DMA_WAVES) * 256 + lane;
+            uint32_t pv[4];
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) pv[tt] = pstage[tt * 64];
+            flush_fs(pv, base, 0, w ^ N_DMA_WAVES, dma_wave);
+        }
         l3_epilogue(std::integral_constant<int, 1>{});
+        flush_fs(pf1, base, 1, w);
+#ifdef SGN_TIMING
+        tmark(ldsi, w, lane);  // block3.2 pass-1 epilogue done
+#endif
         // alpha: reduce the 16 row partials over the 32 lanes (units) of each half,
         // reduce-scatter style; lane j ends with row index i = 8 b1 + 4 b2 + 2 b3 + b4 (b = bits of j)
         float bq[8];
@@ -1012,7 +1131,24 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
                                                                                 : k_agg_rows<KB + SP>)
                                      : (ksb == 0 ? k_agg_rows<0> : ksb == KS_HID ? k_agg_rows<KS_HID>
                                                                                 : k_agg_rows<KB>);
+#ifdef SGN_TIMING
+            static unsigned long long *tbuf = nullptr;
+            const size_t tn = (size_t)TDBG_BLOCKS * 8 * TDBG_EV;
+            if (!tbuf) {
+                SGN_CHECK_HIP(hipMalloc(&tbuf, tn * 8));
+                SGN_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tdbg), &tbuf, sizeof(tbuf)));
+            }
+            SGN_CHECK_HIP(hipMemsetAsync(tbuf, 0, tn * 8, st));
+#endif
             hipLaunchKernelGGL(kern, g1, dim3(ROWS_TPB), 0, st, a);
+#ifdef SGN_TIMING
+            if (const char *path = getenv("SGN_TDBG")) {
+                std::vector<unsigned long long> h(tn);
+                SGN_CHECK_HIP(hipMemcpyAsync(h.data(), tbuf, tn * 8, hipMemcpyDeviceToHost, st));
+                SGN_CHECK_HIP(hipStreamSynchronize(st));
+                if (FILE *f = fopen(path, "wb")) { fwrite(h.data(), 8, tn, f); fclose(f); }
+            }
+#endif
         }
         int64_t wg2 = (n + 32 * (COL_TPB / 64) - 1) / (32 * (COL_TPB / 64));  // 32 samples per wave
         dim3 g2((unsigned)(wg2 < 256 ? wg2 : 256));  // persistent: colour weights loaded once per CU
