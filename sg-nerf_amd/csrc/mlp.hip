@@ -84,8 +84,15 @@ constexpr int FRAG_PD = SGN_FRAG_PD;  // weight fragments in flight per wave (LD
 // stay in registers, the accumulators of 8 tiles would not fit beside them)
 __host__ __device__ constexpr int layer_tp(int L) { return L == 0 ? 8 : 4; }
 __host__ __device__ constexpr int layer_np(int L) { return 8 / layer_tp(L); }
-__host__ __device__ constexpr int layer_kc(int L) { return CHUNK_FRAGS / layer_tp(L); }
-constexpr int SLOT_BYTES = CHUNK_FRAGS * (int)FRAG;
+// block3.0 (17 k-steps: 256 chained + the colour/dir channels) goes in chunks of 9 + 8 k-steps
+// instead of 8 + 8 + 1: a 4-fragment tail chunk cost a whole boundary (~2.3 k cycles for 4
+// MFMAs per wave, tools/tdbg.py)
+#ifndef SGN_KC2
+#define SGN_KC2 9
+#endif
+__host__ __device__ constexpr int layer_kc(int L) { return L == 2 ? SGN_KC2 : CHUNK_FRAGS / layer_tp(L); }
+constexpr int MAX_CHUNK_FRAGS = SGN_KC2 * 4 > CHUNK_FRAGS ? SGN_KC2 * 4 : CHUNK_FRAGS;
+constexpr int SLOT_BYTES = MAX_CHUNK_FRAGS * (int)FRAG;
 // LAG > 0: waves WG_WAVES/2.. (followers, one per SIMD) run LAG chunks behind waves 0..
 // (leaders, one per SIMD), so on every SIMD one wave's VALU epilogue overlaps the other's
 // MFMAs instead of both stalling the matrix pipe at once.  The leaders issue every LDS-DMA;
@@ -106,6 +113,7 @@ constexpr int LAG = SGN_LAG;
 #endif
 constexpr int N_DMA_WAVES = (LAG || SGN_DMA_HALF) ? WG_WAVES / 2 : WG_WAVES;
 constexpr int PF_N = CHUNK_FRAGS / N_DMA_WAVES;  // LDS-DMA instructions per issuing wave per chunk
+constexpr int PF_MAX = (MAX_CHUNK_FRAGS + N_DMA_WAVES - 1) / N_DMA_WAVES;
 #ifndef SGN_DIST
 #define SGN_DIST 1  // measured: 1 chunk in flight beats 2 by 12 % (k_agg_rows 13.65 -> 11.97 ms, same box)
 #endif
@@ -185,28 +193,35 @@ __host__ __device__ constexpr int chunk_P(int KSB, int n) {
 __host__ __device__ constexpr int chunk_C(int KSB, int n) {
     return (n - chunk_base(KSB, chunk_L(KSB, n))) % pass_chunks(KSB, chunk_L(KSB, n));
 }
-static_assert(CHUNK_FRAGS != 32 || n_chunks(0) == 5 + 2 * (2 + 3 + 2), "base stream");
-static_assert(CHUNK_FRAGS != 32 || (chunk_L(ks_bp(BP_DIM), 9) == 4 && chunk_L(ks_bp(BP_DIM), 8) == 1 &&
-                                     chunk_L(ks_bp(BP_DIM), 15) == 2 && n_chunks(ks_bp(BP_DIM)) == 25),
+static_assert(CHUNK_FRAGS != 32 || SGN_KC2 != 9 || n_chunks(0) == 5 + 2 * (2 + 2 + 2), "base stream");
+static_assert(CHUNK_FRAGS != 32 || SGN_KC2 != 9 ||
+                  (chunk_L(ks_bp(BP_DIM), 9) == 4 && chunk_L(ks_bp(BP_DIM), 8) == 1 &&
+                   chunk_L(ks_bp(BP_DIM), 15) == 2 && n_chunks(ks_bp(BP_DIM)) == 23),
               "SG stream order");
-static_assert(CHUNK_FRAGS != 32 || (n_chunks(256) == 1 + 2 * (2 + 3 + 2) && chunk_L(256, 1) == 1), "split stream");
+static_assert(CHUNK_FRAGS != 32 || SGN_KC2 != 9 || (n_chunks(256) == 1 + 2 * (2 + 2 + 2) && chunk_L(256, 1) == 1),
+              "split stream");
 
 // Issue the LDS-DMA of stream chunk N into LDS slot `dst`: each wave moves fragments
-// w + WG_WAVES*j (1 KiB, lane-linear) with buffer_load ... lds; indices past the chunk
-// re-load its last fragment into unused slot space so every wave issues exactly PF_N
-// DMAs per chunk (the counted vmcnt below relies on it).
+// w + WG_WAVES*j (1 KiB, lane-linear) with buffer_load ... lds.  With DIST > 1 (counted
+// vmcnt below) every chunk is full and each wave issues exactly PF_N DMAs; with DIST = 1 the
+// boundary waits for vmcnt(0) and a wave issues only the fragments of the chunk it owns.
 template <int KSB, int N>
 __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
     constexpr int L = chunk_L(KSB, N), P = chunk_P(KSB, N), C = chunk_C(KSB, N);
     constexpr int nf = chunk_nk(KSB, L, C) * layer_tp(L);
-#pragma unroll
-    for (int j = 0; j < PF_N; ++j) {
-        const int i = w + N_DMA_WAVES * j;
-        const int src = min(i, nf - 1);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            wb.rsrc, (__attribute__((address_space(3))) void *)(dst + i * (int)FRAG), 16,
-            lane * 16, chunk_off(KSB, L, P, C) + (uint32_t)(src * (int)FRAG + lz), 0, 0);
-    }
+    static_assert(DIST == 1 || (nf == CHUNK_FRAGS && MAX_CHUNK_FRAGS == CHUNK_FRAGS), "counted vmcnt needs full chunks");
+    static_for<PF_MAX>([&](auto jj) {
+        constexpr int J = decltype(jj)::value;
+        if constexpr (N_DMA_WAVES * J < nf) {
+            const int i = w + N_DMA_WAVES * J;
+            if (DIST > 1 || N_DMA_WAVES * (J + 1) <= nf || i < nf) {  // wave-uniform
+                const int src = min(i, nf - 1);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    wb.rsrc, (__attribute__((address_space(3))) void *)(dst + i * (int)FRAG), 16,
+                    lane * 16, chunk_off(KSB, L, P, C) + (uint32_t)(src * (int)FRAG + lz), 0, 0);
+            }
+        }
+    });
 }
 
 // Chunk boundary: wait for this wave's DMAs of the chunk about to be read (all but the
