@@ -105,6 +105,9 @@ constexpr int LAG = SGN_LAG;
 // waves 4..7 never wait on memory at a boundary, so they issue the workgroup's mid-tile global
 // stores (their own and, through LDS, those of waves 0..3): a store's ~2.5 us acknowledgement
 // otherwise stalls the issuing wave's next boundary.
+#ifndef SGN_NT_GATHER
+#define SGN_NT_GATHER 0
+#endif
 #ifndef SGN_STAGGER
 #define SGN_STAGGER 1
 #endif
@@ -209,10 +212,11 @@ template <int KSB, int N>
 __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
     constexpr int L = chunk_L(KSB, N), P = chunk_P(KSB, N), C = chunk_C(KSB, N);
     constexpr int nf = chunk_nk(KSB, L, C) * layer_tp(L);
-    static_assert(DIST == 1 || (nf == CHUNK_FRAGS && MAX_CHUNK_FRAGS == CHUNK_FRAGS), "counted vmcnt needs full chunks");
+    static_assert(DIST == 1 || MAX_CHUNK_FRAGS == CHUNK_FRAGS, "counted vmcnt needs equal chunk slots");
     static_for<PF_MAX>([&](auto jj) {
         constexpr int J = decltype(jj)::value;
-        if constexpr (N_DMA_WAVES * J < nf) {
+        // DIST > 1: always PF_N DMAs (short chunks re-load their last fragment into spare slot space)
+        if constexpr (DIST > 1 ? J < PF_N : N_DMA_WAVES * J < nf) {
             const int i = w + N_DMA_WAVES * J;
             if (DIST > 1 || N_DMA_WAVES * (J + 1) <= nf || i < nf) {  // wave-uniform
                 const int src = min(i, nf - 1);
@@ -235,13 +239,17 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slo
     constexpr int younger = (DIST - 1) * PF_N;  // DMAs issued after this chunk's
     static_assert(younger == 0 || younger == 4 || younger == 8, "add the vmcnt immediate");
     const bool issuer = w < N_DMA_WAVES;  // wave-uniform
+#ifndef SGN_ABLATE_VMWAIT  // timing experiment only: boundaries do not wait for the DMA (wrong results)
     if (issuer) {
         if constexpr (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else if constexpr (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     }
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef SGN_ABLATE_BARRIER  // timing experiment only: no workgroup barrier at boundaries (wrong results)
     __builtin_amdgcn_s_barrier();
+#endif
 #ifdef SGN_TIMING
     tmark(lds, w, lane);
 #endif
@@ -330,8 +338,13 @@ __device__ __forceinline__ void load_proj(const _Float16 *proj, int pid, int lan
 #endif
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
+#if SGN_NT_GATHER  // streaming hint: keep the weight stream resident in L2 (timing option)
+        pv[2 * t] = __builtin_nontemporal_load(src + (2 * t + h) * 2);
+        pv[2 * t + 1] = __builtin_nontemporal_load(src + (2 * t + h) * 2 + 1);
+#else
         pv[2 * t] = src[(2 * t + h) * 2];
         pv[2 * t + 1] = src[(2 * t + h) * 2 + 1];
+#endif
     }
 }
 
@@ -484,7 +497,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
             for (int tt = 0; tt < 4; ++tt)  // tile offset in the instruction's immediate
 #ifndef SGN_ABLATE_FS  // timing experiment only: no blended-feature stores (wrong results)
                 __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(pv[tt] >> (16 * k2)), fs_rsrc, off,
-                                                      64 * (4 * P + tt), 0);
+                                                      64 * (4 * P + tt), SGN_NT_GATHER ? 2 : 0);
 #else
                 (void)off;
 #endif
