@@ -155,8 +155,11 @@ class HipTrainer:
         self.points = points
         self.mlp = FlatMLP(mlp_state, self.device)
         self.point_params = [points.points_embeding, points.points_color, points.points_dir, points.points_conf]
-        self.opt_net = torch.optim.Adam([self.mlp.flat], lr=lr, betas=(0.9, 0.999))
-        self.opt_pts = torch.optim.Adam(self.point_params, lr=plr, betas=(0.9, 0.999))
+        # the reference's two Adam groups (mvs_points_volumetric_model.py:100-108); fused: one
+        # kernel per group for the dense 47 M-element point update instead of the foreach chain
+        fused = self.device.type == "cuda"
+        self.opt_net = torch.optim.Adam([self.mlp.flat], lr=lr, betas=(0.9, 0.999), fused=fused)
+        self.opt_pts = torch.optim.Adam(self.point_params, lr=plr, betas=(0.9, 0.999), fused=fused)
         self.base_lr = (lr, plr)
         self.decay = (lr_decay_exp, lr_decay_iters)
         self.step_count = 0
