@@ -480,7 +480,9 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG_SAMPLES + w * 4 + q, end, lane);
     asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));  // waited for here (once), see block3.0
     h8 pnext[16];  // split block1.0: the next tile's P rows (see run_split_l0)
-    if constexpr (SPLIT) load_proj(a.proj, nx.pid, lane, pnext);
+    if constexpr (SPLIT) {
+        if (a.item0 + (int)blockIdx.x * WG_SAMPLES < end) load_proj(a.proj, nx.pid, lane, pnext);  // P[0] exists
+    }
     // blended features of a block3.2 pass as fp16 pairs (tile tt, half k2) -> pf[tt]; pass 0's
     // are stored after block3.2 pass 1's first chunk boundary (see run_pass), pass 1's at once
     // (the next tile's first boundary waits on its gather loads anyway)

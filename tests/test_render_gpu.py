@@ -194,3 +194,19 @@ def test_render_sg_semantic_matches_oracle_room():
     print(f"SG room: max |rgb - oracle| = {err:.3e}, valid rays {int(mask.sum())}/{mask.numel()}")
     assert err <= RGB_TOL
     assert int(mask.sum()) > 0.5 * mask.numel()
+
+
+def test_render_without_hits_is_background():
+    """No ray reaches an occupied voxel (camera outside the room, looking away): zero work items
+    reach the aggregator kernels; every ray is invalid and gets the white background
+    (fill_invalid, neural_points_volumetric_model.py:158-195)."""
+    pc = small_room(50_000, seed=2)
+    o = HotPathOpts(SR=24)
+    mlp = init_mlp(2, bias_std=0.01)
+    view = make_view(16, 24, yaw=45.0, pitch=0.0, campos=(9.0, 9.0, 1.5))
+    pts = dict(xyz=pc.xyz, embedding=pc.embedding, color=pc.color, dir=pc.dir, conf=pc.conf)
+    r, out = _render(pts, mlp, view, o)
+    assert int(out.query.counters[1]) == 0
+    assert not bool(out.ray_mask.any())
+    assert torch.equal(out.rgb.cpu(), torch.ones(view.raydir.shape[0], 3))
+    assert torch.equal(out.bg_transmission.cpu(), torch.ones(view.raydir.shape[0]))
