@@ -125,7 +125,14 @@ constexpr int NSLOT = DIST + LAG + 1;         // ring slots (the DMA target was 
 constexpr int LDS_F32_OFF = NSLOT * SLOT_BYTES;
 constexpr int STAGE_OFF = LDS_F32_OFF + (int)(N_F32 + HID) * 4;  // + block2_bpnet bias (SG)
 constexpr int STAGE_BYTES = N_DMA_WAVES < WG_WAVES ? WG_WAVES * 1024 : 0;  // block3.2 pass-0 features, per wave
-constexpr int LDS_BYTES = STAGE_OFF + STAGE_BYTES;
+// SGN_FS_WIDE: blended features leave through a per-wave LDS transpose as one 16-B store per
+// lane and block3.2 pass (full 128-B lines) instead of eight 2-B scattered stores
+#ifndef SGN_FS_WIDE
+#define SGN_FS_WIDE 1
+#endif
+constexpr int FSW_OFF = STAGE_OFF + STAGE_BYTES;
+constexpr int FSW_BYTES = SGN_FS_WIDE ? WG_WAVES * 1024 : 0;  // [wave][4 samples][128 units] fp16
+constexpr int LDS_BYTES = FSW_OFF + FSW_BYTES;
 static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the waves");
 #ifdef SGN_TIMING
 // Timing build only: every chunk boundary of the first TDBG_BLOCKS workgroups writes the wave's
@@ -491,6 +498,24 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     // stores as wave ww; drop = true sends them out of the buffer's range (discarded by the
     // hardware) so the wave-role choice below needs no branch (a branch here costs ~20 spills)
     auto flush_fs = [&](const uint32_t (&pv)[4], int pbase, int P, int ww, bool drop = false) {
+#if SGN_FS_WIDE
+        if constexpr (FSW_BYTES > 0) {
+            // lane (unit jl, half h) holds samples h (lo) and h + 2 (hi) of tiles 4P + tt
+            _Float16 *st = (_Float16 *)(lds + FSW_OFF + w * 1024);
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                st[h * 128 + 32 * tt + jl] = __builtin_bit_cast(_Float16, (unsigned short)(pv[tt] & 0xffff));
+                st[(h + 2) * 128 + 32 * tt + jl] = __builtin_bit_cast(_Float16, (unsigned short)(pv[tt] >> 16));
+            }
+            // lane L: sample L >> 4, units 8 (L & 15) .. +7 of the pass (16 B)
+            const u32x4 v = *(const u32x4 *)(st + (lane >> 4) * 128 + 8 * (lane & 15));
+            const int it = pbase + ww * 4 + (lane >> 4);
+            const uint32_t off = (it < end && !drop) ? (uint32_t)((it - a.item0) * HID + 128 * P + 8 * (lane & 15)) * 2
+                                                     : 0xFFFF0000u;
+            __builtin_amdgcn_raw_buffer_store_b128(v, fs_rsrc, off, 0, 0);
+            return;
+        }
+#endif
 #pragma unroll
         for (int k2 = 0; k2 < 2; ++k2) {
             const int it = pbase + ww * 4 + h + 2 * k2;
