@@ -76,17 +76,43 @@ __device__ __forceinline__ h8 plain_frag(const f32x16 &acc, int s2) {
     return pack8(acc[r], acc[r + 1], acc[r + 2], acc[r + 3], acc[r + 4], acc[r + 5], acc[r + 6], acc[r + 7]);
 }
 
-// acc[t] = sum_ks T[t0 + t][ks] * in[ks] for NT row tiles of a transposed layer
-template <int NT>
-__device__ __forceinline__ void tmul(const WBlob &tb, size_t off, int t0, const h8 (&in)[16], f32x16 (&acc)[NT],
-                                     int lane) {
+// The workgroup's 4 waves (one per SIMD) run the same sequence of products on different rows:
+// each product's NT x 16 weight fragments are staged once per workgroup in LDS by LDS-DMA
+// (16 per wave in flight together) and read from there by all four waves.  Read one by one
+// from L2 instead, the MFMAs waited on every fragment (one wave per SIMD, ~5 % MFMA rate).
+constexpr int BWD_TPB = 256;
+constexpr int BWD_LDS = 8 * 16 * (int)FRAG;  // the largest product: 8 tiles x 16 k-steps
+
+// acc[t] (+)= sum_ks W(t, ks) * in[ks]; offf(ks, t) = the fragment's byte offset in the blob
+template <int NT, class OffFn>
+__device__ __forceinline__ void lds_mul(char *lds, const WBlob &wb, OffFn &&offf, const h8 (&in)[16],
+                                        f32x16 (&acc)[NT], int w, int lane) {
+    constexpr int NF = 16 * NT;
+    static_assert(NF * (int)FRAG <= BWD_LDS && NF % 4 == 0, "staging area");
+    __syncthreads();  // the previous product's readers are done with the area
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    for (int i = 0; i < NF / 4; ++i) {
+        const int n = w + 4 * i;  // fragment n = (ks, t) = (n / NT, n % NT)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)(lds + n * (int)FRAG),
+                                                 16, lane * 16, offf(n / NT, n % NT), 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-            acc[t] = mfma32(tb.frag((uint32_t)(off + ((size_t)(t0 + t) * 16 + ks) * FRAG), lane), in[ks], acc[t]);
+            acc[t] = mfma32(*(const h8 *)(lds + (ks * NT + t) * (int)FRAG + lane * 16), in[ks], acc[t]);
+}
+
+// acc[t] = sum_ks T[t0 + t][ks] * in[ks] for NT row tiles of a transposed layer
+template <int NT>
+__device__ __forceinline__ void tmul(char *lds, const WBlob &tb, size_t off, int t0, const h8 (&in)[16],
+                                     f32x16 (&acc)[NT], int w, int lane) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    lds_mul<NT>(lds, tb, [&](int ks, int t) { return (uint32_t)(off + ((size_t)(t0 + t) * 16 + ks) * FRAG); }, in,
+                acc, w, lane);
 }
 
 // d feat[c] contribution of layer-0 local channel C (mlp_layout.h l0 order): PE(feat) chain rule
@@ -103,7 +129,8 @@ __device__ __forceinline__ void l0_backward(float d, const float (&feat)[16], fl
     // C >= 112: PE(dists) -> point xyz / sample positions (not trained)
 }
 
-__global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
+__global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
+    __shared__ __attribute__((aligned(16))) char lds[BWD_LDS];
     const AggArgs &a = b.a;
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, j = lane & 31, q = j >> 3;
@@ -114,7 +141,10 @@ __global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
     const float *F = (const float *)((const char *)a.blob + OFF_F32);
     const float scale = *b.scale, inv = 1.f / scale;
     const int end = b.n_items;
-    for (int base = (blockIdx.x * 4 + w) * 4; base < end; base += gridDim.x * 16) {
+    // trip count uniform over the workgroup (its waves meet at the staging barriers); rows past
+    // the end are masked (ok = false)
+    for (int bbase = blockIdx.x * 16; bbase < end; bbase += gridDim.x * 16) {
+        const int base = bbase + w * 4;
         const int item = base + q;
         const int64_t row0 = (int64_t)base * 8;
         float feat[16], dist[3];
@@ -130,12 +160,9 @@ __global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
             for (int s = 0; s < 16; ++s) x3[s] = load_frag(b.sh3, 256, row0, s, lane, ok);
 #pragma unroll
             for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
-#pragma unroll
-            for (int ks = 0; ks < 16; ++ks)
-#pragma unroll
-                for (int t = 0; t < 8; ++t)
-                    acc[t] = mfma32(wb.frag((uint32_t)(OFF_W3 + ((size_t)((t >> 2) * KS_HID + ks) * 4 + (t & 3)) * FRAG), lane),
-                                    x3[ks], acc[t]);
+            lds_mul<8>(lds, wb, [&](int ks, int t) {
+                return (uint32_t)(OFF_W3 + ((size_t)((t >> 2) * KS_HID + ks) * 4 + (t & 3)) * FRAG);
+            }, x3, acc, w, lane);
         }
         // ---- pass 1: h4, alpha logit, <h4, d f_s> ------------------------------------------
         const float *dfs = b.dfs + (int64_t)it * HID;
@@ -195,7 +222,7 @@ __global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            tmul<4>(tb, OFF_T3, 4 * p, dl, ac, lane);
+            tmul<4>(lds, tb, OFF_T3, 4 * p, dl, ac, w, lane);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -209,7 +236,7 @@ __global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            tmul<4>(tb, OFF_T2, 4 * p, dn, ac, lane);
+            tmul<4>(lds, tb, OFF_T2, 4 * p, dn, ac, w, lane);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -221,7 +248,7 @@ __global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
         }
         {
             f32x16 ae[1];
-            tmul<1>(tb, OFF_T2, 8, dn, ae, lane);
+            tmul<1>(lds, tb, OFF_T2, 8, dn, ae, w, lane);
             // tile 8 = inputs 256..262: half 0 regs 0..3 -> colour 0..2, (dir - v)_0;
             // half 1 regs 0..2 -> (dir - v)_1, (dir - v)_2, <dir, v>   (:639-652)
             const float o0 = __shfl_xor(ae[0][0], 32), o1 = __shfl_xor(ae[0][1], 32), o2 = __shfl_xor(ae[0][2], 32);
@@ -243,7 +270,7 @@ __global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            tmul<4>(tb, OFF_T1, 4 * p, dl, ac, lane);
+            tmul<4>(lds, tb, OFF_T1, 4 * p, dl, ac, w, lane);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -260,7 +287,7 @@ __global__ __launch_bounds__(256) void k_agg_bwd(BwdArgs b) {
         static_for<3>([&](auto pp) {
             constexpr int P = decltype(pp)::value;
             f32x16 ac[3];
-            tmul<3>(tb, OFF_T0, 3 * P, dn, ac, lane);
+            tmul<3>(lds, tb, OFF_T0, 3 * P, dn, ac, w, lane);
             static_for<3>([&](auto ttc) {
                 constexpr int T = 3 * P + decltype(ttc)::value;
                 static_for<16>([&](auto rr) {
@@ -406,7 +433,7 @@ int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, i
     b.n_items = n_items;
     const int64_t waves = ((int64_t)n_items + 3) / 4;
     const int64_t blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL(k_agg_bwd, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, as_stream(stream), b);
+    hipLaunchKernelGGL(k_agg_bwd, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(BWD_TPB), 0, as_stream(stream), b);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }
