@@ -4,19 +4,22 @@
 // PointAggregator.forward + viewmlp (point_aggregators.py:868-959, :561-786) for the
 // ScanNet configuration (agg_dist_pers 20, linear kernel, agg_intrp_order 2).
 //
-// k_agg_rows: one wave owns a 32-row column tile = 4 shading samples x K=8 neighbours.
+// k_point_proj: P[point] = W0a [feat | PE(feat)] + b0, block1.0's 224 per-point input
+//   channels, once per frame (fp16, accumulator order).
+// k_agg_rows: one wave owns a 32-row column tile = 4 shading samples x K=8 neighbours; a
+//   512-thread workgroup (8 waves) = one 256-row work tile.
 //   prologue : gather point records by index, pers transform, 6-d dists, inverse-distance
 //              weights normalised over the 8 rows of a sample (lane butterflies), conf
-//              clamp, positional encodings -> 18 fp16 B fragments (288 channels)
-//   block1   : 284->256->256, block3: 263->256->256 as MFMA chains; each layer's
-//              accumulator tile is converted in place into the next layer's B operand
-//              (no LDS, no transpose; the k permutation lives in the packed weights)
-//   alpha    : per-row dot with the alpha weights, softplus(x - 1), K-blend
-//   K-blend  : f_s = sum_k w_k h_k over the sample's 8 lanes -> fp16 feature rows
+//              clamp; accumulators start at P[pid]
+//   block1   : PE(dists) -> 256 (layer 0, 4 k-steps) -> 256; block3: 263 -> 256 -> 256, as
+//              MFMA chains; each layer's accumulator tile is converted in place into the
+//              next layer's B operand (the k permutation lives in the packed weights)
+//   block3.2 : transposed, so the alpha dot product and the K-blend f_s = sum_k w_k h_k are
+//              per-lane FMAs; f_s leaves as fp16 rows for k_color
 // k_color: one wave = 32 samples: [f_s | PE(viewdir)] -> 128 -> 128 -> 128 -> 3, sigmoid.
 //
-// A fragments (weights) are read straight from global memory (L2-resident, 672 KB);
-// activations never leave registers between layers.
+// Weights stream through an LDS ring filled by LDS-DMA and shared by the workgroup's 8 waves;
+// activations never leave registers between layers.  DESIGN.md section 3.1 has the timing.
 #include <cstdio>
 #include <cstdlib>
 #include <utility>
@@ -27,44 +30,16 @@
 namespace sgn {
 namespace {
 
-// One dense layer, output chained into the next layer's B fragments (16 k-steps).
-// KS k-steps of input: the first min(KS, NIN) from `in`, step NIN (if KS > NIN) from `extra`.
-template <int KS, int NIN, int NT = 8>
-__device__ __forceinline__ void layer_chain(const WBlob &wb, uint32_t woff, uint32_t boff,
-                                            const h8 (&in)[NIN], h8 extra, h8 (&out)[2 * NT], int lane) {
-    const int h = lane >> 5;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        f32x16 acc = {};
-#pragma unroll
-        for (int k = 0; k < KS; ++k)
-            acc = mfma32(wb.frag(woff + (uint32_t)(t * KS + k) * FRAG, lane), k < NIN ? in[k] : extra, acc);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            f32x4 b = wb.acc4(boff, t, g, h);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                int r = 4 * g + c;
-                out[2 * t + (r >> 3)][r & 7] = (_Float16)lrelu(acc[r] + b[c]);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep one tile's weight loads in flight, not eight
-    }
-}
-
-
-constexpr int AGG_TPB = 256;
 
 // ---- workgroup-shared weight stream, k-outer ---------------------------------------
 // A workgroup = 8 waves (2 per SIMD) = 32 samples x 8 neighbours = 256 rows, 32 rows per
-// wave.  Per layer each wave keeps all eight 32x32 output tiles as MFMA accumulators
-// (128 AGPRs) and walks the input k-steps in order, so an input fragment dies as soon as it
-// has been multiplied into the 8 tiles: layer-0 fragments are even generated just in time
-// (positional encodings computed per k-step, interleaved with the MFMAs of the partner wave).
-// Block1/block3 weights (536 fragments of 1 KiB, packed [layer][k-step][tile]) stream through
-// a 2-slot LDS ring, one chunk = KC k-steps x 8 tiles; chunk c+1 is fetched global->VGPR at
-// the start of chunk c and stored to the other slot after chunk c's MFMAs (one barrier per
-// chunk).  Every fragment fetched into LDS feeds 8 waves.
+// wave.  Per layer pass each wave keeps its output tiles as MFMA accumulators and walks the
+// input k-steps in order, so an input fragment dies as soon as it has been multiplied into the
+// pass's tiles (layer-0 fragments are generated just in time from the row's dists).  The
+// weights (424 fragments of 1 KiB per tile, packed [layer][pass][k-step][tile]) stream through
+// a 2-slot LDS ring of chunks of up to 36 fragments filled by LDS-DMA (buffer_load ... lds),
+// the next chunk in flight while the current one is read; one barrier per chunk.  Every
+// fragment fetched into LDS feeds 8 waves.
 constexpr int ROWS_TPB = 512;
 constexpr int WG_WAVES = ROWS_TPB / 64;
 constexpr int WG_SAMPLES = WG_WAVES * 4;  // 32
