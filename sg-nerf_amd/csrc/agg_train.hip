@@ -76,43 +76,68 @@ __device__ __forceinline__ h8 plain_frag(const f32x16 &acc, int s2) {
     return pack8(acc[r], acc[r + 1], acc[r + 2], acc[r + 3], acc[r + 4], acc[r + 5], acc[r + 6], acc[r + 7]);
 }
 
-// The workgroup's 4 waves (one per SIMD) run the same sequence of products on different rows:
-// each product's NT x 16 weight fragments are staged once per workgroup in LDS by LDS-DMA
-// (16 per wave in flight together) and read from there by all four waves.  Read one by one
-// from L2 instead, the MFMAs waited on every fragment (one wave per SIMD, ~5 % MFMA rate).
+// The workgroup's 4 waves (one per SIMD) run the same sequence of 12 weight products per tile
+// on different rows.  Each product's NT x 16 fragments are staged once per workgroup in LDS by
+// LDS-DMA and read there by all four waves; two slots, the next product's DMA in flight while
+// the current one multiplies (the forward's ring protocol: boundary = vmcnt(0) + barrier, then
+// issue the next DMA into the slot read one product ago).  Read one by one from L2 instead, the
+// MFMAs waited on every fragment (one wave per SIMD, ~5 % of the MFMA rate).
 constexpr int BWD_TPB = 256;
-constexpr int BWD_LDS = 8 * 16 * (int)FRAG;  // the largest product: 8 tiles x 16 k-steps
+constexpr int BWD_SLOT = 4 * 16 * (int)FRAG;  // the largest product: 4 tiles x 16 k-steps
+constexpr int BWD_LDS = 2 * BWD_SLOT;
+constexpr int N_PROD = 12;
 
-// acc[t] (+)= sum_ks W(t, ks) * in[ks]; offf(ks, t) = the fragment's byte offset in the blob
-template <int NT, class OffFn>
-__device__ __forceinline__ void lds_mul(char *lds, const WBlob &wb, OffFn &&offf, const h8 (&in)[16],
-                                        f32x16 (&acc)[NT], int w, int lane) {
-    constexpr int NF = 16 * NT;
-    static_assert(NF * (int)FRAG <= BWD_LDS && NF % 4 == 0, "staging area");
-    __syncthreads();  // the previous product's readers are done with the area
+// product I: 0-1 block3.2 recompute (W3, tiles 4I..), 2-3 W3^T, 4-5 W2^T, 6 W2^T's input tile 8
+// (colour / dir channels), 7-8 W1^T, 9-11 W0^T (3 row tiles each)
+__host__ __device__ constexpr int prod_nt(int I) { return I == 6 ? 1 : I >= 9 ? 3 : 4; }
+__host__ __device__ constexpr uint32_t prod_off(int I, int ks, int t) {
+    return (uint32_t)(I < 2 ? OFF_W3 + ((size_t)(I * KS_HID + ks) * 4 + t) * FRAG
+                    : I < 4 ? OFF_T3 + ((size_t)((I - 2) * 4 + t) * 16 + ks) * FRAG
+                    : I < 6 ? OFF_T2 + ((size_t)((I - 4) * 4 + t) * 16 + ks) * FRAG
+                    : I == 6 ? OFF_T2 + ((size_t)(8 + t) * 16 + ks) * FRAG
+                    : I < 9 ? OFF_T1 + ((size_t)((I - 7) * 4 + t) * 16 + ks) * FRAG
+                            : OFF_T0 + ((size_t)((I - 9) * 3 + t) * 16 + ks) * FRAG);
+}
+
+template <int I>
+__device__ __forceinline__ void prod_dma(char *lds, const WBlob &wb, const WBlob &tb, int w, int lane) {
+    constexpr int NT = prod_nt(I), NF = 16 * NT;
+    static_assert(NF % 4 == 0 && NF * (int)FRAG <= BWD_SLOT, "staging slot");
+    const WBlob &src = I < 2 ? wb : tb;
+    char *dst = lds + (I & 1) * BWD_SLOT;
 #pragma unroll
     for (int i = 0; i < NF / 4; ++i) {
         const int n = w + 4 * i;  // fragment n = (ks, t) = (n / NT, n % NT)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)(lds + n * (int)FRAG),
-                                                 16, lane * 16, offf(n / NT, n % NT), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rsrc, (__attribute__((address_space(3))) void *)(dst + n * (int)FRAG),
+                                                 16, lane * 16, prod_off(I, n / NT, n % NT), 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+}
+
+// acc[t] (+)= sum_ks W_I(t, ks) * in[ks]; `more`: the workgroup has another tile (product 11's
+// successor is the next tile's product 0)
+template <int I, int NT>
+__device__ __forceinline__ void prod_mul(char *lds, const WBlob &wb, const WBlob &tb, const h8 (&in)[16],
+                                         f32x16 (&acc)[NT], int w, int lane, bool more) {
+    static_assert(NT == prod_nt(I), "product width");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of product I landed
+    __syncthreads();  // everyone's, and everyone is done with product I - 1's slot
+    if constexpr (I + 1 < N_PROD) prod_dma<I + 1>(lds, wb, tb, w, lane);
+    else if (more) prod_dma<0>(lds, wb, tb, w, lane);
+    const char *sl = lds + (I & 1) * BWD_SLOT;
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-            acc[t] = mfma32(*(const h8 *)(lds + (ks * NT + t) * (int)FRAG + lane * 16), in[ks], acc[t]);
+            acc[t] = mfma32(*(const h8 *)(sl + (ks * NT + t) * (int)FRAG + lane * 16), in[ks], acc[t]);
 }
 
-// acc[t] = sum_ks T[t0 + t][ks] * in[ks] for NT row tiles of a transposed layer
-template <int NT>
-__device__ __forceinline__ void tmul(char *lds, const WBlob &tb, size_t off, int t0, const h8 (&in)[16],
-                                     f32x16 (&acc)[NT], int w, int lane) {
+// acc[t] = sum_ks T[t0 + t][ks] * in[ks] for the NT row tiles of transposed product I
+template <int I, int NT>
+__device__ __forceinline__ void tmul(char *lds, const WBlob &wb, const WBlob &tb, const h8 (&in)[16],
+                                     f32x16 (&acc)[NT], int w, int lane, bool more) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
-    lds_mul<NT>(lds, tb, [&](int ks, int t) { return (uint32_t)(off + ((size_t)(t0 + t) * 16 + ks) * FRAG); }, in,
-                acc, w, lane);
+    prod_mul<I, NT>(lds, wb, tb, in, acc, w, lane, more);
 }
 
 // d feat[c] contribution of layer-0 local channel C (mlp_layout.h l0 order): PE(feat) chain rule
@@ -141,10 +166,12 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
     const float *F = (const float *)((const char *)a.blob + OFF_F32);
     const float scale = *b.scale, inv = 1.f / scale;
     const int end = b.n_items;
+    if (blockIdx.x * 16 < end) prod_dma<0>(lds, wb, tb, w, lane);  // stream prologue
     // trip count uniform over the workgroup (its waves meet at the staging barriers); rows past
     // the end are masked (ok = false)
     for (int bbase = blockIdx.x * 16; bbase < end; bbase += gridDim.x * 16) {
         const int base = bbase + w * 4;
+        const bool more = bbase + (int)gridDim.x * 16 < end;
         const int item = base + q;
         const int64_t row0 = (int64_t)base * 8;
         float feat[16], dist[3];
@@ -160,9 +187,8 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
             for (int s = 0; s < 16; ++s) x3[s] = load_frag(b.sh3, 256, row0, s, lane, ok);
 #pragma unroll
             for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
-            lds_mul<8>(lds, wb, [&](int ks, int t) {
-                return (uint32_t)(OFF_W3 + ((size_t)((t >> 2) * KS_HID + ks) * 4 + (t & 3)) * FRAG);
-            }, x3, acc, w, lane);
+            prod_mul<0, 4>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[0], w, lane, more);
+            prod_mul<1, 4>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[4], w, lane, more);
         }
         // ---- pass 1: h4, alpha logit, <h4, d f_s> ------------------------------------------
         const float *dfs = b.dfs + (int64_t)it * HID;
@@ -222,7 +248,8 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            tmul<4>(lds, tb, OFF_T3, 4 * p, dl, ac, w, lane);
+            if (p == 0) tmul<2, 4>(lds, wb, tb, dl, ac, w, lane, more);
+            else tmul<3, 4>(lds, wb, tb, dl, ac, w, lane, more);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -236,7 +263,8 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            tmul<4>(lds, tb, OFF_T2, 4 * p, dn, ac, w, lane);
+            if (p == 0) tmul<4, 4>(lds, wb, tb, dn, ac, w, lane, more);
+            else tmul<5, 4>(lds, wb, tb, dn, ac, w, lane, more);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -248,7 +276,7 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
         }
         {
             f32x16 ae[1];
-            tmul<1>(lds, tb, OFF_T2, 8, dn, ae, w, lane);
+            tmul<6, 1>(lds, wb, tb, dn, ae, w, lane, more);
             // tile 8 = inputs 256..262: half 0 regs 0..3 -> colour 0..2, (dir - v)_0;
             // half 1 regs 0..2 -> (dir - v)_1, (dir - v)_2, <dir, v>   (:639-652)
             const float o0 = __shfl_xor(ae[0][0], 32), o1 = __shfl_xor(ae[0][1], 32), o2 = __shfl_xor(ae[0][2], 32);
@@ -270,7 +298,8 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            tmul<4>(lds, tb, OFF_T1, 4 * p, dl, ac, w, lane);
+            if (p == 0) tmul<7, 4>(lds, wb, tb, dl, ac, w, lane, more);
+            else tmul<8, 4>(lds, wb, tb, dl, ac, w, lane, more);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -287,7 +316,7 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
         static_for<3>([&](auto pp) {
             constexpr int P = decltype(pp)::value;
             f32x16 ac[3];
-            tmul<3>(lds, tb, OFF_T0, 3 * P, dn, ac, w, lane);
+            tmul<9 + P, 3>(lds, wb, tb, dn, ac, w, lane, more);
             static_for<3>([&](auto ttc) {
                 constexpr int T = 3 * P + decltype(ttc)::value;
                 static_for<16>([&](auto rr) {
