@@ -41,15 +41,42 @@ __global__ __launch_bounds__(TPB) void k_march(GridView g, const float *__restri
     const float dx = raydir[r * 3 + 0], dy = raydir[r * 3 + 1], dz = raydir[r * 3 + 2];
     const float *tt = PER_RAY_T ? t_table + r * (int64_t)D : t_table;
     const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+    // Candidates whose t lies outside the ray's span through the grid box, widened by two voxels
+    // on every side (far beyond the rounding of ray_coord / vox_coord), are out of the grid and
+    // never flagged: the scan covers [d_lo, d_hi] only (the test inside is unchanged).
+    float t_in = -INFINITY, t_out = INFINITY;
+    {
+        const float c[3] = {cx, cy, cz}, dv[3] = {dx, dy, dz};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float lo = g.shift[a] - 2.f * g.vs[a], hi = g.shift[a] + (g.dims[a] + 2.f) * g.vs[a];
+            if (dv[a] != 0.f) {
+                const float t1 = (lo - c[a]) / dv[a], t2 = (hi - c[a]) / dv[a];
+                t_in = fmaxf(t_in, fminf(t1, t2));
+                t_out = fminf(t_out, fmaxf(t1, t2));
+            } else if (c[a] < lo || c[a] > hi) {
+                t_out = -INFINITY;
+            }
+        }
+    }
+    int d_lo = 0, d_hi = -1;  // first / last candidate index with t in [t_in, t_out]
+    if (t_in <= t_out) {
+        int lo = 0, hi = D;  // first d with tt[d] >= t_in
+        while (lo < hi) { const int m = (lo + hi) >> 1; if (tt[m] < t_in) lo = m + 1; else hi = m; }
+        d_lo = lo;
+        lo = d_lo; hi = D;  // first d with tt[d] > t_out
+        while (lo < hi) { const int m = (lo + hi) >> 1; if (tt[m] <= t_out) lo = m + 1; else hi = m; }
+        d_hi = lo - 1;
+    }
     int cnt = 0;
     constexpr int U = 8;  // candidates whose grid words are in flight together
-    for (int d0 = 0; d0 < D && cnt < SR; d0 += U) {
+    for (int d0 = d_lo; d0 <= d_hi && cnt < SR; d0 += U) {
         int32_t word[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             int d = d0 + u;
             word[u] = VOX_UNFLAGGED;
-            if (d < D) {
+            if (d <= d_hi) {
                 float t = tt[d];
                 int ix = vox_coord(ray_coord(cx, dx, t), g.shift[0], g.vs[0]);
                 int iy = vox_coord(ray_coord(cy, dy, t), g.shift[1], g.vs[1]);
