@@ -192,10 +192,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # SGN_BENCH_BACKEND=gloo: rehearsal of the N > 1 code path with every rank on the visible
+    # GPU(s) (RCCL refuses two ranks on one device); frames are then not all-gathered
+    backend = os.environ.get("SGN_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
+        args.no_gather = True
     if dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.train:
