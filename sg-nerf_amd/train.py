@@ -236,6 +236,47 @@ def _allreduce_buckets(grads, bucket_elems):
             off += g.numel()
 
 
+def _allreduce_point_rows(grads):
+    """Mean over ranks of per-point gradients ([N, C_i] tensors sharing N), sparse: each rank
+    sends only the rows its rays touched (a 4096-ray batch touches ~50 k of 1.2 M points), as
+    an all-gather of (index, row) padded to the largest count; every rank then adds the ranks'
+    slices in rank order (indices unique within a slice), so all ranks get identical sums.
+    Equals the dense all-reduce up to the order of the fp32 additions; ~30x fewer bytes than
+    all-reducing 187 MB of point gradients per step over xGMI at 8 GPUs."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    n = dist.get_world_size()
+    dev = grads[0].device
+    touched = torch.zeros(grads[0].shape[0], dtype=torch.bool, device=dev)
+    for g in grads:
+        touched |= (g != 0).reshape(g.shape[0], -1).any(1)
+    idx = torch.nonzero(touched).reshape(-1)
+    cnt = torch.tensor([idx.numel()], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(cnt) for _ in range(n)]
+    dist.all_gather(counts, cnt)
+    counts = [int(c.item()) for c in counts]
+    m = max(max(counts), 1)
+    widths = [g.reshape(g.shape[0], -1).shape[1] for g in grads]
+    rows = torch.zeros(m, sum(widths), dtype=grads[0].dtype, device=dev)
+    if idx.numel():
+        rows[:idx.numel()] = torch.cat([g.reshape(g.shape[0], -1)[idx] for g in grads], 1)
+    pidx = torch.zeros(m, dtype=torch.int64, device=dev)
+    pidx[:idx.numel()] = idx
+    all_idx = torch.empty(n * m, dtype=torch.int64, device=dev)
+    all_rows = torch.empty(n * m, rows.shape[1], dtype=rows.dtype, device=dev)
+    dist.all_gather_into_tensor(all_idx, pidx)
+    dist.all_gather_into_tensor(all_rows, rows)
+    acc = torch.zeros(grads[0].shape[0], rows.shape[1], dtype=rows.dtype, device=dev)
+    for r in range(n):
+        c = counts[r]
+        acc.index_add_(0, all_idx[r * m:r * m + c], all_rows[r * m:r * m + c])
+    acc /= n
+    off = 0
+    for g, wdt in zip(grads, widths):
+        g.copy_(acc[:, off:off + wdt].reshape(g.shape))
+        off += wdt
+
+
 class Trainer:
     """One data-parallel training step per call (config 5: 4096 random rays per rank)."""
 
@@ -287,7 +328,8 @@ class Trainer:
         for p in self.point_params + self.net_params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-        self.allreduce_grads(self.net_params + self.point_params)
+        self.allreduce_grads(self.net_params)
+        _allreduce_point_rows([p.grad for p in self.point_params])
         parts["total"] = total.detach()
         return parts, full.detach(), ray_mask
 

@@ -32,7 +32,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .opts import HotPathOpts
-from .train import PointParams, _pe, composite_losses, _allreduce_buckets
+from .train import PointParams, _pe, composite_losses, _allreduce_buckets, _allreduce_point_rows
 from .weights import LAYERS, strip_prefix
 
 N_F32 = 2056
@@ -283,7 +283,8 @@ class HipTrainer:
                                                 ctypes.byref(deltas), ctypes.byref(grads), st),
                        "sgn_aggregate_backward")
             self._weight_grads(n * 8, scale)
-        self.allreduce_grads([self.mlp.flat] + self.point_params)
+        self.allreduce_grads([self.mlp.flat])
+        _allreduce_point_rows([p.grad for p in self.point_params])
         parts["total"] = total.detach()
         return parts, full.detach(), ray_mask
 

@@ -144,7 +144,7 @@ def test_data_parallel_step_world2():
         assert np.array_equal(res[0][0][k], res[1][0][k]), k
     assert np.array_equal(res[0][1], res[1][1])
     # == one Adam step on the mean of the two ranks' gradients, computed here
-    grads = []
+    grads, pgrads = [], []
     for rank in range(world):
         pc, view, qd, mlp, gt = _setup(seed=2, yaw=30.0 + 40.0 * rank)
         points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, "cpu")
@@ -153,6 +153,15 @@ def test_data_parallel_step_world2():
                                     torch.from_numpy(view.raydir), gt, O)
         total.backward()
         grads.append([p.grad.clone() for p in net.parameters()])
+        pgrads.append(points.points_embeding.grad.clone())
+    # the point embedding: one Adam step (plr 2e-3) on the mean of the ranks' dense gradients
+    # (the trainer all-gathers only the touched rows)
+    pts0 = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, "cpu")
+    popt = torch.optim.Adam([pts0.points_embeding], lr=2e-3, betas=(0.9, 0.999))
+    pts0.points_embeding.grad = (pgrads[0] + pgrads[1]) / 2
+    popt.step()
+    assert int((pgrads[0] != 0).any(1).sum()) < pgrads[0].shape[0] // 2  # the exchange really is sparse
+    torch.testing.assert_close(torch.from_numpy(res[0][1]), pts0.points_embeding.detach(), rtol=1e-5, atol=1e-7)
     net0 = ViewMLP(init_mlp(2, bias_std=0.01) | {"alpha_branch.0.bias": init_mlp(2, bias_std=0.01)["alpha_branch.0.bias"] + 100.0})
     opt = torch.optim.Adam(net0.parameters(), lr=5e-4, betas=(0.9, 0.999))
     for p, g0, g1 in zip(net0.parameters(), *grads):
