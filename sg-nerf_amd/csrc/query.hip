@@ -295,16 +295,30 @@ __global__ __launch_bounds__(TPB) void k_knn27(GridView g, const float *__restri
         if (SEMANTIC) center_label = ray_labels[r];
         int2 sc[27];
         {
+            // Branch-free: every load reads a valid address (clamped voxel, slot 0 for empty ones;
+            // a sample exists only if some voxel is flagged, so slot 0 exists) and a select drops
+            // it.  With `cond ? load : default` the compiler issued each {start, count} load in
+            // its own branch and waited for it before the next: 27 serial memory latencies.
             int32_t wd[27];
 #pragma unroll
             for (int v = 0; v < 27; ++v) {
                 const int x = fx + v / 9 - 1, y = fy + (v / 3) % 3 - 1, z = fz + v % 3 - 1;
                 const bool in = (unsigned)x < (unsigned)g.dims[0] && (unsigned)y < (unsigned)g.dims[1] &&
                                 (unsigned)z < (unsigned)g.dims[2];
-                wd[v] = in ? g.vox[(int64_t)x * plane + (int64_t)y * g.dims[2] + z] : -1;
+                const int xc = min(max(x, 0), g.dims[0] - 1), yc = min(max(y, 0), g.dims[1] - 1),
+                          zc = min(max(z, 0), g.dims[2] - 1);
+                const int32_t word = g.vox[(int64_t)xc * plane + (int64_t)yc * g.dims[2] + zc];
+                wd[v] = in ? word : -1;
             }
+            int2 e[27];
 #pragma unroll
-            for (int v = 0; v < 27; ++v) sc[v] = wd[v] >= 0 ? g.sc[wd[v]] : make_int2(0, 0);
+            for (int v = 0; v < 27; ++v) e[v] = g.sc[wd[v] >= 0 ? wd[v] : 0];
+            // the empty asm consumes every result unconditionally, so the optimizer cannot sink a
+            // load into a branch on its own condition (which serialised them)
+#pragma unroll
+            for (int v = 0; v < 27; ++v) asm volatile("" : "+v"(e[v].x), "+v"(e[v].y));
+#pragma unroll
+            for (int v = 0; v < 27; ++v) sc[v] = wd[v] >= 0 ? e[v] : make_int2(0, 0);
         }
         KBuf<K> kb;
         kb.init();
