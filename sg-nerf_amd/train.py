@@ -182,10 +182,10 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     ray_mask = vd.any(-1)
     full = torch.where(ray_mask[:, None], color, bgv.expand(R, 3))
     # ray_masked_coarse_raycolor (weight 1), ray_miss / coarse (weight 0): each adds 1e-6 (:560)
-    if bool(ray_mask.any()):
-        l_col = F.mse_loss(full[ray_mask], gt[ray_mask])
-    else:
-        l_col = torch.zeros((), device=dev)
+    # = F.mse_loss(full[ray_mask], gt[ray_mask]) (0 when no ray is valid), as a masked mean so
+    # the step issues no host sync (boolean indexing would wait for the mask's count)
+    wm = ray_mask.to(full.dtype)[:, None]
+    l_col = torch.sum((full - gt) ** 2 * wm) / torch.clamp(wm.sum() * 3, min=1.0)
     # zero_one_loss on conf_coefficient (:607-614) over the reference's dense [R'', SR, K] tensor
     # (point_aggregators.py:951-958): every (slot, k) of a valid ray, where empty slots and masked
     # neighbours read conf at the clamped index 0 (neural_points.py:956-967)

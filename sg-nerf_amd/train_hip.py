@@ -24,6 +24,7 @@ MLP weights live in ONE flat fp32 parameter (LAYERS order), so the MFMA blobs ar
 the device every step by index gathers (sgn_mlp_pack_index / sgn_train_pack_index).
 """
 import ctypes
+import os
 import math
 
 import torch
@@ -108,16 +109,21 @@ _MM_OUT_DTYPE = None
 _BMM_OUT_DTYPE = None
 
 
-def _gemm_rows_f32(a, b, split):
-    """a^T b over the row dimension: a [rows, M], b [rows, N] fp16 -> [M, N] fp32, as `split`
-    batched GEMMs over row chunks (split-K: a 256 x 288 output alone would occupy ~20 of the
-    256 CUs) summed in fp32.  rows % split == 0."""
+def _gemm_rows_f32(a, b, chunk):
+    """a^T b over the row dimension: a [rows, M], b [rows, N] fp16 -> [M, N] fp32.
+
+    Split-K: the rows go in `chunk`-row batches through one batched GEMM (a 256 x 288 output
+    alone is ~8 macro tiles, so a plain GEMM would occupy a handful of the 256 CUs and walk
+    K = 160 k rows serially), the batch partials summed in fp32; a ragged tail of rows takes
+    one more plain GEMM.  Every row is summed exactly once whatever `chunk` is."""
     global _BMM_OUT_DTYPE
     rows = a.shape[0]
-    if split <= 1:
+    nb = rows // chunk if chunk > 0 else 0
+    if nb <= 1:
         return _mm_f32(a.t(), b)
-    at = a.view(split, rows // split, a.shape[1]).transpose(1, 2)
-    bt = b.view(split, rows // split, b.shape[1])
+    body = nb * chunk
+    at = a[:body].view(nb, chunk, a.shape[1]).transpose(1, 2)
+    bt = b[:body].view(nb, chunk, b.shape[1])
     if _BMM_OUT_DTYPE is None:
         try:
             torch.bmm(at[:1, :1, :1], bt[:1, :1, :1], out_dtype=torch.float32)
@@ -125,8 +131,16 @@ def _gemm_rows_f32(a, b, split):
         except Exception:
             _BMM_OUT_DTYPE = False
     if _BMM_OUT_DTYPE:
-        return torch.bmm(at, bt, out_dtype=torch.float32).sum(0)
-    return torch.bmm(at.float(), bt.float()).sum(0)
+        G = torch.bmm(at, bt, out_dtype=torch.float32).sum(0)
+    else:
+        G = torch.bmm(at.float(), bt.float()).sum(0)
+    if body < rows:
+        G += _mm_f32(a[body:].t(), b[body:])
+    return G
+
+
+# rows per split-K batch of the weight-gradient GEMMs (SGN_DW_CHUNK overrides, for sweeps)
+DW_CHUNK = int(os.environ.get("SGN_DW_CHUNK", "512"))
 
 
 def _mm_f32(a, b):
@@ -295,9 +309,7 @@ class HipTrainer:
         inv = 1.0 / scale
         iu = self.inv_chain
         rp = ((rows + 255) // 256) * 256      # rows padded to a multiple of 256 (buffers are)
-        split = max(1, min(32, rp // 8192))
-        while split > 1 and rp % split:
-            split //= 2
+        chunk = max(DW_CHUNK, -(-rp // 512))  # at most 512 batches
         for t in self.d + [self.x0, self.h1, self.h2, self.h3]:
             t[rows:rp].zero_()                 # stale tails must not reach the GEMM (0 * NaN)
         for name, d, x, ix in (("block3.2", self.d[3], self.h3, self.inv_chain),
@@ -305,7 +317,7 @@ class HipTrainer:
                                ("block1.2", self.d[1], self.h1, self.inv_chain),
                                ("block1.0", self.d[0], self.x0, self.inv_x0)):
             dr, xr = d[:rp], x[:rp]
-            G = _gemm_rows_f32(dr, xr, split)    # [256 stored][C stored]
+            G = _gemm_rows_f32(dr, xr, chunk)    # [256 stored][C stored]
             m.w(name, g).add_(G[iu][:, ix] * inv)        # gathers, no scatter
             m.b(name, g).add_(torch.sum(dr, 0, dtype=torch.float32)[iu] * inv)
         # alpha branch: dWa = dza^T h4, dba = sum dza
