@@ -240,6 +240,22 @@ int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, i
                            const sgn_agg_deltas *deltas, const sgn_point_grads *grads,
                            sgn_stream_t stream);
 
+/* ---- training: point-parameter Adam and bias-gradient column sums ------------------
+ * Replaces torch.optim.Adam.step for the neural-point group (the reference's optimizer,
+ * models/mvs_points_volumetric_model.py:100-108; no weight decay, no amsgrad): one fp32
+ * tensor of n elements, state tensors exp_avg / exp_avg_sq as torch keeps them, step =
+ * the 1-based step count after this update.  zero_grad != 0 also clears d_grad (the next
+ * step's zero_grad).  All buffers 16-B aligned. */
+int sgn_adam_step(float *d_param, float *d_grad, float *d_exp_avg, float *d_exp_avg_sq, int64_t n, double lr,
+                  double beta1, double beta2, double eps, int64_t step, int32_t zero_grad, sgn_stream_t stream);
+/* d_out[i][c] = sum over r < rows of d_x[i][r][c] (fp16 in, fp32 out, deterministic order),
+ * for count <= 8 matrices [rows][256] (the bias gradients db = sum of the deltas,
+ * torch.sum(d, 0) in the reference's autograd of nn.Linear).  d_x: host array of device
+ * pointers; d_ws: sgn_colsum_workspace_bytes(count) of device scratch. */
+size_t sgn_colsum_workspace_bytes(int32_t count);
+int sgn_colsum_f16(int32_t count, const void *const *d_x, int64_t rows, int32_t cols, float *d_ws, float *d_out,
+                   sgn_stream_t stream);
+
 /* ---- composite --------------------------------------------------------- */
 
 typedef struct {

@@ -96,6 +96,10 @@ SIGNATURES = {
     "sgn_aggregate_backward": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp,
                                        ctypes.POINTER(AggSaved), c_vp, c_vp, c_vp, ctypes.POINTER(AggDeltas),
                                        ctypes.POINTER(PointGrads), c_vp]),
+    "sgn_adam_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                               ctypes.c_double, c_i64, c_i32, c_vp]),
+    "sgn_colsum_workspace_bytes": (c_sz, [c_i32]),
+    "sgn_colsum_f16": (c_i32, [c_i32, ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp, c_vp]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
                               c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_ray_march_dense": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.POINTER(c_f32), c_vp, c_vp, c_vp,

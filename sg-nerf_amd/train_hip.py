@@ -157,6 +157,39 @@ def _mm_f32(a, b):
     return a.float() @ b.float()
 
 
+class PointAdam(torch.optim.Adam):
+    """torch.optim.Adam (same param_groups, state keys and state_dict) whose step is one
+    sgn_adam_step launch per tensor; with zero_grad the launch also clears the gradient, so
+    the next step skips its fill pass.  For the dense ~47 M-element point group."""
+
+    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, zero_grad=True):
+        super().__init__(params, lr=lr, betas=betas, eps=eps)
+        self.zero_grad_in_step = zero_grad
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        assert closure is None
+        L = _lib.lib()
+        st = _lib.stream_handle()
+        for g in self.param_groups:
+            b1, b2 = g["betas"]
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                assert p.is_contiguous() and p.grad.is_contiguous() and p.dtype == torch.float32
+                s = self.state[p]
+                if not s:
+                    s["step"] = torch.tensor(0.0)
+                    s["exp_avg"] = torch.zeros_like(p)
+                    s["exp_avg_sq"] = torch.zeros_like(p)
+                s["step"] += 1
+                _lib.check(L.sgn_adam_step(_lib.ptr(p), _lib.ptr(p.grad), _lib.ptr(s["exp_avg"]),
+                                           _lib.ptr(s["exp_avg_sq"]), p.numel(), float(g["lr"]), b1, b2,
+                                           float(g["eps"]), int(s["step"].item()), int(self.zero_grad_in_step),
+                                           st), "sgn_adam_step")
+        return None
+
+
 class HipTrainer:
     """One data-parallel training step per call on the HIP path (config 5)."""
 
@@ -173,7 +206,11 @@ class HipTrainer:
         # kernel per group for the dense 47 M-element point update instead of the foreach chain
         fused = self.device.type == "cuda"
         self.opt_net = torch.optim.Adam([self.mlp.flat], lr=lr, betas=(0.9, 0.999), fused=fused)
-        self.opt_pts = torch.optim.Adam(self.point_params, lr=plr, betas=(0.9, 0.999), fused=fused)
+        if fused:
+            self.opt_pts = PointAdam(self.point_params, lr=plr, betas=(0.9, 0.999))
+        else:
+            self.opt_pts = torch.optim.Adam(self.point_params, lr=plr, betas=(0.9, 0.999))
+        self._pts_grad_clean = False  # PointAdam left the point gradients zeroed
         self.base_lr = (lr, plr)
         self.decay = (lr_decay_exp, lr_decay_iters)
         self.step_count = 0
@@ -266,8 +303,9 @@ class HipTrainer:
         for p in self.point_params + [self.mlp.flat]:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-            else:
+            elif not (self._pts_grad_clean and p is not self.mlp.flat):
                 p.grad.zero_()
+        self._pts_grad_clean = False
         # ---- colour MLP + composite + losses (torch autograd, per sample / per ray) ----------
         samp = q.work[:n].long()
         fs_t = self.fs[:n].float().requires_grad_(True)
@@ -312,14 +350,22 @@ class HipTrainer:
         chunk = max(DW_CHUNK, -(-rp // 512))  # at most 512 batches
         for t in self.d + [self.x0, self.h1, self.h2, self.h3]:
             t[rows:rp].zero_()                 # stale tails must not reach the GEMM (0 * NaN)
-        for name, d, x, ix in (("block3.2", self.d[3], self.h3, self.inv_chain),
-                               ("block3.0", self.d[2], self.h2, self.inv_h2),
-                               ("block1.2", self.d[1], self.h1, self.inv_chain),
-                               ("block1.0", self.d[0], self.x0, self.inv_x0)):
+        # db_l = column sums of the four delta tiles, in one pair of launches
+        if not hasattr(self, "_cs_out"):
+            self._cs_ws = torch.empty(int(_lib.lib().sgn_colsum_workspace_bytes(4)) // 4, dtype=torch.float32,
+                                      device=self.device)
+            self._cs_out = torch.empty(4, 256, dtype=torch.float32, device=self.device)
+        ds = (ctypes.c_void_p * 4)(*(t.data_ptr() for t in (self.d[3], self.d[2], self.d[1], self.d[0])))
+        _lib.check(_lib.lib().sgn_colsum_f16(4, ds, rows, 256, _lib.ptr(self._cs_ws), _lib.ptr(self._cs_out),
+                                             _lib.stream_handle()), "sgn_colsum_f16")
+        for li, (name, d, x, ix) in enumerate((("block3.2", self.d[3], self.h3, self.inv_chain),
+                                               ("block3.0", self.d[2], self.h2, self.inv_h2),
+                                               ("block1.2", self.d[1], self.h1, self.inv_chain),
+                                               ("block1.0", self.d[0], self.x0, self.inv_x0))):
             dr, xr = d[:rp], x[:rp]
             G = _gemm_rows_f32(dr, xr, chunk)    # [256 stored][C stored]
             m.w(name, g).add_(G[iu][:, ix] * inv)        # gathers, no scatter
-            m.b(name, g).add_(torch.sum(dr, 0, dtype=torch.float32)[iu] * inv)
+            m.b(name, g).add_(self._cs_out[li][iu] * inv)
         # alpha branch: dWa = dza^T h4, dba = sum dza
         ga = _mm_f32(self.dza[:rows].to(torch.float16)[None, :], self.h4[:rows])[0]
         m.w("alpha_branch.0", g)[0].add_(ga[iu] * inv)
@@ -339,6 +385,7 @@ class HipTrainer:
         self._set_lr()
         self.opt_net.step()
         self.opt_pts.step()
+        self._pts_grad_clean = isinstance(self.opt_pts, PointAdam) and self.opt_pts.zero_grad_in_step
         self.step_count += 1
 
     def step(self, campos, rot, raydir, near, far, gt):

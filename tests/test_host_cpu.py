@@ -71,6 +71,15 @@ def test_argument_errors_are_reported_without_gpu():
     assert rc != 0 and b"null" in L.sgn_last_error()
     rc = L.sgn_grid_build(None, 10, None, None, ctypes.byref(ctypes.c_void_p()))
     assert rc != 0
+    rc = L.sgn_adam_step(fake, fake, fake, fake, 64, 1e-3, 0.9, 0.999, 1e-8, 0, 1, None)
+    assert rc != 0 and b"step >= 1" in L.sgn_last_error()
+    rc = L.sgn_adam_step(ctypes.c_void_p(20), fake, fake, fake, 64, 1e-3, 0.9, 0.999, 1e-8, 1, 1, None)
+    assert rc != 0 and b"aligned" in L.sgn_last_error()
+    xs = (ctypes.c_void_p * 1)(16)
+    rc = L.sgn_colsum_f16(1, xs, 100, 128, fake, fake, None)
+    assert rc != 0 and b"256" in L.sgn_last_error()
+    rc = L.sgn_colsum_f16(9, xs, 100, 256, fake, fake, None)
+    assert rc != 0 and b"count" in L.sgn_last_error()
 
 
 # ---- options ------------------------------------------------------------------------

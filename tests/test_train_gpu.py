@@ -161,3 +161,52 @@ def test_model_plugin_training_surface(tmp_path):
     m.optimize_parameters(total_steps=7)
     assert np.isfinite(float(m.get_current_losses()["total"]))
     assert m.test()["coarse_raycolor"].shape == before.shape
+
+
+@pytest.mark.parametrize("n", [4096, 1003, 3])
+def test_point_adam_matches_torch_adam(n):
+    """PointAdam (sgn_adam_step) against torch.optim.Adam (fp32, single-tensor) over three
+    steps with changing gradients and a decayed lr: parameters and both moments within fp32
+    rounding; the gradient is cleared by the step when zero_grad is on."""
+    from sgnerf_amd.train_hip import PointAdam
+    g = torch.Generator().manual_seed(n)
+    p0 = torch.randn(n, generator=g)
+    a = torch.nn.Parameter(p0.clone().to(DEV))
+    b = torch.nn.Parameter(p0.clone().to(DEV))
+    oa = PointAdam([a], lr=2e-3, betas=(0.9, 0.999))
+    ob = torch.optim.Adam([b], lr=2e-3, betas=(0.9, 0.999), foreach=False)
+    for it in range(3):
+        gr = (torch.randn(n, generator=g) * 10 ** (it - 1)).to(DEV)
+        gr[::7] = 0.0                                    # untouched points still decay
+        a.grad = gr.clone()
+        b.grad = gr.clone()
+        for o in (oa, ob):
+            o.param_groups[0]["lr"] = 2e-3 * 0.9 ** it
+        oa.step()
+        ob.step()
+        assert torch.count_nonzero(a.grad) == 0
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+        for k in ("exp_avg", "exp_avg_sq"):
+            ref = ob.state[b][k]   # atol: fp32 rounding at the tensor's scale (m cancels to ~0)
+            torch.testing.assert_close(oa.state[a][k], ref, rtol=1e-6, atol=1e-6 * float(ref.abs().max()))
+    assert float(oa.state[a]["step"]) == 3.0
+
+
+@pytest.mark.parametrize("rows", [0, 1, 777, 165_000])
+def test_colsum_matches_torch_sum(rows):
+    """sgn_colsum_f16 (bias gradients) against a float64 column sum of the same fp16 tiles,
+    and bit-identical across two calls (fixed summation order)."""
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(rows)
+    xs = [torch.randn(max(rows, 1), 256, generator=g).half().to(DEV) for _ in range(4)]
+    ws = torch.empty(int(L.sgn_colsum_workspace_bytes(4)) // 4, device=DEV)
+    outs = []
+    for _ in range(2):
+        out = torch.full((4, 256), float("nan"), device=DEV)
+        ptrs = (ctypes.c_void_p * 4)(*(x.data_ptr() for x in xs))
+        _lib.check(L.sgn_colsum_f16(4, ptrs, rows, 256, _lib.ptr(ws), _lib.ptr(out), _lib.stream_handle()),
+                   "sgn_colsum_f16")
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.stack([x[:rows].double().sum(0) for x in xs]).float().cpu()
+    torch.testing.assert_close(outs[0], ref, rtol=1e-5, atol=1e-5 * max(rows, 1) ** 0.5)
