@@ -159,8 +159,8 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     rot = rot.reshape(3, 3)
     S = q["samp_ray"].shape[0]
     dev = raydir.device
-    sr = q["samp_ray"].long()
-    slot = torch.arange(S, device=dev) - q["ray_soff"].long()[sr]
+    sr = q["samp_ray"]          # int32 or int64 indices
+    slot = torch.arange(S, device=dev) - q["ray_soff"][sr]
     fd = torch.zeros(R, SR, 4, device=dev).index_put((sr, slot), feat)
     vd = torch.zeros(R, SR, dtype=torch.bool, device=dev).index_put((sr, slot), valid)
     ld = torch.zeros(R, SR, 3, device=dev).index_put((sr, slot), q["samp_locw"])
@@ -190,7 +190,8 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     # (point_aggregators.py:951-958): every (slot, k) of a valid ray, where empty slots and masked
     # neighbours read conf at the clamped index 0 (neural_points.py:956-967)
     K = q["pidx"].shape[1]
-    pd = torch.full((R, SR, K), -1, dtype=torch.long, device=dev).index_put((sr, slot), q["pidx"].long())
+    pidx = q["pidx"]
+    pd = torch.full((R, SR, K), -1, dtype=pidx.dtype, device=dev).index_put((sr, slot), pidx)
     # Empty entries all read conf[0]: gather them as one scalar (its gradient is a reduction)
     # and spread their gather indices, so the index_select backward does not pile every empty
     # entry's atomic add onto point 0.  Invalid rays are weighted out instead of compacted

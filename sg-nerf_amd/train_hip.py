@@ -241,7 +241,7 @@ class HipTrainer:
             self.feat = torch.zeros(S_cap, 4, dtype=torch.float32, device=dev)
             self._scap = S_cap
         if n_items > self._cap:
-            cap = max(32, ((n_items + 31) // 32) * 32)
+            cap = max(64, ((n_items + 63) // 64) * 64)   # rows (8 per item) a multiple of 512
             rows = cap * 8
             h = dict(dtype=torch.float16, device=dev)
             self.fs = torch.empty(cap, 256, **h)
@@ -307,16 +307,16 @@ class HipTrainer:
                 p.grad.zero_()
         self._pts_grad_clean = False
         # ---- colour MLP + composite + losses (torch autograd, per sample / per ray) ----------
-        samp = q.work[:n].long()
+        samp = q.work[:n]   # int32 indices throughout (no widening copies)
         fs_t = self.fs[:n].float().requires_grad_(True)
         alpha_t = self.feat[samp, 0].clone().requires_grad_(True)
-        v = raydir[q.samp_ray[samp].long()]
+        v = raydir[q.samp_ray[samp]]
         feat_s = torch.cat([alpha_t[:, None], self._colour(fs_t, v)], dim=-1)
         featS = torch.zeros(S, 4, device=dev).index_put((samp,), feat_s)
         validS = torch.zeros(S, dtype=torch.bool, device=dev)
         validS[samp] = True
-        qd = {"ray_ns": q.ray_ns[:R].long(), "ray_soff": q.ray_soff[:R].long(), "samp_ray": q.samp_ray[:S].long(),
-              "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K).long()}
+        qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
+              "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
         total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, campos, rot, raydir, gt, o)
         total.backward()
         # ---- HIP backward of the per-row part -----------------------------------------------
@@ -346,10 +346,11 @@ class HipTrainer:
         g = m.flat.grad
         inv = 1.0 / scale
         iu = self.inv_chain
-        rp = ((rows + 255) // 256) * 256      # rows padded to a multiple of 256 (buffers are)
+        rp = ((rows + 511) // 512) * 512      # rows padded to a multiple of 512 (buffers are)
         chunk = max(DW_CHUNK, -(-rp // 512))  # at most 512 batches
-        for t in self.d + [self.x0, self.h1, self.h2, self.h3]:
-            t[rows:rp].zero_()                 # stale tails must not reach the GEMM (0 * NaN)
+        if rp > rows:
+            for t in self.d + [self.x0, self.h1, self.h2, self.h3]:
+                t[rows:rp].zero_()             # stale tails must not reach the GEMM (0 * NaN)
         # db_l = column sums of the four delta tiles, in one pair of launches
         if not hasattr(self, "_cs_out"):
             self._cs_ws = torch.empty(int(_lib.lib().sgn_colsum_workspace_bytes(4)) // 4, dtype=torch.float32,
