@@ -149,10 +149,32 @@ def loss_from_query(points, mlp, q, campos, rot, raydir, gt, opts: HotPathOpts, 
                             zero_eps)
 
 
+class _CumprodPositive(torch.autograd.Function):
+    """torch.cumprod along the last dim for strictly positive inputs (the transmittance
+    factors 1 - o + 1e-10), with the backward torch itself takes when no input is zero
+    (reversed cumsum of grad * out, divided by the input) but without torch's device-to-host
+    check for zeros, so the step stays free of syncs and can be captured in a HIP graph."""
+
+    @staticmethod
+    def forward(ctx, x):
+        out = torch.cumprod(x, dim=-1)
+        ctx.save_for_backward(x, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        x, out = ctx.saved_tensors
+        return (grad * out).flip(-1).cumsum(-1).flip(-1).div(x)
+
+
 def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotPathOpts, bg=(1.0, 1.0, 1.0),
-                     zero_one_weight=1e-4, zero_eps=1e-3):
+                     zero_one_weight=1e-4, zero_eps=1e-3, s_count=None):
     """ray_dist + ray_march + the reference losses from per-sample features feat [S,4]
-    (alpha, r, g, b) and the per-sample validity (>= 1 neighbour)."""
+    (alpha, r, g, b) and the per-sample validity (>= 1 neighbour).
+
+    s_count (device scalar, optional): only the first s_count of the S sample entries are
+    real; the rest (capacity padding, for a graph-captured step with static shapes) are routed
+    to a sentinel ray row that is dropped, so the result equals the unpadded call."""
     R = raydir.shape[0]
     SR = opts.SR
     campos = campos.reshape(1, 3)
@@ -160,10 +182,19 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     S = q["samp_ray"].shape[0]
     dev = raydir.device
     sr = q["samp_ray"]          # int32 or int64 indices
-    slot = torch.arange(S, device=dev) - q["ray_soff"][sr]
-    fd = torch.zeros(R, SR, 4, device=dev).index_put((sr, slot), feat)
-    vd = torch.zeros(R, SR, dtype=torch.bool, device=dev).index_put((sr, slot), valid)
-    ld = torch.zeros(R, SR, 3, device=dev).index_put((sr, slot), q["samp_locw"])
+    ar = torch.arange(S, device=dev)
+    Rd = R
+    if s_count is None:
+        slot = ar - q["ray_soff"][sr]
+    else:
+        ok_s = ar < s_count
+        sr_c = torch.where(ok_s, sr, 0)
+        slot = torch.where(ok_s, ar - q["ray_soff"][sr_c], 0)
+        sr = torch.where(ok_s, sr, R)
+        Rd = R + 1
+    fd = torch.zeros(Rd, SR, 4, device=dev).index_put((sr, slot), feat)[:R]
+    vd = torch.zeros(Rd, SR, dtype=torch.bool, device=dev).index_put((sr, slot), valid)[:R]
+    ld = torch.zeros(Rd, SR, 3, device=dev).index_put((sr, slot), q["samp_locw"])[:R]
     z = _w2pers(ld, rot, campos)[..., 2]
     cm = torch.cummax(z, dim=-1)[0]
     rd = torch.cat([cm[:, 1:] - cm[:, :-1], torch.full((R, 1), float(opts.vsize[2]), device=dev)], dim=-1)
@@ -174,10 +205,10 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     rd = (rd * (1 - msk) + msk * float(opts.vsize[2])) * vd.float()
     sigma = fd[..., 0] * vd.float()
     o = 1 - torch.exp(-sigma * rd)
-    acc = torch.cumprod(1 - o + 1e-10, dim=-1)
+    acc = _CumprodPositive.apply(1 - o + 1e-10)
     bg_t = acc[:, -1:]
     acc = torch.cat([torch.ones(R, 1, device=dev), acc[:, :-1]], dim=-1)
-    bgv = torch.tensor(bg, dtype=torch.float32, device=dev)
+    bgv = torch.cat([torch.full((1,), float(b), device=dev) for b in bg])  # no host copy (graph-safe)
     color = torch.sum(fd[..., 1:4] * (o * acc)[..., None], dim=1) + bgv * bg_t
     ray_mask = vd.any(-1)
     full = torch.where(ray_mask[:, None], color, bgv.expand(R, 3))
@@ -191,7 +222,7 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     # neighbours read conf at the clamped index 0 (neural_points.py:956-967)
     K = q["pidx"].shape[1]
     pidx = q["pidx"]
-    pd = torch.full((R, SR, K), -1, dtype=pidx.dtype, device=dev).index_put((sr, slot), pidx)
+    pd = torch.full((Rd, SR, K), -1, dtype=pidx.dtype, device=dev).index_put((sr, slot), pidx)[:R]
     # Empty entries all read conf[0]: gather them as one scalar (its gradient is a reduction)
     # and spread their gather indices, so the index_select backward does not pile every empty
     # entry's atomic add onto point 0.  Invalid rays are weighted out instead of compacted

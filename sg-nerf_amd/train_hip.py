@@ -225,6 +225,9 @@ class HipTrainer:
         self.inv_x0 = self._inverse(self.map_x0, 284)
         self.inv_h2 = self._inverse(self.map_h2, 263)
         self._cap = 0
+        # the colour/composite/loss stage as one replayed HIP graph (SGN_TRAIN_GRAPH=0: eager)
+        self.use_graph = os.environ.get("SGN_TRAIN_GRAPH", "1") != "0"
+        self._gstate = None
 
     @staticmethod
     def _inverse(m, n):
@@ -289,7 +292,11 @@ class HipTrainer:
         R = raydir.shape[0]
         q = self._query(campos, raydir, near, far)
         S, n = (int(x) for x in q.counters[:2].tolist())  # one host sync per step
-        self._buffers(n, max(S, 1))
+        graph = self.use_graph and dev.type == "cuda"
+        if graph:
+            self._buffers(R * o.SR, R * o.SR)   # static shapes: every buffer at the batch's capacity
+        else:
+            self._buffers(n, max(S, 1))
         blob, tblob = self.packer.pack(self.mlp.flat)
         L = _lib.lib()
         st = _lib.stream_handle()
@@ -307,24 +314,30 @@ class HipTrainer:
                 p.grad.zero_()
         self._pts_grad_clean = False
         # ---- colour MLP + composite + losses (torch autograd, per sample / per ray) ----------
-        samp = q.work[:n]   # int32 indices throughout (no widening copies)
-        fs_t = self.fs[:n].float().requires_grad_(True)
-        alpha_t = self.feat[samp, 0].clone().requires_grad_(True)
-        v = raydir[q.samp_ray[samp]]
-        feat_s = torch.cat([alpha_t[:, None], self._colour(fs_t, v)], dim=-1)
-        featS = torch.zeros(S, 4, device=dev).index_put((samp,), feat_s)
-        validS = torch.zeros(S, dtype=torch.bool, device=dev)
-        validS[samp] = True
-        qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
-              "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
-        total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, campos, rot, raydir, gt, o)
-        total.backward()
+        if graph:
+            out = self._graph_losses(q, campos, rot, raydir, gt, R)
+            total, parts, full, ray_mask = out["total"], dict(out["parts"]), out["full"], out["ray_mask"]
+            dfs, dal, scale = out["dfs"], out["dal"], out["scale"]
+        else:
+            samp = q.work[:n]   # int32 indices throughout (no widening copies)
+            fs_t = self.fs[:n].float().requires_grad_(True)
+            alpha_t = self.feat[samp, 0].clone().requires_grad_(True)
+            v = raydir[q.samp_ray[samp]]
+            feat_s = torch.cat([alpha_t[:, None], self._colour(fs_t, v)], dim=-1)
+            featS = torch.zeros(S, 4, device=dev).index_put((samp,), feat_s)
+            validS = torch.zeros(S, dtype=torch.bool, device=dev)
+            validS[samp] = True
+            qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
+                  "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
+            total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, campos, rot, raydir, gt, o)
+            total.backward()
+            if n > 0:
+                dfs = fs_t.grad.contiguous()
+                dal = alpha_t.grad.contiguous()
+                m = torch.maximum(dfs.abs().amax(), dal.abs().amax())
+                scale = torch.exp2(-torch.floor(torch.log2(torch.clamp(m, min=1e-30)))).reshape(1).contiguous()
         # ---- HIP backward of the per-row part -----------------------------------------------
         if n > 0:
-            dfs = fs_t.grad.contiguous()
-            dal = alpha_t.grad.contiguous()
-            m = torch.maximum(dfs.abs().amax(), dal.abs().amax())
-            scale = torch.exp2(-torch.floor(torch.log2(torch.clamp(m, min=1e-30)))).reshape(1).contiguous()
             deltas = _lib.AggDeltas(self.d[3].data_ptr(), self.d[2].data_ptr(), self.d[1].data_ptr(),
                                     self.d[0].data_ptr(), self.h4.data_ptr(), self.dza.data_ptr())
             P = self.points
@@ -339,6 +352,83 @@ class HipTrainer:
         _allreduce_point_rows([p.grad for p in self.point_params])
         parts["total"] = total.detach()
         return parts, full.detach(), ray_mask
+
+    # -- graph-captured loss stage -----------------------------------------------------------
+    def _loss_body(self, st):
+        """Colour MLP + composite + losses + their autograd over the batch's full sample capacity
+        (R * SR entries, static shapes, no host sync): items past the device count n and samples
+        past S are padding, zeroed on input and routed to sentinel rows, so the gradients equal
+        the eager path's.  Runs inside a HIP graph capture (and its warm-up)."""
+        o, dev, R = self.opts, self.device, st["R"]
+        Sc = R * o.SR
+        q = st["q"]
+        ar = st["ar"]
+        ok_i = ar < q.counters[1]
+        work = q.work[:Sc]
+        samp = torch.where(ok_i, work, Sc)      # padding items -> sentinel sample Sc
+        samp_c = torch.where(ok_i, work, 0)
+        fs32, al32 = st["fs32"], st["al32"]
+        with torch.no_grad():
+            fs32.copy_(torch.where(ok_i[:, None], self.fs[:Sc].float(), 0.0))
+            al32.copy_(torch.where(ok_i, self.feat[:, 0][samp_c], 0.0))
+            fs32.grad.zero_()
+            al32.grad.zero_()
+        v = st["raydir"][q.samp_ray[:Sc][samp_c]]
+        feat_s = torch.cat([al32[:, None], self._colour(fs32, v)], dim=-1)
+        featS = torch.zeros(Sc + 1, 4, device=dev).index_put((samp,), feat_s)[:Sc]
+        validS = torch.zeros(Sc + 1, dtype=torch.bool, device=dev).index_put((samp,), st["true"])[:Sc]
+        qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:Sc],
+              "samp_locw": q.samp_locw[:Sc * 3].view(Sc, 3), "pidx": q.pidx[:Sc * o.K].view(Sc, o.K)}
+        total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, st["campos"], st["rot"],
+                                                        st["raydir"], st["gt"], o, s_count=q.counters[0])
+        total.backward()
+        dfs, dal = fs32.grad, al32.grad
+        m = torch.maximum(dfs.abs().amax(), dal.abs().amax())
+        scale = torch.exp2(-torch.floor(torch.log2(torch.clamp(m, min=1e-30)))).reshape(1)
+        return {"total": total.detach(), "parts": parts, "full": full.detach(), "ray_mask": ray_mask,
+                "dfs": dfs, "dal": dal, "scale": scale}
+
+    def _graph_losses(self, q, campos, rot, raydir, gt, R):
+        """Replay the captured loss stage (captured again when a buffer it reads moved)."""
+        dev = self.device
+        P, fl = self.points, self.mlp.flat
+        key = (R, q.work.data_ptr(), q.counters.data_ptr(), self.fs.data_ptr(), self.feat.data_ptr(), fl.data_ptr(),
+               fl.grad.data_ptr(), P.points_conf.data_ptr(), P.points_conf.grad.data_ptr())
+        st = self._gstate
+        if st is None or st["key"] != key:
+            self._gstate = None
+            Sc = R * self.opts.SR
+            st = {"key": key, "R": R, "q": q, "ar": torch.arange(Sc, device=dev),
+                  "true": torch.ones((), dtype=torch.bool, device=dev),
+                  "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
+                  "campos": campos.clone(), "rot": rot.clone(),
+                  "fs32": torch.zeros(Sc, 256, device=dev, requires_grad=True),
+                  "al32": torch.zeros(Sc, device=dev, requires_grad=True)}
+            st["fs32"].grad = torch.zeros_like(st["fs32"])
+            st["al32"].grad = torch.zeros_like(st["al32"])
+            keep = [fl.grad.clone(), P.points_conf.grad.clone()]   # warm-up accumulates into them
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self._loss_body(st)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st["out"] = self._loss_body(st)
+            fl.grad.copy_(keep[0])
+            P.points_conf.grad.copy_(keep[1])
+            st["graph"] = g
+            self._gstate = st
+        st["raydir"].copy_(raydir)
+        st["gt"].copy_(gt.reshape(-1, 3))
+        st["campos"].copy_(campos)
+        st["rot"].copy_(rot)
+        st["graph"].replay()
+        out = st["out"]
+        return {"total": out["total"].clone(), "parts": {k: v.clone() for k, v in out["parts"].items()},
+                "full": out["full"].clone(), "ray_mask": out["ray_mask"].clone(),
+                "dfs": out["dfs"], "dal": out["dal"], "scale": out["scale"]}
 
     def _weight_grads(self, rows, scale):
         """dW_l = delta_l^T x_l (fp16 GEMM, fp32 out), db_l = sum delta_l, unpermuted."""

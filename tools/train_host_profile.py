@@ -39,6 +39,28 @@ t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
 print(f"host issue {1e3 * (t1 - t0) / 10:.3f} ms/step, drain after {1e3 * (t2 - t1):.3f} ms")
+# in-process A/B of the graph-captured loss stage: blocks of 10 steps, alternated
+res = {False: [], True: []}
+for rep in range(4):
+    for ug in (False, True):
+        tr.use_graph = ug
+        for b in batches[:2]:
+            tr.step(*b[:3], 0.1, 8.0, b[3])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b in batches[5:15]:
+            tr.step(*b[:3], 0.1, 8.0, b[3])
+        torch.cuda.synchronize()
+        res[ug].append(1e3 * (time.perf_counter() - t0) / 10)
+for ug in (False, True):
+    print(f"use_graph={ug}: ms/step " + " ".join(f"{x:.3f}" for x in res[ug]))
+tr.use_graph = True
+t0 = time.perf_counter()
+for b in batches[5:15]:
+    tr.step(*b[:3], 0.1, 8.0, b[3])
+t1 = time.perf_counter()
+torch.cuda.synchronize()
+print(f"graph: host issue {1e3 * (t1 - t0) / 10:.3f} ms/step, drain after {1e3 * (time.perf_counter() - t1):.3f} ms")
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 with profile(activities=[ProfilerActivity.CPU]) as prof:
     for b in batches[15:20]:
