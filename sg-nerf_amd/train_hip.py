@@ -139,6 +139,10 @@ def _gemm_rows_f32(a, b, chunk):
     return G
 
 
+# loss-stage graphs: capacity bucket (items / samples) and how many captured graphs are kept
+GRAPH_BUCKET = int(os.environ.get("SGN_GRAPH_BUCKET", "8192"))
+GRAPH_CACHE = 8
+
 # rows per split-K batch of the weight-gradient GEMMs (SGN_DW_CHUNK overrides, for sweeps)
 DW_CHUNK = int(os.environ.get("SGN_DW_CHUNK", "512"))
 
@@ -227,7 +231,8 @@ class HipTrainer:
         self._cap = 0
         # the colour/composite/loss stage as one replayed HIP graph (SGN_TRAIN_GRAPH=0: eager)
         self.use_graph = os.environ.get("SGN_TRAIN_GRAPH", "1") != "0"
-        self._gstate = None
+        self._graphs = {}
+        self._flat_maps = {}
 
     @staticmethod
     def _inverse(m, n):
@@ -291,13 +296,21 @@ class HipTrainer:
         raydir = raydir.reshape(-1, 3).to(dev, torch.float32).contiguous()
         R = raydir.shape[0]
         q = self._query(campos, raydir, near, far)
+        # work that does not depend on the query is queued before the step's one host sync, so
+        # the GPU runs it while the host waits
+        blob, tblob = self.packer.pack(self.mlp.flat)
+        for p in self.point_params + [self.mlp.flat]:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            elif not (self._pts_grad_clean and p is not self.mlp.flat):
+                p.grad.zero_()
+        self._pts_grad_clean = False
         S, n = (int(x) for x in q.counters[:2].tolist())  # one host sync per step
         graph = self.use_graph and dev.type == "cuda"
         if graph:
             self._buffers(R * o.SR, R * o.SR)   # static shapes: every buffer at the batch's capacity
         else:
             self._buffers(n, max(S, 1))
-        blob, tblob = self.packer.pack(self.mlp.flat)
         L = _lib.lib()
         st = _lib.stream_handle()
         pt = self._tables(campos, rot, raydir)
@@ -307,15 +320,9 @@ class HipTrainer:
             _lib.check(L.sgn_aggregate_train_fwd(ctypes.byref(pt), ctypes.byref(qo), n, o.K, _lib.ptr(blob),
                                                  _lib.ptr(self.feat), _lib.ptr(self.fs), ctypes.byref(saved), st),
                        "sgn_aggregate_train_fwd")
-        for p in self.point_params + [self.mlp.flat]:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            elif not (self._pts_grad_clean and p is not self.mlp.flat):
-                p.grad.zero_()
-        self._pts_grad_clean = False
         # ---- colour MLP + composite + losses (torch autograd, per sample / per ray) ----------
         if graph:
-            out = self._graph_losses(q, campos, rot, raydir, gt, R)
+            out = self._graph_losses(q, campos, rot, raydir, gt, R, S, n)
             total, parts, full, ray_mask = out["total"], dict(out["parts"]), out["full"], out["ray_mask"]
             dfs, dal, scale = out["dfs"], out["dal"], out["scale"]
         else:
@@ -360,16 +367,15 @@ class HipTrainer:
         past S are padding, zeroed on input and routed to sentinel rows, so the gradients equal
         the eager path's.  Runs inside a HIP graph capture (and its warm-up)."""
         o, dev, R = self.opts, self.device, st["R"]
-        Sc = R * o.SR
+        Sc, Nc = st["Sc"], st["Nc"]             # sample / item capacity of this graph
         q = st["q"]
-        ar = st["ar"]
-        ok_i = ar < q.counters[1]
-        work = q.work[:Sc]
+        ok_i = st["ar"][:Nc] < q.counters[1]
+        work = q.work[:Nc]
         samp = torch.where(ok_i, work, Sc)      # padding items -> sentinel sample Sc
         samp_c = torch.where(ok_i, work, 0)
         fs32, al32 = st["fs32"], st["al32"]
         with torch.no_grad():
-            fs32.copy_(torch.where(ok_i[:, None], self.fs[:Sc].float(), 0.0))
+            fs32.copy_(torch.where(ok_i[:, None], self.fs[:Nc].float(), 0.0))
             al32.copy_(torch.where(ok_i, self.feat[:, 0][samp_c], 0.0))
             fs32.grad.zero_()
             al32.grad.zero_()
@@ -388,22 +394,27 @@ class HipTrainer:
         return {"total": total.detach(), "parts": parts, "full": full.detach(), "ray_mask": ray_mask,
                 "dfs": dfs, "dal": dal, "scale": scale}
 
-    def _graph_losses(self, q, campos, rot, raydir, gt, R):
-        """Replay the captured loss stage (captured again when a buffer it reads moved)."""
+    def _graph_losses(self, q, campos, rot, raydir, gt, R, S, n):
+        """Replay the captured loss stage for this step's capacity bucket (item / sample counts
+        rounded up to GRAPH_BUCKET); captured on first use and again when a buffer it reads
+        moved.  At most GRAPH_CACHE graphs are kept."""
         dev = self.device
         P, fl = self.points, self.mlp.flat
-        key = (R, q.work.data_ptr(), q.counters.data_ptr(), self.fs.data_ptr(), self.feat.data_ptr(), fl.data_ptr(),
-               fl.grad.data_ptr(), P.points_conf.data_ptr(), P.points_conf.grad.data_ptr())
-        st = self._gstate
-        if st is None or st["key"] != key:
-            self._gstate = None
-            Sc = R * self.opts.SR
-            st = {"key": key, "R": R, "q": q, "ar": torch.arange(Sc, device=dev),
+        cap = R * self.opts.SR
+        Sc = min(cap, -(-max(S, 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
+        Nc = min(Sc, -(-max(n, 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
+        key = (R, Sc, Nc, q.work.data_ptr(), q.counters.data_ptr(), self.fs.data_ptr(), self.feat.data_ptr(),
+               fl.data_ptr(), fl.grad.data_ptr(), P.points_conf.data_ptr(), P.points_conf.grad.data_ptr())
+        st = self._graphs.get(key)
+        if st is None:
+            if len(self._graphs) >= GRAPH_CACHE:
+                self._graphs.pop(next(iter(self._graphs)))
+            st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "ar": torch.arange(Sc, device=dev),
                   "true": torch.ones((), dtype=torch.bool, device=dev),
                   "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
                   "campos": campos.clone(), "rot": rot.clone(),
-                  "fs32": torch.zeros(Sc, 256, device=dev, requires_grad=True),
-                  "al32": torch.zeros(Sc, device=dev, requires_grad=True)}
+                  "fs32": torch.zeros(Nc, 256, device=dev, requires_grad=True),
+                  "al32": torch.zeros(Nc, device=dev, requires_grad=True)}
             st["fs32"].grad = torch.zeros_like(st["fs32"])
             st["al32"].grad = torch.zeros_like(st["al32"])
             keep = [fl.grad.clone(), P.points_conf.grad.clone()]   # warm-up accumulates into them
@@ -419,7 +430,7 @@ class HipTrainer:
             fl.grad.copy_(keep[0])
             P.points_conf.grad.copy_(keep[1])
             st["graph"] = g
-            self._gstate = st
+            self._graphs[key] = st
         st["raydir"].copy_(raydir)
         st["gt"].copy_(gt.reshape(-1, 3))
         st["campos"].copy_(campos)
@@ -455,8 +466,13 @@ class HipTrainer:
                                                ("block1.0", self.d[0], self.x0, self.inv_x0))):
             dr, xr = d[:rp], x[:rp]
             G = _gemm_rows_f32(dr, xr, chunk)    # [256 stored][C stored]
-            m.w(name, g).add_(G[iu][:, ix] * inv)        # gathers, no scatter
-            m.b(name, g).add_(self._cs_out[li][iu] * inv)
+            fi = self._flat_maps.get(name)
+            if fi is None:                       # stored (unit, column) of each reference weight
+                fi = (iu[:, None] * x.shape[1] + ix[None, :]).reshape(-1)
+                self._flat_maps[name] = fi
+            w = m.w(name, g)
+            w.addcmul_(G.view(-1).index_select(0, fi).view(w.shape), inv)   # gather, no scatter
+            m.b(name, g).addcmul_(self._cs_out[li].index_select(0, iu), inv)
         # alpha branch: dWa = dza^T h4, dba = sum dza
         ga = _mm_f32(self.dza[:rows].to(torch.float16)[None, :], self.h4[:rows])[0]
         m.w("alpha_branch.0", g)[0].add_(ga[iu] * inv)
