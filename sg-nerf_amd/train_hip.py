@@ -276,13 +276,32 @@ class HipTrainer:
         pt.campos, pt.camrotc2w, pt.raydir = campos.data_ptr(), rot.data_ptr(), raydir.data_ptr()
         return pt
 
-    def _colour(self, fs, v):
+    _COLOUR = ("color_branch.0", "color_branch.2", "color_branch.4", "color_branch.6")
+
+    def _colour_span(self):
+        """[c0, c1): the colour branch's weights and biases, contiguous in the flat parameter."""
+        sl = self.mlp.slices
+        c0 = min(sl[n][0] for n in self._COLOUR)
+        c1 = max(sl[n][0] + sl[n][1] * sl[n][2] + sl[n][1] for n in self._COLOUR)
+        assert c1 - c0 == sum(sl[n][1] * sl[n][2] + sl[n][1] for n in self._COLOUR)
+        return c0, c1
+
+    def _colour(self, fs, v, src=None, base=0):
+        """colour MLP (point_aggregators.py color_branch); weights from the flat parameter, or
+        from `src` = a copy of its [base, base + len) span."""
         m = self.mlp
         vpe = _pe(v, 4, ori=True)[..., 3:]
         c = torch.cat([fs, vpe], dim=-1)
-        for name in ("color_branch.0", "color_branch.2", "color_branch.4"):
-            c = F.leaky_relu(F.linear(c, m.w(name), m.b(name)), 0.01)
-        c = F.linear(c, m.w("color_branch.6"), m.b("color_branch.6"))
+        for name in self._COLOUR:
+            if src is None:
+                w, b = m.w(name), m.b(name)
+            else:
+                off, o, i = m.slices[name]
+                w = src[off - base:off - base + o * i].view(o, i)
+                b = src[off - base + o * i:off - base + o * i + o]
+            c = F.linear(c, w, b)
+            if name != "color_branch.6":
+                c = F.leaky_relu(c, 0.01)
         return torch.sigmoid(c) * (1 + 2 * 0.001) - 0.001
 
     # -- one step ------------------------------------------------------------------------
@@ -373,14 +392,17 @@ class HipTrainer:
         work = q.work[:Nc]
         samp = torch.where(ok_i, work, Sc)      # padding items -> sentinel sample Sc
         samp_c = torch.where(ok_i, work, 0)
-        fs32, al32 = st["fs32"], st["al32"]
+        fs32, al32, cw = st["fs32"], st["al32"], st["cw"]
+        c0, c1 = st["cspan"]
+        fl = self.mlp.flat
         with torch.no_grad():
             fs32.copy_(torch.where(ok_i[:, None], self.fs[:Nc].float(), 0.0))
             al32.copy_(torch.where(ok_i, self.feat[:, 0][samp_c], 0.0))
-            fs32.grad.zero_()
-            al32.grad.zero_()
+            cw.copy_(fl[c0:c1])                 # colour weights as their own leaf: autograd
+            for t in (fs32, al32, cw):          # never touches the full flat parameter
+                t.grad.zero_()
         v = st["raydir"][q.samp_ray[:Sc][samp_c]]
-        feat_s = torch.cat([al32[:, None], self._colour(fs32, v)], dim=-1)
+        feat_s = torch.cat([al32[:, None], self._colour(fs32, v, cw, c0)], dim=-1)
         featS = torch.zeros(Sc + 1, 4, device=dev).index_put((samp,), feat_s)[:Sc]
         validS = torch.zeros(Sc + 1, dtype=torch.bool, device=dev).index_put((samp,), st["true"])[:Sc]
         qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:Sc],
@@ -388,6 +410,8 @@ class HipTrainer:
         total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, st["campos"], st["rot"],
                                                         st["raydir"], st["gt"], o, s_count=q.counters[0])
         total.backward()
+        with torch.no_grad():
+            fl.grad[c0:c1].add_(cw.grad)
         dfs, dal = fs32.grad, al32.grad
         m = torch.maximum(dfs.abs().amax(), dal.abs().amax())
         scale = torch.exp2(-torch.floor(torch.log2(torch.clamp(m, min=1e-30)))).reshape(1)
@@ -414,7 +438,9 @@ class HipTrainer:
                   "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
                   "campos": campos.clone(), "rot": rot.clone(),
                   "fs32": torch.zeros(Nc, 256, device=dev, requires_grad=True),
-                  "al32": torch.zeros(Nc, device=dev, requires_grad=True)}
+                  "al32": torch.zeros(Nc, device=dev, requires_grad=True), "cspan": self._colour_span()}
+            st["cw"] = torch.zeros(st["cspan"][1] - st["cspan"][0], device=dev, requires_grad=True)
+            st["cw"].grad = torch.zeros_like(st["cw"])
             st["fs32"].grad = torch.zeros_like(st["fs32"])
             st["al32"].grad = torch.zeros_like(st["al32"])
             keep = [fl.grad.clone(), P.points_conf.grad.clone()]   # warm-up accumulates into them
