@@ -17,6 +17,7 @@
 //     one thread per real sample instead of R*SR threads;
 //   * a voxel's candidate points are one contiguous float4 run (grid.hip).
 #include <hipcub/hipcub.hpp>
+#include <cstdlib>
 #include <utility>
 
 #include "sgn_common.h"
@@ -26,21 +27,18 @@ namespace {
 
 constexpr int TPB = 256;
 
+// Ray batches up to this size march one wave per ray (k_march_wave), larger ones one thread
+// per ray (k_march); SGN_MARCH_WAVE_MAX_RAYS overrides (0: always a thread per ray).
+int64_t march_wave_max_rays() {
+    const char *e = getenv("SGN_MARCH_WAVE_MAX_RAYS");
+    return e ? (int64_t)atoll(e) : (int64_t)65536;
+}
+
 // ---- march -----------------------------------------------------------------
-// Candidate d of ray r is flagged when its voxel is inside the grid and
-// coor_occ == 1 (vox != -2).  The first SR flagged candidates become slots.
-template <bool PER_RAY_T>
-__global__ __launch_bounds__(TPB) void k_march(GridView g, const float *__restrict__ campos,
-                                               const float *__restrict__ raydir, int64_t R,
-                                               const float *__restrict__ t_table, int D, int SR,
-                                               int32_t *__restrict__ ray_ns,
-                                               int16_t *__restrict__ ray_slot_d) {
-    int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (r >= R) return;
-    const float cx = campos[0], cy = campos[1], cz = campos[2];
-    const float dx = raydir[r * 3 + 0], dy = raydir[r * 3 + 1], dz = raydir[r * 3 + 2];
-    const float *tt = PER_RAY_T ? t_table + r * (int64_t)D : t_table;
-    const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+// [d_lo, d_hi]: the candidates of a ray inside its span through the grid box.
+__device__ __forceinline__ void ray_span(const GridView &g, float cx, float cy, float cz, float dx, float dy,
+                                         float dz, const float *__restrict__ tt, int D, int &d_lo_out,
+                                         int &d_hi_out) {
     // Candidates whose t lies outside the ray's span through the grid box, widened by two voxels
     // on every side (far beyond the rounding of ray_coord / vox_coord), are out of the grid and
     // never flagged: the scan covers [d_lo, d_hi] only (the test inside is unchanged).
@@ -68,6 +66,26 @@ __global__ __launch_bounds__(TPB) void k_march(GridView g, const float *__restri
         while (lo < hi) { const int m = (lo + hi) >> 1; if (tt[m] <= t_out) lo = m + 1; else hi = m; }
         d_hi = lo - 1;
     }
+    d_lo_out = d_lo;
+    d_hi_out = d_hi;
+}
+
+// Candidate d of ray r is flagged when its voxel is inside the grid and
+// coor_occ == 1 (vox != -2).  The first SR flagged candidates become slots.
+template <bool PER_RAY_T>
+__global__ __launch_bounds__(TPB) void k_march(GridView g, const float *__restrict__ campos,
+                                               const float *__restrict__ raydir, int64_t R,
+                                               const float *__restrict__ t_table, int D, int SR,
+                                               int32_t *__restrict__ ray_ns,
+                                               int16_t *__restrict__ ray_slot_d) {
+    int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    const float cx = campos[0], cy = campos[1], cz = campos[2];
+    const float dx = raydir[r * 3 + 0], dy = raydir[r * 3 + 1], dz = raydir[r * 3 + 2];
+    const float *tt = PER_RAY_T ? t_table + r * (int64_t)D : t_table;
+    const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+    int d_lo, d_hi;
+    ray_span(g, cx, cy, cz, dx, dy, dz, tt, D, d_lo, d_hi);
     int cnt = 0;
     constexpr int U = 8;  // candidates whose grid words are in flight together
     for (int d0 = d_lo; d0 <= d_hi && cnt < SR; d0 += U) {
@@ -94,6 +112,47 @@ __global__ __launch_bounds__(TPB) void k_march(GridView g, const float *__restri
         }
     }
     ray_ns[r] = cnt;
+}
+
+// Same slots as k_march, one 64-lane wave per ray (for small ray batches, e.g. the 4096-ray
+// training step, where a thread per ray leaves most of the chip idle): lane l tests candidate
+// base + l, a ballot and the lanes-below popcount give each flagged candidate its slot, so
+// the first SR flagged candidates land in scan order exactly as in the serial loop.
+template <bool PER_RAY_T>
+__global__ __launch_bounds__(TPB) void k_march_wave(GridView g, const float *__restrict__ campos,
+                                                    const float *__restrict__ raydir, int64_t R,
+                                                    const float *__restrict__ t_table, int D, int SR,
+                                                    int32_t *__restrict__ ray_ns,
+                                                    int16_t *__restrict__ ray_slot_d) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = blockIdx.x * (int64_t)(TPB / 64) + (threadIdx.x >> 6);
+    if (r >= R) return;  // wave-uniform
+    const float cx = campos[0], cy = campos[1], cz = campos[2];
+    const float dx = raydir[r * 3 + 0], dy = raydir[r * 3 + 1], dz = raydir[r * 3 + 2];
+    const float *tt = PER_RAY_T ? t_table + r * (int64_t)D : t_table;
+    const int64_t plane = (int64_t)g.dims[1] * g.dims[2];
+    int d_lo, d_hi;
+    ray_span(g, cx, cy, cz, dx, dy, dz, tt, D, d_lo, d_hi);
+    int cnt = 0;
+    for (int base = d_lo; base <= d_hi && cnt < SR; base += 64) {
+        const int d = base + lane;
+        int32_t word = VOX_UNFLAGGED;
+        if (d <= d_hi) {
+            const float t = tt[d];
+            const int ix = vox_coord(ray_coord(cx, dx, t), g.shift[0], g.vs[0]);
+            const int iy = vox_coord(ray_coord(cy, dy, t), g.shift[1], g.vs[1]);
+            const int iz = vox_coord(ray_coord(cz, dz, t), g.shift[2], g.vs[2]);
+            if (ix >= 0 && ix < g.dims[0] && iy >= 0 && iy < g.dims[1] && iz >= 0 && iz < g.dims[2])
+                word = g.vox[(int64_t)ix * plane + (int64_t)iy * g.dims[2] + iz];
+        }
+        const bool flagged = word != VOX_UNFLAGGED;
+        const uint64_t mask = __ballot(flagged);
+        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (flagged && cnt + rank < SR) ray_slot_d[r * SR + cnt + rank] = (int16_t)d;
+        cnt += __popcll(mask);
+    }
+    if (lane == 0) ray_ns[r] = cnt < SR ? cnt : SR;
 }
 
 __global__ void k_sample_total(const int32_t *__restrict__ soff, const int32_t *__restrict__ ns,
@@ -459,12 +518,21 @@ int sgn_query(const sgn_grid *grid, const sgn_query_params *qp, const float *d_c
     int16_t *slot_d = (int16_t *)(ws + ((scan + 255) / 256) * 256);
     GridView g = grid->view();
     dim3 rg((unsigned)((R + TPB - 1) / TPB));
-    if (qp->per_ray_t)
+    if (R <= march_wave_max_rays()) {  // small batches: one wave per ray
+        dim3 wg((unsigned)((R + TPB / 64 - 1) / (TPB / 64)));
+        if (qp->per_ray_t)
+            hipLaunchKernelGGL((k_march_wave<true>), wg, dim3(TPB), 0, st, g, d_campos, d_raydir, R, d_t_table,
+                               qp->D, qp->SR, o->ray_ns, slot_d);
+        else
+            hipLaunchKernelGGL((k_march_wave<false>), wg, dim3(TPB), 0, st, g, d_campos, d_raydir, R, d_t_table,
+                               qp->D, qp->SR, o->ray_ns, slot_d);
+    } else if (qp->per_ray_t) {
         hipLaunchKernelGGL((k_march<true>), rg, dim3(TPB), 0, st, g, d_campos, d_raydir, R, d_t_table,
                            qp->D, qp->SR, o->ray_ns, slot_d);
-    else
+    } else {
         hipLaunchKernelGGL((k_march<false>), rg, dim3(TPB), 0, st, g, d_campos, d_raydir, R, d_t_table,
                            qp->D, qp->SR, o->ray_ns, slot_d);
+    }
     SGN_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ws, scan, o->ray_ns, o->ray_soff, (int)R, st));
     hipLaunchKernelGGL(k_sample_total, dim3(1), dim3(64), 0, st, o->ray_soff, o->ray_ns, R, o->counters);
     hipLaunchKernelGGL(k_emit_samples, rg, dim3(TPB), 0, st, o->ray_ns, o->ray_soff, slot_d, R, qp->SR,

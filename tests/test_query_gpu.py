@@ -85,7 +85,20 @@ def test_query_parity(room, kw):
     assert res.n_samples() > 0
 
 
-def test_query_parity_jittered_rays(room):
+@pytest.mark.parametrize("march", ["wave", "thread"])
+def test_query_parity_both_march_kernels(room, march, monkeypatch):
+    """Small batches march one wave per ray (k_march_wave), large ones a thread per ray
+    (k_march): both give the oracle's slots (the threshold forced to 0 selects k_march)."""
+    monkeypatch.setenv("SGN_MARCH_WAVE_MAX_RAYS", "1000000000" if march == "wave" else "0")
+    for kw in (dict(), dict(SR=64, K=16), dict(SR=1, K=4)):
+        o = mkopts(**kw)
+        og, g, res, ref = _run(room, o, make_view(40, 56, yaw=35.0, pitch=-12.0))
+        _check(og, g, res, ref, o)
+
+
+@pytest.mark.parametrize("march", ["wave", "thread"])
+def test_query_parity_jittered_rays(room, march, monkeypatch):
+    monkeypatch.setenv("SGN_MARCH_WAVE_MAX_RAYS", "1000000000" if march == "wave" else "0")
     o = mkopts(SR=32)
     view = make_view(24, 24, yaw=200.0, pitch=5.0)
     R = view.raydir.shape[0]
