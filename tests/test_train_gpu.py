@@ -210,3 +210,48 @@ def test_colsum_matches_torch_sum(rows):
     assert torch.equal(outs[0], outs[1])
     ref = torch.stack([x[:rows].double().sum(0) for x in xs]).float().cpu()
     torch.testing.assert_close(outs[0], ref, rtol=1e-5, atol=1e-5 * max(rows, 1) ** 0.5)
+
+
+def test_graph_captured_step_matches_eager_step():
+    """The loss stage replayed as a HIP graph over padded capacity (HipTrainer.use_graph) gives
+    the eager step's loss, gradients and, over three steps with Adam, parameters: padding items
+    and samples contribute nothing (bar fp32 summation order in differently shaped GEMMs)."""
+    pc, view, qd, mlp, gt = _setup(seed=7)
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    runs = {}
+    for use_graph in (False, True):
+        points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+        tr = HipTrainer(points, mlp, O, DEV)
+        tr.use_graph = use_graph
+        losses, grads = [], None
+        for it in range(3):
+            torch.manual_seed(100 + it)                   # same jittered depth table in both runs
+            gti = torch.rand(gt.shape, generator=torch.Generator().manual_seed(it)).to(DEV)
+            parts, full, mask = tr.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gti)
+            if it == 0:
+                grads = {k: v.cpu() for k, v in grads_named(tr).items()}
+                first = (full.cpu(), mask.cpu())
+            tr.apply()
+            losses.append(float(parts["total"]))
+        torch.cuda.synchronize()
+        params = {k: getattr(points, k).detach().cpu().clone()
+                  for k in ("points_embeding", "points_color", "points_dir", "points_conf")}
+        params["mlp"] = tr.mlp.flat.detach().cpu().clone()
+        runs[use_graph] = (losses, grads, params, first)
+    (le, ge, pe, fe), (lg, gg, pg, fg) = runs[False], runs[True]
+    assert tr._graphs, "the graph path did not run"
+    assert torch.equal(fe[1], fg[1])
+    assert float((fe[0] - fg[0]).abs().max()) <= 1e-5
+    ge_err = {k: _rel(gg[k], ge[k]) for k in ge}
+    # parameters after three Adam steps: m / sqrt(v) normalises near-zero gradients, so rounding
+    # differences reach lr-sized updates on a few elements; the bound is relative L2 over tensors
+    pe_err = {k: float(torch.linalg.vector_norm((pg[k] - pe[k]).double())
+                       / torch.linalg.vector_norm((pe[k] - 0).double())) for k in pe}
+    print("losses eager", le, "graph", lg)
+    print("grad rel L2", {k: f"{v:.1e}" for k, v in ge_err.items()})
+    print("param rel L2", {k: f"{v:.1e}" for k, v in pe_err.items()})
+    assert abs(le[0] - lg[0]) <= 1e-5 * abs(le[0])
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 1e-3 * abs(a)
+    assert max(ge_err.values()) <= 1e-3, ge_err
+    assert max(pe_err.values()) <= 1e-4, pe_err
