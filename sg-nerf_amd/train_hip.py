@@ -144,7 +144,7 @@ GRAPH_BUCKET = int(os.environ.get("SGN_GRAPH_BUCKET", "8192"))
 GRAPH_CACHE = 8
 
 # rows per split-K batch of the weight-gradient GEMMs (SGN_DW_CHUNK overrides, for sweeps)
-DW_CHUNK = int(os.environ.get("SGN_DW_CHUNK", "512"))
+DW_CHUNK = int(os.environ.get("SGN_DW_CHUNK", "1024"))
 
 
 def _mm_f32(a, b):
@@ -249,7 +249,7 @@ class HipTrainer:
             self.feat = torch.zeros(S_cap, 4, dtype=torch.float32, device=dev)
             self._scap = S_cap
         if n_items > self._cap:
-            cap = max(64, ((n_items + 63) // 64) * 64)   # rows (8 per item) a multiple of 512
+            cap = max(128, ((n_items + 127) // 128) * 128)   # rows (8 per item) a multiple of 1024
             rows = cap * 8
             h = dict(dtype=torch.float16, device=dev)
             self.fs = torch.empty(cap, 256, **h)
@@ -473,8 +473,8 @@ class HipTrainer:
         g = m.flat.grad
         inv = 1.0 / scale
         iu = self.inv_chain
-        rp = ((rows + 511) // 512) * 512      # rows padded to a multiple of 512 (buffers are)
-        chunk = max(DW_CHUNK, -(-rp // 512))  # at most 512 batches
+        rp = ((rows + 1023) // 1024) * 1024   # rows padded to the split-K batch (buffers are)
+        chunk = max(DW_CHUNK, -(-rp // 512))  # at most 512 batches (no ragged tail up to 512 * DW_CHUNK rows)
         if rp > rows:
             for t in self.d + [self.x0, self.h1, self.h2, self.h3]:
                 t[rows:rp].zero_()             # stale tails must not reach the GEMM (0 * NaN)
