@@ -1,0 +1,821 @@
+// mlp_x3.hip -- fp32-faithful neural-point aggregator on fp16 MFMA (gfx950): every fp32
+// product of the reference's nn.Linear layers is carried as three fp16 MFMA products.
+//
+// Same path as mlp.hip (NeuralPoints gather neural_points.py:942-988, PointAggregator.forward /
+// viewmlp point_aggregators.py:868-959, :561-786), at the reference's arithmetic precision:
+//
+//   w = 2^-s (w_hi + w_lo), x = x_hi + x_lo, all four fp16; w x ~ 2^-s (w_hi x_hi + w_hi x_lo + w_lo x_hi)
+//
+// with fp32 accumulation (an fp16 x fp16 product is exact in fp32).  The weights of each layer are
+// pre-scaled by a power of two 2^s (max |w| 2^s < 2^14) so w_lo stays a normal fp16 number; the
+// epilogue multiplies by 2^-s exactly.  Per product the representation error is <= 2^-22 |w x|
+// (+ 2^-25 |w| for activations below fp16's normal range), the dropped w_lo x_lo term <= 2^-22
+// |w x|: the layer sums agree with an fp32 evaluation to a few fp32 ulps of sum |w x|.
+// Activations must stay inside fp16's range (|x| < 65504) -- the MLP's hidden features do.
+// The positional encodings use the accurate sinf/cosf of the scaled argument (x 2^f is exact),
+// as torch.sin does (networks.py:175-192).  dtype of this path: "f32 (3xf16 split MFMA, fp32
+// accumulate)"; 3 MFMAs per product, so its MFMA ceiling is 1/3 of the fp16 dense peak.
+//
+// Kernels (one wave per SIMD: hi/lo activations of a 32-row tile are 128 registers per layer):
+//   k_point_proj_x3 : P[p] = 2^s0 (W0a [feat | PE(feat)] + b0), fp32 [point][half][tile][16]
+//   k_agg_rows_x3   : 4 waves x 32 rows (4 samples x K = 8): layer 0 (PE(dists) part) on top of
+//                     P[pid], block1.2, block3.0, block3.2 (transposed), alpha, K-blend -> f_s fp32
+//   k_color_x3      : 4 waves x 32 samples: [f_s | PE(viewdir)] -> 128 -> 128 -> 128 -> 3, sigmoid
+// Weight fragment pairs (hi, lo) stream through a 2-slot LDS ring of 64-KiB chunks filled by
+// LDS-DMA, shared by the workgroup's 4 waves (the mlp.hip scheme with 2-KiB pairs).
+#include <cstdio>
+#include <cstdlib>
+#include <cmath>
+#include <utility>
+#include <vector>
+
+#include "agg_device.h"
+
+namespace sgn {
+namespace {
+namespace x3 {
+
+constexpr int NW = 4;             // waves per workgroup (one per SIMD)
+constexpr int TPB = NW * 64;
+constexpr int PAIR = 2048;        // hi fragment (1 KiB) then lo fragment (1 KiB)
+constexpr int SLOT_PAIRS = 32;
+constexpr int SLOT = SLOT_PAIRS * PAIR;  // 64 KiB
+constexpr int NSLOT = 2;
+#ifndef SGN_X3_PD
+#define SGN_X3_PD 2
+#endif
+#ifndef SGN_X3_PIN
+#define SGN_X3_PIN 1
+#endif
+#ifndef SGN_X3_PF
+#define SGN_X3_PF 0  // 1: next tile's P rows loaded during the previous tile's last chunk (spills)
+#endif
+constexpr int PD = SGN_X3_PD;     // fragment pairs in flight per wave (LDS -> VGPR queue)
+
+// ---- blob layout (byte offsets) ------------------------------------------------------
+// pair f of a layer with np passes of tp tiles and ks k-steps: f = (P ks + k) tp + t, output
+// tile P tp + t (k-outer stream order inside a pass, as mlp.hip)
+constexpr uint32_t OFF_W0B = 0;                              // block1.0 PE(dists) part: 4 ks x 8 tiles
+constexpr uint32_t OFF_W1 = OFF_W0B + 32 * PAIR;             // block1.2: 2 x 16 x 4
+constexpr uint32_t OFF_W2 = OFF_W1 + 128 * PAIR;             // block3.0: 2 x 17 x 4
+constexpr uint32_t OFF_W3 = OFF_W2 + 136 * PAIR;             // block3.2: 2 x 16 x 4 (transposed use)
+constexpr uint32_t OFF_C0 = OFF_W3 + 128 * PAIR;             // colour 0: 1 x 18 x 4
+constexpr uint32_t OFF_C1 = OFF_C0 + 72 * PAIR;              // colour 1: 1 x 8 x 4
+constexpr uint32_t OFF_C2 = OFF_C1 + 32 * PAIR;              // colour 2: 1 x 8 x 4
+constexpr uint32_t OFF_W0A = OFF_C2 + 32 * PAIR;             // block1.0 per-point part: 1 x 14 x 8
+constexpr uint32_t OFF_XF32 = OFF_W0A + 112 * PAIR;
+// fp32 section: mlp_layout.h's F_* vectors (biases of MFMA layers pre-scaled by 2^s, block3.2
+// bias natural and unscaled) + the inverse scales 2^-s of the seven MFMA layers
+constexpr int XF_INV = (int)N_F32;  // [0] block1.0 [1] block1.2 [2] block3.0 [3] block3.2 [4..6] colour 0..2
+constexpr int N_XF32 = XF_INV + 8;
+constexpr size_t BLOB_BYTES = OFF_XF32 + (size_t)N_XF32 * 4;
+constexpr size_t PROJ_BYTES_PER_POINT = HID * 4;  // fp32 [half][tile][16]
+
+struct XL {
+    int ks, tp, np, kc;
+    uint32_t off;
+};
+__host__ __device__ constexpr int nch(XL l) { return (l.ks + l.kc - 1) / l.kc; }
+__host__ __device__ constexpr int nk(XL l, int c) { return l.ks - c * l.kc < l.kc ? l.ks - c * l.kc : l.kc; }
+
+// A "net" is the ordered list of layers one kernel streams per work tile.
+struct NetRows {
+    static constexpr int NL = 4;
+    static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, 4, 2, 8, OFF_W1}, {17, 4, 2, 6, OFF_W2},
+                                 {16, 4, 2, 8, OFF_W3}};
+};
+struct NetColor {
+    static constexpr int NL = 3;
+    static constexpr XL L[NL] = {{18, 4, 1, 8, OFF_C0}, {8, 4, 1, 8, OFF_C1}, {8, 4, 1, 8, OFF_C2}};
+};
+struct NetProj {
+    static constexpr int NL = 1;
+    static constexpr XL L[NL] = {{14, 8, 1, 4, OFF_W0A}};
+};
+
+template <class Net>
+struct Sched {
+    static constexpr int layer_chunks(int l) { return Net::L[l].np * nch(Net::L[l]); }
+    static constexpr int base(int l) { return l == 0 ? 0 : base(l - 1) + layer_chunks(l - 1); }
+    static constexpr int total() { return base(Net::NL); }
+    static constexpr int idx(int l, int p, int c) { return base(l) + p * nch(Net::L[l]) + c; }
+    static constexpr int cl(int n, int l = 0) { return (l + 1 >= Net::NL || n < base(l + 1)) ? l : cl(n, l + 1); }
+    static constexpr int cp(int n) { return (n - base(cl(n))) / nch(Net::L[cl(n)]); }
+    static constexpr int cc(int n) { return (n - base(cl(n))) % nch(Net::L[cl(n)]); }
+    static constexpr uint32_t off(int n) {
+        return Net::L[cl(n)].off +
+               (uint32_t)((cp(n) * Net::L[cl(n)].ks + cc(n) * Net::L[cl(n)].kc) * Net::L[cl(n)].tp) * PAIR;
+    }
+    static constexpr int pairs(int n) { return nk(Net::L[cl(n)], cc(n)) * Net::L[cl(n)].tp; }
+};
+static_assert(Sched<NetRows>::total() == 15 && Sched<NetRows>::pairs(0) == 32 && Sched<NetRows>::pairs(7) == 20,
+              "row stream");
+static_assert(Sched<NetColor>::total() == 5 && Sched<NetColor>::pairs(2) == 8, "colour stream");
+static_assert(Sched<NetProj>::total() == 4 && Sched<NetProj>::pairs(3) == 16, "projection stream");
+
+struct X3B {
+    h8 hi, lo;
+};
+
+// x -> (hi, lo): hi = fp16(x), lo = fp16(x - hi) (the difference is exact in fp32)
+__device__ __forceinline__ X3B split8(const float (&v)[8]) {
+    X3B r;
+    r.hi = pack8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+    float d[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = v[e] - (float)r.hi[e];
+    r.lo = pack8(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+    return r;
+}
+
+// one 1-KiB LDS-DMA piece: 16 B per lane from blob byte offset `off` (+ lane * 16)
+__device__ __forceinline__ void lds_dma_1k(const WBlob &wb, char *dst, int lane, uint32_t off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)dst, 16, lane * 16, off,
+                                             0, 0);
+}
+
+// LDS-DMA of stream chunk N into `dst`: 2 * pairs 1-KiB pieces, wave w moves pieces w + NW j
+template <class Net, int N>
+__device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
+    using S = Sched<Net>;
+    constexpr int nf = 2 * S::pairs(N);
+    static_for<(nf + NW - 1) / NW>([&](auto jj) {
+        constexpr int J = decltype(jj)::value;
+        const int i = w + NW * J;
+        if (NW * (J + 1) <= nf || i < nf)  // wave-uniform
+            lds_dma_1k(wb, dst + i * 1024, lane, S::off(N) + (uint32_t)(i * 1024 + lz));
+    });
+}
+
+// chunk boundary: this wave's DMAs of chunk N landed, LDS reads drained, barrier; then chunk N+1
+// goes into the slot every wave finished reading one chunk ago
+template <class Net, int N>
+__device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    dma_chunk<Net, (N + 1) % Sched<Net>::total()>(wb, lds + (slot ^ 1) * SLOT, w, lane, lz);
+}
+
+struct NoHook {
+    template <class C>
+    __device__ void operator()(C) const {}
+};
+
+// One pass of layer L, k-outer: acc[t] += W[tp P + t] in(k) over the pass's chunks, three
+// MFMAs per (k-step, tile).  TRANS: activations are the A operand (accumulators hold D^T).
+// The accumulators arrive initialised (bias, P, or zero).  post(integral_constant C) runs right
+// after the boundary of every chunk C of the pass.
+template <class Net, int L, int P, bool TRANS = false, class InFn, class PostFn = NoHook>
+__device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
+                                         f32x16 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{}) {
+    constexpr XL ly = Net::L[L];
+    constexpr int TP = ly.tp;
+    static_for<nch(ly)>([&](auto cc) {
+        constexpr int C = decltype(cc)::value;
+        chunk_enter<Net, Sched<Net>::idx(L, P, C)>(wb, lds, slot, w, lane, lz);
+        post(cc);
+        const char *sl = lds + slot * SLOT;
+        constexpr int NF = nk(ly, C) * TP;
+        auto frag = [&](int f, int part) { return *(const h8 *)(sl + (2 * f + part) * 1024 + lane * 16); };
+        h8 fh[PD], fl[PD];
+#pragma unroll
+        for (int f = 0; f < PD; ++f) {
+            fh[f] = frag(f, 0);
+            fl[f] = frag(f, 1);
+        }
+#if SGN_X3_PIN
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
+#endif
+        static_for<nk(ly, C)>([&](auto kk) {
+            constexpr int KK = decltype(kk)::value;
+            const X3B B = in(std::integral_constant<int, C * ly.kc + KK>{});
+            static_for<TP>([&](auto tt) {
+                constexpr int t = decltype(tt)::value, F = KK * TP + t;
+                const h8 Ah = fh[F % PD], Al = fl[F % PD];
+                if constexpr (F + PD < NF) {
+                    fh[F % PD] = frag(F + PD, 0);
+                    fl[F % PD] = frag(F + PD, 1);
+                }
+                if constexpr (TRANS) {
+                    acc[t] = mfma32(B.hi, Ah, acc[t]);
+                    acc[t] = mfma32(B.lo, Ah, acc[t]);
+                    acc[t] = mfma32(B.hi, Al, acc[t]);
+                } else {
+                    acc[t] = mfma32(Ah, B.hi, acc[t]);
+                    acc[t] = mfma32(Ah, B.lo, acc[t]);
+                    acc[t] = mfma32(Al, B.hi, acc[t]);
+                }
+#if SGN_X3_PIN
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#endif
+            });
+        });
+        slot ^= 1;
+        __builtin_amdgcn_sched_barrier(0);
+    });
+}
+
+// accumulators (2^s units) -> LeakyReLU(2^-s acc) as next-layer B fragments (hi/lo), tiles
+// TP*P.. -> k-steps 2t, 2t+1 (the chained k order is folded into the packed weights)
+template <int TP, int P, int NOUT>
+__device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], float inv, X3B (&out)[NOUT]) {
+#pragma unroll
+    for (int tt = 0; tt < TP; ++tt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float y = acc[tt][8 * s2 + e] * inv;
+                v[e] = fmaxf(y, 0.01f * y);
+            }
+            out[2 * (TP * P + tt) + s2] = split8(v);
+        }
+}
+
+// accurate sin/cos of x 2^F (the scaling is exact; torch.sin on the product, networks.py:186)
+template <int F>
+__device__ __forceinline__ void sincos_f(float x, float &s, float &c) {
+    sincosf(x * (float)(1 << F), &s, &c);
+}
+
+// ---- per-point block1.0 projection ------------------------------------------------------
+struct ProjArgs {
+    const float *emb;
+    int64_t n;
+    const void *blob;
+    float *proj;
+};
+
+constexpr int LDS_F32_OFF = NSLOT * SLOT;
+constexpr int PROJ_LDS = LDS_F32_OFF + N_XF32 * 4;
+
+__global__ __launch_bounds__(TPB, 1) void k_point_proj_x3(ProjArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[PROJ_LDS];
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const WBlob wb = make_blob(a.blob, BLOB_BYTES);
+    {
+        const float *src = (const float *)((const char *)a.blob + OFF_XF32);
+        float *dst = (float *)(lds + LDS_F32_OFF);
+        for (int i = threadIdx.x; i < N_XF32; i += TPB) dst[i] = src[i];
+    }
+    __syncthreads();
+    int slot = 0;
+    dma_chunk<NetProj, 0>(wb, lds, w, lane, 0);
+    const int64_t ntile = (a.n + 32 * NW - 1) / (32 * NW);
+    for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        const float *Fl = (const float *)(lds + lz + LDS_F32_OFF);
+        const int64_t p = tile * (32 * NW) + w * 32 + (lane & 31);
+        const bool ok = p < a.n;
+        float feat[16];
+        {
+            const f32x4 *e4 = (const f32x4 *)(a.emb + (ok ? p : 0) * 32 + 16 * h);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 v = e4[g];
+                feat[4 * g] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
+            }
+        }
+        // channels 16..111 of the lane-half: PE(feat) (mlp_layout.h l0 order): m = c - 16,
+        // d = m / 6, f = (m % 6) / 2, sin for even m, cos for odd
+        float pe[96];
+        static_for<16>([&](auto dd) {
+            constexpr int d = decltype(dd)::value;
+            static_for<3>([&](auto ff) {
+                constexpr int f = decltype(ff)::value;
+                float s, c;
+                sincos_f<f>(feat[d], s, c);
+                pe[d * 6 + 2 * f] = s;
+                pe[d * 6 + 2 * f + 1] = c;
+            });
+        });
+        f32x16 acc[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const f32x4 *b = (const f32x4 *)(Fl + F_B0 + (t * 2 + h) * 16);
+            const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+            acc[t] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                            b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+        }
+        run_pass<NetProj, 0, 0>(wb, lds + lz, slot, w, lane, lz, acc, [&](auto k) {
+            constexpr int K = decltype(k)::value;
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int c = 8 * K + e;
+                v[e] = c < 16 ? feat[c < 16 ? c : 0] : pe[c >= 16 ? c - 16 : 0];
+            }
+            return split8(v);
+        });
+        if (ok) {
+            f32x4 *dst = (f32x4 *)(a.proj + p * HID + h * 128);  // [half][tile][16]
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    dst[t * 4 + g] = f32x4{acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]};
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- per-neighbour rows --------------------------------------------------------------
+constexpr int WG_SAMPLES = NW * 4;  // 16 samples x 8 neighbours = 128 rows per workgroup tile
+constexpr int FSW_OFF = LDS_F32_OFF + N_XF32 * 4;
+constexpr int FSW_BYTES = NW * 2048;  // [wave][4 samples][128 units] fp32 (one block3.2 pass)
+constexpr int ROWS_LDS = FSW_OFF + FSW_BYTES;
+static_assert(ROWS_LDS <= 163840, "LDS budget");
+
+__device__ __forceinline__ void load_proj_x3(const float *proj, int pid, int lane, f32x16 (&pv)[8]) {
+    const int h = lane >> 5;
+    const f32x16 *src = (const f32x16 *)(proj + (int64_t)(pid < 0 ? 0 : pid) * HID + h * 128);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) pv[t] = src[t];
+}
+
+// PE(dists) of a lane-half: local channels 112..141 (mlp_layout.h): m = c - 112, dd = m / 10,
+// f = (m % 10) / 2, sin for even m, cos for odd; 142, 143 zero -> 4 k-steps (KS_P0..KS_P0+3)
+__device__ __forceinline__ void pe_dists(const float (&dist)[3], X3B (&B)[4]) {
+    float v[32];
+    static_for<3>([&](auto d3) {
+        constexpr int dd = decltype(d3)::value;
+        static_for<5>([&](auto ff) {
+            constexpr int f = decltype(ff)::value;
+            float s, c;
+            sincos_f<f>(dist[dd], s, c);
+            v[dd * 10 + 2 * f] = s;
+            v[dd * 10 + 2 * f + 1] = c;
+        });
+    });
+    v[30] = 0.f;
+    v[31] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float u[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) u[e] = v[8 * k + e];
+        B[k] = split8(u);
+    }
+}
+
+__global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[ROWS_LDS];
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, kk = lane & 7, q = (lane & 31) >> 3;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwork = a.counters[1];
+    const int end = min(nwork, a.item0 + a.n_items);
+    const Cam cam = load_cam(a.campos, a.rot);
+    const WBlob wb = make_blob(a.blob, BLOB_BYTES);
+    const __amdgpu_buffer_rsrc_t fs_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.fs, (short)0, 0x7fffffff, 0x00020000);
+    const float *proj = (const float *)a.proj;
+    {
+        const float *src = (const float *)((const char *)a.blob + OFF_XF32);
+        float *dst = (float *)(lds + LDS_F32_OFF);
+        for (int i = threadIdx.x; i < N_XF32; i += TPB) dst[i] = src[i];
+    }
+    __syncthreads();
+    int slot = 0;
+    dma_chunk<NetRows, 0>(wb, lds, w, lane, 0);
+    RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG_SAMPLES + w * 4 + q, end, lane);
+    asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
+    f32x16 pnext[8];
+    if (SGN_X3_PF && a.item0 + (int)blockIdx.x * WG_SAMPLES < end) load_proj_x3(proj, nx.pid, lane, pnext);
+    const int jl = lane & 31;
+
+    for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        char *ldsi = lds + lz;
+        const float *Fl = (const float *)(ldsi + LDS_F32_OFF);
+        const int item = base + w * 4 + q;
+        const int nitem = item + gridDim.x * WG_SAMPLES;
+        float feat[16], dist[3], extf[8];
+        const RowIn ri = gather_row_f<false>(a, cam, nx, lane, feat, dist, extf);
+        const X3B ext = split8(extf);
+        X3B actA[16], actB[16];
+        {   // block1.0: accumulators start at P[pid] (per-point part), + W0b PE(dists)
+            X3B B0[4];
+            pe_dists(dist, B0);
+            f32x16 acc0[8];
+            if constexpr (!SGN_X3_PF) load_proj_x3(proj, nx.pid, lane, pnext);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc0[t] = pnext[t];
+            run_pass<NetRows, 0, 0>(wb, ldsi, slot, w, lane, lz, acc0,
+                                    [&](auto k) { return B0[decltype(k)::value]; });
+            chain_out<8, 0>(acc0, Fl[XF_INV + 0], actA);
+        }
+        f32x16 acc[4];
+        auto bias_init = [&](int fb, int P) {
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                const f32x4 *b = (const f32x4 *)(Fl + fb + ((4 * P + tt) * 2 + h) * 16);
+                const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+                acc[tt] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                                 b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+            }
+        };
+        // block1.2: 256 -> 256
+        auto inA = [&](auto k) { return actA[decltype(k)::value]; };
+        bias_init(F_B1, 0);
+        run_pass<NetRows, 1, 0>(wb, ldsi, slot, w, lane, lz, acc, inA);
+        chain_out<4, 0>(acc, Fl[XF_INV + 1], actB);
+        bias_init(F_B1, 1);
+        run_pass<NetRows, 1, 1>(wb, ldsi, slot, w, lane, lz, acc, inA);
+        const int s_next = nitem < end ? a.work[nitem] : 0;
+        chain_out<4, 1>(acc, Fl[XF_INV + 1], actB);
+        // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256
+        auto inB = [&](auto k) {
+            constexpr int K = decltype(k)::value;
+            if constexpr (K < 16) return actB[K]; else return ext;
+        };
+        bias_init(F_B2, 0);
+        run_pass<NetRows, 2, 0>(wb, ldsi, slot, w, lane, lz, acc, inB);
+        nx.sval = nitem < end;
+        nx.s = s_next;
+        nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
+        nx.ray = a.samp_ray[s_next];
+        chain_out<4, 0>(acc, Fl[XF_INV + 2], actA);
+        bias_init(F_B2, 1);
+        run_pass<NetRows, 2, 1>(wb, ldsi, slot, w, lane, lz, acc, inB);
+        asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
+        chain_out<4, 1>(acc, Fl[XF_INV + 2], actA);
+        // block3.2: 256 -> 256 transposed (lane = output unit j of tile t, register i = row
+        // (i & 3) + 8 (i >> 2) + 4h), alpha partials and the K-blend as per-lane FMAs
+        float wv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            wv[i] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
+                                                  ((i & 3) + 8 * (i >> 2) + 4 * h) * 4, __builtin_bit_cast(int, ri.wgt)));
+        float ap[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ap[i] = 0.f;
+        const float inv3 = Fl[XF_INV + 3];
+        float fsv[2][8];  // blended features of the pass: [pass][tile tt * 2 + (sample h | h + 2)]
+        auto l3_epilogue = [&](auto pp) {
+            constexpr int P = decltype(pp)::value;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                const int t = 4 * P + tt;
+                const float bu = Fl[F_B3 + 32 * t + jl], wau = Fl[F_WA + 32 * t + jl];
+                float fg[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float y = __builtin_fmaf(acc[tt][i], inv3, bu);
+                    const float hv = fmaxf(y, 0.01f * y);
+                    ap[i] = __builtin_fmaf(wau, hv, ap[i]);
+                    fg[i >> 2] = __builtin_fmaf(wv[i], hv, fg[i >> 2]);
+                }
+                float x0 = fg[0], y0 = fg[1], x1 = fg[2], y1 = fg[3];
+                permlane32_swap(x0, y0);
+                permlane32_swap(x1, y1);
+                fsv[P][2 * tt] = x0 + y0;      // sample h
+                fsv[P][2 * tt + 1] = x1 + y1;  // sample h + 2
+            }
+        };
+        // f_s of pass P -> LDS transpose -> two 16-B stores per lane (sample L >> 4, 8 units)
+        auto flush_fs = [&](int P) {
+            float *st = (float *)(ldsi + FSW_OFF + w * 2048);
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                st[h * 128 + 32 * tt + jl] = fsv[P][2 * tt];
+                st[(h + 2) * 128 + 32 * tt + jl] = fsv[P][2 * tt + 1];
+            }
+            const f32x4 v0 = *(const f32x4 *)(st + (lane >> 4) * 128 + 8 * (lane & 15));
+            const f32x4 v1 = *(const f32x4 *)(st + (lane >> 4) * 128 + 8 * (lane & 15) + 4);
+            const int it = base + w * 4 + (lane >> 4);
+            const uint32_t off = it < end ? (uint32_t)((it - a.item0) * HID + 128 * P + 8 * (lane & 15)) * 4 : 0xFFFF0000u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), fs_rsrc, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), fs_rsrc, off, 16, 0);
+        };
+        auto inA3 = [&](auto k) { return actA[decltype(k)::value]; };
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
+        run_pass<NetRows, 3, 0, true>(wb, ldsi, slot, w, lane, lz, acc, inA3);
+        l3_epilogue(std::integral_constant<int, 0>{});
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
+        // pass-0 stores right after pass 1's first boundary (acknowledged one chunk later); the
+        // next tile's P rows after its last boundary, in flight under that chunk's MFMAs
+        run_pass<NetRows, 3, 1, true>(wb, ldsi, slot, w, lane, lz, acc, inA3, [&](auto c) {
+            if constexpr (decltype(c)::value == 0) flush_fs(0);
+            if constexpr (SGN_X3_PF && decltype(c)::value == nch(NetRows::L[3]) - 1) {
+                if (nx.sval) load_proj_x3(proj, nx.pid, lane, pnext);
+            }
+        });
+        l3_epilogue(std::integral_constant<int, 1>{});
+        flush_fs(1);
+        // alpha: reduce the 16 row partials over the 32 units of each half (mlp.hip's scheme)
+        float bq[8];
+#pragma unroll
+        for (int p2 = 0; p2 < 8; ++p2) {
+            float x = ap[2 * p2], y = ap[2 * p2 + 1];
+            permlane16_swap(x, y);
+            bq[p2] = x + y;
+        }
+        auto rs_step = [&](float lo, float hi, bool upper, auto ctrl) {
+            const float keep = upper ? hi : lo, send = upper ? lo : hi;
+            return keep + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send),
+                                                                             decltype(ctrl)::value, 0xF, 0xF, true));
+        };
+        float cq[4], dq[2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            cq[u] = rs_step(bq[2 * u], bq[2 * u + 1], (jl & 8) != 0, std::integral_constant<int, 0x128>{});
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+            dq[v] = rs_step(cq[2 * v], cq[2 * v + 1], (jl & 4) != 0, std::integral_constant<int, 0x141>{});
+        float eq = rs_step(dq[0], dq[1], (jl & 2) != 0, std::integral_constant<int, 0x4E>{});
+        eq += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, eq), 0xB1, 0xF, 0xF, true));
+        const float alpha_val = softplus(eq + Fl[F_BA] - 1.f);
+        const int ri_ = (jl & 3) + 4 * (jl >> 3);
+        const int src = 32 * ((jl >> 2) & 1) + 2 * ((ri_ >> 3) & 1) + 4 * ((ri_ >> 2) & 1) + 8 * ((ri_ >> 1) & 1) +
+                        16 * (ri_ & 1);
+        const float alpha_row =
+            __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src * 4, __builtin_bit_cast(int, alpha_val)));
+        const float alpha_s = dpp_sum8(ri.wgt * alpha_row);
+        if (ri.sval && kk == 0 && h == 0) a.feat[(int64_t)ri.s * 4 + 0] = alpha_s;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- colour MLP ------------------------------------------------------------------------
+struct ColorArgs {
+    const int32_t *counters, *work, *samp_ray;
+    const float *raydir;
+    const void *blob;
+    const float *fs;
+    float *feat;
+    int32_t item0, n_items;
+};
+constexpr int COL_LDS = LDS_F32_OFF + N_XF32 * 4;
+
+__global__ __launch_bounds__(TPB, 1) void k_color_x3(ColorArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[COL_LDS];
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, j = lane & 31;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwork = a.counters[1];
+    const int end = min(nwork, a.item0 + a.n_items);
+    const WBlob wb = make_blob(a.blob, BLOB_BYTES);
+    {
+        const float *src = (const float *)((const char *)a.blob + OFF_XF32);
+        float *dst = (float *)(lds + LDS_F32_OFF);
+        for (int i = threadIdx.x; i < N_XF32; i += TPB) dst[i] = src[i];
+    }
+    __syncthreads();
+    int slot = 0;
+    dma_chunk<NetColor, 0>(wb, lds, w, lane, 0);
+    for (int base = a.item0 + blockIdx.x * (32 * NW); base < end; base += gridDim.x * (32 * NW)) {
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        char *ldsi = lds + lz;
+        const float *Fc = (const float *)(ldsi + LDS_F32_OFF);
+        const int item = base + w * 32 + j;
+        const bool sval = item < end;
+        const int s = sval ? a.work[item] : 0;
+        const int ray = a.samp_ray[s];
+        X3B x[KS_C0];
+        {
+            const f32x4 *row = (const f32x4 *)(a.fs + (int64_t)(sval ? item - a.item0 : 0) * HID);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {  // units 16 k + 8 h + e (natural order, col_c0)
+                const f32x4 u0 = row[4 * k + 2 * h], u1 = row[4 * k + 2 * h + 1];
+                const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+                x[k] = split8(v);
+            }
+        }
+        // PE(viewdir) ori=True, channels [3:] (point_aggregators.py:579-585, networks.py:175-192):
+        // pe[d*4+f] = sin(v_d 2^f), pe[12+d*4+f] = cos(v_d 2^f)
+        const float v3[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1], a.raydir[(int64_t)ray * 3 + 2]};
+        float pe[24];
+        static_for<3>([&](auto d3) {
+            constexpr int d = decltype(d3)::value;
+            static_for<4>([&](auto ff) {
+                constexpr int f = decltype(ff)::value;
+                sincos_f<f>(v3[d], pe[d * 4 + f], pe[12 + d * 4 + f]);
+            });
+        });
+        {
+            float u[8], z[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                u[e] = h ? pe[8 + e] : pe[e];
+                z[e] = h ? 0.f : pe[16 + e];
+            }
+            x[16] = split8(u);
+            x[17] = split8(z);
+        }
+        f32x16 acc[4];
+        auto bias_init = [&](int fb) {
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                const f32x4 *b = (const f32x4 *)(Fc + fb + (tt * 2 + h) * 16);
+                const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+                acc[tt] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                                 b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+            }
+        };
+        X3B y1[KS_CH], y2[KS_CH];
+        bias_init(F_CB0);
+        run_pass<NetColor, 0, 0>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) { return x[decltype(k)::value]; });
+        chain_out<4, 0>(acc, Fc[XF_INV + 4], y1);
+        bias_init(F_CB1);
+        run_pass<NetColor, 1, 0>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) { return y1[decltype(k)::value]; });
+        chain_out<4, 0>(acc, Fc[XF_INV + 5], y2);
+        bias_init(F_CB2);
+        run_pass<NetColor, 2, 0>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) { return y2[decltype(k)::value]; });
+        const float inv = Fc[XF_INV + 6];
+        float o[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float *w0 = Fc + F_WC3 + (t * 2 + h) * 16;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float y = acc[t][r] * inv;
+                const float hv = fmaxf(y, 0.01f * y);
+                o[0] = __builtin_fmaf(w0[r], hv, o[0]);
+                o[1] = __builtin_fmaf(w0[128 + r], hv, o[1]);
+                o[2] = __builtin_fmaf(w0[256 + r], hv, o[2]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float z = o[c] + __shfl_xor(o[c], 32) + Fc[F_BC3 + c];
+            o[c] = (1.f / (1.f + expf(-z))) * (1.f + 2.f * 0.001f) - 0.001f;
+        }
+        if (sval && h == 0) {
+            a.feat[(int64_t)s * 4 + 1] = o[0];
+            a.feat[(int64_t)s * 4 + 2] = o[1];
+            a.feat[(int64_t)s * 4 + 3] = o[2];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- host-side packing ---------------------------------------------------------------------
+int col_l0(int ks, int p) { return l0_ref_col(p >> 3, 8 * ks + (p & 7)); }
+int col_chain(int ks, int p) { return 16 * ks + perm_acc(p); }
+int col_l2(int ks, int p) { return ks < 16 ? col_chain(ks, p) : (p < 7 ? 256 + p : -1); }
+int col_l0b(int ks, int p) { return l0_ref_col(p >> 3, 8 * (KS_P0 + ks) + (p & 7)); }
+int col_c0(int ks, int p) { return ks < 16 ? 16 * ks + p : (16 * (ks - 16) + p < 24 ? 256 + 16 * (ks - 16) + p : -1); }
+
+// power of two 2^s with max |W| 2^s < 2^14 (so lo parts stay normal fp16 numbers)
+int layer_shift(const float *W, size_t n) {
+    float m = 0.f;
+    for (size_t i = 0; i < n; ++i) m = fmaxf(m, fabsf(W[i]));
+    if (!(m > 0.f) || !std::isfinite(m)) return 0;
+    int e;
+    frexpf(m, &e);  // m < 2^e
+    return 14 - e;
+}
+
+template <typename ColFn>
+void pack_pairs(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles, int KS, int tp, int shift, ColFn col) {
+    const float sc = ldexpf(1.f, shift);
+    for (int tout = 0; tout < n_tiles; ++tout)
+        for (int ks = 0; ks < KS; ++ks) {
+            const size_t f = ((size_t)(tout / tp) * KS + ks) * tp + (tout % tp);
+            for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                    const int row = 32 * tout + (lane & 31);
+                    const int c = col(ks, 8 * (lane >> 5) + e);
+                    const float v = (row < n_out && c >= 0 && c < n_in) ? W[(size_t)row * n_in + c] * sc : 0.f;
+                    const _Float16 hi = (_Float16)v;
+                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    dst[((2 * f) * 64 + lane) * 8 + e] = hi;
+                    dst[((2 * f + 1) * 64 + lane) * 8 + e] = lo;
+                }
+        }
+}
+
+void pack_acc_order(float *dst, const float *v, int n_tiles, float sc) {
+    for (int t = 0; t < n_tiles; ++t)
+        for (int h = 0; h < 2; ++h)
+            for (int r = 0; r < 16; ++r) dst[(t * 2 + h) * 16 + r] = v[32 * t + acc_unit(r, h)] * sc;
+}
+
+void pack_blob_x3(const float *const *w, const float *const *b, uint8_t *blob) {
+    static const int shape[9][2] = {{256, 284}, {256, 256}, {256, 263}, {256, 256}, {1, 256},
+                                    {128, 280}, {128, 128}, {128, 128}, {3, 128}};
+    int s[9] = {};
+    for (int L : {0, 1, 2, 3, 5, 6, 7}) s[L] = layer_shift(w[L], (size_t)shape[L][0] * shape[L][1]);
+    auto fr = [&](uint32_t off) { return (_Float16 *)(blob + off); };
+    pack_pairs(fr(OFF_W0B), w[0], 256, 284, T_HID, KS_L0S, 8, s[0], col_l0b);
+    pack_pairs(fr(OFF_W1), w[1], 256, 256, T_HID, KS_HID, 4, s[1], col_chain);
+    pack_pairs(fr(OFF_W2), w[2], 256, 263, T_HID, KS_L2, 4, s[2], col_l2);
+    pack_pairs(fr(OFF_W3), w[3], 256, 256, T_HID, KS_HID, 4, s[3], col_chain);
+    pack_pairs(fr(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, 4, s[5], col_c0);
+    pack_pairs(fr(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, 4, s[6], col_chain);
+    pack_pairs(fr(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, 4, s[7], col_chain);
+    pack_pairs(fr(OFF_W0A), w[0], 256, 284, T_HID, KS_P0, 8, s[0], [](int ks, int p) { return col_l0(ks, p); });
+    float *F = (float *)(blob + OFF_XF32);
+    pack_acc_order(F + F_B0, b[0], T_HID, ldexpf(1.f, s[0]));
+    pack_acc_order(F + F_B1, b[1], T_HID, ldexpf(1.f, s[1]));
+    pack_acc_order(F + F_B2, b[2], T_HID, ldexpf(1.f, s[2]));
+    for (int u = 0; u < HID; ++u) F[F_B3 + u] = b[3][u];  // natural, unscaled: block3.2 epilogue adds it
+    pack_acc_order(F + F_CB0, b[5], T_CHID, ldexpf(1.f, s[5]));
+    pack_acc_order(F + F_CB1, b[6], T_CHID, ldexpf(1.f, s[6]));
+    pack_acc_order(F + F_CB2, b[7], T_CHID, ldexpf(1.f, s[7]));
+    for (int u = 0; u < HID; ++u) F[F_WA + u] = w[4][u];
+    F[F_BA] = b[4][0];
+    for (int c = 0; c < 3; ++c) {
+        pack_acc_order(F + F_WC3 + c * 128, w[8] + c * 128, T_CHID, 1.f);
+        F[F_BC3 + c] = b[8][c];
+    }
+    const int li[7] = {0, 1, 2, 3, 5, 6, 7};
+    for (int i = 0; i < 7; ++i) F[XF_INV + i] = ldexpf(1.f, -s[li[i]]);
+    F[XF_INV + 7] = 0.f;
+}
+
+}  // namespace x3
+}  // namespace
+}  // namespace sgn
+
+extern "C" {
+
+size_t sgn_mlp_packed_bytes_f32(void) { return sgn::x3::BLOB_BYTES; }
+
+int sgn_mlp_pack_f32(const float *const *w, const float *const *b, void *d_packed, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(w && b && d_packed, "null argument");
+    for (int L = 0; L < 9; ++L) SGN_REQUIRE(w[L] && b[L], "null layer pointer");
+    std::vector<uint8_t> blob(x3::BLOB_BYTES, 0);
+    x3::pack_blob_x3(w, b, blob.data());
+    hipStream_t st = as_stream(stream);
+    SGN_CHECK_HIP(hipMemcpyAsync(d_packed, blob.data(), blob.size(), hipMemcpyHostToDevice, st));
+    SGN_CHECK_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+size_t sgn_point_proj_bytes_f32(int64_t n_points) {
+    return (size_t)(n_points > 0 ? n_points : 0) * sgn::x3::PROJ_BYTES_PER_POINT;
+}
+
+int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void *d_proj, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(pt && d_packed && d_proj, "null argument");
+    SGN_REQUIRE(pt->n_points >= 0 && (pt->n_points == 0 || pt->embedding), "embedding required");
+    SGN_REQUIRE(((uintptr_t)d_proj & 15) == 0 && ((uintptr_t)pt->embedding & 15) == 0, "16-byte alignment required");
+    if (pt->n_points == 0) return 0;
+    x3::ProjArgs a{pt->embedding, pt->n_points, d_packed, (float *)d_proj};
+    const int64_t tiles = (pt->n_points + 32 * x3::NW - 1) / (32 * x3::NW);
+    hipLaunchKernelGGL(x3::k_point_proj_x3, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB), 0,
+                       as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+size_t sgn_aggregate_workspace_bytes_f32(int64_t S) {
+    if (S < 32) S = 32;
+    return (size_t)S * sgn::mlp::HID * sizeof(float);
+}
+
+int sgn_aggregate_f32(const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
+                      int32_t K, const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
+                      void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace && d_point_proj, "null argument");
+    SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
+    SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir, "camera (campos, camrotc2w, raydir) required");
+    SGN_REQUIRE((pt->pers == nullptr) == (pt->samp_pers == nullptr), "pers and samp_pers go together");
+    SGN_REQUIRE(S_capacity >= 0 && S_capacity < (1 << 30), "S_capacity out of range");
+    SGN_REQUIRE(((uintptr_t)d_workspace & 15) == 0 && ((uintptr_t)d_point_proj & 15) == 0, "16-byte alignment required");
+    hipStream_t st = as_stream(stream);
+    const int64_t chunk = (int64_t)(workspace_bytes / (mlp::HID * sizeof(float)));
+    SGN_REQUIRE(chunk >= 32, "aggregate workspace too small");
+    AggArgs a{};
+    a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
+    a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
+    a.pers = pt->pers; a.samp_pers = pt->samp_pers;
+    a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
+    a.samp_locw = q->samp_locw;
+    a.blob = d_packed; a.blob_bytes = x3::BLOB_BYTES;
+    a.proj = (const _Float16 *)d_point_proj;  // fp32 table (k_agg_rows_x3 reads it as float)
+    a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
+    x3::ColorArgs c{q->counters, q->work, q->samp_ray, pt->raydir, d_packed, (const float *)d_workspace, d_out_feat, 0, 0};
+    for (int64_t i0 = 0; i0 < S_capacity; i0 += chunk) {
+        const int64_t n = S_capacity - i0 < chunk ? S_capacity - i0 : chunk;
+        a.item0 = c.item0 = (int32_t)i0;
+        a.n_items = c.n_items = (int32_t)n;
+        const int64_t wg = (n + x3::WG_SAMPLES - 1) / x3::WG_SAMPLES;
+        if (stages & 1)
+            hipLaunchKernelGGL(x3::k_agg_rows_x3, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(x3::TPB), 0, st, a);
+        const int64_t wg2 = (n + 32 * x3::NW - 1) / (32 * x3::NW);
+        if (stages & 2)
+            hipLaunchKernelGGL(x3::k_color_x3, dim3((unsigned)(wg2 < 256 ? wg2 : 256)), dim3(x3::TPB), 0, st, c);
+    }
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

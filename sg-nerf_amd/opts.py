@@ -69,7 +69,10 @@ class HotPathOpts:
     which_render_func: str = "radiance"
     which_blend_func: str = "alpha"
     bg_color: str = "white"
-    # parity-mode knobs of this implementation (no reference counterpart)
+    # knobs of this implementation (no reference counterpart)
+    # aggregator arithmetic: "f32" = the reference's fp32 products, each carried as three fp16 MFMA
+    # products with fp32 accumulation (mlp_x3.hip); "f16" = fp16 MFMA operands (mlp.hip, faster)
+    precision: str = "f32"
     fix_occ0: int = 0          # 1: do not reproduce the `voxel_idx > 0` bug (worldcoords.py:395)
     reservoir_seed: int = 0    # replaces the reference's wall-clock curand seed (:314, :402)
     is_train: int = 0
@@ -126,6 +129,8 @@ class HotPathOpts:
             bad.append("dist_xyz_deno=0, apply_pnt_mask=1, agg_weight_norm=1 required")
         if self.which_render_func != "radiance" or self.which_blend_func != "alpha":
             bad.append("radiance render + alpha blend required")
+        if self.precision not in ("f32", "f16"):
+            bad.append("precision must be 'f32' (reference arithmetic) or 'f16'")
         if self.inverse != 0:
             bad.append("inverse (disparity) ray generation is not implemented")
         if bad:

@@ -78,7 +78,10 @@ class HipRenderer:
         if self.variant != self.opts.bpnet_variant:
             raise ValueError(f"aggregator weights are block2_bpnet variant {self.variant}, options say "
                              f"{self.opts.bpnet_variant} (shading_feature_mlp_layer2_bpnet / predict_semantic)")
-        self.packed = pack_mlp(self.mlp_state, self.device)
+        self.f32 = self.opts.precision == "f32"
+        if self.f32 and self.variant[0]:
+            raise NotImplementedError("block2_bpnet (SG) runs with precision='f16' only")
+        self.packed = pack_mlp(self.mlp_state, self.device, self.opts.precision)
 
     def _buffers(self, R):
         SR = self.opts.SR
@@ -87,7 +90,8 @@ class HipRenderer:
             dev = self.device
             self.feat = torch.empty(cap, 4, dtype=torch.float32, device=dev)
             self.blend = torch.empty(cap, 8, dtype=torch.float32, device=dev)
-            nb = int(_lib.lib().sgn_aggregate_workspace_bytes(cap))
+            L = _lib.lib()
+            nb = int(L.sgn_aggregate_workspace_bytes_f32(cap) if self.f32 else L.sgn_aggregate_workspace_bytes(cap))
             self.agg_ws = torch.empty(nb, dtype=torch.uint8, device=dev)
             self.rgb = torch.empty(max(R, 1), 3, dtype=torch.float32, device=dev)
             self.mask = torch.empty(max(R, 1), dtype=torch.int8, device=dev)
@@ -137,18 +141,27 @@ class HipRenderer:
         bp = _lib.ptr(self.points.bpnet16) if dim else None
         # split block1.0: P[point] = W0a [feat | PE(feat)] + b0 for every point, once per frame
         mark("proj")
-        nproj = int(L.sgn_point_proj_bytes(self.points.n))
+        nproj = int(L.sgn_point_proj_bytes_f32(self.points.n) if self.f32 else L.sgn_point_proj_bytes(self.points.n))
         if self._proj is None or self._proj.numel() < nproj:
             self._proj = torch.empty(max(nproj, 16), dtype=torch.uint8, device=self.device)
-        _lib.check(L.sgn_point_project(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
-                   "sgn_point_project")
+        if self.f32:
+            _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
+                       "sgn_point_project_f32")
+        else:
+            _lib.check(L.sgn_point_project(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
+                       "sgn_point_project")
         for stage, name in ((1, "agg_rows"), (2, "agg_color")):
             mark(name)
-            _lib.check(L.sgn_aggregate_sg(nl, dim, bp, _lib.ptr(self._proj), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
-                                          _lib.ptr(self.packed), _lib.ptr(self.feat),
-                                          _lib.ptr(self.blend) if want_blend else None,
-                                          _lib.ptr(self.wnorm) if want_weights and stage == 1 else None,
-                                          _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate_sg")
+            blend = _lib.ptr(self.blend) if want_blend else None
+            wnorm = _lib.ptr(self.wnorm) if want_weights and stage == 1 else None
+            if self.f32:
+                _lib.check(L.sgn_aggregate_f32(_lib.ptr(self._proj), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
+                                               _lib.ptr(self.packed), _lib.ptr(self.feat), blend, wnorm,
+                                               _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate_f32")
+            else:
+                _lib.check(L.sgn_aggregate_sg(nl, dim, bp, _lib.ptr(self._proj), ctypes.byref(pt), ctypes.byref(qo), cap,
+                                              o.K, _lib.ptr(self.packed), _lib.ptr(self.feat), blend, wnorm,
+                                              _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate_sg")
         mark("composite")
         cp = _lib.CompositeParams()
         cp.SR, cp.vsize_z, cp.raydist_mode_unit = o.SR, float(o.vsize[2]), o.raydist_mode_unit

@@ -88,19 +88,26 @@ def check_shapes(state):
             raise ValueError(f"{name}: expected weight {(o, i)} bias {(o,)}, got {tuple(w.shape)} {tuple(b.shape)}")
 
 
-def pack_mlp(state, device):
-    """fp32 state -> packed fp16 MFMA fragment blob on `device` (uint8 tensor)."""
+def pack_mlp(state, device, precision="f16"):
+    """fp32 state -> packed MFMA fragment blob on `device` (uint8 tensor).  precision "f16":
+    fp16 fragments (mlp.hip); "f32": (hi, lo) fp16 fragment pairs of 2^s-scaled weights plus
+    fp32 biases (mlp_x3.hip, the reference's fp32 arithmetic)."""
     state = strip_prefix(state)
     check_shapes(state)
     nl, dim = mlp_variant(state)
     layers = layers_for(nl, dim)
     L = _lib.lib()
-    nbytes = int(L.sgn_mlp_packed_bytes_sg(nl, dim))
+    if precision == "f32" and nl:
+        raise NotImplementedError("block2_bpnet (SG) is packed for precision 'f16' only")
+    nbytes = int(L.sgn_mlp_packed_bytes_f32() if precision == "f32" else L.sgn_mlp_packed_bytes_sg(nl, dim))
     out = torch.empty(nbytes, dtype=torch.uint8, device=device)
     ws = [np.ascontiguousarray(torch.as_tensor(state[n + ".weight"]).detach().cpu().float().numpy()) for n, *_ in layers]
     bs = [np.ascontiguousarray(torch.as_tensor(state[n + ".bias"]).detach().cpu().float().numpy()) for n, *_ in layers]
     wp = (ctypes.c_void_p * len(layers))(*[w.ctypes.data for w in ws])
     bp = (ctypes.c_void_p * len(layers))(*[b.ctypes.data for b in bs])
     with torch.cuda.device(device):
-        _lib.check(L.sgn_mlp_pack_sg(nl, dim, wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_sg")
+        if precision == "f32":
+            _lib.check(L.sgn_mlp_pack_f32(wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_f32")
+        else:
+            _lib.check(L.sgn_mlp_pack_sg(nl, dim, wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_sg")
     return out
