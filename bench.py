@@ -10,8 +10,10 @@ the timed region; the voxel grid is built once per point cloud (timed separately
 Scene: synthetic "synth-room" (no dataset/checkpoint exists offline),
 random-init aggregator weights of the reference architecture.
 Multi-GPU: frame sharding (weak scaling), rank r renders spiral pose (step*N + r) % 120.
+Precision: the headline runs the aggregator at the reference's fp32 arithmetic (mlp_x3.hip,
+every fp32 product as three fp16 MFMA products); the fp16-operand mode is an extra key.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]      (N > 1: launches N ranks itself)
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -40,6 +42,10 @@ FLOP_PER_ROW_SPLIT = FLOP_PER_NB - 2 * 224 * 256                          # 428,
 FLOP_PER_POINT_PROJ = 2 * 224 * 256                                         # 114,688
 FLOP_PER_SMP = 2 * (280 * 128 + 128 * 128 * 2 + 128 * 3)                 # 137,984
 PEAK_F16_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12  # dense fp16 MFMA, MI355X_MICROARCH.md (~2.5 PF)
+# fp32 mode: each fp32 product is three fp16 MFMA products, so its MFMA ceiling is a third of the
+# fp16 peak (the native f32-input MFMA peak, 157.3 TF, is reported beside it)
+PEAK_X3_TFLOPS = PEAK_F16_TFLOPS / 3
+PEAK_F32_NATIVE_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
@@ -64,12 +70,33 @@ def parse():
                     help="config 5 on the torch-autograd restatement (train.Trainer) instead of the HIP backward")
     ap.add_argument("--sg", action="store_true",
                     help="SG-NeRF variant: semantic-guided kNN + block2_bpnet (352->256) on the config-2 frame")
+    ap.add_argument("--precision", choices=["f32", "f16"], default="f32",
+                    help="aggregator arithmetic of the headline (f32: the reference's; f16: fp16 MFMA operands)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the extra keys (f16-mode frame rate, config-5 training rate)")
     return ap.parse_args()
 
 
-def train_main(args, world, rank, dev, dist):
+def self_launch(args):
+    """`--gpus N` (N > 1) without a launcher: run this script under torch.distributed.run as a
+    child process (one rank per GPU, rendezvous on 127.0.0.1) and return its exit code.  Nothing
+    here touches the GPU, so the child ranks initialise it themselves."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
     """Config 5: one training step = 4096 random rays of a random spiral pose per rank, HIP query,
-    device autograd through aggregator + composite, bucketed RCCL all-reduce, two Adam groups."""
+    device autograd through aggregator + composite, bucketed RCCL all-reduce, two Adam groups.
+    Returns the result dict (rank 0 prints it when run as the headline)."""
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
     from sgnerf_amd.train import PointParams, Trainer
     from sgnerf_amd.train_hip import HipTrainer
     o = HotPathOpts(SR=24, is_train=1)
@@ -79,7 +106,7 @@ def train_main(args, world, rank, dev, dist):
     points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, dev)
     tr = (Trainer if args.train_torch else HipTrainer)(points, mlp, o, dev)
     g = torch.Generator().manual_seed(1 + rank)
-    n_steps = args.warmup + args.steps
+    n_steps = warmup + steps
     batches = []
     for i in range(n_steps):
         v = pose_view(int(torch.randint(0, 120, (1,), generator=g)), args.h, args.w)
@@ -88,7 +115,7 @@ def train_main(args, world, rank, dev, dist):
         batches.append(tuple(x.to(dev) for x in (torch.from_numpy(v.campos), torch.from_numpy(v.camrotc2w),
                                                    torch.from_numpy(v.raydir)[idx], gt)))
     tr.querier = None
-    for i in range(args.warmup):
+    for i in range(warmup):
         c, r_, d, gt = batches[i]
         tr.step(c, r_, d, 0.1, 8.0, gt)
     torch.cuda.synchronize()
@@ -97,7 +124,7 @@ def train_main(args, world, rank, dev, dist):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     losses = []
-    for i in range(args.warmup, n_steps):
+    for i in range(warmup, n_steps):
         c, r_, d, gt = batches[i]
         parts, _, _ = tr.step(c, r_, d, 0.1, 8.0, gt)
         losses.append(parts["total"])
@@ -108,10 +135,10 @@ def train_main(args, world, rank, dev, dist):
     if dist:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(el.item())
-    rays = args.train_rays * args.steps * world
+    rays = args.train_rays * steps * world
     res = {"metric": "training rays/sec, 4096-ray batches with backward, DP (BASELINE config 5)",
-           "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+           "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "f32" if args.train_torch else "f16", "data": "synthetic",
            "config": {"workload": f"synth-room, {args.train_rays} random rays per rank per step, SR=24, K=8, "
                                   f"{args.points} neural points, HIP query + "
@@ -120,8 +147,7 @@ def train_main(args, world, rank, dev, dist):
                                   + " + RCCL all-reduce",
                       "parallelism": f"dp{world}"},
            "final_loss": float(torch.stack(losses).mean().item())}
-    if rank == 0:
-        print(json.dumps(res))
+    return res
 
 
 def lego_pose_view(i, h, w, n_poses=120):
@@ -134,105 +160,98 @@ def pose_view(i, h, w, n_poses=120):
     return scene.room_view(h, w, yaw=yaw + 15.0, pitch=pitch - 5.0)
 
 
-def cpu_baseline(pc, mlp, o, view, stride=4):
-    """Oracle ('port'): C restatement of the query + torch-CPU aggregator/composite, on a
-    bounded sample of the same frame (every `stride`-th pixel in x and y)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import agg_ref
-    import oracle_query as oq
-    from sgnerf_amd.hyper import grid_hyperparameters
-    from sgnerf_amd.raygen import depth_table
-    idx = np.arange(view.h * view.w).reshape(view.h, view.w)[::stride, ::stride].reshape(-1)
-    raydir = view.raydir[idx]
-    hy = grid_hyperparameters(o, torch.from_numpy(pc.xyz.min(0)), torch.from_numpy(pc.xyz.max(0)))
-    og = oq.OracleGrid(pc.xyz, hy, o)
-    t = depth_table(view.near, view.far, o.z_depth_dim).numpy()
-    pts = {k: torch.from_numpy(getattr(pc, k)) for k in ("xyz", "embedding", "color", "dir", "conf")}
-
-    def run(rd):
-        t0 = time.perf_counter()
-        q = og.query(view.campos, rd, t)
-        with torch.no_grad():
-            agg_ref.render(pts, mlp, torch.from_numpy(view.campos), torch.from_numpy(view.camrotc2w),
-                           torch.from_numpy(rd), q, o.SR)
-        return time.perf_counter() - t0
-
-    dt = run(raydir)
-    threads = torch.get_num_threads()
-    # single-thread rate on a quarter of the sample (OpenMP query + torch both pinned to 1)
-    sub = raydir[::4]
-    torch.set_num_threads(1)
-    oq.lib().sgnref_set_threads(1)
-    dt1 = run(sub)
-    torch.set_num_threads(threads)
-    oq.lib().sgnref_set_threads(threads)
-    cpu = "unknown"
+def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": len(idx) / dt, "unit": "rays/s", "cores": threads, "kind": "port",
-            "value_1thread": len(sub) / dt1, "cpu_model": cpu,
-            "sample": f"{len(idx)} rays ({view.h // stride}x{view.w // stride} strided subset of frame 0, SR={o.SR}), "
-                      f"{dt:.2f} s on {threads} threads; 1-thread: {len(sub)} rays in {dt1:.2f} s; "
-                      f"C query (OpenMP) + torch-CPU aggregator/composite"}
+    return "unknown"
 
 
-def main():
-    args = parse()
-    lego = args.scene == "lego"
-    if args.sr is None:
-        args.sr = 128 if lego else 64
-    if args.points is None:
-        args.points = 300_000 if lego else 1_200_000
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    # SGN_BENCH_BACKEND=gloo: rehearsal of the N > 1 code path with every rank on the visible
-    # GPU(s) (RCCL refuses two ranks on one device); frames are then not all-gathered
-    backend = os.environ.get("SGN_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(torch.cuda.device_count(), 1)
-        args.no_gather = True
-    if dist:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            torch.distributed.init_process_group(backend)
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    if args.train:
-        train_main(args, world, rank, dev, dist)
-        if dist:
-            torch.distributed.destroy_process_group()
-        return
+def cpu_baseline(pc, mlp, o, view, stride=4):
+    """Oracle ('port'): C restatement of the query + torch-CPU fp32 aggregator/composite on the GPU
+    box's host cores.  Main number: BASELINE config 1 (one 200x200 view at 32 samples per ray, the
+    reference's CPU case) of the benched scene and pose; beside it a bounded sample of the
+    headline workload itself (every `stride`-th pixel of the 800x800 SR-64 frame) and a
+    1-thread rate."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import agg_ref
+    import oracle_query as oq
+    from dataclasses import replace
+    from sgnerf_amd.hyper import grid_hyperparameters
+    from sgnerf_amd.raygen import depth_table
+    pts = {k: torch.from_numpy(getattr(pc, k)) for k in ("xyz", "embedding", "color", "dir", "conf")}
+
+    def runner(oo):
+        hy = grid_hyperparameters(oo, torch.from_numpy(pc.xyz.min(0)), torch.from_numpy(pc.xyz.max(0)))
+        og = oq.OracleGrid(pc.xyz, hy, oo)
+
+        def run(v, rd):
+            t = depth_table(v.near, v.far, oo.z_depth_dim).numpy()
+            t0 = time.perf_counter()
+            q = og.query(v.campos, rd, t)
+            with torch.no_grad():
+                agg_ref.render(pts, mlp, torch.from_numpy(v.campos), torch.from_numpy(v.camrotc2w),
+                               torch.from_numpy(rd), q, oo.SR)
+            return time.perf_counter() - t0
+        return run
+
+    threads = torch.get_num_threads()
+    # config 1: 200x200 view of the same pose (focal scaled with the image), SR 32
+    yaw, pitch = scene.spiral_yaw_pitch(0, 120)
+    v1 = scene.room_view(200, 200, yaw=yaw + 15.0, pitch=pitch - 5.0)
+    run1 = runner(replace(o, SR=32))
+    dt_c1 = run1(v1, v1.raydir)
+    # sample of the headline workload (SR 64)
+    idx = np.arange(view.h * view.w).reshape(view.h, view.w)[::stride, ::stride].reshape(-1)
+    run2 = runner(o)
+    dt2 = run2(view, view.raydir[idx])
+    sub = view.raydir[idx][::4]
+    torch.set_num_threads(1)
+    oq.lib().sgnref_set_threads(1)
+    dt1 = run2(view, sub)
+    torch.set_num_threads(threads)
+    oq.lib().sgnref_set_threads(threads)
+    n1 = v1.raydir.shape[0]
+    return {"value": n1 / dt_c1, "unit": "rays/s", "cores": threads, "kind": "port",
+            "ms_per_frame": dt_c1 * 1e3,
+            "sample": f"BASELINE config 1: one 200x200 view (focal 100) of the benched scene at SR=32, {n1} rays in "
+                      f"{dt_c1:.2f} s on {threads} threads; C query (OpenMP) + torch-CPU fp32 aggregator/composite",
+            "config2_sample": {"value": len(idx) / dt2, "unit": "rays/s", "cores": threads,
+                               "sample": f"{len(idx)} rays ({view.h // stride}x{view.w // stride} strided subset of "
+                                         f"the 800x800 SR={o.SR} frame 0) in {dt2:.2f} s"},
+            "value_1thread": len(sub) / dt1,
+            "sample_1thread": f"{len(sub)} rays of the config-2 sample in {dt1:.2f} s on 1 thread",
+            "cpu_model": _cpu_model()}
+
+
+def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, want_stats=True):
+    """Headline-shaped frame loop at `precision`; returns the result fields (no cpu baseline)."""
     sg = dict(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1) if args.sg else {}
-    o = HotPathOpts(SR=args.sr, **sg)
+    o = HotPathOpts(SR=args.sr, precision=precision, **sg)
     pc = scene.lego_standin(args.points, seed=0) if lego else scene.synth_room(args.points, seed=0)
     if args.sg:
         pc = scene.with_semantics(pc, seed=1, n_classes=20, cell=0.5)
     mlp = init_mlp(0, bias_std=0.01, bpnet_layers=1 if args.sg else 0, bpnet_dim=96 if args.sg else 0)
     mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0  # opaque surfaces, as a trained scene
     r = HipRenderer(PointTables.from_cloud(pc, dev), mlp, o, dev)
-    n_frames = args.warmup + args.steps
+    n_frames = warmup + steps
     poses = [(s * world + rank) for s in range(n_frames)]
     views = [(lego_pose_view if lego else pose_view)(p, args.h, args.w) for p in poses]
     rays = [torch.from_numpy(v.raydir).to(dev) for v in views]
     cams = [(torch.from_numpy(v.campos).to(dev), torch.from_numpy(v.camrotc2w).to(dev)) for v in views]
     R = args.h * args.w
-    # grid build (once per point cloud), timed separately
+    # grid build (once per point cloud), timed separately: host-synchronous wall time of the first
+    # build (two size read-backs inside) and the HIP-event time of a rebuild
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     r.querier.grid_for(r.points.xyz)
     torch.cuda.synchronize()
     grid_ms = (time.perf_counter() - t0) * 1e3
-    gathered = torch.empty(world * R, 3, dtype=torch.float32, device=dev) if dist and not args.no_gather else None
+    gathered = [torch.empty(world * R, 3, dtype=torch.float32, device=dev) for _ in range(2)] \
+        if dist and not args.no_gather else None
 
     sem = [{} for _ in range(n_frames)]
     if args.sg:
@@ -252,17 +271,40 @@ def main():
             rl[has] = pl[q.pidx[first[has] * 8].long()]
             sem[i] = dict(point_labels=pl, ray_labels=rl.contiguous(), seconds=12)
 
+    # N > 1: the finished frame is all-gathered on a side stream while the next frame renders;
+    # frames alternate between two colour buffers so the collective never reads a buffer the
+    # renderer is writing
+    comm = torch.cuda.Stream(dev) if gathered is not None else None
+    rgb_bufs = [None, None]
+    gather_done = [None, None]
+
     def frame(i, marks=None, count=False):
-        out = r.render(cams[i][0], cams[i][1], rays[i], views[i].near, views[i].far, want_opacity=False, marks=marks,
+        out = r.render(cams[i][0], cams[i][1], rays[i], views[i].near, views[i].far, want_opacity=True, marks=marks,
                        count_traffic=count, **sem[i])
         if gathered is not None:
-            torch.distributed.all_gather_into_tensor(gathered, out.rgb)
+            b = i & 1
+            if rgb_bufs[b] is None:
+                rgb_bufs[b] = torch.empty_like(out.rgb)
+            if gather_done[b] is not None:  # the gather of frame i - 2 still reads this buffer
+                torch.cuda.current_stream().wait_event(gather_done[b])
+            rgb_bufs[b].copy_(out.rgb)
+            ready = torch.cuda.Event()
+            ready.record()
+            with torch.cuda.stream(comm):
+                comm.wait_event(ready)
+                torch.distributed.all_gather_into_tensor(gathered[b], rgb_bufs[b])
+                gather_done[b] = torch.cuda.Event()
+                gather_done[b].record(comm)
         return out
 
-    for i in range(args.warmup):
+    def drain():
+        if comm is not None:
+            torch.cuda.current_stream().wait_stream(comm)
+
+    for i in range(warmup):
         frame(i)
+        drain()
     torch.cuda.synchronize()
-    # timed region
     events = []
 
     def marks(name):
@@ -274,9 +316,10 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.warmup, n_frames):
+    for i in range(warmup, n_frames):
         events.append({})
         frame(i, marks)
+    drain()
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
@@ -289,10 +332,28 @@ def main():
     order = stage_names + ["end"]
     stage_ms = {n: float(np.mean([ev[n].elapsed_time(ev[order[j + 1]]) for ev in events]))
                 for j, n in enumerate(stage_names)}
+    total_rays = R * steps * world
+    res = {"value": total_rays / elapsed, "ms_per_frame": elapsed / steps * 1e3, "stages_ms": stage_ms,
+           "grid_build_ms": grid_ms, "o": o, "r": r, "pc": pc, "mlp": mlp, "views": views}
+    if not want_stats:
+        return res
+    # grid rebuild on the device clock (no host read-back inside the timed span: the build's two
+    # size read-backs synchronise, so this is wall time of the stream with those syncs)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    e0.record()
+    from sgnerf_amd.querier import HipGrid
+    g2 = HipGrid(r.points.xyz, o)
+    e1.record()
+    torch.cuda.synchronize()
+    g2.close()
+    res["grid_rebuild_ms"] = {"hip_events": e0.elapsed_time(e1), "wall": (time.perf_counter() - t1) * 1e3}
     # occupancy / algorithmic work of the timed frames (deterministic re-render, untimed)
     n_nb, n_smp, n_samples, q_bytes = [], [], [], []
-    for i in range(args.warmup, n_frames):
+    for i in range(warmup, n_frames):
         out = frame(i, count=True)
+        drain()
         q = out.query
         S = q.n_samples()
         cnt = [c & 0xFFFFFFFF for c in q.counters.tolist()]  # [3] is uint32
@@ -305,32 +366,80 @@ def main():
         q_bytes.append(R * (12 + 4 + 4 + 2 * args.sr) + 4 * cnt[2] + 16 * cnt[3] + S * (4 + 4 + 12 + 12 + 4 + 4 * 8)
                        + 4 * W)
     torch.cuda.synchronize()
+    res.update(n_nb=float(np.mean(n_nb)), n_smp=float(np.mean(n_smp)), n_samples=float(np.mean(n_samples)),
+               q_bytes=float(np.mean(q_bytes)))
+    return res
+
+
+def main():
+    args = parse()
+    lego = args.scene == "lego"
+    if args.sr is None:
+        args.sr = 128 if lego else 64
+    if args.points is None:
+        args.points = 300_000 if lego else 1_200_000
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch with matching counts)")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    # SGN_BENCH_BACKEND=gloo: rehearsal of the N > 1 code path with every rank on the visible
+    # GPU(s) (RCCL refuses two ranks on one device); frames are then not all-gathered
+    backend = os.environ.get("SGN_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
+        args.no_gather = True
+    if dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if args.train:
+        res = train_main(args, world, rank, dev, dist)
+        if rank == 0:
+            print(json.dumps(res))
+        if dist:
+            torch.distributed.destroy_process_group()
+        return
+    if args.sg and args.precision == "f32":
+        args.precision = "f16"  # block2_bpnet is built for the fp16-operand kernels only
+    x3 = args.precision == "f32"
+    h = render_run(args, args.precision, world, rank, dev, dist, args.steps, args.warmup, lego)
+    R = args.h * args.w
+    stage_ms = h["stages_ms"]
     flop_nb = FLOP_PER_ROW_SPLIT + (2 * 352 * 256 if args.sg else 0)  # + block2_bpnet.0 (SG)
-    rows_flop = flop_nb * float(np.mean(n_nb))
-    ref_flop = (FLOP_PER_NB + (2 * 352 * 256 if args.sg else 0)) * float(np.mean(n_nb))
+    rows_flop = flop_nb * h["n_nb"]
+    ref_flop = (FLOP_PER_NB + (2 * 352 * 256 if args.sg else 0)) * h["n_nb"]
     achieved = rows_flop / (stage_ms["agg_rows"] * 1e-3) / 1e12
+    peak = PEAK_X3_TFLOPS if x3 else PEAK_F16_TFLOPS
+    kname = "k_agg_rows_x3" if x3 else "k_agg_rows"
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("kernel") and tj.get("workload_key") == f"{args.h}x{args.w}x{args.sr}":
+            if tj.get("kernel") == kname and tj.get("workload_key") == f"{args.h}x{args.w}x{args.sr}":
                 traffic = tj.get("bytes_per_launch")
         except Exception:
             traffic = None
-    total_rays = R * args.steps * world
-    value = total_rays / elapsed
     res = {
         "metric": METRIC,
-        "value": value,
+        "value": h["value"],
         "unit": "rays/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": h["ms_per_frame"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f16",
+        "dtype": "f32 (3xf16 split MFMA, fp32 accumulate)" if x3 else "f16",
         "data": "synthetic",
         "config": {
             "workload": (f"synth-lego stand-in {args.h}x{args.w} rays x SR={args.sr} samples, D=400, K=8, P=26, "
@@ -340,14 +449,18 @@ def main():
                          f"{args.points} neural points (BASELINE config 2, 1 frame per rank per step)")
                         + (" + SG-NeRF variant: semantic-guided kNN (20 labels), block2_bpnet 352->256" if args.sg else ""),
             "rays_per_frame": R, "SR": args.sr, "K": 8, "D": 400, "points": args.points,
-            "parallelism": f"frame-sharded x{world}" + ("" if gathered is None else " + all-gather of frames"),
+            "parallelism": f"frame-sharded x{world}" + ("" if (not dist or args.no_gather)
+                                                         else " + all-gather of frames (side stream, double-buffered)"),
             "mlp": "viewmlp 284-256-256 / 263-256-256 / alpha / colour 280-128x3-3 (341,764 params, random init)",
+            "outputs": "rgb, ray mask, background transmission, coarse_point_opacity [R, SR]",
         },
         "roofline": {
-            "kernel": "k_agg_rows (per-neighbour MLP 284->256->256->" + ("352->256->" if args.sg else "")
+            "kernel": kname + " (per-neighbour MLP 284->256->256->" + ("352->256->" if args.sg else "")
                       + "263->256->256 + alpha + K-blend)",
-            "bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / PEAK_F16_TFLOPS, "traffic": traffic,
+            "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+            "frac": achieved / peak, "traffic": traffic,
+            "peak_note": ("fp16 dense MFMA peak / 3 (each fp32 product = 3 fp16 MFMA products); native f32-input "
+                          f"MFMA peak {PEAK_F32_NATIVE_TFLOPS} TF/s") if x3 else "fp16 dense MFMA peak",
             "flop_per_launch": rows_flop, "flop_per_valid_row": flop_nb, "avg_launch_ms": stage_ms["agg_rows"],
             "reference_formulation_TFLOPs": ref_flop / (stage_ms["agg_rows"] * 1e-3) / 1e12,
         },
@@ -357,26 +470,41 @@ def main():
             # counted each time a sample reads it.  Most of those re-reads hit L2/MALL, so this
             # effective rate can exceed the HBM peak; HBM bytes proper come from the PMC passes
             # (profiles/, FETCH_SIZE + WRITE_SIZE of k_knn / k_march).
-            "effective_GBps_no_reuse_credit": float(np.mean(q_bytes)) / (stage_ms["query"] * 1e-3) / 1e9,
+            "effective_GBps_no_reuse_credit": h["q_bytes"] / (stage_ms["query"] * 1e-3) / 1e9,
             "hbm_peak_GBps": PEAK_HBM_GBS,
-            "bytes_per_frame_no_reuse_credit": float(np.mean(q_bytes)),
+            "bytes_per_frame_no_reuse_credit": h["q_bytes"],
         },
         "roofline_proj": {
-            "kernel": "k_point_proj (block1.0 point inputs, all points, once per frame)", "bound": "mfma",
-            "achieved": FLOP_PER_POINT_PROJ * args.points / (stage_ms["proj"] * 1e-3) / 1e12, "peak": PEAK_F16_TFLOPS,
-            "unit": "TFLOP/s", "avg_launch_ms": stage_ms["proj"],
+            "kernel": ("k_point_proj_x3" if x3 else "k_point_proj") + " (block1.0 point inputs, all points, once per frame)",
+            "bound": "mfma", "achieved": FLOP_PER_POINT_PROJ * args.points / (stage_ms["proj"] * 1e-3) / 1e12,
+            "peak": peak, "unit": "TFLOP/s", "avg_launch_ms": stage_ms["proj"],
         },
         "stages_ms": stage_ms,
-        "grid_build_ms": grid_ms,
+        "grid_build_ms": h["grid_build_ms"],
+        "grid_rebuild_ms": h["grid_rebuild_ms"],
         "occupancy": {
-            "samples_per_ray": float(np.mean(n_samples)) / R,
-            "valid_samples_per_ray": float(np.mean(n_smp)) / R,
-            "valid_neighbours_per_ray": float(np.mean(n_nb)) / R,
+            "samples_per_ray": h["n_samples"] / R,
+            "valid_samples_per_ray": h["n_smp"] / R,
+            "valid_neighbours_per_ray": h["n_nb"] / R,
         },
-        "ms_per_frame": elapsed / args.steps * 1e3,
+        "ms_per_frame": h["ms_per_frame"],
     }
+    if not args.no_extras and not args.sg:
+        # the other arithmetic mode on the same frames (extra key; the headline stays the reference's fp32)
+        other = "f16" if x3 else "f32"
+        e = render_run(args, other, world, rank, dev, dist, args.steps, args.warmup, lego, want_stats=False)
+        peak_o = PEAK_F16_TFLOPS if x3 else PEAK_X3_TFLOPS
+        res[f"{other}_mode"] = {"value": e["value"], "unit": "rays/s", "ms_per_frame": e["ms_per_frame"],
+                                "dtype": "f16" if x3 else "f32 (3xf16 split MFMA)", "stages_ms": e["stages_ms"],
+                                "roofline_frac": rows_flop / (e["stages_ms"]["agg_rows"] * 1e-3) / 1e12 / peak_o}
+        del e
+        torch.cuda.empty_cache()
+        # BASELINE config 5 (training step, 4096-ray batches, DP over the ranks)
+        tr = train_main(args, world, rank, dev, dist, steps=max(args.steps, 20), warmup=5)
+        res["train_config5"] = {k: tr[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype",
+                                                      "final_loss", "config")}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(pc, mlp, o, views[0])
+        res["cpu_baseline"] = cpu_baseline(h["pc"], h["mlp"], h["o"], h["views"][0])
     if rank == 0:
         print(json.dumps(res))
     if dist:
