@@ -200,19 +200,24 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
  * 2^-s (w_hi x_hi + w_hi x_lo + w_lo x_hi) with fp32 accumulation (w pre-scaled by a per-layer
  * power of two 2^s; x = x_hi + x_lo), positional encodings from accurate sinf/cosf.  The results
  * agree with an fp32 evaluation to a few fp32 ulps of sum |w x| per layer.  Hidden activations
- * must stay inside fp16 range (|x| < 65504).  Base ScanNet viewmlp (no block2_bpnet).
- *   sgn_mlp_pack_f32        : 9 layers as sgn_mlp_pack -> blob of sgn_mlp_packed_bytes_f32()
+ * must stay inside fp16 range (|x| < 65504).  bpnet_layers / bpnet_dim select the SG-NeRF
+ * block2_bpnet variant as in sgn_mlp_pack_sg (0/0 = base ScanNet viewmlp).
+ *   sgn_mlp_pack_f32        : 9 (+ block2_bpnet.0) layers as sgn_mlp_pack_sg -> blob of
+ *                             sgn_mlp_packed_bytes_f32(bpnet_layers, bpnet_dim) bytes (0: unsupported)
  *   sgn_point_project_f32   : P[p] fp32 (sgn_point_proj_bytes_f32(N)), the block1.0 per-point part
- *   sgn_aggregate_f32       : as sgn_aggregate (same outputs, stages bits), d_point_proj required;
+ *   sgn_aggregate_f32       : as sgn_aggregate_sg (same outputs, stages bits), d_point_proj required;
+ *                             d_bpnet = fp32 [N, 96] BPNet point embedding when bpnet_dim = 96;
  *                             workspace sgn_aggregate_workspace_bytes_f32(S) (fp32 blended features)
  * 16-byte aligned device buffers. */
-size_t sgn_mlp_packed_bytes_f32(void);
-int sgn_mlp_pack_f32(const float *const *w, const float *const *b, void *d_packed, sgn_stream_t stream);
+size_t sgn_mlp_packed_bytes_f32(int32_t bpnet_layers, int32_t bpnet_dim);
+int sgn_mlp_pack_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,
+                     void *d_packed, sgn_stream_t stream);
 size_t sgn_point_proj_bytes_f32(int64_t n_points);
 int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed_mlp, void *d_proj, sgn_stream_t stream);
 size_t sgn_aggregate_workspace_bytes_f32(int64_t S);
-int sgn_aggregate_f32(const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
-                      int32_t K, const void *d_packed_mlp, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
+int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet, const void *d_point_proj,
+                      const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                      const void *d_packed_mlp, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
                       void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream);
 
 /* ---- training: forward with saved activations + backward ---

@@ -100,12 +100,12 @@ SIGNATURES = {
                                ctypes.c_double, c_i64, c_i32, c_vp]),
     "sgn_colsum_workspace_bytes": (c_sz, [c_i32]),
     "sgn_colsum_f16": (c_i32, [c_i32, ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp, c_vp]),
-    "sgn_mlp_packed_bytes_f32": (c_sz, []),
-    "sgn_mlp_pack_f32": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
+    "sgn_mlp_packed_bytes_f32": (c_sz, [c_i32, c_i32]),
+    "sgn_mlp_pack_f32": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
     "sgn_point_proj_bytes_f32": (c_sz, [c_i64]),
     "sgn_point_project_f32": (c_i32, [ctypes.POINTER(PointTables), c_vp, c_vp, c_vp]),
     "sgn_aggregate_workspace_bytes_f32": (c_sz, [c_i64]),
-    "sgn_aggregate_f32": (c_i32, [c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32, c_vp,
+    "sgn_aggregate_f32": (c_i32, [c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
                               c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -87,6 +87,7 @@ struct AggArgs {
     const void *blob;
     size_t blob_bytes;
     const _Float16 *bpnet;  // [N, bpnet_dim] fp16 (SG variant with predict_semantic = 1), else null
+    const float *bpnet32;   // [N, bpnet_dim] fp32 (the same table for the fp32-faithful kernels)
     // outputs
     float *feat;      // float4 per sample id: .x alpha written here
     float *blend;     // [S*8] weight * conf (optional)

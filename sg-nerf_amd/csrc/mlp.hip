@@ -1106,9 +1106,13 @@ int sgn_mlp_pack_index(int32_t which, int32_t *out, int64_t n) {
     return 0;
 }
 
+// Work items per launch: the blended features are stored through a buffer descriptor (31-bit
+// byte range) based at the launch's first item, so at most 2^31 / 512 B items per launch.
+constexpr int64_t F16_MAX_CHUNK = ((int64_t)0x7fffffff / (sgn::mlp::HID * 2)) / 32 * 32;
+
 size_t sgn_aggregate_workspace_bytes(int64_t S) {
-    // blended-feature rows of every possible work item (fp16, 512 B each): one launch per
-    // stage; a smaller workspace is accepted and processed in chunks.
+    // blended-feature rows of every work item (fp16, 512 B each), so the two stages may be called
+    // separately; a smaller workspace is accepted with stages = 3 (both stages per chunk)
     if (S < 32) S = 32;
     return (size_t)S * sgn::mlp::HID * sizeof(_Float16);
 }
@@ -1125,8 +1129,13 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
     SGN_REQUIRE(ksb <= KS_HID || d_bpnet_f16, "bpnet_dim > 0 needs the fp16 BPNet point embedding");
     SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
     hipStream_t st = as_stream(stream);
-    int64_t chunk = (int64_t)(workspace_bytes / (HID * sizeof(_Float16)));
-    SGN_REQUIRE(chunk >= 32, "aggregate workspace too small");
+    const int64_t ws_items = (int64_t)(workspace_bytes / (HID * sizeof(_Float16)));
+    SGN_REQUIRE(ws_items >= 32, "aggregate workspace too small");
+    SGN_REQUIRE(stages == 3 || ws_items >= S_capacity,
+                "stages 1 and 2 called separately need a workspace for all S_capacity items");
+    // chunk = items per launch; with a full-size workspace chunk c keeps its rows at item c * chunk
+    const bool full = ws_items >= S_capacity;
+    const int64_t chunk = ws_items < F16_MAX_CHUNK ? ws_items : F16_MAX_CHUNK;
     const uint8_t *P = (const uint8_t *)d_packed;
     AggArgs a;
     a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
@@ -1148,6 +1157,8 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
         int64_t n = S_capacity - i0 < chunk ? S_capacity - i0 : chunk;
         a.item0 = c.item0 = (int32_t)i0;
         a.n_items = c.n_items = (int32_t)n;
+        a.fs = (_Float16 *)d_workspace + (full ? i0 * HID : 0);
+        c.fs = a.fs;
         int64_t wg = (n + WG_SAMPLES - 1) / WG_SAMPLES;  // persistent: one workgroup per CU
         dim3 g1((unsigned)(wg < 256 ? wg : 256));
         if (stages & 1) {

@@ -65,10 +65,16 @@ constexpr uint32_t OFF_C2 = OFF_C1 + 32 * PAIR;              // colour 2: 1 x 8 
 constexpr uint32_t OFF_W0A = OFF_C2 + 32 * PAIR;             // block1.0 per-point part: 1 x 14 x 8
 constexpr uint32_t OFF_XF32 = OFF_W0A + 112 * PAIR;
 // fp32 section: mlp_layout.h's F_* vectors (biases of MFMA layers pre-scaled by 2^s, block3.2
-// bias natural and unscaled) + the inverse scales 2^-s of the seven MFMA layers
-constexpr int XF_INV = (int)N_F32;  // [0] block1.0 [1] block1.2 [2] block3.0 [3] block3.2 [4..6] colour 0..2
-constexpr int N_XF32 = XF_INV + 8;
+// bias natural and unscaled) + the inverse scales 2^-s of the MFMA layers + block2_bpnet's bias
+constexpr int XF_INV = (int)N_F32;  // [0] block1.0 [1] block1.2 [2] block3.0 [3] block3.2 [4..6] colour 0..2 [7] block2_bpnet
+constexpr int XF_BB = XF_INV + 8;   // block2_bpnet.0 bias (acc order, scaled; SG only)
+constexpr int N_XF32 = XF_BB + HID;
 constexpr size_t BLOB_BYTES = OFF_XF32 + (size_t)N_XF32 * 4;
+// SG-NeRF block2_bpnet.0 (Linear(256 + bpnet_dim -> 256), point_aggregators.py:345-354, :629-636):
+// 2 passes x KSB k-steps x 4 tiles after the base blob; k-steps 0..15 the chained block1 output,
+// 16.. the gathered fp32 BPNet embedding (channel 16 (k - 16) + 8 h + e, natural order)
+constexpr uint32_t OFF_WB = (uint32_t)((BLOB_BYTES + PAIR - 1) / PAIR * PAIR);
+__host__ __device__ constexpr size_t blob_bytes_sg(int ksb) { return ksb ? OFF_WB + (size_t)8 * ksb * PAIR : BLOB_BYTES; }
 constexpr size_t PROJ_BYTES_PER_POINT = HID * 4;  // fp32 [half][tile][16]
 
 struct XL {
@@ -83,6 +89,12 @@ struct NetRows {
     static constexpr int NL = 4;
     static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, 4, 2, 8, OFF_W1}, {17, 4, 2, 6, OFF_W2},
                                  {16, 4, 2, 8, OFF_W3}};
+};
+template <int KSB>
+struct NetRowsSG {
+    static constexpr int NL = 5;
+    static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, 4, 2, 8, OFF_W1}, {KSB, 4, 2, 8, OFF_WB},
+                                 {17, 4, 2, 6, OFF_W2}, {16, 4, 2, 8, OFF_W3}};
 };
 struct NetColor {
     static constexpr int NL = 3;
@@ -366,7 +378,12 @@ __device__ __forceinline__ void pe_dists(const float (&dist)[3], X3B (&B)[4]) {
     }
 }
 
+// KSB: k-steps of block2_bpnet.0 (0: base ScanNet viewmlp; 16: SG with bpnet_dim 0; 22: bpnet_dim 96)
+template <int KSB>
 __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
+    using Net = std::conditional_t<(KSB > 0), NetRowsSG<KSB>, NetRows>;
+    constexpr int LB = 2, L2 = KSB ? 3 : 2, L3 = KSB ? 4 : 3;  // stream positions of the layers
+    constexpr int NBP = KSB > KS_HID ? KSB - KS_HID : 0;        // BPNet k-steps
     __shared__ __attribute__((aligned(16))) char lds[ROWS_LDS];
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, kk = lane & 7, q = (lane & 31) >> 3;
@@ -374,7 +391,7 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
     const int nwork = a.counters[1];
     const int end = min(nwork, a.item0 + a.n_items);
     const Cam cam = load_cam(a.campos, a.rot);
-    const WBlob wb = make_blob(a.blob, BLOB_BYTES);
+    const WBlob wb = make_blob(a.blob, blob_bytes_sg(KSB));
     const __amdgpu_buffer_rsrc_t fs_rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.fs, (short)0, 0x7fffffff, 0x00020000);
     const float *proj = (const float *)a.proj;
@@ -385,7 +402,7 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
     }
     __syncthreads();
     int slot = 0;
-    dma_chunk<NetRows, 0>(wb, lds, w, lane, 0);
+    dma_chunk<Net, 0>(wb, lds, w, lane, 0);
     RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG_SAMPLES + w * 4 + q, end, lane);
     asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
     f32x16 pnext[8];
@@ -410,8 +427,7 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
             if constexpr (!SGN_X3_PF) load_proj_x3(proj, nx.pid, lane, pnext);
 #pragma unroll
             for (int t = 0; t < 8; ++t) acc0[t] = pnext[t];
-            run_pass<NetRows, 0, 0>(wb, ldsi, slot, w, lane, lz, acc0,
-                                    [&](auto k) { return B0[decltype(k)::value]; });
+            run_pass<Net, 0, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) { return B0[decltype(k)::value]; });
             chain_out<8, 0>(acc0, Fl[XF_INV + 0], actA);
         }
         f32x16 acc[4];
@@ -427,28 +443,54 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
         // block1.2: 256 -> 256
         auto inA = [&](auto k) { return actA[decltype(k)::value]; };
         bias_init(F_B1, 0);
-        run_pass<NetRows, 1, 0>(wb, ldsi, slot, w, lane, lz, acc, inA);
+        run_pass<Net, 1, 0>(wb, ldsi, slot, w, lane, lz, acc, inA);
         chain_out<4, 0>(acc, Fl[XF_INV + 1], actB);
         bias_init(F_B1, 1);
-        run_pass<NetRows, 1, 1>(wb, ldsi, slot, w, lane, lz, acc, inA);
+        run_pass<Net, 1, 1>(wb, ldsi, slot, w, lane, lz, acc, inA);
         const int s_next = nitem < end ? a.work[nitem] : 0;
         chain_out<4, 1>(acc, Fl[XF_INV + 1], actB);
-        // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256
+        if constexpr (KSB > 0) {
+            // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256; the row's fp32 embedding
+            // (channels 16 j + 8 h .. +7 for k-step 16 + j) is gathered and split here
+            X3B bpv[NBP > 0 ? NBP : 1];
+            if constexpr (NBP > 0) {
+                const float *src = a.bpnet32 + (int64_t)(ri.pid < 0 ? 0 : ri.pid) * (NBP * 16) + 8 * h;
+#pragma unroll
+                for (int j = 0; j < NBP; ++j) {
+                    const f32x4 u0 = *(const f32x4 *)(src + 16 * j), u1 = *(const f32x4 *)(src + 16 * j + 4);
+                    const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+                    bpv[j] = split8(v);
+                }
+            }
+            auto inBP = [&](auto k) {
+                constexpr int K = decltype(k)::value;
+                if constexpr (K < 16) return actB[K]; else return bpv[K - 16];
+            };
+            bias_init(XF_BB, 0);
+            run_pass<Net, LB, 0>(wb, ldsi, slot, w, lane, lz, acc, inBP);
+            chain_out<4, 0>(acc, Fl[XF_INV + 7], actA);
+            bias_init(XF_BB, 1);
+            run_pass<Net, LB, 1>(wb, ldsi, slot, w, lane, lz, acc, inBP);
+            chain_out<4, 1>(acc, Fl[XF_INV + 7], actA);
+        }
+        // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input in actB, or actA after block2_bpnet)
+        auto &in3 = pick<(KSB > 0)>(actA, actB);
+        auto &out3 = pick<(KSB > 0)>(actB, actA);
         auto inB = [&](auto k) {
             constexpr int K = decltype(k)::value;
-            if constexpr (K < 16) return actB[K]; else return ext;
+            if constexpr (K < 16) return in3[K]; else return ext;
         };
         bias_init(F_B2, 0);
-        run_pass<NetRows, 2, 0>(wb, ldsi, slot, w, lane, lz, acc, inB);
+        run_pass<Net, L2, 0>(wb, ldsi, slot, w, lane, lz, acc, inB);
         nx.sval = nitem < end;
         nx.s = s_next;
         nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
         nx.ray = a.samp_ray[s_next];
-        chain_out<4, 0>(acc, Fl[XF_INV + 2], actA);
+        chain_out<4, 0>(acc, Fl[XF_INV + 2], out3);
         bias_init(F_B2, 1);
-        run_pass<NetRows, 2, 1>(wb, ldsi, slot, w, lane, lz, acc, inB);
+        run_pass<Net, L2, 1>(wb, ldsi, slot, w, lane, lz, acc, inB);
         asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
-        chain_out<4, 1>(acc, Fl[XF_INV + 2], actA);
+        chain_out<4, 1>(acc, Fl[XF_INV + 2], out3);
         // block3.2: 256 -> 256 transposed (lane = output unit j of tile t, register i = row
         // (i & 3) + 8 (i >> 2) + 4h), alpha partials and the K-blend as per-lane FMAs
         float wv[16];
@@ -497,18 +539,18 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), fs_rsrc, off, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), fs_rsrc, off, 16, 0);
         };
-        auto inA3 = [&](auto k) { return actA[decltype(k)::value]; };
+        auto inA3 = [&](auto k) { return out3[decltype(k)::value]; };
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
-        run_pass<NetRows, 3, 0, true>(wb, ldsi, slot, w, lane, lz, acc, inA3);
+        run_pass<Net, L3, 0, true>(wb, ldsi, slot, w, lane, lz, acc, inA3);
         l3_epilogue(std::integral_constant<int, 0>{});
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
         // pass-0 stores right after pass 1's first boundary (acknowledged one chunk later); the
         // next tile's P rows after its last boundary, in flight under that chunk's MFMAs
-        run_pass<NetRows, 3, 1, true>(wb, ldsi, slot, w, lane, lz, acc, inA3, [&](auto c) {
+        run_pass<Net, L3, 1, true>(wb, ldsi, slot, w, lane, lz, acc, inA3, [&](auto c) {
             if constexpr (decltype(c)::value == 0) flush_fs(0);
-            if constexpr (SGN_X3_PF && decltype(c)::value == nch(NetRows::L[3]) - 1) {
+            if constexpr (SGN_X3_PF && decltype(c)::value == nch(Net::L[L3]) - 1) {
                 if (nx.sval) load_proj_x3(proj, nx.pid, lane, pnext);
             }
         });
@@ -704,7 +746,10 @@ void pack_acc_order(float *dst, const float *v, int n_tiles, float sc) {
             for (int r = 0; r < 16; ++r) dst[(t * 2 + h) * 16 + r] = v[32 * t + acc_unit(r, h)] * sc;
 }
 
-void pack_blob_x3(const float *const *w, const float *const *b, uint8_t *blob) {
+int col_bp(int ks, int p) { return ks < 16 ? col_chain(ks, p) : 256 + 16 * (ks - 16) + p; }
+
+// ksb > 0: w[9] / b[9] = block2_bpnet.0 ([256][256 + bpnet_dim], [256])
+void pack_blob_x3(int ksb, int bpnet_dim, const float *const *w, const float *const *b, uint8_t *blob) {
     static const int shape[9][2] = {{256, 284}, {256, 256}, {256, 263}, {256, 256}, {1, 256},
                                     {128, 280}, {128, 128}, {128, 128}, {3, 128}};
     int s[9] = {};
@@ -734,7 +779,19 @@ void pack_blob_x3(const float *const *w, const float *const *b, uint8_t *blob) {
     }
     const int li[7] = {0, 1, 2, 3, 5, 6, 7};
     for (int i = 0; i < 7; ++i) F[XF_INV + i] = ldexpf(1.f, -s[li[i]]);
-    F[XF_INV + 7] = 0.f;
+    F[XF_INV + 7] = 1.f;
+    if (ksb > 0) {
+        const int nin = 256 + bpnet_dim, sb = layer_shift(w[9], (size_t)256 * nin);
+        pack_pairs(fr(OFF_WB), w[9], 256, nin, T_HID, ksb, 4, sb, col_bp);
+        pack_acc_order(F + XF_BB, b[9], T_HID, ldexpf(1.f, sb));
+        F[XF_INV + 7] = ldexpf(1.f, -sb);
+    }
+}
+
+int variant_ksb(int32_t bpnet_layers, int32_t bpnet_dim) {
+    if (bpnet_layers == 0) return 0;
+    if (bpnet_layers == 1 && (bpnet_dim == 0 || bpnet_dim == BP_DIM)) return ks_bp(bpnet_dim);
+    return -1;
 }
 
 }  // namespace x3
@@ -743,14 +800,20 @@ void pack_blob_x3(const float *const *w, const float *const *b, uint8_t *blob) {
 
 extern "C" {
 
-size_t sgn_mlp_packed_bytes_f32(void) { return sgn::x3::BLOB_BYTES; }
+size_t sgn_mlp_packed_bytes_f32(int32_t bpnet_layers, int32_t bpnet_dim) {
+    const int ksb = sgn::x3::variant_ksb(bpnet_layers, bpnet_dim);
+    return ksb < 0 ? 0 : sgn::x3::blob_bytes_sg(ksb);
+}
 
-int sgn_mlp_pack_f32(const float *const *w, const float *const *b, void *d_packed, sgn_stream_t stream) {
+int sgn_mlp_pack_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,
+                     void *d_packed, sgn_stream_t stream) {
     using namespace sgn;
     SGN_REQUIRE(w && b && d_packed, "null argument");
-    for (int L = 0; L < 9; ++L) SGN_REQUIRE(w[L] && b[L], "null layer pointer");
-    std::vector<uint8_t> blob(x3::BLOB_BYTES, 0);
-    x3::pack_blob_x3(w, b, blob.data());
+    const int ksb = x3::variant_ksb(bpnet_layers, bpnet_dim);
+    SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    for (int L = 0; L < (ksb ? 10 : 9); ++L) SGN_REQUIRE(w[L] && b[L], "null layer pointer");
+    std::vector<uint8_t> blob(x3::blob_bytes_sg(ksb), 0);
+    x3::pack_blob_x3(ksb, bpnet_dim, w, b, blob.data());
     hipStream_t st = as_stream(stream);
     SGN_CHECK_HIP(hipMemcpyAsync(d_packed, blob.data(), blob.size(), hipMemcpyHostToDevice, st));
     SGN_CHECK_HIP(hipStreamSynchronize(st));
@@ -775,31 +838,50 @@ int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void
     return 0;
 }
 
+// Work items per launch: the fp32 blended features of a launch are stored through a buffer
+// descriptor (31-bit byte range) based at the launch's first item, so at most 2^31 / 1 KiB items
+// per launch; a frame with more runs several launches per stage.
+constexpr int64_t X3_MAX_CHUNK = ((int64_t)0x7fffffff / (sgn::mlp::HID * 4)) / 16 * 16;
+
 size_t sgn_aggregate_workspace_bytes_f32(int64_t S) {
+    // blended features of every work item (fp32, 1 KiB each), so the two stages may be called
+    // separately; a smaller workspace is accepted with stages = 3 (both stages per chunk)
     if (S < 32) S = 32;
     return (size_t)S * sgn::mlp::HID * sizeof(float);
 }
 
-int sgn_aggregate_f32(const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity,
-                      int32_t K, const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
+int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet, const void *d_point_proj,
+                      const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                      const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
                       void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
     using namespace sgn;
+    using namespace sgn::mlp;
     SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace && d_point_proj, "null argument");
+    const int ksb = x3::variant_ksb(bpnet_layers, bpnet_dim);
+    SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    SGN_REQUIRE(bpnet_dim == 0 || (d_bpnet && ((uintptr_t)d_bpnet & 15) == 0),
+                "bpnet_dim > 0 needs the 16-byte aligned fp32 BPNet point embedding");
     SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
     SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir, "camera (campos, camrotc2w, raydir) required");
     SGN_REQUIRE((pt->pers == nullptr) == (pt->samp_pers == nullptr), "pers and samp_pers go together");
     SGN_REQUIRE(S_capacity >= 0 && S_capacity < (1 << 30), "S_capacity out of range");
     SGN_REQUIRE(((uintptr_t)d_workspace & 15) == 0 && ((uintptr_t)d_point_proj & 15) == 0, "16-byte alignment required");
     hipStream_t st = as_stream(stream);
-    const int64_t chunk = (int64_t)(workspace_bytes / (mlp::HID * sizeof(float)));
-    SGN_REQUIRE(chunk >= 32, "aggregate workspace too small");
+    const int64_t ws_items = (int64_t)(workspace_bytes / (mlp::HID * sizeof(float)));
+    SGN_REQUIRE(ws_items >= 32, "aggregate workspace too small");
+    SGN_REQUIRE(stages == 3 || ws_items >= S_capacity,
+                "stages 1 and 2 called separately need a workspace for all S_capacity items");
+    // chunk = items per launch; with a full-size workspace chunk c keeps its rows at item c * chunk
+    const bool full = ws_items >= S_capacity;
+    const int64_t chunk = ws_items < X3_MAX_CHUNK ? ws_items : X3_MAX_CHUNK;
     AggArgs a{};
     a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
     a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
     a.pers = pt->pers; a.samp_pers = pt->samp_pers;
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
-    a.blob = d_packed; a.blob_bytes = x3::BLOB_BYTES;
+    a.blob = d_packed; a.blob_bytes = x3::blob_bytes_sg(ksb);
+    a.bpnet32 = d_bpnet;
     a.proj = (const _Float16 *)d_point_proj;  // fp32 table (k_agg_rows_x3 reads it as float)
     a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
     x3::ColorArgs c{q->counters, q->work, q->samp_ray, pt->raydir, d_packed, (const float *)d_workspace, d_out_feat, 0, 0};
@@ -807,9 +889,15 @@ int sgn_aggregate_f32(const void *d_point_proj, const sgn_point_tables *pt, cons
         const int64_t n = S_capacity - i0 < chunk ? S_capacity - i0 : chunk;
         a.item0 = c.item0 = (int32_t)i0;
         a.n_items = c.n_items = (int32_t)n;
+        float *fs = (float *)d_workspace + (full ? i0 * mlp::HID : 0);
+        a.fs = (_Float16 *)fs;
+        c.fs = fs;
         const int64_t wg = (n + x3::WG_SAMPLES - 1) / x3::WG_SAMPLES;
-        if (stages & 1)
-            hipLaunchKernelGGL(x3::k_agg_rows_x3, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(x3::TPB), 0, st, a);
+        if (stages & 1) {
+            auto kern = ksb == 0 ? x3::k_agg_rows_x3<0> : ksb == KS_HID ? x3::k_agg_rows_x3<KS_HID>
+                                                                        : x3::k_agg_rows_x3<ks_bp(BP_DIM)>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(x3::TPB), 0, st, a);
+        }
         const int64_t wg2 = (n + 32 * x3::NW - 1) / (32 * x3::NW);
         if (stages & 2)
             hipLaunchKernelGGL(x3::k_color_x3, dim3((unsigned)(wg2 < 256 ? wg2 : 256)), dim3(x3::TPB), 0, st, c);

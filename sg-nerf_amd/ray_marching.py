@@ -263,7 +263,9 @@ class PointAggregator:
         self.device = torch.device(device)
         state = strip_prefix(aggregator_state)
         self.variant = mlp_variant(state)
-        self.packed = pack_mlp(state, self.device)
+        # fp32 arithmetic (the reference's) unless opts say f16
+        self.f32 = self.opts.precision == "f32"
+        self.packed = pack_mlp(state, self.device, self.opts.precision)
 
     def forward(self, sampled_color, sampled_label_embedding, sampled_Rw2c, sampled_dir, sampled_conf,
                 sampled_embedding, sampled_xyz_pers, sampled_xyz, sample_pnt_mask, sample_loc, sample_loc_w,
@@ -305,10 +307,13 @@ class PointAggregator:
         if dim:  # point_aggregators.py:631-635: [h | sampled_label_embedding] into block2_bpnet
             if sampled_label_embedding is None:
                 raise ValueError("block2_bpnet with predict_semantic = 1 needs sampled_label_embedding")
-            bp = torch.empty(S * K, 96, dtype=torch.float16, device=dev)
             lab = f(sampled_label_embedding, 96)
-            _lib.check(_lib.lib().sgn_bpnet_pack(_lib.ptr(lab), S * K, 96, _lib.ptr(bp), _lib.stream_handle()),
-                       "sgn_bpnet_pack")
+            if self.f32:
+                bp = lab
+            else:
+                bp = torch.empty(S * K, 96, dtype=torch.float16, device=dev)
+                _lib.check(_lib.lib().sgn_bpnet_pack(_lib.ptr(lab), S * K, 96, _lib.ptr(bp), _lib.stream_handle()),
+                           "sgn_bpnet_pack")
         qo = _lib.QueryOut()
         qo.ray_ns = qo.ray_soff = qo.samp_d = nnb.data_ptr()
         qo.samp_ray, qo.samp_nnb, qo.pidx = samp_ray.data_ptr(), nnb.data_ptr(), pidx.data_ptr()
@@ -316,10 +321,21 @@ class PointAggregator:
         feat = torch.zeros(S, 4, dtype=torch.float32, device=dev)
         wnorm = torch.zeros(S, K, dtype=torch.float32, device=dev)
         L = _lib.lib()
-        ws = torch.empty(int(L.sgn_aggregate_workspace_bytes(S)), dtype=torch.uint8, device=dev)
-        _lib.check(L.sgn_aggregate_sg(nl, dim, _lib.ptr(bp), None, ctypes.byref(pt), ctypes.byref(qo), S, K,
-                                      _lib.ptr(self.packed), _lib.ptr(feat), None, _lib.ptr(wnorm), _lib.ptr(ws),
-                                      ws.numel(), 3, _lib.stream_handle()), "sgn_aggregate_sg")
+        st = _lib.stream_handle()
+        if self.f32:
+            # block1.0's per-point part over the gathered rows (each row is its own "point")
+            proj = torch.empty(int(L.sgn_point_proj_bytes_f32(S * K)), dtype=torch.uint8, device=dev)
+            _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(proj), st),
+                       "sgn_point_project_f32")
+            ws = torch.empty(int(L.sgn_aggregate_workspace_bytes_f32(S)), dtype=torch.uint8, device=dev)
+            _lib.check(L.sgn_aggregate_f32(nl, dim, _lib.ptr(bp), _lib.ptr(proj), ctypes.byref(pt), ctypes.byref(qo), S, K,
+                                           _lib.ptr(self.packed), _lib.ptr(feat), None, _lib.ptr(wnorm), _lib.ptr(ws),
+                                           ws.numel(), 3, st), "sgn_aggregate_f32")
+        else:
+            ws = torch.empty(int(L.sgn_aggregate_workspace_bytes(S)), dtype=torch.uint8, device=dev)
+            _lib.check(L.sgn_aggregate_sg(nl, dim, _lib.ptr(bp), None, ctypes.byref(pt), ctypes.byref(qo), S, K,
+                                          _lib.ptr(self.packed), _lib.ptr(feat), None, _lib.ptr(wnorm), _lib.ptr(ws),
+                                          ws.numel(), 3, st), "sgn_aggregate_sg")
         # point_aggregators.py:951-953 (forward value of the straight-through clamp)
         conf_coef = torch.clamp(sampled_conf.to(dev)[..., 0], 1e-4, 1.0)
         return feat.view(shp + (4,)), ray_valid.view(shp), wnorm.view(shp + (K,)), conf_coef

@@ -42,6 +42,7 @@ class PointTables:
         self.conf = t(conf, 1)
         self.n = self.xyz.shape[0]
         self.bpnet16 = None
+        self.bpnet32 = None
         if bpnet is not None:
             self.set_bpnet(bpnet)
 
@@ -51,6 +52,7 @@ class PointTables:
         b = torch.as_tensor(bpnet).reshape(-1, 96).to(device=self.xyz.device, dtype=torch.float32).contiguous()
         if b.shape[0] != self.n:
             raise ValueError(f"bpnet embedding has {b.shape[0]} rows for {self.n} points")
+        self.bpnet32 = b  # fp32 table of the fp32-faithful aggregator
         self.bpnet16 = torch.empty(self.n, 96, dtype=torch.float16, device=self.xyz.device)
         with torch.cuda.device(self.xyz.device):
             _lib.check(_lib.lib().sgn_bpnet_pack(_lib.ptr(b), self.n, 96, _lib.ptr(self.bpnet16),
@@ -79,8 +81,6 @@ class HipRenderer:
             raise ValueError(f"aggregator weights are block2_bpnet variant {self.variant}, options say "
                              f"{self.opts.bpnet_variant} (shading_feature_mlp_layer2_bpnet / predict_semantic)")
         self.f32 = self.opts.precision == "f32"
-        if self.f32 and self.variant[0]:
-            raise NotImplementedError("block2_bpnet (SG) runs with precision='f16' only")
         self.packed = pack_mlp(self.mlp_state, self.device, self.opts.precision)
 
     def _buffers(self, R):
@@ -138,7 +138,7 @@ class HipRenderer:
         nl, dim = self.variant
         if dim and self.points.bpnet16 is None:
             raise ValueError("block2_bpnet with predict_semantic = 1 needs the points' BPNet embedding (set_bpnet)")
-        bp = _lib.ptr(self.points.bpnet16) if dim else None
+        bp = (_lib.ptr(self.points.bpnet32) if self.f32 else _lib.ptr(self.points.bpnet16)) if dim else None
         # split block1.0: P[point] = W0a [feat | PE(feat)] + b0 for every point, once per frame
         mark("proj")
         nproj = int(L.sgn_point_proj_bytes_f32(self.points.n) if self.f32 else L.sgn_point_proj_bytes(self.points.n))
@@ -155,7 +155,7 @@ class HipRenderer:
             blend = _lib.ptr(self.blend) if want_blend else None
             wnorm = _lib.ptr(self.wnorm) if want_weights and stage == 1 else None
             if self.f32:
-                _lib.check(L.sgn_aggregate_f32(_lib.ptr(self._proj), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
+                _lib.check(L.sgn_aggregate_f32(nl, dim, bp, _lib.ptr(self._proj), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
                                                _lib.ptr(self.packed), _lib.ptr(self.feat), blend, wnorm,
                                                _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate_f32")
             else:

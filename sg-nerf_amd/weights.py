@@ -97,9 +97,7 @@ def pack_mlp(state, device, precision="f16"):
     nl, dim = mlp_variant(state)
     layers = layers_for(nl, dim)
     L = _lib.lib()
-    if precision == "f32" and nl:
-        raise NotImplementedError("block2_bpnet (SG) is packed for precision 'f16' only")
-    nbytes = int(L.sgn_mlp_packed_bytes_f32() if precision == "f32" else L.sgn_mlp_packed_bytes_sg(nl, dim))
+    nbytes = int(L.sgn_mlp_packed_bytes_f32(nl, dim) if precision == "f32" else L.sgn_mlp_packed_bytes_sg(nl, dim))
     out = torch.empty(nbytes, dtype=torch.uint8, device=device)
     ws = [np.ascontiguousarray(torch.as_tensor(state[n + ".weight"]).detach().cpu().float().numpy()) for n, *_ in layers]
     bs = [np.ascontiguousarray(torch.as_tensor(state[n + ".bias"]).detach().cpu().float().numpy()) for n, *_ in layers]
@@ -107,7 +105,7 @@ def pack_mlp(state, device, precision="f16"):
     bp = (ctypes.c_void_p * len(layers))(*[b.ctypes.data for b in bs])
     with torch.cuda.device(device):
         if precision == "f32":
-            _lib.check(L.sgn_mlp_pack_f32(wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_f32")
+            _lib.check(L.sgn_mlp_pack_f32(nl, dim, wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_f32")
         else:
             _lib.check(L.sgn_mlp_pack_sg(nl, dim, wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_sg")
     return out

@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 RGB_TOL = 1e-3
 FEAT_TOL = 4e-3
+F32_TOL = 1e-5  # precision "f32" (reference arithmetic): decoded features
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_aggregator.npz")
 CASES = ["patch", "patch64", "dense"]
 
@@ -44,10 +45,12 @@ def _inputs(case, bg=(1.0, 1.0, 1.0)):
             "pixel_idx": torch.zeros(1, R, 2, device=DEV), "h": 1, "w": R}
 
 
+@pytest.mark.parametrize("prec", ["f32", "f16"])
 @pytest.mark.parametrize("name", CASES)
-def test_ray_marching_forward_matches_reference(name):
+def test_ray_marching_forward_matches_reference(name, prec):
     pts, mlp, case = _load(name)
-    o = HotPathOpts(SR=int(case["SR"]), K=int(case["K"]))
+    o = HotPathOpts(SR=int(case["SR"]), K=int(case["K"]), precision=prec)
+    rgb_tol, feat_tol = (F32_TOL, F32_TOL) if prec == "f32" else (RGB_TOL, FEAT_TOL)
     npnts = NeuralPoints(pts["xyz"], pts["embedding"], pts["color"], pts["dir"], pts["conf"], DEV)
     net = NeuralPointsRayMarching(npnts, {"aggregator." + k: v for k, v in mlp.items()}, o, DEV)
     inp = _inputs(case)
@@ -55,9 +58,9 @@ def test_ray_marching_forward_matches_reference(name):
     np.testing.assert_array_equal(out["ray_mask"][0].cpu().numpy(), case["ray_mask"])
     n_keep = int(case["ray_mask"].sum())
     assert out["coarse_raycolor"].shape == (1, n_keep, 3)
-    assert np.abs(out["coarse_raycolor"][0].cpu().numpy() - case["ray_color"]).max() <= RGB_TOL
-    assert np.abs(out["coarse_point_opacity"][0].cpu().numpy() - case["opacity"]).max() <= FEAT_TOL
-    assert np.abs(out["coarse_is_background"][0, :, 0].cpu().numpy() - case["bg_transmission"]).max() <= RGB_TOL
+    assert np.abs(out["coarse_raycolor"][0].cpu().numpy() - case["ray_color"]).max() <= rgb_tol
+    assert np.abs(out["coarse_point_opacity"][0].cpu().numpy() - case["opacity"]).max() <= feat_tol
+    assert np.abs(out["coarse_is_background"][0, :, 0].cpu().numpy() - case["bg_transmission"]).max() <= rgb_tol
     assert float(out["queried_shading"].abs().sum()) == 0.0
     np.testing.assert_allclose(out["weight"][0].cpu().numpy(), case["weight"], atol=1e-5, rtol=1e-4)
     np.testing.assert_array_equal(out["conf_coefficient"][0].cpu().numpy(), case["conf_coefficient"])
@@ -67,7 +70,7 @@ def test_ray_marching_forward_matches_reference(name):
     dense = net.render(inp)
     for k in ("coarse_raycolor", "coarse_point_opacity", "coarse_is_background", "queried_shading"):
         torch.testing.assert_close(full[k], dense[k], rtol=0, atol=0, msg=k)
-    assert np.abs(dense["coarse_raycolor"][0].cpu().numpy() - case["full_color"]).max() <= RGB_TOL
+    assert np.abs(dense["coarse_raycolor"][0].cpu().numpy() - case["full_color"]).max() <= rgb_tol
 
 
 def test_ray_marching_black_background():
@@ -102,15 +105,16 @@ def _gathered(pts, case):
                 vsize=np.array([0.008] * 3, np.float32), grid_vox_sz=0)
 
 
+@pytest.mark.parametrize("prec", ["f32", "f16"])
 @pytest.mark.parametrize("name", CASES)
-def test_point_aggregator_matches_reference(name):
+def test_point_aggregator_matches_reference(name, prec):
     pts, mlp, case = _load(name)
-    agg = PointAggregator(mlp, HotPathOpts(SR=int(case["SR"])), DEV)
+    agg = PointAggregator(mlp, HotPathOpts(SR=int(case["SR"]), precision=prec), DEV)
     dec, valid, weight, conf = agg(**_gathered(pts, case))
     np.testing.assert_array_equal(valid[0].cpu().numpy(), case["ray_valid"])
     err = np.abs(dec[0].cpu().numpy() - case["decoded"]).max()
-    print(f"{name}: PointAggregator max |decoded - reference| = {err:.3e}")
-    assert err <= FEAT_TOL
+    print(f"{name} [{prec}]: PointAggregator max |decoded - reference| = {err:.3e}")
+    assert err <= (F32_TOL if prec == "f32" else FEAT_TOL)
     np.testing.assert_allclose(weight[0].cpu().numpy(), case["weight"], atol=1e-5, rtol=1e-4)
     np.testing.assert_array_equal(conf[0].cpu().numpy(), case["conf_coefficient"])
 
@@ -192,11 +196,13 @@ def _load_sg(name):
     return pts, mlp, case
 
 
+@pytest.mark.parametrize("prec", ["f32", "f16"])
 @pytest.mark.parametrize("name", ["sg96", "sg0"])
-def test_point_aggregator_sg_matches_reference(name):
+def test_point_aggregator_sg_matches_reference(name, prec):
     pts, mlp, case = _load_sg(name)
     ps = 1 if name == "sg96" else 0
-    o = HotPathOpts(SR=int(case["SR"]), shading_feature_mlp_layer2_bpnet=1, predict_semantic=ps, semantic_guidance=ps)
+    o = HotPathOpts(SR=int(case["SR"]), shading_feature_mlp_layer2_bpnet=1, predict_semantic=ps, semantic_guidance=ps,
+                    precision=prec)
     agg = PointAggregator(mlp, o, DEV)
     args = _gathered(pts, case)
     if ps:  # neural_points.py:970-972
@@ -207,8 +213,8 @@ def test_point_aggregator_sg_matches_reference(name):
     dec, valid, weight, conf = agg(**args)
     np.testing.assert_array_equal(valid[0].cpu().numpy(), case["ray_valid"])
     err = np.abs(dec[0].cpu().numpy() - case["decoded"]).max()
-    print(f"{name}: PointAggregator (SG) max |decoded - reference| = {err:.3e}")
-    assert err <= FEAT_TOL
+    print(f"{name} [{prec}]: PointAggregator (SG) max |decoded - reference| = {err:.3e}")
+    assert err <= (F32_TOL if prec == "f32" else FEAT_TOL)
 
 
 def test_ray_marching_forward_sg_matches_reference():
