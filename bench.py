@@ -408,8 +408,6 @@ def main():
         if dist:
             torch.distributed.destroy_process_group()
         return
-    if args.sg and args.precision == "f32":
-        args.precision = "f16"  # block2_bpnet is built for the fp16-operand kernels only
     x3 = args.precision == "f32"
     h = render_run(args, args.precision, world, rank, dev, dist, args.steps, args.warmup, lego)
     R = args.h * args.w
@@ -489,7 +487,7 @@ def main():
         },
         "ms_per_frame": h["ms_per_frame"],
     }
-    if not args.no_extras and not args.sg:
+    if not args.no_extras:
         # the other arithmetic mode on the same frames (extra key; the headline stays the reference's fp32)
         other = "f16" if x3 else "f32"
         e = render_run(args, other, world, rank, dev, dist, args.steps, args.warmup, lego, want_stats=False)
