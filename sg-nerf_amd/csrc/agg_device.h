@@ -259,11 +259,12 @@ __device__ __forceinline__ RowIdx row_index(const AggArgs &a, int item, int end,
     return x;
 }
 
-// FEAT = false: the point features are not needed (split block1.0).  extf: block3's extra
-// channels in fp32 (colour, dir - v, <dir, v>, 0), lane-half 0 only (zero on half 1).
-template <bool FEAT = true>
-__device__ __forceinline__ RowIn gather_row_f(const AggArgs &a, const Cam &cam, const RowIdx &ix, int lane,
-                                              float (&feat)[16], float (&dist)[3], float (&extf)[8]) {
+// FEAT = false: the point features are not needed (split block1.0).  Block3's extra channels
+// (colour, dir - v, <dir, v>, 0; lane-half 0 only, zero on half 1) go to `ext` as fp16 or, with
+// F32EXT, to `extf` in fp32 (the fp32-faithful kernels split them themselves).
+template <bool FEAT, bool F32EXT>
+__device__ __forceinline__ RowIn gather_row_impl(const AggArgs &a, const Cam &cam, const RowIdx &ix, int lane,
+                                                 float (&feat)[16], float (&dist)[3], h8 &ext, float (&extf)[8]) {
     const int h = lane >> 5, kk = lane & 7;
     RowIn ri;
     ri.sval = ix.sval;
@@ -328,25 +329,39 @@ __device__ __forceinline__ RowIn gather_row_f(const AggArgs &a, const Cam &cam, 
     if (a.blend && ri.sval && h == 0) a.blend[(int64_t)s * 8 + kk] = ri.wgt;
     if (a.wnorm && ri.sval && h == 1) a.wnorm[(int64_t)s * 8 + kk] = w;
     // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane-half 0 only
-    const bool e = h == 0 && m;
-    extf[0] = e ? col[0] : 0.f;
-    extf[1] = e ? col[1] : 0.f;
-    extf[2] = e ? col[2] : 0.f;
-    extf[3] = e ? __fsub_rn(pdr[0], vx) : 0.f;
-    extf[4] = e ? __fsub_rn(pdr[1], vy) : 0.f;
-    extf[5] = e ? __fsub_rn(pdr[2], vz) : 0.f;
-    extf[6] = e ? __fadd_rn(__fadd_rn(__fmul_rn(pdr[0], vx), __fmul_rn(pdr[1], vy)), __fmul_rn(pdr[2], vz)) : 0.f;
-    extf[7] = 0.f;
+    if constexpr (F32EXT) {
+        const bool e = h == 0 && m;
+        extf[0] = e ? col[0] : 0.f;
+        extf[1] = e ? col[1] : 0.f;
+        extf[2] = e ? col[2] : 0.f;
+        extf[3] = e ? __fsub_rn(pdr[0], vx) : 0.f;
+        extf[4] = e ? __fsub_rn(pdr[1], vy) : 0.f;
+        extf[5] = e ? __fsub_rn(pdr[2], vz) : 0.f;
+        extf[6] = e ? __fadd_rn(__fadd_rn(__fmul_rn(pdr[0], vx), __fmul_rn(pdr[1], vy)), __fmul_rn(pdr[2], vz)) : 0.f;
+        extf[7] = 0.f;
+    } else {
+        h8 e = {};
+        if (h == 0 && m) {
+            e = pack8(col[0], col[1], col[2], __fsub_rn(pdr[0], vx), __fsub_rn(pdr[1], vy), __fsub_rn(pdr[2], vz),
+                      __fadd_rn(__fadd_rn(__fmul_rn(pdr[0], vx), __fmul_rn(pdr[1], vy)), __fmul_rn(pdr[2], vz)), 0.f);
+        }
+        ext = e;
+    }
     return ri;
 }
 
 template <bool FEAT = true>
 __device__ __forceinline__ RowIn gather_row(const AggArgs &a, const Cam &cam, const RowIdx &ix, int lane,
                                             float (&feat)[16], float (&dist)[3], h8 &ext) {
-    float e[8];
-    const RowIn ri = gather_row_f<FEAT>(a, cam, ix, lane, feat, dist, e);
-    ext = pack8(e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7]);
-    return ri;
+    float unused[8];
+    return gather_row_impl<FEAT, false>(a, cam, ix, lane, feat, dist, ext, unused);
+}
+
+template <bool FEAT = true>
+__device__ __forceinline__ RowIn gather_row_f(const AggArgs &a, const Cam &cam, const RowIdx &ix, int lane,
+                                              float (&feat)[16], float (&dist)[3], float (&extf)[8]) {
+    h8 unused;
+    return gather_row_impl<FEAT, true>(a, cam, ix, lane, feat, dist, unused, extf);
 }
 
 template <bool FEAT = true>

@@ -31,57 +31,95 @@ __device__ __forceinline__ float pers_z(const float *campos, const float *rot, f
     return __fadd_rn(__fadd_rn(__fmul_rn(sx, rot[2]), __fmul_rn(sy, rot[5])), __fmul_rn(sz, rot[8]));
 }
 
-__global__ __launch_bounds__(256) void k_composite(CompArgs a) {
-    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (r >= a.R) return;
-    const int ns = a.ray_ns[r], off = a.ray_soff[r];
-    const float z0 = pers_z(a.campos, a.rot, 0.f, 0.f, 0.f);
-    float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
-    bool any_valid = false;
-    float prev_cm = 0.f;
-    // slot s-1 state while slot s's z is read
-    bool pv = false;
-    float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto process = [&](int slot, float dist) {
-        const bool mask = dist < 1e-8f || (a.unit && dist > 2.f * a.vz);
-        dist = mask ? a.vz : dist;
-        const float valid = pv ? 1.f : 0.f;
-        dist = dist * valid;
-        const float sigma = (pv ? pf.x : 0.f) * valid;
-        const float o = 1.f - expf(-sigma * dist);
-        const float wgt = o * T;
-        if (pv) {
-            cr += pf.y * wgt;
-            cg += pf.z * wgt;
-            cb += pf.w * wgt;
+// One wave = 64 rays (lane = ray).  A ray's loop stops after its last selected sample: every
+// later slot is a padding slot (sigma 0), whose opacity is exactly 0 and whose transmittance
+// factor 1 - 0 + 1e-10 rounds to 1.0f, so skipping them changes no bit.  The [R, SR] opacity /
+// blend-weight rows are staged in LDS ([ray][SR + 1] floats, zero-filled) and leave as coalesced
+// 16-B stores of the wave's contiguous 64 x SR block.
+constexpr int COMP_RAYS = 64;
+
+__device__ __forceinline__ void store_rows(float *dst, const float *st, int SR, int nrows, int lane) {
+    const int n = nrows * SR;
+    if ((SR & 3) == 0) {  // 16-B stores (dst is 16-B aligned: 64 SR floats per wave block)
+        for (int i = lane * 4; i < n; i += 64 * 4) {
+            const int row = i / SR, col = i - row * SR;
+            const float *p = st + row * (SR + 1) + col;
+            *(float4 *)(dst + i) = make_float4(p[0], p[1], p[2], p[3]);
         }
-        if (a.out_blendw) a.out_blendw[r * a.SR + slot] = wgt;
-        T = T * (1.f - o + 1e-10f);
-        if (a.out_opacity) a.out_opacity[r * a.SR + slot] = o;
-    };
-    for (int s = 0; s < a.SR; ++s) {
-        float z = z0;
-        bool v = false;
-        float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (s < ns) {
-            const int64_t id = off + s;
-            z = pers_z(a.campos, a.rot, a.samp_locw[id * 3], a.samp_locw[id * 3 + 1], a.samp_locw[id * 3 + 2]);
-            v = a.samp_nnb[id] > 0;
-            if (v) f = *(const float4 *)(a.feat + id * 4);
+    } else {
+        for (int i = lane; i < n; i += 64) {
+            const int row = i / SR;
+            dst[i] = st[row * (SR + 1) + i - row * SR];
         }
-        const float cm = s == 0 ? z : fmaxf(prev_cm, z);
-        if (s > 0) process(s - 1, cm - prev_cm);
-        prev_cm = cm;
-        pv = v;
-        pf = f;
-        any_valid |= v;
     }
-    process(a.SR - 1, a.vz);
-    a.out_mask[r] = any_valid ? 1 : 0;
-    a.out_rgb[r * 3 + 0] = any_valid ? cr + a.bg0 * T : a.bg0;
-    a.out_rgb[r * 3 + 1] = any_valid ? cg + a.bg1 * T : a.bg1;
-    a.out_rgb[r * 3 + 2] = any_valid ? cb + a.bg2 * T : a.bg2;
-    if (a.out_bgT) a.out_bgT[r] = any_valid ? T : 1.f;
+}
+
+__global__ __launch_bounds__(COMP_RAYS) void k_composite(CompArgs a) {
+    extern __shared__ float st[];  // [2][64][SR + 1]: opacity, blend weight
+    const int lane = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * COMP_RAYS, r = r0 + lane;
+    const int nrows = a.R - r0 < COMP_RAYS ? (int)(a.R - r0) : COMP_RAYS;
+    const int SR = a.SR, ld = SR + 1;
+    float *so = st + lane * ld, *sb = st + (COMP_RAYS + lane) * ld;
+    const bool want_o = a.out_opacity != nullptr, want_b = a.out_blendw != nullptr;
+    if (want_o)
+        for (int s = 0; s < SR; ++s) so[s] = 0.f;
+    if (want_b)
+        for (int s = 0; s < SR; ++s) sb[s] = 0.f;
+    if (r < a.R) {
+        const int ns = a.ray_ns[r], off = a.ray_soff[r];
+        const float z0 = pers_z(a.campos, a.rot, 0.f, 0.f, 0.f);
+        float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
+        bool any_valid = false;
+        float prev_cm = 0.f;
+        // slot s-1 state while slot s's z is read
+        bool pv = false;
+        float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto process = [&](int slot, float dist) {
+            const bool mask = dist < 1e-8f || (a.unit && dist > 2.f * a.vz);
+            dist = mask ? a.vz : dist;
+            const float valid = pv ? 1.f : 0.f;
+            dist = dist * valid;
+            const float sigma = (pv ? pf.x : 0.f) * valid;
+            const float o = 1.f - expf(-sigma * dist);
+            const float wgt = o * T;
+            if (pv) {
+                cr += pf.y * wgt;
+                cg += pf.z * wgt;
+                cb += pf.w * wgt;
+            }
+            if (want_b) sb[slot] = wgt;
+            T = T * (1.f - o + 1e-10f);
+            if (want_o) so[slot] = o;
+        };
+        const int last = ns < SR ? ns : SR - 1;  // slot ns (padding, z0) closes the last interval
+        for (int s = 0; s <= last; ++s) {
+            float z = z0;
+            bool v = false;
+            float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (s < ns) {
+                const int64_t id = off + s;
+                z = pers_z(a.campos, a.rot, a.samp_locw[id * 3], a.samp_locw[id * 3 + 1], a.samp_locw[id * 3 + 2]);
+                v = a.samp_nnb[id] > 0;
+                if (v) f = *(const float4 *)(a.feat + id * 4);
+            }
+            const float cm = s == 0 ? z : fmaxf(prev_cm, z);
+            if (s > 0) process(s - 1, cm - prev_cm);
+            prev_cm = cm;
+            pv = v;
+            pf = f;
+            any_valid |= v;
+        }
+        if (ns >= SR) process(SR - 1, a.vz);  // a full ray's last slot: interval vsize[2]
+        a.out_mask[r] = any_valid ? 1 : 0;
+        a.out_rgb[r * 3 + 0] = any_valid ? cr + a.bg0 * T : a.bg0;
+        a.out_rgb[r * 3 + 1] = any_valid ? cg + a.bg1 * T : a.bg1;
+        a.out_rgb[r * 3 + 2] = any_valid ? cb + a.bg2 * T : a.bg2;
+        if (a.out_bgT) a.out_bgT[r] = any_valid ? T : 1.f;
+    }
+    __syncthreads();
+    if (want_o) store_rows(a.out_opacity + r0 * SR, st, SR, nrows, lane);
+    if (want_b) store_rows(a.out_blendw + r0 * SR, st + COMP_RAYS * ld, SR, nrows, lane);
 }
 
 // ---- dense ray_march (compatibility sub-boundary, diff_ray_marching.py:509-555) ----------
@@ -159,7 +197,10 @@ extern "C" int sgn_composite(const sgn_composite_params *cp, const float *d_camp
     a.bg0 = cp->bg[0]; a.bg1 = cp->bg[1]; a.bg2 = cp->bg[2];
     a.out_rgb = d_out_rgb; a.out_bgT = d_out_bgT; a.out_opacity = d_out_opacity; a.out_mask = d_out_mask;
     a.out_blendw = d_out_blendw;
-    hipLaunchKernelGGL(k_composite, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, as_stream(stream), a);
+    SGN_REQUIRE(cp->SR <= 256, "SR must be at most 256");
+    const size_t lds = (size_t)2 * COMP_RAYS * (cp->SR + 1) * sizeof(float);
+    hipLaunchKernelGGL(k_composite, dim3((unsigned)((R + COMP_RAYS - 1) / COMP_RAYS)), dim3(COMP_RAYS), lds,
+                       as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }
