@@ -42,10 +42,13 @@ constexpr int SLOT_PAIRS = 32;
 constexpr int SLOT = SLOT_PAIRS * PAIR;  // 64 KiB
 constexpr int NSLOT = 2;
 #ifndef SGN_X3_PD
-#define SGN_X3_PD 2
+#define SGN_X3_PD 3
 #endif
 #ifndef SGN_X3_PIN
 #define SGN_X3_PIN 1
+#endif
+#ifndef SGN_X3_SPREAD
+#define SGN_X3_SPREAD 1  // next chunk's LDS-DMA pieces interleaved with the current chunk's MFMAs
 #endif
 #ifndef SGN_X3_PF
 #define SGN_X3_PF 0  // 1: next tile's P rows loaded during the previous tile's last chunk (spills)
@@ -159,14 +162,27 @@ __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int
     });
 }
 
+// piece J (of this wave's ceil(2 pairs / NW)) of chunk N
+template <class Net, int N, int J>
+__device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int lane, int lz) {
+    using S = Sched<Net>;
+    constexpr int nf = 2 * S::pairs(N);
+    const int i = w + NW * J;
+    if (NW * (J + 1) <= nf || i < nf)  // wave-uniform
+        lds_dma_1k(wb, dst + i * 1024, lane, S::off(N) + (uint32_t)(i * 1024 + lz));
+}
+template <class Net, int N>
+constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NW - 1) / NW; }
+
 // chunk boundary: this wave's DMAs of chunk N landed, LDS reads drained, barrier; then chunk N+1
-// goes into the slot every wave finished reading one chunk ago
+// goes into the slot every wave finished reading one chunk ago (here, or spread over the chunk's
+// MFMAs by run_pass with SGN_X3_SPREAD)
 template <class Net, int N>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    dma_chunk<Net, (N + 1) % Sched<Net>::total()>(wb, lds + (slot ^ 1) * SLOT, w, lane, lz);
+    if constexpr (!SGN_X3_SPREAD) dma_chunk<Net, (N + 1) % Sched<Net>::total()>(wb, lds + (slot ^ 1) * SLOT, w, lane, lz);
 }
 
 struct NoHook {
@@ -185,10 +201,13 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
     constexpr int TP = ly.tp;
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
-        chunk_enter<Net, Sched<Net>::idx(L, P, C)>(wb, lds, slot, w, lane, lz);
+        constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
+        chunk_enter<Net, N>(wb, lds, slot, w, lane, lz);
         post(cc);
         const char *sl = lds + slot * SLOT;
+        char *dnext = lds + (slot ^ 1) * SLOT;
         constexpr int NF = nk(ly, C) * TP;
+        constexpr int PW = dma_pieces<Net, NN>();  // this wave's pieces of the next chunk
         auto frag = [&](int f, int part) { return *(const h8 *)(sl + (2 * f + part) * 1024 + lane * 16); };
         h8 fh[PD], fl[PD];
 #pragma unroll
@@ -217,6 +236,11 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
                     acc[t] = mfma32(Ah, B.hi, acc[t]);
                     acc[t] = mfma32(Ah, B.lo, acc[t]);
                     acc[t] = mfma32(Al, B.hi, acc[t]);
+                }
+                if constexpr (SGN_X3_SPREAD) {  // pieces [F PW / NF, (F + 1) PW / NF) after pair F
+                    static_for<(F + 1) * PW / NF - F * PW / NF>([&](auto jj) {
+                        dma_piece<Net, NN, F * PW / NF + decltype(jj)::value>(wb, dnext, w, lane, lz);
+                    });
                 }
 #if SGN_X3_PIN
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -644,7 +668,10 @@ __global__ __launch_bounds__(TPB, 1) void k_color_x3(ColorArgs a) {
             constexpr int d = decltype(d3)::value;
             static_for<4>([&](auto ff) {
                 constexpr int f = decltype(ff)::value;
-                sincos_f<f>(v3[d], pe[d * 4 + f], pe[12 + d * 4 + f]);
+                float sv, cv;
+                sincos_f<f>(v3[d], sv, cv);
+                pe[d * 4 + f] = sv;
+                pe[12 + d * 4 + f] = cv;
             });
         });
         {
