@@ -101,6 +101,7 @@ struct AggArgs {
     _Float16 *sh1;    // [rows][256] block1.2 inputs (chain order)
     _Float16 *sh2;    // [rows][272] block3.0 inputs (chain order | colour, dir - v, <dir, v>)
     _Float16 *sh3;    // [rows][256] block3.2 inputs (chain order)
+    unsigned long long *tdbg;  // timing builds only (SGN_X3_TIMING): per-wave clock stamps
 };
 
 // training save: one 16-byte fragment of a 32-row tile -> [rows][C] (C multiple of 16)

@@ -50,6 +50,16 @@ constexpr int NSLOT = 2;
 #ifndef SGN_X3_SPREAD
 #define SGN_X3_SPREAD 1  // next chunk's LDS-DMA pieces interleaved with the current chunk's MFMAs
 #endif
+#ifndef SGN_X3_SPREAD_DIV
+#define SGN_X3_SPREAD_DIV 1  // DMA pieces spread over the first NF / DIV pairs of a chunk
+#endif
+#ifndef SGN_X3_EPI_BARRIER
+#define SGN_X3_EPI_BARRIER 0  // 1: scheduling barrier after each layer epilogue
+#endif
+#ifndef SGN_X3_TP8
+#define SGN_X3_TP8 0  // 1: block1.2 and block3.2 as one pass over all 8 output tiles
+#endif
+constexpr int TPL = SGN_X3_TP8 ? 8 : 4, NPL = 8 / TPL, KCL = SGN_X3_TP8 ? 4 : 8;  // block1.2 / block3.2 passes
 #ifndef SGN_X3_PF
 #define SGN_X3_PF 0  // 1: next tile's P rows loaded during the previous tile's last chunk (spills)
 #endif
@@ -90,14 +100,14 @@ __host__ __device__ constexpr int nk(XL l, int c) { return l.ks - c * l.kc < l.k
 // A "net" is the ordered list of layers one kernel streams per work tile.
 struct NetRows {
     static constexpr int NL = 4;
-    static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, 4, 2, 8, OFF_W1}, {17, 4, 2, 6, OFF_W2},
-                                 {16, 4, 2, 8, OFF_W3}};
+    static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, TPL, NPL, KCL, OFF_W1}, {17, 4, 2, 6, OFF_W2},
+                                 {16, TPL, NPL, KCL, OFF_W3}};
 };
 template <int KSB>
 struct NetRowsSG {
     static constexpr int NL = 5;
-    static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, 4, 2, 8, OFF_W1}, {KSB, 4, 2, 8, OFF_WB},
-                                 {17, 4, 2, 6, OFF_W2}, {16, 4, 2, 8, OFF_W3}};
+    static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, TPL, NPL, KCL, OFF_W1}, {KSB, 4, 2, 8, OFF_WB},
+                                 {17, 4, 2, 6, OFF_W2}, {16, TPL, NPL, KCL, OFF_W3}};
 };
 struct NetColor {
     static constexpr int NL = 3;
@@ -132,19 +142,52 @@ struct X3B {
     h8 hi, lo;
 };
 
+#ifndef SGN_X3_MIX
+#define SGN_X3_MIX 1  // x - fp32(hi) as one v_fma_mix_f32 reading the packed fp16 hi
+#endif
 // x -> (hi, lo): hi = fp16(x), lo = fp16(x - hi) (the difference is exact in fp32)
 __device__ __forceinline__ X3B split8(const float (&v)[8]) {
     X3B r;
     r.hi = pack8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
     float d[8];
+#if SGN_X3_MIX
+    const u32x4 hp = __builtin_bit_cast(u32x4, r.hi);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        // d = hi * -1.0 + x with hi read as the low / high fp16 half of the packed word
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d[2 * q]) : "v"(hp[q]), "v"(v[2 * q]));
+        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+            : "=v"(d[2 * q + 1]) : "v"(hp[q]), "v"(v[2 * q + 1]));
+    }
+#else
 #pragma unroll
     for (int e = 0; e < 8; ++e) d[e] = v[e] - (float)r.hi[e];
+#endif
     r.lo = pack8(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
     return r;
 }
 
+// Timing build (SGN_X3_TIMING): wave w of the first TD_BLOCKS workgroups stamps the clock at the
+// kernel's phase points into tdbg[(block * NW + w) * TD_EV + seq] (tools/x3_timing.py reads it).
+constexpr int TD_BLOCKS = 8, TD_EV = 2048;
+struct TStamp {
+    unsigned long long *buf;
+    int seq;
+    __device__ __forceinline__ void operator()(int lane) {
+#ifdef SGN_X3_TIMING
+        if (buf && lane == 0 && seq < TD_EV) buf[seq] = clock64();
+        ++seq;
+#else
+        (void)lane;
+#endif
+    }
+};
+
 // one 1-KiB LDS-DMA piece: 16 B per lane from blob byte offset `off` (+ lane * 16)
 __device__ __forceinline__ void lds_dma_1k(const WBlob &wb, char *dst, int lane, uint32_t off) {
+#ifdef SGN_X3_ABLATE_DMA  // timing experiment only: no weight stream (wrong results)
+    return;
+#endif
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)dst, 16, lane * 16, off,
                                              0, 0);
 }
@@ -178,10 +221,18 @@ constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NW - 1) / NW; }
 // goes into the slot every wave finished reading one chunk ago (here, or spread over the chunk's
 // MFMAs by run_pass with SGN_X3_SPREAD)
 template <class Net, int N>
-__device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz) {
+__device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz,
+                                            TStamp *ts = nullptr) {
+#ifndef SGN_X3_ABLATE_BARRIER  // timing experiment only: no boundary waits / barrier (wrong results)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+#endif
+#ifdef SGN_X3_TIMING
+    if (ts) (*ts)(lane);
+#else
+    (void)ts;
+#endif
     if constexpr (!SGN_X3_SPREAD) dma_chunk<Net, (N + 1) % Sched<Net>::total()>(wb, lds + (slot ^ 1) * SLOT, w, lane, lz);
 }
 
@@ -190,19 +241,22 @@ struct NoHook {
     __device__ void operator()(C) const {}
 };
 
+
+
 // One pass of layer L, k-outer: acc[t] += W[tp P + t] in(k) over the pass's chunks, three
 // MFMAs per (k-step, tile).  TRANS: activations are the A operand (accumulators hold D^T).
 // The accumulators arrive initialised (bias, P, or zero).  post(integral_constant C) runs right
 // after the boundary of every chunk C of the pass.
 template <class Net, int L, int P, bool TRANS = false, class InFn, class PostFn = NoHook>
 __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
-                                         f32x16 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{}) {
+                                         f32x16 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{},
+                                         TStamp *ts = nullptr) {
     constexpr XL ly = Net::L[L];
     constexpr int TP = ly.tp;
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
         constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
-        chunk_enter<Net, N>(wb, lds, slot, w, lane, lz);
+        chunk_enter<Net, N>(wb, lds, slot, w, lane, lz, ts);
         post(cc);
         const char *sl = lds + slot * SLOT;
         char *dnext = lds + (slot ^ 1) * SLOT;
@@ -237,10 +291,13 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
                     acc[t] = mfma32(Ah, B.lo, acc[t]);
                     acc[t] = mfma32(Al, B.hi, acc[t]);
                 }
-                if constexpr (SGN_X3_SPREAD) {  // pieces [F PW / NF, (F + 1) PW / NF) after pair F
-                    static_for<(F + 1) * PW / NF - F * PW / NF>([&](auto jj) {
-                        dma_piece<Net, NN, F * PW / NF + decltype(jj)::value>(wb, dnext, w, lane, lz);
-                    });
+                if constexpr (SGN_X3_SPREAD) {  // pieces [F PW / NS, (F + 1) PW / NS) after pair F < NS
+                    constexpr int NS = NF / SGN_X3_SPREAD_DIV > 0 ? NF / SGN_X3_SPREAD_DIV : 1;
+                    if constexpr (F < NS) {
+                        static_for<(F + 1) * PW / NS - F * PW / NS>([&](auto jj) {
+                            dma_piece<Net, NN, F * PW / NS + decltype(jj)::value>(wb, dnext, w, lane, lz);
+                        });
+                    }
                 }
 #if SGN_X3_PIN
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -260,6 +317,7 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
 // TP*P.. -> k-steps 2t, 2t+1 (the chained k order is folded into the packed weights)
 template <int TP, int P, int NOUT>
 __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], float inv, X3B (&out)[NOUT]) {
+    if constexpr (SGN_X3_EPI_BARRIER) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int tt = 0; tt < TP; ++tt)
 #pragma unroll
@@ -272,12 +330,41 @@ __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], float inv, X3
             }
             out[2 * (TP * P + tt) + s2] = split8(v);
         }
+    if constexpr (SGN_X3_EPI_BARRIER) __builtin_amdgcn_sched_barrier(0);
+}
+
+#ifndef SGN_X3_FASTSC
+#define SGN_X3_FASTSC 1
+#endif
+// sin and cos of x (fp32, within ~1 ulp): quadrant q = rint(x 2/pi), r = x - q pi/2 in double
+// (exact to far below fp32 resolution for |x| < 2^20), cephes' minimax polynomials on
+// [-pi/4, pi/4]; |x| >= 2^20 (never met by the encodings' arguments) takes the library sincosf.
+__device__ __forceinline__ void sincos_acc(float x, float &s, float &c) {
+#if SGN_X3_FASTSC
+    if (__builtin_expect(__builtin_fabsf(x) >= 1048576.f, 0)) {
+        sincosf(x, &s, &c);
+        return;
+    }
+    const float qf = __builtin_rintf(x * 0.63661977236758134f);
+    const float r = (float)__builtin_fma((double)qf, -1.5707963267948966, (double)x);
+    const float z = r * r;
+    const float sp = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
+                                                   -1.6666654611e-1f), z * r, r);
+    const float cp = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                                                   4.166664568298827e-2f), z * z, __builtin_fmaf(-0.5f, z, 1.f));
+    const int q = (int)qf;
+    const float s0 = (q & 1) ? cp : sp, c0 = (q & 1) ? sp : cp;
+    s = (q & 2) ? -s0 : s0;
+    c = ((q + 1) & 2) ? -c0 : c0;
+#else
+    sincosf(x, &s, &c);
+#endif
 }
 
 // accurate sin/cos of x 2^F (the scaling is exact; torch.sin on the product, networks.py:186)
 template <int F>
 __device__ __forceinline__ void sincos_f(float x, float &s, float &c) {
-    sincosf(x * (float)(1 << F), &s, &c);
+    sincos_acc(x * (float)(1 << F), s, c);
 }
 
 // ---- per-point block1.0 projection ------------------------------------------------------
@@ -432,6 +519,14 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
     f32x16 pnext[8];
     if (SGN_X3_PF && a.item0 + (int)blockIdx.x * WG_SAMPLES < end) load_proj_x3(proj, nx.pid, lane, pnext);
     const int jl = lane & 31;
+#ifdef SGN_X3_TIMING
+    TStamp tsv{blockIdx.x < TD_BLOCKS && a.tdbg ? a.tdbg + ((int64_t)blockIdx.x * NW + w) * TD_EV : nullptr, 0};
+    TStamp *ts = &tsv;
+#define X3T() tsv(lane)
+#else
+    TStamp *ts = nullptr;
+#define X3T()
+#endif
 
     for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
         int lz = 0;
@@ -441,6 +536,7 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
         const int item = base + w * 4 + q;
         const int nitem = item + gridDim.x * WG_SAMPLES;
         float feat[16], dist[3], extf[8];
+        X3T();  // tile start
         const RowIn ri = gather_row_f<false>(a, cam, nx, lane, feat, dist, extf);
         const X3B ext = split8(extf);
         X3B actA[16], actB[16];
@@ -451,8 +547,11 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
             if constexpr (!SGN_X3_PF) load_proj_x3(proj, nx.pid, lane, pnext);
 #pragma unroll
             for (int t = 0; t < 8; ++t) acc0[t] = pnext[t];
-            run_pass<Net, 0, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) { return B0[decltype(k)::value]; });
+            X3T();  // gather + PE(dists) issued
+            run_pass<Net, 0, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) { return B0[decltype(k)::value]; },
+                                NoHook{}, ts);
             chain_out<8, 0>(acc0, Fl[XF_INV + 0], actA);
+            X3T();
         }
         f32x16 acc[4];
         auto bias_init = [&](int fb, int P) {
@@ -466,13 +565,30 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
         };
         // block1.2: 256 -> 256
         auto inA = [&](auto k) { return actA[decltype(k)::value]; };
-        bias_init(F_B1, 0);
-        run_pass<Net, 1, 0>(wb, ldsi, slot, w, lane, lz, acc, inA);
-        chain_out<4, 0>(acc, Fl[XF_INV + 1], actB);
-        bias_init(F_B1, 1);
-        run_pass<Net, 1, 1>(wb, ldsi, slot, w, lane, lz, acc, inA);
+        if constexpr (SGN_X3_TP8) {
+            f32x16 acc8[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const f32x4 *b = (const f32x4 *)(Fl + F_B1 + (t * 2 + h) * 16);
+                const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+                acc8[t] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
+                                 b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
+            }
+            run_pass<Net, 1, 0>(wb, ldsi, slot, w, lane, lz, acc8, inA, NoHook{}, ts);
+            chain_out<8, 0>(acc8, Fl[XF_INV + 1], actB);
+            X3T();
+            X3T();
+        } else {
+            bias_init(F_B1, 0);
+            run_pass<Net, 1, 0>(wb, ldsi, slot, w, lane, lz, acc, inA, NoHook{}, ts);
+            chain_out<4, 0>(acc, Fl[XF_INV + 1], actB);
+            X3T();
+            bias_init(F_B1, 1);
+            run_pass<Net, 1, 1>(wb, ldsi, slot, w, lane, lz, acc, inA, NoHook{}, ts);
+            chain_out<4, 1>(acc, Fl[XF_INV + 1], actB);
+            X3T();
+        }
         const int s_next = nitem < end ? a.work[nitem] : 0;
-        chain_out<4, 1>(acc, Fl[XF_INV + 1], actB);
         if constexpr (KSB > 0) {
             // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256; the row's fp32 embedding
             // (channels 16 j + 8 h .. +7 for k-step 16 + j) is gathered and split here
@@ -491,11 +607,13 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
                 if constexpr (K < 16) return actB[K]; else return bpv[K - 16];
             };
             bias_init(XF_BB, 0);
-            run_pass<Net, LB, 0>(wb, ldsi, slot, w, lane, lz, acc, inBP);
+            run_pass<Net, LB, 0>(wb, ldsi, slot, w, lane, lz, acc, inBP, NoHook{}, ts);
             chain_out<4, 0>(acc, Fl[XF_INV + 7], actA);
+            X3T();
             bias_init(XF_BB, 1);
-            run_pass<Net, LB, 1>(wb, ldsi, slot, w, lane, lz, acc, inBP);
+            run_pass<Net, LB, 1>(wb, ldsi, slot, w, lane, lz, acc, inBP, NoHook{}, ts);
             chain_out<4, 1>(acc, Fl[XF_INV + 7], actA);
+            X3T();
         }
         // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input in actB, or actA after block2_bpnet)
         auto &in3 = pick<(KSB > 0)>(actA, actB);
@@ -505,16 +623,18 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
             if constexpr (K < 16) return in3[K]; else return ext;
         };
         bias_init(F_B2, 0);
-        run_pass<Net, L2, 0>(wb, ldsi, slot, w, lane, lz, acc, inB);
+        run_pass<Net, L2, 0>(wb, ldsi, slot, w, lane, lz, acc, inB, NoHook{}, ts);
         nx.sval = nitem < end;
         nx.s = s_next;
         nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
         nx.ray = a.samp_ray[s_next];
         chain_out<4, 0>(acc, Fl[XF_INV + 2], out3);
+        X3T();
         bias_init(F_B2, 1);
-        run_pass<Net, L2, 1>(wb, ldsi, slot, w, lane, lz, acc, inB);
+        run_pass<Net, L2, 1>(wb, ldsi, slot, w, lane, lz, acc, inB, NoHook{}, ts);
         asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
         chain_out<4, 1>(acc, Fl[XF_INV + 2], out3);
+        X3T();
         // block3.2: 256 -> 256 transposed (lane = output unit j of tile t, register i = row
         // (i & 3) + 8 (i >> 2) + 4h), alpha partials and the K-blend as per-lane FMAs
         float wv[16];
@@ -526,9 +646,10 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) ap[i] = 0.f;
         const float inv3 = Fl[XF_INV + 3];
-        float fsv[2][8];  // blended features of the pass: [pass][tile tt * 2 + (sample h | h + 2)]
-        auto l3_epilogue = [&](auto pp) {
-            constexpr int P = decltype(pp)::value;
+        float fsv[2][8];  // blended features of a half: [half][tile tt * 2 + (sample h | h + 2)]
+        // tiles 4 P .. 4 P + 3 of accumulators `ac` (tile index 4 P + tt - T0 in ac)
+        auto l3_epilogue = [&](auto pp, auto &ac, auto t0c) {
+            constexpr int P = decltype(pp)::value, T0 = decltype(t0c)::value;
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt) {
                 const int t = 4 * P + tt;
@@ -536,7 +657,7 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
                 float fg[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const float y = __builtin_fmaf(acc[tt][i], inv3, bu);
+                    const float y = __builtin_fmaf(ac[4 * P + tt - T0][i], inv3, bu);
                     const float hv = fmaxf(y, 0.01f * y);
                     ap[i] = __builtin_fmaf(wau, hv, ap[i]);
                     fg[i >> 2] = __builtin_fmaf(wv[i], hv, fg[i >> 2]);
@@ -548,7 +669,7 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
                 fsv[P][2 * tt + 1] = x1 + y1;  // sample h + 2
             }
         };
-        // f_s of pass P -> LDS transpose -> two 16-B stores per lane (sample L >> 4, 8 units)
+        // f_s of half P -> LDS transpose -> two 16-B stores per lane (sample L >> 4, 8 units)
         auto flush_fs = [&](int P) {
             float *st = (float *)(ldsi + FSW_OFF + w * 2048);
 #pragma unroll
@@ -564,22 +685,41 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), fs_rsrc, off, 16, 0);
         };
         auto inA3 = [&](auto k) { return out3[decltype(k)::value]; };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I4 = std::integral_constant<int, 4>;
+        if constexpr (SGN_X3_TP8) {
+            f32x16 acc8[8];
 #pragma unroll
-        for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
-        run_pass<Net, L3, 0, true>(wb, ldsi, slot, w, lane, lz, acc, inA3);
-        l3_epilogue(std::integral_constant<int, 0>{});
+            for (int t = 0; t < 8; ++t) acc8[t] = f32x16{};
+            run_pass<Net, L3, 0, true>(wb, ldsi, slot, w, lane, lz, acc8, inA3, NoHook{}, ts);
+            l3_epilogue(I0{}, acc8, I0{});
+            flush_fs(0);
+            X3T();
+            X3T();
+            l3_epilogue(I1{}, acc8, I0{});
+            flush_fs(1);
+            X3T();
+        } else {
 #pragma unroll
-        for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
-        // pass-0 stores right after pass 1's first boundary (acknowledged one chunk later); the
-        // next tile's P rows after its last boundary, in flight under that chunk's MFMAs
-        run_pass<Net, L3, 1, true>(wb, ldsi, slot, w, lane, lz, acc, inA3, [&](auto c) {
-            if constexpr (decltype(c)::value == 0) flush_fs(0);
-            if constexpr (SGN_X3_PF && decltype(c)::value == nch(Net::L[L3]) - 1) {
-                if (nx.sval) load_proj_x3(proj, nx.pid, lane, pnext);
-            }
-        });
-        l3_epilogue(std::integral_constant<int, 1>{});
-        flush_fs(1);
+            for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
+            run_pass<Net, L3, 0, true>(wb, ldsi, slot, w, lane, lz, acc, inA3, NoHook{}, ts);
+            l3_epilogue(I0{}, acc, I0{});
+            X3T();
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
+            // pass-0 stores right after pass 1's first boundary (acknowledged one chunk later); the
+            // next tile's P rows after its last boundary, in flight under that chunk's MFMAs
+            run_pass<Net, L3, 1, true>(wb, ldsi, slot, w, lane, lz, acc, inA3, [&](auto c) {
+                if constexpr (decltype(c)::value == 0) flush_fs(0);
+                if constexpr (SGN_X3_PF && decltype(c)::value == nch(Net::L[L3]) - 1) {
+                    if (nx.sval) load_proj_x3(proj, nx.pid, lane, pnext);
+                }
+            }, ts);
+            l3_epilogue(I1{}, acc, I4{});
+            flush_fs(1);
+            X3T();
+        }
         // alpha: reduce the 16 row partials over the 32 units of each half (mlp.hip's scheme)
         float bq[8];
 #pragma unroll
@@ -610,7 +750,9 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
             __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src * 4, __builtin_bit_cast(int, alpha_val)));
         const float alpha_s = dpp_sum8(ri.wgt * alpha_row);
         if (ri.sval && kk == 0 && h == 0) a.feat[(int64_t)ri.s * 4 + 0] = alpha_s;
+        X3T();  // tile end
     }
+#undef X3T
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -783,9 +925,9 @@ void pack_blob_x3(int ksb, int bpnet_dim, const float *const *w, const float *co
     for (int L : {0, 1, 2, 3, 5, 6, 7}) s[L] = layer_shift(w[L], (size_t)shape[L][0] * shape[L][1]);
     auto fr = [&](uint32_t off) { return (_Float16 *)(blob + off); };
     pack_pairs(fr(OFF_W0B), w[0], 256, 284, T_HID, KS_L0S, 8, s[0], col_l0b);
-    pack_pairs(fr(OFF_W1), w[1], 256, 256, T_HID, KS_HID, 4, s[1], col_chain);
+    pack_pairs(fr(OFF_W1), w[1], 256, 256, T_HID, KS_HID, TPL, s[1], col_chain);
     pack_pairs(fr(OFF_W2), w[2], 256, 263, T_HID, KS_L2, 4, s[2], col_l2);
-    pack_pairs(fr(OFF_W3), w[3], 256, 256, T_HID, KS_HID, 4, s[3], col_chain);
+    pack_pairs(fr(OFF_W3), w[3], 256, 256, T_HID, KS_HID, TPL, s[3], col_chain);
     pack_pairs(fr(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, 4, s[5], col_c0);
     pack_pairs(fr(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, 4, s[6], col_chain);
     pack_pairs(fr(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, 4, s[7], col_chain);
@@ -911,6 +1053,13 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     a.bpnet32 = d_bpnet;
     a.proj = (const _Float16 *)d_point_proj;  // fp32 table (k_agg_rows_x3 reads it as float)
     a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
+#ifdef SGN_X3_TIMING
+    static unsigned long long *tbuf = nullptr;
+    const size_t tn = (size_t)x3::TD_BLOCKS * x3::NW * x3::TD_EV;
+    if (!tbuf) SGN_CHECK_HIP(hipMalloc(&tbuf, tn * 8));
+    SGN_CHECK_HIP(hipMemsetAsync(tbuf, 0, tn * 8, st));
+    a.tdbg = tbuf;
+#endif
     x3::ColorArgs c{q->counters, q->work, q->samp_ray, pt->raydir, d_packed, (const float *)d_workspace, d_out_feat, 0, 0};
     for (int64_t i0 = 0; i0 < S_capacity; i0 += chunk) {
         const int64_t n = S_capacity - i0 < chunk ? S_capacity - i0 : chunk;
@@ -925,6 +1074,15 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
                                                                         : x3::k_agg_rows_x3<ks_bp(BP_DIM)>;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(x3::TPB), 0, st, a);
         }
+#ifdef SGN_X3_TIMING
+        if ((stages & 1) && i0 == 0)
+            if (const char *path = getenv("SGN_X3_TDBG")) {
+                std::vector<unsigned long long> hb(tn);
+                SGN_CHECK_HIP(hipMemcpyAsync(hb.data(), tbuf, tn * 8, hipMemcpyDeviceToHost, st));
+                SGN_CHECK_HIP(hipStreamSynchronize(st));
+                if (FILE *f = fopen(path, "wb")) { fwrite(hb.data(), 8, tn, f); fclose(f); }
+            }
+#endif
         const int64_t wg2 = (n + 32 * x3::NW - 1) / (32 * x3::NW);
         if (stages & 2)
             hipLaunchKernelGGL(x3::k_color_x3, dim3((unsigned)(wg2 < 256 ? wg2 : 256)), dim3(x3::TPB), 0, st, c);
