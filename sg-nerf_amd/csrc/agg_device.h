@@ -256,7 +256,7 @@ __device__ __forceinline__ RowIdx row_index(const AggArgs &a, int item, int end,
 #else
     x.pid = x.sval ? a.pidx[(int64_t)x.s * 8 + (lane & 7)] : -1;
 #endif
-    x.ray = a.samp_ray[x.s];
+    x.ray = x.sval ? a.samp_ray[x.s] : 0;  // no sample id to follow without a work item
     return x;
 }
 

@@ -87,7 +87,7 @@ constexpr size_t BLOB_BYTES = OFF_XF32 + (size_t)N_XF32 * 4;
 // 2 passes x KSB k-steps x 4 tiles after the base blob; k-steps 0..15 the chained block1 output,
 // 16.. the gathered fp32 BPNet embedding (channel 16 (k - 16) + 8 h + e, natural order)
 constexpr uint32_t OFF_WB = (uint32_t)((BLOB_BYTES + PAIR - 1) / PAIR * PAIR);
-__host__ __device__ constexpr size_t blob_bytes_sg(int ksb) { return ksb ? OFF_WB + (size_t)8 * ksb * PAIR : BLOB_BYTES; }
+__host__ __device__ constexpr size_t blob_bytes_sg(int ksb);  // all sections (defined with the 16x16 layout)
 constexpr size_t PROJ_BYTES_PER_POINT = HID * 4;  // fp32 [half][tile][16]
 
 struct XL {
@@ -192,35 +192,36 @@ __device__ __forceinline__ void lds_dma_1k(const WBlob &wb, char *dst, int lane,
                                              0, 0);
 }
 
-// LDS-DMA of stream chunk N into `dst`: 2 * pairs 1-KiB pieces, wave w moves pieces w + NW j
-template <class Net, int N>
+// LDS-DMA of stream chunk N into `dst`: 2 * pairs 1-KiB pieces, wave w (of NWv) moves pieces
+// w + NWv j
+template <class Net, int N, int NWv = NW>
 __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
     using S = Sched<Net>;
     constexpr int nf = 2 * S::pairs(N);
-    static_for<(nf + NW - 1) / NW>([&](auto jj) {
+    static_for<(nf + NWv - 1) / NWv>([&](auto jj) {
         constexpr int J = decltype(jj)::value;
-        const int i = w + NW * J;
-        if (NW * (J + 1) <= nf || i < nf)  // wave-uniform
+        const int i = w + NWv * J;
+        if (NWv * (J + 1) <= nf || i < nf)  // wave-uniform
             lds_dma_1k(wb, dst + i * 1024, lane, S::off(N) + (uint32_t)(i * 1024 + lz));
     });
 }
 
-// piece J (of this wave's ceil(2 pairs / NW)) of chunk N
-template <class Net, int N, int J>
+// piece J (of this wave's ceil(2 pairs / NWv)) of chunk N
+template <class Net, int N, int J, int NWv = NW>
 __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int lane, int lz) {
     using S = Sched<Net>;
     constexpr int nf = 2 * S::pairs(N);
-    const int i = w + NW * J;
-    if (NW * (J + 1) <= nf || i < nf)  // wave-uniform
+    const int i = w + NWv * J;
+    if (NWv * (J + 1) <= nf || i < nf)  // wave-uniform
         lds_dma_1k(wb, dst + i * 1024, lane, S::off(N) + (uint32_t)(i * 1024 + lz));
 }
-template <class Net, int N>
-constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NW - 1) / NW; }
+template <class Net, int N, int NWv = NW>
+constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NWv - 1) / NWv; }
 
 // chunk boundary: this wave's DMAs of chunk N landed, LDS reads drained, barrier; then chunk N+1
 // goes into the slot every wave finished reading one chunk ago (here, or spread over the chunk's
 // MFMAs by run_pass with SGN_X3_SPREAD)
-template <class Net, int N>
+template <class Net, int N, int NWv = NW>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz,
                                             TStamp *ts = nullptr) {
 #ifndef SGN_X3_ABLATE_BARRIER  // timing experiment only: no boundary waits / barrier (wrong results)
@@ -233,7 +234,8 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot
 #else
     (void)ts;
 #endif
-    if constexpr (!SGN_X3_SPREAD) dma_chunk<Net, (N + 1) % Sched<Net>::total()>(wb, lds + (slot ^ 1) * SLOT, w, lane, lz);
+    if constexpr (!SGN_X3_SPREAD)
+        dma_chunk<Net, (N + 1) % Sched<Net>::total(), NWv>(wb, lds + (slot ^ 1) * SLOT, w, lane, lz);
 }
 
 struct NoHook {
@@ -756,6 +758,593 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// =====================================================================================
+// 2 waves per SIMD: v_mfma_f32_16x16x32_f16, 8 waves x 16 rows (2 samples x K = 8) per
+// 128-row workgroup tile.  A wave's registers hold 16 rows (hi/lo layer input 64, all 16 output
+// tiles' accumulators 64), so two waves share a SIMD and hide each other's LDS-DMA issue,
+// epilogue VALU and gather latency.  Each 1-KiB weight fragment (16 units x 32 inputs) serves
+// 8 waves.  Lane l: row r = l & 15, group g = l >> 4.  A operand: A[unit l&15][k 8g+j];
+// B operand: B[k 8g+j][row l&15]; D: lane holds D[unit 4g+i][row l&15] (i = 0..3) of its tile,
+// i.e. units 16 t + 4 g + i of tile t -- natural order, so P and the biases are natural-order
+// vectors.  Chained layers: k-step s of the next layer takes tiles 2s, 2s+1 of this one as
+// element j <- unit 16 (j >> 2) + 4 g + (j & 3) (perm16, folded into the packed weights).
+// =====================================================================================
+constexpr int NW16 = 8, TPB16 = NW16 * 64;
+constexpr uint32_t OFF16_BASE = OFF_WB + 8u * 22u * PAIR;   // after the largest 32x32 SG section
+constexpr uint32_t OFF16_W0B = OFF16_BASE;                  // block1.0 PE(dists): 2 ks x 16 tiles
+constexpr uint32_t OFF16_W1 = OFF16_W0B + 32 * PAIR;        // block1.2: 8 x 16
+constexpr uint32_t OFF16_W2 = OFF16_W1 + 128 * PAIR;        // block3.0: 9 x 16
+constexpr uint32_t OFF16_W3 = OFF16_W2 + 144 * PAIR;        // block3.2: 8 x 16 (transposed use)
+constexpr uint32_t OFF16_W0A = OFF16_W3 + 128 * PAIR;       // block1.0 per point: 7 x 16
+constexpr uint32_t OFF16_WB = OFF16_W0A + 112 * PAIR;       // block2_bpnet.0 (SG): 8 + 3 x 16
+constexpr uint32_t OFF16_F32 = OFF16_WB + 176 * PAIR;
+// natural-order fp32 section of the 16x16 kernels
+constexpr int Y_B0 = 0, Y_B1 = 256, Y_B2 = 512, Y_B3 = 768, Y_WA = 1024, Y_BB = 1280, Y_BA = 1536, Y_INV = 1537;
+constexpr int N_Y32 = Y_INV + 8 + 3;  // 1548 (multiple of 4)
+constexpr size_t BLOB_BYTES_ALL = OFF16_F32 + (size_t)N_Y32 * 4;
+__host__ __device__ constexpr size_t blob_bytes_sg(int) { return BLOB_BYTES_ALL; }
+static_assert(N_Y32 % 4 == 0, "fp32 section in 16-B units");
+
+struct NetR16 {
+    static constexpr int NL = 4;
+    static constexpr XL L[NL] = {{2, 16, 1, 2, OFF16_W0B}, {8, 16, 1, 2, OFF16_W1}, {9, 16, 1, 2, OFF16_W2},
+                                 {8, 16, 1, 2, OFF16_W3}};
+};
+template <int KB>
+struct NetR16SG {
+    static constexpr int NL = 5;
+    static constexpr XL L[NL] = {{2, 16, 1, 2, OFF16_W0B}, {8, 16, 1, 2, OFF16_W1}, {KB, 16, 1, 2, OFF16_WB},
+                                 {9, 16, 1, 2, OFF16_W2}, {8, 16, 1, 2, OFF16_W3}};
+};
+struct NetProj16 {
+    static constexpr int NL = 1;
+    static constexpr XL L[NL] = {{7, 16, 1, 2, OFF16_W0A}};
+};
+static_assert(Sched<NetR16>::total() == 14 && Sched<NetR16>::pairs(9) == 16, "16x16 row stream");
+
+__device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// One layer, k-outer over all 16 output tiles: acc[t] += W[t] in(k), three MFMAs per
+// (k-step, tile), next chunk's LDS-DMA pieces spread over the first pairs.  TRANS: activations
+// are the A operand (acc[t] holds D[row 4g+i][unit 16t + (l & 15)]).
+template <class Net, int L, bool TRANS = false, class InFn, class PostFn = NoHook>
+__device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
+                                            f32x4 (&acc)[16], InFn &&in, PostFn &&post = PostFn{},
+                                            TStamp *ts = nullptr) {
+    constexpr XL ly = Net::L[L];
+    static_assert(ly.tp == 16 && ly.np == 1, "16-tile single-pass layers");
+    static_for<nch(ly)>([&](auto cc) {
+        constexpr int C = decltype(cc)::value;
+        constexpr int N = Sched<Net>::idx(L, 0, C), NN = (N + 1) % Sched<Net>::total();
+        chunk_enter<Net, N, NW16>(wb, lds, slot, w, lane, lz, ts);
+        post(cc);
+        const char *sl = lds + slot * SLOT;
+        char *dnext = lds + (slot ^ 1) * SLOT;
+        constexpr int NF = nk(ly, C) * 16;
+        constexpr int PW = dma_pieces<Net, NN, NW16>();
+        auto frag = [&](int f, int part) { return *(const h8 *)(sl + (2 * f + part) * 1024 + lane * 16); };
+        h8 fh[PD], fl[PD];
+#pragma unroll
+        for (int f = 0; f < PD; ++f) {
+            fh[f] = frag(f, 0);
+            fl[f] = frag(f, 1);
+        }
+#if SGN_X3_PIN
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
+#endif
+        static_for<nk(ly, C)>([&](auto kk) {
+            constexpr int KK = decltype(kk)::value;
+            const X3B B = in(std::integral_constant<int, C * ly.kc + KK>{});
+            static_for<16>([&](auto tt) {
+                constexpr int t = decltype(tt)::value, F = KK * 16 + t;
+                const h8 Ah = fh[F % PD], Al = fl[F % PD];
+                if constexpr (F + PD < NF) {
+                    fh[F % PD] = frag(F + PD, 0);
+                    fl[F % PD] = frag(F + PD, 1);
+                }
+                if constexpr (TRANS) {
+                    acc[t] = mfma16(B.hi, Ah, acc[t]);
+                    acc[t] = mfma16(B.lo, Ah, acc[t]);
+                    acc[t] = mfma16(B.hi, Al, acc[t]);
+                } else {
+                    acc[t] = mfma16(Ah, B.hi, acc[t]);
+                    acc[t] = mfma16(Ah, B.lo, acc[t]);
+                    acc[t] = mfma16(Al, B.hi, acc[t]);
+                }
+                constexpr int NS = NF / SGN_X3_SPREAD_DIV > 0 ? NF / SGN_X3_SPREAD_DIV : 1;
+                if constexpr (F < NS) {
+                    static_for<(F + 1) * PW / NS - F * PW / NS>([&](auto jj) {
+                        dma_piece<Net, NN, F * PW / NS + decltype(jj)::value, NW16>(wb, dnext, w, lane, lz);
+                    });
+                }
+#if SGN_X3_PIN
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#endif
+            });
+        });
+        slot ^= 1;
+        __builtin_amdgcn_sched_barrier(0);
+    });
+}
+
+// LeakyReLU(2^-s acc + add) of 16 tiles -> the next layer's 8 k-step B fragments (hi/lo)
+template <bool ADD>
+__device__ __forceinline__ void chain_out16(const f32x4 (&acc)[16], const f32x4 (&add)[16], float inv, X3B (&out)[8]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float a = acc[2 * s + (j >> 2)][j & 3];
+            const float y = ADD ? (a + add[2 * s + (j >> 2)][j & 3]) * inv : a * inv;
+            v[j] = fmaxf(y, 0.01f * y);
+        }
+        out[s] = split8(v);
+    }
+}
+
+// ---- per-point block1.0 projection (16x16): P[p] fp32 [256] in natural unit order ----
+struct Proj16Args {
+    const float *emb;
+    int64_t n;
+    const void *blob;
+    float *proj;
+};
+constexpr int Y_LDS_OFF = NSLOT * SLOT;
+constexpr int PROJ16_LDS = Y_LDS_OFF + N_Y32 * 4;
+
+__global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
+    __shared__ __attribute__((aligned(16))) char lds[PROJ16_LDS];
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const WBlob wb = make_blob(a.blob, BLOB_BYTES_ALL);
+    {
+        const float *src = (const float *)((const char *)a.blob + OFF16_F32);
+        float *dst = (float *)(lds + Y_LDS_OFF);
+        for (int i = threadIdx.x; i < N_Y32; i += TPB16) dst[i] = src[i];
+    }
+    __syncthreads();
+    int slot = 0;
+    dma_chunk<NetProj16, 0, NW16>(wb, lds, w, lane, 0);
+    const int64_t ntile = (a.n + 16 * NW16 - 1) / (16 * NW16);
+    for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        const float *Yl = (const float *)(lds + lz + Y_LDS_OFF);
+        const int64_t p = tile * (16 * NW16) + w * 16 + (lane & 15);
+        const bool ok = p < a.n;
+        // lane group g owns features 8 g .. 8 g + 7: k-step 0 slot j = feat[8 g + j]; k-step S >= 1
+        // slot j = PE channel q = 8 (S - 1) + j of those features (feature 8 g + q / 6, frequency
+        // (q % 6) / 2, sin / cos for even / odd q) -- col_proj16 maps it to the reference column
+        float f8[8];
+        {
+            const f32x4 *e4 = (const f32x4 *)(a.emb + (ok ? p : 0) * 32 + 8 * g);
+            const f32x4 u0 = e4[0], u1 = e4[1];
+            f8[0] = u0[0]; f8[1] = u0[1]; f8[2] = u0[2]; f8[3] = u0[3];
+            f8[4] = u1[0]; f8[5] = u1[1]; f8[6] = u1[2]; f8[7] = u1[3];
+        }
+        f32x4 acc[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) acc[t] = *(const f32x4 *)(Yl + Y_B0 + 16 * t + 4 * g);
+        auto in = [&](auto k) {
+            constexpr int S = decltype(k)::value;
+            float v[8];
+            if constexpr (S == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = f8[j];
+            } else {
+                static_for<4>([&](auto jp) {
+                    constexpr int q = 8 * (S - 1) + 2 * decltype(jp)::value, dl = q / 6, f = (q % 6) / 2;
+                    float sv, cv;
+                    sincos_f<f>(f8[dl], sv, cv);
+                    v[2 * decltype(jp)::value] = sv;
+                    v[2 * decltype(jp)::value + 1] = cv;
+                });
+            }
+            return split8(v);
+        };
+        run_layer16<NetProj16, 0>(wb, lds + lz, slot, w, lane, lz, acc, in);
+        if (ok) {  // natural unit order: tile t of lane group g at 16 t + 4 g (64 B per point per store)
+            float *dst = a.proj + p * HID + 4 * g;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) *(f32x4 *)(dst + 16 * t) = acc[t];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- per-neighbour rows (16x16) -------------------------------------------------------------
+constexpr int WG16_SAMPLES = NW16 * 2;            // 16 samples = 128 rows per workgroup tile
+constexpr int FSW16_OFF = Y_LDS_OFF + N_Y32 * 4;
+constexpr int FSW16_BYTES = NW16 * 2048;          // [wave][2 samples][256] fp32
+constexpr int ROWS16_LDS = FSW16_OFF + FSW16_BYTES;
+static_assert(ROWS16_LDS <= 163840, "LDS budget (16x16 rows)");
+
+// row r's point record, its sample position and view direction (+ the caller's pers
+// coordinates on the compatibility path)
+struct Rec16 {
+    float p[3], col[3], dir[3], cf, l[3], v[3], pp[3], pl[3];
+};
+// Rows without a work item (ix.sval false: the tail of the work list, or a launch with no
+// samples at all, where samp_ray holds no written entry) read nothing.
+__device__ __forceinline__ Rec16 load_rec16(const AggArgs &a, const RowIdx &ix) {
+    Rec16 r;
+    const bool v = ix.sval;
+    const int pid = ix.pid, s = ix.s, ray = ix.ray;
+    const bool m = v && pid >= 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        r.p[c] = m ? a.xyz[(int64_t)pid * 3 + c] : 0.f;
+        r.col[c] = m ? a.color[(int64_t)pid * 3 + c] : 0.f;
+        r.dir[c] = m ? a.dir[(int64_t)pid * 3 + c] : 0.f;
+        r.l[c] = v ? a.samp_locw[(int64_t)s * 3 + c] : 0.f;
+        r.v[c] = v ? a.raydir[(int64_t)ray * 3 + c] : 0.f;
+        r.pp[c] = (a.pers && m) ? a.pers[(int64_t)pid * 3 + c] : 0.f;
+        r.pl[c] = (a.pers && v) ? a.samp_pers[(int64_t)s * 3 + c] : 0.f;
+    }
+    r.cf = m ? a.conf[pid] : 0.f;
+    return r;
+}
+
+// dists (point_aggregators.py:917-925): d[0..2] world offsets, d[3..5] pers-space terms; the
+// linear-kernel weight normalised over the sample's 8 rows times the clamped conf (:946-953)
+struct Row16 {
+    float d[6];
+    float wgt, wn;
+};
+__device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, const Rec16 &rc, bool m) {
+    Row16 o;
+    const float dwx = __fsub_rn(rc.p[0], rc.l[0]), dwy = __fsub_rn(rc.p[1], rc.l[1]), dwz = __fsub_rn(rc.p[2], rc.l[2]);
+    o.d[0] = m ? dwx : 0.f;
+    o.d[1] = m ? dwy : 0.f;
+    o.d[2] = m ? dwz : 0.f;
+    float xp, yp, zp, xl, yl, zl;
+    if (a.pers) {
+        xp = rc.pp[0]; yp = rc.pp[1]; zp = rc.pp[2];
+        xl = rc.pl[0]; yl = rc.pl[1]; zl = rc.pl[2];
+    } else {
+        cam.pers(rc.p[0], rc.p[1], rc.p[2], xp, yp, zp);
+        cam.pers(rc.l[0], rc.l[1], rc.l[2], xl, yl, zl);
+    }
+    o.d[3] = m ? __fsub_rn(__fmul_rn(xp, zp), __fmul_rn(xl, zl)) : 0.f;
+    o.d[4] = m ? __fsub_rn(__fmul_rn(yp, zp), __fmul_rn(yl, zl)) : 0.f;
+    o.d[5] = m ? __fsub_rn(zp, zl) : 0.f;
+    float w = 0.f;
+    if (m) {
+        const float n2 = __fadd_rn(__fadd_rn(__fmul_rn(dwx, dwx), __fmul_rn(dwy, dwy)), __fmul_rn(dwz, dwz));
+        w = 1.f / fmaxf(sqrtf(n2), 1e-6f);
+    }
+    const float wsum = dpp_sum8(w);
+    w = w / fmaxf(wsum, 1e-8f);
+    o.wn = w;
+    o.wgt = w * fminf(fmaxf(rc.cf, 1e-4f), 1.f);
+    return o;
+}
+
+// PE(dists) of the row (networks.py:175-192, 6 values x 5 frequencies): (value, frequency) pair
+// pp = 8 g + c of lane group g, c = 0..7 (pairs 30, 31 padding) -> k-step c / 4, slots 2 (c % 4),
+// 2 (c % 4) + 1 = sin, cos of d[pp / 5] 2^(pp % 5) (col_l0b16 maps them to reference columns)
+__device__ __forceinline__ void pe_dists16(const float (&d)[6], int g, X3B (&B)[2]) {
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int pp = 8 * g + c, di = pp / 5, f = pp - 5 * di;
+        float x = d[0];
+#pragma unroll
+        for (int q = 1; q < 6; ++q) x = di == q ? d[q] : x;
+        float sv, cv;
+        sincos_acc(__builtin_ldexpf(x, f), sv, cv);
+        const bool ok = pp < 30;
+        v[2 * c] = ok ? sv : 0.f;
+        v[2 * c + 1] = ok ? cv : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        float u[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[j] = v[8 * s + j];
+        B[s] = split8(u);
+    }
+}
+
+// KB: k-steps of block2_bpnet.0 in 16x16 steps (0: base viewmlp; 8: bpnet_dim 0; 11: dim 96)
+template <int KB>
+__global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
+    using Net = std::conditional_t<(KB > 0), NetR16SG<KB>, NetR16>;
+    constexpr int LB = 2, L2 = KB ? 3 : 2, L3 = KB ? 4 : 3;
+    constexpr int NBP = KB > 8 ? KB - 8 : 0;  // BPNet k-steps (32 channels each)
+    __shared__ __attribute__((aligned(16))) char lds[ROWS16_LDS];
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, r = lane & 15, kk = lane & 7, sc = r >> 3;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwork = a.counters[1];
+    const int end = min(nwork, a.item0 + a.n_items);
+    const Cam cam = load_cam(a.campos, a.rot);
+    const WBlob wb = make_blob(a.blob, BLOB_BYTES_ALL);
+    const __amdgpu_buffer_rsrc_t fs_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.fs, (short)0, 0x7fffffff, 0x00020000);
+    const float *proj = (const float *)a.proj;
+    {
+        const float *src = (const float *)((const char *)a.blob + OFF16_F32);
+        float *dst = (float *)(lds + Y_LDS_OFF);
+        for (int i = threadIdx.x; i < N_Y32; i += TPB16) dst[i] = src[i];
+    }
+    __syncthreads();
+    int slot = 0;
+    dma_chunk<Net, 0, NW16>(wb, lds, w, lane, 0);
+    // The next tile's chain, prefetched inside the current tile so each step lands under MFMAs:
+    // work entry (block1.2), neighbour / ray index (block3.0), point record + sample position and
+    // the P row (block3.2).  First tile: here.
+    RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG16_SAMPLES + w * 2 + sc, end, lane);
+    Rec16 rnext = load_rec16(a, nx);
+    // P row of point pid into `dst`: natural unit order, tile t of lane group g at 16 t + 4 g, so the
+    // 4 lanes of a row read one contiguous 64 B per load instruction
+    auto load_p = [&](int pid, f32x4 (&dst)[16]) {
+        const float *src = proj + (int64_t)(pid < 0 ? 0 : pid) * HID + 4 * g;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) dst[t] = *(const f32x4 *)(src + 16 * t);
+    };
+    // accA: block1.0's accumulators start at P[pid]; the next tile's P is loaded into the array
+    // block3.0 accumulated in (dead once block3.2 has consumed it), so it lands during the
+    // block3.2 epilogue and the tile transition without extra registers
+    f32x4 accA[16], accB[16];
+    load_p(nx.pid, pick<(KB > 0)>(accB, accA));  // SG: where the tile loop copies it from
+#ifdef SGN_X3_TIMING
+    TStamp tsv{blockIdx.x < TD_BLOCKS && a.tdbg ? a.tdbg + ((int64_t)blockIdx.x * NW16 + w) * TD_EV : nullptr, 0};
+    TStamp *ts = &tsv;
+#define X3T() tsv(lane)
+#else
+    TStamp *ts = nullptr;
+#define X3T()
+#endif
+
+    for (int base = a.item0 + blockIdx.x * WG16_SAMPLES; base < end; base += gridDim.x * WG16_SAMPLES) {
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        char *ldsi = lds + lz;
+        const float *Yl = (const float *)(ldsi + Y_LDS_OFF);
+        const int item = base + w * 2 + sc;
+        const int nitem = item + gridDim.x * WG16_SAMPLES;
+        X3T();  // tile start
+        const RowIdx ix = nx;
+        const bool m = ix.pid >= 0;
+        const Rec16 rc = rnext;
+        const Row16 rw = row_math16(a, cam, rc, m);
+        if (a.blend && ix.sval && g == 0) a.blend[(int64_t)ix.s * 8 + kk] = rw.wgt;
+        if (a.wnorm && ix.sval && g == 1) a.wnorm[(int64_t)ix.s * 8 + kk] = rw.wn;
+        X3B ext;
+        {   // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane group 0
+            const bool e = g == 0 && m;
+            float u[8];
+            u[0] = e ? rc.col[0] : 0.f; u[1] = e ? rc.col[1] : 0.f; u[2] = e ? rc.col[2] : 0.f;
+            u[3] = e ? __fsub_rn(rc.dir[0], rc.v[0]) : 0.f;
+            u[4] = e ? __fsub_rn(rc.dir[1], rc.v[1]) : 0.f;
+            u[5] = e ? __fsub_rn(rc.dir[2], rc.v[2]) : 0.f;
+            u[6] = e ? __fadd_rn(__fadd_rn(__fmul_rn(rc.dir[0], rc.v[0]), __fmul_rn(rc.dir[1], rc.v[1])),
+                                 __fmul_rn(rc.dir[2], rc.v[2])) : 0.f;
+            u[7] = 0.f;
+            ext = split8(u);
+        }
+        // Each layer's epilogue (LeakyReLU + hi/lo split of its accumulators) runs lazily inside the
+        // next layer's k-loop: k-step k converts tiles 2k, 2k+1 only, so the VALU work overlaps the
+        // MFMAs in flight instead of idling the matrix pipe between layers.
+        auto chain_k = [&](const f32x4 (&ac)[16], float inv, auto kc) {
+            constexpr int S = decltype(kc)::value;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float y = ac[2 * S + (j >> 2)][j & 3] * inv;
+                v[j] = fmaxf(y, 0.01f * y);
+            }
+            return split8(v);
+        };
+        auto bias_init = [&](f32x4 (&ac)[16], int yb) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) ac[t] = *(const f32x4 *)(Yl + yb + 16 * t + 4 * g);
+        };
+        {   // block1.0: W0b PE(dists) on MFMA, + P[pid] (W0a [feat | PE(feat)] + b0, k_point_proj16)
+            X3B B0[2];
+            pe_dists16(rw.d, g, B0);
+            X3T();  // gather + PE
+            if constexpr (KB > 0) {  // SG: five layers, the P array alternates -- copy it back
+#pragma unroll
+                for (int t = 0; t < 16; ++t) accA[t] = accB[t];
+            }
+            run_layer16<Net, 0>(wb, ldsi, slot, w, lane, lz, accA, [&](auto k) { return B0[decltype(k)::value]; },
+                                NoHook{}, ts);
+        }
+        // block1.2: 256 -> 256 (input: block1.0 accumulators)
+        const float inv0 = Yl[Y_INV + 0], inv1 = Yl[Y_INV + 1], inv2 = Yl[Y_INV + 2], inv7 = Yl[Y_INV + 7];
+        bias_init(accB, Y_B1);
+        int s_next = 0;
+        run_layer16<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) { return chain_k(accA, inv0, k); },
+                            [&](auto c) {
+                                if constexpr (decltype(c)::value == 0) s_next = nitem < end ? a.work[nitem] : 0;
+                            }, ts);
+        if constexpr (KB > 0) {
+            // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256; the row's fp32 embedding
+            // (channels 32 m + 8 g .. +7 for k-step 8 + m) gathered and split here
+            X3B bpv[NBP > 0 ? NBP : 1];
+            if constexpr (NBP > 0) {
+                const float *src = a.bpnet32 + (int64_t)(m ? ix.pid : 0) * (NBP * 32) + 8 * g;
+#pragma unroll
+                for (int q = 0; q < NBP; ++q) {
+                    const f32x4 u0 = *(const f32x4 *)(src + 32 * q), u1 = *(const f32x4 *)(src + 32 * q + 4);
+                    const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+                    bpv[q] = split8(v);
+                }
+            }
+            bias_init(accA, Y_BB);
+            run_layer16<Net, LB>(wb, ldsi, slot, w, lane, lz, accA, [&](auto k) {
+                constexpr int K = decltype(k)::value;
+                if constexpr (K < 8) return chain_k(accB, inv1, k); else return bpv[K - 8];
+            }, NoHook{}, ts);
+        }
+        // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input: block1.2 or block2_bpnet)
+        auto &in2 = pick<(KB > 0)>(accA, accB);
+        auto &acc2 = pick<(KB > 0)>(accB, accA);
+        const float inv_in2 = KB > 0 ? inv7 : inv1;
+        bias_init(acc2, Y_B2);
+        run_layer16<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {
+            constexpr int K = decltype(k)::value;
+            if constexpr (K < 8) return chain_k(in2, inv_in2, k); else return ext;
+        }, [&](auto c) {
+            constexpr int C = decltype(c)::value;
+            if constexpr (C == 0) {  // s_next landed at the previous boundaries
+                nx.sval = nitem < end;
+                nx.s = s_next;
+                nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
+                nx.ray = nx.sval ? a.samp_ray[s_next] : 0;
+            }
+        }, ts);
+        // block3.2: 256 -> 256 transposed: acc[t][i] = h[row 4 g + i][unit 16 t + (l & 15)]
+        auto &acc = in2;  // block3.0's input is dead: its registers take block3.2's accumulators
+#pragma unroll
+        for (int t = 0; t < 16; ++t) acc[t] = f32x4{};
+        run_layer16<Net, L3, true>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) { return chain_k(acc2, inv2, k); },
+                                  [&](auto c) {
+                                      constexpr int C = decltype(c)::value;
+                                      if constexpr (C == 0) rnext = load_rec16(a, nx);
+                                  }, ts);
+        load_p(nx.pid, acc2);  // the next tile's P (see accA)
+        X3T();  // block3.2 MFMAs issued
+        // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads
+        // from the compiler's wait tracking, which would otherwise wait for the epilogue's stores
+        asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            asm volatile("" : "+v"(rnext.p[c]), "+v"(rnext.col[c]), "+v"(rnext.dir[c]), "+v"(rnext.l[c]), "+v"(rnext.v[c]),
+                              "+v"(rnext.pp[c]), "+v"(rnext.pl[c]));
+        asm volatile("" : "+v"(rnext.cf));
+
+        float wv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            wv[i] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, rw.wgt)));
+        const float inv3 = Yl[Y_INV + 3];
+        float ap[4] = {0.f, 0.f, 0.f, 0.f}, fs[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const float bu = Yl[Y_B3 + 16 * t + r], wau = Yl[Y_WA + 16 * t + r];
+            float fg = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float y = __builtin_fmaf(acc[t][i], inv3, bu);
+                const float hv = fmaxf(y, 0.01f * y);
+                ap[i] = __builtin_fmaf(wau, hv, ap[i]);
+                fg = __builtin_fmaf(wv[i], hv, fg);
+            }
+            // + the sample's other 4 neighbours (lane group g ^ 1, 16 lanes away)
+            float x = fg, y = fg;
+            permlane16_swap(x, y);
+            fs[t] = x + y;
+        }
+        X3T();  // block3.2 epilogue (K-blend, alpha partials)
+        {   // f_s (units 16 t + r of sample g >> 1) -> LDS transpose -> two 16-B stores per lane
+            float *st = (float *)(ldsi + FSW16_OFF + w * 2048);
+            if ((g & 1) == 0) {
+#pragma unroll
+                for (int t = 0; t < 16; ++t) st[(g >> 1) * 256 + 16 * t + r] = fs[t];
+            }
+            const f32x4 v0 = *(const f32x4 *)(st + (lane >> 5) * 256 + 8 * (lane & 31));
+            const f32x4 v1 = *(const f32x4 *)(st + (lane >> 5) * 256 + 8 * (lane & 31) + 4);
+            const int it = base + w * 2 + (lane >> 5);
+            const uint32_t off = it < end ? (uint32_t)((it - a.item0) * HID + 8 * (lane & 31)) * 4 : 0xFFFF0000u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), fs_rsrc, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), fs_rsrc, off, 16, 0);
+        }
+        // alpha: row logits summed over the 16 lanes (units) of the group, softplus(x + b - 1),
+        // blended over the sample's 8 rows (4 here, 4 in group g ^ 1)
+        float as = 0.f;
+        const float ba = Yl[Y_BA];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float x = dpp_sum8(ap[i]);
+            x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
+            as = __builtin_fmaf(wv[i], softplus(x + ba - 1.f), as);
+        }
+        {
+            float x = as, y = as;
+            permlane16_swap(x, y);
+            as = x + y;
+        }
+        // sample g >> 1 of this wave: its id sits in row 8 (g >> 1) (lane 8 (g >> 1))
+        const int s_of = __builtin_amdgcn_ds_bpermute((8 * (g >> 1)) * 4, ix.s);
+        const int it = base + w * 2 + (g >> 1);
+        if (r == 0 && (g & 1) == 0 && it < end) a.feat[(int64_t)s_of * 4 + 0] = as;
+        X3T();  // tile end
+    }
+#undef X3T
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- host packing of the 16x16 sections -------------------------------------------------
+// B position p = 8 g + j of a chained k-step -> unit offset inside the 32-wide step
+int perm16(int p) { return 16 * ((p & 7) >> 2) + 4 * (p >> 3) + (p & 3); }
+int col_chain16(int ks, int p) { return 32 * ks + perm16(p); }
+int col_l2_16(int ks, int p) { return ks < 8 ? col_chain16(ks, p) : (p < 7 ? 256 + p : -1); }
+int col_l0b16(int s, int p) {  // pe_dists16: pair 8 g + 4 s + j / 2, sin / cos by j parity
+    const int pp = 8 * (p >> 3) + 4 * s + ((p & 7) >> 1);
+    return pp < 30 ? 224 + 2 * pp + (p & 1) : -1;
+}
+int col_proj16(int s, int p) { return s == 0 ? p : 32 + 48 * (p >> 3) + 8 * (s - 1) + (p & 7); }
+int col_bp16(int ks, int p) { return ks < 8 ? col_chain16(ks, p) : 256 + 32 * (ks - 8) + p; }
+
+// 16 output tiles of 16 units, one pass, k-outer: pair f = ks * 16 + t; A[unit][k] fragment
+// lane l: unit 16 t + (l & 15), input col(ks, 8 (l >> 4) + e)
+template <typename ColFn>
+void pack_pairs16(_Float16 *dst, const float *W, int n_out, int n_in, int KS, int shift, ColFn col) {
+    const float sc = ldexpf(1.f, shift);
+    for (int t = 0; t < 16; ++t)
+        for (int ks = 0; ks < KS; ++ks) {
+            const size_t f = (size_t)ks * 16 + t;
+            for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                    const int row = 16 * t + (lane & 15);
+                    const int c = col(ks, 8 * (lane >> 4) + e);
+                    const float v = (row < n_out && c >= 0 && c < n_in) ? W[(size_t)row * n_in + c] * sc : 0.f;
+                    const _Float16 hi = (_Float16)v;
+                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    dst[((2 * f) * 64 + lane) * 8 + e] = hi;
+                    dst[((2 * f + 1) * 64 + lane) * 8 + e] = lo;
+                }
+        }
+}
+
+void pack_blob16(int ksb, int bpnet_dim, const float *const *w, const float *const *b, const int *s, int sb,
+                 uint8_t *blob) {
+    auto fr = [&](uint32_t off) { return (_Float16 *)(blob + off); };
+    pack_pairs16(fr(OFF16_W0B), w[0], 256, 284, 2, s[0], col_l0b16);
+    pack_pairs16(fr(OFF16_W1), w[1], 256, 256, 8, s[1], col_chain16);
+    pack_pairs16(fr(OFF16_W2), w[2], 256, 263, 9, s[2], col_l2_16);
+    pack_pairs16(fr(OFF16_W3), w[3], 256, 256, 8, s[3], col_chain16);
+    pack_pairs16(fr(OFF16_W0A), w[0], 256, 284, 7, s[0], col_proj16);
+    float *Y = (float *)(blob + OFF16_F32);
+    for (int u = 0; u < HID; ++u) {
+        Y[Y_B0 + u] = b[0][u] * ldexpf(1.f, s[0]);
+        Y[Y_B1 + u] = b[1][u] * ldexpf(1.f, s[1]);
+        Y[Y_B2 + u] = b[2][u] * ldexpf(1.f, s[2]);
+        Y[Y_B3 + u] = b[3][u];
+        Y[Y_WA + u] = w[4][u];
+    }
+    Y[Y_BA] = b[4][0];
+    const int li[7] = {0, 1, 2, 3, 5, 6, 7};
+    for (int i = 0; i < 7; ++i) Y[Y_INV + i] = ldexpf(1.f, -s[li[i]]);
+    Y[Y_INV + 7] = 1.f;
+    if (ksb > 0) {
+        const int nin = 256 + bpnet_dim;
+        pack_pairs16(fr(OFF16_WB), w[9], 256, nin, 8 + bpnet_dim / 32, sb, col_bp16);
+        for (int u = 0; u < HID; ++u) Y[Y_BB + u] = b[9][u] * ldexpf(1.f, sb);
+        Y[Y_INV + 7] = ldexpf(1.f, -sb);
+    }
+}
+
 // ---- colour MLP ------------------------------------------------------------------------
 struct ColorArgs {
     const int32_t *counters, *work, *samp_ray;
@@ -949,12 +1538,15 @@ void pack_blob_x3(int ksb, int bpnet_dim, const float *const *w, const float *co
     const int li[7] = {0, 1, 2, 3, 5, 6, 7};
     for (int i = 0; i < 7; ++i) F[XF_INV + i] = ldexpf(1.f, -s[li[i]]);
     F[XF_INV + 7] = 1.f;
+    int sb = 0;
     if (ksb > 0) {
-        const int nin = 256 + bpnet_dim, sb = layer_shift(w[9], (size_t)256 * nin);
+        const int nin = 256 + bpnet_dim;
+        sb = layer_shift(w[9], (size_t)256 * nin);
         pack_pairs(fr(OFF_WB), w[9], 256, nin, T_HID, ksb, 4, sb, col_bp);
         pack_acc_order(F + XF_BB, b[9], T_HID, ldexpf(1.f, sb));
         F[XF_INV + 7] = ldexpf(1.f, -sb);
     }
+    pack_blob16(ksb, bpnet_dim, w, b, s, sb, blob);
 }
 
 int variant_ksb(int32_t bpnet_layers, int32_t bpnet_dim) {
@@ -964,6 +1556,20 @@ int variant_ksb(int32_t bpnet_layers, int32_t bpnet_dim) {
 }
 
 }  // namespace x3
+}  // namespace
+}  // namespace sgn
+
+namespace sgn {
+namespace {
+// 1 (default): the 2-waves-per-SIMD 16x16x32 row / projection kernels; 0: the 32x32x16 ones
+// (SGN_X3_W16=0 in the environment, read once; both produce identical-precision results)
+int x3_w16() {
+    static const int v = [] {
+        const char *e = getenv("SGN_X3_W16");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
 }  // namespace
 }  // namespace sgn
 
@@ -999,10 +1605,17 @@ int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void
     SGN_REQUIRE(pt->n_points >= 0 && (pt->n_points == 0 || pt->embedding), "embedding required");
     SGN_REQUIRE(((uintptr_t)d_proj & 15) == 0 && ((uintptr_t)pt->embedding & 15) == 0, "16-byte alignment required");
     if (pt->n_points == 0) return 0;
-    x3::ProjArgs a{pt->embedding, pt->n_points, d_packed, (float *)d_proj};
-    const int64_t tiles = (pt->n_points + 32 * x3::NW - 1) / (32 * x3::NW);
-    hipLaunchKernelGGL(x3::k_point_proj_x3, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB), 0,
-                       as_stream(stream), a);
+    if (x3_w16()) {
+        x3::Proj16Args a{pt->embedding, pt->n_points, d_packed, (float *)d_proj};
+        const int64_t tiles = (pt->n_points + 16 * x3::NW16 - 1) / (16 * x3::NW16);
+        hipLaunchKernelGGL(x3::k_point_proj16, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB16), 0,
+                           as_stream(stream), a);
+    } else {
+        x3::ProjArgs a{pt->embedding, pt->n_points, d_packed, (float *)d_proj};
+        const int64_t tiles = (pt->n_points + 32 * x3::NW - 1) / (32 * x3::NW);
+        hipLaunchKernelGGL(x3::k_point_proj_x3, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB), 0,
+                           as_stream(stream), a);
+    }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }
@@ -1055,7 +1668,7 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
 #ifdef SGN_X3_TIMING
     static unsigned long long *tbuf = nullptr;
-    const size_t tn = (size_t)x3::TD_BLOCKS * x3::NW * x3::TD_EV;
+    const size_t tn = (size_t)x3::TD_BLOCKS * x3::NW16 * x3::TD_EV;
     if (!tbuf) SGN_CHECK_HIP(hipMalloc(&tbuf, tn * 8));
     SGN_CHECK_HIP(hipMemsetAsync(tbuf, 0, tn * 8, st));
     a.tdbg = tbuf;
@@ -1069,7 +1682,11 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
         a.fs = (_Float16 *)fs;
         c.fs = fs;
         const int64_t wg = (n + x3::WG_SAMPLES - 1) / x3::WG_SAMPLES;
-        if (stages & 1) {
+        if ((stages & 1) && x3_w16()) {
+            auto kern = ksb == 0 ? x3::k_rows16<0> : ksb == KS_HID ? x3::k_rows16<8> : x3::k_rows16<11>;
+            const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES;
+            hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < 256 ? wg16 : 256)), dim3(x3::TPB16), 0, st, a);
+        } else if (stages & 1) {
             auto kern = ksb == 0 ? x3::k_agg_rows_x3<0> : ksb == KS_HID ? x3::k_agg_rows_x3<KS_HID>
                                                                         : x3::k_agg_rows_x3<ks_bp(BP_DIM)>;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(x3::TPB), 0, st, a);

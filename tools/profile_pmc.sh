@@ -4,7 +4,7 @@
 set -e
 OUT=${1:-gpurun_out/pmc}
 shift || true
-ARGS=${@:---steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${@:---steps 2 --warmup 1 --no-cpu-baseline --no-extras}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p "$OUT"
 i=0
@@ -15,7 +15,7 @@ for grp in \
   "FETCH_SIZE TCC_HIT_sum" \
   "WRITE_SIZE TCC_MISS_sum" ; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-k_agg_rows|k_knn|k_march|k_color|k_composite}" \
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-k_agg_rows|k_rows16|k_point_proj|k_knn|k_march|k_color|k_composite}" \
       -d "$OUT/p$i" -o pmc --output-format csv -- python bench.py $ARGS > "$OUT/p$i.log" 2>&1
 done
 echo PMC_DONE
