@@ -17,17 +17,48 @@ groups lr / plr with iter_exponential_decay, DP all-reduce when torch.distribute
 setup_optimizer / clean_optimizer / init_scheduler / prune_points / grow_points follow
 models/mvs_points_volumetric_model.py:47-141,195-270 and neural_points.py:520-572.  The
 trainable tensors are shared with `neural_points`, so test() renders the current state.
+
+SG-NeRF's extra surface: the probe ranking (update_rank_ray_miss / rank_ray_miss /
+reset_ray_miss_ranking, top_ray_miss_loss / top_ray_miss_ids, mvs_points_volumetric_model.py:
+157-189) fed by the ray_miss_coarse_raycolor loss of every step; the semantic dumps
+saveSemanticEmbedding / saveSemanticPoints / saveSemanticPoints_test
+(neural_points_volumetric_model.py:337-362, 674-720); checkpoints carry
+neural_points.points_feats / points_label / bpnet_points_embedding.  set_bg (plane background)
+is refused: that background model is not on the hot path.  Pruning keeps the semantic
+per-point arrays aligned with the points (the reference leaves them unpruned).
 """
 import dataclasses
 import os
 
+import numpy as np
 import torch
 
 from .opts import HotPathOpts
 from .ray_marching import NeuralPoints, NeuralPointsRayMarching
 from .weights import strip_prefix
 
-LOSS_NAMES = ["total", "ray_masked_coarse_raycolor", "conf_coefficient"]
+LOSS_NAMES = ["total", "ray_masked_coarse_raycolor", "ray_miss_coarse_raycolor", "coarse_raycolor",
+              "conf_coefficient"]
+
+# ScanNet-20 label colours of the reference's point dumps (neural_points_volumetric_model.py:35-57)
+LABEL_RGB = {0: (174, 198, 232), 1: (151, 223, 137), 2: (31, 120, 180), 3: (255, 188, 120), 4: (188, 189, 35),
+             5: (140, 86, 74), 6: (255, 152, 151), 7: (213, 39, 40), 8: (196, 176, 213), 9: (148, 103, 188),
+             10: (196, 156, 148), 11: (23, 190, 208), 12: (247, 183, 210), 13: (218, 219, 141),
+             14: (254, 127, 14), 15: (227, 119, 194), 16: (158, 218, 229), 17: (43, 160, 45),
+             18: (112, 128, 144), 19: (82, 83, 163), 255: (255, 255, 170)}
+
+
+def label_colours(labels):
+    """[N] integer labels -> [N,3] RGB (0..255) through LABEL_RGB; an unknown label raises
+    KeyError, as the reference's dict lookup does."""
+    lab = np.asarray(labels).reshape(-1).astype(np.int64)
+    lut = np.full((256, 3), -1, np.int64)
+    for k, c in LABEL_RGB.items():
+        lut[k] = c
+    bad = (lab < 0) | (lab > 255)
+    if bad.any() or (lut[np.clip(lab, 0, 255), 0] < 0).any():
+        raise KeyError(f"label without a colour: {sorted(set(lab[bad | (lut[np.clip(lab, 0, 255), 0] < 0)].tolist()))[:8]}")
+    return lut[lab].astype(np.float32)
 
 
 class HipPointsVolumetricModel:
@@ -70,12 +101,32 @@ class HipPointsVolumetricModel:
         if self.is_train and self.neural_points is not None:
             self.setup_optimizer(opt)
             self.init_scheduler(int(getattr(opt, "resume_step", 0) or 0), opt)
+        # probe ranking buffers (mvs_points_volumetric_model.py:178-184)
+        prob_freq = int(getattr(opt, "prob_freq", 0) or 0)
+        nstep = int(getattr(opt, "prob_num_step", 100) or 0)
+        if prob_freq > 0 and train_len is not None and nstep > 1:
+            self.num_probe = train_len // nstep
+            self.reset_ray_miss_ranking()
+        elif prob_freq > 0 and train_len is not None and nstep == 1:
+            self.top_ray_miss_loss = torch.zeros([1], dtype=torch.float32, device=self.device)
 
-    def set_points(self, xyz, points_embeding, points_conf=None, points_dir=None, points_color=None,
-                   aggregator_state=None, Rw2c=None, **unused):
-        """neural_points.py:520-572; also takes the aggregator weights when no checkpoint is loaded.
-        In training the optimizers are rebuilt over the new points (mvs_points_volumetric_model.py:191-199)."""
-        self.neural_points = NeuralPoints(xyz, points_embeding, points_color, points_dir, points_conf, self.device)
+    def set_points(self, points_xyz, points_feats=None, points_embedding=None, points_label=None, points_color=None,
+                   points_dir=None, points_conf=None, points_semantic=None, Rw2c=None, eulers=None, editing=False,
+                   aggregator_state=None):
+        """mvs_points_volumetric_model.py:191-199 -> neural_points.py:575-600 (same argument names
+        and order); also takes the aggregator weights when no checkpoint is loaded.  In training
+        the optimizers are rebuilt over the new points."""
+        if editing:
+            raise NotImplementedError("set_points(editing=True) (point-cloud editing) is outside the HIP hot path")
+        if points_embedding is None:
+            raise ValueError("set_points: points_embedding is required")
+        if points_conf is None:
+            points_conf = torch.ones(points_embedding.shape[:-1] + (1,), dtype=torch.float32)
+        for name, t in (("points_color", points_color), ("points_dir", points_dir)):
+            if t is None:
+                raise NotImplementedError(f"set_points without {name}: the MFMA aggregator's inputs include it")
+        self.neural_points = NeuralPoints(points_xyz, points_embedding, points_color, points_dir, points_conf,
+                                          self.device, points_feats=points_feats, points_label=points_label)
         if aggregator_state is not None or self.net_ray_marching is None:
             if aggregator_state is None:
                 raise ValueError("set_points: aggregator_state required before the first render")
@@ -149,21 +200,33 @@ class HipPointsVolumetricModel:
         self._sync_weights()
         p = self.neural_points
         mask = p.points_conf[0, :, 0] >= thresh
+        keep = lambda t: None if t is None or t.shape[-2 if t.dim() == 3 else 0] != mask.shape[0] else (  # noqa: E731
+            t[:, mask] if t.dim() == 3 else t[mask])
         self.neural_points = NeuralPoints(p.xyz[mask], p.points_embeding[:, mask], p.points_color[:, mask],
-                                          p.points_dir[:, mask], p.points_conf[:, mask], self.device)
+                                          p.points_dir[:, mask], p.points_conf[:, mask], self.device,
+                                          points_feats=keep(p.points_feats), points_label=keep(p.points_label),
+                                          bpnet_points_embedding=keep(p.bpnet_points_embedding))
         self.net_ray_marching.neural_points = self.neural_points
         return int((~mask).sum())
 
     def grow_points(self, add_xyz, add_embedding, add_color, add_dir, add_conf, add_label=None, **unused):
-        """neural_points.py:546-572: append points (embedding/colour/dir/conf given as [M, C])."""
+        """neural_points.py:546-572: append points (embedding/colour/dir/conf given as [M, C]).
+        Labels are appended when both sides have them (:550); points_feats is kept as it is,
+        as the reference keeps it."""
         self._sync_weights()
         p = self.neural_points
         f = lambda t, c: torch.as_tensor(t).to(self.device, torch.float32).reshape(1, -1, c)  # noqa: E731
+        label = p.points_label
+        if label is not None and add_label is not None:
+            label = torch.cat([label, torch.as_tensor(add_label).to(label.device, label.dtype).reshape(-1, 1)], 0)
+        elif label is not None:
+            label = None   # the reference's cat would fail; an unlabelled tail invalidates the labels
         self.neural_points = NeuralPoints(
             torch.cat([p.xyz, f(add_xyz, 3)[0]], 0),
             torch.cat([p.points_embeding, f(add_embedding, p.points_embeding.shape[-1])], 1),
             torch.cat([p.points_color, f(add_color, 3)], 1), torch.cat([p.points_dir, f(add_dir, 3)], 1),
-            torch.cat([p.points_conf, f(add_conf, 1)], 1), self.device)
+            torch.cat([p.points_conf, f(add_conf, 1)], 1), self.device, points_feats=p.points_feats,
+            points_label=label)
         self.net_ray_marching.neural_points = self.neural_points
         if self.is_train and getattr(self, "trainer", None) is not None:
             self.setup_optimizer(self.opt)
@@ -220,7 +283,94 @@ class HipPointsVolumetricModel:
         self.output = {"coarse_raycolor": full[None], "ray_mask": ray_mask[None].to(torch.int8)}
         self.coarse_raycolor = self.output["coarse_raycolor"]
         self.ray_mask = self.output["ray_mask"]
+        self.update_rank_ray_miss(total_steps)   # neural_points_volumetric_model.py:328-330
         return parts
+
+    # -- probe ranking (mvs_points_volumetric_model.py:157-184) ------------------------------
+    def update_rank_ray_miss(self, total_steps):
+        """Rank this frame by its ray_miss_coarse_raycolor loss among the top frames the next
+        probe visits (prob_num_step > 1), or keep the running maximum (prob_num_step == 1)."""
+        opt = self.opt
+        if getattr(self, "top_ray_miss_loss", None) is None or not hasattr(self, "loss_ray_miss_coarse_raycolor"):
+            return
+        ks = getattr(opt, "prob_kernel_size", None)
+        tiers = getattr(opt, "prob_tiers", 250000)
+        if ks is not None and np.sum(np.asarray(tiers) < total_steps) >= len(ks) // 3:
+            return
+        prob_freq = int(getattr(opt, "prob_freq", 0) or 0)
+        nstep = int(getattr(opt, "prob_num_step", 100) or 0)
+        loss = self.loss_ray_miss_coarse_raycolor.reshape(()).to(self.top_ray_miss_loss.device)
+        if prob_freq > 0 and nstep > 1:
+            self.top_ray_miss_loss, self.top_ray_miss_ids = self.rank_ray_miss(
+                self.input["id"][0], loss, self.top_ray_miss_ids, self.top_ray_miss_loss)
+        elif prob_freq > 0 and nstep == 1:
+            self.top_ray_miss_loss[0] = torch.maximum(loss, self.top_ray_miss_loss[0])
+
+    def rank_ray_miss(self, new_id, newloss, inds, losses):
+        """mvs_points_volumetric_model.py:166-176: a frame already ranked keeps its largest loss,
+        a new frame replaces the last entry; then sort by loss, descending.  Branch-free on the
+        device (the reference's `if torch.sum(mask) > 0` is a host sync per step)."""
+        with torch.no_grad():
+            new_id = torch.as_tensor(new_id, device=inds.device).reshape(()).to(inds.dtype)
+            newloss = torch.as_tensor(newloss, device=losses.device).reshape(()).to(losses.dtype)
+            mask = inds == new_id
+            hit = mask.any()
+            last = torch.zeros_like(mask)
+            last[-1] = True
+            losses = torch.where(hit, torch.where(mask, torch.maximum(losses, newloss), losses),
+                                 torch.where(last, newloss, losses))
+            inds = torch.where(hit, inds, torch.where(last, new_id, inds))
+            losses, order = torch.sort(losses, descending=True)
+            return losses, inds[order]
+
+    def reset_ray_miss_ranking(self):
+        """mvs_points_volumetric_model.py:187-189."""
+        self.top_ray_miss_loss = torch.zeros([self.num_probe + 1], dtype=torch.float32, device=self.device)
+        self.top_ray_miss_ids = torch.arange(self.num_probe + 1, dtype=torch.int32, device=self.device)
+
+    def set_bg(self, xyz_world_sect_plane, img_lst, c2ws_lst, w2cs_lst, intrinsics_all, HDWD_lst, plane_color=None,
+               fg_masks=None, **kwargs):
+        """mvs_points_volumetric_model.py:305-343 warps source images onto a background plane for
+        bgmodel '*plane'.  That background model is outside the per-ray hot path: refuse it."""
+        raise NotImplementedError("set_bg: bgmodel '*plane' (image-warped plane background) is not part of the "
+                                  "HIP hot path; use bgmodel 'no' with a bg_color")
+
+    # -- semantic dumps (neural_points_volumetric_model.py:337-362, 674-720) ------------------
+    def _semantic_dir(self):
+        return os.path.join(getattr(self.opt, "checkpoints_dir", "."), getattr(self.opt, "name", "sgn"))
+
+    def saveSemanticEmbedding(self, epoch):
+        """`{epoch}_semanticEmbedding.pth`: the BPNet per-point embedding [N,96] on the CPU
+        (None when BPNet never ran, as in the reference)."""
+        e = self.neural_points.bpnet_points_embedding if self.neural_points is not None else None
+        e = None if e is None else e.detach().reshape(e.shape[-2], e.shape[-1]).cpu()
+        path = os.path.join(self._semantic_dir(), f"{epoch}_semanticEmbedding.pth")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        torch.save(e, path)
+        return path
+
+    def _save_label_points(self, path):
+        p = self.neural_points
+        if p is None or p.points_label is None:
+            raise RuntimeError("saveSemanticPoints: no per-point labels (set_points(points_label=...) or "
+                               "neural_points.set_bpnet_feats)")
+        lab = p.points_label.reshape(-1).cpu().numpy()
+        xyz = p.xyz.detach().cpu().numpy()
+        if lab.shape[0] != xyz.shape[0]:
+            raise RuntimeError(f"saveSemanticPoints: {lab.shape[0]} labels for {xyz.shape[0]} points")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        np.savetxt(path, np.concatenate([xyz.astype(np.float32), label_colours(lab)], 1), fmt="%f")
+        print("savepoints:", path)
+        return path
+
+    def saveSemanticPoints(self, train_steps):
+        """`predict_points_{train_steps}.txt`: x y z r g b per point, the label's colour."""
+        return self._save_label_points(os.path.join(self._semantic_dir(), f"predict_points_{train_steps}.txt"))
+
+    def saveSemanticPoints_test(self, totalIter, imgNum):
+        """`test_{totalIter}/test_predict_points_iter{totalIter}_imgNum{imgNum}.txt`."""
+        return self._save_label_points(os.path.join(self._semantic_dir(), f"test_{totalIter}",
+                                                    f"test_predict_points_iter{totalIter}_imgNum{imgNum}.txt"))
 
     def update_learning_rate(self, opt=None, total_steps=None, **k):
         """Schedulers are the trainer's iter_exponential_decay, applied at every step."""

@@ -51,9 +51,14 @@ class NeuralPoints:
     """Neural point parameters under the reference names (neural_points.py:321-423):
     xyz [N,3], points_embeding [1,N,F], points_color [1,N,3], points_dir [1,N,3],
     points_conf [1,N,1].  `tables()` gives the flat fp32 device view the kernels read;
-    it is rebuilt only when a tensor changes (torch version counter)."""
+    it is rebuilt only when a tensor changes (torch version counter).
 
-    def __init__(self, xyz, points_embeding, points_color, points_dir, points_conf, device="cuda"):
+    The semantic attributes ride along: points_feats [N,3] (the init cloud's RGB in 0..255,
+    BPNet's input, scannet_ft_dataset.py:482 / neural_points.py:589-590), points_label [N,1]
+    and bpnet_points_embedding [1,N,96] (neural_points.py:653-665)."""
+
+    def __init__(self, xyz, points_embeding, points_color, points_dir, points_conf, device="cuda",
+                 points_feats=None, points_label=None, bpnet_points_embedding=None):
         dev = torch.device(device)
         f = dict(dtype=torch.float32, device=dev)
         self.xyz = torch.as_tensor(xyz).to(**f).reshape(-1, 3)
@@ -68,6 +73,11 @@ class NeuralPoints:
         self.bpnet_points_embedding = None  # [1,N,96], detached
         self.points_label = None            # [N,1]
         self.points_label_prob = None
+        self.points_feats = None if points_feats is None else torch.as_tensor(points_feats).to(**f).reshape(-1, 3)
+        if points_label is not None:
+            self.points_label = torch.as_tensor(points_label).to(dev).reshape(-1, 1)
+        if bpnet_points_embedding is not None:
+            self.bpnet_points_embedding = torch.as_tensor(bpnet_points_embedding).detach().to(**f).reshape(1, n, -1)
         self._tables = None
         self._key = None
 
@@ -81,17 +91,32 @@ class NeuralPoints:
 
     @classmethod
     def from_state_dict(cls, sd, device="cuda", prefix="neural_points."):
-        """Reference checkpoint layout (`*_net_ray_marching.pth`: neural_points.xyz, ...)."""
+        """Reference checkpoint layout (`*_net_ray_marching.pth`: neural_points.xyz, ...;
+        neural_points.py:321-386).  points_feats / points_label / bpnet_points_embedding are
+        read when the file holds them (the reference requires points_feats, :362; the other
+        two are optional here as they are there)."""
         g = lambda k: sd[prefix + k]  # noqa: E731
-        return cls(g("xyz"), g("points_embeding"), g("points_color"), g("points_dir"), g("points_conf"), device)
+        o = lambda k: sd.get(prefix + k)  # noqa: E731
+        p = cls(g("xyz"), g("points_embeding"), g("points_color"), g("points_dir"), g("points_conf"), device,
+                points_feats=o("points_feats"), points_label=o("points_label"),
+                bpnet_points_embedding=o("bpnet_points_embedding"))
+        if o("Rw2c") is not None:
+            p.Rw2c = torch.as_tensor(o("Rw2c")).to(p.device, torch.float32)
+        return p
 
     @classmethod
     def from_cloud(cls, pc, device="cuda"):
         return cls(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, device)
 
     def state_dict(self, prefix="neural_points."):
-        return {prefix + k: getattr(self, k) for k in
-                ("xyz", "points_embeding", "points_color", "points_dir", "points_conf", "Rw2c")}
+        """The reference's keys; the semantic ones only when set (a reference loader reads
+        points_feats unconditionally, so checkpoints meant for it need set_points(points_feats=...))."""
+        sd = {prefix + k: getattr(self, k) for k in
+              ("xyz", "points_embeding", "points_color", "points_dir", "points_conf", "Rw2c")}
+        for k in ("points_feats", "points_label", "bpnet_points_embedding"):
+            if getattr(self, k) is not None:
+                sd[prefix + k] = getattr(self, k)
+        return sd
 
     def _version_key(self):
         ts = (self.xyz, self.points_embeding, self.points_color, self.points_dir, self.points_conf)

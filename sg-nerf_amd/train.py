@@ -216,7 +216,14 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     # = F.mse_loss(full[ray_mask], gt[ray_mask]) (0 when no ray is valid), as a masked mean so
     # the step issues no host sync (boolean indexing would wait for the mask's count)
     wm = ray_mask.to(full.dtype)[:, None]
-    l_col = torch.sum((full - gt) ** 2 * wm) / torch.clamp(wm.sum() * 3, min=1.0)
+    se = (full - gt) ** 2
+    l_col = torch.sum(se * wm) / torch.clamp(wm.sum() * 3, min=1.0)
+    # ray_miss_coarse_raycolor (:553-563) = mse over the missed rays x their count = their sum / 3;
+    # coarse_raycolor = mse over every ray.  Both carry weight 0: logged, and ranked per frame by
+    # the probe (mvs_points_volumetric_model.py:157-176), never differentiated.
+    with torch.no_grad():
+        l_miss = torch.sum(se * (1 - wm)) / 3
+        l_all = se.mean()
     # zero_one_loss on conf_coefficient (:607-614) over the reference's dense [R'', SR, K] tensor
     # (point_aggregators.py:951-958): every (slot, k) of a valid ray, where empty slots and masked
     # neighbours read conf at the clamped index 0 (neural_points.py:956-967)
@@ -238,7 +245,8 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     n_e = wr.sum() * (SR * K)
     l_zo = torch.sum((torch.log(val) + torch.log(1 - val)) * wr) / torch.clamp(n_e, min=1.0)
     total = l_col + 3e-6 + zero_one_weight * l_zo
-    return total, {"ray_masked_coarse_raycolor": l_col.detach(), "conf_coefficient": l_zo.detach()}, full, ray_mask
+    return total, {"ray_masked_coarse_raycolor": l_col.detach(), "ray_miss_coarse_raycolor": l_miss,
+                   "coarse_raycolor": l_all, "conf_coefficient": l_zo.detach()}, full, ray_mask
 
 
 def _allreduce_buckets(grads, bucket_elems):

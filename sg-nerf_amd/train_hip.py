@@ -401,7 +401,9 @@ class HipTrainer:
             cw.copy_(fl[c0:c1])                 # colour weights as their own leaf: autograd
             for t in (fs32, al32, cw):          # never touches the full flat parameter
                 t.grad.zero_()
-        v = st["raydir"][q.samp_ray[:Sc][samp_c]]
+        # padding items read sample 0's ray, which is unwritten when the step has no samples:
+        # mask the gathered ray index too, so the raydir gather stays in bounds
+        v = st["raydir"][torch.where(ok_i, q.samp_ray[:Sc][samp_c], 0)]
         feat_s = torch.cat([al32[:, None], self._colour(fs32, v, cw, c0)], dim=-1)
         featS = torch.zeros(Sc + 1, 4, device=dev).index_put((samp,), feat_s)[:Sc]
         validS = torch.zeros(Sc + 1, dtype=torch.bool, device=dev).index_put((samp,), st["true"])[:Sc]

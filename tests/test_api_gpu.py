@@ -146,8 +146,8 @@ def test_model_plugin_checkpoint_roundtrip(tmp_path):
     HipPointsVolumetricModel.modify_commandline_options(argparse.ArgumentParser(), False)
     m = HipPointsVolumetricModel()
     m.initialize(opt)
-    m.set_points(pts["xyz"], pts["embedding"], points_conf=pts["conf"], points_dir=pts["dir"],
-                 points_color=pts["color"], aggregator_state=mlp)
+    m.set_points(points_xyz=pts["xyz"], points_embedding=pts["embedding"], points_conf=pts["conf"],
+                 points_dir=pts["dir"], points_color=pts["color"], aggregator_state=mlp)
     m.set_input(_inputs(case))
     out1 = {k: v.clone() for k, v in m.test().items()}
     assert np.abs(out1["coarse_raycolor"][0].cpu().numpy() - case["full_color"]).max() <= RGB_TOL

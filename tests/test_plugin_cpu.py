@@ -1,0 +1,199 @@
+"""The model plugin's host-side surface on the CPU (no kernels run): checkpoint keys the
+reference's NeuralPoints reads, the train_ft.py save block and probe guard, the ray-miss
+ranking, the semantic point dumps and set_bg's refusal.
+
+  run/train_ft.py:1006-1020   save block (saveSemanticEmbedding + save_networks in try/except)
+  run/train_ft.py:888-891     probe guard (top_ray_miss_loss[0] > 1e-5 ...)
+  models/neural_points/neural_points.py:321-386   checkpoint key reads
+  models/mvs_points_volumetric_model.py:157-189   update_rank_ray_miss / rank_ray_miss / reset
+  models/neural_points_volumetric_model.py:674-720 saveSemanticPoints(_test) text format
+"""
+import argparse
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from sgnerf_amd.model import LABEL_RGB, HipPointsVolumetricModel, label_colours
+from sgnerf_amd.ray_marching import NeuralPoints
+
+N = 50
+
+
+def _points(seed=0, labels=True, bpnet=True):
+    g = torch.Generator().manual_seed(seed)
+    r = lambda *s: torch.rand(*s, generator=g)  # noqa: E731
+    lab = torch.randint(0, 20, (N,), generator=g)
+    lab[:3] = 255
+    return NeuralPoints(r(N, 3), r(1, N, 32), r(1, N, 3), r(1, N, 3), r(1, N, 1), "cpu",
+                        points_feats=r(N, 3) * 255, points_label=lab if labels else None,
+                        bpnet_points_embedding=r(N, 96) if bpnet else None)
+
+
+def _model(tmp_path, **extra):
+    opt = argparse.Namespace(SR=24, K=8, gpu_ids=[0], is_train=True, checkpoints_dir=str(tmp_path), name="scene",
+                             bg_color="white", **extra)
+    m = HipPointsVolumetricModel()
+    m.initialize(opt)
+    m.device = torch.device("cpu")     # host-only: no renderer, no kernels
+    m.is_train = False                 # no HipTrainer (setup() would build one)
+    m.neural_points = _points()
+    mlp = {"block1.0.weight": torch.ones(2, 2)}
+    m.net_ray_marching = types.SimpleNamespace(renderer=types.SimpleNamespace(mlp_state=mlp))
+    return m
+
+
+def _reference_key_reads(sd):
+    """What NeuralPoints.__init__ reads from a checkpoint (neural_points.py:332-386): xyz and
+    points_feats unconditionally, the rest when present."""
+    got = {"xyz": sd["neural_points.xyz"], "points_feats": sd["neural_points.points_feats"]}
+    for k in ("points_embeding", "points_conf", "points_dir", "points_color", "eulers", "Rw2c"):
+        if "neural_points." + k in sd:
+            got[k] = sd["neural_points." + k]
+    return got
+
+
+def test_checkpoint_keys_round_trip(tmp_path):
+    m = _model(tmp_path)
+    m.save_networks(7, {"total_steps": 7})
+    sd = torch.load(tmp_path / "scene" / "7_net_ray_marching.pth", map_location="cpu", weights_only=True)
+    got = _reference_key_reads(sd)
+    p = m.neural_points
+    assert got["points_feats"].shape == (N, 3) and torch.equal(got["points_feats"], p.points_feats)
+    assert got["points_embeding"].shape == (1, N, 32)
+    assert torch.equal(sd["neural_points.points_label"].reshape(-1), p.points_label.reshape(-1))
+    assert sd["neural_points.bpnet_points_embedding"].shape == (1, N, 96)
+    assert "aggregator.block1.0.weight" in sd
+    q = NeuralPoints.from_state_dict(sd, "cpu")
+    for k in ("xyz", "points_embeding", "points_color", "points_dir", "points_conf", "points_feats", "points_label",
+              "bpnet_points_embedding"):
+        assert torch.equal(getattr(q, k), getattr(p, k)), k
+    # without the optional semantic keys the file still loads (labels / embedding stay unset)
+    for k in ("neural_points.points_label", "neural_points.bpnet_points_embedding"):
+        del sd[k]
+    q = NeuralPoints.from_state_dict(sd, "cpu")
+    assert q.points_label is None and q.bpnet_points_embedding is None
+    assert torch.load(tmp_path / "scene" / "7_states.pth", weights_only=True) == {"total_steps": 7}
+
+
+def test_save_block_replay(tmp_path):
+    """train_ft.py:1006-1020 with total_steps == 1: embedding dump, then the checkpoint."""
+    m = _model(tmp_path)
+    total_steps, best_PSNR, best_iter, epoch = 1, 0.0, 0, 0
+    errors = []
+    try:
+        if total_steps == 1 or (total_steps % 1000 == 0 and total_steps > 0):
+            m.saveSemanticEmbedding(total_steps)
+            other_states = {"best_PSNR": best_PSNR, "best_iter": best_iter, "epoch_count": epoch,
+                            "total_steps": total_steps}
+            m.save_networks(total_steps, other_states)
+    except Exception as e:  # the reference prints and carries on
+        errors.append(e)
+    assert not errors
+    emb = torch.load(tmp_path / "scene" / "1_semanticEmbedding.pth", weights_only=True)
+    assert emb.shape == (N, 96) and torch.equal(emb, m.neural_points.bpnet_points_embedding[0])
+    assert (tmp_path / "scene" / "1_net_ray_marching.pth").is_file()
+    # before BPNet ran the reference saves None
+    m.neural_points.bpnet_points_embedding = None
+    m.saveSemanticEmbedding(2)
+    assert torch.load(tmp_path / "scene" / "2_semanticEmbedding.pth", weights_only=True) is None
+
+
+def _rank_ref(new_id, newloss, inds, losses):
+    """Plain restatement of mvs_points_volumetric_model.py:166-176 on lists."""
+    inds, losses = list(inds), list(losses)
+    hit = [i for i, x in enumerate(inds) if x == new_id]
+    if hit:
+        for i in hit:
+            losses[i] = max(newloss, losses[i])
+    else:
+        inds[-1], losses[-1] = new_id, newloss
+    order = sorted(range(len(losses)), key=lambda i: -losses[i])
+    return [losses[i] for i in order], [inds[i] for i in order]
+
+
+def test_ray_miss_ranking_and_probe_guard(tmp_path):
+    m = _model(tmp_path, prob_freq=10, prob_num_step=4, prob_kernel_size=None, prob_mode=0, far_thresh=-1.0)
+    m.setup(m.opt, train_len=20)
+    assert m.num_probe == 5
+    assert m.top_ray_miss_loss.tolist() == [0.0] * 6 and m.top_ray_miss_ids.tolist() == list(range(6))
+    assert m.top_ray_miss_ids.dtype == torch.int32
+    rng = np.random.default_rng(0)
+    ref_l, ref_i = [0.0] * 6, list(range(6))
+    for step in range(40):
+        fid = int(rng.integers(0, 20))
+        loss = float(rng.random()) * 1e-3      # distinct losses: the sort has no ties
+        m.input = {"id": torch.tensor([fid])}
+        m.loss_ray_miss_coarse_raycolor = torch.tensor(loss)
+        m.update_rank_ray_miss(step)
+        ref_l, ref_i = _rank_ref(fid, loss, ref_i, ref_l)
+        np.testing.assert_allclose(m.top_ray_miss_loss.numpy(), np.float32(ref_l), rtol=0, atol=0)
+        assert m.top_ray_miss_ids.tolist() == ref_i
+    # train_ft.py:888-891 probe guard reads the ranking's head
+    opt = m.opt
+    assert (m.top_ray_miss_loss[0] > 1e-5 or opt.prob_mode != 0 or opt.far_thresh > 0)
+    # the probe resets the ranking afterwards (train_ft.py:532-533)
+    m.reset_ray_miss_ranking()
+    assert not (m.top_ray_miss_loss[0] > 1e-5 or opt.prob_mode != 0 or opt.far_thresh > 0)
+    # prob_num_step == 1: a running maximum in one slot
+    m1 = _model(tmp_path, prob_freq=10, prob_num_step=1, prob_kernel_size=None)
+    m1.setup(m1.opt, train_len=20)
+    for loss in (0.3, 0.7, 0.5):
+        m1.input = {"id": torch.tensor([0])}
+        m1.loss_ray_miss_coarse_raycolor = torch.tensor(loss)
+        m1.update_rank_ray_miss(1)
+    assert m1.top_ray_miss_loss.tolist() == [pytest.approx(0.7)]
+    # past the last probe tier nothing is ranked (mvs_points_volumetric_model.py:158)
+    m2 = _model(tmp_path, prob_freq=10, prob_num_step=4, prob_kernel_size=[1.0, 1.0, 1.0], prob_tiers=[5])
+    m2.setup(m2.opt, train_len=20)
+    m2.input = {"id": torch.tensor([3])}
+    m2.loss_ray_miss_coarse_raycolor = torch.tensor(0.5)
+    m2.update_rank_ray_miss(100)
+    assert float(m2.top_ray_miss_loss.max()) == 0.0
+    m2.update_rank_ray_miss(2)
+    assert float(m2.top_ray_miss_loss[0]) == 0.5
+
+
+def test_semantic_point_dumps(tmp_path):
+    m = _model(tmp_path)
+    p = m.neural_points
+    f = m.saveSemanticPoints(1000)
+    assert f == os.path.join(str(tmp_path), "scene", "predict_points_1000.txt")
+    a = np.loadtxt(f)
+    assert a.shape == (N, 6)
+    np.testing.assert_allclose(a[:, :3], p.xyz.numpy(), atol=5e-7)
+    want = np.array([LABEL_RGB[int(x)] for x in p.points_label.reshape(-1)], np.float64)
+    np.testing.assert_array_equal(a[:, 3:], want)
+    with open(f) as fh:
+        assert fh.readline().split()[3] == "255.000000"      # np.savetxt fmt="%f" as the reference
+    g = m.saveSemanticPoints_test(300, 2)
+    assert g.endswith(os.path.join("test_300", "test_predict_points_iter300_imgNum2.txt"))
+    np.testing.assert_array_equal(np.loadtxt(g), a)
+    with pytest.raises(KeyError):
+        label_colours([21])
+    m.neural_points.points_label = None
+    with pytest.raises(RuntimeError):
+        m.saveSemanticPoints(1)
+
+
+def test_set_bg_refuses_plane_background(tmp_path):
+    m = _model(tmp_path)
+    with pytest.raises(NotImplementedError, match="plane"):
+        m.set_bg(None, [], [], [], [], [], plane_color=None)
+
+
+def test_set_points_reference_signature(tmp_path):
+    """mvs_points_volumetric_model.py:191 argument names, as run/train_ft.py:797 passes them."""
+    m = _model(tmp_path)
+    p = _points(1)
+    kw = dict(points_xyz=p.xyz, points_feats=p.points_feats, points_embedding=p.points_embeding,
+              points_color=p.points_color, points_dir=p.points_dir, points_conf=p.points_conf, Rw2c=None)
+    # a renderer already exists: the new points are bound to it without repacking weights
+    m._sync_weights = lambda: None
+    m.set_points(**kw)
+    assert torch.equal(m.neural_points.points_feats, p.points_feats)
+    assert m.net_ray_marching.neural_points is m.neural_points
+    with pytest.raises(NotImplementedError):
+        m.set_points(**kw, editing=True)

@@ -105,8 +105,8 @@ def test_model_plugin_training_surface(tmp_path):
                              lr=5e-4, plr=2e-3, lr_decay_exp=0.1, lr_decay_iters=1_000_000, bg_color="white")
     m = HipPointsVolumetricModel()
     m.initialize(opt)
-    m.set_points(pc.xyz, pc.embedding, points_conf=pc.conf, points_dir=pc.dir, points_color=pc.color,
-                 aggregator_state=mlp)
+    m.set_points(points_xyz=pc.xyz, points_feats=pc.color * 255.0, points_embedding=pc.embedding,
+                 points_color=pc.color, points_dir=pc.dir, points_conf=pc.conf, aggregator_state=mlp)
     m.setup(opt)
     inputs = {"campos": d(view.campos)[None], "raydir": d(view.raydir)[None], "camrotc2w": d(view.camrotc2w)[None],
               "near": torch.tensor([[[0.1]]]), "far": torch.tensor([[[8.0]]]), "gt_image": gt[None].to(DEV)}
@@ -255,3 +255,66 @@ def test_graph_captured_step_matches_eager_step():
         assert abs(a - b) <= 1e-3 * abs(a)
     assert max(ge_err.values()) <= 1e-3, ge_err
     assert max(pe_err.values()) <= 1e-4, pe_err
+
+
+def test_graph_step_without_hits():
+    """A batch whose rays all miss the cloud (the graph loss stage read sample 0's ray
+    when the step had no samples): eager and graph steps both run, render the background,
+    report a zero masked loss and leave every gradient at zero."""
+    pc, view, qd, mlp, gt = _setup(seed=3)
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    campos = d(view.campos) + 100.0
+    for use_graph in (False, True):
+        points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+        tr = HipTrainer(points, mlp, O, DEV)
+        tr.use_graph = use_graph
+        for _ in range(2):   # the second step replays the captured graph
+            parts, full, mask = tr.backward(campos, d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV))
+        torch.cuda.synchronize()
+        assert not bool(mask.any())
+        assert torch.equal(full.cpu(), torch.ones_like(full.cpu()))
+        assert float(parts["ray_masked_coarse_raycolor"]) == 0.0
+        assert abs(float(parts["ray_miss_coarse_raycolor"]) - float(((1 - gt) ** 2).sum() / 3)) <= 1e-4 * float(
+            ((1 - gt) ** 2).sum())
+        for k, g in grads_named(tr).items():
+            assert float(g.abs().max()) == 0.0, k
+        tr.apply()
+        assert all(torch.isfinite(getattr(points, k)).all() for k in ("points_embeding", "points_conf"))
+    assert tr._graphs, "the graph path did not run"
+
+
+def test_model_ranks_frames_by_ray_miss_loss(tmp_path):
+    """optimize_parameters -> update_rank_ray_miss (neural_points_volumetric_model.py:328-330,
+    mvs_points_volumetric_model.py:157-176) on real steps: the logged ray-miss loss is the
+    missed rays' squared error summed / 3, and the ranking keeps the worst frames first."""
+    import argparse
+
+    from sgnerf_amd.model import HipPointsVolumetricModel
+    pc, view, qd, mlp, gt = _setup(seed=3)
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    opt = argparse.Namespace(SR=24, K=8, gpu_ids=[0], is_train=True, checkpoints_dir=str(tmp_path), name="scene",
+                             bg_color="white", prob_freq=100, prob_num_step=2, prob_kernel_size=None)
+    m = HipPointsVolumetricModel()
+    m.initialize(opt)
+    m.set_points(points_xyz=pc.xyz, points_feats=pc.color * 255.0, points_embedding=pc.embedding,
+                 points_color=pc.color, points_dir=pc.dir, points_conf=pc.conf, aggregator_state=mlp)
+    m.setup(opt, train_len=6)
+    assert m.top_ray_miss_loss.shape == (4,)
+    seen = {}
+    for step, fid in enumerate((4, 1, 4, 0)):
+        gti = torch.rand(gt.shape, generator=torch.Generator().manual_seed(step))
+        m.set_input({"campos": d(view.campos)[None], "raydir": d(view.raydir)[None],
+                     "camrotc2w": d(view.camrotc2w)[None], "near": torch.tensor([[[0.1]]]),
+                     "far": torch.tensor([[[8.0]]]), "gt_image": gti[None], "id": torch.tensor([fid])})
+        m.optimize_parameters(total_steps=step)
+        miss = ~m.ray_mask[0].bool().cpu()
+        want = float(((m.coarse_raycolor[0].cpu() - gti) ** 2)[miss].sum() / 3)
+        got = float(m.get_current_losses()["ray_miss_coarse_raycolor"])
+        assert abs(got - want) <= 1e-5 * max(want, 1e-6), (got, want)
+        seen[fid] = max(seen.get(fid, 0.0), got)
+    ids = m.top_ray_miss_ids.cpu().tolist()
+    losses = m.top_ray_miss_loss.cpu().tolist()
+    assert losses == sorted(losses, reverse=True)
+    for fid, l in seen.items():
+        if l > 0:
+            assert fid in ids and abs(losses[ids.index(fid)] - l) <= 1e-6 * l
