@@ -248,7 +248,7 @@ class HipTrainer:
         if S_cap > getattr(self, "_scap", 0):
             self.feat = torch.zeros(S_cap, 4, dtype=torch.float32, device=dev)
             self._scap = S_cap
-        if n_items > self._cap:
+        if n_items > self._cap or not hasattr(self, "x0"):   # a first step without hits allocates too
             cap = max(128, ((n_items + 127) // 128) * 128)   # rows (8 per item) a multiple of 1024
             rows = cap * 8
             h = dict(dtype=torch.float16, device=dev)
