@@ -30,6 +30,15 @@ def spiral_views(n_frames, h, w, campos=(2.0, 2.0, 1.5)):
     return out
 
 
+def default_scene(n_points=1_200_000):
+    """Config 3's synthetic stand-in: synth-room cloud and a random aggregator whose alpha
+    bias (+50) makes the volume opaque (median background transmission ~0.4 at SR 24)."""
+    pc = scene.synth_room(n_points, seed=0)
+    mlp = init_mlp(0, bias_std=0.01)
+    mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
+    return pc, mlp
+
+
 def render_views(renderer: HipRenderer, views, device):
     """All views -> [n, h*w, 3] on every rank (frame i rendered by rank i % N)."""
     h, w = views[0].h, views[0].w
@@ -68,6 +77,7 @@ def main(argv=None):
     ap.add_argument("--points", type=int, default=1_200_000)
     ap.add_argument("--checkpoint", default=None, help="reference *_net_ray_marching.pth (weights_only load)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--precision", default="f32", choices=["f32", "f16"])
     args = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -76,7 +86,7 @@ def main(argv=None):
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.distributed.init_process_group("nccl", device_id=dev)
-    o = HotPathOpts(SR=args.sr)
+    o = HotPathOpts(SR=args.sr, precision=args.precision)
     if args.checkpoint:
         from .ray_marching import NeuralPoints
         from .weights import strip_prefix
@@ -84,9 +94,7 @@ def main(argv=None):
         npnts = NeuralPoints.from_state_dict(sd_, dev)
         r = HipRenderer(npnts.tables(), strip_prefix(sd_), o, dev)
     else:
-        pc = scene.synth_room(args.points, seed=0)
-        mlp = init_mlp(0, bias_std=0.01)
-        mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
+        pc, mlp = default_scene(args.points)
         r = HipRenderer(PointTables.from_cloud(pc, dev), mlp, o, dev)
     views = spiral_views(args.frames, args.h, args.w)
     torch.cuda.synchronize()
@@ -105,6 +113,7 @@ def main(argv=None):
             write_frames(frames, args.h, args.w, args.out)
     if world > 1:
         torch.distributed.destroy_process_group()
+    return frames, ms
 
 
 if __name__ == "__main__":

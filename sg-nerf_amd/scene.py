@@ -95,6 +95,26 @@ def synth_room(n_points=1_200_000, seed=0, jitter=0.002):
     return PointCloud(xyz, *_attributes(rng, len(xyz)))
 
 
+def room_corner(n_points=60_000, seed=0, jitter=0.002):
+    """A 1.2 m room corner (floor and two walls) with two boxes in front of it, at the
+    ScanNet-like surface density of synth_room(1.2M) (~14k points / m^2): a small scene whose
+    rays cross several surfaces (about 6 samples per ray, 7 of 8 neighbours per sample)."""
+    rng = np.random.default_rng(seed)
+    lo, hi = np.array([1.0, 1.0, 0.0]), np.array([2.2, 2.2, 1.2])
+    faces = []
+    for ax in range(3):      # the three faces through `lo`
+        a1, a2 = [a for a in range(3) if a != ax]
+        u = np.zeros(3); u[a1] = hi[a1] - lo[a1]
+        v = np.zeros(3); v[a2] = hi[a2] - lo[a2]
+        faces.append((lo.copy(), u, v, u[a1] * v[a2]))
+    faces += _box_faces((1.25, 1.3, 0.0), (1.6, 1.65, 0.35))
+    faces += _box_faces((1.55, 1.75, 0.0), (1.8, 2.0, 0.5))
+    xyz = _sample_faces(rng, faces, n_points)
+    xyz = xyz + rng.normal(0.0, jitter, xyz.shape)
+    xyz = xyz[rng.permutation(len(xyz))].astype(np.float32)
+    return PointCloud(xyz, *_attributes(rng, len(xyz)))
+
+
 def dense_cube(n_points=500_000, seed=0, center=(2.0, 2.0, 3.2), side=1.0):
     rng = np.random.default_rng(seed)
     xyz = (np.asarray(center)[None] + (rng.random((n_points, 3)) - 0.5) * side).astype(np.float32)

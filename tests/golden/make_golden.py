@@ -18,6 +18,7 @@ querier's w2pers (worldcoords.py:125-132) and ray_dist
 
 Usage:  python -B tests/golden/make_golden.py         (reference_aggregator.npz)
         python -B tests/golden/make_golden.py --sg    (reference_sg.npz, SG block2_bpnet variant)
+        python -B tests/golden/make_golden.py --opaque (reference_opaque.npz, opaque regime)
 """
 import argparse
 import os
@@ -72,7 +73,12 @@ def w2pers_samples(point_xyz_w, camrotc2w, campos):
     return torch.stack([x_pers, y_pers, z_pers], dim=-1)
 
 
-def make_case(name, pc, view, o, agg, refmods, pc_name=None, bpnet=None):
+def cloud_checksum(pc):
+    """float64 sums of a cloud's arrays: pins a regenerated cloud to the one the reference saw."""
+    return np.array([np.float64(getattr(pc, k)).sum() for k in ("xyz", "embedding", "color", "dir", "conf")])
+
+
+def make_case(name, pc, view, o, agg, refmods, pc_name=None, bpnet=None, gen=None):
     import oracle_query as oq
     from sgnerf_amd.hyper import grid_hyperparameters
     near_far_linear_ray_generation, ray_march, alpha_blend, radiance_render = refmods
@@ -139,9 +145,13 @@ def make_case(name, pc, view, o, agg, refmods, pc_name=None, bpnet=None):
     full = torch.ones(R, 3)  # fill_invalid: white background (tonemap off), :179-181
     full[keep] = ray_color[0]
     pc_name = pc_name or name
+    if gen is not None:   # a seeded generator call instead of the arrays (kept out of the repo)
+        pts = {f"{pc_name}/gen": np.array(gen), f"{pc_name}/checksum": cloud_checksum(pc)}
+    else:
+        pts = {f"{pc_name}/xyz": pc.xyz, f"{pc_name}/embedding": pc.embedding, f"{pc_name}/color": pc.color,
+               f"{pc_name}/dir": pc.dir, f"{pc_name}/conf": pc.conf}
     return {
-        f"{pc_name}/xyz": pc.xyz, f"{pc_name}/embedding": pc.embedding, f"{pc_name}/color": pc.color,
-        f"{pc_name}/dir": pc.dir, f"{pc_name}/conf": pc.conf, f"{name}/points": np.array(pc_name),
+        **pts, f"{name}/points": np.array(pc_name),
         f"{name}/campos": view.campos, f"{name}/camrotc2w": view.camrotc2w, f"{name}/raydir": view.raydir,
         f"{name}/near_far": np.array([view.near, view.far], np.float32),
         f"{name}/SR": np.int32(o.SR), f"{name}/K": np.int32(o.K),
@@ -259,8 +269,65 @@ def main():
               "valid samples", int(out[f"{k}/ray_valid"].sum()), "valid nb", int((out[f"{k}/sample_pidx"] >= 0).sum()))
 
 
+def main_opaque():
+    """tests/golden/reference_opaque.npz: the reference in the opaque regime:
+    alpha_branch bias + OPAQUE_BIAS, so bg_transmission <= 0.5 on (nearly) every ray and a colour
+    error cannot hide behind a transparent volume.
+      opq_patch   the 'patch' cloud, SR 24 (median bg_transmission ~0.03)
+      corner64    scene.room_corner(80000, 0): ScanNet-like density, ~8.5 samples per ray,
+                  ~7.5 of 8 neighbours per sample, SR 64 (median bg_transmission ~0.24)
+      sparse32    scene.room_corner(20000, 1): partially empty K on most samples, SR 32
+    The room-corner clouds are stored as their generator call plus a checksum."""
+    from models.aggregators.point_aggregators import PointAggregator
+    from models.rendering.diff_ray_marching import near_far_linear_ray_generation, ray_march
+    from models.rendering.diff_render_func import alpha_blend, radiance_render
+    import sgnerf_amd  # noqa: F401
+    from sgnerf_amd import scene
+    from sgnerf_amd.opts import HotPathOpts
+
+    agg = seeded_aggregator(PointAggregator, 0, 1)
+    with torch.no_grad():
+        agg.alpha_branch[0].bias.add_(OPAQUE_BIAS)
+    out = {f"mlp/{k}": v.detach().numpy() for k, v in agg.state_dict().items()}
+    refmods = (near_far_linear_ray_generation, ray_march, alpha_blend, radiance_render)
+    rng = np.random.default_rng(11)          # the 'patch' cloud of main()
+    n = 9000
+    xyz = np.stack([rng.uniform(1.7, 2.3, n), np.full(n, 3.0), rng.uniform(1.2, 1.8, n)], 1)
+    xyz[: n // 4, 1] = rng.uniform(2.8, 3.0, n // 4)
+    xyz += rng.normal(0, 0.002, xyz.shape)
+    pc = scene.PointCloud(xyz.astype(np.float32), *scene._attributes(rng, n))
+    view = scene.room_view(16, 16, yaw=90.0, pitch=0.0, campos=(2.0, 2.2, 1.5), focal=40.0)
+    out.update(make_case("opq_patch", pc, view, HotPathOpts(SR=24), agg, refmods))
+    corner_view = scene.room_view(16, 16, yaw=225.0, pitch=-30.0, campos=(2.3, 2.2, 0.8), focal=18.0)
+    pc = scene.room_corner(80000, 0)
+    out.update(make_case("corner64", pc, corner_view, HotPathOpts(SR=64, K=8), agg, refmods,
+                         gen="room_corner:80000:0"))
+    pc = scene.room_corner(20000, 1)
+    out.update(make_case("sparse32", pc, corner_view, HotPathOpts(SR=32, K=8), agg, refmods,
+                         gen="room_corner:20000:1"))
+    path = os.path.join(HERE, "reference_opaque.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path) / 1e6, "MB")
+    for k in ("opq_patch", "corner64", "sparse32"):
+        rm = out[f"{k}/ray_mask"].astype(bool)
+        nb = (out[f"{k}/sample_pidx"] >= 0).sum(-1)
+        bt = out[f"{k}/bg_transmission"]
+        print(k, "valid rays", int(rm.sum()), "samples/ray", float(out[f"{k}/ray_valid"].sum() / max(rm.sum(), 1)),
+              "nb/sample", float(nb[nb > 0].mean()), "partial-K frac", float((nb[nb > 0] < 8).mean()),
+              "bg_t median", float(np.median(bt)), "frac bg_t<=0.5", float((bt <= 0.5).mean()))
+
+
+OPAQUE_BIAS = 50.0
+
 if __name__ == "__main__":
-    if "--sg" in sys.argv:
+    if "--opaque" in sys.argv:
+        assert os.path.isdir(REF), "the golden generator runs only where /root/reference exists"
+        sys.dont_write_bytecode = True
+        sys.path.insert(0, REF)
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        main_opaque()
+    elif "--sg" in sys.argv:
         assert os.path.isdir(REF), "the golden generator runs only where /root/reference exists"
         sys.dont_write_bytecode = True
         sys.path.insert(0, REF)

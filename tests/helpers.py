@@ -1,4 +1,6 @@
-"""Shared test helpers: seeded scenes, options, hyper-parameters."""
+"""Shared test helpers: seeded scenes, options, hyper-parameters, golden files."""
+import os
+
 import numpy as np
 import torch
 
@@ -40,3 +42,29 @@ def assert_equal_arrays(a, b, what):
         diff = np.nonzero((a != b).reshape(-1))[0]
         raise AssertionError(f"{what}: {diff.size} mismatches, first at {diff[:10]}: "
                              f"{a.reshape(-1)[diff[:5]]} vs {b.reshape(-1)[diff[:5]]}")
+
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden_points(g, pcn):
+    """A golden file's point cloud: stored arrays, or (`{pcn}/gen`) the seeded scene generator
+    call the reference was run on, checked against the stored float64 checksums."""
+    keys = ("xyz", "embedding", "color", "dir", "conf")
+    if f"{pcn}/gen" not in g.files:
+        return {k: g[f"{pcn}/{k}"] for k in keys}
+    fn, n, seed = str(g[f"{pcn}/gen"]).split(":")
+    pc = getattr(scene, fn)(int(n), int(seed))
+    pts = dict(zip(keys, (pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf)))
+    got = np.array([np.float64(pts[k]).sum() for k in keys])
+    np.testing.assert_array_equal(got, g[f"{pcn}/checksum"], err_msg=f"regenerated cloud {pcn} differs")
+    return pts
+
+
+def load_golden(file, name):
+    """(points, aggregator state, case arrays) of one golden case."""
+    g = np.load(os.path.join(GOLDEN_DIR, file), allow_pickle=False)
+    pts = golden_points(g, str(g[f"{name}/points"]))
+    mlp = {k[4:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("mlp/")}
+    case = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(name + "/")}
+    return pts, mlp, case

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 import torch
 
+from helpers import load_golden
 from sgnerf_amd.opts import HotPathOpts
 from sgnerf_amd.ray_marching import NeuralPoints, NeuralPointsRayMarching, PointAggregator, fill_invalid, ray_march
 
@@ -22,17 +23,15 @@ DEV = "cuda:0"
 RGB_TOL = 1e-3
 FEAT_TOL = 4e-3
 F32_TOL = 1e-5  # precision "f32" (reference arithmetic): decoded features
-GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_aggregator.npz")
-CASES = ["patch", "patch64", "dense"]
+# reference_aggregator.npz (transparent-to-mid regime) and reference_opaque.npz (alpha bias
+# +50: bg_transmission <= 0.5 on nearly every ray; a ScanNet-density SR-64 corner and a
+# partially-empty-K case)
+OPAQUE = ["opq_patch", "corner64", "sparse32"]
+CASES = ["patch", "patch64", "dense"] + OPAQUE
 
 
 def _load(name):
-    g = np.load(GOLD, allow_pickle=False)
-    pcn = str(g[f"{name}/points"])
-    pts = {k: g[f"{pcn}/{k}"] for k in ("xyz", "embedding", "color", "dir", "conf")}
-    mlp = {k[4:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("mlp/")}
-    case = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(name + "/")}
-    return pts, mlp, case
+    return load_golden("reference_opaque.npz" if name in OPAQUE else "reference_aggregator.npz", name)
 
 
 def _inputs(case, bg=(1.0, 1.0, 1.0)):

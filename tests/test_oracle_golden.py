@@ -8,13 +8,14 @@ import torch
 
 import agg_ref
 import oracle_query as oq
-from helpers import assert_equal_arrays
+from helpers import assert_equal_arrays, load_golden
 from sgnerf_amd import raygen
 from sgnerf_amd.hyper import grid_hyperparameters
 from sgnerf_amd.opts import HotPathOpts
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_aggregator.npz")
-CASES = ["patch", "patch64", "dense"]
+OPAQUE = ["opq_patch", "corner64", "sparse32"]   # reference_opaque.npz (alpha bias +50)
+CASES = ["patch", "patch64", "dense"] + OPAQUE
 
 
 @pytest.fixture(scope="module")
@@ -22,11 +23,26 @@ def gold():
     return np.load(GOLD, allow_pickle=False)
 
 
+class _Gold:
+    """One golden case under the flat `{name}/...` keys, its cloud regenerated when stored as
+    a generator call."""
+
+    def __init__(self, name):
+        pts, mlp, c = load_golden("reference_opaque.npz" if name in OPAQUE else "reference_aggregator.npz", name)
+        self.pts, self.mlp = pts, mlp
+        self.d = {f"{name}/{k}": v for k, v in c.items()}
+        self.d[f"{name}/points"] = np.array(name)
+        for k, v in pts.items():
+            self.d[f"{name}/{k}"] = v
+
+    def __getitem__(self, k):
+        return self.d[k]
+
+
 def case(gold, name):
-    pcn = str(gold[f"{name}/points"])
-    pts = {k: torch.from_numpy(gold[f"{pcn}/{k}"]) for k in ("xyz", "embedding", "color", "dir", "conf")}
-    mlp = {k[len("mlp/"):]: torch.from_numpy(gold[k]) for k in gold.files if k.startswith("mlp/")}
-    return pts, mlp
+    if not isinstance(gold, _Gold):
+        gold = _Gold(name)
+    return {k: torch.from_numpy(v) for k, v in gold.pts.items()}, gold.mlp
 
 
 def test_positional_encoding_golden(gold):
@@ -36,7 +52,8 @@ def test_positional_encoding_golden(gold):
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_depth_table_and_raypos_golden(gold, name):
+def test_depth_table_and_raypos_golden(name):
+    gold = _Gold(name)
     near, far = gold[f"{name}/near_far"]
     t = raygen.depth_table(float(near), float(far), 400)
     assert_equal_arrays(t.numpy(), gold[f"{name}/t_table"], "depth table")
@@ -48,7 +65,8 @@ def test_depth_table_and_raypos_golden(gold, name):
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_oracle_render_matches_reference(gold, name):
+def test_oracle_render_matches_reference(name):
+    gold = _Gold(name)
     pts, mlp = case(gold, name)
     SR, K = int(gold[f"{name}/SR"]), int(gold[f"{name}/K"])
     o = HotPathOpts(SR=SR, K=K)

@@ -14,7 +14,7 @@ import torch
 
 import agg_ref
 import oracle_query as oq
-from helpers import hyper_for, make_view, small_room
+from helpers import hyper_for, load_golden, make_view, small_room
 from sgnerf_amd import scene
 from sgnerf_amd.opts import HotPathOpts
 from sgnerf_amd.render import HipRenderer, PointTables
@@ -48,13 +48,14 @@ def _render(pts, mlp, view, o):
     return r, out
 
 
+OPAQUE = ["opq_patch", "corner64", "sparse32"]   # reference_opaque.npz (alpha bias +50)
+
+
 @pytest.mark.parametrize("prec", ["f32", "f16"])
-@pytest.mark.parametrize("name", ["patch", "patch64", "dense"])
+@pytest.mark.parametrize("name", ["patch", "patch64", "dense"] + OPAQUE)
 def test_render_matches_reference_golden(name, prec):
-    g = np.load(GOLD, allow_pickle=False)
-    pcn = str(g[f"{name}/points"])
-    pts = {k: g[f"{pcn}/{k}"] for k in ("xyz", "embedding", "color", "dir", "conf")}
-    mlp = {k[4:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("mlp/")}
+    pts, mlp, case = load_golden("reference_opaque.npz" if name in OPAQUE else "reference_aggregator.npz", name)
+    g = {f"{name}/{k}": v for k, v in case.items()}
     near, far = (float(x) for x in g[f"{name}/near_far"])
     view = scene.View(g[f"{name}/campos"], g[f"{name}/camrotc2w"], g[f"{name}/raydir"], None, None, 0, 0, near, far)
     o = HotPathOpts(SR=int(g[f"{name}/SR"]), K=int(g[f"{name}/K"]), precision=prec)
@@ -261,3 +262,44 @@ def test_full_frame_config2_properties():
     err = float((sub.rgb.cpu() - ref).abs().max())
     print(f"config 2 full frame: {n_work} work items; subset max |rgb - oracle| = {err:.3e}")
     assert err <= RGB_TOL
+
+
+def test_render_vid_config3_spiral_matches_oracle(tmp_path):
+    """BASELINE config 3 through its driver (render_vid.main, run/render_vid.py:26-69): an
+    8-frame spiral at 800x800, SR 24, over the 1.2M-point room with the opaque aggregator,
+    rendered and written; every 97th ray of each frame (offset by the frame index) is checked
+    against the oracle (C query + torch fp32 aggregator / ray_march): RGB within the f32
+    mode's 1e-5 (a missed or extra ray would show as a background-coloured error), and the
+    written float16 stack equals the frames to fp16 rounding."""
+    from sgnerf_amd import raygen, render_vid
+    H = W = 800
+    frames, ms = render_vid.main(["--frames", "8", "--h", str(H), "--w", str(W), "--sr", "24", "--out",
+                                  str(tmp_path)])
+    assert frames.shape == (8, H * W, 3) and ms > 0
+    stack = np.load(tmp_path / "frames.npy")
+    assert stack.shape == (8, H, W, 3) and (tmp_path / "frame_0007.png").exists()
+    fr = frames.cpu().numpy()
+    np.testing.assert_allclose(stack.reshape(8, -1, 3).astype(np.float32), fr, atol=2.5e-4, rtol=0)
+    pc, mlp = render_vid.default_scene()
+    o = HotPathOpts(SR=24)
+    og = oq.OracleGrid(pc.xyz, hyper_for(pc, o), o)
+    tp = {k: torch.from_numpy(getattr(pc, k)) for k in ("xyz", "embedding", "color", "dir", "conf")}
+    tt = raygen.depth_table(0.1, 8.0, o.z_depth_dim).numpy()
+    worst, n_valid, n_rays, bgt_med = 0.0, 0, 0, []
+    for f, v in enumerate(render_vid.spiral_views(8, H, W)):
+        idx = np.arange(f, H * W, 97)
+        rd = np.ascontiguousarray(v.raydir[idx])
+        q = og.query(v.campos, rd, tt)
+        with torch.no_grad():
+            full, mask, fd, opacity, bg_t = agg_ref.render(tp, mlp, torch.from_numpy(v.campos),
+                                                           torch.from_numpy(v.camrotc2w), torch.from_numpy(rd), q, 24)
+        err = float(np.abs(fr[f, idx] - full.numpy()).max())
+        worst = max(worst, err)
+        n_valid += int(mask.sum())
+        n_rays += len(idx)
+        bgt_med.append(float(bg_t[mask].median()))
+        assert err <= F32_TOL, (f, err)          # render_vid runs the f32 (reference-precision) mode
+    print(f"config 3: 8 frames {H}x{W} in {ms:.1f} ms; {n_rays} rays checked, {n_valid} valid, "
+          f"max |rgb - oracle| {worst:.3e}, median bg_transmission per frame {np.round(bgt_med, 3).tolist()}")
+    assert n_valid > 0.9 * n_rays
+    assert max(bgt_med) <= 0.5
