@@ -111,8 +111,10 @@ def test_point_aggregator_matches_reference(name, prec):
     agg = PointAggregator(mlp, HotPathOpts(SR=int(case["SR"]), precision=prec), DEV)
     dec, valid, weight, conf = agg(**_gathered(pts, case))
     np.testing.assert_array_equal(valid[0].cpu().numpy(), case["ray_valid"])
-    err = np.abs(dec[0].cpu().numpy() - case["decoded"]).max()
-    print(f"{name} [{prec}]: PointAggregator max |decoded - reference| = {err:.3e}")
+    # relative above 1: alpha reaches ~50 in the opaque cases, where fp32's own spacing is 4e-6
+    ref = case["decoded"]
+    err = (np.abs(dec[0].cpu().numpy() - ref) / np.maximum(1.0, np.abs(ref))).max()
+    print(f"{name} [{prec}]: PointAggregator max |decoded - reference| / max(1, |ref|) = {err:.3e}")
     assert err <= (F32_TOL if prec == "f32" else FEAT_TOL)
     np.testing.assert_allclose(weight[0].cpu().numpy(), case["weight"], atol=1e-5, rtol=1e-4)
     np.testing.assert_array_equal(conf[0].cpu().numpy(), case["conf_coefficient"])
