@@ -78,17 +78,10 @@ def parse():
 
 
 def self_launch(args):
-    """`--gpus N` (N > 1) without a launcher: run this script under torch.distributed.run as a
-    child process (one rank per GPU, rendezvous on 127.0.0.1) and return its exit code.  Nothing
-    here touches the GPU, so the child ranks initialise it themselves."""
-    import socket
-    import subprocess
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd, env=dict(os.environ))
+    """`--gpus N` (N > 1) without a launcher: run this script as N ranks under
+    torch.distributed.run (sgnerf_amd.dist.launch_ranks) and return the exit code."""
+    from sgnerf_amd import dist as sd
+    return sd.launch_ranks(__file__, args.gpus, sys.argv[1:]).returncode
 
 
 def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
@@ -417,7 +410,8 @@ def main():
     ref_flop = (FLOP_PER_NB + (2 * 352 * 256 if args.sg else 0)) * h["n_nb"]
     achieved = rows_flop / (stage_ms["agg_rows"] * 1e-3) / 1e12
     peak = PEAK_X3_TFLOPS if x3 else PEAK_F16_TFLOPS
-    kname = "k_agg_rows_x3" if x3 else "k_agg_rows"
+    w16 = os.environ.get("SGN_X3_W16", "1") != "0"     # mlp_x3.hip: 16x16 two-waves-per-SIMD kernels
+    kname = ("k_rows16" if w16 else "k_agg_rows_x3") if x3 else "k_agg_rows"
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -473,7 +467,7 @@ def main():
             "bytes_per_frame_no_reuse_credit": h["q_bytes"],
         },
         "roofline_proj": {
-            "kernel": ("k_point_proj_x3" if x3 else "k_point_proj") + " (block1.0 point inputs, all points, once per frame)",
+            "kernel": (("k_point_proj16" if w16 else "k_point_proj_x3") if x3 else "k_point_proj") + " (block1.0 point inputs, all points, once per frame)",
             "bound": "mfma", "achieved": FLOP_PER_POINT_PROJ * args.points / (stage_ms["proj"] * 1e-3) / 1e12,
             "peak": peak, "unit": "TFLOP/s", "avg_launch_ms": stage_ms["proj"],
         },

@@ -13,6 +13,11 @@ The collective is torch.distributed all_gather_into_tensor: RCCL over xGMI on th
 GPU box (backend "nccl"), gloo on CPU in the tests.  Rendering itself is passed in
 as a callable, so these functions are the same for the HIP renderer and the tests.
 """
+import os
+import socket
+import subprocess
+import sys
+
 import torch
 import torch.distributed as dist
 
@@ -85,3 +90,15 @@ def max_over_ranks(x, device):
     if n > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def launch_ranks(script, nproc, argv, env=None, capture=False):
+    """Run `script argv` as nproc ranks under torch.distributed.run (one node, rendezvous on
+    127.0.0.1, a free port) in a child process; returns its CompletedProcess.  Nothing here
+    touches the GPU, so each rank initialises its own device (bench.py --gpus N)."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(script)] + list(argv)
+    return subprocess.run(cmd, env=dict(os.environ if env is None else env), capture_output=capture, text=True)

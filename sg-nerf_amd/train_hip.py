@@ -29,11 +29,13 @@ import math
 
 import torch
 import torch.nn as nn
+import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import _lib
 from .opts import HotPathOpts
-from .train import PointParams, _pe, composite_losses, _allreduce_buckets, _allreduce_point_rows
+from .train import (PointParams, _allreduce_buckets, _allreduce_point_rows, _pe, composite_losses, gather_counts,
+                    touched_rows)
 from .weights import LAYERS, strip_prefix
 
 N_F32 = 2056
@@ -324,7 +326,13 @@ class HipTrainer:
             elif not (self._pts_grad_clean and p is not self.mlp.flat):
                 p.grad.zero_()
         self._pts_grad_clean = False
-        S, n = (int(x) for x in q.counters[:2].tolist())  # one host sync per step
+        dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if dp:   # the point rows this rank's step can touch, and every rank's count, ride the same sync
+            t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, self.points.xyz.shape[0])
+            sync = torch.cat([q.counters[:2].to(torch.int64), gather_counts(t_cnt)])
+        else:
+            sync = q.counters[:2]
+        S, n, *t_counts = (int(x) for x in sync.tolist())  # one host sync per step
         graph = self.use_graph and dev.type == "cuda"
         if graph:
             self._buffers(R * o.SR, R * o.SR)   # static shapes: every buffer at the batch's capacity
@@ -375,7 +383,8 @@ class HipTrainer:
                        "sgn_aggregate_backward")
             self._weight_grads(n * 8, scale)
         self.allreduce_grads([self.mlp.flat])
-        _allreduce_point_rows([p.grad for p in self.point_params])
+        if dp:
+            _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
         parts["total"] = total.detach()
         return parts, full.detach(), ray_mask
 
