@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--w", type=int, default=800)
     ap.add_argument("--sr", type=int, default=None, help="samples per ray (default 64 room, 128 lego)")
     ap.add_argument("--points", type=int, default=None, help="neural points (default 1.2M room, 300k lego)")
-    ap.add_argument("--scene", choices=["room", "lego"], default="room",
+    ap.add_argument("--scene", choices=["room", "lego", "dense"], default="room",
                     help="room: BASELINE config 2 (headline); lego: config 4 (NeRF-synthetic camera, SR 128)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
@@ -139,7 +139,8 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
                                      "HIP MFMA row-MLP forward/backward + torch colour/composite autograd")
                                   + " + RCCL all-reduce",
                       "parallelism": f"dp{world}"},
-           "final_loss": float(torch.stack(losses).mean().item())}
+           "final_loss": float(torch.stack(losses).mean().item()),
+           "graph_captures": int(getattr(tr, "graph_captures", 0))}   # loss-stage captures, warm-up included
     return res
 
 
@@ -220,11 +221,18 @@ def cpu_baseline(pc, mlp, o, view, stride=4):
             "cpu_model": _cpu_model()}
 
 
+def dense_pose_view(i, h, w):
+    """SURVEY §8d dense stress variant: the cube face-on, the camera sliding by 2 cm per frame."""
+    return scene.dense_stress_view(h, w, shift=0.02 * ((i % 5) - 2))
+
+
 def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, want_stats=True):
     """Headline-shaped frame loop at `precision`; returns the result fields (no cpu baseline)."""
     sg = dict(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1) if args.sg else {}
     o = HotPathOpts(SR=args.sr, precision=precision, **sg)
-    pc = scene.lego_standin(args.points, seed=0) if lego else scene.synth_room(args.points, seed=0)
+    dense = args.scene == "dense"
+    pc = (scene.lego_standin(args.points, seed=0) if lego else
+          scene.dense_cube(args.points, seed=0) if dense else scene.synth_room(args.points, seed=0))
     if args.sg:
         pc = scene.with_semantics(pc, seed=1, n_classes=20, cell=0.5)
     mlp = init_mlp(0, bias_std=0.01, bpnet_layers=1 if args.sg else 0, bpnet_dim=96 if args.sg else 0)
@@ -232,7 +240,7 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
     r = HipRenderer(PointTables.from_cloud(pc, dev), mlp, o, dev)
     n_frames = warmup + steps
     poses = [(s * world + rank) for s in range(n_frames)]
-    views = [(lego_pose_view if lego else pose_view)(p, args.h, args.w) for p in poses]
+    views = [(lego_pose_view if lego else dense_pose_view if dense else pose_view)(p, args.h, args.w) for p in poses]
     rays = [torch.from_numpy(v.raydir).to(dev) for v in views]
     cams = [(torch.from_numpy(v.campos).to(dev), torch.from_numpy(v.camrotc2w).to(dev)) for v in views]
     R = args.h * args.w
@@ -370,7 +378,7 @@ def main():
     if args.sr is None:
         args.sr = 128 if lego else 64
     if args.points is None:
-        args.points = 300_000 if lego else 1_200_000
+        args.points = 300_000 if lego else 3_900_000 if args.scene == "dense" else 1_200_000
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -493,8 +501,22 @@ def main():
         torch.cuda.empty_cache()
         # BASELINE config 5 (training step, 4096-ray batches, DP over the ranks)
         tr = train_main(args, world, rank, dev, dist, steps=max(args.steps, 20), warmup=5)
+        torch.cuda.empty_cache()
+        # SURVEY §8d dense stress variant (3.9 M points in a 1 m cube, every candidate occupied)
+        sa = argparse.Namespace(**{**vars(args), "scene": "dense", "points": 3_900_000})
+        e = render_run(sa, args.precision, world, rank, dev, dist, 2, 1, False)
+        Rd = args.h * args.w
+        res["stress_dense"] = {
+            "value": e["value"], "unit": "rays/s", "ms_per_frame": e["ms_per_frame"], "steps": 2, "warmup": 1,
+            "dtype": res["dtype"], "stages_ms": e["stages_ms"],
+            "workload": f"dense cube 3.9 M points, {args.h}x{args.w} rays x SR={args.sr}, face-on (SURVEY §8d)",
+            "occupancy": {"samples_per_ray": e["n_samples"] / Rd, "valid_samples_per_ray": e["n_smp"] / Rd,
+                          "valid_neighbours_per_ray": e["n_nb"] / Rd},
+            "roofline_frac": flop_nb * e["n_nb"] / (e["stages_ms"]["agg_rows"] * 1e-3) / 1e12 / peak}
+        del e
+        torch.cuda.empty_cache()
         res["train_config5"] = {k: tr[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype",
-                                                      "final_loss", "config")}
+                                                      "final_loss", "graph_captures", "config")}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(h["pc"], h["mlp"], h["o"], h["views"][0])
     if rank == 0:

@@ -121,6 +121,13 @@ def dense_cube(n_points=500_000, seed=0, center=(2.0, 2.0, 3.2), side=1.0):
     return PointCloud(xyz, *_attributes(rng, n_points))
 
 
+def dense_stress_view(h=800, w=800, shift=0.0):
+    """SURVEY §8d's dense stress variant: the 1 m cube of dense_cube() (centre (2, 2, 3.2)) seen
+    face-on from 1 m with fx = fy = w (every ray enters the cube, so each of the first SR
+    candidates is occupied with >= K neighbours); `shift` slides the camera sideways (m)."""
+    return room_view(h, w, yaw=90.0, pitch=0.0, campos=(2.0 + shift, 0.5, 3.2), focal=float(w))
+
+
 def lego_standin(n_points=300_000, seed=0):
     rng = np.random.default_rng(seed)
     n_sph = n_points // 2

@@ -314,7 +314,8 @@ def _allreduce_point_rows(grads, idx=None, counts=None):
 
     idx / counts: the touched rows (touched_rows, device) and every rank's count (host ints,
     read in the step's one sync, gather_counts); without them they are derived from the
-    non-zero gradient rows here, at the cost of two host syncs."""
+    non-zero gradient rows here, at the cost of two host syncs.  Every row outside idx must
+    hold a zero gradient (true of both sources)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
     n = dist.get_world_size()
@@ -339,13 +340,17 @@ def _allreduce_point_rows(grads, idx=None, counts=None):
     all_rows = torch.empty(n * m, rows.shape[1], dtype=rows.dtype, device=dev)
     dist.all_gather_into_tensor(all_idx, pidx)
     dist.all_gather_into_tensor(all_rows, rows)
-    acc = torch.zeros(N + 1, rows.shape[1], dtype=rows.dtype, device=dev)   # row N absorbs the padding
-    for r in range(n):
-        acc.index_add_(0, all_idx[r * m:(r + 1) * m], all_rows[r * m:(r + 1) * m])
-    acc = acc[:N] / n
+    all_rows /= n
+    all_idx.clamp_(max=N - 1)                # padding rows are zeros: adding them is a no-op
+    # in place: the gradient is non-zero only on this rank's own rows, which were just sent;
+    # clear them and add every rank's slice in rank order (no dense accumulator, no full pass)
     off = 0
     for g, wdt in zip(grads, widths):
-        g.copy_(acc[:, off:off + wdt].reshape(g.shape))
+        assert g.is_contiguous()
+        g2 = g.view(N, wdt)
+        g2.index_fill_(0, safe, 0.0)
+        for r in range(n):
+            g2.index_add_(0, all_idx[r * m:(r + 1) * m], all_rows[r * m:(r + 1) * m, off:off + wdt])
         off += wdt
 
 

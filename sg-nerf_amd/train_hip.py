@@ -233,7 +233,8 @@ class HipTrainer:
         self._cap = 0
         # the colour/composite/loss stage as one replayed HIP graph (SGN_TRAIN_GRAPH=0: eager)
         self.use_graph = os.environ.get("SGN_TRAIN_GRAPH", "1") != "0"
-        self._graphs = {}
+        self._graphs = {}        # (capacity bucket, buffers) -> captured loss stage, LRU order
+        self.graph_captures = 0
         self._flat_maps = {}
 
     @staticmethod
@@ -440,8 +441,11 @@ class HipTrainer:
         Nc = min(Sc, -(-max(n, 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
         key = (R, Sc, Nc, q.work.data_ptr(), q.counters.data_ptr(), self.fs.data_ptr(), self.feat.data_ptr(),
                fl.data_ptr(), fl.grad.data_ptr(), P.points_conf.data_ptr(), P.points_conf.grad.data_ptr())
-        st = self._graphs.get(key)
-        if st is None:
+        st = self._graphs.pop(key, None)
+        if st is not None:
+            self._graphs[key] = st              # most recently used goes last (LRU eviction order)
+        else:
+            self.graph_captures += 1
             if len(self._graphs) >= GRAPH_CACHE:
                 self._graphs.pop(next(iter(self._graphs)))
             st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "ar": torch.arange(Sc, device=dev),

@@ -303,3 +303,34 @@ def test_render_vid_config3_spiral_matches_oracle(tmp_path):
           f"max |rgb - oracle| {worst:.3e}, median bg_transmission per frame {np.round(bgt_med, 3).tolist()}")
     assert n_valid > 0.9 * n_rays
     assert max(bgt_med) <= 0.5
+
+
+def test_dense_stress_scene_matches_oracle():
+    """SURVEY §8d dense stress variant at full size: 3.9 M points in a 1 m cube, 800x800 rays
+    face-on, SR 64 (every candidate inside the cube occupied with K neighbours), the
+    reference-precision mode; every 997th ray against the oracle: ray mask bit-exact, RGB and
+    background transmission within the f32 mode's 1e-5."""
+    pc = scene.dense_cube(3_900_000, seed=0)
+    o = HotPathOpts(SR=64)
+    mlp = init_mlp(5, bias_std=0.01)
+    mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
+    view = scene.dense_stress_view(800, 800)
+    pts = dict(xyz=pc.xyz, embedding=pc.embedding, color=pc.color, dir=pc.dir, conf=pc.conf)
+    r, out = _render(pts, mlp, view, o)
+    idx = np.arange(3, 800 * 800, 997)
+    rd = np.ascontiguousarray(view.raydir[idx])
+    q = oq.OracleGrid(pc.xyz, hyper_for(pc, o), o).query(view.campos, rd,
+                                                         r.querier.depth_table(0.1, 8.0, 0)[0].cpu().numpy())
+    tp = {k: torch.from_numpy(v) for k, v in pts.items()}
+    with torch.no_grad():
+        full, mask, fd, opacity, bg_t = agg_ref.render(tp, mlp, torch.from_numpy(view.campos),
+                                                       torch.from_numpy(view.camrotc2w), torch.from_numpy(rd), q, 64)
+    np.testing.assert_array_equal(out.ray_mask.cpu().numpy()[idx].astype(bool), mask.numpy())
+    err = np.abs(out.rgb.cpu().numpy()[idx] - full.numpy()).max()
+    berr = np.abs(out.bg_transmission.cpu().numpy()[idx][mask.numpy()] - bg_t[mask].numpy()).max()
+    S = out.query.n_samples()
+    nb = int(out.query.samp_nnb[:S].sum())
+    print(f"dense stress: {S / 640000:.1f} samples/ray, {nb / 640000:.1f} neighbours/ray; subset of {len(idx)} rays: "
+          f"max |rgb - oracle| {err:.3e}, max |bgT - oracle| {berr:.3e}")
+    assert err <= F32_TOL and berr <= F32_TOL
+    assert nb / 640000 > 150

@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 GRAD_TOL_MLP = 2e-2
 GRAD_TOL_POINTS = 6e-2
+UPDATE_TOL = 5e-2   # graph vs eager Adam updates (relative L2); set from the measured value below
 
 
 def test_device_pack_matches_host_pack():
@@ -223,6 +224,9 @@ def test_graph_captured_step_matches_eager_step():
         points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
         tr = HipTrainer(points, mlp, O, DEV)
         tr.use_graph = use_graph
+        p0 = {k: getattr(points, k).detach().cpu().clone()
+              for k in ("points_embeding", "points_color", "points_dir", "points_conf")}
+        p0["mlp"] = tr.mlp.flat.detach().cpu().clone()
         losses, grads = [], None
         for it in range(3):
             torch.manual_seed(100 + it)                   # same jittered depth table in both runs
@@ -234,28 +238,27 @@ def test_graph_captured_step_matches_eager_step():
             tr.apply()
             losses.append(float(parts["total"]))
         torch.cuda.synchronize()
-        params = {k: getattr(points, k).detach().cpu().clone()
+        params = {k: getattr(points, k).detach().cpu().clone() - p0[k]
                   for k in ("points_embeding", "points_color", "points_dir", "points_conf")}
-        params["mlp"] = tr.mlp.flat.detach().cpu().clone()
+        params["mlp"] = tr.mlp.flat.detach().cpu().clone() - p0["mlp"]
         runs[use_graph] = (losses, grads, params, first)
     (le, ge, pe, fe), (lg, gg, pg, fg) = runs[False], runs[True]
     assert tr._graphs, "the graph path did not run"
     assert torch.equal(fe[1], fg[1])
     assert float((fe[0] - fg[0]).abs().max()) <= 1e-5
     ge_err = {k: _rel(gg[k], ge[k]) for k in ge}
-    # parameters after three Adam steps: m / sqrt(v) normalises near-zero gradients, so rounding
-    # differences reach lr-sized updates on a few elements; the bound is relative L2 over tensors
-    # (measured 1.0-1.1e-4 on points_embeding / the MLP, 1e-6..3e-5 elsewhere)
+    # the three Adam updates (p_3 - p_0), graph vs eager, relative L2 per tensor: m / sqrt(v)
+    # normalises near-zero gradients, so rounding differences become lr-sized on a few elements
     pe_err = {k: float(torch.linalg.vector_norm((pg[k] - pe[k]).double())
-                       / torch.linalg.vector_norm((pe[k] - 0).double())) for k in pe}
+                       / torch.linalg.vector_norm(pe[k].double())) for k in pe}
     print("losses eager", le, "graph", lg)
     print("grad rel L2", {k: f"{v:.1e}" for k, v in ge_err.items()})
     print("param rel L2", {k: f"{v:.1e}" for k, v in pe_err.items()})
     assert abs(le[0] - lg[0]) <= 1e-5 * abs(le[0])
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-3 * abs(a)
-    assert max(ge_err.values()) <= 1e-3, ge_err
-    assert max(pe_err.values()) <= 3e-4, pe_err
+    assert max(ge_err.values()) <= 2e-4, ge_err       # measured <= 8.5e-5 (points_embeding)
+    assert max(pe_err.values()) <= UPDATE_TOL, pe_err
 
 
 def test_graph_step_without_hits():
@@ -319,3 +322,34 @@ def test_model_ranks_frames_by_ray_miss_loss(tmp_path):
     for fid, l in seen.items():
         if l > 0:
             assert fid in ids and abs(losses[ids.index(fid)] - l) <= 1e-6 * l
+
+
+def test_graph_cache_buckets_and_lru(monkeypatch):
+    """Loss-stage graphs per capacity bucket: a batch of another size captures a second graph,
+    returning to the first size replays the first (LRU hit, no capture); with room for one
+    graph every change recaptures.  Each replayed step equals the eager step's loss."""
+    import sgnerf_amd.train_hip as th
+    pc, view, qd, mlp, gt = _setup(seed=7)
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    sizes = [view.raydir.shape[0], view.raydir.shape[0] // 3, view.raydir.shape[0]]
+    monkeypatch.setattr(th, "GRAPH_BUCKET", 64)
+
+    def run(use_graph, cache):
+        monkeypatch.setattr(th, "GRAPH_CACHE", cache)
+        points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+        tr = HipTrainer(points, mlp, O, DEV)
+        tr.use_graph = use_graph
+        out = []
+        for i, R in enumerate(sizes):
+            torch.manual_seed(300 + i)
+            parts, full, mask = tr.backward(d(view.campos), d(view.camrotc2w), d(view.raydir[:R]), 0.1, 8.0,
+                                            gt[:R].to(DEV))
+            out.append(float(parts["total"]))
+        return tr, out
+    _, eager = run(False, 8)
+    tr, graph = run(True, 8)
+    assert tr.graph_captures == 2 and len(tr._graphs) == 2
+    for a, b in zip(eager, graph):
+        assert abs(a - b) <= 1e-5 * abs(a), (eager, graph)
+    tr1, _ = run(True, 1)
+    assert tr1.graph_captures == 3 and len(tr1._graphs) == 1
