@@ -8,6 +8,7 @@ for the per-point parameters (each a sum over the few rows that gather the point
 rounding and LReLU-mask flips near zero do not average out; measured 2.7-3.6e-2); the loss
 within 1e-3 relative and the rendered colour within the north-star 1e-3."""
 import ctypes
+from dataclasses import replace as dataclasses_replace
 
 import numpy as np
 import pytest
@@ -23,7 +24,13 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 GRAD_TOL_MLP = 2e-2
 GRAD_TOL_POINTS = 6e-2
-UPDATE_TOL = 5e-2   # graph vs eager Adam updates (relative L2); set from the measured value below
+# graph vs eager Adam updates after 3 steps, relative L2 per tensor.  Measured 2e-3..7.3e-2 (the
+# eager path against itself: 1e-6..5e-3 across runs, atomic accumulation order).  The padded loss stage sums
+# in another order (fp32, ~1e-7), the fp16 deltas of the HIP backward round a few elements the
+# other way (gradients then differ by <= 8.5e-5 relative L2), and Adam's m / sqrt(v) turns the
+# sign of near-zero gradient components into lr-sized steps.
+UPDATE_TOL = 0.1
+LOSS_CURVE_TOL = 0.02   # HIP vs fp32 torch colour loss, 200 steps, 20-step window means (measured <= 0.0064)
 
 
 def test_device_pack_matches_host_pack():
@@ -220,10 +227,10 @@ def test_graph_captured_step_matches_eager_step():
     pc, view, qd, mlp, gt = _setup(seed=7)
     d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
     runs = {}
-    for use_graph in (False, True):
+    for use_graph in (False, True, "eager2"):
         points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
         tr = HipTrainer(points, mlp, O, DEV)
-        tr.use_graph = use_graph
+        tr.use_graph = use_graph is True
         p0 = {k: getattr(points, k).detach().cpu().clone()
               for k in ("points_embeding", "points_color", "points_dir", "points_conf")}
         p0["mlp"] = tr.mlp.flat.detach().cpu().clone()
@@ -242,8 +249,14 @@ def test_graph_captured_step_matches_eager_step():
                   for k in ("points_embeding", "points_color", "points_dir", "points_conf")}
         params["mlp"] = tr.mlp.flat.detach().cpu().clone() - p0["mlp"]
         runs[use_graph] = (losses, grads, params, first)
+        if use_graph is True:
+            assert tr._graphs, "the graph path did not run"
     (le, ge, pe, fe), (lg, gg, pg, fg) = runs[False], runs[True]
-    assert tr._graphs, "the graph path did not run"
+    # run-to-run spread of the eager path itself (atomic accumulation order in the backward)
+    pe2 = runs["eager2"][2]
+    ee_err = {k: float(torch.linalg.vector_norm((pe2[k] - pe[k]).double())
+                       / torch.linalg.vector_norm(pe[k].double())) for k in pe}
+    print("eager-vs-eager update rel L2", {k: f"{v:.1e}" for k, v in ee_err.items()})
     assert torch.equal(fe[1], fg[1])
     assert float((fe[0] - fg[0]).abs().max()) <= 1e-5
     ge_err = {k: _rel(gg[k], ge[k]) for k in ge}
@@ -258,7 +271,7 @@ def test_graph_captured_step_matches_eager_step():
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-3 * abs(a)
     assert max(ge_err.values()) <= 2e-4, ge_err       # measured <= 8.5e-5 (points_embeding)
-    assert max(pe_err.values()) <= UPDATE_TOL, pe_err
+    assert max(pe_err.values()) <= UPDATE_TOL, (pe_err, ee_err)
 
 
 def test_graph_step_without_hits():
@@ -353,3 +366,50 @@ def test_graph_cache_buckets_and_lru(monkeypatch):
         assert abs(a - b) <= 1e-5 * abs(a), (eager, graph)
     tr1, _ = run(True, 1)
     assert tr1.graph_captures == 3 and len(tr1._graphs) == 1
+
+
+def test_200_step_training_tracks_fp32_torch():
+    """200 training steps of the HIP path (fp16-in MFMA forward, fp16-delta backward) against
+    the fp32 torch-autograd restatement (train.Trainer on the same device, same HIP query and
+    jitter, same batches) fitting a teacher aggregator's renders: both loss curves fall, and
+    the HIP curve stays within LOSS_CURVE_TOL (relative, mean over 20-step windows) of the
+    fp32 one."""
+    from sgnerf_amd.render import HipRenderer, PointTables
+    from sgnerf_amd.scene import synth_room, room_view
+    pc = synth_room(150_000, seed=8)
+    teacher = init_mlp(9, bias_std=0.01)
+    teacher["alpha_branch.0.bias"] = teacher["alpha_branch.0.bias"] + 50.0
+    student = init_mlp(8, bias_std=0.01)
+    student["alpha_branch.0.bias"] = student["alpha_branch.0.bias"] + 50.0
+    r = HipRenderer(PointTables.from_cloud(pc, DEV), teacher, O, DEV)
+    views = [room_view(64, 64, yaw=30.0 * i, pitch=-8.0) for i in range(12)]
+    gts = []
+    for v in views:
+        out = r.render(torch.from_numpy(v.campos), torch.from_numpy(v.camrotc2w), torch.from_numpy(v.raydir),
+                       v.near, v.far)
+        gts.append(out.rgb.clone())
+    del r
+    g = torch.Generator().manual_seed(0)
+    batches = []
+    for i in range(200):
+        v = views[i % len(views)]
+        idx = torch.randperm(64 * 64, generator=g)[:2048]
+        batches.append((torch.from_numpy(v.campos).to(DEV), torch.from_numpy(v.camrotc2w).to(DEV),
+                        torch.from_numpy(v.raydir)[idx].to(DEV), gts[i % len(views)][idx.to(DEV)]))
+    curves = {}
+    for name, cls in (("hip", HipTrainer), ("torch", Trainer)):
+        points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+        tr = cls(points, student, dataclasses_replace(O, is_train=1), DEV, lr=1e-3, plr=2e-3)
+        ls = []
+        for i, (c, rot, rd, gt) in enumerate(batches):
+            torch.manual_seed(5000 + i)          # same depth jitter in both runs
+            parts, _, _ = tr.step(c, rot, rd, 0.1, 8.0, gt)
+            ls.append(float(parts["ray_masked_coarse_raycolor"]))
+        curves[name] = np.array(ls)
+    h, t = curves["hip"], curves["torch"]
+    wh, wt = h.reshape(10, 20).mean(1), t.reshape(10, 20).mean(1)
+    rel = np.abs(wh - wt) / wt
+    print("colour loss per 20-step window: hip", np.round(wh, 5).tolist(), "torch", np.round(wt, 5).tolist(),
+          "rel", np.round(rel, 4).tolist())
+    assert wh[-1] < 0.7 * wh[0] and wt[-1] < 0.7 * wt[0]
+    assert rel.max() <= LOSS_CURVE_TOL, rel
