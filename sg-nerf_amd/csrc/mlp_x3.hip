@@ -1067,8 +1067,6 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     const int end = min(nwork, a.item0 + a.n_items);
     const Cam cam = load_cam(a.campos, a.rot);
     const WBlob wb = make_blob(a.blob, BLOB_BYTES_ALL);
-    const __amdgpu_buffer_rsrc_t fs_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.fs, (short)0, 0x7fffffff, 0x00020000);
     const float *proj = (const float *)a.proj;
     {
         const float *src = (const float *)((const char *)a.blob + OFF16_F32);
@@ -1255,7 +1253,11 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
             const f32x4 v0 = *(const f32x4 *)(st + (lane >> 5) * 256 + 8 * (lane & 31));
             const f32x4 v1 = *(const f32x4 *)(st + (lane >> 5) * 256 + 8 * (lane & 31) + 4);
             const int it = base + w * 2 + (lane >> 5);
-            const uint32_t off = it < end ? (uint32_t)((it - a.item0) * HID + 8 * (lane & 31)) * 4 : 0xFFFF0000u;
+            // descriptor based at this tile's first item (uniform, scalar registers): a launch
+            // may hold more items than a 31-bit byte range covers
+            const __amdgpu_buffer_rsrc_t fs_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)((float *)a.fs + (int64_t)(base - a.item0) * HID), (short)0, 0x7fffffff, 0x00020000);
+            const uint32_t off = it < end ? (uint32_t)((it - base) * HID + 8 * (lane & 31)) * 4 : 0xFFFF0000u;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), fs_rsrc, off, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), fs_rsrc, off, 16, 0);
         }
@@ -1620,9 +1622,9 @@ int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void
     return 0;
 }
 
-// Work items per launch: the fp32 blended features of a launch are stored through a buffer
-// descriptor (31-bit byte range) based at the launch's first item, so at most 2^31 / 1 KiB items
-// per launch; a frame with more runs several launches per stage.
+// Work items per launch of the 32x32 kernel (k_agg_rows_x3): its fp32 blended features are stored
+// through one buffer descriptor (31-bit byte range) based at the launch's first item, so at most
+// 2^31 / 1 KiB items per launch.  k_rows16 bases a descriptor per tile and has no such limit.
 constexpr int64_t X3_MAX_CHUNK = ((int64_t)0x7fffffff / (sgn::mlp::HID * 4)) / 16 * 16;
 
 size_t sgn_aggregate_workspace_bytes_f32(int64_t S) {
@@ -1653,9 +1655,12 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     SGN_REQUIRE(ws_items >= 32, "aggregate workspace too small");
     SGN_REQUIRE(stages == 3 || ws_items >= S_capacity,
                 "stages 1 and 2 called separately need a workspace for all S_capacity items");
-    // chunk = items per launch; with a full-size workspace chunk c keeps its rows at item c * chunk
+    // chunk = items per launch; with a full-size workspace chunk c keeps its rows at item c * chunk.
+    // k_rows16 bases its f_s descriptor per tile (one launch per stage for any frame); the 32x32
+    // kernel's single descriptor limits a launch to X3_MAX_CHUNK items
     const bool full = ws_items >= S_capacity;
-    const int64_t chunk = ws_items < X3_MAX_CHUNK ? ws_items : X3_MAX_CHUNK;
+    const int64_t lim = x3_w16() ? ws_items : (ws_items < X3_MAX_CHUNK ? ws_items : X3_MAX_CHUNK);
+    const int64_t chunk = lim < S_capacity ? lim : (S_capacity > 32 ? S_capacity : 32);
     AggArgs a{};
     a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
     a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
