@@ -102,6 +102,9 @@ struct AggArgs {
     _Float16 *sh2;    // [rows][272] block3.0 inputs (chain order | colour, dir - v, <dir, v>)
     _Float16 *sh3;    // [rows][256] block3.2 inputs (chain order)
     unsigned long long *tdbg;  // timing builds only (SGN_X3_TIMING): per-wave clock stamps
+    // packed point records of the fp32 16x16 kernels (k_point_proj16 writes them beside P):
+    // 64 B per point = {x, y, z, conf}, {r, g, b, 0}, {dx, dy, dz, 0}, {0}; one cache line per row
+    const float *rec;
 };
 
 // training save: one 16-byte fragment of a 32-row tile -> [rows][C] (C multiple of 16)

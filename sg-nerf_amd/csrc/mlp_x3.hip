@@ -895,7 +895,10 @@ struct Proj16Args {
     int64_t n;
     const void *blob;
     float *proj;
+    const float *xyz, *color, *dir, *conf;
+    float *rec;  // [n][16] packed point records (AggArgs::rec), after P in the projection buffer
 };
+constexpr int REC16_FLOATS = 16;
 constexpr int Y_LDS_OFF = NSLOT * SLOT;
 constexpr int PROJ16_LDS = Y_LDS_OFF + N_Y32 * 4;
 
@@ -949,11 +952,20 @@ __global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
             }
             return split8(v);
         };
+        // the point's packed record, lane group g's 16-B quarter: loaded here, stored after the
+        // MFMAs (which hide the loads)
+        f32x4 q{};
+        {
+            const float *src = g == 0 ? a.xyz : g == 1 ? a.color : a.dir;
+            const int64_t pc = ok ? p : 0;
+            if (g < 3) q = f32x4{src[pc * 3], src[pc * 3 + 1], src[pc * 3 + 2], g == 0 ? a.conf[pc] : 0.f};
+        }
         run_layer16<NetProj16, 0>(wb, lds + lz, slot, w, lane, lz, acc, in);
         if (ok) {  // natural unit order: tile t of lane group g at 16 t + 4 g (64 B per point per store)
             float *dst = a.proj + p * HID + 4 * g;
 #pragma unroll
             for (int t = 0; t < 16; ++t) *(f32x4 *)(dst + 16 * t) = acc[t];
+            *(f32x4 *)(a.rec + p * REC16_FLOATS + 4 * g) = q;
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -973,22 +985,26 @@ struct Rec16 {
 };
 // Rows without a work item (ix.sval false: the tail of the work list, or a launch with no
 // samples at all, where samp_ray holds no written entry) read nothing.
+// The point's attributes come from its packed 64-B record (three 16-B loads on one cache line,
+// instead of ten dword gathers from four tables).
 __device__ __forceinline__ Rec16 load_rec16(const AggArgs &a, const RowIdx &ix) {
     Rec16 r;
     const bool v = ix.sval;
     const int pid = ix.pid, s = ix.s, ray = ix.ray;
     const bool m = v && pid >= 0;
+    const f32x4 *rp = (const f32x4 *)(a.rec + (int64_t)(m ? pid : 0) * REC16_FLOATS);
+    const f32x4 q0 = m ? rp[0] : f32x4{}, q1 = m ? rp[1] : f32x4{}, q2 = m ? rp[2] : f32x4{};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        r.p[c] = m ? a.xyz[(int64_t)pid * 3 + c] : 0.f;
-        r.col[c] = m ? a.color[(int64_t)pid * 3 + c] : 0.f;
-        r.dir[c] = m ? a.dir[(int64_t)pid * 3 + c] : 0.f;
+        r.p[c] = q0[c];
+        r.col[c] = q1[c];
+        r.dir[c] = q2[c];
         r.l[c] = v ? a.samp_locw[(int64_t)s * 3 + c] : 0.f;
         r.v[c] = v ? a.raydir[(int64_t)ray * 3 + c] : 0.f;
         r.pp[c] = (a.pers && m) ? a.pers[(int64_t)pid * 3 + c] : 0.f;
         r.pl[c] = (a.pers && v) ? a.samp_pers[(int64_t)s * 3 + c] : 0.f;
     }
-    r.cf = m ? a.conf[pid] : 0.f;
+    r.cf = q0[3];
     return r;
 }
 
@@ -1598,7 +1614,8 @@ int sgn_mlp_pack_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *const
 }
 
 size_t sgn_point_proj_bytes_f32(int64_t n_points) {
-    return (size_t)(n_points > 0 ? n_points : 0) * sgn::x3::PROJ_BYTES_PER_POINT;
+    // P rows, then (16x16 kernels) the packed 64-B point records
+    return (size_t)(n_points > 0 ? n_points : 0) * (sgn::x3::PROJ_BYTES_PER_POINT + sgn::x3::REC16_FLOATS * 4);
 }
 
 int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void *d_proj, sgn_stream_t stream) {
@@ -1608,7 +1625,10 @@ int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void
     SGN_REQUIRE(((uintptr_t)d_proj & 15) == 0 && ((uintptr_t)pt->embedding & 15) == 0, "16-byte alignment required");
     if (pt->n_points == 0) return 0;
     if (x3_w16()) {
-        x3::Proj16Args a{pt->embedding, pt->n_points, d_packed, (float *)d_proj};
+        SGN_REQUIRE(pt->xyz && pt->color && pt->dir && pt->conf, "point tables (xyz, color, dir, conf) required");
+        float *rec = (float *)((char *)d_proj + (size_t)pt->n_points * x3::PROJ_BYTES_PER_POINT);
+        x3::Proj16Args a{pt->embedding, pt->n_points, d_packed, (float *)d_proj, pt->xyz, pt->color, pt->dir,
+                         pt->conf, rec};
         const int64_t tiles = (pt->n_points + 16 * x3::NW16 - 1) / (16 * x3::NW16);
         hipLaunchKernelGGL(x3::k_point_proj16, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB16), 0,
                            as_stream(stream), a);
@@ -1670,6 +1690,7 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     a.blob = d_packed; a.blob_bytes = x3::blob_bytes_sg(ksb);
     a.bpnet32 = d_bpnet;
     a.proj = (const _Float16 *)d_point_proj;  // fp32 table (k_agg_rows_x3 reads it as float)
+    a.rec = (const float *)((const char *)d_point_proj + (size_t)pt->n_points * x3::PROJ_BYTES_PER_POINT);
     a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
 #ifdef SGN_X3_TIMING
     static unsigned long long *tbuf = nullptr;
