@@ -221,11 +221,18 @@ constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NWv - 1) / NWv; 
 // chunk boundary: this wave's DMAs of chunk N landed, LDS reads drained, barrier; then chunk N+1
 // goes into the slot every wave finished reading one chunk ago (here, or spread over the chunk's
 // MFMAs by run_pass with SGN_X3_SPREAD)
-template <class Net, int N, int NWv = NW>
+// VM: vector-memory operations this wave is guaranteed to have issued after its last DMA piece of
+// the chunk being entered (loads placed at the end of the previous chunk, stores): they may stay in
+// flight across the boundary (vmcnt retires in order, so the DMA has landed once at most VM remain)
+template <class Net, int N, int NWv = NW, int VM = 0>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz,
                                             TStamp *ts = nullptr) {
 #ifndef SGN_X3_ABLATE_BARRIER  // timing experiment only: no boundary waits / barrier (wrong results)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    static_assert(VM >= 0 && VM < 64, "vmcnt range");
+    if constexpr (VM == 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else  // vmcnt[3:0] | expcnt 7 | lgkmcnt 15 | vmcnt[5:4] << 14 (gfx9 encoding: wait on vmcnt only)
+        __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 #endif
@@ -241,6 +248,10 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot
 struct NoHook {
     template <class C>
     __device__ void operator()(C) const {}
+};
+// vmcnt allowance at the entry of chunk C of a layer (chunk_enter's VM)
+struct VmZero {
+    static constexpr int vm(int) { return 0; }
 };
 
 
@@ -809,16 +820,17 @@ __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
 // One layer, k-outer over all 16 output tiles: acc[t] += W[t] in(k), three MFMAs per
 // (k-step, tile), next chunk's LDS-DMA pieces spread over the first pairs.  TRANS: activations
 // are the A operand (acc[t] holds D[row 4g+i][unit 16t + (l & 15)]).
-template <class Net, int L, bool TRANS = false, class InFn, class PostFn = NoHook>
+template <class Net, int L, bool TRANS = false, class Vm = VmZero, class InFn, class PostFn = NoHook,
+          class EndFn = NoHook>
 __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
                                             f32x4 (&acc)[16], InFn &&in, PostFn &&post = PostFn{},
-                                            TStamp *ts = nullptr) {
+                                            TStamp *ts = nullptr, EndFn &&end = EndFn{}) {
     constexpr XL ly = Net::L[L];
     static_assert(ly.tp == 16 && ly.np == 1, "16-tile single-pass layers");
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
         constexpr int N = Sched<Net>::idx(L, 0, C), NN = (N + 1) % Sched<Net>::total();
-        chunk_enter<Net, N, NW16>(wb, lds, slot, w, lane, lz, ts);
+        chunk_enter<Net, N, NW16, Vm::vm(C)>(wb, lds, slot, w, lane, lz, ts);
         post(cc);
         const char *sl = lds + slot * SLOT;
         char *dnext = lds + (slot ^ 1) * SLOT;
@@ -868,6 +880,8 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slo
 #endif
             });
         });
+        __builtin_amdgcn_sched_barrier(0);
+        end(cc);  // after every DMA piece of the chunk: loads here may stay in flight one boundary
         slot ^= 1;
         __builtin_amdgcn_sched_barrier(0);
     });
@@ -987,26 +1001,48 @@ struct Rec16 {
 // samples at all, where samp_ray holds no written entry) read nothing.
 // The point's attributes come from its packed 64-B record (three 16-B loads on one cache line,
 // instead of ten dword gathers from four tables).
+// The nine loads of the record, sample position and ray direction are issued unconditionally (rows
+// without a work item or neighbour read the weight blob instead and select zeros), so a caller may
+// count them (REC16_LOADS) in a chunk boundary's vmcnt allowance.
+constexpr int REC16_LOADS = 9;
 __device__ __forceinline__ Rec16 load_rec16(const AggArgs &a, const RowIdx &ix) {
     Rec16 r;
     const bool v = ix.sval;
     const int pid = ix.pid, s = ix.s, ray = ix.ray;
     const bool m = v && pid >= 0;
-    const f32x4 *rp = (const f32x4 *)(a.rec + (int64_t)(m ? pid : 0) * REC16_FLOATS);
-    const f32x4 q0 = m ? rp[0] : f32x4{}, q1 = m ? rp[1] : f32x4{}, q2 = m ? rp[2] : f32x4{};
+    const float *dummy = (const float *)a.blob;
+    const f32x4 *rp = (const f32x4 *)(m ? a.rec + (int64_t)pid * REC16_FLOATS : dummy);
+    const float *lp = v ? a.samp_locw + (int64_t)s * 3 : dummy;
+    const float *vp = v ? a.raydir + (int64_t)ray * 3 : dummy;
+    const f32x4 q0 = rp[0], q1 = rp[1], q2 = rp[2];
+    float l3[3], v3[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        r.p[c] = q0[c];
-        r.col[c] = q1[c];
-        r.dir[c] = q2[c];
-        r.l[c] = v ? a.samp_locw[(int64_t)s * 3 + c] : 0.f;
-        r.v[c] = v ? a.raydir[(int64_t)ray * 3 + c] : 0.f;
+        l3[c] = lp[c];
+        v3[c] = vp[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        r.p[c] = m ? q0[c] : 0.f;
+        r.col[c] = m ? q1[c] : 0.f;
+        r.dir[c] = m ? q2[c] : 0.f;
+        r.l[c] = v ? l3[c] : 0.f;
+        r.v[c] = v ? v3[c] : 0.f;
         r.pp[c] = (a.pers && m) ? a.pers[(int64_t)pid * 3 + c] : 0.f;
         r.pl[c] = (a.pers && v) ? a.samp_pers[(int64_t)s * 3 + c] : 0.f;
     }
-    r.cf = q0[3];
+    r.cf = m ? q0[3] : 0.f;
     return r;
 }
+// vmcnt allowances of k_rows16's boundaries (chunk_enter VM): block3.2 ends chunk 0 with the next
+// tile's record (REC16_LOADS loads); after block3.2 come the next tile's 16 P loads and the
+// epilogue's two unconditional f_s stores, all younger than block1.0's DMA
+struct VmL3 {
+    static constexpr int vm(int c) { return c == 1 ? REC16_LOADS : 0; }
+};
+struct VmL0 {
+    static constexpr int vm(int) { return 16 + 2; }
+};
 
 // dists (point_aggregators.py:917-925): d[0..2] world offsets, d[3..5] pers-space terms; the
 // linear-kernel weight normalised over the sample's 8 rows times the clamped conf (:946-953)
@@ -1170,8 +1206,8 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
 #pragma unroll
                 for (int t = 0; t < 16; ++t) accA[t] = accB[t];
             }
-            run_layer16<Net, 0>(wb, ldsi, slot, w, lane, lz, accA, [&](auto k) { return B0[decltype(k)::value]; },
-                                NoHook{}, ts);
+            run_layer16<Net, 0, false, VmL0>(wb, ldsi, slot, w, lane, lz, accA,
+                                             [&](auto k) { return B0[decltype(k)::value]; }, NoHook{}, ts);
         }
         // block1.2: 256 -> 256 (input: block1.0 accumulators)
         const float inv0 = Yl[Y_INV + 0], inv1 = Yl[Y_INV + 1], inv2 = Yl[Y_INV + 2], inv7 = Yl[Y_INV + 7];
@@ -1221,11 +1257,14 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         auto &acc = in2;  // block3.0's input is dead: its registers take block3.2's accumulators
 #pragma unroll
         for (int t = 0; t < 16; ++t) acc[t] = f32x4{};
-        run_layer16<Net, L3, true>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) { return chain_k(acc2, inv2, k); },
-                                  [&](auto c) {
-                                      constexpr int C = decltype(c)::value;
-                                      if constexpr (C == 0) rnext = load_rec16(a, nx);
-                                  }, ts);
+        // the next tile's record and P rows go out at the ends of block3.2's chunks (after each chunk's
+        // DMA pieces, so they stay in flight across one boundary, VmL3): P tiles 4C..4C+3 into block3.0's
+        // accumulators, dead once chunk C's k-steps 2C, 2C+1 have consumed them (see accA)
+        run_layer16<Net, L3, true, VmL3>(wb, ldsi, slot, w, lane, lz, acc,
+                                         [&](auto k) { return chain_k(acc2, inv2, k); }, NoHook{}, ts,
+                                         [&](auto c) {
+                                             if constexpr (decltype(c)::value == 0) rnext = load_rec16(a, nx);
+                                         });
         load_p(nx.pid, acc2);  // the next tile's P (see accA)
         X3T();  // block3.2 MFMAs issued
         // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads
