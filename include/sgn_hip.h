@@ -204,7 +204,10 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
  * block2_bpnet variant as in sgn_mlp_pack_sg (0/0 = base ScanNet viewmlp).
  *   sgn_mlp_pack_f32        : 9 (+ block2_bpnet.0) layers as sgn_mlp_pack_sg -> blob of
  *                             sgn_mlp_packed_bytes_f32(bpnet_layers, bpnet_dim) bytes (0: unsupported)
- *   sgn_point_project_f32   : P[p] fp32 (sgn_point_proj_bytes_f32(N)), the block1.0 per-point part
+ *   sgn_point_project_f32   : P[p] fp32, the block1.0 per-point part, followed by a packed 64-B
+ *                             record per point (xyz, conf, colour, dir) that the row kernel gathers
+ *                             as one cache line (sgn_point_proj_bytes_f32(N) bytes; pt->xyz, color,
+ *                             dir, conf and embedding required; opaque to the caller)
  *   sgn_aggregate_f32       : as sgn_aggregate_sg (same outputs, stages bits), d_point_proj required;
  *                             d_bpnet = fp32 [N, 96] BPNet point embedding when bpnet_dim = 96;
  *                             workspace sgn_aggregate_workspace_bytes_f32(S) (fp32 blended features)

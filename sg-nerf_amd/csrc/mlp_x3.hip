@@ -1265,7 +1265,6 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
                                          [&](auto c) {
                                              if constexpr (decltype(c)::value == 0) rnext = load_rec16(a, nx);
                                          });
-        load_p(nx.pid, acc2);  // the next tile's P (see accA)
         X3T();  // block3.2 MFMAs issued
         // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads
         // from the compiler's wait tracking, which would otherwise wait for the epilogue's stores
@@ -1282,8 +1281,11 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
             wv[i] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, rw.wgt)));
         const float inv3 = Yl[Y_INV + 3];
         float ap[4] = {0.f, 0.f, 0.f, 0.f}, fs[16];
+        // the next tile's P rows (see accA) go out tile by tile between the epilogue's VALU work
+        const float *psrc = proj + (int64_t)(nx.pid < 0 ? 0 : nx.pid) * HID + 4 * g;
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
+            acc2[t] = *(const f32x4 *)(psrc + 16 * t);
             const float bu = Yl[Y_B3 + 16 * t + r], wau = Yl[Y_WA + 16 * t + r];
             float fg = 0.f;
 #pragma unroll
