@@ -1082,10 +1082,13 @@ __device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, co
 // PE(dists) of the row (networks.py:175-192, 6 values x 5 frequencies): (value, frequency) pair
 // pp = 8 g + c of lane group g, c = 0..7 (pairs 30, 31 padding) -> k-step c / 4, slots 2 (c % 4),
 // 2 (c % 4) + 1 = sin, cos of d[pp / 5] 2^(pp % 5) (col_l0b16 maps them to reference columns)
-__device__ __forceinline__ void pe_dists16(const float (&d)[6], int g, X3B (&B)[2]) {
-    float v[16];
+// k-step S's fragment: pairs c = 4 S .. 4 S + 3 (block1.0 computes it inside its k-loop, so the
+// second k-step's sin / cos overlap the first one's MFMAs)
+template <int S>
+__device__ __forceinline__ X3B pe_dists16_k(const float (&d)[6], int g) {
+    float u[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 4 * S; c < 4 * S + 4; ++c) {
         const int pp = 8 * g + c, di = pp / 5, f = pp - 5 * di;
         float x = d[0];
 #pragma unroll
@@ -1093,16 +1096,10 @@ __device__ __forceinline__ void pe_dists16(const float (&d)[6], int g, X3B (&B)[
         float sv, cv;
         sincos_acc(__builtin_ldexpf(x, f), sv, cv);
         const bool ok = pp < 30;
-        v[2 * c] = ok ? sv : 0.f;
-        v[2 * c + 1] = ok ? cv : 0.f;
+        u[2 * (c - 4 * S)] = ok ? sv : 0.f;
+        u[2 * (c - 4 * S) + 1] = ok ? cv : 0.f;
     }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        float u[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) u[j] = v[8 * s + j];
-        B[s] = split8(u);
-    }
+    return split8(u);
 }
 
 // KB: k-steps of block2_bpnet.0 in 16x16 steps (0: base viewmlp; 8: bpnet_dim 0; 11: dim 96)
@@ -1199,15 +1196,14 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
             for (int t = 0; t < 16; ++t) ac[t] = *(const f32x4 *)(Yl + yb + 16 * t + 4 * g);
         };
         {   // block1.0: W0b PE(dists) on MFMA, + P[pid] (W0a [feat | PE(feat)] + b0, k_point_proj16)
-            X3B B0[2];
-            pe_dists16(rw.d, g, B0);
-            X3T();  // gather + PE
+            X3T();  // gather (PE inside block1.0's k-loop)
             if constexpr (KB > 0) {  // SG: five layers, the P array alternates -- copy it back
 #pragma unroll
                 for (int t = 0; t < 16; ++t) accA[t] = accB[t];
             }
             run_layer16<Net, 0, false, VmL0>(wb, ldsi, slot, w, lane, lz, accA,
-                                             [&](auto k) { return B0[decltype(k)::value]; }, NoHook{}, ts);
+                                             [&](auto k) { return pe_dists16_k<decltype(k)::value>(rw.d, g); },
+                                             NoHook{}, ts);
         }
         // block1.2: 256 -> 256 (input: block1.0 accumulators)
         const float inv0 = Yl[Y_INV + 0], inv1 = Yl[Y_INV + 1], inv2 = Yl[Y_INV + 2], inv7 = Yl[Y_INV + 7];
