@@ -42,7 +42,7 @@ constexpr int SLOT_PAIRS = 32;
 constexpr int SLOT = SLOT_PAIRS * PAIR;  // 64 KiB
 constexpr int NSLOT = 2;
 #ifndef SGN_X3_PD
-#define SGN_X3_PD 3
+#define SGN_X3_PD 2
 #endif
 #ifndef SGN_X3_PIN
 #define SGN_X3_PIN 1
@@ -51,7 +51,7 @@ constexpr int NSLOT = 2;
 #define SGN_X3_SPREAD 1  // next chunk's LDS-DMA pieces interleaved with the current chunk's MFMAs
 #endif
 #ifndef SGN_X3_SPREAD_DIV
-#define SGN_X3_SPREAD_DIV 1  // DMA pieces spread over the first NF / DIV pairs of a chunk
+#define SGN_X3_SPREAD_DIV 2  // DMA pieces spread over the first NF / DIV pairs of a chunk
 #endif
 #ifndef SGN_X3_EPI_BARRIER
 #define SGN_X3_EPI_BARRIER 0  // 1: scheduling barrier after each layer epilogue

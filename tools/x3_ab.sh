@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 PREC=$1; shift
 cp sg-nerf_amd/libsgn_hip.so /tmp/base.so
 mkdir -p gpurun_out
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
     SGN_VARIANT=base timeout -k 10 120 python tools/agg_time.py $PREC >> gpurun_out/ab.jsonl 2>/dev/null || { echo FAIL base; break; }
     for v in "$@"; do
         cp "$v" sg-nerf_amd/libsgn_hip.so
