@@ -1564,6 +1564,24 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
     __syncthreads();
     int slot = 0;
     dma_chunk<NetColor16, 0, NW16>(wb, lds, w, lane, 0);
+    // the tile's f_s rows, sample ids and ray directions; the next tile's are loaded during colour 1
+    f32x4 fr[16];
+    float vd[3];
+    int sn = 0;
+    auto load_rows = [&](int item) {
+        const bool ok = item < end;
+        sn = ok ? a.work[item] : 0;
+        const int ray = a.samp_ray[sn];
+        const f32x4 *row = (const f32x4 *)(a.fs + (int64_t)(ok ? item - a.item0 : 0) * HID + 8 * g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            fr[2 * k] = row[8 * k];
+            fr[2 * k + 1] = row[8 * k + 1];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) vd[c] = a.raydir[(int64_t)ray * 3 + c];
+    };
+    load_rows(a.item0 + blockIdx.x * (16 * NW16) + w * 16 + r);
     for (int base = a.item0 + blockIdx.x * (16 * NW16); base < end; base += gridDim.x * (16 * NW16)) {
         int lz = 0;
         asm volatile("" : "+s"(lz));
@@ -1571,18 +1589,8 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
         const float *Yl = (const float *)(ldsi + Y_LDS_OFF);
         const int item = base + w * 16 + r;
         const bool sval = item < end;
-        const int s = sval ? a.work[item] : 0;
-        const int ray = a.samp_ray[s];
-        f32x4 fr[16];
-        {
-            const f32x4 *row = (const f32x4 *)(a.fs + (int64_t)(sval ? item - a.item0 : 0) * HID + 8 * g);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                fr[2 * k] = row[8 * k];
-                fr[2 * k + 1] = row[8 * k + 1];
-            }
-        }
-        const float v3[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1], a.raydir[(int64_t)ray * 3 + 2]};
+        const int s = sn;
+        const float v3[3] = {vd[0], vd[1], vd[2]};
         auto bias = [&](f32x4 (&ac)[8], int yb) {
 #pragma unroll
             for (int t = 0; t < 8; ++t) ac[t] = *(const f32x4 *)(Yl + yb + 16 * t + 4 * g);
@@ -1622,7 +1630,9 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
         });
         bias(c1, Y_CB1);
         const float inv4 = Yl[Y_INV + 4], inv5 = Yl[Y_INV + 5], inv6 = Yl[Y_INV + 6];
-        run_layer16<NetColor16, 1>(wb, ldsi, slot, w, lane, lz, c1, [&](auto k) { return chain(c0, inv4, k); });
+        // colour 0 consumed fr: the next tile's rows go out after colour 1's boundary (land under it)
+        run_layer16<NetColor16, 1>(wb, ldsi, slot, w, lane, lz, c1, [&](auto k) { return chain(c0, inv4, k); },
+                                   [&](auto) { load_rows(item + gridDim.x * (16 * NW16)); });
         bias(c0, Y_CB2);
         run_layer16<NetColor16, 2>(wb, ldsi, slot, w, lane, lz, c0, [&](auto k) { return chain(c1, inv5, k); });
         // output layer: units 16 t + 4 g + i of this lane, summed over the 4 lane groups
