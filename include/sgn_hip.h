@@ -270,6 +270,31 @@ int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, i
                            const sgn_agg_deltas *deltas, const sgn_point_grads *grads,
                            sgn_stream_t stream);
 
+/* ---- training of the SG-NeRF variant (block2_bpnet, point_aggregators.py:345-354, :629-636) ----
+ * Gradients of block2_bpnet.0 = Linear(256 + bpnet_dim -> 256) + LReLU between block1 and
+ * block3, on the fp16 blob of sgn_mlp_pack_sg (bpnet_layers 1, bpnet_dim 0 or 96; 0 layers =
+ * the base functions).  The forward additionally saves block2_bpnet's inputs h (d_h2b, fp16
+ * [rows][256], chain order) and saved->h2 holds block3.0's inputs (block2_bpnet's output + the
+ * colour / dir channels); the backward writes block2_bpnet's scaled deltas (d_db, fp16
+ * [rows][256]) and deltas->d2 = block1.2's.  The BPNet embedding is a detached input
+ * (neural_points.py:662): it gets no gradient.  The transposed blob gains block2_bpnet.0's
+ * first 256 input columns (sgn_train_pack_t_sg, w[0..3] and w[4] = block2_bpnet.0's weight). */
+int sgn_aggregate_train_fwd_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpnet_f16,
+                               const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                               const void *d_packed_mlp, float *d_out_feat, void *d_fs, const sgn_agg_saved *saved,
+                               void *d_h2b, sgn_stream_t stream);
+int sgn_aggregate_backward_sg(int32_t bpnet_layers, int32_t bpnet_dim, const sgn_point_tables *pt,
+                              const sgn_query_out *q, int32_t n_items, const void *d_packed_mlp, const void *d_tblob,
+                              const sgn_agg_saved *saved, const void *d_h2b, const float *d_dfs, const float *d_dalpha,
+                              const float *d_scale, const sgn_agg_deltas *deltas, void *d_db,
+                              const sgn_point_grads *grads, sgn_stream_t stream);
+int sgn_train_pack_t_sg(const float *const *w, int32_t bpnet_dim, void *d_tblob, sgn_stream_t stream);
+/* Index maps over the SG flat vector (the 9 base layers, then block2_bpnet.0 weight and bias):
+ * sgn_mlp_pack_index_sg which 3 = block2_bpnet fragments (n = (bias offset - OFF_WB) / 2 fp16
+ * elements), 4 = its bias (n = 256 fp32); sgn_train_pack_index_sg = the transposed blob. */
+int sgn_mlp_pack_index_sg(int32_t bpnet_layers, int32_t bpnet_dim, int32_t which, int32_t *out, int64_t n);
+int sgn_train_pack_index_sg(int32_t bpnet_dim, int32_t *out, int64_t n);
+
 /* ---- training: point-parameter Adam and bias-gradient column sums ------------------
  * Replaces torch.optim.Adam.step for the neural-point group (the reference's optimizer,
  * models/mvs_points_volumetric_model.py:100-108; no weight decay, no amsgrad): one fp32

@@ -96,6 +96,14 @@ SIGNATURES = {
     "sgn_aggregate_backward": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp,
                                        ctypes.POINTER(AggSaved), c_vp, c_vp, c_vp, ctypes.POINTER(AggDeltas),
                                        ctypes.POINTER(PointGrads), c_vp]),
+    "sgn_aggregate_train_fwd_sg": (c_i32, [c_i32, c_i32, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut),
+                                           c_i64, c_i32, c_vp, c_vp, c_vp, ctypes.POINTER(AggSaved), c_vp, c_vp]),
+    "sgn_aggregate_backward_sg": (c_i32, [c_i32, c_i32, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32,
+                                          c_vp, c_vp, ctypes.POINTER(AggSaved), c_vp, c_vp, c_vp, c_vp,
+                                          ctypes.POINTER(AggDeltas), c_vp, ctypes.POINTER(PointGrads), c_vp]),
+    "sgn_train_pack_t_sg": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp]),
+    "sgn_mlp_pack_index_sg": (c_i32, [c_i32, c_i32, c_i32, ctypes.POINTER(c_i32), c_i64]),
+    "sgn_train_pack_index_sg": (c_i32, [c_i32, ctypes.POINTER(c_i32), c_i64]),
     "sgn_adam_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                ctypes.c_double, c_i64, c_i32, c_vp]),
     "sgn_colsum_workspace_bytes": (c_sz, [c_i32]),

@@ -101,6 +101,8 @@ struct AggArgs {
     _Float16 *sh1;    // [rows][256] block1.2 inputs (chain order)
     _Float16 *sh2;    // [rows][272] block3.0 inputs (chain order | colour, dir - v, <dir, v>)
     _Float16 *sh3;    // [rows][256] block3.2 inputs (chain order)
+    _Float16 *sh2b;   // [rows][256] block2_bpnet inputs h (chain order; SG save mode, where sh2 then
+                      // holds block3.0's inputs [block2_bpnet output | colour, dir - v, <dir, v>])
     unsigned long long *tdbg;  // timing builds only (SGN_X3_TIMING): per-wave clock stamps
     // packed point records of the fp32 16x16 kernels (k_point_proj16 writes them beside P):
     // 64 B per point = {x, y, z, conf}, {r, g, b, 0}, {dx, dy, dz, 0}, {0}; one cache line per row

@@ -39,7 +39,10 @@ constexpr size_t OFF_T3 = 0;
 constexpr size_t OFF_T2 = OFF_T3 + (size_t)TT3 * 16 * FRAG;
 constexpr size_t OFF_T1 = OFF_T2 + (size_t)TT2 * 16 * FRAG;
 constexpr size_t OFF_T0 = OFF_T1 + (size_t)TT1 * 16 * FRAG;
-constexpr size_t T_BYTES = OFF_T0 + (size_t)TT0 * 16 * FRAG;
+// SG: block2_bpnet.0's first 256 inputs (the block1 output h; the BPNet embedding is not trained)
+constexpr int TTB = 8;
+constexpr size_t OFF_TB = OFF_T0 + (size_t)TT0 * 16 * FRAG;
+constexpr size_t T_BYTES = OFF_TB + (size_t)TTB * 16 * FRAG;
 
 struct BwdArgs {
     AggArgs a;                 // point tables, query, forward blob (gather + W3 recompute)
@@ -53,6 +56,8 @@ struct BwdArgs {
     float *dza;                // [rows] scaled d alpha-logit
     float *g_emb, *g_color, *g_dir, *g_conf;  // [N,32] [N,3] [N,3] [N] (atomic add, unscaled)
     int32_t n_items;
+    const _Float16 *sh2b;      // SG: [rows][256] block2_bpnet inputs h (chain order)
+    _Float16 *db;              // SG: [rows][256] scaled block2_bpnet deltas (chain order)
 };
 
 __device__ __forceinline__ h8 load_frag(const _Float16 *base, int C, int64_t row0, int s, int lane, bool ok) {
@@ -85,23 +90,25 @@ __device__ __forceinline__ h8 plain_frag(const f32x16 &acc, int s2) {
 constexpr int BWD_TPB = 256;
 constexpr int BWD_SLOT = 4 * 16 * (int)FRAG;  // the largest product: 4 tiles x 16 k-steps
 constexpr int BWD_LDS = 2 * BWD_SLOT;
-constexpr int N_PROD = 12;
-
 // product I: 0-1 block3.2 recompute (W3, tiles 4I..), 2-3 W3^T, 4-5 W2^T, 6 W2^T's input tile 8
-// (colour / dir channels), 7-8 W1^T, 9-11 W0^T (3 row tiles each)
-__host__ __device__ constexpr int prod_nt(int I) { return I == 6 ? 1 : I >= 9 ? 3 : 4; }
-__host__ __device__ constexpr uint32_t prod_off(int I, int ks, int t) {
+// (colour / dir channels), [SG: 7-8 W_B^T], then W1^T (2 products), W0^T (3, 3 row tiles each)
+__host__ __device__ constexpr int n_prod(bool sg) { return sg ? 14 : 12; }
+__host__ __device__ constexpr int prod_w1(bool sg) { return sg ? 9 : 7; }
+__host__ __device__ constexpr int prod_w0(bool sg) { return sg ? 11 : 9; }
+__host__ __device__ constexpr int prod_nt(int I, bool sg = false) { return I == 6 ? 1 : I >= prod_w0(sg) ? 3 : 4; }
+__host__ __device__ constexpr uint32_t prod_off(int I, int ks, int t, bool sg = false) {
     return (uint32_t)(I < 2 ? OFF_W3 + ((size_t)(I * KS_HID + ks) * 4 + t) * FRAG
                     : I < 4 ? OFF_T3 + ((size_t)((I - 2) * 4 + t) * 16 + ks) * FRAG
                     : I < 6 ? OFF_T2 + ((size_t)((I - 4) * 4 + t) * 16 + ks) * FRAG
                     : I == 6 ? OFF_T2 + ((size_t)(8 + t) * 16 + ks) * FRAG
-                    : I < 9 ? OFF_T1 + ((size_t)((I - 7) * 4 + t) * 16 + ks) * FRAG
-                            : OFF_T0 + ((size_t)((I - 9) * 3 + t) * 16 + ks) * FRAG);
+                    : (sg && I < 9) ? OFF_TB + ((size_t)((I - 7) * 4 + t) * 16 + ks) * FRAG
+                    : I < prod_w0(sg) ? OFF_T1 + ((size_t)((I - prod_w1(sg)) * 4 + t) * 16 + ks) * FRAG
+                                      : OFF_T0 + ((size_t)((I - prod_w0(sg)) * 3 + t) * 16 + ks) * FRAG);
 }
 
-template <int I>
+template <int I, bool SG = false>
 __device__ __forceinline__ void prod_dma(char *lds, const WBlob &wb, const WBlob &tb, int w, int lane) {
-    constexpr int NT = prod_nt(I), NF = 16 * NT;
+    constexpr int NT = prod_nt(I, SG), NF = 16 * NT;
     static_assert(NF % 4 == 0 && NF * (int)FRAG <= BWD_SLOT, "staging slot");
     const WBlob &src = I < 2 ? wb : tb;
     char *dst = lds + (I & 1) * BWD_SLOT;
@@ -109,20 +116,20 @@ __device__ __forceinline__ void prod_dma(char *lds, const WBlob &wb, const WBlob
     for (int i = 0; i < NF / 4; ++i) {
         const int n = w + 4 * i;  // fragment n = (ks, t) = (n / NT, n % NT)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rsrc, (__attribute__((address_space(3))) void *)(dst + n * (int)FRAG),
-                                                 16, lane * 16, prod_off(I, n / NT, n % NT), 0, 0);
+                                                 16, lane * 16, prod_off(I, n / NT, n % NT, SG), 0, 0);
     }
 }
 
-// acc[t] (+)= sum_ks W_I(t, ks) * in[ks]; `more`: the workgroup has another tile (product 11's
-// successor is the next tile's product 0)
-template <int I, int NT>
+// acc[t] (+)= sum_ks W_I(t, ks) * in[ks]; `more`: the workgroup has another tile (the last
+// product's successor is the next tile's product 0)
+template <int I, int NT, bool SG = false>
 __device__ __forceinline__ void prod_mul(char *lds, const WBlob &wb, const WBlob &tb, const h8 (&in)[16],
                                          f32x16 (&acc)[NT], int w, int lane, bool more) {
-    static_assert(NT == prod_nt(I), "product width");
+    static_assert(NT == prod_nt(I, SG), "product width");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of product I landed
     __syncthreads();  // everyone's, and everyone is done with product I - 1's slot
-    if constexpr (I + 1 < N_PROD) prod_dma<I + 1>(lds, wb, tb, w, lane);
-    else if (more) prod_dma<0>(lds, wb, tb, w, lane);
+    if constexpr (I + 1 < n_prod(SG)) prod_dma<I + 1, SG>(lds, wb, tb, w, lane);
+    else if (more) prod_dma<0, SG>(lds, wb, tb, w, lane);
     const char *sl = lds + (I & 1) * BWD_SLOT;
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks)
@@ -132,12 +139,12 @@ __device__ __forceinline__ void prod_mul(char *lds, const WBlob &wb, const WBlob
 }
 
 // acc[t] = sum_ks T[t0 + t][ks] * in[ks] for the NT row tiles of transposed product I
-template <int I, int NT>
+template <int I, int NT, bool SG = false>
 __device__ __forceinline__ void tmul(char *lds, const WBlob &wb, const WBlob &tb, const h8 (&in)[16],
                                      f32x16 (&acc)[NT], int w, int lane, bool more) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
-    prod_mul<I, NT>(lds, wb, tb, in, acc, w, lane, more);
+    prod_mul<I, NT, SG>(lds, wb, tb, in, acc, w, lane, more);
 }
 
 // d feat[c] contribution of layer-0 local channel C (mlp_layout.h l0 order): PE(feat) chain rule
@@ -154,19 +161,21 @@ __device__ __forceinline__ void l0_backward(float d, const float (&feat)[16], fl
     // C >= 112: PE(dists) -> point xyz / sample positions (not trained)
 }
 
+template <bool SG>
 __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
+    constexpr int IW1 = prod_w1(SG), IW0 = prod_w0(SG);
     __shared__ __attribute__((aligned(16))) char lds[BWD_LDS];
     const AggArgs &a = b.a;
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, j = lane & 31, q = j >> 3;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const Cam cam = load_cam(a.campos, a.rot);
-    const WBlob wb = make_blob(a.blob);
+    const WBlob wb = make_blob(a.blob, a.blob_bytes);
     const WBlob tb = make_blob(b.tblob, T_BYTES);
     const float *F = (const float *)((const char *)a.blob + OFF_F32);
     const float scale = *b.scale, inv = 1.f / scale;
     const int end = b.n_items;
-    if (blockIdx.x * 16 < end) prod_dma<0>(lds, wb, tb, w, lane);  // stream prologue
+    if (blockIdx.x * 16 < end) prod_dma<0, SG>(lds, wb, tb, w, lane);  // stream prologue
     // trip count uniform over the workgroup (its waves meet at the staging barriers); rows past
     // the end are masked (ok = false)
     for (int bbase = blockIdx.x * 16; bbase < end; bbase += gridDim.x * 16) {
@@ -187,8 +196,8 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
             for (int s = 0; s < 16; ++s) x3[s] = load_frag(b.sh3, 256, row0, s, lane, ok);
 #pragma unroll
             for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
-            prod_mul<0, 4>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[0], w, lane, more);
-            prod_mul<1, 4>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[4], w, lane, more);
+            prod_mul<0, 4, SG>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[0], w, lane, more);
+            prod_mul<1, 4, SG>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[4], w, lane, more);
         }
         // ---- pass 1: h4, alpha logit, <h4, d f_s> ------------------------------------------
         const float *dfs = b.dfs + (int64_t)it * HID;
@@ -248,8 +257,8 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            if (p == 0) tmul<2, 4>(lds, wb, tb, dl, ac, w, lane, more);
-            else tmul<3, 4>(lds, wb, tb, dl, ac, w, lane, more);
+            if (p == 0) tmul<2, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
+            else tmul<3, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -260,23 +269,24 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
                 }
         }
         // ---- block3.0 backward: delta2 = (W2^T delta3)[:256] * LReLU'(h2); ext grads -------
+        // (SG: h2 is the block2_bpnet output, so this is block2_bpnet's delta, saved to db)
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            if (p == 0) tmul<4, 4>(lds, wb, tb, dn, ac, w, lane, more);
-            else tmul<5, 4>(lds, wb, tb, dn, ac, w, lane, more);
+            if (p == 0) tmul<4, 4, SG>(lds, wb, tb, dn, ac, w, lane, more);
+            else tmul<5, 4, SG>(lds, wb, tb, dn, ac, w, lane, more);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const int k = 2 * (4 * p + tt) + s2;
                     dl[k] = mask_frag(ac[tt], s2, load_frag(b.sh2, KS_L2 * 16, row0, k, lane, ok));
-                    save_frag(b.d2, 256, row0, k, dl[k], lane, ok);
+                    save_frag(SG ? b.db : b.d2, 256, row0, k, dl[k], lane, ok);
                 }
         }
         {
             f32x16 ae[1];
-            tmul<6, 1>(lds, wb, tb, dn, ae, w, lane, more);
+            tmul<6, 1, SG>(lds, wb, tb, dn, ae, w, lane, more);
             // tile 8 = inputs 256..262: half 0 regs 0..3 -> colour 0..2, (dir - v)_0;
             // half 1 regs 0..2 -> (dir - v)_1, (dir - v)_2, <dir, v>   (:639-652)
             const float o0 = __shfl_xor(ae[0][0], 32), o1 = __shfl_xor(ae[0][1], 32), o2 = __shfl_xor(ae[0][2], 32);
@@ -294,12 +304,31 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
                 atomicAdd(b.g_conf + ri.pid, dwgt * ri.wn * inv);  // straight-through clamp (:863-865)
             }
         }
+        // ---- SG block2_bpnet backward: delta2 = (W_B[:, :256]^T delta_B) * LReLU'(h) ------
+        if constexpr (SG) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                f32x16 ac[4];
+                if (p == 0) tmul<7, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
+                else tmul<8, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
+#pragma unroll
+                for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const int k = 2 * (4 * p + tt) + s2;
+                        dn[k] = mask_frag(ac[tt], s2, load_frag(b.sh2b, 256, row0, k, lane, ok));
+                        save_frag(b.d2, 256, row0, k, dn[k], lane, ok);
+                    }
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) dl[k] = dn[k];
+        }
         // ---- block1.2 backward: delta1 = (W1^T delta2) * LReLU'(h1) ----------------------
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
             f32x16 ac[4];
-            if (p == 0) tmul<7, 4>(lds, wb, tb, dl, ac, w, lane, more);
-            else tmul<8, 4>(lds, wb, tb, dl, ac, w, lane, more);
+            if (p == 0) tmul<IW1, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
+            else tmul<IW1 + 1, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -316,7 +345,7 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
         static_for<3>([&](auto pp) {
             constexpr int P = decltype(pp)::value;
             f32x16 ac[3];
-            tmul<9 + P, 3>(lds, wb, tb, dn, ac, w, lane, more);
+            tmul<IW0 + P, 3, SG>(lds, wb, tb, dn, ac, w, lane, more);
             static_for<3>([&](auto ttc) {
                 constexpr int T = 3 * P + decltype(ttc)::value;
                 static_for<16>([&](auto rr) {
@@ -364,8 +393,10 @@ int t0_row(int pos) {
     return l0_ref_col((jj >> 2) & 1, 16 * t + (jj & 3) + 4 * (jj >> 3));
 }
 
+// w: block1.0, block1.2, block3.0, block3.2 weights, and (SG, wb != nullptr) block2_bpnet.0's
+// [256][256 + bpnet_dim] weight, of which the first 256 input columns are transposed
 template <typename T>
-void pack_tblob(const float *const *w, T *e) {
+void pack_tblob(const float *const *w, T *e, const float *wb = nullptr, int bpnet_dim = 0) {
     const auto idr = [](int r) { return r; };
     std::vector<float> t3 = transpose(w[3], 256, 256), t2 = transpose(w[2], 256, 263), t1 = transpose(w[1], 256, 256),
                        t0 = transpose(w[0], 256, 284);
@@ -373,6 +404,13 @@ void pack_tblob(const float *const *w, T *e) {
     pack_t(e + OFF_T2 / 2, t2.data(), 263, 256, TT2, idr, chain_col);
     pack_t(e + OFF_T1 / 2, t1.data(), 256, 256, TT1, idr, chain_col);
     pack_t(e + OFF_T0 / 2, t0.data(), 284, 256, TT0, t0_row, chain_col);
+    if (wb) {
+        std::vector<float> h((size_t)256 * 256);
+        for (int o = 0; o < 256; ++o)
+            for (int i = 0; i < 256; ++i) h[(size_t)o * 256 + i] = wb[(size_t)o * (256 + bpnet_dim) + i];
+        std::vector<float> tbp = transpose(h.data(), 256, 256);
+        pack_t(e + OFF_TB / 2, tbp.data(), 256, 256, TTB, idr, chain_col);
+    }
 }
 
 }  // namespace
@@ -401,6 +439,41 @@ int sgn_train_pack_index(int32_t *out, int64_t n) {
     std::vector<float> e(T_BYTES / 2, 0.f);
     pack_tblob(wp.data(), e.data());
     for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)e[(size_t)i];
+    return 0;
+}
+
+/* As sgn_train_pack_index for the SG flat vector (the 9 base layers, then block2_bpnet.0 weight
+ * [256][256 + bpnet_dim] and bias): the block2_bpnet section of the transposed blob maps too. */
+int sgn_train_pack_index_sg(int32_t bpnet_dim, int32_t *out, int64_t n) {
+    using namespace sgn;
+    SGN_REQUIRE(bpnet_dim == 0 || bpnet_dim == mlp::BP_DIM, "bpnet_dim must be 0 or 96");
+    SGN_REQUIRE(out && n == (int64_t)(T_BYTES / 2), "sgn_train_pack_index_sg: bad size");
+    const int64_t o0 = 0, o1 = o0 + 256 * 284 + 256, o2 = o1 + 256 * 256 + 256, o3 = o2 + 256 * 263 + 256;
+    const int64_t ob = 341764;  // after the 9 base layers (weights.N_PARAMS)
+    const int64_t offs[5] = {o0, o1, o2, o3, ob};
+    const int64_t sz[5] = {256 * 284, 256 * 256, 256 * 263, 256 * 256, (int64_t)256 * (256 + bpnet_dim)};
+    std::vector<std::vector<float>> wi(5);
+    std::vector<const float *> wp(5);
+    for (int L = 0; L < 5; ++L) {
+        wi[L].resize((size_t)sz[L]);
+        for (int64_t i = 0; i < sz[L]; ++i) wi[L][(size_t)i] = (float)(offs[L] + i + 1);
+        wp[L] = wi[L].data();
+    }
+    std::vector<float> e(T_BYTES / 2, 0.f);
+    pack_tblob(wp.data(), e.data(), wp[4], bpnet_dim);
+    for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)e[(size_t)i];
+    return 0;
+}
+
+int sgn_train_pack_t_sg(const float *const *w, int32_t bpnet_dim, void *d_tblob, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(w && w[0] && w[1] && w[2] && w[3] && w[4], "null weights");
+    SGN_REQUIRE(bpnet_dim == 0 || bpnet_dim == mlp::BP_DIM, "bpnet_dim must be 0 or 96");
+    std::vector<uint8_t> blob(T_BYTES, 0);
+    pack_tblob(w, (_Float16 *)blob.data(), w[4], bpnet_dim);
+    hipStream_t st = as_stream(stream);
+    SGN_CHECK_HIP(hipMemcpyAsync(d_tblob, blob.data(), T_BYTES, hipMemcpyHostToDevice, st));
+    SGN_CHECK_HIP(hipStreamSynchronize(st));
     return 0;
 }
 
@@ -462,7 +535,51 @@ int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, i
     b.n_items = n_items;
     const int64_t waves = ((int64_t)n_items + 3) / 4;
     const int64_t blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL(k_agg_bwd, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(BWD_TPB), 0, as_stream(stream), b);
+    hipLaunchKernelGGL(k_agg_bwd<false>, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(BWD_TPB), 0,
+                       as_stream(stream), b);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_aggregate_backward_sg(int32_t bpnet_layers, int32_t bpnet_dim, const sgn_point_tables *pt,
+                              const sgn_query_out *q, int32_t n_items, const void *d_packed, const void *d_tblob,
+                              const sgn_agg_saved *saved, const void *d_h2b, const float *d_dfs, const float *d_dalpha,
+                              const float *d_scale, const sgn_agg_deltas *deltas, void *d_db,
+                              const sgn_point_grads *grads, sgn_stream_t stream) {
+    using namespace sgn;
+    if (bpnet_layers == 0)
+        return sgn_aggregate_backward(pt, q, n_items, d_packed, d_tblob, saved, d_dfs, d_dalpha, d_scale, deltas, grads,
+                                      stream);
+    SGN_REQUIRE(bpnet_layers == 1 && (bpnet_dim == 0 || bpnet_dim == mlp::BP_DIM),
+                "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    SGN_REQUIRE(pt && q && d_packed && d_tblob && saved && deltas && grads && d_scale && d_h2b && d_db, "null argument");
+    SGN_REQUIRE(n_items >= 0, "n_items < 0");
+    SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
+    if (n_items == 0) return 0;
+    SGN_REQUIRE(d_dfs && d_dalpha && saved->h1 && saved->h2 && saved->h3, "null saved/input tensors");
+    SGN_REQUIRE(deltas->d1 && deltas->d2 && deltas->d3 && deltas->d4 && deltas->h4 && deltas->dza, "null delta outputs");
+    SGN_REQUIRE(grads->embedding && grads->color && grads->dir && grads->conf, "null gradient outputs");
+    BwdArgs b{};
+    AggArgs &a = b.a;
+    a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
+    a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
+    a.pers = nullptr; a.samp_pers = nullptr;
+    a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
+    a.samp_locw = q->samp_locw;
+    a.blob = d_packed; a.blob_bytes = mlp::total_bytes_sg(mlp::ks_bp(bpnet_dim));
+    a.blend = nullptr; a.wnorm = nullptr;
+    b.tblob = d_tblob;
+    b.sh1 = (const _Float16 *)saved->h1; b.sh2 = (const _Float16 *)saved->h2; b.sh3 = (const _Float16 *)saved->h3;
+    b.sh2b = (const _Float16 *)d_h2b; b.db = (_Float16 *)d_db;
+    b.dfs = d_dfs; b.dalpha = d_dalpha; b.scale = d_scale;
+    b.d4 = (_Float16 *)deltas->d4; b.d3 = (_Float16 *)deltas->d3; b.d2 = (_Float16 *)deltas->d2;
+    b.d1 = (_Float16 *)deltas->d1; b.h4 = (_Float16 *)deltas->h4; b.dza = deltas->dza;
+    b.g_emb = grads->embedding; b.g_color = grads->color; b.g_dir = grads->dir; b.g_conf = grads->conf;
+    b.n_items = n_items;
+    const int64_t waves = ((int64_t)n_items + 3) / 4;
+    const int64_t blocks = (waves + 3) / 4;
+    hipLaunchKernelGGL(k_agg_bwd<true>, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(BWD_TPB), 0,
+                       as_stream(stream), b);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

@@ -561,7 +561,10 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         chain_out<4, 0>(acc, actB);
         if constexpr (SAVE) {
 #pragma unroll
-            for (int s2 = 0; s2 < 8; ++s2) save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
+            for (int s2 = 0; s2 < 8; ++s2) {
+                if constexpr (KSB > 0) save_frag(a.sh2b, 256, srow0, s2, actB[s2], lane, ri.sval);
+                else save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
+            }
         }
         run_pass<V, 1, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B1, acc, inA);
         // next tile's index chain: work entry now, neighbour / ray indices one pass later
@@ -569,8 +572,11 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         chain_out<4, 1>(acc, actB);
         if constexpr (SAVE) {
 #pragma unroll
-            for (int s2 = 8; s2 < 16; ++s2) save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
-            save_frag(a.sh2, KS_L2 * 16, srow0, 16, ext, lane, ri.sval);
+            for (int s2 = 8; s2 < 16; ++s2) {
+                if constexpr (KSB > 0) save_frag(a.sh2b, 256, srow0, s2, actB[s2], lane, ri.sval);
+                else save_frag(a.sh2, KS_L2 * 16, srow0, s2, actB[s2], lane, ri.sval);
+            }
+            if constexpr (KSB == 0) save_frag(a.sh2, KS_L2 * 16, srow0, 16, ext, lane, ri.sval);
         }
         if constexpr (KSB > 0) {
             // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256 (point_aggregators.py:629-636)
@@ -584,6 +590,11 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
             chain_out<4, 0>(acc, actA);
             run_pass<V, 4, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
             chain_out<4, 1>(acc, actA);
+            if constexpr (SAVE) {  // block3.0's inputs: the block2_bpnet output + the extra channels
+#pragma unroll
+                for (int s2 = 0; s2 < 16; ++s2) save_frag(a.sh2, KS_L2 * 16, srow0, s2, actA[s2], lane, ri.sval);
+                save_frag(a.sh2, KS_L2 * 16, srow0, 16, ext, lane, ri.sval);
+            }
         }
         // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input in actB, or actA after block2_bpnet)
         auto &in3 = pick<(KSB > 0)>(actA, actB);
@@ -1223,6 +1234,75 @@ int sgn_aggregate_train_fwd(const sgn_point_tables *pt, const sgn_query_out *q, 
     int64_t wg = (S_capacity + WG_SAMPLES - 1) / WG_SAMPLES;
     hipLaunchKernelGGL((k_agg_rows<0, true>), dim3((unsigned)(wg < 256 ? wg : 256)), dim3(ROWS_TPB), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_aggregate_train_fwd_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpnet_f16,
+                               const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                               const void *d_packed, float *d_out_feat, void *d_fs, const sgn_agg_saved *saved,
+                               void *d_h2b, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    const int ksb = mlp_variant_ksb(bpnet_layers, bpnet_dim);
+    SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    if (ksb == 0)
+        return sgn_aggregate_train_fwd(pt, q, S_capacity, K, d_packed, d_out_feat, d_fs, saved, stream);
+    SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_fs && saved && d_h2b, "null argument");
+    SGN_REQUIRE(saved->x0 && saved->h1 && saved->h2 && saved->h3, "null saved-activation buffer");
+    SGN_REQUIRE(ksb <= KS_HID || (d_bpnet_f16 && ((uintptr_t)d_bpnet_f16 & 15) == 0),
+                "bpnet_dim > 0 needs the 16-byte aligned fp16 BPNet point embedding");
+    SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
+    SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
+    SGN_REQUIRE(S_capacity >= 0 && S_capacity < (1 << 27), "S_capacity out of range");
+    if (S_capacity == 0) return 0;
+    AggArgs a{};
+    a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
+    a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
+    a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
+    a.samp_locw = q->samp_locw;
+    a.blob = d_packed; a.blob_bytes = total_bytes_sg(ksb);
+    a.bpnet = (const _Float16 *)d_bpnet_f16;
+    a.feat = d_out_feat; a.fs = (_Float16 *)d_fs;
+    a.item0 = 0; a.n_items = (int32_t)S_capacity;
+    a.sx0 = (_Float16 *)saved->x0; a.sh1 = (_Float16 *)saved->h1; a.sh2 = (_Float16 *)saved->h2;
+    a.sh3 = (_Float16 *)saved->h3; a.sh2b = (_Float16 *)d_h2b;
+    const int64_t wg = (S_capacity + WG_SAMPLES - 1) / WG_SAMPLES;
+    auto kern = ksb == KS_HID ? k_agg_rows<KS_HID, true> : k_agg_rows<ks_bp(BP_DIM), true>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(ROWS_TPB), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+/* Index maps of the SG blob's block2_bpnet sections over the flat parameter vector (the 9 base
+ * layers, then block2_bpnet.0 weight [256][256 + bpnet_dim] and bias): which 3: fragments
+ * [OFF_WB, off_bb) as fp16 elements, 4: the bias (HID fp32, accumulator order). */
+int sgn_mlp_pack_index_sg(int32_t bpnet_layers, int32_t bpnet_dim, int32_t which, int32_t *out, int64_t n) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    const int ksb = mlp_variant_ksb(bpnet_layers, bpnet_dim);
+    SGN_REQUIRE(ksb > 0, "sgn_mlp_pack_index_sg: block2_bpnet variant required");
+    const int64_t want = which == 3 ? (int64_t)((off_bb(ksb) - OFF_WB) / 2) : which == 4 ? (int64_t)HID : -1;
+    SGN_REQUIRE(out && n == want, "sgn_mlp_pack_index_sg: bad map id or size");
+    static const int shape[9][2] = {{256, 284}, {256, 256}, {256, 263}, {256, 256}, {1, 256},
+                                    {128, 280}, {128, 128}, {128, 128}, {3, 128}};
+    std::vector<std::vector<float>> wi(10), bi(10);
+    std::vector<const float *> wp(10), bp(10);
+    int64_t off = 0;
+    for (int L = 0; L < 10; ++L) {
+        const int o = L < 9 ? shape[L][0] : 256, i = L < 9 ? shape[L][1] : 256 + bpnet_dim;
+        wi[L].resize((size_t)o * i);
+        for (size_t j = 0; j < wi[L].size(); ++j) wi[L][j] = (float)(off + (int64_t)j + 1);
+        off += (int64_t)wi[L].size();
+        bi[L].resize(o);
+        for (size_t j = 0; j < bi[L].size(); ++j) bi[L][j] = (float)(off + (int64_t)j + 1);
+        off += (int64_t)bi[L].size();
+        wp[L] = wi[L].data();
+        bp[L] = bi[L].data();
+    }
+    std::vector<float> e16(total_bytes_sg(ksb) / 2, 0.f), F(N_F32, 0.f), BB(HID, 0.f);
+    pack_blob<float>(ksb, bpnet_dim, wp.data(), bp.data(), e16.data(), F.data(), BB.data());
+    const float *src = which == 3 ? e16.data() + OFF_WB / 2 : BB.data();
+    for (int64_t j = 0; j < n; ++j) out[j] = (int32_t)src[j];
     return 0;
 }
 

@@ -150,10 +150,16 @@ class HipPointsVolumetricModel:
         params = PointParams(npnt.xyz, npnt.points_embeding, npnt.points_color, npnt.points_dir, npnt.points_conf,
                              self.device)
         g = lambda k, d: float(getattr(opt, k, d) if getattr(opt, k, None) is not None else d)  # noqa: E731
+        bp = npnt.bpnet_points_embedding if self.opts.bpnet_variant[1] else None
+        if self.opts.bpnet_variant[1] and bp is None:
+            # SG: BPNet's embedding arrives later (neural_points.set_bpnet_feats); the trainer is
+            # built by setup() / the first optimize_parameters once it is there
+            self.trainer = None
+            return
         self.trainer = HipTrainer(params, self.net_ray_marching.renderer.mlp_state,
                                   dataclasses.replace(self.opts, is_train=1), self.device,
                                   lr=g("lr", 5e-4), plr=g("plr", 2e-3), lr_decay_exp=g("lr_decay_exp", 0.1),
-                                  lr_decay_iters=g("lr_decay_iters", 1_000_000))
+                                  lr_decay_iters=g("lr_decay_iters", 1_000_000), bpnet=bp)
         # the renderer reads the trained tensors in place (views; the table cache follows their versions)
         n = params.xyz.shape[0]
         npnt.points_embeding = params.points_embeding.detach().view(1, n, -1)
@@ -212,11 +218,17 @@ class HipPointsVolumetricModel:
     def grow_points(self, add_xyz, add_embedding, add_color, add_dir, add_conf, add_label=None, **unused):
         """neural_points.py:546-572: append points (embedding/colour/dir/conf given as [M, C]).
         Labels are appended when both sides have them (:550); points_feats is kept as it is,
-        as the reference keeps it."""
+        as the reference keeps it.  The BPNet embedding gets zero rows for the new points (the
+        reference leaves it at the old length, which its index_select at neural_points.py:972
+        would then overrun)."""
         self._sync_weights()
         p = self.neural_points
         f = lambda t, c: torch.as_tensor(t).to(self.device, torch.float32).reshape(1, -1, c)  # noqa: E731
         label = p.points_label
+        bp = p.bpnet_points_embedding
+        if bp is not None:
+            m = torch.as_tensor(add_xyz).reshape(-1, 3).shape[0]
+            bp = torch.cat([bp, bp.new_zeros(1, m, bp.shape[-1])], 1)
         if label is not None and add_label is not None:
             label = torch.cat([label, torch.as_tensor(add_label).to(label.device, label.dtype).reshape(-1, 1)], 0)
         elif label is not None:
@@ -226,7 +238,7 @@ class HipPointsVolumetricModel:
             torch.cat([p.points_embeding, f(add_embedding, p.points_embeding.shape[-1])], 1),
             torch.cat([p.points_color, f(add_color, 3)], 1), torch.cat([p.points_dir, f(add_dir, 3)], 1),
             torch.cat([p.points_conf, f(add_conf, 1)], 1), self.device, points_feats=p.points_feats,
-            points_label=label)
+            points_label=label, bpnet_points_embedding=bp)
         self.net_ray_marching.neural_points = self.neural_points
         if self.is_train and getattr(self, "trainer", None) is not None:
             self.setup_optimizer(self.opt)
@@ -272,12 +284,20 @@ class HipPointsVolumetricModel:
         near, far = (float(torch.as_tensor(x).reshape(-1)[0]) for x in (near, far))
         gt = inp["gt_image"].reshape(-1, 3).to(self.device, torch.float32)
         args = (inp["campos"], inp["camrotc2w"], inp["raydir"], near, far, gt)
+        labels = None
+        if self.opts.semantic_guidance == 1:  # neural_points.py:771-785, as the renderer passes them
+            pl = self.neural_points.points_label
+            if pl is None or inp.get("pixel_label") is None:
+                raise ValueError("semantic_guidance = 1 needs neural_points.points_label and inputs['pixel_label']")
+            labels = (pl.reshape(-1).to(self.device, torch.int32).contiguous(),
+                      torch.as_tensor(inp["pixel_label"]).reshape(-1).to(self.device, torch.int32).contiguous(),
+                      inp.get("seconds"))
         tr.step_count = int(total_steps)
         if backward:
-            parts, full, ray_mask = tr.step(*args)
+            parts, full, ray_mask = tr.step(*args, labels=labels)
             self._weights_dirty = True
         else:
-            parts, full, ray_mask = tr.backward(*args)
+            parts, full, ray_mask = tr.backward(*args, labels=labels)
         for k, v in parts.items():
             setattr(self, "loss_" + k, v)
         self.output = {"coarse_raycolor": full[None], "ray_mask": ray_mask[None].to(torch.int8)}

@@ -36,19 +36,21 @@ from . import _lib
 from .opts import HotPathOpts
 from .train import (PointParams, _allreduce_buckets, _allreduce_point_rows, _pe, composite_losses, gather_counts,
                     touched_rows)
-from .weights import LAYERS, strip_prefix
+from .weights import BPNET, LAYERS, layers_for, strip_prefix
 
 N_F32 = 2056
 
 
 class FlatMLP(nn.Module):
-    """The 9 viewmlp layers in one flat fp32 parameter: per layer weight (row-major) then bias."""
+    """The 9 viewmlp layers (+ SG's block2_bpnet.0 after them) in one flat fp32 parameter: per
+    layer weight (row-major) then bias."""
 
-    def __init__(self, state, device):
+    def __init__(self, state, device, layers=LAYERS):
         super().__init__()
         state = strip_prefix(state)
+        self.layers = list(layers)
         parts, self.slices, off = [], {}, 0
-        for name, o, i, _ in LAYERS:
+        for name, o, i, _ in self.layers:
             parts += [torch.as_tensor(state[name + ".weight"]).float().reshape(-1),
                       torch.as_tensor(state[name + ".bias"]).float().reshape(-1)]
             self.slices[name] = (off, o, i)
@@ -65,30 +67,40 @@ class FlatMLP(nn.Module):
 
     def state(self):
         out = {}
-        for name, *_ in LAYERS:
+        for name, *_ in self.layers:
             out[name + ".weight"] = self.w(name).detach().clone()
             out[name + ".bias"] = self.b(name).detach().clone()
         return out
 
 
 class _Packer:
-    """Device-side re-packing of the forward and transposed MFMA blobs from the flat weights."""
+    """Device-side re-packing of the forward and transposed MFMA blobs from the flat weights
+    (variant (1, bpnet_dim): the SG blob, block2_bpnet.0's fragments and bias after the base)."""
 
-    def __init__(self, device):
+    def __init__(self, device, variant=(0, 0)):
         L = _lib.lib()
-        self.total = int(L.sgn_mlp_packed_bytes())
+        self.variant = variant
+        self.base = int(L.sgn_mlp_packed_bytes())
+        self.total = int(L.sgn_mlp_packed_bytes_sg(*variant)) if variant != (0, 0) else self.base
         self.off_f32 = int(L.sgn_mlp_section(0))
         self.off_split = int(L.sgn_mlp_section(1))
         self.tbytes = int(L.sgn_train_tblob_bytes())
-        maps = []
-        for which, n in ((0, self.off_f32 // 2), (1, N_F32), (2, (self.total - self.off_split) // 2)):
+
+        def imap(fn, name, *args, n):
             a = (ctypes.c_int32 * n)()
-            _lib.check(L.sgn_mlp_pack_index(which, a, n), "sgn_mlp_pack_index")
-            maps.append(torch.frombuffer(bytearray(a), dtype=torch.int32).long())
-        a = (ctypes.c_int32 * (self.tbytes // 2))()
-        _lib.check(L.sgn_train_pack_index(a, self.tbytes // 2), "sgn_train_pack_index")
-        maps.append(torch.frombuffer(bytearray(a), dtype=torch.int32).long())
-        self.i16, self.i32, self.isp, self.it = (m.to(device) for m in maps)
+            _lib.check(fn(*args, a, n), name)
+            return torch.frombuffer(bytearray(a), dtype=torch.int32).long().to(device)
+        self.i16 = imap(L.sgn_mlp_pack_index, "sgn_mlp_pack_index", 0, n=self.off_f32 // 2)
+        self.i32 = imap(L.sgn_mlp_pack_index, "sgn_mlp_pack_index", 1, n=N_F32)
+        self.isp = imap(L.sgn_mlp_pack_index, "sgn_mlp_pack_index", 2, n=(self.base - self.off_split) // 2)
+        if variant != (0, 0):
+            self.off_bb = self.total - 4 * 256                   # block2_bpnet bias (fp32, acc order)
+            self.iwb = imap(L.sgn_mlp_pack_index_sg, "sgn_mlp_pack_index_sg", *variant, 3,
+                            n=(self.off_bb - self.base) // 2)
+            self.ibb = imap(L.sgn_mlp_pack_index_sg, "sgn_mlp_pack_index_sg", *variant, 4, n=256)
+            self.it = imap(L.sgn_train_pack_index_sg, "sgn_train_pack_index_sg", variant[1], n=self.tbytes // 2)
+        else:
+            self.it = imap(L.sgn_train_pack_index, "sgn_train_pack_index", n=self.tbytes // 2)
         self.blob = torch.zeros(self.total, dtype=torch.uint8, device=device)
         self.tblob = torch.zeros(self.tbytes, dtype=torch.uint8, device=device)
 
@@ -96,7 +108,10 @@ class _Packer:
         ext = torch.cat([flat.detach().new_zeros(1), flat.detach()])
         self.blob[:self.off_f32].view(torch.float16).copy_(ext[self.i16])
         self.blob[self.off_f32:self.off_f32 + 4 * N_F32].view(torch.float32).copy_(ext[self.i32])
-        self.blob[self.off_split:].view(torch.float16).copy_(ext[self.isp])
+        self.blob[self.off_split:self.base].view(torch.float16).copy_(ext[self.isp])
+        if self.variant != (0, 0):
+            self.blob[self.base:self.off_bb].view(torch.float16).copy_(ext[self.iwb])
+            self.blob[self.off_bb:].view(torch.float32).copy_(ext[self.ibb])
         self.tblob.view(torch.float16).copy_(ext[self.it])
         return self.blob, self.tblob
 
@@ -200,13 +215,23 @@ class HipTrainer:
     """One data-parallel training step per call on the HIP path (config 5)."""
 
     def __init__(self, points: PointParams, mlp_state, opts: HotPathOpts, device, lr=5e-4, plr=2e-3,
-                 lr_decay_exp=0.1, lr_decay_iters=1_000_000, bucket_mb=64, querier=None):
+                 lr_decay_exp=0.1, lr_decay_iters=1_000_000, bucket_mb=64, querier=None, bpnet=None):
+        """bpnet: the SG variant's BPNet point embedding [N, 96] (fp32, detached: it is an input,
+        neural_points.py:662), needed when opts select block2_bpnet with predict_semantic = 1."""
         self.device = torch.device(device)
         self.opts = opts.check_supported()
-        if opts.bpnet_variant != (0, 0):
-            raise NotImplementedError("the HIP training path is built for the base viewmlp (no block2_bpnet)")
+        self.variant = tuple(opts.bpnet_variant)
+        self.sg = self.variant != (0, 0)
         self.points = points
-        self.mlp = FlatMLP(mlp_state, self.device)
+        self.mlp = FlatMLP(mlp_state, self.device, layers_for(*self.variant))
+        self.bpnet16 = None
+        if self.variant[1]:
+            if bpnet is None:
+                raise ValueError("block2_bpnet with predict_semantic = 1 needs the BPNet point embedding")
+            e = torch.as_tensor(bpnet).detach().to(self.device, torch.float32).reshape(-1, self.variant[1]).contiguous()
+            self.bpnet16 = torch.empty(e.shape, dtype=torch.float16, device=self.device)
+            _lib.check(_lib.lib().sgn_bpnet_pack(_lib.ptr(e), e.shape[0], e.shape[1], _lib.ptr(self.bpnet16),
+                                                 _lib.stream_handle()), "sgn_bpnet_pack")
         self.point_params = [points.points_embeding, points.points_color, points.points_dir, points.points_conf]
         # the reference's two Adam groups (mvs_points_volumetric_model.py:100-108); fused: one
         # kernel per group for the dense 47 M-element point update instead of the foreach chain
@@ -222,7 +247,7 @@ class HipTrainer:
         self.step_count = 0
         self.bucket_elems = bucket_mb * (1 << 20) // 4
         self.querier = querier
-        self.packer = _Packer(self.device)
+        self.packer = _Packer(self.device, self.variant)
         # stored column p -> reference index; inverses: reference index -> stored column
         self.map_chain = _colmap(0, 256, self.device)
         self.map_x0 = _colmap(1, 288, self.device)
@@ -262,13 +287,24 @@ class HipTrainer:
             self.h3 = torch.empty(rows, 256, **h)
             self.d = [torch.empty(rows, 256, **h) for _ in range(4)]  # d1..d4
             self.h4 = torch.empty(rows, 256, **h)
+            if self.sg:  # block2_bpnet inputs h and deltas
+                self.h2b = torch.empty(rows, 256, **h)
+                self.db = torch.empty(rows, 256, **h)
             self.dza = torch.empty(rows, dtype=torch.float32, device=dev)
             self._cap = cap
 
-    def _query(self, campos, raydir, near, far):
+    def _query(self, campos, raydir, near, far, labels=None):
         if self.querier is None:
             from .querier import LightningFastQuerier
             self.querier = LightningFastQuerier(self.device, self.opts)
+        if self.opts.semantic_guidance:
+            if labels is None:
+                raise ValueError("semantic_guidance = 1: pass labels=(point_labels [N], ray_labels [R], seconds)")
+            pl, rl, sec = labels
+            return self.querier.query_samples(self.points.xyz, campos, raydir, near, far,
+                                              torch.as_tensor(pl).to(self.device, torch.int32).reshape(-1).contiguous(),
+                                              torch.as_tensor(rl).to(self.device, torch.int32).reshape(-1).contiguous(),
+                                              sec)
         return self.querier.query_samples(self.points.xyz, campos, raydir, near, far)
 
     def _tables(self, campos, rot, raydir):
@@ -308,8 +344,9 @@ class HipTrainer:
         return torch.sigmoid(c) * (1 + 2 * 0.001) - 0.001
 
     # -- one step ------------------------------------------------------------------------
-    def backward(self, campos, rot, raydir, near, far, gt):
-        """Forward + backward + gradient all-reduce (no parameter update).
+    def backward(self, campos, rot, raydir, near, far, gt, labels=None):
+        """Forward + backward + gradient all-reduce (no parameter update).  labels: (point_labels,
+        ray_labels, seconds) for the semantic-guided query (semantic_guidance = 1).
         Returns (loss parts, rendered colour [R,3], ray_mask [R])."""
         o = self.opts
         dev = self.device
@@ -317,7 +354,7 @@ class HipTrainer:
         rot = rot.reshape(3, 3).to(dev, torch.float32).contiguous()
         raydir = raydir.reshape(-1, 3).to(dev, torch.float32).contiguous()
         R = raydir.shape[0]
-        q = self._query(campos, raydir, near, far)
+        q = self._query(campos, raydir, near, far, labels)
         # work that does not depend on the query is queued before the step's one host sync, so
         # the GPU runs it while the host waits
         blob, tblob = self.packer.pack(self.mlp.flat)
@@ -344,7 +381,12 @@ class HipTrainer:
         pt = self._tables(campos, rot, raydir)
         qo = q.abi()
         saved = _lib.AggSaved(self.x0.data_ptr(), self.h1.data_ptr(), self.h2.data_ptr(), self.h3.data_ptr())
-        if n > 0:
+        if n > 0 and self.sg:
+            _lib.check(L.sgn_aggregate_train_fwd_sg(*self.variant, _lib.ptr(self.bpnet16), ctypes.byref(pt),
+                                                    ctypes.byref(qo), n, o.K, _lib.ptr(blob), _lib.ptr(self.feat),
+                                                    _lib.ptr(self.fs), ctypes.byref(saved), _lib.ptr(self.h2b), st),
+                       "sgn_aggregate_train_fwd_sg")
+        elif n > 0:
             _lib.check(L.sgn_aggregate_train_fwd(ctypes.byref(pt), ctypes.byref(qo), n, o.K, _lib.ptr(blob),
                                                  _lib.ptr(self.feat), _lib.ptr(self.fs), ctypes.byref(saved), st),
                        "sgn_aggregate_train_fwd")
@@ -378,11 +420,18 @@ class HipTrainer:
             P = self.points
             grads = _lib.PointGrads(P.points_embeding.grad.data_ptr(), P.points_color.grad.data_ptr(),
                                     P.points_dir.grad.data_ptr(), P.points_conf.grad.data_ptr())
-            _lib.check(L.sgn_aggregate_backward(ctypes.byref(pt), ctypes.byref(qo), n, _lib.ptr(blob), _lib.ptr(tblob),
-                                                ctypes.byref(saved), _lib.ptr(dfs), _lib.ptr(dal), _lib.ptr(scale),
-                                                ctypes.byref(deltas), ctypes.byref(grads), st),
-                       "sgn_aggregate_backward")
-            self._weight_grads(n * 8, scale)
+            if self.sg:
+                _lib.check(L.sgn_aggregate_backward_sg(*self.variant, ctypes.byref(pt), ctypes.byref(qo), n,
+                                                       _lib.ptr(blob), _lib.ptr(tblob), ctypes.byref(saved),
+                                                       _lib.ptr(self.h2b), _lib.ptr(dfs), _lib.ptr(dal),
+                                                       _lib.ptr(scale), ctypes.byref(deltas), _lib.ptr(self.db),
+                                                       ctypes.byref(grads), st), "sgn_aggregate_backward_sg")
+            else:
+                _lib.check(L.sgn_aggregate_backward(ctypes.byref(pt), ctypes.byref(qo), n, _lib.ptr(blob),
+                                                    _lib.ptr(tblob), ctypes.byref(saved), _lib.ptr(dfs), _lib.ptr(dal),
+                                                    _lib.ptr(scale), ctypes.byref(deltas), ctypes.byref(grads), st),
+                           "sgn_aggregate_backward")
+            self._weight_grads(n * 8, scale, q)
         self.allreduce_grads([self.mlp.flat])
         if dp:
             _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
@@ -482,7 +531,7 @@ class HipTrainer:
                 "full": out["full"].clone(), "ray_mask": out["ray_mask"].clone(),
                 "dfs": out["dfs"], "dal": out["dal"], "scale": out["scale"]}
 
-    def _weight_grads(self, rows, scale):
+    def _weight_grads(self, rows, scale, q=None):
         """dW_l = delta_l^T x_l (fp16 GEMM, fp32 out), db_l = sum delta_l, unpermuted."""
         m = self.mlp
         g = m.flat.grad
@@ -491,16 +540,37 @@ class HipTrainer:
         rp = ((rows + 1023) // 1024) * 1024   # rows padded to the split-K batch (buffers are)
         chunk = max(DW_CHUNK, -(-rp // 512))  # at most 512 batches (no ragged tail up to 512 * DW_CHUNK rows)
         if rp > rows:
-            for t in self.d + [self.x0, self.h1, self.h2, self.h3]:
+            for t in self.d + [self.x0, self.h1, self.h2, self.h3] + ([self.h2b, self.db] if self.sg else []):
                 t[rows:rp].zero_()             # stale tails must not reach the GEMM (0 * NaN)
-        # db_l = column sums of the four delta tiles, in one pair of launches
+        # db_l = column sums of the delta tiles (+ block2_bpnet's for SG), in one pair of launches
+        nd = 5 if self.sg else 4
         if not hasattr(self, "_cs_out"):
-            self._cs_ws = torch.empty(int(_lib.lib().sgn_colsum_workspace_bytes(4)) // 4, dtype=torch.float32,
+            self._cs_ws = torch.empty(int(_lib.lib().sgn_colsum_workspace_bytes(nd)) // 4, dtype=torch.float32,
                                       device=self.device)
-            self._cs_out = torch.empty(4, 256, dtype=torch.float32, device=self.device)
-        ds = (ctypes.c_void_p * 4)(*(t.data_ptr() for t in (self.d[3], self.d[2], self.d[1], self.d[0])))
-        _lib.check(_lib.lib().sgn_colsum_f16(4, ds, rows, 256, _lib.ptr(self._cs_ws), _lib.ptr(self._cs_out),
+            self._cs_out = torch.empty(nd, 256, dtype=torch.float32, device=self.device)
+        dl = [self.d[3], self.d[2], self.d[1], self.d[0]] + ([self.db] if self.sg else [])
+        ds = (ctypes.c_void_p * nd)(*(t.data_ptr() for t in dl))
+        _lib.check(_lib.lib().sgn_colsum_f16(nd, ds, rows, 256, _lib.ptr(self._cs_ws), _lib.ptr(self._cs_out),
                                              _lib.stream_handle()), "sgn_colsum_f16")
+        if self.sg:
+            # block2_bpnet.0: x = [h (chain order) | the row's BPNet embedding (natural order)]
+            x = self.h2b[:rp]
+            if self.variant[1]:
+                item = torch.arange(rp, device=self.device) // 8
+                ok = item < rows // 8
+                s_of = q.work[torch.where(ok, item, 0)].long()
+                pid = q.pidx[s_of * 8 + (torch.arange(rp, device=self.device) % 8)].long()
+                bp = self.bpnet16[torch.clamp(pid, min=0)]
+                bp = torch.where((ok & (pid >= 0))[:, None], bp, torch.zeros((), dtype=bp.dtype, device=bp.device))
+                x = torch.cat([x, bp], dim=1)
+            G = _gemm_rows_f32(self.db[:rp], x, chunk)
+            fi = self._flat_maps.get(BPNET)
+            if fi is None:
+                ix = torch.cat([self.inv_chain, 256 + torch.arange(self.variant[1], device=self.device)])
+                fi = (iu[:, None] * x.shape[1] + ix[None, :]).reshape(-1)
+                self._flat_maps[BPNET] = fi
+            m.w(BPNET, g).addcmul_(G.view(-1).index_select(0, fi).view(m.w(BPNET, g).shape), inv)
+            m.b(BPNET, g).addcmul_(self._cs_out[4].index_select(0, iu), inv)
         for li, (name, d, x, ix) in enumerate((("block3.2", self.d[3], self.h3, self.inv_chain),
                                                ("block3.0", self.d[2], self.h2, self.inv_h2),
                                                ("block1.2", self.d[1], self.h1, self.inv_chain),
@@ -536,8 +606,8 @@ class HipTrainer:
         self._pts_grad_clean = isinstance(self.opt_pts, PointAdam) and self.opt_pts.zero_grad_in_step
         self.step_count += 1
 
-    def step(self, campos, rot, raydir, near, far, gt):
-        out = self.backward(campos, rot, raydir, near, far, gt)
+    def step(self, campos, rot, raydir, near, far, gt, labels=None):
+        out = self.backward(campos, rot, raydir, near, far, gt, labels)
         self.apply()
         return out
 
@@ -550,7 +620,7 @@ def grads_named(trainer: HipTrainer):
     m = trainer.mlp
     g = m.flat.grad
     out = {}
-    for name, *_ in LAYERS:
+    for name, *_ in m.layers:
         out[name + ".weight"] = m.w(name, g).detach().clone()
         out[name + ".bias"] = m.b(name, g).detach().clone()
     P = trainer.points
