@@ -92,25 +92,33 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
     warmup = args.warmup if warmup is None else warmup
     from sgnerf_amd.train import PointParams, Trainer
     from sgnerf_amd.train_hip import HipTrainer
-    o = HotPathOpts(SR=24, is_train=1)
+    sg = dict(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1) if args.sg else {}
+    if args.sg and args.train_torch:
+        raise SystemExit("--train-torch covers the base viewmlp only")
+    o = HotPathOpts(SR=24, is_train=1, **sg)
     pc = scene.synth_room(args.points, seed=0)
-    mlp = init_mlp(0, bias_std=0.01)
+    if args.sg:
+        pc = scene.with_semantics(pc, seed=1, n_classes=20, cell=0.5)
+    mlp = init_mlp(0, bias_std=0.01, bpnet_layers=1 if args.sg else 0, bpnet_dim=96 if args.sg else 0)
     mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
     points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, dev)
-    tr = (Trainer if args.train_torch else HipTrainer)(points, mlp, o, dev)
+    tr = Trainer(points, mlp, o, dev) if args.train_torch else HipTrainer(points, mlp, o, dev, bpnet=pc.bpnet)
     g = torch.Generator().manual_seed(1 + rank)
     n_steps = warmup + steps
     batches = []
+    labels = [None] * n_steps
     for i in range(n_steps):
         v = pose_view(int(torch.randint(0, 120, (1,), generator=g)), args.h, args.w)
         idx = torch.randint(0, args.h * args.w, (args.train_rays,), generator=g)
         gt = torch.rand(args.train_rays, 3, generator=g)
         batches.append(tuple(x.to(dev) for x in (torch.from_numpy(v.campos), torch.from_numpy(v.camrotc2w),
                                                    torch.from_numpy(v.raydir)[idx], gt)))
+        if args.sg:   # ray labels: the first neighbour's label of each ray (as render_run), untimed
+            labels[i] = _ray_labels(dev, o, pc, batches[i][0], batches[i][2], 0.1, 8.0)
     tr.querier = None
     for i in range(warmup):
         c, r_, d, gt = batches[i]
-        tr.step(c, r_, d, 0.1, 8.0, gt)
+        tr.step(c, r_, d, 0.1, 8.0, gt, **_lab(labels[i]))
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
@@ -119,7 +127,7 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
     losses = []
     for i in range(warmup, n_steps):
         c, r_, d, gt = batches[i]
-        parts, _, _ = tr.step(c, r_, d, 0.1, 8.0, gt)
+        parts, _, _ = tr.step(c, r_, d, 0.1, 8.0, gt, **_lab(labels[i]))
         losses.append(parts["total"])
     torch.cuda.synchronize()
     if dist:
@@ -137,11 +145,36 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
                                   f"{args.points} neural points, HIP query + "
                                   + ("torch autograd" if args.train_torch else
                                      "HIP MFMA row-MLP forward/backward + torch colour/composite autograd")
+                                  + (" (SG-NeRF variant: semantic-guided kNN, block2_bpnet 352->256)" if args.sg else "")
                                   + " + RCCL all-reduce",
                       "parallelism": f"dp{world}"},
            "final_loss": float(torch.stack(losses).mean().item()),
            "graph_captures": int(getattr(tr, "graph_captures", 0))}   # loss-stage captures, warm-up included
     return res
+
+
+def _lab(labels):
+    return {} if labels is None else {"labels": labels}
+
+
+def _ray_labels(dev, o, pc, campos, raydir, near, far):
+    """SG stand-in for BPNet's per-pixel labels: the label of the first neighbour of each ray's
+    first occupied sample under the plain query; (point_labels, ray_labels, seconds)."""
+    from sgnerf_amd.querier import LightningFastQuerier
+    import dataclasses
+    qr = LightningFastQuerier(dev, dataclasses.replace(o, semantic_guidance=0))
+    xyz = torch.from_numpy(pc.xyz).to(dev)
+    q = qr.query_samples(xyz, campos, raydir, near, far)
+    S, R, K = q.n_samples(), raydir.shape[0], o.K
+    pl = torch.from_numpy(pc.labels).to(dev)
+    sr = q.samp_ray[:S].long()
+    ok = q.samp_nnb[:S] > 0
+    first = torch.full((R,), S, dtype=torch.int64, device=dev)
+    first.scatter_reduce_(0, sr[ok], torch.arange(S, device=dev)[ok], reduce="amin")
+    has = first < S
+    rl = torch.zeros(R, dtype=torch.int32, device=dev)
+    rl[has] = pl[q.pidx[first[has] * K].long()]
+    return pl, rl.contiguous(), 12
 
 
 def lego_pose_view(i, h, w, n_poses=120):
