@@ -107,6 +107,13 @@ struct AggArgs {
     // packed point records of the fp32 16x16 kernels (k_point_proj16 writes them beside P):
     // 64 B per point = {x, y, z, conf}, {r, g, b, 0}, {dx, dy, dz, 0}, {0}; one cache line per row
     const float *rec;
+    // paired sample slots of k_rows16 (k_pair_slots): per 8-row half the row table
+    // rows[8 slot + kk] = s * 8 + k (-1: idle row) and the entry {A item | nA << 28,
+    // B item | nB << 28, A sample, B sample} (items relative to item0); slot_n[0] = slots
+    const int32_t *rows;
+    const int4 *slots;
+    const int32_t *slot_n;
+    float *fs_scratch;  // 1 KiB row the stores of a missing segment go to
 };
 
 // training save: one 16-byte fragment of a 32-row tile -> [rows][C] (C multiple of 16)
@@ -250,6 +257,7 @@ struct RowIn {
 struct RowIdx {
     int s, pid, ray;
     bool sval;
+    bool a = true;  // k_rows16: the row belongs to its half's sample A (rows 0..nA-1)
 };
 
 __device__ __forceinline__ RowIdx row_index(const AggArgs &a, int item, int end, int lane) {

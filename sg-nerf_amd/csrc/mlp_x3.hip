@@ -1045,15 +1045,141 @@ __device__ __forceinline__ Rec16 load_rec16(const AggArgs &a, const RowIdx &ix) 
     r.cf = m ? q0[3] : 0.f;
     return r;
 }
-// vmcnt allowances of k_rows16's boundaries (chunk_enter VM): block3.2 ends chunk 0 with the next
-// tile's record (REC16_LOADS loads); after block3.2 come the next tile's 16 P loads and the
-// epilogue's two unconditional f_s stores, all younger than block1.0's DMA
+// vmcnt allowances of k_rows16's boundaries (chunk_enter VM): block3.2 ends chunk 0 with the slot
+// entry load and then the next tile's record (REC16_LOADS loads, the youngest); after block3.2 come
+// the next tile's 16 P loads and the epilogue's four unconditional f_s stores (two per segment),
+// all younger than block1.0's DMA
 struct VmL3 {
     static constexpr int vm(int c) { return c == 1 ? REC16_LOADS : 0; }
 };
 struct VmL0 {
-    static constexpr int vm(int) { return 16 + 2; }
+    static constexpr int vm(int) { return 16 + 4; }
 };
+
+// ---- paired samples: k_rows16's 8-row halves ----------------------------------------------------
+// A work item with n < 8 valid neighbours (a prefix of its K slots, KBuf) leaves 8 - n rows of its
+// half idle: 11 % of the rows at config 2, where 21 % of the samples have 1..7 neighbours, about
+// evenly spread over 1..7.  Two samples whose counts sum to <= 8 share one half: sample A on rows
+// 0..nA-1, sample B on rows oB..oB+nB-1, oB = max(nA, 4), so B never spans the two lane groups of
+// 4 rows the K-blend chains run in (the K-blend, the weight normalisation and alpha are then
+// two-segment sums with the same bits as for a sample alone, see k_rows16).  Per 1024 consecutive work items (neighbours in the work list
+// are neighbours in the frame, so the P gathers keep their locality) the items are ranked per count
+// (stable), then paired 7+1, 6+2, 5+3, 4+4 in rank order and the leftover 1..4s consecutively;
+// 8s and unpaired 5..7s run alone.  Writes per slot (half) the row table rows[8 slot + kk] =
+// s * 8 + k (-1: idle row; s * 8 + k is the pidx index of the row) and the entry
+// {A item | nA << 28, B item | nB << 28, A sample, B sample} (items relative to item0, < 2^28);
+// slots of a block are contiguous, blocks in atomic order (a sample's values depend only on its
+// block, so results do not depend on that order).
+constexpr int PAIR_TPB = 1024, PAIR_NW = PAIR_TPB / 64;
+__global__ __launch_bounds__(PAIR_TPB) void k_pair_slots(const int32_t *__restrict__ counters,
+                                                         const int32_t *__restrict__ work,
+                                                         const int32_t *__restrict__ nnb, int32_t item0,
+                                                         int32_t n_items, int32_t *__restrict__ rows,
+                                                         int4 *__restrict__ slots, int32_t *__restrict__ slot_n) {
+    __shared__ int wc[PAIR_NW][9];
+    __shared__ int16_t blist[9][PAIR_TPB];  // count -> rank -> thread
+    __shared__ int ss[PAIR_TPB];            // thread -> sample
+    __shared__ int8_t sc[PAIR_TPB];         // thread -> count
+    __shared__ int wl[PAIR_NW], sbase;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int end = min(counters[1], item0 + n_items);
+    const int rel0 = blockIdx.x * PAIR_TPB;
+    if (item0 + rel0 >= end) return;  // the grid covers the capacity, the work list is shorter
+    const int item = item0 + rel0 + tid;
+    const bool ok = item < end;
+    const int s = ok ? work[item] : 0;
+    const int c = ok ? min(max(nnb[s], 1), 8) : 0;
+    ss[tid] = s;
+    sc[tid] = (int8_t)c;
+    const uint64_t below = (1ull << lane) - 1ull;
+    int rank = 0;
+#pragma unroll
+    for (int b = 1; b <= 8; ++b) {
+        const uint64_t m = __ballot(c == b);
+        if (c == b) rank = __popcll(m & below);
+        if (lane == 0) wc[wv][b] = __popcll(m);
+    }
+    __syncthreads();
+    int n[9];
+#pragma unroll
+    for (int b = 1; b <= 8; ++b) {
+        int tot = 0;
+        for (int q = 0; q < PAIR_NW; ++q) {
+            const int v = wc[q][b];
+            if (q < wv && b == c) rank += v;
+            tot += v;
+        }
+        n[b] = tot;
+    }
+    if (ok) blist[c][rank] = (int16_t)tid;
+    __syncthreads();
+    const int p17 = min(n[1], n[7]), p26 = min(n[2], n[6]), p35 = min(n[3], n[5]), p44 = n[4] / 2;
+    const int L1 = n[1] - p17, L2 = n[2] - p26, L3 = n[3] - p35, L4 = n[4] - 2 * p44;
+    const int Lt = L1 + L2 + L3 + L4;
+    auto left = [&](int j) -> int {  // leftover j (counts 1..4 in count, rank order) -> thread
+        if (j < L1) return blist[1][p17 + j];
+        j -= L1;
+        if (j < L2) return blist[2][p26 + j];
+        j -= L2;
+        if (j < L3) return blist[3][p35 + j];
+        return blist[4][2 * p44 + j - L3];
+    };
+    bool lead = ok;
+    int partner = -1;
+    if (ok && c >= 5 && c <= 7) {
+        const int pc = c == 7 ? p17 : c == 6 ? p26 : p35;
+        if (rank < pc) partner = blist[8 - c][rank];
+    } else if (ok && c <= 4) {
+        const int pc = c == 1 ? p17 : c == 2 ? p26 : c == 3 ? p35 : 2 * p44;
+        if (rank < pc) {
+            if (c < 4 || (rank & 1)) lead = false;  // the 7, 6, 5 (or the even-ranked 4) leads
+            else partner = blist[4][rank + 1];
+        } else {
+            const int j = (c == 1 ? 0 : c == 2 ? L1 : c == 3 ? L1 + L2 : L1 + L2 + L3) + rank - pc;
+            if (j & 1) lead = false;
+            else if (j + 1 < Lt) partner = left(j + 1);
+        }
+    }
+#ifdef SGN_NO_PAIR  // experiment only: every sample alone in its half
+    lead = ok;
+    partner = -1;
+#endif
+    const uint64_t lm = __ballot(lead);
+    int idx = __popcll(lm & below);
+    if (lane == 0) wl[wv] = __popcll(lm);
+    __syncthreads();
+    if (tid == 0) {
+        int tot = 0;
+        for (int q = 0; q < PAIR_NW; ++q) tot += wl[q];
+        sbase = tot ? atomicAdd(slot_n, tot) : 0;
+    }
+    for (int q = 0; q < wv; ++q) idx += wl[q];
+    __syncthreads();
+    if (!lead) return;
+    const int slot = sbase + idx;
+    const int nb = partner >= 0 ? sc[partner] : 0, sb = partner >= 0 ? ss[partner] : 0;
+    int r8[8];
+    const int ob = c > 4 ? c : 4;  // B's first row: never across the 4-row lane-group boundary
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r8[k] = k < c ? s * 8 + k : (k >= ob && k < ob + nb ? sb * 8 + (k - ob) : -1);
+    int4 *rp = (int4 *)(rows + (int64_t)slot * 8);
+    rp[0] = make_int4(r8[0], r8[1], r8[2], r8[3]);
+    rp[1] = make_int4(r8[4], r8[5], r8[6], r8[7]);
+    slots[slot] = make_int4((int)((uint32_t)(rel0 + tid) | ((uint32_t)c << 28)),
+                            partner >= 0 ? (int)((uint32_t)(rel0 + partner) | ((uint32_t)nb << 28)) : 0, s, sb);
+}
+
+// the lane's row of slot `slot` (half of the wave), row kk of the half: rows table -> pidx index v
+__device__ __forceinline__ RowIdx row_index16(const AggArgs &a, int slot, int nslots, int kk) {
+    RowIdx x;
+    const int v = slot < nslots ? a.rows[(int64_t)slot * 8 + kk] : -1;
+    x.sval = v >= 0;
+    x.s = x.sval ? v >> 3 : 0;
+    x.a = (v & 7) == kk;  // B rows sit nA rows after their k
+    x.pid = x.sval ? a.pidx[v] : -1;
+    x.ray = x.sval ? a.samp_ray[x.s] : 0;
+    return x;
+}
 
 // dists (point_aggregators.py:917-925): d[0..2] world offsets, d[3..5] pers-space terms; the
 // linear-kernel weight normalised over the sample's 8 rows times the clamped conf (:946-953)
@@ -1061,7 +1187,8 @@ struct Row16 {
     float d[6];
     float wgt, wn;
 };
-__device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, const Rec16 &rc, bool m) {
+__device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, const Rec16 &rc, bool m, bool isA,
+                                            int nA, int kk, int lane) {
     Row16 o;
     const float dwx = __fsub_rn(rc.p[0], rc.l[0]), dwy = __fsub_rn(rc.p[1], rc.l[1]), dwz = __fsub_rn(rc.p[2], rc.l[2]);
     o.d[0] = m ? dwx : 0.f;
@@ -1083,7 +1210,15 @@ __device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, co
         const float n2 = __fadd_rn(__fadd_rn(__fmul_rn(dwx, dwx), __fmul_rn(dwy, dwy)), __fmul_rn(dwz, dwz));
         w = 1.f / fmaxf(sqrtf(n2), 1e-6f);
     }
-    const float wsum = dpp_sum8(w);
+    // normalised over the rows of the row's own sample (A: rows 0..nA-1 of the half, B: rows
+    // oB = max(nA, 4) ..; idle rows carry w = 0).  B's weights are first moved down to rows 0..nB-1, so
+    // both samples sum exactly as they would alone in a half: a sample's values do not depend on its
+    // partner.
+    const int oB = nA > 4 ? nA : 4;
+    const float wb0 = isA ? 0.f : w;
+    const float wbs = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(((lane + oB) & 63) * 4, __builtin_bit_cast(int, wb0)));
+    const float wsa = dpp_sum8(isA ? w : 0.f), wsb = dpp_sum8(kk + oB < 8 ? wbs : 0.f);
+    const float wsum = isA ? wsa : wsb;
     w = w / fmaxf(wsum, 1e-8f);
     o.wn = w;
     o.wgt = w * fminf(fmaxf(rc.cf, 1e-4f), 1.f);
@@ -1123,8 +1258,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4, r = lane & 15, kk = lane & 7, sc = r >> 3;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwork = a.counters[1];
-    const int end = min(nwork, a.item0 + a.n_items);
+    const int nslots = a.slot_n[0];  // paired halves (k_pair_slots), 2 per wave and tile
     const Cam cam = load_cam(a.campos, a.rot);
     const WBlob wb = make_blob(a.blob, BLOB_BYTES_ALL);
     const float *proj = (const float *)a.proj;
@@ -1137,9 +1271,9 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     int slot = 0;
     dma_chunk<Net, 0, NW16>(wb, lds, w, lane, 0);
     // The next tile's chain, prefetched inside the current tile so each step lands under MFMAs:
-    // work entry (block1.2), neighbour / ray index (block3.0), point record + sample position and
-    // the P row (block3.2).  First tile: here.
-    RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG16_SAMPLES + w * 2 + sc, end, lane);
+    // row-table entry (block1.2), neighbour / ray index (block3.0), point record + sample position
+    // and the P row (block3.2).  First tile: here.
+    RowIdx nx = row_index16(a, blockIdx.x * WG16_SAMPLES + w * 2 + sc, nslots, kk);
     Rec16 rnext = load_rec16(a, nx);
     // P row of point pid into `dst`: natural unit order, tile t of lane group g at 16 t + 4 g, so the
     // 4 lanes of a row read one contiguous 64 B per load instruction
@@ -1162,20 +1296,25 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
 #define X3T()
 #endif
 
-    for (int base = a.item0 + blockIdx.x * WG16_SAMPLES; base < end; base += gridDim.x * WG16_SAMPLES) {
+    for (int base = blockIdx.x * WG16_SAMPLES; base < nslots; base += gridDim.x * WG16_SAMPLES) {
         int lz = 0;
         asm volatile("" : "+s"(lz));
         char *ldsi = lds + lz;
         const float *Yl = (const float *)(ldsi + Y_LDS_OFF);
-        const int item = base + w * 2 + sc;
-        const int nitem = item + gridDim.x * WG16_SAMPLES;
+        const int hslot = base + w * 2 + sc;  // this lane's half (the LDS ring slot is `slot`)
+        const int nslot = hslot + gridDim.x * WG16_SAMPLES;
         X3T();  // tile start
         const RowIdx ix = nx;
         const bool m = ix.pid >= 0;
         const Rec16 rc = rnext;
-        const Row16 rw = row_math16(a, cam, rc, m);
-        if (a.blend && ix.sval && g == 0) a.blend[(int64_t)ix.s * 8 + kk] = rw.wgt;
-        if (a.wnorm && ix.sval && g == 1) a.wnorm[(int64_t)ix.s * 8 + kk] = rw.wn;
+        // rows of the two segments (lane group 0 = rows 0..15): bits 8 h .. 8 h + 7 are half h's
+        const uint64_t mrowA = __ballot(ix.sval && ix.a), mrowB = __ballot(ix.sval && !ix.a);
+        const Row16 rw = row_math16(a, cam, rc, m, ix.a, __popcll((mrowA >> (8 * sc)) & 0xFFull), kk, lane);
+        if ((a.blend || a.wnorm) && ix.sval) {  // optional outputs: the row's pidx index from the table
+            const int v = a.rows[(int64_t)hslot * 8 + kk];
+            if (a.blend && g == 0) a.blend[v] = rw.wgt;
+            if (a.wnorm && g == 1) a.wnorm[v] = rw.wn;
+        }
         X3B ext;
         {   // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane group 0
             const bool e = g == 0 && m;
@@ -1219,10 +1358,11 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         // block1.2: 256 -> 256 (input: block1.0 accumulators)
         const float inv0 = Yl[Y_INV + 0], inv1 = Yl[Y_INV + 1], inv2 = Yl[Y_INV + 2], inv7 = Yl[Y_INV + 7];
         bias_init(accB, Y_B1);
-        int s_next = 0;
+        int v_next = -1;
         run_layer16<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) { return chain_k(accA, inv0, k); },
                             [&](auto c) {
-                                if constexpr (decltype(c)::value == 0) s_next = nitem < end ? a.work[nitem] : 0;
+                                if constexpr (decltype(c)::value == 0)
+                                    v_next = nslot < nslots ? a.rows[(int64_t)nslot * 8 + kk] : -1;
                             }, ts);
         if constexpr (KB > 0) {
             // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256; the row's fp32 embedding
@@ -1253,24 +1393,31 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
             if constexpr (K < 8) return chain_k(in2, inv_in2, k); else return ext;
         }, [&](auto c) {
             constexpr int C = decltype(c)::value;
-            if constexpr (C == 0) {  // s_next landed at the previous boundaries
-                nx.sval = nitem < end;
-                nx.s = s_next;
-                nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
-                nx.ray = nx.sval ? a.samp_ray[s_next] : 0;
+            if constexpr (C == 0) {  // v_next landed at the previous boundaries
+                nx.sval = v_next >= 0;
+                nx.s = nx.sval ? v_next >> 3 : 0;
+                nx.a = (v_next & 7) == kk;
+                nx.pid = nx.sval ? a.pidx[v_next] : -1;
+                nx.ray = nx.sval ? a.samp_ray[nx.s] : 0;
             }
         }, ts);
         // block3.2: 256 -> 256 transposed: acc[t][i] = h[row 4 g + i][unit 16 t + (l & 15)]
         auto &acc = in2;  // block3.0's input is dead: its registers take block3.2's accumulators
 #pragma unroll
         for (int t = 0; t < 16; ++t) acc[t] = f32x4{};
-        // the next tile's record and P rows go out at the ends of block3.2's chunks (after each chunk's
-        // DMA pieces, so they stay in flight across one boundary, VmL3): P tiles 4C..4C+3 into block3.0's
-        // accumulators, dead once chunk C's k-steps 2C, 2C+1 have consumed them (see accA)
+        // the next tile's record goes out at the end of block3.2's first chunk (after the chunk's DMA
+        // pieces, so it stays in flight across one boundary, VmL3); the slot entry of this lane's half
+        // in the epilogue's layout (half g >> 1: {A item | nA << 28, B item | nB << 28, ..}) at the end
+        // of the last chunk (first used by the f_s stores, after the epilogue's P loads)
+        int2 ce = make_int2(0, 0);
+        const int eslot = base + w * 2 + (g >> 1);
         run_layer16<Net, L3, true, VmL3>(wb, ldsi, slot, w, lane, lz, acc,
                                          [&](auto k) { return chain_k(acc2, inv2, k); }, NoHook{}, ts,
                                          [&](auto c) {
-                                             if constexpr (decltype(c)::value == 0) rnext = load_rec16(a, nx);
+                                             constexpr int C = decltype(c)::value;
+                                             if constexpr (C == 0) rnext = load_rec16(a, nx);
+                                             if constexpr (C == nch(Net::L[L3]) - 1)
+                                                 ce = *(const int2 *)(a.slots + (eslot < nslots ? eslot : 0));
                                          });
         X3T();  // block3.2 MFMAs issued
         // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads
@@ -1281,11 +1428,19 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
             asm volatile("" : "+v"(rnext.p[c]), "+v"(rnext.col[c]), "+v"(rnext.dir[c]), "+v"(rnext.l[c]), "+v"(rnext.v[c]),
                               "+v"(rnext.pp[c]), "+v"(rnext.pl[c]));
         asm volatile("" : "+v"(rnext.cf));
+        const int hsh = 8 * (g >> 1);  // half g >> 1's row bits
+        const int nA = __popcll((mrowA >> hsh) & 0xFFull), nB = __popcll((mrowB >> hsh) & 0xFFull);
 
-        float wv[4];
+        // row weights of this lane's rows 4 g + i (position 4 (g & 1) + i of half g >> 1), split by
+        // segment: A = positions < nA, B = the rest (idle rows weigh 0)
+        float wa[4], wb4[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            wv[i] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, rw.wgt)));
+        for (int i = 0; i < 4; ++i) {
+            const float wi = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, rw.wgt)));
+            const bool inA = 4 * (g & 1) + i < nA;
+            wa[i] = inA ? wi : 0.f;
+            wb4[i] = inA ? 0.f : wi;
+        }
         const float inv3 = Yl[Y_INV + 3];
         float ap[4] = {0.f, 0.f, 0.f, 0.f}, fs[16];
         // the next tile's P rows (see accA) go out tile by tile between the epilogue's VALU work
@@ -1294,56 +1449,64 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         for (int t = 0; t < 16; ++t) {
             acc2[t] = *(const f32x4 *)(psrc + 16 * t);
             const float bu = Yl[Y_B3 + 16 * t + r], wau = Yl[Y_WA + 16 * t + r];
-            float fg = 0.f;
+            float fa = 0.f, fb = 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float y = __builtin_fmaf(acc[t][i], inv3, bu);
                 const float hv = fmaxf(y, 0.01f * y);
                 ap[i] = __builtin_fmaf(wau, hv, ap[i]);
-                fg = __builtin_fmaf(wv[i], hv, fg);
+                fa = __builtin_fmaf(wa[i], hv, fa);
+                fb = __builtin_fmaf(wb4[i], hv, fb);
             }
-            // + the sample's other 4 neighbours (lane group g ^ 1, 16 lanes away)
-            float x = fg, y = fg;
-            permlane16_swap(x, y);
-            fs[t] = x + y;
+            // + the half's other 4 rows (lane group g ^ 1, 16 lanes away): the swap leaves A's pair of
+            // chains in the even groups and B's in the odd ones.  Per sample this is (chain over its
+            // rows 0..3) + (chain over rows 4..7) at any offset: B sits in one group (zero-weight rows
+            // leave a chain unchanged, the other group's chain is 0)
+            permlane16_swap(fa, fb);
+            fs[t] = fa + fb;
         }
         X3T();  // block3.2 epilogue (K-blend, alpha partials)
-        {   // f_s (units 16 t + r of sample g >> 1) -> LDS transpose -> two 16-B stores per lane
+        {   // f_s (units 16 t + r; A of half g >> 1 in even groups, B in odd ones) -> LDS transpose ->
+            // two 16-B stores per lane and segment, into the segment's work-item row (lane half
+            // lane >> 5 == g >> 1, so `ce` is the entry of the half it stores); a missing segment
+            // stores to the scratch row, so every wave issues the same four stores (VmL0)
             float *st = (float *)(ldsi + FSW16_OFF + w * 2048);
-            if ((g & 1) == 0) {
+            const int uo = 8 * (lane & 31);
 #pragma unroll
-                for (int t = 0; t < 16; ++t) st[(g >> 1) * 256 + 16 * t + r] = fs[t];
+            for (int seg = 0; seg < 2; ++seg) {
+                if ((g & 1) == seg) {
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) st[(g >> 1) * 256 + 16 * t + r] = fs[t];
+                }
+                // other lanes wrote the row: without the clobber the compiler reuses the lanes' first
+                // round loads in the second (nothing this lane stored in between, per thread)
+                asm volatile("" ::: "memory");
+                const f32x4 v0 = *(const f32x4 *)(st + (lane >> 5) * 256 + uo);
+                const f32x4 v1 = *(const f32x4 *)(st + (lane >> 5) * 256 + uo + 4);
+                const bool have = (seg ? nB > 0 : nA > 0) && eslot < nslots;
+                const uint32_t e = (uint32_t)(seg ? ce.y : ce.x) & 0x0FFFFFFFu;
+                float *dst = (have ? (float *)a.fs + (int64_t)e * HID : a.fs_scratch) + uo;
+                *(f32x4 *)dst = v0;
+                *(f32x4 *)(dst + 4) = v1;
             }
-            const f32x4 v0 = *(const f32x4 *)(st + (lane >> 5) * 256 + 8 * (lane & 31));
-            const f32x4 v1 = *(const f32x4 *)(st + (lane >> 5) * 256 + 8 * (lane & 31) + 4);
-            const int it = base + w * 2 + (lane >> 5);
-            // descriptor based at this tile's first item (uniform, scalar registers): a launch
-            // may hold more items than a 31-bit byte range covers
-            const __amdgpu_buffer_rsrc_t fs_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)((float *)a.fs + (int64_t)(base - a.item0) * HID), (short)0, 0x7fffffff, 0x00020000);
-            const uint32_t off = it < end ? (uint32_t)((it - base) * HID + 8 * (lane & 31)) * 4 : 0xFFFF0000u;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), fs_rsrc, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), fs_rsrc, off, 16, 0);
         }
         // alpha: row logits summed over the 16 lanes (units) of the group, softplus(x + b - 1),
         // blended over the sample's 8 rows (4 here, 4 in group g ^ 1)
-        float as = 0.f;
+        float asa = 0.f, asb = 0.f;
         const float ba = Yl[Y_BA];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float x = dpp_sum8(ap[i]);
             x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
-            as = __builtin_fmaf(wv[i], softplus(x + ba - 1.f), as);
+            const float sp = softplus(x + ba - 1.f);
+            asa = __builtin_fmaf(wa[i], sp, asa);
+            asb = __builtin_fmaf(wb4[i], sp, asb);
         }
-        {
-            float x = as, y = as;
-            permlane16_swap(x, y);
-            as = x + y;
-        }
-        // sample g >> 1 of this wave: its id sits in row 8 (g >> 1) (lane 8 (g >> 1))
-        const int s_of = __builtin_amdgcn_ds_bpermute((8 * (g >> 1)) * 4, ix.s);
-        const int it = base + w * 2 + (g >> 1);
-        if (r == 0 && (g & 1) == 0 && it < end) a.feat[(int64_t)s_of * 4 + 0] = as;
+        permlane16_swap(asa, asb);
+        const float as = asa + asb;  // even groups: A's alpha, odd groups: B's
+        // the segment's sample: row 0 (A) or row max(nA, 4) (B) of the half (lanes 0..15 hold rows 0..15)
+        const int s_of = __builtin_amdgcn_ds_bpermute((hsh + ((g & 1) ? (nA > 4 ? nA : 4) : 0)) * 4, ix.s);
+        if (r == 0 && ((g & 1) ? nB > 0 : nA > 0)) a.feat[(int64_t)s_of * 4 + 0] = as;
         X3T();  // tile end
     }
 #undef X3T
@@ -1830,11 +1993,14 @@ int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void
 // 2^31 / 1 KiB items per launch.  k_rows16 bases a descriptor per tile and has no such limit.
 constexpr int64_t X3_MAX_CHUNK = ((int64_t)0x7fffffff / (sgn::mlp::HID * 4)) / 16 * 16;
 
+// Workspace: blended features of every work item (fp32, 1 KiB each), so the two stages may be
+// called separately, then k_pair_slots' row table (32 B) and slot entries (16 B) per item, then a
+// 2-KiB tail (slot count, the scratch row of missing segments).  A smaller workspace is accepted
+// with stages = 3 (both stages per chunk).
+constexpr int64_t WS_PER_ITEM = sgn::mlp::HID * 4 + 32 + 16, WS_TAIL = 2048;
 size_t sgn_aggregate_workspace_bytes_f32(int64_t S) {
-    // blended features of every work item (fp32, 1 KiB each), so the two stages may be called
-    // separately; a smaller workspace is accepted with stages = 3 (both stages per chunk)
     if (S < 32) S = 32;
-    return (size_t)S * sgn::mlp::HID * sizeof(float);
+    return (size_t)(S * WS_PER_ITEM + WS_TAIL);
 }
 
 int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet, const void *d_point_proj,
@@ -1854,7 +2020,7 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     SGN_REQUIRE(S_capacity >= 0 && S_capacity < (1 << 30), "S_capacity out of range");
     SGN_REQUIRE(((uintptr_t)d_workspace & 15) == 0 && ((uintptr_t)d_point_proj & 15) == 0, "16-byte alignment required");
     hipStream_t st = as_stream(stream);
-    const int64_t ws_items = (int64_t)(workspace_bytes / (mlp::HID * sizeof(float)));
+    const int64_t ws_items = workspace_bytes > (size_t)WS_TAIL ? (int64_t)((workspace_bytes - WS_TAIL) / WS_PER_ITEM) : 0;
     SGN_REQUIRE(ws_items >= 32, "aggregate workspace too small");
     SGN_REQUIRE(stages == 3 || ws_items >= S_capacity,
                 "stages 1 and 2 called separately need a workspace for all S_capacity items");
@@ -1862,7 +2028,9 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     // k_rows16 bases its f_s descriptor per tile (one launch per stage for any frame); the 32x32
     // kernel's single descriptor limits a launch to X3_MAX_CHUNK items
     const bool full = ws_items >= S_capacity;
-    const int64_t lim = x3_w16() ? ws_items : (ws_items < X3_MAX_CHUNK ? ws_items : X3_MAX_CHUNK);
+    // (k_pair_slots packs chunk-relative items in 28 bits)
+    const int64_t lim = x3_w16() ? (ws_items < (1 << 27) ? ws_items : (1 << 27))
+                                 : (ws_items < X3_MAX_CHUNK ? ws_items : X3_MAX_CHUNK);
     const int64_t chunk = lim < S_capacity ? lim : (S_capacity > 32 ? S_capacity : 32);
     AggArgs a{};
     a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
@@ -1875,6 +2043,17 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     a.proj = (const _Float16 *)d_point_proj;  // fp32 table (k_agg_rows_x3 reads it as float)
     a.rec = (const float *)((const char *)d_point_proj + (size_t)pt->n_points * x3::PROJ_BYTES_PER_POINT);
     a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
+    char *ws_end = (char *)d_workspace + ws_items * WS_PER_ITEM + WS_TAIL;
+    int32_t *rows = (int32_t *)((char *)d_workspace + ws_items * mlp::HID * 4);
+    int4 *slots = (int4 *)(rows + ws_items * 8);
+    int32_t *slot_n = (int32_t *)(ws_end - WS_TAIL);
+    a.rows = rows; a.slots = slots; a.slot_n = slot_n;
+    a.fs_scratch = (float *)(ws_end - 1024);
+    if ((stages & 1) && x3_w16()) {
+        // a paired half writes only its samples' valid rows: the optional per-slot outputs start at 0
+        if (d_out_blend) SGN_CHECK_HIP(hipMemsetAsync(d_out_blend, 0, (size_t)S_capacity * 8 * 4, st));
+        if (d_out_wnorm) SGN_CHECK_HIP(hipMemsetAsync(d_out_wnorm, 0, (size_t)S_capacity * 8 * 4, st));
+    }
 #ifdef SGN_X3_TIMING
     static unsigned long long *tbuf = nullptr;
     const size_t tn = (size_t)x3::TD_BLOCKS * x3::NW16 * x3::TD_EV;
@@ -1892,6 +2071,10 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
         c.fs = fs;
         const int64_t wg = (n + x3::WG_SAMPLES - 1) / x3::WG_SAMPLES;
         if ((stages & 1) && x3_w16()) {
+            SGN_CHECK_HIP(hipMemsetAsync(slot_n, 0, 4, st));
+            hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)((n + x3::PAIR_TPB - 1) / x3::PAIR_TPB)),
+                               dim3(x3::PAIR_TPB), 0, st, q->counters, q->work, q->samp_nnb, (int32_t)i0, (int32_t)n,
+                               rows, slots, slot_n);
             auto kern = ksb == 0 ? x3::k_rows16<0> : ksb == KS_HID ? x3::k_rows16<8> : x3::k_rows16<11>;
             const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < 256 ? wg16 : 256)), dim3(x3::TPB16), 0, st, a);
