@@ -113,7 +113,6 @@ struct AggArgs {
     const int32_t *rows;
     const int4 *slots;
     const int32_t *slot_n;
-    float *fs_scratch;  // 1 KiB row the stores of a missing segment go to
 };
 
 // training save: one 16-byte fragment of a 32-row tile -> [rows][C] (C multiple of 16)

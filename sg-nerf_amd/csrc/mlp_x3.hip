@@ -998,9 +998,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
 
 // ---- per-neighbour rows (16x16) -------------------------------------------------------------
 constexpr int WG16_SAMPLES = NW16 * 2;            // 16 samples = 128 rows per workgroup tile
-constexpr int FSW16_OFF = Y_LDS_OFF + N_Y32 * 4;
-constexpr int FSW16_BYTES = NW16 * 2048;          // [wave][2 samples][256] fp32
-constexpr int ROWS16_LDS = FSW16_OFF + FSW16_BYTES;
+constexpr int ROWS16_LDS = Y_LDS_OFF + N_Y32 * 4;
 static_assert(ROWS16_LDS <= 163840, "LDS budget (16x16 rows)");
 
 // row r's point record, its sample position and view direction (+ the caller's pers
@@ -1045,15 +1043,15 @@ __device__ __forceinline__ Rec16 load_rec16(const AggArgs &a, const RowIdx &ix) 
     r.cf = m ? q0[3] : 0.f;
     return r;
 }
-// vmcnt allowances of k_rows16's boundaries (chunk_enter VM): block3.2 ends chunk 0 with the slot
-// entry load and then the next tile's record (REC16_LOADS loads, the youngest); after block3.2 come
-// the next tile's 16 P loads and the epilogue's four unconditional f_s stores (two per segment),
-// all younger than block1.0's DMA
+// vmcnt allowances of k_rows16's boundaries (chunk_enter VM): block3.2 ends chunk 0 with the next
+// tile's record (REC16_LOADS loads, the youngest); after block3.2 come the next tile's 16 P loads
+// (and the epilogue's f_s stores, masked per segment, so not counted), all younger than block1.0's
+// DMA
 struct VmL3 {
     static constexpr int vm(int c) { return c == 1 ? REC16_LOADS : 0; }
 };
 struct VmL0 {
-    static constexpr int vm(int) { return 16 + 4; }
+    static constexpr int vm(int) { return 16; }
 };
 
 // ---- paired samples: k_rows16's 8-row halves ----------------------------------------------------
@@ -1188,7 +1186,7 @@ struct Row16 {
     float wgt, wn;
 };
 __device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, const Rec16 &rc, bool m, bool isA,
-                                            int nA, int kk, int lane) {
+                                            int nA, bool waveB) {
     Row16 o;
     const float dwx = __fsub_rn(rc.p[0], rc.l[0]), dwy = __fsub_rn(rc.p[1], rc.l[1]), dwz = __fsub_rn(rc.p[2], rc.l[2]);
     o.d[0] = m ? dwx : 0.f;
@@ -1211,14 +1209,25 @@ __device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, co
         w = 1.f / fmaxf(sqrtf(n2), 1e-6f);
     }
     // normalised over the rows of the row's own sample (A: rows 0..nA-1 of the half, B: rows
-    // oB = max(nA, 4) ..; idle rows carry w = 0).  B's weights are first moved down to rows 0..nB-1, so
-    // both samples sum exactly as they would alone in a half: a sample's values do not depend on its
+    // oB = max(nA, 4) .. 7, always in the upper quad; idle rows carry w = 0).  B's weights are first
+    // rotated inside that quad so its rows start at row 4 (the rows rotated in are A's or idle: 0),
+    // so both samples sum in the same tree as alone in a half: a sample's values do not depend on its
     // partner.
-    const int oB = nA > 4 ? nA : 4;
-    const float wb0 = isA ? 0.f : w;
-    const float wbs = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(((lane + oB) & 63) * 4, __builtin_bit_cast(int, wb0)));
-    const float wsa = dpp_sum8(isA ? w : 0.f), wsb = dpp_sum8(kk + oB < 8 ? wbs : 0.f);
-    const float wsum = isA ? wsa : wsb;
+    // (waveB: the wave holds a B sample, else every row is A's or idle and one sum does)
+    float wsum;
+    if (waveB) {
+        const float wb0 = isA ? 0.f : w;
+        const int rb0 = __builtin_bit_cast(int, wb0);
+        const int r1 = __builtin_amdgcn_mov_dpp(rb0, 0x39, 0xF, 0xF, true);  // quad_perm [1,2,3,0]
+        const int r2 = __builtin_amdgcn_mov_dpp(rb0, 0x4E, 0xF, 0xF, true);  // [2,3,0,1]
+        const int r3 = __builtin_amdgcn_mov_dpp(rb0, 0x93, 0xF, 0xF, true);  // [3,0,1,2]
+        const int rot = nA > 4 ? nA - 4 : 0;
+        const float wbs = __builtin_bit_cast(float, rot == 0 ? rb0 : rot == 1 ? r1 : rot == 2 ? r2 : r3);
+        const float wsa = dpp_sum8(isA ? w : 0.f), wsb = dpp_sum8(wbs);
+        wsum = isA ? wsa : wsb;
+    } else {
+        wsum = dpp_sum8(w);
+    }
     w = w / fmaxf(wsum, 1e-8f);
     o.wn = w;
     o.wgt = w * fminf(fmaxf(rc.cf, 1e-4f), 1.f);
@@ -1309,7 +1318,9 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         const Rec16 rc = rnext;
         // rows of the two segments (lane group 0 = rows 0..15): bits 8 h .. 8 h + 7 are half h's
         const uint64_t mrowA = __ballot(ix.sval && ix.a), mrowB = __ballot(ix.sval && !ix.a);
-        const Row16 rw = row_math16(a, cam, rc, m, ix.a, __popcll((mrowA >> (8 * sc)) & 0xFFull), kk, lane);
+        const int nA0 = __popc((uint32_t)mrowA & 0xFFu), nA1 = __popc(((uint32_t)mrowA >> 8) & 0xFFu);
+        const bool waveB = (mrowB & 0xFFFFull) != 0;  // wave-uniform: a B sample in either half
+        const Row16 rw = row_math16(a, cam, rc, m, ix.a, sc ? nA1 : nA0, waveB);
         if ((a.blend || a.wnorm) && ix.sval) {  // optional outputs: the row's pidx index from the table
             const int v = a.rows[(int64_t)hslot * 8 + kk];
             if (a.blend && g == 0) a.blend[v] = rw.wgt;
@@ -1408,7 +1419,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         // the next tile's record goes out at the end of block3.2's first chunk (after the chunk's DMA
         // pieces, so it stays in flight across one boundary, VmL3); the slot entry of this lane's half
         // in the epilogue's layout (half g >> 1: {A item | nA << 28, B item | nB << 28, ..}) at the end
-        // of the last chunk (first used by the f_s stores, after the epilogue's P loads)
+        // of the third (landed by the epilogue's first f_s store)
         int2 ce = make_int2(0, 0);
         const int eslot = base + w * 2 + (g >> 1);
         run_layer16<Net, L3, true, VmL3>(wb, ldsi, slot, w, lane, lz, acc,
@@ -1416,7 +1427,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
                                          [&](auto c) {
                                              constexpr int C = decltype(c)::value;
                                              if constexpr (C == 0) rnext = load_rec16(a, nx);
-                                             if constexpr (C == nch(Net::L[L3]) - 1)
+                                             if constexpr (C == nch(Net::L[L3]) - 2)
                                                  ce = *(const int2 *)(a.slots + (eslot < nslots ? eslot : 0));
                                          });
         X3T();  // block3.2 MFMAs issued
@@ -1430,83 +1441,64 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         asm volatile("" : "+v"(rnext.cf));
         const int hsh = 8 * (g >> 1);  // half g >> 1's row bits
         const int nA = __popcll((mrowA >> hsh) & 0xFFull), nB = __popcll((mrowB >> hsh) & 0xFFull);
-
-        // row weights of this lane's rows 4 g + i (position 4 (g & 1) + i of half g >> 1), split by
-        // segment: A = positions < nA, B = the rest (idle rows weigh 0)
-        float wa[4], wb4[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float wi = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, rw.wgt)));
-            const bool inA = 4 * (g & 1) + i < nA;
-            wa[i] = inA ? wi : 0.f;
-            wb4[i] = inA ? 0.f : wi;
-        }
-        const float inv3 = Yl[Y_INV + 3];
-        float ap[4] = {0.f, 0.f, 0.f, 0.f}, fs[16];
-        // the next tile's P rows (see accA) go out tile by tile between the epilogue's VALU work
-        const float *psrc = proj + (int64_t)(nx.pid < 0 ? 0 : nx.pid) * HID + 4 * g;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            acc2[t] = *(const f32x4 *)(psrc + 16 * t);
-            const float bu = Yl[Y_B3 + 16 * t + r], wau = Yl[Y_WA + 16 * t + r];
-            float fa = 0.f, fb = 0.f;
+        {   // epilogue
+            // row weights of this lane's rows 4 g + i (position 4 (g & 1) + i of half g >> 1), split by
+            // segment: A = positions < nA, B = the rest (idle rows weigh 0)
+            float wa[4], wb4[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float y = __builtin_fmaf(acc[t][i], inv3, bu);
-                const float hv = fmaxf(y, 0.01f * y);
-                ap[i] = __builtin_fmaf(wau, hv, ap[i]);
-                fa = __builtin_fmaf(wa[i], hv, fa);
-                fb = __builtin_fmaf(wb4[i], hv, fb);
+                const float wi = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, rw.wgt)));
+                const bool inA = 4 * (g & 1) + i < nA;
+                wa[i] = inA ? wi : 0.f;
+                wb4[i] = inA ? 0.f : wi;
             }
-            // + the half's other 4 rows (lane group g ^ 1, 16 lanes away): the swap leaves A's pair of
-            // chains in the even groups and B's in the odd ones.  Per sample this is (chain over its
-            // rows 0..3) + (chain over rows 4..7) at any offset: B sits in one group (zero-weight rows
-            // leave a chain unchanged, the other group's chain is 0)
-            permlane16_swap(fa, fb);
-            fs[t] = fa + fb;
-        }
-        X3T();  // block3.2 epilogue (K-blend, alpha partials)
-        {   // f_s (units 16 t + r; A of half g >> 1 in even groups, B in odd ones) -> LDS transpose ->
-            // two 16-B stores per lane and segment, into the segment's work-item row (lane half
-            // lane >> 5 == g >> 1, so `ce` is the entry of the half it stores); a missing segment
-            // stores to the scratch row, so every wave issues the same four stores (VmL0)
-            float *st = (float *)(ldsi + FSW16_OFF + w * 2048);
-            const int uo = 8 * (lane & 31);
+            const float inv3 = Yl[Y_INV + 3];
+            float ap[4] = {0.f, 0.f, 0.f, 0.f};
+            // f_s of this lane's segment (A of half g >> 1 in even groups, B in odd ones), unit 16 t + r,
+            // stored as each t is blended: 16 lanes write 64 contiguous bytes of the work item's row
+            const bool fs_have = ((g & 1) ? nB > 0 : nA > 0) && eslot < nslots;
+            float *fs_dst = (float *)a.fs + (int64_t)((uint32_t)((g & 1) ? ce.y : ce.x) & 0x0FFFFFFFu) * HID + r;
+            // the next tile's P rows (see accA) go out tile by tile between the epilogue's VALU work
+            const float *psrc = proj + (int64_t)(nx.pid < 0 ? 0 : nx.pid) * HID + 4 * g;
 #pragma unroll
-            for (int seg = 0; seg < 2; ++seg) {
-                if ((g & 1) == seg) {
+            for (int t = 0; t < 16; ++t) {
+                acc2[t] = *(const f32x4 *)(psrc + 16 * t);
+                const float bu = Yl[Y_B3 + 16 * t + r], wau = Yl[Y_WA + 16 * t + r];
+                float fa = 0.f, fb = 0.f;
 #pragma unroll
-                    for (int t = 0; t < 16; ++t) st[(g >> 1) * 256 + 16 * t + r] = fs[t];
+                for (int i = 0; i < 4; ++i) {
+                    const float y = __builtin_fmaf(acc[t][i], inv3, bu);
+                    const float hv = fmaxf(y, 0.01f * y);
+                    ap[i] = __builtin_fmaf(wau, hv, ap[i]);
+                    fa = __builtin_fmaf(wa[i], hv, fa);
+                    fb = __builtin_fmaf(wb4[i], hv, fb);
                 }
-                // other lanes wrote the row: without the clobber the compiler reuses the lanes' first
-                // round loads in the second (nothing this lane stored in between, per thread)
-                asm volatile("" ::: "memory");
-                const f32x4 v0 = *(const f32x4 *)(st + (lane >> 5) * 256 + uo);
-                const f32x4 v1 = *(const f32x4 *)(st + (lane >> 5) * 256 + uo + 4);
-                const bool have = (seg ? nB > 0 : nA > 0) && eslot < nslots;
-                const uint32_t e = (uint32_t)(seg ? ce.y : ce.x) & 0x0FFFFFFFu;
-                float *dst = (have ? (float *)a.fs + (int64_t)e * HID : a.fs_scratch) + uo;
-                *(f32x4 *)dst = v0;
-                *(f32x4 *)(dst + 4) = v1;
+                // + the half's other 4 rows (lane group g ^ 1, 16 lanes away): the swap leaves A's pair
+                // of chains in the even groups and B's in the odd ones.  Per sample this is (chain over
+                // its rows 0..3) + (chain over rows 4..7) at any offset: B sits in one group (zero-weight
+                // rows leave a chain unchanged, the other group's chain is 0)
+                permlane16_swap(fa, fb);
+                if (fs_have) fs_dst[16 * t] = fa + fb;
             }
-        }
-        // alpha: row logits summed over the 16 lanes (units) of the group, softplus(x + b - 1),
-        // blended over the sample's 8 rows (4 here, 4 in group g ^ 1)
-        float asa = 0.f, asb = 0.f;
-        const float ba = Yl[Y_BA];
+            X3T();  // block3.2 epilogue (K-blend, alpha partials)
+            // alpha: row logits summed over the 16 lanes (units) of the group, softplus(x + b - 1),
+            // blended over the segment's rows like f_s
+            float asa = 0.f, asb = 0.f;
+            const float ba = Yl[Y_BA];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float x = dpp_sum8(ap[i]);
-            x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
-            const float sp = softplus(x + ba - 1.f);
-            asa = __builtin_fmaf(wa[i], sp, asa);
-            asb = __builtin_fmaf(wb4[i], sp, asb);
+            for (int i = 0; i < 4; ++i) {
+                float x = dpp_sum8(ap[i]);
+                x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
+                const float sp = softplus(x + ba - 1.f);
+                asa = __builtin_fmaf(wa[i], sp, asa);
+                asb = __builtin_fmaf(wb4[i], sp, asb);
+            }
+            permlane16_swap(asa, asb);
+            const float as = asa + asb;  // even groups: A's alpha, odd groups: B's
+            // the segment's sample: row 0 (A) or row max(nA, 4) (B) of the half (lanes 0..15 hold rows)
+            const int s_of = __builtin_amdgcn_ds_bpermute((hsh + ((g & 1) ? (nA > 4 ? nA : 4) : 0)) * 4, ix.s);
+            if (r == 0 && ((g & 1) ? nB > 0 : nA > 0)) a.feat[(int64_t)s_of * 4 + 0] = as;
         }
-        permlane16_swap(asa, asb);
-        const float as = asa + asb;  // even groups: A's alpha, odd groups: B's
-        // the segment's sample: row 0 (A) or row max(nA, 4) (B) of the half (lanes 0..15 hold rows 0..15)
-        const int s_of = __builtin_amdgcn_ds_bpermute((hsh + ((g & 1) ? (nA > 4 ? nA : 4) : 0)) * 4, ix.s);
-        if (r == 0 && ((g & 1) ? nB > 0 : nA > 0)) a.feat[(int64_t)s_of * 4 + 0] = as;
         X3T();  // tile end
     }
 #undef X3T
@@ -1995,7 +1987,7 @@ constexpr int64_t X3_MAX_CHUNK = ((int64_t)0x7fffffff / (sgn::mlp::HID * 4)) / 1
 
 // Workspace: blended features of every work item (fp32, 1 KiB each), so the two stages may be
 // called separately, then k_pair_slots' row table (32 B) and slot entries (16 B) per item, then a
-// 2-KiB tail (slot count, the scratch row of missing segments).  A smaller workspace is accepted
+// 2-KiB tail (the slot count).  A smaller workspace is accepted
 // with stages = 3 (both stages per chunk).
 constexpr int64_t WS_PER_ITEM = sgn::mlp::HID * 4 + 32 + 16, WS_TAIL = 2048;
 size_t sgn_aggregate_workspace_bytes_f32(int64_t S) {
@@ -2048,7 +2040,6 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     int4 *slots = (int4 *)(rows + ws_items * 8);
     int32_t *slot_n = (int32_t *)(ws_end - WS_TAIL);
     a.rows = rows; a.slots = slots; a.slot_n = slot_n;
-    a.fs_scratch = (float *)(ws_end - 1024);
     if ((stages & 1) && x3_w16()) {
         // a paired half writes only its samples' valid rows: the optional per-slot outputs start at 0
         if (d_out_blend) SGN_CHECK_HIP(hipMemsetAsync(d_out_blend, 0, (size_t)S_capacity * 8 * 4, st));
