@@ -210,7 +210,11 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
  *                             dir, conf and embedding required; opaque to the caller)
  *   sgn_aggregate_f32       : as sgn_aggregate_sg (same outputs, stages bits), d_point_proj required;
  *                             d_bpnet = fp32 [N, 96] BPNet point embedding when bpnet_dim = 96;
- *                             workspace sgn_aggregate_workspace_bytes_f32(S) (fp32 blended features)
+ *                             workspace sgn_aggregate_workspace_bytes_f32(S) (fp32 blended features
+ *                             and the row kernel's paired-sample tables; opaque to the caller);
+ *                             reads q->samp_nnb (valid neighbours are a prefix of each sample's K
+ *                             slots, as sgn_query writes them); optional d_out_blend / d_out_wnorm are
+ *                             zeroed by stage 1 before the valid rows are written
  * 16-byte aligned device buffers. */
 size_t sgn_mlp_packed_bytes_f32(int32_t bpnet_layers, int32_t bpnet_dim);
 int sgn_mlp_pack_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,

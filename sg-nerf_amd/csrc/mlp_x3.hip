@@ -1072,7 +1072,7 @@ constexpr int PAIR_TPB = 1024, PAIR_NW = PAIR_TPB / 64;
 __global__ __launch_bounds__(PAIR_TPB) void k_pair_slots(const int32_t *__restrict__ counters,
                                                          const int32_t *__restrict__ work,
                                                          const int32_t *__restrict__ nnb, int32_t item0,
-                                                         int32_t n_items, int32_t *__restrict__ rows,
+                                                         int32_t n_items, int32_t pair, int32_t *__restrict__ rows,
                                                          int4 *__restrict__ slots, int32_t *__restrict__ slot_n) {
     __shared__ int wc[PAIR_NW][9];
     __shared__ int16_t blist[9][PAIR_TPB];  // count -> rank -> thread
@@ -1138,10 +1138,10 @@ __global__ __launch_bounds__(PAIR_TPB) void k_pair_slots(const int32_t *__restri
             else if (j + 1 < Lt) partner = left(j + 1);
         }
     }
-#ifdef SGN_NO_PAIR  // experiment only: every sample alone in its half
-    lead = ok;
-    partner = -1;
-#endif
+    if (!pair) {  // pairing off (SGN_PAIR=0): every sample alone in its half
+        lead = ok;
+        partner = -1;
+    }
     const uint64_t lm = __ballot(lead);
     int idx = __popcll(lm & below);
     if (lane == 0) wl[wv] = __popcll(lm);
@@ -2040,6 +2040,9 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     int4 *slots = (int4 *)(rows + ws_items * 8);
     int32_t *slot_n = (int32_t *)(ws_end - WS_TAIL);
     a.rows = rows; a.slots = slots; a.slot_n = slot_n;
+    // SGN_PAIR=0 runs every sample alone in its k_rows16 half (same results, bit for bit; tests)
+    const char *pe = getenv("SGN_PAIR");
+    const int32_t pair = !(pe && pe[0] == '0');
     if ((stages & 1) && x3_w16()) {
         // a paired half writes only its samples' valid rows: the optional per-slot outputs start at 0
         if (d_out_blend) SGN_CHECK_HIP(hipMemsetAsync(d_out_blend, 0, (size_t)S_capacity * 8 * 4, st));
@@ -2065,7 +2068,7 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
             SGN_CHECK_HIP(hipMemsetAsync(slot_n, 0, 4, st));
             hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)((n + x3::PAIR_TPB - 1) / x3::PAIR_TPB)),
                                dim3(x3::PAIR_TPB), 0, st, q->counters, q->work, q->samp_nnb, (int32_t)i0, (int32_t)n,
-                               rows, slots, slot_n);
+                               pair, rows, slots, slot_n);
             auto kern = ksb == 0 ? x3::k_rows16<0> : ksb == KS_HID ? x3::k_rows16<8> : x3::k_rows16<11>;
             const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < 256 ? wg16 : 256)), dim3(x3::TPB16), 0, st, a);

@@ -334,3 +334,61 @@ def test_dense_stress_scene_matches_oracle():
           f"max |rgb - oracle| {err:.3e}, max |bgT - oracle| {berr:.3e}")
     assert err <= F32_TOL and berr <= F32_TOL
     assert nb / 640000 > 150
+
+
+def _render_pair_modes(monkeypatch, make):
+    """Two renders of the same input, k_rows16's sample pairing on (default) and off (SGN_PAIR=0)."""
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SGN_PAIR", mode)
+        r, out, n_items = make()
+        q = out.query
+        S = q.n_samples()
+        valid = (q.samp_nnb[:S] > 0).cpu()
+        outs.append((out.rgb.clone(), out.opacity.clone(), out.bg_transmission.clone(), out.feat[:S][valid].clone(),
+                     out.blend[:S][valid].clone()))
+    return outs, n_items
+
+
+@pytest.mark.parametrize("case", ["patch", "room", "sg96"])
+def test_paired_rows_bit_identical_to_unpaired(monkeypatch, case):
+    """k_rows16 packs two samples whose neighbour counts sum to <= 8 into one 8-row half (sample B at
+    row max(nA, 4)); the weight normalisation, K-blend and alpha are arranged so each sample gets the
+    bits it gets alone.  A render with pairing equals one without (SGN_PAIR=0), bit for bit: the
+    frame's colour, opacity, transmission, per-sample (alpha, rgb) and blend weights.  The golden
+    patch has 1,131 B samples among 2,925 work items."""
+    def make():
+        if case == "patch":
+            pts, mlp, c = load_golden("reference_aggregator.npz", "patch")
+            near, far = (float(x) for x in c["near_far"])
+            view = scene.View(c["campos"], c["camrotc2w"], c["raydir"], None, None, 0, 0, near, far)
+            o = HotPathOpts(SR=int(c["SR"]), K=int(c["K"]))
+            r, out = _render(pts, mlp, view, o)
+            kw = {}
+        elif case == "room":
+            pc = small_room(300_000, seed=4)
+            mlp = init_mlp(4, bias_std=0.01)
+            mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
+            view = make_view(64, 96, yaw=75.0, pitch=-12.0)
+            pts = dict(xyz=pc.xyz, embedding=pc.embedding, color=pc.color, dir=pc.dir, conf=pc.conf)
+            r, out = _render(pts, mlp, view, HotPathOpts(SR=64))
+        else:
+            g = np.load(GOLD_SG, allow_pickle=False)
+            mlp = {k[len("mlp_sg96/"):]: torch.from_numpy(g[k]) for k in g.files if k.startswith("mlp_sg96/")}
+            pts = PointTables(*(g[f"sgpatch/{k}"] for k in ("xyz", "embedding", "color", "dir", "conf")), DEV,
+                              bpnet=g["sgpatch/bpnet"])
+            o = HotPathOpts(SR=int(g["sg96/SR"]), shading_feature_mlp_layer2_bpnet=1, predict_semantic=1,
+                            semantic_guidance=1)
+            near, far = (float(x) for x in g["sg96/near_far"])
+            raydir = torch.from_numpy(g["sg96/raydir"])
+            R = raydir.shape[0]
+            r = HipRenderer(pts, mlp, o, DEV)
+            out = r.render(torch.from_numpy(g["sg96/campos"]), torch.from_numpy(g["sg96/camrotc2w"]), raydir, near, far,
+                           want_blend=True, point_labels=torch.zeros(pts.n, dtype=torch.int32, device=DEV),
+                           ray_labels=torch.zeros(R, dtype=torch.int32, device=DEV), seconds=5)
+        torch.cuda.synchronize()
+        return r, out, int(out.query.counters[1])
+    (on, off), n_items = _render_pair_modes(monkeypatch, make)
+    assert n_items > 100
+    for name, a, b in zip(("rgb", "opacity", "bg_transmission", "feat", "blend"), on, off):
+        assert torch.equal(a, b), name
