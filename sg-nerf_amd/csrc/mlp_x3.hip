@@ -1074,97 +1074,104 @@ __global__ __launch_bounds__(PAIR_TPB) void k_pair_slots(const int32_t *__restri
                                                          const int32_t *__restrict__ nnb, int32_t item0,
                                                          int32_t n_items, int32_t pair, int32_t *__restrict__ rows,
                                                          int4 *__restrict__ slots, int32_t *__restrict__ slot_n) {
-    __shared__ int wc[PAIR_NW][9];
+    __shared__ int wc[PAIR_NW][9], nt[9];  // per-wave counts -> exclusive per-wave offsets; totals
     __shared__ int16_t blist[9][PAIR_TPB];  // count -> rank -> thread
     __shared__ int ss[PAIR_TPB];            // thread -> sample
     __shared__ int8_t sc[PAIR_TPB];         // thread -> count
     __shared__ int wl[PAIR_NW], sbase;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int end = min(counters[1], item0 + n_items);
-    const int rel0 = blockIdx.x * PAIR_TPB;
-    if (item0 + rel0 >= end) return;  // the grid covers the capacity, the work list is shorter
-    const int item = item0 + rel0 + tid;
-    const bool ok = item < end;
-    const int s = ok ? work[item] : 0;
-    const int c = ok ? min(max(nnb[s], 1), 8) : 0;
-    ss[tid] = s;
-    sc[tid] = (int8_t)c;
-    const uint64_t below = (1ull << lane) - 1ull;
-    int rank = 0;
+    // grid-stride over 1024-item blocks of the work list (the grid is sized for the capacity, the
+    // list is known on the device only)
+    for (int rel0 = blockIdx.x * PAIR_TPB; item0 + rel0 < end; rel0 += gridDim.x * PAIR_TPB) {
+        __syncthreads();  // the previous block's LDS tables are read
+        const int item = item0 + rel0 + tid;
+        const bool ok = item < end;
+        const int s = ok ? work[item] : 0;
+        const int c = ok ? min(max(nnb[s], 1), 8) : 0;
+        ss[tid] = s;
+        sc[tid] = (int8_t)c;
+        const uint64_t below = (1ull << lane) - 1ull;
+        int rank = 0;
 #pragma unroll
-    for (int b = 1; b <= 8; ++b) {
-        const uint64_t m = __ballot(c == b);
-        if (c == b) rank = __popcll(m & below);
-        if (lane == 0) wc[wv][b] = __popcll(m);
-    }
-    __syncthreads();
-    int n[9];
-#pragma unroll
-    for (int b = 1; b <= 8; ++b) {
-        int tot = 0;
-        for (int q = 0; q < PAIR_NW; ++q) {
-            const int v = wc[q][b];
-            if (q < wv && b == c) rank += v;
-            tot += v;
+        for (int b = 1; b <= 8; ++b) {
+            const uint64_t m = __ballot(c == b);
+            if (c == b) rank = __popcll(m & below);
+            if (lane == 0) wc[wv][b] = __popcll(m);
         }
-        n[b] = tot;
-    }
-    if (ok) blist[c][rank] = (int16_t)tid;
-    __syncthreads();
-    const int p17 = min(n[1], n[7]), p26 = min(n[2], n[6]), p35 = min(n[3], n[5]), p44 = n[4] / 2;
-    const int L1 = n[1] - p17, L2 = n[2] - p26, L3 = n[3] - p35, L4 = n[4] - 2 * p44;
-    const int Lt = L1 + L2 + L3 + L4;
-    auto left = [&](int j) -> int {  // leftover j (counts 1..4 in count, rank order) -> thread
-        if (j < L1) return blist[1][p17 + j];
-        j -= L1;
-        if (j < L2) return blist[2][p26 + j];
-        j -= L2;
-        if (j < L3) return blist[3][p35 + j];
-        return blist[4][2 * p44 + j - L3];
-    };
-    bool lead = ok;
-    int partner = -1;
-    if (ok && c >= 5 && c <= 7) {
-        const int pc = c == 7 ? p17 : c == 6 ? p26 : p35;
-        if (rank < pc) partner = blist[8 - c][rank];
-    } else if (ok && c <= 4) {
-        const int pc = c == 1 ? p17 : c == 2 ? p26 : c == 3 ? p35 : 2 * p44;
-        if (rank < pc) {
-            if (c < 4 || (rank & 1)) lead = false;  // the 7, 6, 5 (or the even-ranked 4) leads
-            else partner = blist[4][rank + 1];
-        } else {
-            const int j = (c == 1 ? 0 : c == 2 ? L1 : c == 3 ? L1 + L2 : L1 + L2 + L3) + rank - pc;
-            if (j & 1) lead = false;
-            else if (j + 1 < Lt) partner = left(j + 1);
+        __syncthreads();
+        if (tid >= 1 && tid <= 8) {  // one thread per count: offsets over the waves, the block's total
+            int tot = 0;
+            for (int q = 0; q < PAIR_NW; ++q) {
+                const int v = wc[q][tid];
+                wc[q][tid] = tot;
+                tot += v;
+            }
+            nt[tid] = tot;
+        }
+        __syncthreads();
+        if (ok) rank += wc[wv][c];
+        int n[9];
+#pragma unroll
+        for (int b = 1; b <= 8; ++b) n[b] = nt[b];
+        if (ok) blist[c][rank] = (int16_t)tid;
+        __syncthreads();
+        const int p17 = min(n[1], n[7]), p26 = min(n[2], n[6]), p35 = min(n[3], n[5]), p44 = n[4] / 2;
+        const int L1 = n[1] - p17, L2 = n[2] - p26, L3 = n[3] - p35, L4 = n[4] - 2 * p44;
+        const int Lt = L1 + L2 + L3 + L4;
+        auto left = [&](int j) -> int {  // leftover j (counts 1..4 in count, rank order) -> thread
+            if (j < L1) return blist[1][p17 + j];
+            j -= L1;
+            if (j < L2) return blist[2][p26 + j];
+            j -= L2;
+            if (j < L3) return blist[3][p35 + j];
+            return blist[4][2 * p44 + j - L3];
+        };
+        bool lead = ok;
+        int partner = -1;
+        if (ok && c >= 5 && c <= 7) {
+            const int pc = c == 7 ? p17 : c == 6 ? p26 : p35;
+            if (rank < pc) partner = blist[8 - c][rank];
+        } else if (ok && c <= 4) {
+            const int pc = c == 1 ? p17 : c == 2 ? p26 : c == 3 ? p35 : 2 * p44;
+            if (rank < pc) {
+                if (c < 4 || (rank & 1)) lead = false;  // the 7, 6, 5 (or the even-ranked 4) leads
+                else partner = blist[4][rank + 1];
+            } else {
+                const int j = (c == 1 ? 0 : c == 2 ? L1 : c == 3 ? L1 + L2 : L1 + L2 + L3) + rank - pc;
+                if (j & 1) lead = false;
+                else if (j + 1 < Lt) partner = left(j + 1);
+            }
+        }
+        if (!pair) {  // pairing off (SGN_PAIR=0): every sample alone in its half
+            lead = ok;
+            partner = -1;
+        }
+        const uint64_t lm = __ballot(lead);
+        int idx = __popcll(lm & below);
+        if (lane == 0) wl[wv] = __popcll(lm);
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int q = 0; q < PAIR_NW; ++q) tot += wl[q];
+            sbase = tot ? atomicAdd(slot_n, tot) : 0;
+        }
+        for (int q = 0; q < wv; ++q) idx += wl[q];
+        __syncthreads();
+        if (lead) {
+            const int slot = sbase + idx;
+            const int nb = partner >= 0 ? sc[partner] : 0, sb = partner >= 0 ? ss[partner] : 0;
+            int r8[8];
+            const int ob = c > 4 ? c : 4;  // B's first row: never across the 4-row lane-group boundary
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r8[k] = k < c ? s * 8 + k : (k >= ob && k < ob + nb ? sb * 8 + (k - ob) : -1);
+            int4 *rp = (int4 *)(rows + (int64_t)slot * 8);
+            rp[0] = make_int4(r8[0], r8[1], r8[2], r8[3]);
+            rp[1] = make_int4(r8[4], r8[5], r8[6], r8[7]);
+            slots[slot] = make_int4((int)((uint32_t)(rel0 + tid) | ((uint32_t)c << 28)),
+                                    partner >= 0 ? (int)((uint32_t)(rel0 + partner) | ((uint32_t)nb << 28)) : 0, s, sb);
         }
     }
-    if (!pair) {  // pairing off (SGN_PAIR=0): every sample alone in its half
-        lead = ok;
-        partner = -1;
-    }
-    const uint64_t lm = __ballot(lead);
-    int idx = __popcll(lm & below);
-    if (lane == 0) wl[wv] = __popcll(lm);
-    __syncthreads();
-    if (tid == 0) {
-        int tot = 0;
-        for (int q = 0; q < PAIR_NW; ++q) tot += wl[q];
-        sbase = tot ? atomicAdd(slot_n, tot) : 0;
-    }
-    for (int q = 0; q < wv; ++q) idx += wl[q];
-    __syncthreads();
-    if (!lead) return;
-    const int slot = sbase + idx;
-    const int nb = partner >= 0 ? sc[partner] : 0, sb = partner >= 0 ? ss[partner] : 0;
-    int r8[8];
-    const int ob = c > 4 ? c : 4;  // B's first row: never across the 4-row lane-group boundary
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r8[k] = k < c ? s * 8 + k : (k >= ob && k < ob + nb ? sb * 8 + (k - ob) : -1);
-    int4 *rp = (int4 *)(rows + (int64_t)slot * 8);
-    rp[0] = make_int4(r8[0], r8[1], r8[2], r8[3]);
-    rp[1] = make_int4(r8[4], r8[5], r8[6], r8[7]);
-    slots[slot] = make_int4((int)((uint32_t)(rel0 + tid) | ((uint32_t)c << 28)),
-                            partner >= 0 ? (int)((uint32_t)(rel0 + partner) | ((uint32_t)nb << 28)) : 0, s, sb);
 }
 
 // the lane's row of slot `slot` (half of the wave), row kk of the half: rows table -> pidx index v
@@ -2066,7 +2073,8 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
         const int64_t wg = (n + x3::WG_SAMPLES - 1) / x3::WG_SAMPLES;
         if ((stages & 1) && x3_w16()) {
             SGN_CHECK_HIP(hipMemsetAsync(slot_n, 0, 4, st));
-            hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)((n + x3::PAIR_TPB - 1) / x3::PAIR_TPB)),
+            const int64_t pb = (n + x3::PAIR_TPB - 1) / x3::PAIR_TPB;
+            hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)(pb < 1024 ? pb : 1024)),
                                dim3(x3::PAIR_TPB), 0, st, q->counters, q->work, q->samp_nnb, (int32_t)i0, (int32_t)n,
                                pair, rows, slots, slot_n);
             auto kern = ksb == 0 ? x3::k_rows16<0> : ksb == KS_HID ? x3::k_rows16<8> : x3::k_rows16<11>;
