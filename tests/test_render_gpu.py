@@ -392,3 +392,49 @@ def test_paired_rows_bit_identical_to_unpaired(monkeypatch, case):
     assert n_items > 100
     for name, a, b in zip(("rgb", "opacity", "bg_transmission", "feat", "blend"), on, off):
         assert torch.equal(a, b), name
+
+
+def test_pair_slots_tables():
+    """k_pair_slots' tables after a config-2-like room frame (white box: the f32 aggregate workspace
+    is [f_s 1 KiB | rows 32 B | entry 16 B] per item + a 2-KiB tail holding the slot count): every work
+    item is sample A or B of exactly one slot, nA + nB <= 8, B's rows start at max(nA, 4), the row
+    table holds s * 8 + k for exactly the sample's valid neighbour slots (pidx >= 0) and -1 elsewhere,
+    and pairing packs the frame into fewer slots than work items."""
+    pc = small_room(300_000, seed=5)
+    mlp = init_mlp(5, bias_std=0.01)
+    view = make_view(96, 128, yaw=200.0, pitch=-10.0)
+    pts = dict(xyz=pc.xyz, embedding=pc.embedding, color=pc.color, dir=pc.dir, conf=pc.conf)
+    r, out = _render(pts, mlp, view, HotPathOpts(SR=64))
+    q = out.query
+    nw = int(q.counters[1])
+    ws = r.agg_ws
+    wsi = (ws.numel() - 2048) // (1024 + 48)
+    ns = int(ws[-2048:-2044].view(torch.int32).item())
+    rows = ws[wsi * 1024: wsi * 1056].view(torch.int32).cpu().numpy().reshape(-1, 8)[:ns]
+    ent = ws[wsi * 1056: wsi * 1072].view(torch.int32).cpu().numpy().reshape(-1, 4)[:ns]
+    work = q.work[:nw].cpu().numpy()
+    nnb = q.samp_nnb.cpu().numpy()
+    pidx = q.pidx.cpu().numpy()
+    assert 0 < ns < nw
+    seen = np.zeros(nw, np.int32)
+    for j in range(ns):
+        ea, eb, sa, sb = (int(x) & 0xFFFFFFFF for x in ent[j])
+        ia, na, ib, nb_ = ea & 0x0FFFFFFF, ea >> 28, eb & 0x0FFFFFFF, eb >> 28
+        assert work[ia] == sa and na == nnb[sa] and 1 <= na <= 8
+        seen[ia] += 1
+        want = [sa * 8 + k if k < na else -1 for k in range(8)]
+        if nb_:
+            assert work[ib] == sb and nb_ == nnb[sb] and na + nb_ <= 8
+            seen[ib] += 1
+            ob = max(na, 4)
+            assert ob + nb_ <= 8
+            for k in range(nb_):
+                want[ob + k] = sb * 8 + k
+        assert list(rows[j]) == want, j
+        for v in want:
+            if v >= 0:
+                assert pidx[v] >= 0
+    assert (seen == 1).all()
+    # the valid slots of every work item are a prefix of its K slots (what the pairing relies on)
+    pw = pidx[(work[:, None] * 8 + np.arange(8)[None, :])]
+    assert ((pw >= 0) == (np.arange(8)[None, :] < nnb[work][:, None])).all()
