@@ -1726,24 +1726,30 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
     __syncthreads();
     int slot = 0;
     dma_chunk<NetColor16, 0, NW16>(wb, lds, w, lane, 0);
-    // the tile's f_s rows, sample ids and ray directions; the next tile's are loaded during colour 1
+    // The tile's f_s rows and sample ids, then its ray ids, then its ray directions: the next tile's
+    // rows and sample ids go out in colour 1, its ray ids in colour 2 and its directions in its own
+    // colour 0 (needed by colour 0's last k-step), each step one chunk after the load it depends on,
+    // so no hook waits on a dependent load
     f32x4 fr[16];
     float vd[3];
-    int sn = 0;
+    int sn = 0, rn = 0;
     auto load_rows = [&](int item) {
         const bool ok = item < end;
         sn = ok ? a.work[item] : 0;
-        const int ray = a.samp_ray[sn];
         const f32x4 *row = (const f32x4 *)(a.fs + (int64_t)(ok ? item - a.item0 : 0) * HID + 8 * g);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             fr[2 * k] = row[8 * k];
             fr[2 * k + 1] = row[8 * k + 1];
         }
+    };
+    auto load_ray = [&]() { rn = a.samp_ray[sn]; };
+    auto load_dir = [&]() {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) vd[c] = a.raydir[(int64_t)ray * 3 + c];
+        for (int c = 0; c < 3; ++c) vd[c] = a.raydir[(int64_t)rn * 3 + c];
     };
     load_rows(a.item0 + blockIdx.x * (16 * NW16) + w * 16 + r);
+    load_ray();
     for (int base = a.item0 + blockIdx.x * (16 * NW16); base < end; base += gridDim.x * (16 * NW16)) {
         int lz = 0;
         asm volatile("" : "+s"(lz));
@@ -1752,7 +1758,6 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
         const int item = base + w * 16 + r;
         const bool sval = item < end;
         const int s = sn;
-        const float v3[3] = {vd[0], vd[1], vd[2]};
         auto bias = [&](f32x4 (&ac)[8], int yb) {
 #pragma unroll
             for (int t = 0; t < 8; ++t) ac[t] = *(const f32x4 *)(Yl + yb + 16 * t + 4 * g);
@@ -1782,13 +1787,15 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int c = 8 * g + j, cc = c % 12, d = cc >> 2, f = cc & 3;
-                    const float x = d == 0 ? v3[0] : d == 1 ? v3[1] : v3[2];
+                    const float x = d == 0 ? vd[0] : d == 1 ? vd[1] : vd[2];
                     float sv, cv;
                     sincos_acc(__builtin_ldexpf(x, f), sv, cv);
                     v[j] = c < 12 ? sv : c < 24 ? cv : 0.f;
                 }
             }
             return split8(v);
+        }, [&](auto c) {
+            if constexpr (decltype(c)::value == 0) load_dir();  // this tile's directions (k-step 8)
         });
         bias(c1, Y_CB1);
         const float inv4 = Yl[Y_INV + 4], inv5 = Yl[Y_INV + 5], inv6 = Yl[Y_INV + 6];
@@ -1796,19 +1803,24 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
         run_layer16<NetColor16, 1>(wb, ldsi, slot, w, lane, lz, c1, [&](auto k) { return chain(c0, inv4, k); },
                                    [&](auto) { load_rows(item + gridDim.x * (16 * NW16)); });
         bias(c0, Y_CB2);
-        run_layer16<NetColor16, 2>(wb, ldsi, slot, w, lane, lz, c0, [&](auto k) { return chain(c1, inv5, k); });
-        // output layer: units 16 t + 4 g + i of this lane, summed over the 4 lane groups
+        run_layer16<NetColor16, 2>(wb, ldsi, slot, w, lane, lz, c0, [&](auto k) { return chain(c1, inv5, k); },
+                                   [&](auto) { load_ray(); });  // the next tile's ray ids
+        // output layer: units 16 t + 4 g + i of this lane, summed over the 4 lane groups (the four
+        // weights of a (t, c) as one 16-B LDS read: this file is built without SLP vectorisation)
         float o[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
+        for (int t = 0; t < 8; ++t) {
+            f32x4 wc[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) wc[c] = *(const f32x4 *)(Yl + Y_CW3 + 128 * c + 16 * t + 4 * g);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int u = 16 * t + 4 * g + i;
                 const float y = c0[t][i] * inv6;
                 const float hv = fmaxf(y, 0.01f * y);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) o[c] = __builtin_fmaf(Yl[Y_CW3 + 128 * c + u], hv, o[c]);
+                for (int c = 0; c < 3; ++c) o[c] = __builtin_fmaf(wc[c][i], hv, o[c]);
             }
+        }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             float x = o[c] + __shfl_xor(o[c], 16);
