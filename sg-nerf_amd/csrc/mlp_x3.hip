@@ -998,7 +998,11 @@ __global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
 
 // ---- per-neighbour rows (16x16) -------------------------------------------------------------
 constexpr int WG16_SAMPLES = NW16 * 2;            // 16 samples = 128 rows per workgroup tile
-constexpr int ROWS16_LDS = Y_LDS_OFF + N_Y32 * 4;
+#ifndef SGN_X3_YT
+#define SGN_X3_YT 1  // block3.2 bias / alpha weights transposed per lane (16-B LDS reads in the epilogue)
+#endif
+constexpr int YT16_OFF = Y_LDS_OFF + N_Y32 * 4;  // [unit r][20] b3 (t = 0..15) then [r][20] alpha w
+constexpr int ROWS16_LDS = YT16_OFF + (SGN_X3_YT ? 2 * 16 * 20 * 4 : 0);
 static_assert(ROWS16_LDS <= 163840, "LDS budget (16x16 rows)");
 
 // row r's point record, its sample position and view direction (+ the caller's pers
@@ -1282,6 +1286,14 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         const float *src = (const float *)((const char *)a.blob + OFF16_F32);
         float *dst = (float *)(lds + Y_LDS_OFF);
         for (int i = threadIdx.x; i < N_Y32; i += TPB16) dst[i] = src[i];
+        if constexpr (SGN_X3_YT) {
+            // row stride 20 floats: the 16 lanes' 16-B reads of one column quad hit disjoint banks
+            float *yt = (float *)(lds + YT16_OFF);
+            for (int i = threadIdx.x; i < 512; i += TPB16) {
+                const int which = i >> 8, u = i & 255, t = u >> 4, rr = u & 15;
+                yt[which * 320 + rr * 20 + t] = src[(which ? Y_WA : Y_B3) + 16 * t + rr];
+            }
+        }
     }
     __syncthreads();
     int slot = 0;
@@ -1467,10 +1479,17 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
             float *fs_dst = (float *)a.fs + (int64_t)((uint32_t)((g & 1) ? ce.y : ce.x) & 0x0FFFFFFFu) * HID + r;
             // the next tile's P rows (see accA) go out tile by tile between the epilogue's VALU work
             const float *psrc = proj + (int64_t)(nx.pid < 0 ? 0 : nx.pid) * HID + 4 * g;
+            f32x4 bu4 = {}, wa4 = {};
+            const float *ytb = (const float *)(ldsi + YT16_OFF) + r * 20;
 #pragma unroll
             for (int t = 0; t < 16; ++t) {
                 acc2[t] = *(const f32x4 *)(psrc + 16 * t);
-                const float bu = Yl[Y_B3 + 16 * t + r], wau = Yl[Y_WA + 16 * t + r];
+                if (SGN_X3_YT && (t & 3) == 0) {
+                    bu4 = *(const f32x4 *)(ytb + t);
+                    wa4 = *(const f32x4 *)(ytb + 320 + t);
+                }
+                const float bu = SGN_X3_YT ? bu4[t & 3] : Yl[Y_B3 + 16 * t + r];
+                const float wau = SGN_X3_YT ? wa4[t & 3] : Yl[Y_WA + 16 * t + r];
                 float fa = 0.f, fb = 0.f;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
