@@ -314,7 +314,7 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
 
     def frame(i, marks=None, count=False):
         out = r.render(cams[i][0], cams[i][1], rays[i], views[i].near, views[i].far, want_opacity=True, marks=marks,
-                       count_traffic=count, **sem[i])
+                       count_traffic=count, check_range="deferred", **sem[i])
         if gathered is not None:
             b = i & 1
             if rgb_bufs[b] is None:
@@ -334,6 +334,7 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
     def drain():
         if comm is not None:
             torch.cuda.current_stream().wait_stream(comm)
+        r.finish()   # the fp16-range guard of the frames rendered so far (raises if one failed)
 
     for i in range(warmup):
         frame(i)

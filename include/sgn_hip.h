@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 4
+#define SGN_ABI_VERSION 5
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -200,7 +200,9 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
  * 2^-s (w_hi x_hi + w_hi x_lo + w_lo x_hi) with fp32 accumulation (w pre-scaled by a per-layer
  * power of two 2^s; x = x_hi + x_lo), positional encodings from accurate sinf/cosf.  The results
  * agree with an fp32 evaluation to a few fp32 ulps of sum |w x| per layer.  Hidden activations
- * must stay inside fp16 range (|x| < 65504).  bpnet_layers / bpnet_dim select the SG-NeRF
+ * must stay inside fp16 range (|x| < 65504): one outside it makes the sample's decoded features
+ * non-finite, which the colour stage records in a flag of the workspace (never returned silently:
+ * sgn_aggregate_check_f32 reports it).  bpnet_layers / bpnet_dim select the SG-NeRF
  * block2_bpnet variant as in sgn_mlp_pack_sg (0/0 = base ScanNet viewmlp).
  *   sgn_mlp_pack_f32        : 9 (+ block2_bpnet.0) layers as sgn_mlp_pack_sg -> blob of
  *                             sgn_mlp_packed_bytes_f32(bpnet_layers, bpnet_dim) bytes (0: unsupported)
@@ -215,6 +217,11 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
  *                             reads q->samp_nnb (valid neighbours are a prefix of each sample's K
  *                             slots, as sgn_query writes them); optional d_out_blend / d_out_wnorm are
  *                             zeroed by stage 1 before the valid rows are written
+ *   sgn_aggregate_check_f32 : synchronises `stream` and returns -1 (sgn_last_error says why) when a
+ *                             sample of the last colour stage run on this workspace had non-finite
+ *                             decoded features (an activation outside fp16 range); 0 otherwise
+ *   sgn_aggregate_flag_offset_f32 : byte offset of that int32 flag inside the workspace (for a
+ *                             caller that reads it asynchronously, e.g. one frame later)
  * 16-byte aligned device buffers. */
 size_t sgn_mlp_packed_bytes_f32(int32_t bpnet_layers, int32_t bpnet_dim);
 int sgn_mlp_pack_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,
@@ -226,6 +233,8 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
                       const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
                       const void *d_packed_mlp, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
                       void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream);
+int sgn_aggregate_check_f32(const void *d_workspace, size_t workspace_bytes, sgn_stream_t stream);
+size_t sgn_aggregate_flag_offset_f32(size_t workspace_bytes);
 
 /* ---- training: forward with saved activations + backward ---
  * Gradients of PointAggregator.forward / viewmlp (point_aggregators.py:868-959, :561-786)

@@ -1,8 +1,8 @@
 // mlp_x3.hip -- fp32-faithful neural-point aggregator on fp16 MFMA (gfx950): every fp32
 // product of the reference's nn.Linear layers is carried as three fp16 MFMA products.
 //
-// Same path as mlp.hip (NeuralPoints gather neural_points.py:942-988, PointAggregator.forward /
-// viewmlp point_aggregators.py:868-959, :561-786), at the reference's arithmetic precision:
+// Path: NeuralPoints gather (neural_points.py:942-988), PointAggregator.forward / viewmlp
+// (point_aggregators.py:868-959, :561-786), at the reference's arithmetic precision:
 //
 //   w = 2^-s (w_hi + w_lo), x = x_hi + x_lo, all four fp16; w x ~ 2^-s (w_hi x_hi + w_hi x_lo + w_lo x_hi)
 //
@@ -11,18 +11,23 @@
 // epilogue multiplies by 2^-s exactly.  Per product the representation error is <= 2^-22 |w x|
 // (+ 2^-25 |w| for activations below fp16's normal range), the dropped w_lo x_lo term <= 2^-22
 // |w x|: the layer sums agree with an fp32 evaluation to a few fp32 ulps of sum |w x|.
-// Activations must stay inside fp16's range (|x| < 65504) -- the MLP's hidden features do.
-// The positional encodings use the accurate sinf/cosf of the scaled argument (x 2^f is exact),
-// as torch.sin does (networks.py:175-192).  dtype of this path: "f32 (3xf16 split MFMA, fp32
+// Activations must stay inside fp16's range (|x| < 65504): an activation outside it turns into
+// inf / NaN in the MFMA operands, which k_color16 detects on the sample's decoded features and
+// reports through the sticky range flag (counters[3], sgn_aggregate_check) -- never silently.
+// The positional encodings use accurate sin/cos of the scaled argument (x 2^f is exact), as
+// torch.sin does (networks.py:175-192).  dtype of this path: "f32 (3xf16 split MFMA, fp32
 // accumulate)"; 3 MFMAs per product, so its MFMA ceiling is 1/3 of the fp16 dense peak.
 //
-// Kernels (one wave per SIMD: hi/lo activations of a 32-row tile are 128 registers per layer):
-//   k_point_proj_x3 : P[p] = 2^s0 (W0a [feat | PE(feat)] + b0), fp32 [point][half][tile][16]
-//   k_agg_rows_x3   : 4 waves x 32 rows (4 samples x K = 8): layer 0 (PE(dists) part) on top of
-//                     P[pid], block1.2, block3.0, block3.2 (transposed), alpha, K-blend -> f_s fp32
-//   k_color_x3      : 4 waves x 32 samples: [f_s | PE(viewdir)] -> 128 -> 128 -> 128 -> 3, sigmoid
+// Kernels (v_mfma_f32_16x16x32_f16, 8 waves per 512-thread workgroup, two per SIMD):
+//   k_point_proj16 : P[p] = 2^s0 (W0a [feat | PE(feat)] + b0) fp32 [256] + the packed 64-B point
+//                    record, once per point-cloud version
+//   k_pair_slots   : packs two samples whose neighbour counts sum to <= 8 into one 8-row half
+//   k_rows16       : 16 samples x 8 neighbours per tile: block1.0's PE(dists) part on top of
+//                    P[pid], block1.2, (block2_bpnet), block3.0, block3.2 (transposed), alpha,
+//                    K-blend -> f_s fp32
+//   k_color16      : 8 waves x 16 samples: [f_s | PE(viewdir)] -> 128 -> 128 -> 128 -> 3, sigmoid
 // Weight fragment pairs (hi, lo) stream through a 2-slot LDS ring of 64-KiB chunks filled by
-// LDS-DMA, shared by the workgroup's 4 waves (the mlp.hip scheme with 2-KiB pairs).
+// LDS-DMA, shared by the workgroup's 8 waves.
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -35,8 +40,7 @@ namespace sgn {
 namespace {
 namespace x3 {
 
-constexpr int NW = 4;             // waves per workgroup (one per SIMD)
-constexpr int TPB = NW * 64;
+constexpr int NW16 = 8, TPB16 = NW16 * 64;
 constexpr int PAIR = 2048;        // hi fragment (1 KiB) then lo fragment (1 KiB)
 constexpr int SLOT_PAIRS = 32;
 constexpr int SLOT = SLOT_PAIRS * PAIR;  // 64 KiB
@@ -47,76 +51,17 @@ constexpr int NSLOT = 2;
 #ifndef SGN_X3_PIN
 #define SGN_X3_PIN 1
 #endif
-#ifndef SGN_X3_SPREAD
-#define SGN_X3_SPREAD 1  // next chunk's LDS-DMA pieces interleaved with the current chunk's MFMAs
-#endif
 #ifndef SGN_X3_SPREAD_DIV
 #define SGN_X3_SPREAD_DIV 2  // DMA pieces spread over the first NF / DIV pairs of a chunk
 #endif
-#ifndef SGN_X3_EPI_BARRIER
-#define SGN_X3_EPI_BARRIER 0  // 1: scheduling barrier after each layer epilogue
-#endif
-#ifndef SGN_X3_TP8
-#define SGN_X3_TP8 0  // 1: block1.2 and block3.2 as one pass over all 8 output tiles
-#endif
-constexpr int TPL = SGN_X3_TP8 ? 8 : 4, NPL = 8 / TPL, KCL = SGN_X3_TP8 ? 4 : 8;  // block1.2 / block3.2 passes
-#ifndef SGN_X3_PF
-#define SGN_X3_PF 0  // 1: next tile's P rows loaded during the previous tile's last chunk (spills)
-#endif
 constexpr int PD = SGN_X3_PD;     // fragment pairs in flight per wave (LDS -> VGPR queue)
-
-// ---- blob layout (byte offsets) ------------------------------------------------------
-// pair f of a layer with np passes of tp tiles and ks k-steps: f = (P ks + k) tp + t, output
-// tile P tp + t (k-outer stream order inside a pass, as mlp.hip)
-constexpr uint32_t OFF_W0B = 0;                              // block1.0 PE(dists) part: 4 ks x 8 tiles
-constexpr uint32_t OFF_W1 = OFF_W0B + 32 * PAIR;             // block1.2: 2 x 16 x 4
-constexpr uint32_t OFF_W2 = OFF_W1 + 128 * PAIR;             // block3.0: 2 x 17 x 4
-constexpr uint32_t OFF_W3 = OFF_W2 + 136 * PAIR;             // block3.2: 2 x 16 x 4 (transposed use)
-constexpr uint32_t OFF_C0 = OFF_W3 + 128 * PAIR;             // colour 0: 1 x 18 x 4
-constexpr uint32_t OFF_C1 = OFF_C0 + 72 * PAIR;              // colour 1: 1 x 8 x 4
-constexpr uint32_t OFF_C2 = OFF_C1 + 32 * PAIR;              // colour 2: 1 x 8 x 4
-constexpr uint32_t OFF_W0A = OFF_C2 + 32 * PAIR;             // block1.0 per-point part: 1 x 14 x 8
-constexpr uint32_t OFF_XF32 = OFF_W0A + 112 * PAIR;
-// fp32 section: mlp_layout.h's F_* vectors (biases of MFMA layers pre-scaled by 2^s, block3.2
-// bias natural and unscaled) + the inverse scales 2^-s of the MFMA layers + block2_bpnet's bias
-constexpr int XF_INV = (int)N_F32;  // [0] block1.0 [1] block1.2 [2] block3.0 [3] block3.2 [4..6] colour 0..2 [7] block2_bpnet
-constexpr int XF_BB = XF_INV + 8;   // block2_bpnet.0 bias (acc order, scaled; SG only)
-constexpr int N_XF32 = XF_BB + HID;
-constexpr size_t BLOB_BYTES = OFF_XF32 + (size_t)N_XF32 * 4;
-// SG-NeRF block2_bpnet.0 (Linear(256 + bpnet_dim -> 256), point_aggregators.py:345-354, :629-636):
-// 2 passes x KSB k-steps x 4 tiles after the base blob; k-steps 0..15 the chained block1 output,
-// 16.. the gathered fp32 BPNet embedding (channel 16 (k - 16) + 8 h + e, natural order)
-constexpr uint32_t OFF_WB = (uint32_t)((BLOB_BYTES + PAIR - 1) / PAIR * PAIR);
-__host__ __device__ constexpr size_t blob_bytes_sg(int ksb);  // all sections (defined with the 16x16 layout)
-constexpr size_t PROJ_BYTES_PER_POINT = HID * 4;  // fp32 [half][tile][16]
-
+constexpr size_t PROJ_BYTES_PER_POINT = HID * 4;  // P row: fp32 [256], natural unit order
 struct XL {
     int ks, tp, np, kc;
     uint32_t off;
 };
 __host__ __device__ constexpr int nch(XL l) { return (l.ks + l.kc - 1) / l.kc; }
 __host__ __device__ constexpr int nk(XL l, int c) { return l.ks - c * l.kc < l.kc ? l.ks - c * l.kc : l.kc; }
-
-// A "net" is the ordered list of layers one kernel streams per work tile.
-struct NetRows {
-    static constexpr int NL = 4;
-    static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, TPL, NPL, KCL, OFF_W1}, {17, 4, 2, 6, OFF_W2},
-                                 {16, TPL, NPL, KCL, OFF_W3}};
-};
-template <int KSB>
-struct NetRowsSG {
-    static constexpr int NL = 5;
-    static constexpr XL L[NL] = {{4, 8, 1, 4, OFF_W0B}, {16, TPL, NPL, KCL, OFF_W1}, {KSB, 4, 2, 8, OFF_WB},
-                                 {17, 4, 2, 6, OFF_W2}, {16, TPL, NPL, KCL, OFF_W3}};
-};
-struct NetColor {
-    static constexpr int NL = 3;
-    static constexpr XL L[NL] = {{18, 4, 1, 8, OFF_C0}, {8, 4, 1, 8, OFF_C1}, {8, 4, 1, 8, OFF_C2}};
-};
-struct NetProj {
-    static constexpr int NL = 1;
-    static constexpr XL L[NL] = {{14, 8, 1, 4, OFF_W0A}};
-};
 
 template <class Net>
 struct Sched {
@@ -133,11 +78,6 @@ struct Sched {
     }
     static constexpr int pairs(int n) { return nk(Net::L[cl(n)], cc(n)) * Net::L[cl(n)].tp; }
 };
-static_assert(Sched<NetRows>::total() == 15 && Sched<NetRows>::pairs(0) == 32 && Sched<NetRows>::pairs(7) == 20,
-              "row stream");
-static_assert(Sched<NetColor>::total() == 5 && Sched<NetColor>::pairs(2) == 8, "colour stream");
-static_assert(Sched<NetProj>::total() == 4 && Sched<NetProj>::pairs(3) == 16, "projection stream");
-
 struct X3B {
     h8 hi, lo;
 };
@@ -168,8 +108,8 @@ __device__ __forceinline__ X3B split8(const float (&v)[8]) {
 }
 
 // Timing build (SGN_X3_TIMING): wave w of the first TD_BLOCKS workgroups stamps the clock at the
-// kernel's phase points into tdbg[(block * NW + w) * TD_EV + seq] (tools/x3_timing.py reads it).
-constexpr int TD_BLOCKS = 8, TD_EV = 2048;
+// kernel's phase points into tdbg[(block * NW16 + w) * TD_EV + seq] (tools/x3_timing16.py reads it).
+[[maybe_unused]] constexpr int TD_BLOCKS = 8, TD_EV = 2048;
 struct TStamp {
     unsigned long long *buf;
     int seq;
@@ -194,7 +134,7 @@ __device__ __forceinline__ void lds_dma_1k(const WBlob &wb, char *dst, int lane,
 
 // LDS-DMA of stream chunk N into `dst`: 2 * pairs 1-KiB pieces, wave w (of NWv) moves pieces
 // w + NWv j
-template <class Net, int N, int NWv = NW>
+template <class Net, int N, int NWv = NW16>
 __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
     using S = Sched<Net>;
     constexpr int nf = 2 * S::pairs(N);
@@ -207,7 +147,7 @@ __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int
 }
 
 // piece J (of this wave's ceil(2 pairs / NWv)) of chunk N
-template <class Net, int N, int J, int NWv = NW>
+template <class Net, int N, int J, int NWv = NW16>
 __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int lane, int lz) {
     using S = Sched<Net>;
     constexpr int nf = 2 * S::pairs(N);
@@ -215,16 +155,16 @@ __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int
     if (NWv * (J + 1) <= nf || i < nf)  // wave-uniform
         lds_dma_1k(wb, dst + i * 1024, lane, S::off(N) + (uint32_t)(i * 1024 + lz));
 }
-template <class Net, int N, int NWv = NW>
+template <class Net, int N, int NWv = NW16>
 constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NWv - 1) / NWv; }
 
 // chunk boundary: this wave's DMAs of chunk N landed, LDS reads drained, barrier; then chunk N+1
-// goes into the slot every wave finished reading one chunk ago (here, or spread over the chunk's
-// MFMAs by run_pass with SGN_X3_SPREAD)
+// goes into the slot every wave finished reading one chunk ago (its pieces are spread over the
+// chunk's MFMAs by run_layer16)
 // VM: vector-memory operations this wave is guaranteed to have issued after its last DMA piece of
 // the chunk being entered (loads placed at the end of the previous chunk, stores): they may stay in
 // flight across the boundary (vmcnt retires in order, so the DMA has landed once at most VM remain)
-template <class Net, int N, int NWv = NW, int VM = 0>
+template <class Net, int N, int NWv = NW16, int VM = 0>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz,
                                             TStamp *ts = nullptr) {
 #ifndef SGN_X3_ABLATE_BARRIER  // timing experiment only: no boundary waits / barrier (wrong results)
@@ -241,8 +181,6 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot
 #else
     (void)ts;
 #endif
-    if constexpr (!SGN_X3_SPREAD)
-        dma_chunk<Net, (N + 1) % Sched<Net>::total(), NWv>(wb, lds + (slot ^ 1) * SLOT, w, lane, lz);
 }
 
 struct NoHook {
@@ -254,97 +192,6 @@ struct VmZero {
     static constexpr int vm(int) { return 0; }
 };
 
-
-
-// One pass of layer L, k-outer: acc[t] += W[tp P + t] in(k) over the pass's chunks, three
-// MFMAs per (k-step, tile).  TRANS: activations are the A operand (accumulators hold D^T).
-// The accumulators arrive initialised (bias, P, or zero).  post(integral_constant C) runs right
-// after the boundary of every chunk C of the pass.
-template <class Net, int L, int P, bool TRANS = false, class InFn, class PostFn = NoHook>
-__device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
-                                         f32x16 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{},
-                                         TStamp *ts = nullptr) {
-    constexpr XL ly = Net::L[L];
-    constexpr int TP = ly.tp;
-    static_for<nch(ly)>([&](auto cc) {
-        constexpr int C = decltype(cc)::value;
-        constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
-        chunk_enter<Net, N>(wb, lds, slot, w, lane, lz, ts);
-        post(cc);
-        const char *sl = lds + slot * SLOT;
-        char *dnext = lds + (slot ^ 1) * SLOT;
-        constexpr int NF = nk(ly, C) * TP;
-        constexpr int PW = dma_pieces<Net, NN>();  // this wave's pieces of the next chunk
-        auto frag = [&](int f, int part) { return *(const h8 *)(sl + (2 * f + part) * 1024 + lane * 16); };
-        h8 fh[PD], fl[PD];
-#pragma unroll
-        for (int f = 0; f < PD; ++f) {
-            fh[f] = frag(f, 0);
-            fl[f] = frag(f, 1);
-        }
-#if SGN_X3_PIN
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
-#endif
-        static_for<nk(ly, C)>([&](auto kk) {
-            constexpr int KK = decltype(kk)::value;
-            const X3B B = in(std::integral_constant<int, C * ly.kc + KK>{});
-            static_for<TP>([&](auto tt) {
-                constexpr int t = decltype(tt)::value, F = KK * TP + t;
-                const h8 Ah = fh[F % PD], Al = fl[F % PD];
-                if constexpr (F + PD < NF) {
-                    fh[F % PD] = frag(F + PD, 0);
-                    fl[F % PD] = frag(F + PD, 1);
-                }
-                if constexpr (TRANS) {
-                    acc[t] = mfma32(B.hi, Ah, acc[t]);
-                    acc[t] = mfma32(B.lo, Ah, acc[t]);
-                    acc[t] = mfma32(B.hi, Al, acc[t]);
-                } else {
-                    acc[t] = mfma32(Ah, B.hi, acc[t]);
-                    acc[t] = mfma32(Ah, B.lo, acc[t]);
-                    acc[t] = mfma32(Al, B.hi, acc[t]);
-                }
-                if constexpr (SGN_X3_SPREAD) {  // pieces [F PW / NS, (F + 1) PW / NS) after pair F < NS
-                    constexpr int NS = NF / SGN_X3_SPREAD_DIV > 0 ? NF / SGN_X3_SPREAD_DIV : 1;
-                    if constexpr (F < NS) {
-                        static_for<(F + 1) * PW / NS - F * PW / NS>([&](auto jj) {
-                            dma_piece<Net, NN, F * PW / NS + decltype(jj)::value>(wb, dnext, w, lane, lz);
-                        });
-                    }
-                }
-#if SGN_X3_PIN
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-#endif
-            });
-        });
-        slot ^= 1;
-        __builtin_amdgcn_sched_barrier(0);
-    });
-}
-
-// accumulators (2^s units) -> LeakyReLU(2^-s acc) as next-layer B fragments (hi/lo), tiles
-// TP*P.. -> k-steps 2t, 2t+1 (the chained k order is folded into the packed weights)
-template <int TP, int P, int NOUT>
-__device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], float inv, X3B (&out)[NOUT]) {
-    if constexpr (SGN_X3_EPI_BARRIER) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int tt = 0; tt < TP; ++tt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float y = acc[tt][8 * s2 + e] * inv;
-                v[e] = fmaxf(y, 0.01f * y);
-            }
-            out[2 * (TP * P + tt) + s2] = split8(v);
-        }
-    if constexpr (SGN_X3_EPI_BARRIER) __builtin_amdgcn_sched_barrier(0);
-}
 
 #ifndef SGN_X3_FASTSC
 #define SGN_X3_FASTSC 1
@@ -379,396 +226,6 @@ template <int F>
 __device__ __forceinline__ void sincos_f(float x, float &s, float &c) {
     sincos_acc(x * (float)(1 << F), s, c);
 }
-
-// ---- per-point block1.0 projection ------------------------------------------------------
-struct ProjArgs {
-    const float *emb;
-    int64_t n;
-    const void *blob;
-    float *proj;
-};
-
-constexpr int LDS_F32_OFF = NSLOT * SLOT;
-constexpr int PROJ_LDS = LDS_F32_OFF + N_XF32 * 4;
-
-__global__ __launch_bounds__(TPB, 1) void k_point_proj_x3(ProjArgs a) {
-    __shared__ __attribute__((aligned(16))) char lds[PROJ_LDS];
-    const int lane = threadIdx.x & 63, h = lane >> 5;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const WBlob wb = make_blob(a.blob, BLOB_BYTES);
-    {
-        const float *src = (const float *)((const char *)a.blob + OFF_XF32);
-        float *dst = (float *)(lds + LDS_F32_OFF);
-        for (int i = threadIdx.x; i < N_XF32; i += TPB) dst[i] = src[i];
-    }
-    __syncthreads();
-    int slot = 0;
-    dma_chunk<NetProj, 0>(wb, lds, w, lane, 0);
-    const int64_t ntile = (a.n + 32 * NW - 1) / (32 * NW);
-    for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-        int lz = 0;
-        asm volatile("" : "+s"(lz));
-        const float *Fl = (const float *)(lds + lz + LDS_F32_OFF);
-        const int64_t p = tile * (32 * NW) + w * 32 + (lane & 31);
-        const bool ok = p < a.n;
-        float feat[16];
-        {
-            const f32x4 *e4 = (const f32x4 *)(a.emb + (ok ? p : 0) * 32 + 16 * h);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 v = e4[g];
-                feat[4 * g] = v[0]; feat[4 * g + 1] = v[1]; feat[4 * g + 2] = v[2]; feat[4 * g + 3] = v[3];
-            }
-        }
-        // channels 16..111 of the lane-half: PE(feat) (mlp_layout.h l0 order): m = c - 16,
-        // d = m / 6, f = (m % 6) / 2, sin for even m, cos for odd
-        float pe[96];
-        static_for<16>([&](auto dd) {
-            constexpr int d = decltype(dd)::value;
-            static_for<3>([&](auto ff) {
-                constexpr int f = decltype(ff)::value;
-                float s, c;
-                sincos_f<f>(feat[d], s, c);
-                pe[d * 6 + 2 * f] = s;
-                pe[d * 6 + 2 * f + 1] = c;
-            });
-        });
-        f32x16 acc[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const f32x4 *b = (const f32x4 *)(Fl + F_B0 + (t * 2 + h) * 16);
-            const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
-            acc[t] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
-                            b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
-        }
-        run_pass<NetProj, 0, 0>(wb, lds + lz, slot, w, lane, lz, acc, [&](auto k) {
-            constexpr int K = decltype(k)::value;
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int c = 8 * K + e;
-                v[e] = c < 16 ? feat[c < 16 ? c : 0] : pe[c >= 16 ? c - 16 : 0];
-            }
-            return split8(v);
-        });
-        if (ok) {
-            f32x4 *dst = (f32x4 *)(a.proj + p * HID + h * 128);  // [half][tile][16]
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    dst[t * 4 + g] = f32x4{acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]};
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---- per-neighbour rows --------------------------------------------------------------
-constexpr int WG_SAMPLES = NW * 4;  // 16 samples x 8 neighbours = 128 rows per workgroup tile
-constexpr int FSW_OFF = LDS_F32_OFF + N_XF32 * 4;
-constexpr int FSW_BYTES = NW * 2048;  // [wave][4 samples][128 units] fp32 (one block3.2 pass)
-constexpr int ROWS_LDS = FSW_OFF + FSW_BYTES;
-static_assert(ROWS_LDS <= 163840, "LDS budget");
-
-__device__ __forceinline__ void load_proj_x3(const float *proj, int pid, int lane, f32x16 (&pv)[8]) {
-    const int h = lane >> 5;
-    const f32x16 *src = (const f32x16 *)(proj + (int64_t)(pid < 0 ? 0 : pid) * HID + h * 128);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) pv[t] = src[t];
-}
-
-// PE(dists) of a lane-half: local channels 112..141 (mlp_layout.h): m = c - 112, dd = m / 10,
-// f = (m % 10) / 2, sin for even m, cos for odd; 142, 143 zero -> 4 k-steps (KS_P0..KS_P0+3)
-__device__ __forceinline__ void pe_dists(const float (&dist)[3], X3B (&B)[4]) {
-    float v[32];
-    static_for<3>([&](auto d3) {
-        constexpr int dd = decltype(d3)::value;
-        static_for<5>([&](auto ff) {
-            constexpr int f = decltype(ff)::value;
-            float s, c;
-            sincos_f<f>(dist[dd], s, c);
-            v[dd * 10 + 2 * f] = s;
-            v[dd * 10 + 2 * f + 1] = c;
-        });
-    });
-    v[30] = 0.f;
-    v[31] = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float u[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) u[e] = v[8 * k + e];
-        B[k] = split8(u);
-    }
-}
-
-// KSB: k-steps of block2_bpnet.0 (0: base ScanNet viewmlp; 16: SG with bpnet_dim 0; 22: bpnet_dim 96)
-template <int KSB>
-__global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
-    using Net = std::conditional_t<(KSB > 0), NetRowsSG<KSB>, NetRows>;
-    constexpr int LB = 2, L2 = KSB ? 3 : 2, L3 = KSB ? 4 : 3;  // stream positions of the layers
-    constexpr int NBP = KSB > KS_HID ? KSB - KS_HID : 0;        // BPNet k-steps
-    __shared__ __attribute__((aligned(16))) char lds[ROWS_LDS];
-    const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, kk = lane & 7, q = (lane & 31) >> 3;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwork = a.counters[1];
-    const int end = min(nwork, a.item0 + a.n_items);
-    const Cam cam = load_cam(a.campos, a.rot);
-    const WBlob wb = make_blob(a.blob, blob_bytes_sg(KSB));
-    const __amdgpu_buffer_rsrc_t fs_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.fs, (short)0, 0x7fffffff, 0x00020000);
-    const float *proj = (const float *)a.proj;
-    {
-        const float *src = (const float *)((const char *)a.blob + OFF_XF32);
-        float *dst = (float *)(lds + LDS_F32_OFF);
-        for (int i = threadIdx.x; i < N_XF32; i += TPB) dst[i] = src[i];
-    }
-    __syncthreads();
-    int slot = 0;
-    dma_chunk<Net, 0>(wb, lds, w, lane, 0);
-    RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG_SAMPLES + w * 4 + q, end, lane);
-    asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
-    f32x16 pnext[8];
-    if (SGN_X3_PF && a.item0 + (int)blockIdx.x * WG_SAMPLES < end) load_proj_x3(proj, nx.pid, lane, pnext);
-    const int jl = lane & 31;
-#ifdef SGN_X3_TIMING
-    TStamp tsv{blockIdx.x < TD_BLOCKS && a.tdbg ? a.tdbg + ((int64_t)blockIdx.x * NW + w) * TD_EV : nullptr, 0};
-    TStamp *ts = &tsv;
-#define X3T() tsv(lane)
-#else
-    TStamp *ts = nullptr;
-#define X3T()
-#endif
-
-    for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
-        int lz = 0;
-        asm volatile("" : "+s"(lz));
-        char *ldsi = lds + lz;
-        const float *Fl = (const float *)(ldsi + LDS_F32_OFF);
-        const int item = base + w * 4 + q;
-        const int nitem = item + gridDim.x * WG_SAMPLES;
-        float feat[16], dist[3], extf[8];
-        X3T();  // tile start
-        const RowIn ri = gather_row_f<false>(a, cam, nx, lane, feat, dist, extf);
-        const X3B ext = split8(extf);
-        X3B actA[16], actB[16];
-        {   // block1.0: accumulators start at P[pid] (per-point part), + W0b PE(dists)
-            X3B B0[4];
-            pe_dists(dist, B0);
-            f32x16 acc0[8];
-            if constexpr (!SGN_X3_PF) load_proj_x3(proj, nx.pid, lane, pnext);
-#pragma unroll
-            for (int t = 0; t < 8; ++t) acc0[t] = pnext[t];
-            X3T();  // gather + PE(dists) issued
-            run_pass<Net, 0, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) { return B0[decltype(k)::value]; },
-                                NoHook{}, ts);
-            chain_out<8, 0>(acc0, Fl[XF_INV + 0], actA);
-            X3T();
-        }
-        f32x16 acc[4];
-        auto bias_init = [&](int fb, int P) {
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) {
-                const f32x4 *b = (const f32x4 *)(Fl + fb + ((4 * P + tt) * 2 + h) * 16);
-                const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
-                acc[tt] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
-                                 b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
-            }
-        };
-        // block1.2: 256 -> 256
-        auto inA = [&](auto k) { return actA[decltype(k)::value]; };
-        if constexpr (SGN_X3_TP8) {
-            f32x16 acc8[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const f32x4 *b = (const f32x4 *)(Fl + F_B1 + (t * 2 + h) * 16);
-                const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
-                acc8[t] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
-                                 b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
-            }
-            run_pass<Net, 1, 0>(wb, ldsi, slot, w, lane, lz, acc8, inA, NoHook{}, ts);
-            chain_out<8, 0>(acc8, Fl[XF_INV + 1], actB);
-            X3T();
-            X3T();
-        } else {
-            bias_init(F_B1, 0);
-            run_pass<Net, 1, 0>(wb, ldsi, slot, w, lane, lz, acc, inA, NoHook{}, ts);
-            chain_out<4, 0>(acc, Fl[XF_INV + 1], actB);
-            X3T();
-            bias_init(F_B1, 1);
-            run_pass<Net, 1, 1>(wb, ldsi, slot, w, lane, lz, acc, inA, NoHook{}, ts);
-            chain_out<4, 1>(acc, Fl[XF_INV + 1], actB);
-            X3T();
-        }
-        const int s_next = nitem < end ? a.work[nitem] : 0;
-        if constexpr (KSB > 0) {
-            // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256; the row's fp32 embedding
-            // (channels 16 j + 8 h .. +7 for k-step 16 + j) is gathered and split here
-            X3B bpv[NBP > 0 ? NBP : 1];
-            if constexpr (NBP > 0) {
-                const float *src = a.bpnet32 + (int64_t)(ri.pid < 0 ? 0 : ri.pid) * (NBP * 16) + 8 * h;
-#pragma unroll
-                for (int j = 0; j < NBP; ++j) {
-                    const f32x4 u0 = *(const f32x4 *)(src + 16 * j), u1 = *(const f32x4 *)(src + 16 * j + 4);
-                    const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-                    bpv[j] = split8(v);
-                }
-            }
-            auto inBP = [&](auto k) {
-                constexpr int K = decltype(k)::value;
-                if constexpr (K < 16) return actB[K]; else return bpv[K - 16];
-            };
-            bias_init(XF_BB, 0);
-            run_pass<Net, LB, 0>(wb, ldsi, slot, w, lane, lz, acc, inBP, NoHook{}, ts);
-            chain_out<4, 0>(acc, Fl[XF_INV + 7], actA);
-            X3T();
-            bias_init(XF_BB, 1);
-            run_pass<Net, LB, 1>(wb, ldsi, slot, w, lane, lz, acc, inBP, NoHook{}, ts);
-            chain_out<4, 1>(acc, Fl[XF_INV + 7], actA);
-            X3T();
-        }
-        // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input in actB, or actA after block2_bpnet)
-        auto &in3 = pick<(KSB > 0)>(actA, actB);
-        auto &out3 = pick<(KSB > 0)>(actB, actA);
-        auto inB = [&](auto k) {
-            constexpr int K = decltype(k)::value;
-            if constexpr (K < 16) return in3[K]; else return ext;
-        };
-        bias_init(F_B2, 0);
-        run_pass<Net, L2, 0>(wb, ldsi, slot, w, lane, lz, acc, inB, NoHook{}, ts);
-        nx.sval = nitem < end;
-        nx.s = s_next;
-        nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
-        nx.ray = a.samp_ray[s_next];
-        chain_out<4, 0>(acc, Fl[XF_INV + 2], out3);
-        X3T();
-        bias_init(F_B2, 1);
-        run_pass<Net, L2, 1>(wb, ldsi, slot, w, lane, lz, acc, inB, NoHook{}, ts);
-        asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
-        chain_out<4, 1>(acc, Fl[XF_INV + 2], out3);
-        X3T();
-        // block3.2: 256 -> 256 transposed (lane = output unit j of tile t, register i = row
-        // (i & 3) + 8 (i >> 2) + 4h), alpha partials and the K-blend as per-lane FMAs
-        float wv[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            wv[i] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(
-                                                  ((i & 3) + 8 * (i >> 2) + 4 * h) * 4, __builtin_bit_cast(int, ri.wgt)));
-        float ap[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) ap[i] = 0.f;
-        const float inv3 = Fl[XF_INV + 3];
-        float fsv[2][8];  // blended features of a half: [half][tile tt * 2 + (sample h | h + 2)]
-        // tiles 4 P .. 4 P + 3 of accumulators `ac` (tile index 4 P + tt - T0 in ac)
-        auto l3_epilogue = [&](auto pp, auto &ac, auto t0c) {
-            constexpr int P = decltype(pp)::value, T0 = decltype(t0c)::value;
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) {
-                const int t = 4 * P + tt;
-                const float bu = Fl[F_B3 + 32 * t + jl], wau = Fl[F_WA + 32 * t + jl];
-                float fg[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float y = __builtin_fmaf(ac[4 * P + tt - T0][i], inv3, bu);
-                    const float hv = fmaxf(y, 0.01f * y);
-                    ap[i] = __builtin_fmaf(wau, hv, ap[i]);
-                    fg[i >> 2] = __builtin_fmaf(wv[i], hv, fg[i >> 2]);
-                }
-                float x0 = fg[0], y0 = fg[1], x1 = fg[2], y1 = fg[3];
-                permlane32_swap(x0, y0);
-                permlane32_swap(x1, y1);
-                fsv[P][2 * tt] = x0 + y0;      // sample h
-                fsv[P][2 * tt + 1] = x1 + y1;  // sample h + 2
-            }
-        };
-        // f_s of half P -> LDS transpose -> two 16-B stores per lane (sample L >> 4, 8 units)
-        auto flush_fs = [&](int P) {
-            float *st = (float *)(ldsi + FSW_OFF + w * 2048);
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) {
-                st[h * 128 + 32 * tt + jl] = fsv[P][2 * tt];
-                st[(h + 2) * 128 + 32 * tt + jl] = fsv[P][2 * tt + 1];
-            }
-            const f32x4 v0 = *(const f32x4 *)(st + (lane >> 4) * 128 + 8 * (lane & 15));
-            const f32x4 v1 = *(const f32x4 *)(st + (lane >> 4) * 128 + 8 * (lane & 15) + 4);
-            const int it = base + w * 4 + (lane >> 4);
-            const uint32_t off = it < end ? (uint32_t)((it - a.item0) * HID + 128 * P + 8 * (lane & 15)) * 4 : 0xFFFF0000u;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), fs_rsrc, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v1), fs_rsrc, off, 16, 0);
-        };
-        auto inA3 = [&](auto k) { return out3[decltype(k)::value]; };
-        using I0 = std::integral_constant<int, 0>;
-        using I1 = std::integral_constant<int, 1>;
-        using I4 = std::integral_constant<int, 4>;
-        if constexpr (SGN_X3_TP8) {
-            f32x16 acc8[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) acc8[t] = f32x16{};
-            run_pass<Net, L3, 0, true>(wb, ldsi, slot, w, lane, lz, acc8, inA3, NoHook{}, ts);
-            l3_epilogue(I0{}, acc8, I0{});
-            flush_fs(0);
-            X3T();
-            X3T();
-            l3_epilogue(I1{}, acc8, I0{});
-            flush_fs(1);
-            X3T();
-        } else {
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
-            run_pass<Net, L3, 0, true>(wb, ldsi, slot, w, lane, lz, acc, inA3, NoHook{}, ts);
-            l3_epilogue(I0{}, acc, I0{});
-            X3T();
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) acc[tt] = f32x16{};
-            // pass-0 stores right after pass 1's first boundary (acknowledged one chunk later); the
-            // next tile's P rows after its last boundary, in flight under that chunk's MFMAs
-            run_pass<Net, L3, 1, true>(wb, ldsi, slot, w, lane, lz, acc, inA3, [&](auto c) {
-                if constexpr (decltype(c)::value == 0) flush_fs(0);
-                if constexpr (SGN_X3_PF && decltype(c)::value == nch(Net::L[L3]) - 1) {
-                    if (nx.sval) load_proj_x3(proj, nx.pid, lane, pnext);
-                }
-            }, ts);
-            l3_epilogue(I1{}, acc, I4{});
-            flush_fs(1);
-            X3T();
-        }
-        // alpha: reduce the 16 row partials over the 32 units of each half (mlp.hip's scheme)
-        float bq[8];
-#pragma unroll
-        for (int p2 = 0; p2 < 8; ++p2) {
-            float x = ap[2 * p2], y = ap[2 * p2 + 1];
-            permlane16_swap(x, y);
-            bq[p2] = x + y;
-        }
-        auto rs_step = [&](float lo, float hi, bool upper, auto ctrl) {
-            const float keep = upper ? hi : lo, send = upper ? lo : hi;
-            return keep + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send),
-                                                                             decltype(ctrl)::value, 0xF, 0xF, true));
-        };
-        float cq[4], dq[2];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            cq[u] = rs_step(bq[2 * u], bq[2 * u + 1], (jl & 8) != 0, std::integral_constant<int, 0x128>{});
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-            dq[v] = rs_step(cq[2 * v], cq[2 * v + 1], (jl & 4) != 0, std::integral_constant<int, 0x141>{});
-        float eq = rs_step(dq[0], dq[1], (jl & 2) != 0, std::integral_constant<int, 0x4E>{});
-        eq += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, eq), 0xB1, 0xF, 0xF, true));
-        const float alpha_val = softplus(eq + Fl[F_BA] - 1.f);
-        const int ri_ = (jl & 3) + 4 * (jl >> 3);
-        const int src = 32 * ((jl >> 2) & 1) + 2 * ((ri_ >> 3) & 1) + 4 * ((ri_ >> 2) & 1) + 8 * ((ri_ >> 1) & 1) +
-                        16 * (ri_ & 1);
-        const float alpha_row =
-            __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src * 4, __builtin_bit_cast(int, alpha_val)));
-        const float alpha_s = dpp_sum8(ri.wgt * alpha_row);
-        if (ri.sval && kk == 0 && h == 0) a.feat[(int64_t)ri.s * 4 + 0] = alpha_s;
-        X3T();  // tile end
-    }
-#undef X3T
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // =====================================================================================
 // 2 waves per SIMD: v_mfma_f32_16x16x32_f16, 8 waves x 16 rows (2 samples x K = 8) per
 // 128-row workgroup tile.  A wave's registers hold 16 rows (hi/lo layer input 64, all 16 output
@@ -780,8 +237,7 @@ __global__ __launch_bounds__(TPB, 1) void k_agg_rows_x3(AggArgs a) {
 // vectors.  Chained layers: k-step s of the next layer takes tiles 2s, 2s+1 of this one as
 // element j <- unit 16 (j >> 2) + 4 g + (j & 3) (perm16, folded into the packed weights).
 // =====================================================================================
-constexpr int NW16 = 8, TPB16 = NW16 * 64;
-constexpr uint32_t OFF16_BASE = OFF_WB + 8u * 22u * PAIR;   // after the largest 32x32 SG section
+constexpr uint32_t OFF16_BASE = 0;
 constexpr uint32_t OFF16_W0B = OFF16_BASE;                  // block1.0 PE(dists): 2 ks x 16 tiles
 constexpr uint32_t OFF16_W1 = OFF16_W0B + 32 * PAIR;        // block1.2: 8 x 16
 constexpr uint32_t OFF16_W2 = OFF16_W1 + 128 * PAIR;        // block3.0: 9 x 16
@@ -1603,7 +1059,6 @@ void pack_blob16(int ksb, int bpnet_dim, const float *const *w, const float *con
     }
     for (int c = 0; c < 3; ++c) Y[Y_CB3 + c] = b[8][c];
 }
-
 // ---- colour MLP ------------------------------------------------------------------------
 struct ColorArgs {
     const int32_t *counters, *work, *samp_ray;
@@ -1611,116 +1066,9 @@ struct ColorArgs {
     const void *blob;
     const float *fs;
     float *feat;
+    int32_t *range_flag;  // set to 1 when a sample's decoded features are not finite (fp16 range exceeded)
     int32_t item0, n_items;
 };
-constexpr int COL_LDS = LDS_F32_OFF + N_XF32 * 4;
-
-__global__ __launch_bounds__(TPB, 1) void k_color_x3(ColorArgs a) {
-    __shared__ __attribute__((aligned(16))) char lds[COL_LDS];
-    const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, j = lane & 31;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwork = a.counters[1];
-    const int end = min(nwork, a.item0 + a.n_items);
-    const WBlob wb = make_blob(a.blob, BLOB_BYTES);
-    {
-        const float *src = (const float *)((const char *)a.blob + OFF_XF32);
-        float *dst = (float *)(lds + LDS_F32_OFF);
-        for (int i = threadIdx.x; i < N_XF32; i += TPB) dst[i] = src[i];
-    }
-    __syncthreads();
-    int slot = 0;
-    dma_chunk<NetColor, 0>(wb, lds, w, lane, 0);
-    for (int base = a.item0 + blockIdx.x * (32 * NW); base < end; base += gridDim.x * (32 * NW)) {
-        int lz = 0;
-        asm volatile("" : "+s"(lz));
-        char *ldsi = lds + lz;
-        const float *Fc = (const float *)(ldsi + LDS_F32_OFF);
-        const int item = base + w * 32 + j;
-        const bool sval = item < end;
-        const int s = sval ? a.work[item] : 0;
-        const int ray = a.samp_ray[s];
-        X3B x[KS_C0];
-        {
-            const f32x4 *row = (const f32x4 *)(a.fs + (int64_t)(sval ? item - a.item0 : 0) * HID);
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {  // units 16 k + 8 h + e (natural order, col_c0)
-                const f32x4 u0 = row[4 * k + 2 * h], u1 = row[4 * k + 2 * h + 1];
-                const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-                x[k] = split8(v);
-            }
-        }
-        // PE(viewdir) ori=True, channels [3:] (point_aggregators.py:579-585, networks.py:175-192):
-        // pe[d*4+f] = sin(v_d 2^f), pe[12+d*4+f] = cos(v_d 2^f)
-        const float v3[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1], a.raydir[(int64_t)ray * 3 + 2]};
-        float pe[24];
-        static_for<3>([&](auto d3) {
-            constexpr int d = decltype(d3)::value;
-            static_for<4>([&](auto ff) {
-                constexpr int f = decltype(ff)::value;
-                float sv, cv;
-                sincos_f<f>(v3[d], sv, cv);
-                pe[d * 4 + f] = sv;
-                pe[12 + d * 4 + f] = cv;
-            });
-        });
-        {
-            float u[8], z[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                u[e] = h ? pe[8 + e] : pe[e];
-                z[e] = h ? 0.f : pe[16 + e];
-            }
-            x[16] = split8(u);
-            x[17] = split8(z);
-        }
-        f32x16 acc[4];
-        auto bias_init = [&](int fb) {
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) {
-                const f32x4 *b = (const f32x4 *)(Fc + fb + (tt * 2 + h) * 16);
-                const f32x4 b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
-                acc[tt] = f32x16{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3],
-                                 b2[0], b2[1], b2[2], b2[3], b3[0], b3[1], b3[2], b3[3]};
-            }
-        };
-        X3B y1[KS_CH], y2[KS_CH];
-        bias_init(F_CB0);
-        run_pass<NetColor, 0, 0>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) { return x[decltype(k)::value]; });
-        chain_out<4, 0>(acc, Fc[XF_INV + 4], y1);
-        bias_init(F_CB1);
-        run_pass<NetColor, 1, 0>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) { return y1[decltype(k)::value]; });
-        chain_out<4, 0>(acc, Fc[XF_INV + 5], y2);
-        bias_init(F_CB2);
-        run_pass<NetColor, 2, 0>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) { return y2[decltype(k)::value]; });
-        const float inv = Fc[XF_INV + 6];
-        float o[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float *w0 = Fc + F_WC3 + (t * 2 + h) * 16;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float y = acc[t][r] * inv;
-                const float hv = fmaxf(y, 0.01f * y);
-                o[0] = __builtin_fmaf(w0[r], hv, o[0]);
-                o[1] = __builtin_fmaf(w0[128 + r], hv, o[1]);
-                o[2] = __builtin_fmaf(w0[256 + r], hv, o[2]);
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float z = o[c] + __shfl_xor(o[c], 32) + Fc[F_BC3 + c];
-            o[c] = (1.f / (1.f + expf(-z))) * (1.f + 2.f * 0.001f) - 0.001f;
-        }
-        if (sval && h == 0) {
-            a.feat[(int64_t)s * 4 + 1] = o[0];
-            a.feat[(int64_t)s * 4 + 2] = o[1];
-            a.feat[(int64_t)s * 4 + 3] = o[2];
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // ---- colour MLP, 16x16 (2 waves per SIMD): 8 waves x 16 samples per 128-sample tile --------
 // Lane (sample r = l & 15, group g = l >> 4).  Colour 0's k-step s < 8 takes f_s units 32 s + 8 g + j
 // (natural order, two 16-B loads per lane), k-step 8 the PE(viewdir) channels 8 g + j < 24; colour
@@ -1840,29 +1188,27 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
                 for (int c = 0; c < 3; ++c) o[c] = __builtin_fmaf(wc[c][i], hv, o[c]);
             }
         }
+        bool fin = true;  // the logits (the sigmoid maps +-inf to finite values) and k_rows16's alpha
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             float x = o[c] + __shfl_xor(o[c], 16);
             x += __shfl_xor(x, 32);
             const float z = x + Yl[Y_CB3 + c];
+            fin = fin && __builtin_isfinite(z);
             o[c] = (1.f / (1.f + expf(-z))) * (1.f + 2.f * 0.001f) - 0.001f;
         }
         if (sval && g == 0) {
             a.feat[(int64_t)s * 4 + 1] = o[0];
             a.feat[(int64_t)s * 4 + 2] = o[1];
             a.feat[(int64_t)s * 4 + 3] = o[2];
+            // fp16-range guard: an activation >= 65504 became inf in its hi part and NaN / inf in
+            // every layer after it (mlp_x3.hip header); flag the call instead of returning it
+            if (!(fin && __builtin_isfinite(a.feat[(int64_t)s * 4]))) *a.range_flag = 1;
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-
 // ---- host-side packing ---------------------------------------------------------------------
-int col_l0(int ks, int p) { return l0_ref_col(p >> 3, 8 * ks + (p & 7)); }
-int col_chain(int ks, int p) { return 16 * ks + perm_acc(p); }
-int col_l2(int ks, int p) { return ks < 16 ? col_chain(ks, p) : (p < 7 ? 256 + p : -1); }
-int col_l0b(int ks, int p) { return l0_ref_col(p >> 3, 8 * (KS_P0 + ks) + (p & 7)); }
-int col_c0(int ks, int p) { return ks < 16 ? 16 * ks + p : (16 * (ks - 16) + p < 24 ? 256 + 16 * (ks - 16) + p : -1); }
-
 // power of two 2^s with max |W| 2^s < 2^14 (so lo parts stay normal fp16 numbers)
 int layer_shift(const float *W, size_t n) {
     float m = 0.f;
@@ -1872,74 +1218,13 @@ int layer_shift(const float *W, size_t n) {
     frexpf(m, &e);  // m < 2^e
     return 14 - e;
 }
-
-template <typename ColFn>
-void pack_pairs(_Float16 *dst, const float *W, int n_out, int n_in, int n_tiles, int KS, int tp, int shift, ColFn col) {
-    const float sc = ldexpf(1.f, shift);
-    for (int tout = 0; tout < n_tiles; ++tout)
-        for (int ks = 0; ks < KS; ++ks) {
-            const size_t f = ((size_t)(tout / tp) * KS + ks) * tp + (tout % tp);
-            for (int lane = 0; lane < 64; ++lane)
-                for (int e = 0; e < 8; ++e) {
-                    const int row = 32 * tout + (lane & 31);
-                    const int c = col(ks, 8 * (lane >> 5) + e);
-                    const float v = (row < n_out && c >= 0 && c < n_in) ? W[(size_t)row * n_in + c] * sc : 0.f;
-                    const _Float16 hi = (_Float16)v;
-                    const _Float16 lo = (_Float16)(v - (float)hi);
-                    dst[((2 * f) * 64 + lane) * 8 + e] = hi;
-                    dst[((2 * f + 1) * 64 + lane) * 8 + e] = lo;
-                }
-        }
-}
-
-void pack_acc_order(float *dst, const float *v, int n_tiles, float sc) {
-    for (int t = 0; t < n_tiles; ++t)
-        for (int h = 0; h < 2; ++h)
-            for (int r = 0; r < 16; ++r) dst[(t * 2 + h) * 16 + r] = v[32 * t + acc_unit(r, h)] * sc;
-}
-
-int col_bp(int ks, int p) { return ks < 16 ? col_chain(ks, p) : 256 + 16 * (ks - 16) + p; }
-
 // ksb > 0: w[9] / b[9] = block2_bpnet.0 ([256][256 + bpnet_dim], [256])
 void pack_blob_x3(int ksb, int bpnet_dim, const float *const *w, const float *const *b, uint8_t *blob) {
     static const int shape[9][2] = {{256, 284}, {256, 256}, {256, 263}, {256, 256}, {1, 256},
                                     {128, 280}, {128, 128}, {128, 128}, {3, 128}};
     int s[9] = {};
     for (int L : {0, 1, 2, 3, 5, 6, 7}) s[L] = layer_shift(w[L], (size_t)shape[L][0] * shape[L][1]);
-    auto fr = [&](uint32_t off) { return (_Float16 *)(blob + off); };
-    pack_pairs(fr(OFF_W0B), w[0], 256, 284, T_HID, KS_L0S, 8, s[0], col_l0b);
-    pack_pairs(fr(OFF_W1), w[1], 256, 256, T_HID, KS_HID, TPL, s[1], col_chain);
-    pack_pairs(fr(OFF_W2), w[2], 256, 263, T_HID, KS_L2, 4, s[2], col_l2);
-    pack_pairs(fr(OFF_W3), w[3], 256, 256, T_HID, KS_HID, TPL, s[3], col_chain);
-    pack_pairs(fr(OFF_C0), w[5], 128, 280, T_CHID, KS_C0, 4, s[5], col_c0);
-    pack_pairs(fr(OFF_C1), w[6], 128, 128, T_CHID, KS_CH, 4, s[6], col_chain);
-    pack_pairs(fr(OFF_C2), w[7], 128, 128, T_CHID, KS_CH, 4, s[7], col_chain);
-    pack_pairs(fr(OFF_W0A), w[0], 256, 284, T_HID, KS_P0, 8, s[0], [](int ks, int p) { return col_l0(ks, p); });
-    float *F = (float *)(blob + OFF_XF32);
-    pack_acc_order(F + F_B0, b[0], T_HID, ldexpf(1.f, s[0]));
-    pack_acc_order(F + F_B1, b[1], T_HID, ldexpf(1.f, s[1]));
-    pack_acc_order(F + F_B2, b[2], T_HID, ldexpf(1.f, s[2]));
-    for (int u = 0; u < HID; ++u) F[F_B3 + u] = b[3][u];  // natural, unscaled: block3.2 epilogue adds it
-    pack_acc_order(F + F_CB0, b[5], T_CHID, ldexpf(1.f, s[5]));
-    pack_acc_order(F + F_CB1, b[6], T_CHID, ldexpf(1.f, s[6]));
-    pack_acc_order(F + F_CB2, b[7], T_CHID, ldexpf(1.f, s[7]));
-    for (int u = 0; u < HID; ++u) F[F_WA + u] = w[4][u];
-    F[F_BA] = b[4][0];
-    for (int c = 0; c < 3; ++c) {
-        pack_acc_order(F + F_WC3 + c * 128, w[8] + c * 128, T_CHID, 1.f);
-        F[F_BC3 + c] = b[8][c];
-    }
-    const int li[7] = {0, 1, 2, 3, 5, 6, 7};
-    for (int i = 0; i < 7; ++i) F[XF_INV + i] = ldexpf(1.f, -s[li[i]]);
-    F[XF_INV + 7] = 1.f;
-    int sb = 0;
-    if (ksb > 0) {
-        const int nin = 256 + bpnet_dim;
-        sb = layer_shift(w[9], (size_t)256 * nin);
-        pack_pairs(fr(OFF_WB), w[9], 256, nin, T_HID, ksb, 4, sb, col_bp);
-        pack_acc_order(F + XF_BB, b[9], T_HID, ldexpf(1.f, sb));
-        F[XF_INV + 7] = ldexpf(1.f, -sb);
-    }
+    const int sb = ksb > 0 ? layer_shift(w[9], (size_t)256 * (256 + bpnet_dim)) : 0;
     pack_blob16(ksb, bpnet_dim, w, b, s, sb, blob);
 }
 
@@ -1952,21 +1237,6 @@ int variant_ksb(int32_t bpnet_layers, int32_t bpnet_dim) {
 }  // namespace x3
 }  // namespace
 }  // namespace sgn
-
-namespace sgn {
-namespace {
-// 1 (default): the 2-waves-per-SIMD 16x16x32 row / projection kernels; 0: the 32x32x16 ones
-// (SGN_X3_W16=0 in the environment, read once; both produce identical-precision results)
-int x3_w16() {
-    static const int v = [] {
-        const char *e = getenv("SGN_X3_W16");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
-}  // namespace
-}  // namespace sgn
-
 extern "C" {
 
 size_t sgn_mlp_packed_bytes_f32(int32_t bpnet_layers, int32_t bpnet_dim) {
@@ -1990,7 +1260,7 @@ int sgn_mlp_pack_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *const
 }
 
 size_t sgn_point_proj_bytes_f32(int64_t n_points) {
-    // P rows, then (16x16 kernels) the packed 64-B point records
+    // P rows, then the packed 64-B point records
     return (size_t)(n_points > 0 ? n_points : 0) * (sgn::x3::PROJ_BYTES_PER_POINT + sgn::x3::REC16_FLOATS * 4);
 }
 
@@ -2000,38 +1270,33 @@ int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void
     SGN_REQUIRE(pt->n_points >= 0 && (pt->n_points == 0 || pt->embedding), "embedding required");
     SGN_REQUIRE(((uintptr_t)d_proj & 15) == 0 && ((uintptr_t)pt->embedding & 15) == 0, "16-byte alignment required");
     if (pt->n_points == 0) return 0;
-    if (x3_w16()) {
-        SGN_REQUIRE(pt->xyz && pt->color && pt->dir && pt->conf, "point tables (xyz, color, dir, conf) required");
-        float *rec = (float *)((char *)d_proj + (size_t)pt->n_points * x3::PROJ_BYTES_PER_POINT);
-        x3::Proj16Args a{pt->embedding, pt->n_points, d_packed, (float *)d_proj, pt->xyz, pt->color, pt->dir,
-                         pt->conf, rec};
-        const int64_t tiles = (pt->n_points + 16 * x3::NW16 - 1) / (16 * x3::NW16);
-        hipLaunchKernelGGL(x3::k_point_proj16, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB16), 0,
-                           as_stream(stream), a);
-    } else {
-        x3::ProjArgs a{pt->embedding, pt->n_points, d_packed, (float *)d_proj};
-        const int64_t tiles = (pt->n_points + 32 * x3::NW - 1) / (32 * x3::NW);
-        hipLaunchKernelGGL(x3::k_point_proj_x3, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB), 0,
-                           as_stream(stream), a);
-    }
+    SGN_REQUIRE(pt->xyz && pt->color && pt->dir && pt->conf, "point tables (xyz, color, dir, conf) required");
+    float *rec = (float *)((char *)d_proj + (size_t)pt->n_points * x3::PROJ_BYTES_PER_POINT);
+    x3::Proj16Args a{pt->embedding, pt->n_points, d_packed, (float *)d_proj, pt->xyz, pt->color, pt->dir,
+                     pt->conf, rec};
+    const int64_t tiles = (pt->n_points + 16 * x3::NW16 - 1) / (16 * x3::NW16);
+    hipLaunchKernelGGL(x3::k_point_proj16, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB16), 0,
+                       as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }
 
-// Work items per launch of the 32x32 kernel (k_agg_rows_x3): its fp32 blended features are stored
-// through one buffer descriptor (31-bit byte range) based at the launch's first item, so at most
-// 2^31 / 1 KiB items per launch.  k_rows16 bases a descriptor per tile and has no such limit.
-constexpr int64_t X3_MAX_CHUNK = ((int64_t)0x7fffffff / (sgn::mlp::HID * 4)) / 16 * 16;
-
 // Workspace: blended features of every work item (fp32, 1 KiB each), so the two stages may be
 // called separately, then k_pair_slots' row table (32 B) and slot entries (16 B) per item, then a
-// 2-KiB tail (the slot count).  A smaller workspace is accepted
-// with stages = 3 (both stages per chunk).
+// 2-KiB tail: [0] the slot count, [1] the fp16-range flag (k_color16; sgn_aggregate_check_f32).
+// A smaller workspace is accepted with stages = 3 (both stages per chunk).
 constexpr int64_t WS_PER_ITEM = sgn::mlp::HID * 4 + 32 + 16, WS_TAIL = 2048;
 size_t sgn_aggregate_workspace_bytes_f32(int64_t S) {
     if (S < 32) S = 32;
     return (size_t)(S * WS_PER_ITEM + WS_TAIL);
 }
+
+namespace {
+int32_t *ws_tail(void *d_workspace, size_t workspace_bytes) {
+    const int64_t ws_items = workspace_bytes > (size_t)WS_TAIL ? (int64_t)((workspace_bytes - WS_TAIL) / WS_PER_ITEM) : 0;
+    return (int32_t *)((char *)d_workspace + ws_items * WS_PER_ITEM);
+}
+}  // namespace
 
 int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet, const void *d_point_proj,
                       const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
@@ -2040,6 +1305,7 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     using namespace sgn;
     using namespace sgn::mlp;
     SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace && d_point_proj, "null argument");
+    SGN_REQUIRE(stages >= 1 && stages <= 3, "stages must be 1 (rows), 2 (colour) or 3 (both)");
     const int ksb = x3::variant_ksb(bpnet_layers, bpnet_dim);
     SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
     SGN_REQUIRE(bpnet_dim == 0 || (d_bpnet && ((uintptr_t)d_bpnet & 15) == 0),
@@ -2055,12 +1321,10 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     SGN_REQUIRE(stages == 3 || ws_items >= S_capacity,
                 "stages 1 and 2 called separately need a workspace for all S_capacity items");
     // chunk = items per launch; with a full-size workspace chunk c keeps its rows at item c * chunk.
-    // k_rows16 bases its f_s descriptor per tile (one launch per stage for any frame); the 32x32
-    // kernel's single descriptor limits a launch to X3_MAX_CHUNK items
+    // k_rows16 bases its f_s descriptor per tile (one launch per stage for any frame); k_pair_slots
+    // packs chunk-relative items in 28 bits
     const bool full = ws_items >= S_capacity;
-    // (k_pair_slots packs chunk-relative items in 28 bits)
-    const int64_t lim = x3_w16() ? (ws_items < (1 << 27) ? ws_items : (1 << 27))
-                                 : (ws_items < X3_MAX_CHUNK ? ws_items : X3_MAX_CHUNK);
+    const int64_t lim = ws_items < (1 << 27) ? ws_items : (1 << 27);
     const int64_t chunk = lim < S_capacity ? lim : (S_capacity > 32 ? S_capacity : 32);
     AggArgs a{};
     a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
@@ -2070,22 +1334,24 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     a.samp_locw = q->samp_locw;
     a.blob = d_packed; a.blob_bytes = x3::blob_bytes_sg(ksb);
     a.bpnet32 = d_bpnet;
-    a.proj = (const _Float16 *)d_point_proj;  // fp32 table (k_agg_rows_x3 reads it as float)
+    a.proj = (const _Float16 *)d_point_proj;  // fp32 P table (k_rows16 reads it as float)
     a.rec = (const float *)((const char *)d_point_proj + (size_t)pt->n_points * x3::PROJ_BYTES_PER_POINT);
     a.feat = d_out_feat; a.blend = d_out_blend; a.wnorm = d_out_wnorm; a.fs = (_Float16 *)d_workspace;
-    char *ws_end = (char *)d_workspace + ws_items * WS_PER_ITEM + WS_TAIL;
+    int32_t *tail = ws_tail(d_workspace, workspace_bytes);
     int32_t *rows = (int32_t *)((char *)d_workspace + ws_items * mlp::HID * 4);
     int4 *slots = (int4 *)(rows + ws_items * 8);
-    int32_t *slot_n = (int32_t *)(ws_end - WS_TAIL);
+    int32_t *slot_n = tail;
     a.rows = rows; a.slots = slots; a.slot_n = slot_n;
     // SGN_PAIR=0 runs every sample alone in its k_rows16 half (same results, bit for bit; tests)
     const char *pe = getenv("SGN_PAIR");
     const int32_t pair = !(pe && pe[0] == '0');
-    if ((stages & 1) && x3_w16()) {
+    if (stages & 1) {
         // a paired half writes only its samples' valid rows: the optional per-slot outputs start at 0
         if (d_out_blend) SGN_CHECK_HIP(hipMemsetAsync(d_out_blend, 0, (size_t)S_capacity * 8 * 4, st));
         if (d_out_wnorm) SGN_CHECK_HIP(hipMemsetAsync(d_out_wnorm, 0, (size_t)S_capacity * 8 * 4, st));
     }
+    // the fp16-range flag covers the samples of this call's colour stage (cleared with its first chunk)
+    if (stages & 2) SGN_CHECK_HIP(hipMemsetAsync(tail + 1, 0, 4, st));
 #ifdef SGN_X3_TIMING
     static unsigned long long *tbuf = nullptr;
     const size_t tn = (size_t)x3::TD_BLOCKS * x3::NW16 * x3::TD_EV;
@@ -2093,7 +1359,8 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     SGN_CHECK_HIP(hipMemsetAsync(tbuf, 0, tn * 8, st));
     a.tdbg = tbuf;
 #endif
-    x3::ColorArgs c{q->counters, q->work, q->samp_ray, pt->raydir, d_packed, (const float *)d_workspace, d_out_feat, 0, 0};
+    x3::ColorArgs c{q->counters, q->work, q->samp_ray, pt->raydir, d_packed, (const float *)d_workspace, d_out_feat,
+                    tail + 1, 0, 0};
     for (int64_t i0 = 0; i0 < S_capacity; i0 += chunk) {
         const int64_t n = S_capacity - i0 < chunk ? S_capacity - i0 : chunk;
         a.item0 = c.item0 = (int32_t)i0;
@@ -2101,8 +1368,7 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
         float *fs = (float *)d_workspace + (full ? i0 * mlp::HID : 0);
         a.fs = (_Float16 *)fs;
         c.fs = fs;
-        const int64_t wg = (n + x3::WG_SAMPLES - 1) / x3::WG_SAMPLES;
-        if ((stages & 1) && x3_w16()) {
+        if (stages & 1) {
             SGN_CHECK_HIP(hipMemsetAsync(slot_n, 0, 4, st));
             const int64_t pb = (n + x3::PAIR_TPB - 1) / x3::PAIR_TPB;
             hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)(pb < 1024 ? pb : 1024)),
@@ -2111,10 +1377,6 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
             auto kern = ksb == 0 ? x3::k_rows16<0> : ksb == KS_HID ? x3::k_rows16<8> : x3::k_rows16<11>;
             const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < 256 ? wg16 : 256)), dim3(x3::TPB16), 0, st, a);
-        } else if (stages & 1) {
-            auto kern = ksb == 0 ? x3::k_agg_rows_x3<0> : ksb == KS_HID ? x3::k_agg_rows_x3<KS_HID>
-                                                                        : x3::k_agg_rows_x3<ks_bp(BP_DIM)>;
-            hipLaunchKernelGGL(kern, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(x3::TPB), 0, st, a);
         }
 #ifdef SGN_X3_TIMING
         if ((stages & 1) && i0 == 0)
@@ -2125,16 +1387,32 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
                 if (FILE *f = fopen(path, "wb")) { fwrite(hb.data(), 8, tn, f); fclose(f); }
             }
 #endif
-        if ((stages & 2) && x3_w16()) {
+        if (stages & 2) {
             const int64_t wgc = (n + 16 * x3::NW16 - 1) / (16 * x3::NW16);
             hipLaunchKernelGGL(x3::k_color16, dim3((unsigned)(wgc < 256 ? wgc : 256)), dim3(x3::TPB16), 0, st, c);
-        } else if (stages & 2) {
-            const int64_t wg2 = (n + 32 * x3::NW - 1) / (32 * x3::NW);
-            hipLaunchKernelGGL(x3::k_color_x3, dim3((unsigned)(wg2 < 256 ? wg2 : 256)), dim3(x3::TPB), 0, st, c);
         }
     }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
+}
+
+int sgn_aggregate_check_f32(const void *d_workspace, size_t workspace_bytes, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(d_workspace && workspace_bytes >= (size_t)(32 * WS_PER_ITEM + WS_TAIL), "null or too small workspace");
+    const int32_t *flag = ws_tail(const_cast<void *>(d_workspace), workspace_bytes) + 1;
+    int32_t h = 0;
+    hipStream_t st = as_stream(stream);
+    SGN_CHECK_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, st));
+    SGN_CHECK_HIP(hipStreamSynchronize(st));
+    SGN_REQUIRE(h == 0, "fp16 range exceeded: an aggregator activation or point feature reached |x| >= 65504, so "
+                        "the split-fp16 MFMA operands overflowed and the decoded features of the last "
+                        "sgn_aggregate_f32 call are not finite");
+    return 0;
+}
+
+size_t sgn_aggregate_flag_offset_f32(size_t workspace_bytes) {
+    const int64_t ws_items = workspace_bytes > (size_t)WS_TAIL ? (int64_t)((workspace_bytes - WS_TAIL) / WS_PER_ITEM) : 0;
+    return (size_t)(ws_items * WS_PER_ITEM + 4);
 }
 
 }  // extern "C"

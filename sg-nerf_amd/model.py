@@ -277,6 +277,9 @@ class HipPointsVolumetricModel:
         """neural_points_volumetric_model.py:320-331: forward, losses, backward, both Adam steps."""
         if getattr(self, "trainer", None) is None:
             self.setup_optimizer(self.opt)
+        if self.trainer is None:  # SG with predict_semantic: setup_optimizer waits for the embedding
+            raise ValueError("optimize_parameters: the SG-NeRF aggregator (predict_semantic = 1) needs the points' "
+                             "BPNet embedding first (neural_points.set_bpnet_feats / bpnet_points_embedding)")
         inp = self.input
         tr = self.trainer
         near = inp["near"] if "near" in inp else self.opts.near_plane

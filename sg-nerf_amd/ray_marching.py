@@ -307,7 +307,16 @@ class PointAggregator:
         if S == 0:
             return (torch.zeros(shp + (4,), device=dev), ray_valid.view(shp), None, None)
         rows = torch.arange(S * K, device=dev, dtype=torch.int32).view(S, K)
-        pidx = torch.where(mask, rows, torch.full_like(rows, -1)).contiguous()
+        pidx = torch.where(mask, rows, torch.full_like(rows, -1))
+        order = None
+        if self.f32:
+            # the f32 row kernel reads a sample's valid neighbours as a prefix of its K slots (as the
+            # query writes them); a caller's mask may have holes: move each sample's valid slots to
+            # the front (stable, so the K-blend sums them in the reference's slot order; the empty
+            # slots only added zeros) and scatter the per-slot outputs back afterwards
+            order = torch.argsort((~mask).to(torch.int8), dim=1, stable=True)
+            pidx = torch.gather(pidx, 1, order)
+        pidx = pidx.contiguous()
         # work list: valid samples first, counts on the device (no host sync)
         work = torch.argsort((~ray_valid).to(torch.int8), stable=True).to(torch.int32)
         counters = torch.zeros(4, dtype=torch.int32, device=dev)
@@ -356,6 +365,8 @@ class PointAggregator:
             _lib.check(L.sgn_aggregate_f32(nl, dim, _lib.ptr(bp), _lib.ptr(proj), ctypes.byref(pt), ctypes.byref(qo), S, K,
                                            _lib.ptr(self.packed), _lib.ptr(feat), None, _lib.ptr(wnorm), _lib.ptr(ws),
                                            ws.numel(), 3, st), "sgn_aggregate_f32")
+            _lib.check(L.sgn_aggregate_check_f32(_lib.ptr(ws), ws.numel(), st), "sgn_aggregate_f32 (fp16 range)")
+            wnorm = torch.zeros_like(wnorm).scatter_(1, order, wnorm)   # back to the caller's slot order
         else:
             ws = torch.empty(int(L.sgn_aggregate_workspace_bytes(S)), dtype=torch.uint8, device=dev)
             _lib.check(L.sgn_aggregate_sg(nl, dim, _lib.ptr(bp), None, ctypes.byref(pt), ctypes.byref(qo), S, K,

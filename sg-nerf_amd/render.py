@@ -72,6 +72,8 @@ class HipRenderer:
         self.set_mlp(mlp_state)
         self._cap = None
         self._proj = None
+        self._pending = []   # deferred fp16-range checks: (pinned flag copy, event)
+        self._flag_host = None
 
     def set_mlp(self, mlp_state):
         self.mlp_state = {k: torch.as_tensor(v).detach().to("cpu", torch.float32)
@@ -101,15 +103,52 @@ class HipRenderer:
             self.blendw = None
             self._cap = (R, cap)
 
+    def _range_check(self, mode):
+        """f32 mode: the colour stage flags samples whose decoded features are not finite (an
+        activation outside fp16 range, mlp_x3.hip header).  "sync": check now (one stream sync);
+        "deferred": copy the flag to pinned memory and check it after the NEXT frame has been
+        enqueued (or at finish()), so frames stay pipelined; False: no check."""
+        if not self.f32 or not mode:
+            return
+        L = _lib.lib()
+        if mode == "sync":
+            _lib.check(L.sgn_aggregate_check_f32(_lib.ptr(self.agg_ws), self.agg_ws.numel(), _lib.stream_handle()),
+                       "sgn_aggregate_check_f32")
+            return
+        off = int(L.sgn_aggregate_flag_offset_f32(self.agg_ws.numel()))
+        if self._flag_host is None:
+            self._flag_host = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        prev = self._pending.pop(0) if self._pending else None   # at most one frame is pending
+        buf = self._flag_host[1] if prev is not None and prev[0] is self._flag_host[0] else self._flag_host[0]
+        buf.copy_(self.agg_ws[off:off + 4].view(torch.int32), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending.append((buf, ev))
+        if prev is not None:
+            self._raise_if_flagged(*prev)
+
+    @staticmethod
+    def _raise_if_flagged(buf, ev):
+        ev.synchronize()
+        if int(buf.item()) != 0:
+            raise _lib.SgnError("sgn_aggregate_f32: fp16 range exceeded -- an aggregator activation or point "
+                                "feature reached |x| >= 65504, so the decoded features of a frame are not finite")
+
+    def finish(self):
+        """Wait for the deferred range checks of the frames rendered so far (raises if one failed)."""
+        while self._pending:
+            self._raise_if_flagged(*self._pending.pop(0))
+
     def render(self, campos, camrotc2w, raydir, near, far, want_opacity=True, want_blend=False, marks=None,
                bg=None, want_weights=False, point_labels=None, ray_labels=None, seconds=None,
-               count_traffic=False):
+               count_traffic=False, check_range="sync"):
         """One frame.  `marks(name)` (optional) is called between stages on the host thread
         (bench.py records HIP events on the current stream there).  `bg`: 3 floats
         overriding opts.bg_color.  `want_weights`: also produce the normalised neighbour
         weights and the per-slot alpha-blend weights (reference `weight`, `blend_weight`).
         `point_labels` [N] / `ray_labels` [R] int32 (+ `seconds`): the SG semantic-guided kNN
-        (semantic_guidance = 1, worldcoords.py:839-938)."""
+        (semantic_guidance = 1, worldcoords.py:839-938).  `check_range`: the f32 mode's fp16-range
+        guard ("sync" default, "deferred" for pipelined frame loops + finish(), False)."""
         o = self.opts
         mark = marks or (lambda name: None)
         campos = campos.reshape(3).to(self.device, torch.float32).contiguous()
@@ -175,6 +214,7 @@ class HipRenderer:
                                    _lib.ptr(self.opacity) if want_opacity else None,
                                    _lib.ptr(self.blendw) if want_weights else None, st), "sgn_composite")
         mark("end")
+        self._range_check(check_range)
         return RenderOut(self.rgb[:R], self.mask[:R], self.bgT[:R], self.opacity[:R], q, self.feat, self.blend,
                          self.wnorm if want_weights else None, self.blendw[:R] if want_weights else None)
 

@@ -68,3 +68,32 @@ def load_golden(file, name):
     mlp = {k[4:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("mlp/")}
     case = {k.split("/", 1)[1]: g[k] for k in g.files if k.startswith(name + "/")}
     return pts, mlp, case
+
+
+def check_query_sample_major(q, ref, R, K):
+    """A renderer's sample-major query (querier.QueryResult) against an oracle query of the same
+    rays (OracleGrid.query, dense [R, SR, ...]): ray_ns, every sample's K neighbour indices,
+    depth index and position, neighbour count and the work list, all bit-exact."""
+    assert_equal_arrays(q.ray_ns[:R].cpu().numpy(), ref["ray_ns"], "ray_ns")
+    S = q.n_samples()
+    assert S == int(ref["ray_ns"].sum())
+    sr = q.samp_ray[:S].cpu().numpy()
+    slot = np.arange(S) - q.ray_soff[:R].cpu().numpy()[sr]
+    assert_equal_arrays(q.pidx[:S * K].view(S, K).cpu().numpy(), ref["pidx"][sr, slot], "sample_pidx")
+    assert_equal_arrays(q.samp_d[:S].cpu().numpy(), ref["ray_d"][sr, slot], "samp_d")
+    assert_equal_arrays(q.samp_locw[:S * 3].view(S, 3).cpu().numpy(), ref["loc_w"][sr, slot], "sample_loc_w")
+    nnb = (ref["pidx"][sr, slot] >= 0).sum(-1)
+    assert_equal_arrays(q.samp_nnb[:S].cpu().numpy(), nnb, "samp_nnb")
+    nwork = int(q.counters[1].item())
+    assert_equal_arrays(np.sort(q.work[:nwork].cpu().numpy()), np.nonzero(nnb > 0)[0], "worklist")
+    return S
+
+
+def check_grid(g, og):
+    """HipGrid.export() against the oracle's reference-format grid tensors, bit-exact."""
+    coor_occ, coor_2_occ, numpnts, lists = g.export()
+    assert_equal_arrays(coor_occ.cpu().numpy(), og.coor_occ, "coor_occ")
+    assert_equal_arrays(coor_2_occ.cpu().numpy(), og.coor_2_occ, "coor_2_occ")
+    assert_equal_arrays(numpnts.cpu().numpy(), og.occ_numpnts, "occ_numpnts")
+    assert_equal_arrays(lists.cpu().numpy(), og.occ_2_pnts, "occ_2_pnts")
+    assert g.info()["n_claimed"] == og.occ_idx

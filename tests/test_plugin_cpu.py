@@ -197,3 +197,14 @@ def test_set_points_reference_signature(tmp_path):
     assert m.net_ray_marching.neural_points is m.neural_points
     with pytest.raises(NotImplementedError):
         m.set_points(**kw, editing=True)
+
+
+def test_sg_optimize_without_bpnet_embedding_raises(tmp_path):
+    """SG with predict_semantic = 1: setup_optimizer leaves the trainer unset until the BPNet
+    embedding exists (neural_points.py:653-665); optimize_parameters then says so instead of
+    failing on a None trainer."""
+    m = _model(tmp_path, shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1)
+    m.neural_points = _points(bpnet=False)
+    m.input = {}
+    with pytest.raises(ValueError, match="BPNet embedding"):
+        m.optimize_parameters(total_steps=1)

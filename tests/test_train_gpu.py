@@ -18,6 +18,8 @@ from sgnerf_amd import _lib
 from sgnerf_amd.train import PointParams, Trainer
 from sgnerf_amd.train_hip import FlatMLP, HipTrainer, _Packer, grads_named
 from sgnerf_amd.weights import LAYERS, init_mlp, pack_mlp
+import oracle_query as oq
+from helpers import hyper_for, t_table
 from test_train_cpu import O, _setup
 
 pytestmark = pytest.mark.gpu
@@ -52,18 +54,19 @@ def _rel(a, b):
     return float(torch.linalg.vector_norm(a.double() - b.double()) / max(torch.linalg.vector_norm(b.double()), 1e-30))
 
 
-@pytest.mark.parametrize("seed", [3, 5])
-def test_hip_training_gradients_match_torch_fp32(seed):
-    pc, view, qd, mlp, gt = _setup(seed=seed)
+def _grads_vs_fp32(pc, campos, rot, raydir, qd, mlp, gt):
+    """One HIP backward (GPU) and one fp32 torch-autograd backward (train.Trainer on the CPU, on
+    the oracle's query of the same rays): the loss, colour and every gradient compared at the
+    module's bars.  Returns the per-tensor relative L2 errors."""
     points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
     tr = HipTrainer(points, mlp, O, DEV)
     d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
-    parts, full, ray_mask = tr.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV))
+    parts, full, ray_mask = tr.backward(d(campos), d(rot), d(raydir), 0.1, 8.0, gt.to(DEV))
     torch.cuda.synchronize()
     pc_points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, "cpu")
     ref = Trainer(pc_points, mlp, O, "cpu")
-    parts_c, full_c, mask_c = ref.backward(torch.from_numpy(view.campos), torch.from_numpy(view.camrotc2w),
-                                           torch.from_numpy(view.raydir), 0.1, 8.0, gt, q=qd)
+    parts_c, full_c, mask_c = ref.backward(torch.from_numpy(campos), torch.from_numpy(rot),
+                                           torch.from_numpy(raydir), 0.1, 8.0, gt, q=qd)
     assert torch.equal(ray_mask.cpu(), mask_c)
     assert abs(float(parts["total"]) - float(parts_c["total"])) <= 1e-3 * abs(float(parts_c["total"]))
     assert float((full.cpu() - full_c).abs().max()) <= 1e-3  # north-star RGB bound
@@ -81,6 +84,38 @@ def test_hip_training_gradients_match_torch_fp32(seed):
     print("relative L2 gradient errors:", {k: f"{v:.2e}" for k, v in worst.items()})
     bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
     assert not bad, bad
+    return worst, int(ray_mask.sum())
+
+
+@pytest.mark.parametrize("seed", [3, 5])
+def test_hip_training_gradients_match_torch_fp32(seed):
+    pc, view, qd, mlp, gt = _setup(seed=seed)
+    _grads_vs_fp32(pc, view.campos, view.camrotc2w, view.raydir, qd, mlp, gt)
+
+
+def test_config5_batch_gradients_match_torch_fp32():
+    """BASELINE config 5 at its workload: one 4096-ray batch (random pixels of a spiral pose of the
+    800x800 frame, as bench.py's training key draws them) over the 1.2 M-point synth-room, SR 24,
+    the opaque aggregator; HIP backward against fp32 autograd of the torch restatement on the
+    oracle's query of the same rays, at the module's gradient bars."""
+    from sgnerf_amd import scene
+    pc = scene.synth_room(1_200_000, seed=0)
+    yaw, pitch = scene.spiral_yaw_pitch(37, 120)
+    view = scene.room_view(800, 800, yaw=yaw + 15.0, pitch=pitch - 5.0)
+    g = torch.Generator().manual_seed(2)
+    idx = torch.randint(0, 800 * 800, (4096,), generator=g).numpy()
+    raydir = np.ascontiguousarray(view.raydir[idx])
+    gt = torch.rand(4096, 3, generator=g)
+    q = oq.OracleGrid(pc.xyz, hyper_for(pc, O), O).query(view.campos, raydir, t_table(O).numpy())
+    rr, ss = np.nonzero(np.arange(O.SR)[None, :] < q["ray_ns"][:, None])
+    ray_ns = torch.from_numpy(q["ray_ns"]).long()
+    qd = {"ray_ns": ray_ns, "ray_soff": torch.cumsum(ray_ns, 0) - ray_ns, "samp_ray": torch.from_numpy(rr).long(),
+          "samp_locw": torch.from_numpy(q["loc_w"][rr, ss]), "pidx": torch.from_numpy(q["pidx"][rr, ss]).long()}
+    mlp = init_mlp(0, bias_std=0.01)
+    mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
+    worst, n_valid = _grads_vs_fp32(pc, view.campos, view.camrotc2w, raydir, qd, mlp, gt)
+    print(f"config 5: 4096 rays, {n_valid} valid, {len(rr)} samples")
+    assert n_valid > 3000
 
 
 def test_hip_training_steps_lower_loss():
