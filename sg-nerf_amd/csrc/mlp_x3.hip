@@ -107,6 +107,60 @@ __device__ __forceinline__ X3B split8(const float (&v)[8]) {
     return r;
 }
 
+// t -> (hi, lo) of x = t * inv (inv a power of two, so x is exact): hi = fp16(x), lo = fp16(x - hi), each
+// half written by one v_fma_mix{lo,hi}_f16 (fp32 FMA, rounded once to fp16): 4 instructions per 2
+// values instead of a multiply each, a pack and the two fma_mix + pack of split8 -- the same bits
+__device__ __forceinline__ X3B split8s(const float (&t)[8], float inv) {
+    u32x4 hi, lo;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t h, l;
+        asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(t[2 * q]), "v"(inv));
+        asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(t[2 * q + 1]), "v"(inv));
+        asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(t[2 * q]), "v"(inv), "v"(h));
+        asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+            : "+v"(l) : "v"(t[2 * q + 1]), "v"(inv), "v"(h));
+        hi[q] = h;
+        lo[q] = l;
+    }
+    return X3B{__builtin_bit_cast(h8, hi), __builtin_bit_cast(h8, lo)};
+}
+// LeakyReLU(0.01) exactly as the reference (x, or fp32(0.01 x) below zero): max(x, 0.01 x) as one
+// v_max_f32 in inline asm -- fmaxf on an MFMA result makes the compiler canonicalise the operand with
+// an extra v_max_f32 x, x, x first (IEEE mode); NaN / inf still propagate (the fp16-range guard)
+#ifndef SGN_X3_LRELU_ASM
+#define SGN_X3_LRELU_ASM 1
+#endif
+__device__ __forceinline__ float lrelu_x3(float a) {
+#if SGN_X3_LRELU_ASM
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(0.01f * a));
+    return r;
+#else
+    return fmaxf(a, 0.01f * a);
+#endif
+}
+#ifndef SGN_X3_MIXCHAIN
+#define SGN_X3_MIXCHAIN 0
+#endif
+// LeakyReLU(2^-s a) as the next layer's (hi, lo) fragment: LeakyReLU commutes with the exact
+// power-of-two scaling, so the scale rides in the fp16 conversion (split8s)
+__device__ __forceinline__ X3B lrelu_split8(const float (&a)[8], float inv) {
+    float v[8];
+#if SGN_X3_MIXCHAIN
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = lrelu_x3(a[j]);
+    return split8s(v, inv);
+#else
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float y = a[j] * inv;
+        v[j] = fmaxf(y, 0.01f * y);
+    }
+    return split8(v);
+#endif
+}
+
 // Timing build (SGN_X3_TIMING): wave w of the first TD_BLOCKS workgroups stamps the clock at the
 // kernel's phase points into tdbg[(block * NW16 + w) * TD_EV + seq] (tools/x3_timing16.py reads it).
 [[maybe_unused]] constexpr int TD_BLOCKS = 8, TD_EV = 2048;
@@ -115,7 +169,7 @@ struct TStamp {
     int seq;
     __device__ __forceinline__ void operator()(int lane) {
 #ifdef SGN_X3_TIMING
-        if (buf && lane == 0 && seq < TD_EV) buf[seq] = clock64();
+        if (buf && lane == 0 && seq < TD_EV - 4) buf[seq] = clock64();
         ++seq;
 #else
         (void)lane;
@@ -123,37 +177,44 @@ struct TStamp {
     }
 };
 
-// one 1-KiB LDS-DMA piece: 16 B per lane from blob byte offset `off` (+ lane * 16)
-__device__ __forceinline__ void lds_dma_1k(const WBlob &wb, char *dst, int lane, uint32_t off) {
+// one 1-KiB LDS-DMA piece of wave w: 16 B per lane from blob byte offset soff + w * 1024 + lane * 16 into
+// LDS dst + w * 1024 (+ lane * 16).  The constant part of the offset is made opaque at its use, so the
+// compiler materialises it right there (one s_mov) instead of hoisting ~70 per-tile offsets into
+// SGPRs that then spill into VGPR lanes.
+__device__ __forceinline__ void lds_dma_1k(const WBlob &wb, char *dst, int w, int lane, uint32_t soff) {
 #ifdef SGN_X3_ABLATE_DMA  // timing experiment only: no weight stream (wrong results)
     return;
 #endif
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)dst, 16, lane * 16, off,
-                                             0, 0);
+#ifndef SGN_X3_DMAOPQ
+#define SGN_X3_DMAOPQ 1
+#endif
+    if (SGN_X3_DMAOPQ) asm volatile("" : "+s"(soff));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)(dst + w * 1024), 16,
+                                             lane * 16 + w * 1024, soff, 0, 0);
 }
 
 // LDS-DMA of stream chunk N into `dst`: 2 * pairs 1-KiB pieces, wave w (of NWv) moves pieces
 // w + NWv j
 template <class Net, int N, int NWv = NW16>
-__device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
+__device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int) {
     using S = Sched<Net>;
     constexpr int nf = 2 * S::pairs(N);
     static_for<(nf + NWv - 1) / NWv>([&](auto jj) {
         constexpr int J = decltype(jj)::value;
         const int i = w + NWv * J;
         if (NWv * (J + 1) <= nf || i < nf)  // wave-uniform
-            lds_dma_1k(wb, dst + i * 1024, lane, S::off(N) + (uint32_t)(i * 1024 + lz));
+            lds_dma_1k(wb, dst + NWv * J * 1024, w, lane, S::off(N) + (uint32_t)(NWv * J * 1024));
     });
 }
 
 // piece J (of this wave's ceil(2 pairs / NWv)) of chunk N
 template <class Net, int N, int J, int NWv = NW16>
-__device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int lane, int lz) {
+__device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int lane, int) {
     using S = Sched<Net>;
     constexpr int nf = 2 * S::pairs(N);
     const int i = w + NWv * J;
     if (NWv * (J + 1) <= nf || i < nf)  // wave-uniform
-        lds_dma_1k(wb, dst + i * 1024, lane, S::off(N) + (uint32_t)(i * 1024 + lz));
+        lds_dma_1k(wb, dst + NWv * J * 1024, w, lane, S::off(N) + (uint32_t)(NWv * J * 1024));
 }
 template <class Net, int N, int NWv = NW16>
 constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NWv - 1) / NWv; }
@@ -193,18 +254,10 @@ struct VmZero {
 };
 
 
-#ifndef SGN_X3_FASTSC
-#define SGN_X3_FASTSC 1
-#endif
 // sin and cos of x (fp32, within ~1 ulp): quadrant q = rint(x 2/pi), r = x - q pi/2 in double
 // (exact to far below fp32 resolution for |x| < 2^20), cephes' minimax polynomials on
 // [-pi/4, pi/4]; |x| >= 2^20 (never met by the encodings' arguments) takes the library sincosf.
-__device__ __forceinline__ void sincos_acc(float x, float &s, float &c) {
-#if SGN_X3_FASTSC
-    if (__builtin_expect(__builtin_fabsf(x) >= 1048576.f, 0)) {
-        sincosf(x, &s, &c);
-        return;
-    }
+__device__ __forceinline__ void sincos_acc_fast(float x, float &s, float &c) {  // |x| < 2^20
     const float qf = __builtin_rintf(x * 0.63661977236758134f);
     const float r = (float)__builtin_fma((double)qf, -1.5707963267948966, (double)x);
     const float z = r * r;
@@ -216,9 +269,13 @@ __device__ __forceinline__ void sincos_acc(float x, float &s, float &c) {
     const float s0 = (q & 1) ? cp : sp, c0 = (q & 1) ? sp : cp;
     s = (q & 2) ? -s0 : s0;
     c = ((q + 1) & 2) ? -c0 : c0;
-#else
-    sincosf(x, &s, &c);
-#endif
+}
+__device__ __forceinline__ void sincos_acc(float x, float &s, float &c) {
+    if (__builtin_expect(__builtin_fabsf(x) >= 1048576.f, 0)) {
+        sincosf(x, &s, &c);
+        return;
+    }
+    sincos_acc_fast(x, s, c);
 }
 
 // accurate sin/cos of x 2^F (the scaling is exact; torch.sin on the product, networks.py:186)
@@ -257,16 +314,21 @@ constexpr size_t BLOB_BYTES_ALL = OFF16_F32 + (size_t)N_Y32 * 4;
 __host__ __device__ constexpr size_t blob_bytes_sg(int) { return BLOB_BYTES_ALL; }
 static_assert(N_Y32 % 4 == 0, "fp32 section in 16-B units");
 
+// block3.2 in two passes of 8 output tiles (SGN_X3_SPLIT3): pass 0 converts the input once and keeps it
+// as (hi, lo) fragments, and the epilogue (K-blend, alpha) of its 8 tiles runs between pass 1's MFMAs
+#ifndef SGN_X3_SPLIT3
+#define SGN_X3_SPLIT3 1
+#endif
+constexpr XL L3_16 = SGN_X3_SPLIT3 ? XL{8, 8, 2, 4, OFF16_W3} : XL{8, 16, 1, 2, OFF16_W3};
 struct NetR16 {
     static constexpr int NL = 4;
-    static constexpr XL L[NL] = {{2, 16, 1, 2, OFF16_W0B}, {8, 16, 1, 2, OFF16_W1}, {9, 16, 1, 2, OFF16_W2},
-                                 {8, 16, 1, 2, OFF16_W3}};
+    static constexpr XL L[NL] = {{2, 16, 1, 2, OFF16_W0B}, {8, 16, 1, 2, OFF16_W1}, {9, 16, 1, 2, OFF16_W2}, L3_16};
 };
 template <int KB>
 struct NetR16SG {
     static constexpr int NL = 5;
     static constexpr XL L[NL] = {{2, 16, 1, 2, OFF16_W0B}, {8, 16, 1, 2, OFF16_W1}, {KB, 16, 1, 2, OFF16_WB},
-                                 {9, 16, 1, 2, OFF16_W2}, {8, 16, 1, 2, OFF16_W3}};
+                                 {9, 16, 1, 2, OFF16_W2}, L3_16};
 };
 struct NetProj16 {
     static constexpr int NL = 1;
@@ -286,17 +348,19 @@ __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
 // One layer, k-outer over all 16 output tiles: acc[t] += W[t] in(k), three MFMAs per
 // (k-step, tile), next chunk's LDS-DMA pieces spread over the first pairs.  TRANS: activations
 // are the A operand (acc[t] holds D[row 4g+i][unit 16t + (l & 15)]).
-template <class Net, int L, bool TRANS = false, class Vm = VmZero, class InFn, class PostFn = NoHook,
-          class EndFn = NoHook>
+// mid(integral_constant F) runs after pair F's MFMAs of every chunk (F counted over the layer: k-step
+// K, tile t -> F = K TP + t), so per-pair VALU work of another stage can ride between the MFMAs.
+template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, class InFn, class PostFn = NoHook,
+          class EndFn = NoHook, class MidFn = NoHook>
 __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
                                             f32x4 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{},
-                                            TStamp *ts = nullptr, EndFn &&end = EndFn{}) {
+                                            TStamp *ts = nullptr, EndFn &&end = EndFn{}, MidFn &&mid = MidFn{}) {
     constexpr XL ly = Net::L[L];
     constexpr int TP = ly.tp;
-    static_assert((TP == 16 || TP == 8) && ly.np == 1, "single-pass layers of 16 or 8 output tiles");
+    static_assert((TP == 16 || TP == 8) && P < ly.np, "passes of 16 or 8 output tiles");
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
-        constexpr int N = Sched<Net>::idx(L, 0, C), NN = (N + 1) % Sched<Net>::total();
+        constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
         chunk_enter<Net, N, NW16, Vm::vm(C)>(wb, lds, slot, w, lane, lz, ts);
         post(cc);
         const char *sl = lds + slot * SLOT;
@@ -338,6 +402,7 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slo
                         dma_piece<Net, NN, F * PW / NS + decltype(jj)::value, NW16>(wb, dnext, w, lane, lz);
                     });
                 }
+                mid(std::integral_constant<int, (C * ly.kc + KK) * TP + t>{});
 #if SGN_X3_PIN
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -454,17 +519,16 @@ __global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
 
 // ---- per-neighbour rows (16x16) -------------------------------------------------------------
 constexpr int WG16_SAMPLES = NW16 * 2;            // 16 samples = 128 rows per workgroup tile
-#ifndef SGN_X3_YT
-#define SGN_X3_YT 1  // block3.2 bias / alpha weights transposed per lane (16-B LDS reads in the epilogue)
-#endif
-constexpr int YT16_OFF = Y_LDS_OFF + N_Y32 * 4;  // [unit r][20] b3 (t = 0..15) then [r][20] alpha w
-constexpr int ROWS16_LDS = YT16_OFF + (SGN_X3_YT ? 2 * 16 * 20 * 4 : 0);
+constexpr int YT16_OFF = Y_LDS_OFF + N_Y32 * 4;  // [unit r][20] 2^s3 b3 (t = 0..15) then [r][20] 2^-s3 alpha w
+constexpr int ROWS16_LDS = YT16_OFF + 2 * 16 * 20 * 4;
 static_assert(ROWS16_LDS <= 163840, "LDS budget (16x16 rows)");
 
 // row r's point record, its sample position and view direction (+ the caller's pers
 // coordinates on the compatibility path)
+template <bool PERS>
 struct Rec16 {
-    float p[3], col[3], dir[3], cf, l[3], v[3], pp[3], pl[3];
+    float p[3], col[3], dir[3], cf, l[3], v[3];
+    float pp[PERS ? 3 : 1], pl[PERS ? 3 : 1];  // the caller's pers coordinates (PointAggregator path only)
 };
 // Rows without a work item (ix.sval false: the tail of the work list, or a launch with no
 // samples at all, where samp_ray holds no written entry) read nothing.
@@ -474,8 +538,9 @@ struct Rec16 {
 // without a work item or neighbour read the weight blob instead and select zeros), so a caller may
 // count them (REC16_LOADS) in a chunk boundary's vmcnt allowance.
 constexpr int REC16_LOADS = 9;
-__device__ __forceinline__ Rec16 load_rec16(const AggArgs &a, const RowIdx &ix) {
-    Rec16 r;
+template <bool PERS>
+__device__ __forceinline__ Rec16<PERS> load_rec16(const AggArgs &a, const RowIdx &ix) {
+    Rec16<PERS> r;
     const bool v = ix.sval;
     const int pid = ix.pid, s = ix.s, ray = ix.ray;
     const bool m = v && pid >= 0;
@@ -497,8 +562,10 @@ __device__ __forceinline__ Rec16 load_rec16(const AggArgs &a, const RowIdx &ix) 
         r.dir[c] = m ? q2[c] : 0.f;
         r.l[c] = v ? l3[c] : 0.f;
         r.v[c] = v ? v3[c] : 0.f;
-        r.pp[c] = (a.pers && m) ? a.pers[(int64_t)pid * 3 + c] : 0.f;
-        r.pl[c] = (a.pers && v) ? a.samp_pers[(int64_t)s * 3 + c] : 0.f;
+        if constexpr (PERS) {
+            r.pp[c] = m ? a.pers[(int64_t)pid * 3 + c] : 0.f;
+            r.pl[c] = v ? a.samp_pers[(int64_t)s * 3 + c] : 0.f;
+        }
     }
     r.cf = m ? q0[3] : 0.f;
     return r;
@@ -507,8 +574,12 @@ __device__ __forceinline__ Rec16 load_rec16(const AggArgs &a, const RowIdx &ix) 
 // tile's record (REC16_LOADS loads, the youngest); after block3.2 come the next tile's 16 P loads
 // (and the epilogue's f_s stores, masked per segment, so not counted), all younger than block1.0's
 // DMA
-struct VmL3 {
-    static constexpr int vm(int c) { return c == 1 ? REC16_LOADS : 0; }
+// vmcnt allowances of k_rows16's boundaries (chunk_enter VM): block3.2 ends its first chunk with the next
+// tile's record (REC16_LOADS loads) and this tile's slot entry (1), the youngest; after block3.2 come the
+// next tile's 16 P loads (and the epilogue's f_s stores, masked per segment, so not counted), all
+// younger than block1.0's DMA
+struct VmL3P0 {
+    static constexpr int vm(int c) { return c == 1 ? REC16_LOADS + 1 : 0; }
 };
 struct VmL0 {
     static constexpr int vm(int) { return 16; }
@@ -652,7 +723,8 @@ struct Row16 {
     float d[6];
     float wgt, wn;
 };
-__device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, const Rec16 &rc, bool m, bool isA,
+template <bool PERS>
+__device__ __forceinline__ Row16 row_math16(const Cam &cam, const Rec16<PERS> &rc, bool m, bool isA,
                                             int nA, bool waveB) {
     Row16 o;
     const float dwx = __fsub_rn(rc.p[0], rc.l[0]), dwy = __fsub_rn(rc.p[1], rc.l[1]), dwz = __fsub_rn(rc.p[2], rc.l[2]);
@@ -660,7 +732,7 @@ __device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, co
     o.d[1] = m ? dwy : 0.f;
     o.d[2] = m ? dwz : 0.f;
     float xp, yp, zp, xl, yl, zl;
-    if (a.pers) {
+    if constexpr (PERS) {
         xp = rc.pp[0]; yp = rc.pp[1]; zp = rc.pp[2];
         xl = rc.pl[0]; yl = rc.pl[1]; zl = rc.pl[2];
     } else {
@@ -701,31 +773,85 @@ __device__ __forceinline__ Row16 row_math16(const AggArgs &a, const Cam &cam, co
     return o;
 }
 
-// PE(dists) of the row (networks.py:175-192, 6 values x 5 frequencies): (value, frequency) pair
-// pp = 8 g + c of lane group g, c = 0..7 (pairs 30, 31 padding) -> k-step c / 4, slots 2 (c % 4),
-// 2 (c % 4) + 1 = sin, cos of d[pp / 5] 2^(pp % 5) (col_l0b16 maps them to reference columns)
-// k-step S's fragment: pairs c = 4 S .. 4 S + 3 (block1.0 computes it inside its k-loop, so the
-// second k-step's sin / cos overlap the first one's MFMAs)
+// PE(dists) of the row (networks.py:175-192, 6 values x 5 frequencies, sin / cos interleaved): pair
+// slot c = 0..7 of lane group g (k-step c / 4, B slots 2 (c % 4), 2 (c % 4) + 1 = sin, cos) holds
+//   c < 5 : component g,           frequency c
+//   c = 5 : component 4 + (g & 1), frequency (g >= 2)        c = 6 : the same, frequency 2 + (g >= 2)
+//   c = 7 : component 4 + (g & 1), frequency 4 (g < 2; padding for g >= 2)
+// so every frequency is a compile-time power of two and a lane selects only its two components once
+// per tile (PeRow); col_l0b16 maps the slots to the reference columns.
+struct PeRow {
+    float lo, hi, shi;  // d[g], d[4 + (g & 1)], 2 if g >= 2 else 1
+};
+__device__ __forceinline__ PeRow pe_row16(const float (&d)[6], int g) {
+    PeRow r;
+    r.lo = g == 0 ? d[0] : g == 1 ? d[1] : g == 2 ? d[2] : d[3];
+    r.hi = (g & 1) ? d[5] : d[4];
+    r.shi = g >= 2 ? 2.f : 1.f;
+    return r;
+}
+// slot c's argument: the component times its frequency 2^f (exact scaling, as positions * freq_bands)
+template <int C>
+__device__ __forceinline__ float pe_arg16(const PeRow &r) {
+    if constexpr (C < 5) return r.lo * (float)(1 << C);
+    else if constexpr (C == 7) return r.hi * 16.f;
+    else return r.hi * (r.shi * (float)(1 << (2 * (C - 5))));
+}
+// k-step S's fragment: slots c = 4 S .. 4 S + 3 (block1.0 computes it inside its k-loop, so the
+// second k-step's sin / cos overlap the first one's MFMAs).  Arguments of 2^20 and above (never met
+// by the aggregator's distances) take the library sincosf, behind one wave-uniform branch.
 template <int S>
-__device__ __forceinline__ X3B pe_dists16_k(const float (&d)[6], int g) {
-    float u[8];
+__device__ __forceinline__ X3B pe_dists16_k(const PeRow &r) {
+    float x[4], u[8];
+    static_for<4>([&](auto cc) { x[decltype(cc)::value] = pe_arg16<4 * S + decltype(cc)::value>(r); });
+    const float m = fmaxf(fmaxf(__builtin_fabsf(x[0]), __builtin_fabsf(x[1])), fmaxf(__builtin_fabsf(x[2]), __builtin_fabsf(x[3])));
+    if (__builtin_expect(__ballot(!(m < 1048576.f)) != 0, 0)) {
 #pragma unroll
-    for (int c = 4 * S; c < 4 * S + 4; ++c) {
-        const int pp = 8 * g + c, di = pp / 5, f = pp - 5 * di;
-        float x = d[0];
+        for (int q = 0; q < 4; ++q) sincosf(x[q], &u[2 * q], &u[2 * q + 1]);
+    } else {
 #pragma unroll
-        for (int q = 1; q < 6; ++q) x = di == q ? d[q] : x;
-        float sv, cv;
-        sincos_acc(__builtin_ldexpf(x, f), sv, cv);
-        const bool ok = pp < 30;
-        u[2 * (c - 4 * S)] = ok ? sv : 0.f;
-        u[2 * (c - 4 * S) + 1] = ok ? cv : 0.f;
+        for (int q = 0; q < 4; ++q) sincos_acc_fast(x[q], u[2 * q], u[2 * q + 1]);
     }
     return split8(u);
 }
 
+// block3.2 epilogue of a tile (K-blend -> f_s, alpha), per lane: rows 4 g + i of half g >> 1
+#ifndef SGN_X3_B3FOLD
+#define SGN_X3_B3FOLD 1  // block3.2's bias in its accumulator init, 2^-s3 folded into the blend / alpha weights
+#endif
+#ifndef SGN_X3_STORE1
+#define SGN_X3_STORE1 0  // 1: each f_s value stored as it is blended (else per 4 under one branch)
+#endif
+struct Epi16 {
+    float wsa[4], wsb[4];   // the rows' blend weights split by segment (A: positions < nA, B: the rest),
+                            // times 2^-s3 (block3.2's accumulators hold 2^s3 (W x + b))
+    float ap[4];            // alpha partials of the 4 rows over this lane's units
+    float fsv[4];           // blended features of units 16 t + r, t = 4 (T / 4) .. + 3, stored per 4
+    float *fs_dst;
+    bool fs_have;
+    float inv3;
+};
+
+// a workgroup's tiles under the XCD-aware order: tiles first, first + step, ... < end
+struct XcdTiles {
+    int first, end, step;
+};
+__device__ __forceinline__ XcdTiles xcd_tiles(int ntiles) {
+#ifndef SGN_X3_XCD
+#define SGN_X3_XCD 0
+#endif
+    const int nx = SGN_X3_XCD && gridDim.x % 8 == 0 ? 8 : 1;  // only when the grid covers the XCDs evenly
+    const int per = gridDim.x / nx, x = blockIdx.x % nx, j = blockIdx.x / nx;
+    const int len = (ntiles + nx - 1) / nx, r0 = x * len;
+    XcdTiles t;
+    t.first = r0 + j;
+    t.end = min(ntiles, r0 + len);
+    t.step = per;
+    return t;
+}
+
 // KB: k-steps of block2_bpnet.0 in 16x16 steps (0: base viewmlp; 8: bpnet_dim 0; 11: dim 96)
-template <int KB>
+template <int KB, bool PERS>
 __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     using Net = std::conditional_t<(KB > 0), NetR16SG<KB>, NetR16>;
     constexpr int LB = 2, L2 = KB ? 3 : 2, L3 = KB ? 4 : 3;
@@ -742,7 +868,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         const float *src = (const float *)((const char *)a.blob + OFF16_F32);
         float *dst = (float *)(lds + Y_LDS_OFF);
         for (int i = threadIdx.x; i < N_Y32; i += TPB16) dst[i] = src[i];
-        if constexpr (SGN_X3_YT) {
+        {
             // row stride 20 floats: the 16 lanes' 16-B reads of one column quad hit disjoint banks
             float *yt = (float *)(lds + YT16_OFF);
             for (int i = threadIdx.x; i < 512; i += TPB16) {
@@ -757,8 +883,13 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     // The next tile's chain, prefetched inside the current tile so each step lands under MFMAs:
     // row-table entry (block1.2), neighbour / ray index (block3.0), point record + sample position
     // and the P row (block3.2).  First tile: here.
-    RowIdx nx = row_index16(a, blockIdx.x * WG16_SAMPLES + w * 2 + sc, nslots, kk);
-    Rec16 rnext = load_rec16(a, nx);
+    // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one),
+    // so XCD x = b % 8 walks its own contiguous eighth of the tiles.  Neighbouring tiles hold samples of
+    // neighbouring rays, which gather largely the same points: their P rows and records then meet in
+    // that XCD's L2 instead of being fetched from HBM by all eight.
+    const XcdTiles xt = xcd_tiles((nslots + WG16_SAMPLES - 1) / WG16_SAMPLES);
+    RowIdx nx = row_index16(a, xt.first * WG16_SAMPLES + w * 2 + sc, nslots, kk);
+    Rec16<PERS> rnext = load_rec16<PERS>(a, nx);
     // P row of point pid into `dst`: natural unit order, tile t of lane group g at 16 t + 4 g, so the
     // 4 lanes of a row read one contiguous 64 B per load instruction
     auto load_p = [&](int pid, f32x4 (&dst)[16]) {
@@ -774,28 +905,115 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
 #ifdef SGN_X3_TIMING
     TStamp tsv{blockIdx.x < TD_BLOCKS && a.tdbg ? a.tdbg + ((int64_t)blockIdx.x * NW16 + w) * TD_EV : nullptr, 0};
     TStamp *ts = &tsv;
+    // in-kernel clock (MI355X_MICROARCH.md 'DVFS give-back' item 6): s_memtime and s_memrealtime
+    // (100 MHz) around the tile loop, in the last four words of the wave's stamp area
+    if (tsv.buf && lane == 0) {
+        tsv.buf[TD_EV - 4] = __builtin_amdgcn_s_memtime();
+        tsv.buf[TD_EV - 3] = __builtin_amdgcn_s_memrealtime();
+    }
 #define X3T() tsv(lane)
 #else
     TStamp *ts = nullptr;
 #define X3T()
 #endif
 
-    for (int base = blockIdx.x * WG16_SAMPLES; base < nslots; base += gridDim.x * WG16_SAMPLES) {
+    // epilogue pieces (LDS reads through the tile's opaque base)
+    auto epi_begin = [&](Epi16 &e, const char *ldsi, float wgt, int nA, int nB, int2 ce, bool ok) {
+        const float inv3 = ((const float *)(ldsi + Y_LDS_OFF))[Y_INV + 3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float wi = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, wgt)));
+            const bool inA = 4 * (g & 1) + i < nA;
+            const float ws = SGN_X3_B3FOLD ? wi * inv3 : wi;
+            e.wsa[i] = inA ? ws : 0.f;
+            e.wsb[i] = inA ? 0.f : ws;
+            e.ap[i] = 0.f;
+        }
+        e.fs_have = ((g & 1) ? nB > 0 : nA > 0) && ok;
+        e.inv3 = inv3;
+        e.fs_dst = (float *)a.fs + (int64_t)((uint32_t)((g & 1) ? ce.y : ce.x) & 0x0FFFFFFFu) * HID + r;
+    };
+    // block3.2 output tile T of accumulators `ac` (2^s3 (W x + b)): LeakyReLU, alpha partials, K-blend
+    auto epi_step = [&](Epi16 &e, const char *ldsi, const f32x4 (&ac)[16], auto tc) {
+        constexpr int T = decltype(tc)::value;
+        const float wau = ((const float *)(ldsi + YT16_OFF))[320 + r * 20 + T];  // 2^-s3 alpha weight
+        float fa = 0.f, fb = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float hv = SGN_X3_B3FOLD ? lrelu_x3(ac[T][i])
+                                           : lrelu_x3(__builtin_fmaf(ac[T][i], e.inv3,
+                                                                     ((const float *)(ldsi + YT16_OFF))[r * 20 + T]));
+            e.ap[i] = __builtin_fmaf(wau, hv, e.ap[i]);
+            fa = __builtin_fmaf(e.wsa[i], hv, fa);
+            fb = __builtin_fmaf(e.wsb[i], hv, fb);
+        }
+        // + the half's other 4 rows (lane group g ^ 1, 16 lanes away): the swap leaves A's pair of chains
+        // in the even groups and B's in the odd ones.  Per sample this is (chain over its rows 0..3) +
+        // (chain over rows 4..7) at any offset: B sits in one group (zero-weight rows leave a chain
+        // unchanged, the other group's chain is 0)
+        permlane16_swap(fa, fb);
+        e.fsv[T & 3] = fa + fb;
+        if constexpr (SGN_X3_STORE1) {
+            if (e.fs_have) e.fs_dst[16 * T] = e.fsv[T & 3];
+        } else if constexpr ((T & 3) == 3) {  // 16 lanes write 64 contiguous bytes of the work item's row, per 4
+            if (e.fs_have) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) e.fs_dst[16 * (T - 3 + u)] = e.fsv[u];
+            }
+        }
+    };
+    auto epi_end = [&](Epi16 &e, const char *ldsi, int nA, int nB, int s_ix) {
+        // alpha: row logits summed over the 16 lanes (units) of the group, softplus(x + b - 1), blended
+        // over the segment's rows like f_s
+        const float ba = ((const float *)(ldsi + Y_LDS_OFF))[Y_BA];
+        const float sc3 = SGN_X3_B3FOLD ? 1.f / e.inv3 : 1.f;  // 2^s3, exact
+        float xr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float x = dpp_sum8(e.ap[i]);
+            x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
+            xr[i] = x;
+        }
+        // one softplus per lane: lane r takes row 4 g + (r & 3), and each lane then reads the four rows'
+        // values from its quad (quad_perm broadcasts) -- 16x fewer log1p / exp than every lane
+        // evaluating its four rows
+        const int q4 = r & 3;
+        const float spm = softplus((q4 == 0 ? xr[0] : q4 == 1 ? xr[1] : q4 == 2 ? xr[2] : xr[3]) + ba - 1.f);
+        const int spi = __builtin_bit_cast(int, spm);
+        const float sp4[4] = {__builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(spi, 0x00, 0xF, 0xF, true)),
+                              __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(spi, 0x55, 0xF, 0xF, true)),
+                              __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(spi, 0xAA, 0xF, 0xF, true)),
+                              __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(spi, 0xFF, 0xF, 0xF, true))};
+        float asa = 0.f, asb = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // the rows' weights: 2^s3 (2^-s3 w), exact
+            asa = __builtin_fmaf(e.wsa[i] * sc3, sp4[i], asa);
+            asb = __builtin_fmaf(e.wsb[i] * sc3, sp4[i], asb);
+        }
+        permlane16_swap(asa, asb);
+        const float as = asa + asb;  // even groups: A's alpha, odd groups: B's
+        // the segment's sample: row 0 (A) or row max(nA, 4) (B) of the half (lanes 0..15 hold rows)
+        const int s_of = __builtin_amdgcn_ds_bpermute((8 * (g >> 1) + ((g & 1) ? (nA > 4 ? nA : 4) : 0)) * 4, s_ix);
+        if (r == 0 && ((g & 1) ? nB > 0 : nA > 0)) a.feat[(int64_t)s_of * 4 + 0] = as;
+    };
+
+    for (int tile = xt.first; tile < xt.end; tile += xt.step) {
+        const int base = tile * WG16_SAMPLES;
         int lz = 0;
         asm volatile("" : "+s"(lz));
         char *ldsi = lds + lz;
         const float *Yl = (const float *)(ldsi + Y_LDS_OFF);
         const int hslot = base + w * 2 + sc;  // this lane's half (the LDS ring slot is `slot`)
-        const int nslot = hslot + gridDim.x * WG16_SAMPLES;
+        const int nslot = tile + xt.step < xt.end ? hslot + xt.step * WG16_SAMPLES : nslots;  // next tile's half
         X3T();  // tile start
         const RowIdx ix = nx;
         const bool m = ix.pid >= 0;
-        const Rec16 rc = rnext;
+        const Rec16<PERS> rc = rnext;
         // rows of the two segments (lane group 0 = rows 0..15): bits 8 h .. 8 h + 7 are half h's
         const uint64_t mrowA = __ballot(ix.sval && ix.a), mrowB = __ballot(ix.sval && !ix.a);
         const int nA0 = __popc((uint32_t)mrowA & 0xFFu), nA1 = __popc(((uint32_t)mrowA >> 8) & 0xFFu);
         const bool waveB = (mrowB & 0xFFFFull) != 0;  // wave-uniform: a B sample in either half
-        const Row16 rw = row_math16(a, cam, rc, m, ix.a, sc ? nA1 : nA0, waveB);
+        const Row16 rw = row_math16<PERS>(cam, rc, m, ix.a, sc ? nA1 : nA0, waveB);
         if ((a.blend || a.wnorm) && ix.sval) {  // optional outputs: the row's pidx index from the table
             const int v = a.rows[(int64_t)hslot * 8 + kk];
             if (a.blend && g == 0) a.blend[v] = rw.wgt;
@@ -821,24 +1039,22 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
             constexpr int S = decltype(kc)::value;
             float v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float y = ac[2 * S + (j >> 2)][j & 3] * inv;
-                v[j] = fmaxf(y, 0.01f * y);
-            }
-            return split8(v);
+            for (int j = 0; j < 8; ++j) v[j] = ac[2 * S + (j >> 2)][j & 3];
+            return lrelu_split8(v, inv);
         };
         auto bias_init = [&](f32x4 (&ac)[16], int yb) {
 #pragma unroll
             for (int t = 0; t < 16; ++t) ac[t] = *(const f32x4 *)(Yl + yb + 16 * t + 4 * g);
         };
         {   // block1.0: W0b PE(dists) on MFMA, + P[pid] (W0a [feat | PE(feat)] + b0, k_point_proj16)
+            const PeRow pr = pe_row16(rw.d, g);
             X3T();  // gather (PE inside block1.0's k-loop)
             if constexpr (KB > 0) {  // SG: five layers, the P array alternates -- copy it back
 #pragma unroll
                 for (int t = 0; t < 16; ++t) accA[t] = accB[t];
             }
             run_layer16<Net, 0, false, VmL0>(wb, ldsi, slot, w, lane, lz, accA,
-                                             [&](auto k) { return pe_dists16_k<decltype(k)::value>(rw.d, g); },
+                                             [&](auto k) { return pe_dists16_k<decltype(k)::value>(pr); },
                                              NoHook{}, ts);
         }
         // block1.2: 256 -> 256 (input: block1.0 accumulators)
@@ -889,100 +1105,86 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         }, ts);
         // block3.2: 256 -> 256 transposed: acc[t][i] = h[row 4 g + i][unit 16 t + (l & 15)]
         auto &acc = in2;  // block3.0's input is dead: its registers take block3.2's accumulators
+        {   // start at the bias (2^s3 b3[16 t + r], the transposed LDS copy: 4 x 16 B per lane)
+            const float *ytb = (const float *)(ldsi + YT16_OFF) + r * 20;
 #pragma unroll
-        for (int t = 0; t < 16; ++t) acc[t] = f32x4{};
-        // the next tile's record goes out at the end of block3.2's first chunk (after the chunk's DMA
-        // pieces, so it stays in flight across one boundary, VmL3); the slot entry of this lane's half
-        // in the epilogue's layout (half g >> 1: {A item | nA << 28, B item | nB << 28, ..}) at the end
-        // of the third (landed by the epilogue's first f_s store)
+            for (int t4 = 0; t4 < 4; ++t4) {
+                const f32x4 b = *(const f32x4 *)(ytb + 4 * t4);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[4 * t4 + u] = SGN_X3_B3FOLD ? f32x4{b[u], b[u], b[u], b[u]} : f32x4{};
+            }
+        }
+        // the next tile's record (and this tile's slot entry for the epilogue: half g >> 1's
+        // {A item | nA << 28, B item | nB << 28, ..}) go out at the end of block3.2's first chunk, after
+        // the chunk's DMA pieces, so they stay in flight across one boundary (VmL3)
         int2 ce = make_int2(0, 0);
         const int eslot = base + w * 2 + (g >> 1);
-        run_layer16<Net, L3, true, VmL3>(wb, ldsi, slot, w, lane, lz, acc,
-                                         [&](auto k) { return chain_k(acc2, inv2, k); }, NoHook{}, ts,
-                                         [&](auto c) {
-                                             constexpr int C = decltype(c)::value;
-                                             if constexpr (C == 0) rnext = load_rec16(a, nx);
-                                             if constexpr (C == nch(Net::L[L3]) - 2)
-                                                 ce = *(const int2 *)(a.slots + (eslot < nslots ? eslot : 0));
-                                         });
+        const int hsh = 8 * (g >> 1);  // half g >> 1's row bits
+        const int nA = __popcll((mrowA >> hsh) & 0xFFull), nB = __popcll((mrowB >> hsh) & 0xFFull);
+        auto first_chunk_loads = [&](auto c) {
+            if constexpr (decltype(c)::value == 0) {
+                rnext = load_rec16<PERS>(a, nx);
+                ce = *(const int2 *)(a.slots + (eslot < nslots ? eslot : 0));
+            }
+        };
+        Epi16 e;
+        if constexpr (SGN_X3_SPLIT3) {
+            // pass 0 (output tiles 0..7) converts block3.0's output once into (hi, lo) fragments (in the
+            // registers it frees) and pass 1 (tiles 8..15) reuses them; pass 1 carries the epilogue of
+            // pass 0's tiles, output tile T after k-step T (one per 8 MFMA pairs)
+            X3B in3[8];
+            auto &acc0 = reinterpret_cast<f32x4(&)[8]>(acc[0]);
+            auto &acc1 = reinterpret_cast<f32x4(&)[8]>(acc[8]);
+            run_layer16<Net, L3, true, VmL3P0, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) {
+                constexpr int K = decltype(k)::value;
+                in3[K] = chain_k(acc2, inv2, k);
+                return in3[K];
+            }, NoHook{}, ts, first_chunk_loads);
+            epi_begin(e, ldsi, rw.wgt, nA, nB, ce, eslot < nslots);
+            run_layer16<Net, L3, true, VmZero, 1>(wb, ldsi, slot, w, lane, lz, acc1,
+                                                  [&](auto k) { return in3[decltype(k)::value]; }, NoHook{}, ts,
+                                                  NoHook{}, [&](auto f) {
+                                                      constexpr int F = decltype(f)::value;
+                                                      if constexpr ((F & 7) == 7)
+                                                          epi_step(e, ldsi, acc, std::integral_constant<int, F / 8>{});
+                                                  });
+        } else {
+            run_layer16<Net, L3, true, VmL3P0>(wb, ldsi, slot, w, lane, lz, acc,
+                                               [&](auto k) { return chain_k(acc2, inv2, k); }, NoHook{}, ts,
+                                               first_chunk_loads);
+            epi_begin(e, ldsi, rw.wgt, nA, nB, ce, eslot < nslots);
+        }
         X3T();  // block3.2 MFMAs issued
         // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads
         // from the compiler's wait tracking, which would otherwise wait for the epilogue's stores
         asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-            asm volatile("" : "+v"(rnext.p[c]), "+v"(rnext.col[c]), "+v"(rnext.dir[c]), "+v"(rnext.l[c]), "+v"(rnext.v[c]),
-                              "+v"(rnext.pp[c]), "+v"(rnext.pl[c]));
+        for (int c = 0; c < 3; ++c) {
+            asm volatile("" : "+v"(rnext.p[c]), "+v"(rnext.col[c]), "+v"(rnext.dir[c]), "+v"(rnext.l[c]), "+v"(rnext.v[c]));
+            if constexpr (PERS) asm volatile("" : "+v"(rnext.pp[c]), "+v"(rnext.pl[c]));
+        }
         asm volatile("" : "+v"(rnext.cf));
-        const int hsh = 8 * (g >> 1);  // half g >> 1's row bits
-        const int nA = __popcll((mrowA >> hsh) & 0xFFull), nB = __popcll((mrowB >> hsh) & 0xFFull);
-        {   // epilogue
-            // row weights of this lane's rows 4 g + i (position 4 (g & 1) + i of half g >> 1), split by
-            // segment: A = positions < nA, B = the rest (idle rows weigh 0)
-            float wa[4], wb4[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float wi = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, rw.wgt)));
-                const bool inA = 4 * (g & 1) + i < nA;
-                wa[i] = inA ? wi : 0.f;
-                wb4[i] = inA ? 0.f : wi;
-            }
-            const float inv3 = Yl[Y_INV + 3];
-            float ap[4] = {0.f, 0.f, 0.f, 0.f};
-            // f_s of this lane's segment (A of half g >> 1 in even groups, B in odd ones), unit 16 t + r,
-            // stored as each t is blended: 16 lanes write 64 contiguous bytes of the work item's row
-            const bool fs_have = ((g & 1) ? nB > 0 : nA > 0) && eslot < nslots;
-            float *fs_dst = (float *)a.fs + (int64_t)((uint32_t)((g & 1) ? ce.y : ce.x) & 0x0FFFFFFFu) * HID + r;
-            // the next tile's P rows (see accA) go out tile by tile between the epilogue's VALU work
+        {   // the rest of the epilogue; the next tile's P rows (see accA) go out first, into block3.2's
+            // consumed input registers, and land under it
             const float *psrc = proj + (int64_t)(nx.pid < 0 ? 0 : nx.pid) * HID + 4 * g;
-            f32x4 bu4 = {}, wa4 = {};
-            const float *ytb = (const float *)(ldsi + YT16_OFF) + r * 20;
+            constexpr int NE = SGN_X3_SPLIT3 ? 8 : 16, PPE = 16 / NE;  // epilogue steps left, P loads per step
+            static_for<NE>([&](auto tc) {  // the loads spread between the steps (a burst stalls the issue)
+                constexpr int J = decltype(tc)::value;
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                acc2[t] = *(const f32x4 *)(psrc + 16 * t);
-                if (SGN_X3_YT && (t & 3) == 0) {
-                    bu4 = *(const f32x4 *)(ytb + t);
-                    wa4 = *(const f32x4 *)(ytb + 320 + t);
-                }
-                const float bu = SGN_X3_YT ? bu4[t & 3] : Yl[Y_B3 + 16 * t + r];
-                const float wau = SGN_X3_YT ? wa4[t & 3] : Yl[Y_WA + 16 * t + r];
-                float fa = 0.f, fb = 0.f;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float y = __builtin_fmaf(acc[t][i], inv3, bu);
-                    const float hv = fmaxf(y, 0.01f * y);
-                    ap[i] = __builtin_fmaf(wau, hv, ap[i]);
-                    fa = __builtin_fmaf(wa[i], hv, fa);
-                    fb = __builtin_fmaf(wb4[i], hv, fb);
-                }
-                // + the half's other 4 rows (lane group g ^ 1, 16 lanes away): the swap leaves A's pair
-                // of chains in the even groups and B's in the odd ones.  Per sample this is (chain over
-                // its rows 0..3) + (chain over rows 4..7) at any offset: B sits in one group (zero-weight
-                // rows leave a chain unchanged, the other group's chain is 0)
-                permlane16_swap(fa, fb);
-                if (fs_have) fs_dst[16 * t] = fa + fb;
-            }
+                for (int u = 0; u < PPE; ++u) acc2[PPE * J + u] = *(const f32x4 *)(psrc + 16 * (PPE * J + u));
+                epi_step(e, ldsi, acc, std::integral_constant<int, (16 - NE) + J>{});
+            });
             X3T();  // block3.2 epilogue (K-blend, alpha partials)
-            // alpha: row logits summed over the 16 lanes (units) of the group, softplus(x + b - 1),
-            // blended over the segment's rows like f_s
-            float asa = 0.f, asb = 0.f;
-            const float ba = Yl[Y_BA];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float x = dpp_sum8(ap[i]);
-                x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, true));
-                const float sp = softplus(x + ba - 1.f);
-                asa = __builtin_fmaf(wa[i], sp, asa);
-                asb = __builtin_fmaf(wb4[i], sp, asb);
-            }
-            permlane16_swap(asa, asb);
-            const float as = asa + asb;  // even groups: A's alpha, odd groups: B's
-            // the segment's sample: row 0 (A) or row max(nA, 4) (B) of the half (lanes 0..15 hold rows)
-            const int s_of = __builtin_amdgcn_ds_bpermute((hsh + ((g & 1) ? (nA > 4 ? nA : 4) : 0)) * 4, ix.s);
-            if (r == 0 && ((g & 1) ? nB > 0 : nA > 0)) a.feat[(int64_t)s_of * 4 + 0] = as;
+            epi_end(e, ldsi, nA, nB, ix.s);
         }
         X3T();  // tile end
     }
+#ifdef SGN_X3_TIMING
+    if (tsv.buf && lane == 0) {
+        tsv.buf[TD_EV - 2] = __builtin_amdgcn_s_memtime();
+        tsv.buf[TD_EV - 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 #undef X3T
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -992,22 +1194,37 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
 int perm16(int p) { return 16 * ((p & 7) >> 2) + 4 * (p >> 3) + (p & 3); }
 int col_chain16(int ks, int p) { return 32 * ks + perm16(p); }
 int col_l2_16(int ks, int p) { return ks < 8 ? col_chain16(ks, p) : (p < 7 ? 256 + p : -1); }
-int col_l0b16(int s, int p) {  // pe_dists16: pair 8 g + 4 s + j / 2, sin / cos by j parity
-    const int pp = 8 * (p >> 3) + 4 * s + ((p & 7) >> 1);
-    return pp < 30 ? 224 + 2 * pp + (p & 1) : -1;
+int col_l0b16(int s, int p) {  // pe_dists16_k: slot c = 4 s + e / 2 of lane group g, sin / cos by e parity
+    const int g = p >> 3, c = 4 * s + ((p & 7) >> 1);
+    int comp, f;
+    if (c < 5) {
+        comp = g;
+        f = c;
+    } else {
+        comp = 4 + (g & 1);
+        f = c == 5 ? (g >= 2) : c == 6 ? 2 + (g >= 2) : 4;
+        if (c == 7 && g >= 2) return -1;  // padding
+    }
+    return 224 + 2 * (5 * comp + f) + (p & 1);
 }
 int col_proj16(int s, int p) { return s == 0 ? p : 32 + 48 * (p >> 3) + 8 * (s - 1) + (p & 7); }
 int col_bp16(int ks, int p) { return ks < 8 ? col_chain16(ks, p) : 256 + 32 * (ks - 8) + p; }
-int col_c016(int ks, int p) { return ks < 8 ? 32 * ks + p : (p < 24 ? 256 + p : -1); }
+int col_c016(int ks, int p) {  // k-step 8: lane group g = p / 8 < 3 holds sin, cos of v_g 2^f at slots 2 f, 2 f + 1
+    if (ks < 8) return 32 * ks + p;
+    const int g = p >> 3, f = (p & 7) >> 1;
+    return g < 3 ? 256 + ((p & 1) ? 12 : 0) + 4 * g + f : -1;
+}
 
 // 16 output tiles of 16 units, one pass, k-outer: pair f = ks * 16 + t; A[unit][k] fragment
 // lane l: unit 16 t + (l & 15), input col(ks, 8 (l >> 4) + e)
 template <typename ColFn>
-void pack_pairs16(_Float16 *dst, const float *W, int n_out, int n_in, int KS, int shift, ColFn col, int NT = 16) {
+void pack_pairs16(_Float16 *dst, const float *W, int n_out, int n_in, int KS, int shift, ColFn col, int NT = 16,
+                  int NP = 1) {
     const float sc = ldexpf(1.f, shift);
+    const int TPP = NT / NP;  // output tiles per pass: pair f = (pass KS + ks) TPP + t % TPP
     for (int t = 0; t < NT; ++t)
         for (int ks = 0; ks < KS; ++ks) {
-            const size_t f = (size_t)ks * NT + t;
+            const size_t f = ((size_t)(t / TPP) * KS + ks) * TPP + t % TPP;
             for (int lane = 0; lane < 64; ++lane)
                 for (int e = 0; e < 8; ++e) {
                     const int row = 16 * t + (lane & 15);
@@ -1027,15 +1244,16 @@ void pack_blob16(int ksb, int bpnet_dim, const float *const *w, const float *con
     pack_pairs16(fr(OFF16_W0B), w[0], 256, 284, 2, s[0], col_l0b16);
     pack_pairs16(fr(OFF16_W1), w[1], 256, 256, 8, s[1], col_chain16);
     pack_pairs16(fr(OFF16_W2), w[2], 256, 263, 9, s[2], col_l2_16);
-    pack_pairs16(fr(OFF16_W3), w[3], 256, 256, 8, s[3], col_chain16);
+    pack_pairs16(fr(OFF16_W3), w[3], 256, 256, 8, s[3], col_chain16, 16, L3_16.np);
     pack_pairs16(fr(OFF16_W0A), w[0], 256, 284, 7, s[0], col_proj16);
     float *Y = (float *)(blob + OFF16_F32);
     for (int u = 0; u < HID; ++u) {
         Y[Y_B0 + u] = b[0][u] * ldexpf(1.f, s[0]);
         Y[Y_B1 + u] = b[1][u] * ldexpf(1.f, s[1]);
         Y[Y_B2 + u] = b[2][u] * ldexpf(1.f, s[2]);
-        Y[Y_B3 + u] = b[3][u];
-        Y[Y_WA + u] = w[4][u];
+        // block3.2's accumulator init and the alpha weights on 2^s3-scaled activations (SGN_X3_B3FOLD)
+        Y[Y_B3 + u] = b[3][u] * (SGN_X3_B3FOLD ? ldexpf(1.f, s[3]) : 1.f);
+        Y[Y_WA + u] = w[4][u] * (SGN_X3_B3FOLD ? ldexpf(1.f, -s[3]) : 1.f);
     }
     Y[Y_BA] = b[4][0];
     const int li[7] = {0, 1, 2, 3, 5, 6, 7};
@@ -1133,11 +1351,8 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
             constexpr int S = decltype(kc)::value;
             float v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float y = ac[2 * S + (j >> 2)][j & 3] * inv;
-                v[j] = fmaxf(y, 0.01f * y);
-            }
-            return split8(v);
+            for (int j = 0; j < 8; ++j) v[j] = ac[2 * S + (j >> 2)][j & 3];
+            return lrelu_split8(v, inv);
         };
         f32x4 c0[8], c1[8];
         bias(c0, Y_CB0);
@@ -1149,15 +1364,22 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
                 v[0] = u0[0]; v[1] = u0[1]; v[2] = u0[2]; v[3] = u0[3];
                 v[4] = u1[0]; v[5] = u1[1]; v[6] = u1[2]; v[7] = u1[3];
             } else {
-                // PE(viewdir) ori=True channel c = 8 g + j (point_aggregators.py:579-585, networks.py:175-192):
-                // c < 12: sin(v_d 2^f), 12 <= c < 24: cos(v_d 2^f), d = (c % 12) / 4, f = c % 4
+                // PE(viewdir) ori=True (point_aggregators.py:579-585, networks.py:175-192): lane group g < 3
+                // holds sin, cos of v_g 2^f, f = 0..3 (slots 2 f, 2 f + 1; col_c016 maps them to the
+                // reference's sin block [0, 12) and cos block [12, 24)), group 3 is padding: 4 sincos per
+                // lane with compile-time frequencies and both results used
+                const float x = g == 0 ? vd[0] : g == 1 ? vd[1] : vd[2];
+                float y[4];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int c = 8 * g + j, cc = c % 12, d = cc >> 2, f = cc & 3;
-                    const float x = d == 0 ? vd[0] : d == 1 ? vd[1] : vd[2];
-                    float sv, cv;
-                    sincos_acc(__builtin_ldexpf(x, f), sv, cv);
-                    v[j] = c < 12 ? sv : c < 24 ? cv : 0.f;
+                for (int f = 0; f < 4; ++f) y[f] = x * (float)(1 << f);
+                const float m = fmaxf(fmaxf(__builtin_fabsf(y[0]), __builtin_fabsf(y[1])),
+                                      fmaxf(__builtin_fabsf(y[2]), __builtin_fabsf(y[3])));
+                if (__builtin_expect(__ballot(!(m < 1048576.f)) != 0, 0)) {
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) sincosf(y[f], &v[2 * f], &v[2 * f + 1]);
+                } else {
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) sincos_acc_fast(y[f], v[2 * f], v[2 * f + 1]);
                 }
             }
             return split8(v);
@@ -1183,7 +1405,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float y = c0[t][i] * inv6;
-                const float hv = fmaxf(y, 0.01f * y);
+                const float hv = lrelu_x3(y);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) o[c] = __builtin_fmaf(wc[c][i], hv, o[c]);
             }
@@ -1374,7 +1596,10 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
             hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)(pb < 1024 ? pb : 1024)),
                                dim3(x3::PAIR_TPB), 0, st, q->counters, q->work, q->samp_nnb, (int32_t)i0, (int32_t)n,
                                pair, rows, slots, slot_n);
-            auto kern = ksb == 0 ? x3::k_rows16<0> : ksb == KS_HID ? x3::k_rows16<8> : x3::k_rows16<11>;
+            auto kern = pt->pers ? (ksb == 0 ? x3::k_rows16<0, true> : ksb == KS_HID ? x3::k_rows16<8, true>
+                                                                                : x3::k_rows16<11, true>)
+                                 : (ksb == 0 ? x3::k_rows16<0, false> : ksb == KS_HID ? x3::k_rows16<8, false>
+                                                                                  : x3::k_rows16<11, false>);
             const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < 256 ? wg16 : 256)), dim3(x3::TPB16), 0, st, a);
         }

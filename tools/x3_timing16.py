@@ -12,10 +12,14 @@ labels = ["tile start -> gather + PE", "-> L0 chunk entered", "L0 (32 pairs) + P
 pairs = [0, 0, 32, 32, 32, 32, 32, 32, 32, 32, 32, 16, 32, 32, 32, 32, 0, 0, 0]
 M = len(labels)
 rows = []
+clocks = []
 for b in range(TB):
     for w in range(NW):
-        s = d[b, w]
+        s = d[b, w][:EV - 4]
         s = s[:int(np.count_nonzero(s))]
+        t0, r0, t1, r1 = d[b, w][EV - 4:]
+        if r1 > r0:
+            clocks.append((t1 - t0) / (r1 - r0) * 100.0)  # MHz (s_memrealtime ticks at 100 MHz)
         nt = (len(s) - 1) // M
         if nt < 3:
             continue
@@ -26,3 +30,5 @@ ideal = sum(pairs) * 48 * 2  # 3 MFMAs x 16 cycles per pair, two waves share a S
 print(f"tiles {a.shape[0]}; median cycles per tile {med.sum():.0f} (MFMA-only ideal per SIMD {ideal}, {ideal / med.sum():.1%})")
 for i in range(M):
     print(f"  {i:2d} {labels[i]:34s} {med[i]:8.0f}   SIMD-ideal {pairs[i] * 96:5d}")
+if clocks:
+    print(f"in-kernel clock (s_memtime / s_memrealtime, median over {len(clocks)} waves): {np.median(clocks):.0f} MHz")
