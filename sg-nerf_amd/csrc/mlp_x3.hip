@@ -817,7 +817,7 @@ __device__ __forceinline__ X3B pe_dists16_k(const PeRow &r) {
 
 // block3.2 epilogue of a tile (K-blend -> f_s, alpha), per lane: rows 4 g + i of half g >> 1
 #ifndef SGN_X3_B3FOLD
-#define SGN_X3_B3FOLD 1  // block3.2's bias in its accumulator init, 2^-s3 folded into the blend / alpha weights
+#define SGN_X3_B3FOLD 0  // block3.2's bias in its accumulator init, 2^-s3 folded into the blend / alpha weights
 #endif
 #ifndef SGN_X3_STORE1
 #define SGN_X3_STORE1 0  // 1: each f_s value stored as it is blended (else per 4 under one branch)
