@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 5
+#define SGN_ABI_VERSION 6
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -222,10 +222,13 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
  *                             decoded features (an activation outside fp16 range); 0 otherwise
  *   sgn_aggregate_flag_offset_f32 : byte offset of that int32 flag inside the workspace (for a
  *                             caller that reads it asynchronously, e.g. one frame later)
+ *   sgn_mlp_pack_f32_host   : sgn_mlp_pack_f32 into host memory (no device call; checkers)
  * 16-byte aligned device buffers. */
 size_t sgn_mlp_packed_bytes_f32(int32_t bpnet_layers, int32_t bpnet_dim);
 int sgn_mlp_pack_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,
                      void *d_packed, sgn_stream_t stream);
+int sgn_mlp_pack_f32_host(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,
+                          void *h_packed);
 size_t sgn_point_proj_bytes_f32(int64_t n_points);
 int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed_mlp, void *d_proj, sgn_stream_t stream);
 size_t sgn_aggregate_workspace_bytes_f32(int64_t S);
@@ -235,6 +238,23 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
                       void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream);
 int sgn_aggregate_check_f32(const void *d_workspace, size_t workspace_bytes, sgn_stream_t stream);
 size_t sgn_aggregate_flag_offset_f32(size_t workspace_bytes);
+
+/* fp32-faithful training forward (SURVEY §8 f1 at the reference's arithmetic): stage 1 of
+ * sgn_aggregate_f32 for the base viewmlp that also writes the pre-activations of block1.0, block1.2
+ * and block3.0 (2^-s (W x + b), before LeakyReLU) as fp32 [S_capacity * 8][256] at row s * 8 + k
+ * (the row's pidx index; rows without a neighbour are left unwritten).  The backward through them
+ * runs in fp32 (train_hip, f32 mode).
+ *   sgn_mlp_layout_f32(0 / 1)   : bytes of the blob's fragment section / fp32 entries after it
+ *   sgn_mlp_pack_index_f32      : the blob as index maps, for packing it on the device from a flat
+ *                                 parameter: which 0 -> per fp16 element (layer << 20 | element)
+ *                                 (| 1 << 30 for the lo part, -1 padding); which 1 -> per fp32 entry
+ *                                 kind << 26 | layer << 20 | element (kinds: see mlp_x3.hip Y32Kind) */
+int sgn_aggregate_train_fwd_f32(const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q,
+                                int64_t S_capacity, int32_t K, const void *d_packed_mlp, float *d_out_feat,
+                                float *d_z1, float *d_z2, float *d_z3, void *d_workspace, size_t workspace_bytes,
+                                sgn_stream_t stream);
+int64_t sgn_mlp_layout_f32(int32_t which);
+int sgn_mlp_pack_index_f32(int32_t bpnet_layers, int32_t bpnet_dim, int32_t which, int32_t *out, int64_t n);
 
 /* ---- training: forward with saved activations + backward ---
  * Gradients of PointAggregator.forward / viewmlp (point_aggregators.py:868-959, :561-786)

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -110,6 +110,7 @@ SIGNATURES = {
     "sgn_colsum_f16": (c_i32, [c_i32, ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp, c_vp]),
     "sgn_mlp_packed_bytes_f32": (c_sz, [c_i32, c_i32]),
     "sgn_mlp_pack_f32": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
+    "sgn_mlp_pack_f32_host": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp]),
     "sgn_point_proj_bytes_f32": (c_sz, [c_i64]),
     "sgn_point_project_f32": (c_i32, [ctypes.POINTER(PointTables), c_vp, c_vp, c_vp]),
     "sgn_aggregate_workspace_bytes_f32": (c_sz, [c_i64]),
@@ -117,6 +118,10 @@ SIGNATURES = {
                                   c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
     "sgn_aggregate_check_f32": (c_i32, [c_vp, c_sz, c_vp]),
     "sgn_aggregate_flag_offset_f32": (c_sz, [c_sz]),
+    "sgn_aggregate_train_fwd_f32": (c_i32, [c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,
+                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "sgn_mlp_layout_f32": (c_i64, [c_i32]),
+    "sgn_mlp_pack_index_f32": (c_i32, [c_i32, c_i32, c_i32, ctypes.POINTER(c_i32), c_i64]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
                               c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_ray_march_dense": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.POINTER(c_f32), c_vp, c_vp, c_vp,

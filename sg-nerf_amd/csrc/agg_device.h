@@ -113,6 +113,10 @@ struct AggArgs {
     const int32_t *rows;
     const int4 *slots;
     const int32_t *slot_n;
+    // fp32-faithful training forward (k_rows16 save mode): the pre-activations 2^-s acc of block1.0,
+    // block1.2 and block3.0 (the inputs of the next layer before LeakyReLU), fp32 natural unit order,
+    // row s * 8 + k (the row's pidx index); rows without a neighbour are not written
+    float *z1, *z2, *z3;
 };
 
 // training save: one 16-byte fragment of a 32-row tile -> [rows][C] (C multiple of 16)

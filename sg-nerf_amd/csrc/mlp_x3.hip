@@ -30,6 +30,7 @@
 // LDS-DMA, shared by the workgroup's 8 waves.
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cmath>
 #include <utility>
 #include <vector>
@@ -851,7 +852,9 @@ __device__ __forceinline__ XcdTiles xcd_tiles(int ntiles) {
 }
 
 // KB: k-steps of block2_bpnet.0 in 16x16 steps (0: base viewmlp; 8: bpnet_dim 0; 11: dim 96)
-template <int KB, bool PERS>
+// SAVE (base viewmlp, training): the pre-activations of block1.0 / 1.2 / 3.0 go to a.z1 / z2 / z3 as
+// the next layer converts them (chain_k)
+template <int KB, bool PERS, bool SAVE = false>
 __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     using Net = std::conditional_t<(KB > 0), NetR16SG<KB>, NetR16>;
     constexpr int LB = 2, L2 = KB ? 3 : 2, L3 = KB ? 4 : 3;
@@ -1014,6 +1017,8 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         const int nA0 = __popc((uint32_t)mrowA & 0xFFu), nA1 = __popc(((uint32_t)mrowA >> 8) & 0xFFu);
         const bool waveB = (mrowB & 0xFFFFull) != 0;  // wave-uniform: a B sample in either half
         const Row16 rw = row_math16<PERS>(cam, rc, m, ix.a, sc ? nA1 : nA0, waveB);
+        // SAVE: the row's pidx index s * 8 + k (from the slot's row table), -1 for rows without a neighbour
+        const int vrow = SAVE && ix.sval && m ? a.rows[(int64_t)hslot * 8 + kk] : -1;
         if ((a.blend || a.wnorm) && ix.sval) {  // optional outputs: the row's pidx index from the table
             const int v = a.rows[(int64_t)hslot * 8 + kk];
             if (a.blend && g == 0) a.blend[v] = rw.wgt;
@@ -1035,11 +1040,18 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         // Each layer's epilogue (LeakyReLU + hi/lo split of its accumulators) runs lazily inside the
         // next layer's k-loop: k-step k converts tiles 2k, 2k+1 only, so the VALU work overlaps the
         // MFMAs in flight instead of idling the matrix pipe between layers.
-        auto chain_k = [&](const f32x4 (&ac)[16], float inv, auto kc) {
+        auto chain_k = [&](const f32x4 (&ac)[16], float inv, auto kc, float *zsave = nullptr) {
             constexpr int S = decltype(kc)::value;
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = ac[2 * S + (j >> 2)][j & 3];
+            if constexpr (SAVE) {  // units 16 t + 4 g .. + 3 of tiles t = 2 S, 2 S + 1
+                if (zsave && vrow >= 0) {
+                    float *zr = zsave + (int64_t)vrow * HID + 4 * g;
+                    *(f32x4 *)(zr + 32 * S) = f32x4{v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv};
+                    *(f32x4 *)(zr + 32 * S + 16) = f32x4{v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv};
+                }
+            }
             return lrelu_split8(v, inv);
         };
         auto bias_init = [&](f32x4 (&ac)[16], int yb) {
@@ -1061,7 +1073,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         const float inv0 = Yl[Y_INV + 0], inv1 = Yl[Y_INV + 1], inv2 = Yl[Y_INV + 2], inv7 = Yl[Y_INV + 7];
         bias_init(accB, Y_B1);
         int v_next = -1;
-        run_layer16<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) { return chain_k(accA, inv0, k); },
+        run_layer16<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) { return chain_k(accA, inv0, k, a.z1); },
                             [&](auto c) {
                                 if constexpr (decltype(c)::value == 0)
                                     v_next = nslot < nslots ? a.rows[(int64_t)nslot * 8 + kk] : -1;
@@ -1092,7 +1104,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         bias_init(acc2, Y_B2);
         run_layer16<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {
             constexpr int K = decltype(k)::value;
-            if constexpr (K < 8) return chain_k(in2, inv_in2, k); else return ext;
+            if constexpr (K < 8) return chain_k(in2, inv_in2, k, a.z2); else return ext;
         }, [&](auto c) {
             constexpr int C = decltype(c)::value;
             if constexpr (C == 0) {  // v_next landed at the previous boundaries
@@ -1137,7 +1149,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
             auto &acc1 = reinterpret_cast<f32x4(&)[8]>(acc[8]);
             run_layer16<Net, L3, true, VmL3P0, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) {
                 constexpr int K = decltype(k)::value;
-                in3[K] = chain_k(acc2, inv2, k);
+                in3[K] = chain_k(acc2, inv2, k, a.z3);
                 return in3[K];
             }, NoHook{}, ts, first_chunk_loads);
             epi_begin(e, ldsi, rw.wgt, nA, nB, ce, eslot < nslots);
@@ -1150,7 +1162,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
                                                   });
         } else {
             run_layer16<Net, L3, true, VmL3P0>(wb, ldsi, slot, w, lane, lz, acc,
-                                               [&](auto k) { return chain_k(acc2, inv2, k); }, NoHook{}, ts,
+                                               [&](auto k) { return chain_k(acc2, inv2, k, a.z3); }, NoHook{}, ts,
                                                first_chunk_loads);
             epi_begin(e, ldsi, rw.wgt, nA, nB, ce, eslot < nslots);
         }
@@ -1238,44 +1250,94 @@ void pack_pairs16(_Float16 *dst, const float *W, int n_out, int n_in, int KS, in
         }
 }
 
+// The blob's layout, once: pairs(off, layer, n_out, n_in, KS, col, NT, NP) places layer's weights as
+// (hi, lo) fragment pairs of 2^s w, f32(Y index, kind, layer, element) an fp32-section entry.  Layers are
+// the w[] / b[] order of sgn_mlp_pack_f32 (weights.LAYERS, then block2_bpnet.0 as 9).
+enum Y32Kind { YK_ZERO = 0, YK_W = 1, YK_B = 2, YK_BS = 3, YK_INV = 4, YK_ONE = 5, YK_WINV = 6, YK_BS_OR_B = 7 };
+template <class Pairs, class F32>
+void layout_blob16(int ksb, int bpnet_dim, Pairs &&pairs, F32 &&f32) {
+    pairs(OFF16_W0B, 0, 256, 284, 2, col_l0b16, 16, 1);
+    pairs(OFF16_W1, 1, 256, 256, 8, col_chain16, 16, 1);
+    pairs(OFF16_W2, 2, 256, 263, 9, col_l2_16, 16, 1);
+    pairs(OFF16_W3, 3, 256, 256, 8, col_chain16, 16, L3_16.np);
+    pairs(OFF16_W0A, 0, 256, 284, 7, col_proj16, 16, 1);
+    for (int u = 0; u < HID; ++u) {
+        f32(Y_B0 + u, YK_BS, 0, u);
+        f32(Y_B1 + u, YK_BS, 1, u);
+        f32(Y_B2 + u, YK_BS, 2, u);
+        // block3.2's accumulator init and the alpha weights on 2^s3-scaled activations (SGN_X3_B3FOLD)
+        f32(Y_B3 + u, SGN_X3_B3FOLD ? YK_BS : YK_B, 3, u);
+        f32(Y_WA + u, SGN_X3_B3FOLD ? YK_WINV : YK_W, 4, u);  // YK_WINV: w 2^-s of layer 3
+    }
+    f32(Y_BA, YK_B, 4, 0);
+    const int li[7] = {0, 1, 2, 3, 5, 6, 7};
+    for (int i = 0; i < 7; ++i) f32(Y_INV + i, YK_INV, li[i], 0);
+    f32(Y_INV + 7, ksb > 0 ? YK_INV : YK_ONE, 9, 0);
+    if (ksb > 0) {
+        pairs(OFF16_WB, 9, 256, 256 + bpnet_dim, 8 + bpnet_dim / 32, col_bp16, 16, 1);
+        for (int u = 0; u < HID; ++u) f32(Y_BB + u, YK_BS, 9, u);
+    }
+    // colour MLP (k_color16): 8 output tiles per layer; k-step 8 of colour 0 holds PE(v)
+    pairs(OFF16_C0, 5, 128, 280, 9, col_c016, 8, 1);
+    pairs(OFF16_C1, 6, 128, 128, 4, col_chain16, 8, 1);
+    pairs(OFF16_C2, 7, 128, 128, 4, col_chain16, 8, 1);
+    for (int u = 0; u < 128; ++u) {
+        f32(Y_CB0 + u, YK_BS, 5, u);
+        f32(Y_CB1 + u, YK_BS, 6, u);
+        f32(Y_CB2 + u, YK_BS, 7, u);
+        for (int c = 0; c < 3; ++c) f32(Y_CW3 + 128 * c + u, YK_W, 8, c * 128 + u);
+    }
+    for (int c = 0; c < 3; ++c) f32(Y_CB3 + c, YK_B, 8, c);
+}
+
 void pack_blob16(int ksb, int bpnet_dim, const float *const *w, const float *const *b, const int *s, int sb,
                  uint8_t *blob) {
-    auto fr = [&](uint32_t off) { return (_Float16 *)(blob + off); };
-    pack_pairs16(fr(OFF16_W0B), w[0], 256, 284, 2, s[0], col_l0b16);
-    pack_pairs16(fr(OFF16_W1), w[1], 256, 256, 8, s[1], col_chain16);
-    pack_pairs16(fr(OFF16_W2), w[2], 256, 263, 9, s[2], col_l2_16);
-    pack_pairs16(fr(OFF16_W3), w[3], 256, 256, 8, s[3], col_chain16, 16, L3_16.np);
-    pack_pairs16(fr(OFF16_W0A), w[0], 256, 284, 7, s[0], col_proj16);
+    auto shift = [&](int L) { return L == 9 ? sb : s[L]; };
     float *Y = (float *)(blob + OFF16_F32);
-    for (int u = 0; u < HID; ++u) {
-        Y[Y_B0 + u] = b[0][u] * ldexpf(1.f, s[0]);
-        Y[Y_B1 + u] = b[1][u] * ldexpf(1.f, s[1]);
-        Y[Y_B2 + u] = b[2][u] * ldexpf(1.f, s[2]);
-        // block3.2's accumulator init and the alpha weights on 2^s3-scaled activations (SGN_X3_B3FOLD)
-        Y[Y_B3 + u] = b[3][u] * (SGN_X3_B3FOLD ? ldexpf(1.f, s[3]) : 1.f);
-        Y[Y_WA + u] = w[4][u] * (SGN_X3_B3FOLD ? ldexpf(1.f, -s[3]) : 1.f);
-    }
-    Y[Y_BA] = b[4][0];
-    const int li[7] = {0, 1, 2, 3, 5, 6, 7};
-    for (int i = 0; i < 7; ++i) Y[Y_INV + i] = ldexpf(1.f, -s[li[i]]);
-    Y[Y_INV + 7] = 1.f;
-    if (ksb > 0) {
-        const int nin = 256 + bpnet_dim;
-        pack_pairs16(fr(OFF16_WB), w[9], 256, nin, 8 + bpnet_dim / 32, sb, col_bp16);
-        for (int u = 0; u < HID; ++u) Y[Y_BB + u] = b[9][u] * ldexpf(1.f, sb);
-        Y[Y_INV + 7] = ldexpf(1.f, -sb);
-    }
-    // colour MLP (k_color16): 8 output tiles per layer; k-step 8 of colour 0 holds PE(v) channel p
-    pack_pairs16(fr(OFF16_C0), w[5], 128, 280, 9, s[5], col_c016, 8);
-    pack_pairs16(fr(OFF16_C1), w[6], 128, 128, 4, s[6], col_chain16, 8);
-    pack_pairs16(fr(OFF16_C2), w[7], 128, 128, 4, s[7], col_chain16, 8);
-    for (int u = 0; u < 128; ++u) {
-        Y[Y_CB0 + u] = b[5][u] * ldexpf(1.f, s[5]);
-        Y[Y_CB1 + u] = b[6][u] * ldexpf(1.f, s[6]);
-        Y[Y_CB2 + u] = b[7][u] * ldexpf(1.f, s[7]);
-        for (int c = 0; c < 3; ++c) Y[Y_CW3 + 128 * c + u] = w[8][c * 128 + u];
-    }
-    for (int c = 0; c < 3; ++c) Y[Y_CB3 + c] = b[8][c];
+    layout_blob16(ksb, bpnet_dim,
+                  [&](uint32_t off, int L, int n_out, int n_in, int KS, auto col, int NT, int NP) {
+                      pack_pairs16((_Float16 *)(blob + off), w[L], n_out, n_in, KS, shift(L), col, NT, NP);
+                  },
+                  [&](int yi, int kind, int L, int e) {
+                      float v = 0.f;
+                      switch (kind) {
+                          case YK_W: v = w[L][e]; break;
+                          case YK_B: v = b[L][e]; break;
+                          case YK_BS: v = b[L][e] * ldexpf(1.f, shift(L)); break;
+                          case YK_INV: v = ldexpf(1.f, -shift(L)); break;
+                          case YK_ONE: v = 1.f; break;
+                          case YK_WINV: v = w[L][e] * ldexpf(1.f, -shift(3)); break;
+                          default: break;
+                      }
+                      Y[yi] = v;
+                  });
+}
+
+// Index maps of the same layout, for packing on the device from a flat parameter (train_hip):
+// fp16 element i of the fragment section -> (layer << 20 | element) | (1 << 30 for the lo part),
+// -1 for padding; fp32 entry j -> kind << 26 | layer << 20 | element (kind 0: zero)
+void index_blob16(int ksb, int bpnet_dim, int32_t *i16, size_t n16, int32_t *i32, size_t n32) {
+    for (size_t i = 0; i < n16; ++i) i16[i] = -1;
+    for (size_t i = 0; i < n32; ++i) i32[i] = 0;
+    layout_blob16(ksb, bpnet_dim,
+                  [&](uint32_t off, int L, int n_out, int n_in, int KS, auto col, int NT, int NP) {
+                      const int TPP = NT / NP;
+                      int32_t *dst = i16 + off / 2;
+                      for (int t = 0; t < NT; ++t)
+                          for (int ks = 0; ks < KS; ++ks) {
+                              const size_t f = ((size_t)(t / TPP) * KS + ks) * TPP + t % TPP;
+                              for (int lane = 0; lane < 64; ++lane)
+                                  for (int e = 0; e < 8; ++e) {
+                                      const int row = 16 * t + (lane & 15);
+                                      const int c = col(ks, 8 * (lane >> 4) + e);
+                                      const bool ok = row < n_out && c >= 0 && c < n_in;
+                                      const int32_t code = ok ? (L << 20) | (row * n_in + c) : -1;
+                                      dst[((2 * f) * 64 + lane) * 8 + e] = code;
+                                      dst[((2 * f + 1) * 64 + lane) * 8 + e] = ok ? code | (1 << 30) : -1;
+                                  }
+                          }
+                  },
+                  [&](int yi, int kind, int L, int e) { i32[yi] = (kind << 26) | (L << 20) | e; });
 }
 // ---- colour MLP ------------------------------------------------------------------------
 struct ColorArgs {
@@ -1481,6 +1543,18 @@ int sgn_mlp_pack_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *const
     return 0;
 }
 
+int sgn_mlp_pack_f32_host(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,
+                          void *h_packed) {
+    using namespace sgn;
+    SGN_REQUIRE(w && b && h_packed, "null argument");
+    const int ksb = x3::variant_ksb(bpnet_layers, bpnet_dim);
+    SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    for (int L = 0; L < (ksb ? 10 : 9); ++L) SGN_REQUIRE(w[L] && b[L], "null layer pointer");
+    std::fill_n((uint8_t *)h_packed, x3::blob_bytes_sg(ksb), (uint8_t)0);
+    x3::pack_blob_x3(ksb, bpnet_dim, w, b, (uint8_t *)h_packed);
+    return 0;
+}
+
 size_t sgn_point_proj_bytes_f32(int64_t n_points) {
     // P rows, then the packed 64-B point records
     return (size_t)(n_points > 0 ? n_points : 0) * (sgn::x3::PROJ_BYTES_PER_POINT + sgn::x3::REC16_FLOATS * 4);
@@ -1520,10 +1594,14 @@ int32_t *ws_tail(void *d_workspace, size_t workspace_bytes) {
 }
 }  // namespace
 
-int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet, const void *d_point_proj,
-                      const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
-                      const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
-                      void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
+}  // extern "C"
+
+namespace {
+int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet, const void *d_point_proj,
+                  const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                  const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
+                  void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream,
+                  float *const *z = nullptr) {
     using namespace sgn;
     using namespace sgn::mlp;
     SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace && d_point_proj, "null argument");
@@ -1564,6 +1642,9 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     int4 *slots = (int4 *)(rows + ws_items * 8);
     int32_t *slot_n = tail;
     a.rows = rows; a.slots = slots; a.slot_n = slot_n;
+    if (z) {
+        a.z1 = z[0]; a.z2 = z[1]; a.z3 = z[2];
+    }
     // SGN_PAIR=0 runs every sample alone in its k_rows16 half (same results, bit for bit; tests)
     const char *pe = getenv("SGN_PAIR");
     const int32_t pair = !(pe && pe[0] == '0');
@@ -1596,10 +1677,11 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
             hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)(pb < 1024 ? pb : 1024)),
                                dim3(x3::PAIR_TPB), 0, st, q->counters, q->work, q->samp_nnb, (int32_t)i0, (int32_t)n,
                                pair, rows, slots, slot_n);
-            auto kern = pt->pers ? (ksb == 0 ? x3::k_rows16<0, true> : ksb == KS_HID ? x3::k_rows16<8, true>
-                                                                                : x3::k_rows16<11, true>)
-                                 : (ksb == 0 ? x3::k_rows16<0, false> : ksb == KS_HID ? x3::k_rows16<8, false>
-                                                                                  : x3::k_rows16<11, false>);
+            auto kern = z ? x3::k_rows16<0, false, true>
+                          : pt->pers ? (ksb == 0 ? x3::k_rows16<0, true> : ksb == KS_HID ? x3::k_rows16<8, true>
+                                                                                      : x3::k_rows16<11, true>)
+                                     : (ksb == 0 ? x3::k_rows16<0, false> : ksb == KS_HID ? x3::k_rows16<8, false>
+                                                                                        : x3::k_rows16<11, false>);
             const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < 256 ? wg16 : 256)), dim3(x3::TPB16), 0, st, a);
         }
@@ -1619,6 +1701,50 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
     }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet, const void *d_point_proj,
+                      const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
+                      const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
+                      void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream) {
+    return aggregate_f32(bpnet_layers, bpnet_dim, d_bpnet, d_point_proj, pt, q, S_capacity, K, d_packed, d_out_feat,
+                         d_out_blend, d_out_wnorm, d_workspace, workspace_bytes, stages, stream);
+}
+
+int sgn_aggregate_train_fwd_f32(const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q,
+                                int64_t S_capacity, int32_t K, const void *d_packed, float *d_out_feat,
+                                float *d_z1, float *d_z2, float *d_z3, void *d_workspace, size_t workspace_bytes,
+                                sgn_stream_t stream) {
+    SGN_REQUIRE(d_z1 && d_z2 && d_z3 && ((uintptr_t)d_z1 & 15) == 0 && ((uintptr_t)d_z2 & 15) == 0 &&
+                    ((uintptr_t)d_z3 & 15) == 0,
+                "16-byte aligned pre-activation buffers z1, z2, z3 required");
+    SGN_REQUIRE(pt && pt->pers == nullptr, "the training forward computes the pers coordinates itself");
+    float *const z[3] = {d_z1, d_z2, d_z3};
+    return aggregate_f32(0, 0, nullptr, d_point_proj, pt, q, S_capacity, K, d_packed, d_out_feat, nullptr, nullptr,
+                         d_workspace, workspace_bytes, 1, stream, z);
+}
+
+int sgn_mlp_pack_index_f32(int32_t bpnet_layers, int32_t bpnet_dim, int32_t which, int32_t *out, int64_t n) {
+    using namespace sgn;
+    const int ksb = x3::variant_ksb(bpnet_layers, bpnet_dim);
+    SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
+    SGN_REQUIRE(out && (which == 0 || which == 1), "which: 0 fragment section, 1 fp32 section");
+    const size_t n16 = x3::OFF16_F32 / 2, n32 = x3::N_Y32;
+    SGN_REQUIRE((size_t)n == (which == 0 ? n16 : n32), "index map length (sgn_mlp_layout_f32)");
+    std::vector<int32_t> a(n16), b(n32);
+    x3::index_blob16(ksb, bpnet_dim, a.data(), n16, b.data(), n32);
+    const std::vector<int32_t> &src = which == 0 ? a : b;
+    for (size_t i = 0; i < src.size(); ++i) out[i] = src[i];
+    return 0;
+}
+
+int64_t sgn_mlp_layout_f32(int32_t which) {
+    // 0: bytes of the fragment section (= byte offset of the fp32 section), 1: fp32 entries after it
+    return which == 0 ? (int64_t)sgn::x3::OFF16_F32 : which == 1 ? (int64_t)sgn::x3::N_Y32 : -1;
 }
 
 int sgn_aggregate_check_f32(const void *d_workspace, size_t workspace_bytes, sgn_stream_t stream) {

@@ -62,6 +62,12 @@ class ViewMLP(nn.Module):
     def f(self, name, x):
         return self.lin[name.replace(".", "_")](x)
 
+    def w(self, name):
+        return self.lin[name.replace(".", "_")].weight
+
+    def b(self, name):
+        return self.lin[name.replace(".", "_")].bias
+
     def state(self):
         out = {}
         for name, *_ in LAYERS:
@@ -90,10 +96,31 @@ def _w2pers(p, rot, campos):
     return torch.stack([c[..., 0] / c[..., 2], c[..., 1] / c[..., 2], c[..., 2]], dim=-1)
 
 
-def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, samp_locw, pidx):
+class _SavedLinear(torch.autograd.Function):
+    """z = x W^T + b whose forward value was computed elsewhere (the HIP fp32-faithful row kernel,
+    k_rows16's save mode) and is passed in; the backward is the plain fp32 one: dx = dz W,
+    dW = dz^T x, db = sum dz."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, z):
+        ctx.save_for_backward(x, w)
+        return z.clone()
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, w = ctx.saved_tensors
+        return gz @ w, gz.t() @ x, gz.sum(0), None
+
+
+def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, samp_locw, pidx, saved=None):
     """Differentiable PointAggregator.forward on sample-major neighbours.
     Returns feat [S,4] (alpha, r, g, b; zeros for samples without neighbours), conf_coefficient
-    [S,K] (straight-through clamp) and the neighbour mask [S,K]."""
+    [S,K] (straight-through clamp) and the neighbour mask [S,K].
+
+    saved = (z1, z2, z3): the pre-activations of block1.0, block1.2 and block3.0 per row s * K + k
+    ([>= S K, 256] fp32, from sgn_aggregate_train_fwd_f32): those three layers then take their
+    forward values from there (_SavedLinear) instead of recomputing them, with the same fp32
+    backward."""
     S, K = pidx.shape
     mask = pidx >= 0
     flat = torch.clamp(pidx, min=0).reshape(-1).long()
@@ -118,11 +145,17 @@ def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, 
     emb = torch.index_select(points.points_embeding, 0, fm)
     x = torch.cat([emb, _pe(emb, 3), _pe(dists.reshape(-1, 6)[m], 5)], dim=-1)
     lr_ = lambda t: F.leaky_relu(t, 0.01)  # noqa: E731
-    h = lr_(mlp.f("block1.2", lr_(mlp.f("block1.0", x))))
+    if saved is not None:
+        rows = torch.nonzero(m).reshape(-1)   # the valid rows s * K + k, in the order of m
+        zs = [z.index_select(0, rows) for z in saved]
+        lin = lambda name, t, zi: _SavedLinear.apply(t, mlp.w(name), mlp.b(name), zs[zi])  # noqa: E731
+    else:
+        lin = lambda name, t, zi: mlp.f(name, t)  # noqa: E731
+    h = lr_(lin("block1.2", lr_(lin("block1.0", x, 0)), 1))
     sd = torch.index_select(points.points_dir, 0, fm)
     ov = ori_v[:, None, :].expand(S, K, 3).reshape(-1, 3)[m]
     h = torch.cat([h, torch.index_select(points.points_color, 0, fm), sd - ov, torch.sum(sd * ov, dim=-1, keepdim=True)], dim=-1)
-    h = lr_(mlp.f("block3.2", lr_(mlp.f("block3.0", h))))
+    h = lr_(mlp.f("block3.2", lr_(lin("block3.0", h, 2))))
     alpha = F.softplus(mlp.f("alpha_branch.0", h) - 1)
     hk = torch.zeros(S * K, h.shape[-1], device=h.device, dtype=h.dtype).masked_scatter(m[:, None], h)
     ak = torch.zeros(S * K, 1, device=h.device, dtype=h.dtype).masked_scatter(m[:, None], alpha)

@@ -65,12 +65,88 @@ class FlatMLP(nn.Module):
         off, o, i = self.slices[name]
         return (self.flat if t is None else t)[off + o * i:off + o * i + o]
 
+    def f(self, name, x):
+        return F.linear(x, self.w(name), self.b(name))
+
     def state(self):
         out = {}
         for name, *_ in self.layers:
             out[name + ".weight"] = self.w(name).detach().clone()
             out[name + ".bias"] = self.b(name).detach().clone()
         return out
+
+
+class _PackerF32:
+    """Device-side packing of the fp32-faithful blob (mlp_x3.hip: (hi, lo) fp16 fragment pairs of
+    2^s-scaled weights + the fp32 section) from the flat parameter, through the layout's index maps
+    (sgn_mlp_pack_index_f32): per layer the shift s = 14 - e with max |W| = f 2^e (frexp), as
+    layer_shift does on the host, then hi = fp16(2^s w), lo = fp16(2^s w - hi).  Equals
+    weights.pack_mlp(state, precision="f32") bit for bit (tests/test_train_gpu.py)."""
+
+    YK_ZERO, YK_W, YK_B, YK_BS, YK_INV, YK_ONE, YK_WINV = range(7)
+
+    def __init__(self, device, mlp: "FlatMLP", variant=(0, 0)):
+        L = _lib.lib()
+        self.n16b = int(L.sgn_mlp_layout_f32(0))
+        n32 = int(L.sgn_mlp_layout_f32(1))
+        self.total = int(L.sgn_mlp_packed_bytes_f32(*variant))
+
+        def imap(which, n):
+            a = (ctypes.c_int32 * n)()
+            _lib.check(L.sgn_mlp_pack_index_f32(*variant, which, a, n), "sgn_mlp_pack_index_f32")
+            return torch.frombuffer(bytearray(a), dtype=torch.int32).long()
+        # the maps are decoded and bounds-checked on the host; the device only gathers
+        nl, nflat = len(mlp.layers), mlp.flat.numel()
+        woff = torch.tensor([mlp.slices[n][0] for n, *_ in mlp.layers], dtype=torch.long)
+        wlen = torch.tensor([mlp.slices[n][1] * mlp.slices[n][2] for n, *_ in mlp.layers], dtype=torch.long)
+        blen = torch.tensor([mlp.slices[n][1] for n, *_ in mlp.layers], dtype=torch.long)
+        self.wspan = [(int(a), int(a + b)) for a, b in zip(woff, wlen)]
+        c16 = imap(0, self.n16b // 2)
+        v16 = c16 >= 0
+        c16 = torch.clamp(c16, min=0)
+        l16 = (c16 >> 20) & 0x3FF
+        assert int(l16[v16].max()) < nl, "fragment map names a layer the flat parameter lacks"
+        l16 = torch.where(v16, l16, 0)
+        e16 = torch.where(v16, c16 & 0xFFFFF, 0)
+        assert bool((e16 < wlen[l16]).all()), "fragment map element out of range"
+        c32 = imap(1, n32)
+        k32 = c32 >> 26
+        l32 = (c32 >> 20) & 63
+        e32 = c32 & 0xFFFFF
+        uses_w = (k32 == self.YK_W) | (k32 == self.YK_WINV)
+        uses_b = (k32 == self.YK_B) | (k32 == self.YK_BS)
+        uses_l = uses_w | uses_b | (k32 == self.YK_INV)
+        assert int(l32[uses_l].max()) < nl, "fp32 map names a layer the flat parameter lacks"
+        l32 = torch.where(uses_l, l32, 0)
+        fw32 = torch.where(uses_w, woff[l32] + e32, 0)
+        fb32 = torch.where(uses_b, woff[l32] + wlen[l32] + e32, 0)
+        assert bool((e32[uses_w] < wlen[l32[uses_w]]).all() and (e32[uses_b] < blen[l32[uses_b]]).all())
+        f16 = woff[l16] + e16
+        assert int(f16.max()) < nflat and int(fw32.max()) < nflat and int(fb32.max()) < nflat
+        d = lambda t: t.to(device)  # noqa: E731
+        self.v16, self.lo16, self.l16, self.f16 = d(v16), d((c16 >> 30) & 1 == 1), d(l16), d(f16)
+        self.k32, self.l32, self.fw32, self.fb32 = d(k32), d(l32), d(fw32), d(fb32)
+        self.blob = torch.zeros(self.total, dtype=torch.uint8, device=device)
+
+    def pack(self, flat):
+        flat = flat.detach()
+        m = torch.stack([flat[a:b].abs().amax() for a, b in self.wspan])
+        _, e = torch.frexp(m)
+        sh = torch.where((m > 0) & torch.isfinite(m), 14 - e, torch.zeros_like(e)).float()
+        v = torch.where(self.v16, flat[self.f16] * torch.exp2(sh[self.l16]), 0.0)
+        hi = v.half()
+        lo = (v - hi.float()).half()
+        self.blob[:self.n16b].view(torch.float16).copy_(torch.where(self.lo16, lo, hi))
+        k, inv = self.k32, torch.exp2(-sh)
+        y = torch.zeros(k.shape, dtype=torch.float32, device=flat.device)
+        y = torch.where(k == self.YK_W, flat[self.fw32], y)
+        y = torch.where(k == self.YK_B, flat[self.fb32], y)
+        y = torch.where(k == self.YK_BS, flat[self.fb32] * torch.exp2(sh[self.l32]), y)
+        y = torch.where(k == self.YK_INV, inv[self.l32], y)
+        y = torch.where(k == self.YK_ONE, torch.ones_like(y), y)
+        y = torch.where(k == self.YK_WINV, flat[self.fw32] * inv[3], y)
+        self.blob[self.n16b:self.n16b + 4 * y.numel()].view(torch.float32).copy_(y)
+        return self.blob
 
 
 class _Packer:
@@ -215,13 +291,23 @@ class HipTrainer:
     """One data-parallel training step per call on the HIP path (config 5)."""
 
     def __init__(self, points: PointParams, mlp_state, opts: HotPathOpts, device, lr=5e-4, plr=2e-3,
-                 lr_decay_exp=0.1, lr_decay_iters=1_000_000, bucket_mb=64, querier=None, bpnet=None):
+                 lr_decay_exp=0.1, lr_decay_iters=1_000_000, bucket_mb=64, querier=None, bpnet=None,
+                 precision="f16"):
         """bpnet: the SG variant's BPNet point embedding [N, 96] (fp32, detached: it is an input,
-        neural_points.py:662), needed when opts select block2_bpnet with predict_semantic = 1."""
+        neural_points.py:662), needed when opts select block2_bpnet with predict_semantic = 1.
+        precision "f16": the fp16-operand HIP forward + backward (k_agg_rows save mode, k_agg_bwd);
+        "f32" (base viewmlp): the reference's fp32 arithmetic -- the HIP fp32-faithful row kernel
+        (k_rows16, 3 fp16 MFMA products per fp32 product) saves the row MLP's pre-activations and the
+        backward runs in fp32 through them (train.aggregate(saved=...), fp32 GEMMs)."""
         self.device = torch.device(device)
         self.opts = opts.check_supported()
         self.variant = tuple(opts.bpnet_variant)
         self.sg = self.variant != (0, 0)
+        if precision not in ("f16", "f32"):
+            raise ValueError("precision: 'f16' or 'f32'")
+        if precision == "f32" and self.sg:
+            raise NotImplementedError("f32 training covers the base viewmlp (the SG variant trains at f16)")
+        self.precision = precision
         self.points = points
         self.mlp = FlatMLP(mlp_state, self.device, layers_for(*self.variant))
         self.bpnet16 = None
@@ -248,6 +334,7 @@ class HipTrainer:
         self.bucket_elems = bucket_mb * (1 << 20) // 4
         self.querier = querier
         self.packer = _Packer(self.device, self.variant)
+        self.packer32 = _PackerF32(self.device, self.mlp, self.variant) if precision == "f32" else None
         # stored column p -> reference index; inverses: reference index -> stored column
         self.map_chain = _colmap(0, 256, self.device)
         self.map_x0 = _colmap(1, 288, self.device)
@@ -348,6 +435,8 @@ class HipTrainer:
         """Forward + backward + gradient all-reduce (no parameter update).  labels: (point_labels,
         ray_labels, seconds) for the semantic-guided query (semantic_guidance = 1).
         Returns (loss parts, rendered colour [R,3], ray_mask [R])."""
+        if self.precision == "f32":
+            return self._backward_f32(campos, rot, raydir, near, far, gt, labels)
         o = self.opts
         dev = self.device
         campos = campos.reshape(3).to(dev, torch.float32).contiguous()
@@ -432,6 +521,69 @@ class HipTrainer:
                                                     _lib.ptr(scale), ctypes.byref(deltas), ctypes.byref(grads), st),
                            "sgn_aggregate_backward")
             self._weight_grads(n * 8, scale, q)
+        self.allreduce_grads([self.mlp.flat])
+        if dp:
+            _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
+        parts["total"] = total.detach()
+        return parts, full.detach(), ray_mask
+
+    # -- fp32-faithful step ---------------------------------------------------------------------
+    def _backward_f32(self, campos, rot, raydir, near, far, gt, labels=None):
+        """The reference's fp32 step: HIP query, the fp32-faithful row MLP on the HIP kernels
+        (k_point_proj16 + k_pair_slots + k_rows16 save mode: block1.0 / 1.2 / 3.0 pre-activations per
+        row), then train.aggregate(saved=...) (those three layers take their forward values from the
+        kernel; block3.2, alpha, K-blend, colour in fp32 torch) -> composite_losses -> fp32 autograd."""
+        from .train import aggregate
+        o = self.opts
+        dev = self.device
+        campos = campos.reshape(3).to(dev, torch.float32).contiguous()
+        rot = rot.reshape(3, 3).to(dev, torch.float32).contiguous()
+        raydir = raydir.reshape(-1, 3).to(dev, torch.float32).contiguous()
+        R = raydir.shape[0]
+        q = self._query(campos, raydir, near, far, labels)
+        blob = self.packer32.pack(self.mlp.flat)
+        for p in self.point_params + [self.mlp.flat]:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            elif not (self._pts_grad_clean and p is not self.mlp.flat):
+                p.grad.zero_()
+        self._pts_grad_clean = False
+        L = _lib.lib()
+        st = _lib.stream_handle()
+        pt = self._tables(campos, rot, raydir)
+        P = self.points
+        npts = P.xyz.shape[0]
+        nproj = int(L.sgn_point_proj_bytes_f32(npts))
+        if getattr(self, "_proj32", None) is None or self._proj32.numel() < nproj:
+            self._proj32 = torch.empty(max(nproj, 16), dtype=torch.uint8, device=dev)
+        _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(self._proj32), st),
+                   "sgn_point_project_f32")
+        cap = max(R * o.SR, 1)
+        if getattr(self, "_cap32", 0) < cap:
+            self._z32 = [torch.zeros(cap * o.K, 256, dtype=torch.float32, device=dev) for _ in range(3)]
+            self._ws32 = torch.empty(int(L.sgn_aggregate_workspace_bytes_f32(cap)), dtype=torch.uint8, device=dev)
+            self._feat32 = torch.empty(cap, 4, dtype=torch.float32, device=dev)
+            self._cap32 = cap
+        qo = q.abi()
+        _lib.check(L.sgn_aggregate_train_fwd_f32(_lib.ptr(self._proj32), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
+                                                 _lib.ptr(blob), _lib.ptr(self._feat32), _lib.ptr(self._z32[0]),
+                                                 _lib.ptr(self._z32[1]), _lib.ptr(self._z32[2]), _lib.ptr(self._ws32),
+                                                 self._ws32.numel(), st), "sgn_aggregate_train_fwd_f32")
+        dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if dp:
+            t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, npts)
+            sync = torch.cat([q.counters[:1].to(torch.int64), gather_counts(t_cnt)])
+        else:
+            sync = q.counters[:1]
+        S, *t_counts = (int(x) for x in sync.tolist())   # one host sync per step
+        qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
+              "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
+        self.last_query = qd   # the step's sample-major query (tests rerun fp32 autograd on it)
+        feat, _, mask = aggregate(P, self.mlp, campos.reshape(1, 3), rot, raydir, qd["samp_ray"], qd["samp_locw"],
+                                  qd["pidx"], saved=self._z32)
+        total, parts, full, ray_mask = composite_losses(P, qd, feat, mask.sum(-1) > 0, campos, rot, raydir,
+                                                        gt.reshape(-1, 3).to(dev, torch.float32), o)
+        total.backward()
         self.allreduce_grads([self.mlp.flat])
         if dp:
             _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)

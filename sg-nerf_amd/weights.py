@@ -103,6 +103,11 @@ def pack_mlp(state, device, precision="f16"):
     bs = [np.ascontiguousarray(torch.as_tensor(state[n + ".bias"]).detach().cpu().float().numpy()) for n, *_ in layers]
     wp = (ctypes.c_void_p * len(layers))(*[w.ctypes.data for w in ws])
     bp = (ctypes.c_void_p * len(layers))(*[b.ctypes.data for b in bs])
+    if torch.device(device).type == "cpu":
+        if precision != "f32":
+            raise ValueError("host packing: precision 'f32' only")
+        _lib.check(L.sgn_mlp_pack_f32_host(nl, dim, wp, bp, out.data_ptr()), "sgn_mlp_pack_f32_host")
+        return out
     with torch.cuda.device(device):
         if precision == "f32":
             _lib.check(L.sgn_mlp_pack_f32(nl, dim, wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_f32")

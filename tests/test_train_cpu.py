@@ -191,3 +191,21 @@ def test_gpu_training_gradients_match_cpu():
         torch.testing.assert_close(a.grad.cpu(), b.grad, rtol=1e-3, atol=1e-7)
     tr.apply()
     assert tr.step_count == 1
+
+
+@pytest.mark.parametrize("seed", [4, 9])
+def test_flat_pack_f32_matches_host_pack(seed):
+    """train_hip._PackerF32 (index gathers from the flat parameter + per-layer shifts, run here on
+    the CPU) against the C packer (pack_blob_x3 into host memory), byte for byte; the layers' weights
+    span several binades so every layer gets its own shift."""
+    from sgnerf_amd.train_hip import FlatMLP, _PackerF32
+    from sgnerf_amd.weights import LAYERS, init_mlp, pack_mlp
+    mlp = init_mlp(seed, bias_std=0.05)
+    for i, (n, *_) in enumerate(LAYERS):
+        mlp[n + ".weight"] = mlp[n + ".weight"] * 2.0 ** (3 - i)
+    flat = FlatMLP(mlp, "cpu")
+    blob = _PackerF32("cpu", flat).pack(flat.flat)
+    host = pack_mlp(mlp, "cpu", precision="f32")
+    assert blob.numel() == host.numel()
+    bad = torch.nonzero(blob != host).reshape(-1)
+    assert bad.numel() == 0, bad[:20]

@@ -16,7 +16,7 @@ import torch
 
 from sgnerf_amd import _lib
 from sgnerf_amd.train import PointParams, Trainer
-from sgnerf_amd.train_hip import FlatMLP, HipTrainer, _Packer, grads_named
+from sgnerf_amd.train_hip import FlatMLP, HipTrainer, _Packer, _PackerF32, grads_named
 from sgnerf_amd.weights import LAYERS, init_mlp, pack_mlp
 import oracle_query as oq
 from helpers import hyper_for, t_table
@@ -32,6 +32,12 @@ GRAD_TOL_POINTS = 6e-2
 # other way (gradients then differ by <= 8.5e-5 relative L2), and Adam's m / sqrt(v) turns the
 # sign of near-zero gradient components into lr-sized steps.
 UPDATE_TOL = 0.1
+GRAD_TOL_F32 = 1e-4     # precision "f32": every gradient, relative L2 vs fp32 autograd
+# precision "f32" point gradients against the CPU restatement on the ORACLE's query: the near-opaque
+# config-5 batch is ill-conditioned -- two fp32 autograd runs of the same restatement on the same query
+# (torch GPU vs torch CPU) already differ by 1.1e-3..1.5e-3 in the point gradients (measured), and the
+# HIP f32 path measured 1.8e-3 here, 1.1e-3 against torch on the GPU (MLP gradients <= 6.4e-5).
+GRAD_TOL_F32_ORACLE_Q = 5e-3
 LOSS_CURVE_TOL = 0.05   # HIP vs fp32 torch colour loss, 200 steps, 20-step window means (measured max 0.0064 and 0.023 in two runs: the atomic accumulation order of the point gradients makes runs differ)
 
 
@@ -50,16 +56,32 @@ def test_device_pack_matches_host_pack():
     assert torch.equal(tblob.cpu(), ref_t.cpu())
 
 
+@pytest.mark.parametrize("seed", [4, 9])
+def test_device_pack_f32_matches_host_pack(seed):
+    """_PackerF32 (index gathers from the flat parameter, per-layer shifts on the device) against
+    sgn_mlp_pack_f32 (pack_blob_x3 on the host), byte for byte; the weights span several binades
+    so the shifts differ per layer."""
+    mlp = init_mlp(seed, bias_std=0.05)
+    for i, (n, *_) in enumerate(LAYERS):
+        mlp[n + ".weight"] = mlp[n + ".weight"] * 2.0 ** (3 - i)
+    flat = FlatMLP(mlp, DEV)
+    blob = _PackerF32(DEV, flat).pack(flat.flat)
+    host = pack_mlp(mlp, DEV, precision="f32")
+    assert blob.numel() == host.numel()
+    assert torch.equal(blob.cpu(), host.cpu())
+
+
 def _rel(a, b):
     return float(torch.linalg.vector_norm(a.double() - b.double()) / max(torch.linalg.vector_norm(b.double()), 1e-30))
 
 
-def _grads_vs_fp32(pc, campos, rot, raydir, qd, mlp, gt):
+def _grads_vs_fp32(pc, campos, rot, raydir, qd, mlp, gt, precision="f16"):
     """One HIP backward (GPU) and one fp32 torch-autograd backward (train.Trainer on the CPU, on
     the oracle's query of the same rays): the loss, colour and every gradient compared at the
-    module's bars.  Returns the per-tensor relative L2 errors."""
+    module's bars (precision "f32": GRAD_TOL_F32 for every tensor).  Returns the per-tensor
+    relative L2 errors."""
     points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
-    tr = HipTrainer(points, mlp, O, DEV)
+    tr = HipTrainer(points, mlp, O, DEV, precision=precision)
     d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
     parts, full, ray_mask = tr.backward(d(campos), d(rot), d(raydir), 0.1, 8.0, gt.to(DEV))
     torch.cuda.synchronize()
@@ -82,7 +104,10 @@ def _grads_vs_fp32(pc, campos, rot, raydir, qd, mlp, gt):
         e = _rel(g[k].cpu().reshape(b.shape), b)
         worst[k] = e
     print("relative L2 gradient errors:", {k: f"{v:.2e}" for k, v in worst.items()})
-    bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
+    if precision == "f32":
+        bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_F32_ORACLE_Q if k.startswith("points_") else GRAD_TOL_F32)}
+    else:
+        bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
     assert not bad, bad
     return worst, int(ray_mask.sum())
 
@@ -93,11 +118,63 @@ def test_hip_training_gradients_match_torch_fp32(seed):
     _grads_vs_fp32(pc, view.campos, view.camrotc2w, view.raydir, qd, mlp, gt)
 
 
-def test_config5_batch_gradients_match_torch_fp32():
-    """BASELINE config 5 at its workload: one 4096-ray batch (random pixels of a spiral pose of the
-    800x800 frame, as bench.py's training key draws them) over the 1.2 M-point synth-room, SR 24,
-    the opaque aggregator; HIP backward against fp32 autograd of the torch restatement on the
-    oracle's query of the same rays, at the module's gradient bars."""
+@pytest.mark.parametrize("seed", [3, 5])
+def test_hip_f32_training_gradients_match_torch_fp32(seed):
+    """precision "f32": the fp32-faithful HIP forward (k_rows16 save mode) + fp32 backward through
+    the saved pre-activations, every gradient within GRAD_TOL_F32 of fp32 autograd."""
+    pc, view, qd, mlp, gt = _setup(seed=seed)
+    _grads_vs_fp32(pc, view.campos, view.camrotc2w, view.raydir, qd, mlp, gt, precision="f32")
+
+
+@pytest.mark.parametrize("cfg", ["small", "config5"])
+def test_f32_training_matches_fp32_autograd_on_same_query(cfg):
+    """precision "f32" against train.Trainer (fp32 torch autograd) on the GPU over the very samples
+    the HIP query produced (HipTrainer.last_query): isolates the aggregator's arithmetic from the
+    query's (whose sample positions differ from the CPU oracle's in the last bits, which the
+    near-opaque config-5 batch amplifies in the point gradients).  The loss and colour within
+    GRAD_TOL_F32; every gradient within GRAD_TOL_F32 or, where the batch is ill-conditioned, within
+    twice the spread of two fp32 autograd runs (torch on the GPU vs torch on the CPU, same query)."""
+    if cfg == "small":
+        pc, view, _, mlp, gt = _setup(seed=3)
+        raydir = view.raydir
+    else:
+        pc, view, raydir, _, mlp, gt, _ = _config5()
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    tr = HipTrainer(points, mlp, O, DEV, precision="f32")
+    parts, full, ray_mask = tr.backward(d(view.campos), d(view.camrotc2w), d(raydir), 0.1, 8.0, gt.to(DEV))
+    qd = {k: v.long() if v.dtype == torch.int32 else v for k, v in tr.last_query.items()}
+    ref_points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    ref = Trainer(ref_points, mlp, O, DEV)
+    parts_c, full_c, mask_c = ref.backward(d(view.campos), d(view.camrotc2w), d(raydir), 0.1, 8.0, gt.to(DEV), q=qd)
+    torch.cuda.synchronize()
+    assert torch.equal(ray_mask, mask_c)
+    assert _rel(full, full_c) <= GRAD_TOL_F32
+    assert abs(float(parts["total"]) - float(parts_c["total"])) <= GRAD_TOL_F32 * abs(float(parts_c["total"]))
+    # the fp32 noise floor of this batch: the same autograd on the CPU, same query
+    cpu_points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, "cpu")
+    cpu = Trainer(cpu_points, mlp, O, "cpu")
+    cpu.backward(torch.from_numpy(view.campos), torch.from_numpy(view.camrotc2w), torch.from_numpy(raydir),
+                 0.1, 8.0, gt, q={k: v.cpu() for k, v in qd.items()})
+
+    def named(trainer, pts):
+        out = {}
+        for name, *_ in LAYERS:
+            m = trainer.mlp.lin[name.replace(".", "_")]
+            out[name + ".weight"], out[name + ".bias"] = m.weight.grad, m.bias.grad
+        for k in ("points_embeding", "points_color", "points_dir", "points_conf"):
+            out[k] = getattr(pts, k).grad
+        return out
+    ref_g, cpu_g, g = named(ref, ref_points), named(cpu, cpu_points), grads_named(tr)
+    worst = {k: _rel(g[k].reshape(b.shape), b) for k, b in ref_g.items()}
+    floor = {k: _rel(cpu_g[k], b.cpu()) for k, b in ref_g.items()}
+    print(f"{cfg}: relative L2 gradient errors (same query):", {k: f"{v:.2e}" for k, v in worst.items()})
+    print(f"{cfg}: fp32 floor, torch GPU vs torch CPU:", {k: f"{v:.2e}" for k, v in floor.items()})
+    bad = {k: (v, floor[k]) for k, v in worst.items() if v > max(GRAD_TOL_F32, 2 * floor[k])}
+    assert not bad, bad
+
+
+def _config5():
     from sgnerf_amd import scene
     pc = scene.synth_room(1_200_000, seed=0)
     yaw, pitch = scene.spiral_yaw_pitch(37, 120)
@@ -113,8 +190,18 @@ def test_config5_batch_gradients_match_torch_fp32():
           "samp_locw": torch.from_numpy(q["loc_w"][rr, ss]), "pidx": torch.from_numpy(q["pidx"][rr, ss]).long()}
     mlp = init_mlp(0, bias_std=0.01)
     mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
-    worst, n_valid = _grads_vs_fp32(pc, view.campos, view.camrotc2w, raydir, qd, mlp, gt)
-    print(f"config 5: 4096 rays, {n_valid} valid, {len(rr)} samples")
+    return pc, view, raydir, qd, mlp, gt, len(rr)
+
+
+@pytest.mark.parametrize("precision", ["f16", "f32"])
+def test_config5_batch_gradients_match_torch_fp32(precision):
+    """BASELINE config 5 at its workload: one 4096-ray batch (random pixels of a spiral pose of the
+    800x800 frame, as bench.py's training key draws them) over the 1.2 M-point synth-room, SR 24,
+    the opaque aggregator; HIP backward against fp32 autograd of the torch restatement on the
+    oracle's query of the same rays, at the module's gradient bars."""
+    pc, view, raydir, qd, mlp, gt, ns = _config5()
+    worst, n_valid = _grads_vs_fp32(pc, view.campos, view.camrotc2w, raydir, qd, mlp, gt, precision)
+    print(f"config 5 ({precision}): 4096 rays, {n_valid} valid, {ns} samples")
     assert n_valid > 3000
 
 
@@ -513,7 +600,10 @@ def test_hip_sg_training_gradients_match_oracle(dim, seed):
         worst[k] = _rel(v.cpu().reshape(ref.shape), ref)
     print(f"SG dim {dim} relative L2 gradient errors:", {k: f"{v:.2e}" for k, v in worst.items()})
     assert "block2_bpnet.0.weight" in worst
-    bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
+    if precision == "f32":
+        bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_F32_ORACLE_Q if k.startswith("points_") else GRAD_TOL_F32)}
+    else:
+        bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
     assert not bad, bad
 
 
