@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="BASELINE config 5: training steps on 4096 random rays per rank (backward + DP all-reduce)")
     ap.add_argument("--train-rays", type=int, default=4096)
+    ap.add_argument("--train-precision", choices=["f32", "f16"], default="f32",
+                    help="config 5 arithmetic (f32: the reference's; f16: fp16-operand row MLP forward/backward)")
     ap.add_argument("--train-torch", action="store_true",
                     help="config 5 on the torch-autograd restatement (train.Trainer) instead of the HIP backward")
     ap.add_argument("--sg", action="store_true",
@@ -84,12 +86,15 @@ def self_launch(args):
     return sd.launch_ranks(__file__, args.gpus, sys.argv[1:]).returncode
 
 
-def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
+def train_main(args, world, rank, dev, dist, steps=None, warmup=None, precision=None):
     """Config 5: one training step = 4096 random rays of a random spiral pose per rank, HIP query,
     device autograd through aggregator + composite, bucketed RCCL all-reduce, two Adam groups.
     Returns the result dict (rank 0 prints it when run as the headline)."""
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
+    precision = args.train_precision if precision is None else precision
+    if args.sg and precision == "f32":
+        precision = "f16"    # the SG variant trains at fp16 operands (HipTrainer)
     from sgnerf_amd.train import PointParams, Trainer
     from sgnerf_amd.train_hip import HipTrainer
     sg = dict(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1) if args.sg else {}
@@ -102,7 +107,8 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
     mlp = init_mlp(0, bias_std=0.01, bpnet_layers=1 if args.sg else 0, bpnet_dim=96 if args.sg else 0)
     mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
     points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, dev)
-    tr = Trainer(points, mlp, o, dev) if args.train_torch else HipTrainer(points, mlp, o, dev, bpnet=pc.bpnet)
+    tr = Trainer(points, mlp, o, dev) if args.train_torch else HipTrainer(points, mlp, o, dev, bpnet=pc.bpnet,
+                                                                                 precision=precision)
     g = torch.Generator().manual_seed(1 + rank)
     n_steps = warmup + steps
     batches = []
@@ -140,11 +146,13 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None):
     res = {"metric": "training rays/sec, 4096-ray batches with backward, DP (BASELINE config 5)",
            "value": rays / elapsed, "unit": "rays/s", "n_gpus": world, "steps": steps, "warmup": warmup,
            "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "f32" if args.train_torch else "f16", "data": "synthetic",
+           "vs_baseline": None, "dtype": "f32" if (args.train_torch or precision == "f32") else "f16",
+           "data": "synthetic",
            "config": {"workload": f"synth-room, {args.train_rays} random rays per rank per step, SR=24, K=8, "
                                   f"{args.points} neural points, HIP query + "
                                   + ("torch autograd" if args.train_torch else
-                                     "HIP MFMA row-MLP forward/backward + torch colour/composite autograd")
+                                     "HIP fp32-faithful row-MLP forward (k_rows16 save mode) + fp32 backward" if precision == "f32"
+                                     else "HIP MFMA row-MLP forward/backward + torch colour/composite autograd")
                                   + (" (SG-NeRF variant: semantic-guided kNN, block2_bpnet 352->256)" if args.sg else "")
                                   + " + RCCL all-reduce",
                       "parallelism": f"dp{world}"},
@@ -452,8 +460,7 @@ def main():
     ref_flop = (FLOP_PER_NB + (2 * 352 * 256 if args.sg else 0)) * h["n_nb"]
     achieved = rows_flop / (stage_ms["agg_rows"] * 1e-3) / 1e12
     peak = PEAK_X3_TFLOPS if x3 else PEAK_F16_TFLOPS
-    w16 = os.environ.get("SGN_X3_W16", "1") != "0"     # mlp_x3.hip: 16x16 two-waves-per-SIMD kernels
-    kname = ("k_rows16" if w16 else "k_agg_rows_x3") if x3 else "k_agg_rows"
+    kname = "k_rows16" if x3 else "k_agg_rows"
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -509,7 +516,7 @@ def main():
             "bytes_per_frame_no_reuse_credit": h["q_bytes"],
         },
         "roofline_proj": {
-            "kernel": (("k_point_proj16" if w16 else "k_point_proj_x3") if x3 else "k_point_proj") + " (block1.0 point inputs, all points, once per frame)",
+            "kernel": ("k_point_proj16" if x3 else "k_point_proj") + " (block1.0 point inputs, all points, once per frame)",
             "bound": "mfma", "achieved": FLOP_PER_POINT_PROJ * args.points / (stage_ms["proj"] * 1e-3) / 1e12,
             "peak": peak, "unit": "TFLOP/s", "avg_launch_ms": stage_ms["proj"],
         },
@@ -536,6 +543,10 @@ def main():
         # BASELINE config 5 (training step, 4096-ray batches, DP over the ranks)
         tr = train_main(args, world, rank, dev, dist, steps=max(args.steps, 20), warmup=5)
         torch.cuda.empty_cache()
+        tr16 = None
+        if tr["dtype"] == "f32":
+            tr16 = train_main(args, world, rank, dev, dist, steps=max(args.steps, 20), warmup=5, precision="f16")
+            torch.cuda.empty_cache()
         # SURVEY §8d dense stress variant (3.9 M points in a 1 m cube, every candidate occupied)
         sa = argparse.Namespace(**{**vars(args), "scene": "dense", "points": 3_900_000})
         e = render_run(sa, args.precision, world, rank, dev, dist, 2, 1, False)
@@ -549,8 +560,10 @@ def main():
             "roofline_frac": flop_nb * e["n_nb"] / (e["stages_ms"]["agg_rows"] * 1e-3) / 1e12 / peak}
         del e
         torch.cuda.empty_cache()
-        res["train_config5"] = {k: tr[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "dtype",
-                                                      "final_loss", "graph_captures", "config")}
+        keys = ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "final_loss", "graph_captures", "config")
+        res["train_config5"] = {k: tr[k] for k in keys}
+        if tr16 is not None:
+            res["train_config5_f16"] = {k: tr16[k] for k in keys}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(h["pc"], h["mlp"], h["o"], h["views"][0])
     if rank == 0:

@@ -34,92 +34,108 @@ __device__ __forceinline__ float pers_z(const float *campos, const float *rot, f
 // One wave = 64 rays (lane = ray).  A ray's loop stops after its last selected sample: every
 // later slot is a padding slot (sigma 0), whose opacity is exactly 0 and whose transmittance
 // factor 1 - 0 + 1e-10 rounds to 1.0f, so skipping them changes no bit.  The [R, SR] opacity /
-// blend-weight rows are staged in LDS ([ray][SR + 1] floats, zero-filled) and leave as coalesced
-// 16-B stores of the wave's contiguous 64 x SR block.
-constexpr int COMP_RAYS = 64;
+// blend-weight rows go out in column chunks of COMP_CW slots: the wave walks the chunks in step
+// (each lane's ray state -- T, colour, running cummax, the previous slot -- stays in registers),
+// stages a chunk's [64][COMP_CW] values in LDS (zero-filled, so padding slots cost nothing) and
+// stores it as coalesced 16-B writes.  The LDS per workgroup (16.9 KiB) does not grow with SR, so
+// a CU holds 9 such waves at any SR (a whole-row [64][SR + 1] staging took 66 KiB at SR 128).
+constexpr int COMP_RAYS = 64, COMP_CW = 32, COMP_LD = COMP_CW + 1;
 
-__device__ __forceinline__ void store_rows(float *dst, const float *st, int SR, int nrows, int lane) {
-    const int n = nrows * SR;
-    if ((SR & 3) == 0) {  // 16-B stores (dst is 16-B aligned: 64 SR floats per wave block)
-        for (int i = lane * 4; i < n; i += 64 * 4) {
-            const int row = i / SR, col = i - row * SR;
-            const float *p = st + row * (SR + 1) + col;
-            *(float4 *)(dst + i) = make_float4(p[0], p[1], p[2], p[3]);
+// chunk [c0, c0 + cw) of the wave's 64 x SR block (row stride SR) from st [64][COMP_LD]
+__device__ __forceinline__ void store_chunk(float *dst, const float *st, int SR, int c0, int cw, int nrows,
+                                            int lane) {
+    if ((SR & 3) == 0 && cw == COMP_CW) {  // 16-B stores: 8 lanes per row chunk (128 B)
+        for (int i = lane; i < nrows * (COMP_CW / 4); i += 64) {
+            const int row = i >> 3, q = (i & 7) * 4;
+            const float *p = st + row * COMP_LD + q;
+            *(float4 *)(dst + (int64_t)row * SR + c0 + q) = make_float4(p[0], p[1], p[2], p[3]);
         }
     } else {
-        for (int i = lane; i < n; i += 64) {
-            const int row = i / SR;
-            dst[i] = st[row * (SR + 1) + i - row * SR];
+        for (int i = lane; i < nrows * cw; i += 64) {
+            const int row = i / cw, col = i - row * cw;
+            dst[(int64_t)row * SR + c0 + col] = st[row * COMP_LD + col];
         }
     }
 }
 
 __global__ __launch_bounds__(COMP_RAYS) void k_composite(CompArgs a) {
-    extern __shared__ float st[];  // [2][64][SR + 1]: opacity, blend weight
+    __shared__ float st[2][COMP_RAYS * COMP_LD];  // chunk staging: opacity, blend weight
     const int lane = threadIdx.x;
     const int64_t r0 = (int64_t)blockIdx.x * COMP_RAYS, r = r0 + lane;
     const int nrows = a.R - r0 < COMP_RAYS ? (int)(a.R - r0) : COMP_RAYS;
-    const int SR = a.SR, ld = SR + 1;
-    float *so = st + lane * ld, *sb = st + (COMP_RAYS + lane) * ld;
+    const int SR = a.SR;
+    float *so = st[0] + lane * COMP_LD, *sb = st[1] + lane * COMP_LD;
     const bool want_o = a.out_opacity != nullptr, want_b = a.out_blendw != nullptr;
-    if (want_o)
-        for (int s = 0; s < SR; ++s) so[s] = 0.f;
-    if (want_b)
-        for (int s = 0; s < SR; ++s) sb[s] = 0.f;
-    if (r < a.R) {
-        const int ns = a.ray_ns[r], off = a.ray_soff[r];
-        const float z0 = pers_z(a.campos, a.rot, 0.f, 0.f, 0.f);
-        float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
-        bool any_valid = false;
-        float prev_cm = 0.f;
-        // slot s-1 state while slot s's z is read
-        bool pv = false;
-        float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
-        auto process = [&](int slot, float dist) {
-            const bool mask = dist < 1e-8f || (a.unit && dist > 2.f * a.vz);
-            dist = mask ? a.vz : dist;
-            const float valid = pv ? 1.f : 0.f;
-            dist = dist * valid;
-            const float sigma = (pv ? pf.x : 0.f) * valid;
-            const float o = 1.f - expf(-sigma * dist);
-            const float wgt = o * T;
-            if (pv) {
-                cr += pf.y * wgt;
-                cg += pf.z * wgt;
-                cb += pf.w * wgt;
-            }
-            if (want_b) sb[slot] = wgt;
-            T = T * (1.f - o + 1e-10f);
-            if (want_o) so[slot] = o;
-        };
-        const int last = ns < SR ? ns : SR - 1;  // slot ns (padding, z0) closes the last interval
-        for (int s = 0; s <= last; ++s) {
-            float z = z0;
-            bool v = false;
-            float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (s < ns) {
-                const int64_t id = off + s;
-                z = pers_z(a.campos, a.rot, a.samp_locw[id * 3], a.samp_locw[id * 3 + 1], a.samp_locw[id * 3 + 2]);
-                v = a.samp_nnb[id] > 0;
-                if (v) f = *(const float4 *)(a.feat + id * 4);
-            }
-            const float cm = s == 0 ? z : fmaxf(prev_cm, z);
-            if (s > 0) process(s - 1, cm - prev_cm);
-            prev_cm = cm;
-            pv = v;
-            pf = f;
-            any_valid |= v;
+    const bool live = r < a.R;
+    const int ns = live ? a.ray_ns[r] : 0, off = live ? a.ray_soff[r] : 0;
+    const float z0 = pers_z(a.campos, a.rot, 0.f, 0.f, 0.f);
+    float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f;
+    bool any_valid = false;
+    float prev_cm = 0.f;
+    // slot s-1 state while slot s's z is read
+    bool pv = false;
+    float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
+    int c0 = 0;  // the chunk being staged: slot s lands at column s - c0
+    auto process = [&](int slot, float dist) {
+        const bool mask = dist < 1e-8f || (a.unit && dist > 2.f * a.vz);
+        dist = mask ? a.vz : dist;
+        const float valid = pv ? 1.f : 0.f;
+        dist = dist * valid;
+        const float sigma = (pv ? pf.x : 0.f) * valid;
+        const float o = 1.f - expf(-sigma * dist);
+        const float wgt = o * T;
+        if (pv) {
+            cr += pf.y * wgt;
+            cg += pf.z * wgt;
+            cb += pf.w * wgt;
         }
-        if (ns >= SR) process(SR - 1, a.vz);  // a full ray's last slot: interval vsize[2]
+        if (want_b) sb[slot - c0] = wgt;
+        T = T * (1.f - o + 1e-10f);
+        if (want_o) so[slot - c0] = o;
+    };
+    // iteration s reads slot s and closes slot s - 1's interval; slot ns (padding, z0) closes the last
+    const int last = !live ? -1 : ns < SR ? ns : SR - 1;
+    auto step = [&](int s) {
+        float z = z0;
+        bool v = false;
+        float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s < ns) {
+            const int64_t id = off + s;
+            z = pers_z(a.campos, a.rot, a.samp_locw[id * 3], a.samp_locw[id * 3 + 1], a.samp_locw[id * 3 + 2]);
+            v = a.samp_nnb[id] > 0;
+            if (v) f = *(const float4 *)(a.feat + id * 4);
+        }
+        const float cm = s == 0 ? z : fmaxf(prev_cm, z);
+        if (s > 0) process(s - 1, cm - prev_cm);
+        prev_cm = cm;
+        pv = v;
+        pf = f;
+        any_valid |= v;
+    };
+    if (last >= 0) step(0);
+    for (c0 = 0; c0 < SR; c0 += COMP_CW) {  // wave-uniform: every lane walks every chunk
+        const int cw = SR - c0 < COMP_CW ? SR - c0 : COMP_CW;
+        if (want_o)
+            for (int c = 0; c < cw; ++c) so[c] = 0.f;
+        if (want_b)
+            for (int c = 0; c < cw; ++c) sb[c] = 0.f;
+        // iterations whose closed slot s - 1 falls in this chunk
+        const int s_end = last < c0 + cw ? last : c0 + cw;
+        for (int s = c0 + 1; s <= s_end; ++s) step(s);
+        if (live && ns >= SR && c0 + cw == SR) process(SR - 1, a.vz);  // a full ray's last slot: interval vsize[2]
+        __syncthreads();
+        if (want_o) store_chunk(a.out_opacity + r0 * SR, st[0], SR, c0, cw, nrows, lane);
+        if (want_b) store_chunk(a.out_blendw + r0 * SR, st[1], SR, c0, cw, nrows, lane);
+        __syncthreads();
+        if (!want_o && !want_b && c0 + cw > last) break;  // nothing staged: stop after the ray's slots
+    }
+    if (live) {
         a.out_mask[r] = any_valid ? 1 : 0;
         a.out_rgb[r * 3 + 0] = any_valid ? cr + a.bg0 * T : a.bg0;
         a.out_rgb[r * 3 + 1] = any_valid ? cg + a.bg1 * T : a.bg1;
         a.out_rgb[r * 3 + 2] = any_valid ? cb + a.bg2 * T : a.bg2;
         if (a.out_bgT) a.out_bgT[r] = any_valid ? T : 1.f;
     }
-    __syncthreads();
-    if (want_o) store_rows(a.out_opacity + r0 * SR, st, SR, nrows, lane);
-    if (want_b) store_rows(a.out_blendw + r0 * SR, st + COMP_RAYS * ld, SR, nrows, lane);
 }
 
 // ---- dense ray_march (compatibility sub-boundary, diff_ray_marching.py:509-555) ----------
@@ -197,9 +213,7 @@ extern "C" int sgn_composite(const sgn_composite_params *cp, const float *d_camp
     a.bg0 = cp->bg[0]; a.bg1 = cp->bg[1]; a.bg2 = cp->bg[2];
     a.out_rgb = d_out_rgb; a.out_bgT = d_out_bgT; a.out_opacity = d_out_opacity; a.out_mask = d_out_mask;
     a.out_blendw = d_out_blendw;
-    SGN_REQUIRE(cp->SR <= 256, "SR must be at most 256");
-    const size_t lds = (size_t)2 * COMP_RAYS * (cp->SR + 1) * sizeof(float);
-    hipLaunchKernelGGL(k_composite, dim3((unsigned)((R + COMP_RAYS - 1) / COMP_RAYS)), dim3(COMP_RAYS), lds,
+    hipLaunchKernelGGL(k_composite, dim3((unsigned)((R + COMP_RAYS - 1) / COMP_RAYS)), dim3(COMP_RAYS), 0,
                        as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;

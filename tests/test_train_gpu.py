@@ -600,10 +600,8 @@ def test_hip_sg_training_gradients_match_oracle(dim, seed):
         worst[k] = _rel(v.cpu().reshape(ref.shape), ref)
     print(f"SG dim {dim} relative L2 gradient errors:", {k: f"{v:.2e}" for k, v in worst.items()})
     assert "block2_bpnet.0.weight" in worst
-    if precision == "f32":
-        bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_F32_ORACLE_Q if k.startswith("points_") else GRAD_TOL_F32)}
-    else:
-        bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
+    # the SG variant trains at fp16 operands (HipTrainer refuses precision "f32" for it): the f16 bars
+    bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
     assert not bad, bad
 
 

@@ -23,12 +23,22 @@ pc = scene.synth_room(1_200_000, seed=0)
 mlp = init_mlp(0, bias_std=0.01)
 mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
 r = HipRenderer(PointTables.from_cloud(pc, dev), mlp, HotPathOpts(SR=64, precision=prec), dev)
+# SGN_RAY_ORDER=B (B > 0): rays fed in B x B pixel blocks (block-major) instead of row-major
+blk = int(os.environ.get("SGN_RAY_ORDER", "0"))
+perm = None
+if blk > 0:
+    yy, xx = np.meshgrid(np.arange(800), np.arange(800), indexing="ij")
+    key = ((yy // blk) * (800 // blk) + (xx // blk)) * (blk * blk) + (yy % blk) * blk + (xx % blk)
+    perm = torch.from_numpy(np.argsort(key.reshape(-1), kind="stable"))
 views = []
 for i in range(3 + nf):
     yaw, pitch = scene.spiral_yaw_pitch(i % 120, 120)
     v = scene.room_view(800, 800, yaw=yaw + 15.0, pitch=pitch - 5.0)
+    rd = torch.from_numpy(v.raydir)
+    if perm is not None:
+        rd = rd[perm].contiguous()
     views.append((torch.from_numpy(v.campos).to(dev), torch.from_numpy(v.camrotc2w).to(dev),
-                  torch.from_numpy(v.raydir).to(dev), v.near, v.far))
+                  rd.to(dev), v.near, v.far))
 ev = []
 
 
@@ -48,4 +58,5 @@ res = {n: float(np.median([e[n].elapsed_time(e[names[j + 1]]) for e in ev])) for
 res["frame"] = float(np.median([e["query"].elapsed_time(e["end"]) for e in ev]))
 res["prec"] = prec
 res["lib"] = os.environ.get("SGN_VARIANT", "base")
+res["ray_block"] = blk
 print(json.dumps(res), flush=True)
