@@ -320,27 +320,51 @@ static_assert(N_Y32 % 4 == 0, "fp32 section in 16-B units");
 #ifndef SGN_X3_SPLIT3
 #define SGN_X3_SPLIT3 1
 #endif
-constexpr XL L3_16 = SGN_X3_SPLIT3 ? XL{8, 8, 2, 4, OFF16_W3} : XL{8, 16, 1, 2, OFF16_W3};
+// Row kernel workgroup (SGN_X3_RW waves): 4 waves (one per SIMD) with a 2 x 32-KiB ring, so two
+// workgroups share a CU and their waves pair up on each SIMD without a common barrier (the barrier
+// of one chunk boundary no longer holds the other workgroup's wave of the SIMD: while one runs its
+// tile transition or epilogue VALU, the other's MFMAs keep the matrix pipe busy); or 8 waves with a
+// 2 x 64-KiB ring (one workgroup per CU, every wave in step)
+#ifndef SGN_X3_RW
+#define SGN_X3_RW 4
+#endif
+constexpr int NWR = SGN_X3_RW, SPR = NWR == 4 ? 16 : 32;  // row waves, ring slot pairs
+static_assert(NWR == 4 || NWR == 8, "row workgroup: 4 or 8 waves");
+constexpr int KCR = SPR / 16;                             // k-steps of 16 tiles per chunk
+constexpr XL L3_16 = SGN_X3_SPLIT3 ? XL{8, 8, 2, 2 * KCR, OFF16_W3} : XL{8, 16, 1, KCR, OFF16_W3};
 struct NetR16 {
+    static constexpr int NW = NWR, SP = SPR;  // waves sharing the ring, fragment pairs per ring slot
     static constexpr int NL = 4;
-    static constexpr XL L[NL] = {{2, 16, 1, 2, OFF16_W0B}, {8, 16, 1, 2, OFF16_W1}, {9, 16, 1, 2, OFF16_W2}, L3_16};
+    static constexpr XL L[NL] = {{2, 16, 1, KCR, OFF16_W0B}, {8, 16, 1, KCR, OFF16_W1}, {9, 16, 1, KCR, OFF16_W2},
+                                 L3_16};
 };
 template <int KB>
 struct NetR16SG {
+    static constexpr int NW = NWR, SP = SPR;
     static constexpr int NL = 5;
-    static constexpr XL L[NL] = {{2, 16, 1, 2, OFF16_W0B}, {8, 16, 1, 2, OFF16_W1}, {KB, 16, 1, 2, OFF16_WB},
-                                 {9, 16, 1, 2, OFF16_W2}, L3_16};
+    static constexpr XL L[NL] = {{2, 16, 1, KCR, OFF16_W0B}, {8, 16, 1, KCR, OFF16_W1}, {KB, 16, 1, KCR, OFF16_WB},
+                                 {9, 16, 1, KCR, OFF16_W2}, L3_16};
 };
 struct NetProj16 {
+    static constexpr int NW = NW16, SP = SLOT_PAIRS;
     static constexpr int NL = 1;
     static constexpr XL L[NL] = {{7, 16, 1, 2, OFF16_W0A}};
 };
+// colour kernel workgroup (SGN_X3_CW waves), as the row kernel's
+#ifndef SGN_X3_CW
+#define SGN_X3_CW 8
+#endif
+constexpr int NWC = SGN_X3_CW, SPC = NWC == 4 ? 16 : 32, KCC = SPC / 8;
+static_assert(NWC == 4 || NWC == 8, "colour workgroup: 4 or 8 waves");
 struct NetColor16 {
+    static constexpr int NW = NWC, SP = SPC;
     static constexpr int NL = 3;
-    static constexpr XL L[NL] = {{9, 8, 1, 4, OFF16_C0}, {4, 8, 1, 4, OFF16_C1}, {4, 8, 1, 4, OFF16_C2}};
+    static constexpr XL L[NL] = {{9, 8, 1, KCC, OFF16_C0}, {4, 8, 1, KCC, OFF16_C1}, {4, 8, 1, KCC, OFF16_C2}};
 };
-static_assert(Sched<NetR16>::total() == 14 && Sched<NetR16>::pairs(9) == 16, "16x16 row stream");
-static_assert(Sched<NetColor16>::total() == 5 && Sched<NetColor16>::pairs(2) == 8, "16x16 colour stream");
+static_assert(NWR == 4 ? Sched<NetR16>::total() == 27 : Sched<NetR16>::total() == 14 && Sched<NetR16>::pairs(9) == 16,
+              "16x16 row stream");
+static_assert(NWC == 4 ? Sched<NetColor16>::total() == 9 && Sched<NetColor16>::pairs(4) == 8
+                       : Sched<NetColor16>::total() == 5 && Sched<NetColor16>::pairs(2) == 8, "16x16 colour stream");
 
 __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -362,12 +386,14 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slo
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
         constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
-        chunk_enter<Net, N, NW16, Vm::vm(C)>(wb, lds, slot, w, lane, lz, ts);
+        constexpr int NWv = Net::NW, SLOTv = Net::SP * PAIR;
+        static_assert(nk(ly, C) * TP <= Net::SP, "chunk larger than a ring slot");
+        chunk_enter<Net, N, NWv, Vm::vm(C)>(wb, lds, slot, w, lane, lz, ts);
         post(cc);
-        const char *sl = lds + slot * SLOT;
-        char *dnext = lds + (slot ^ 1) * SLOT;
+        const char *sl = lds + slot * SLOTv;
+        char *dnext = lds + (slot ^ 1) * SLOTv;
         constexpr int NF = nk(ly, C) * TP;
-        constexpr int PW = dma_pieces<Net, NN, NW16>();
+        constexpr int PW = dma_pieces<Net, NN, NWv>();
         auto frag = [&](int f, int part) { return *(const h8 *)(sl + (2 * f + part) * 1024 + lane * 16); };
         h8 fh[PD], fl[PD];
 #pragma unroll
@@ -390,17 +416,25 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slo
                 }
                 if constexpr (TRANS) {
                     acc[t] = mfma16(B.hi, Ah, acc[t]);
+#ifndef SGN_X3_ABLATE_MFMA3
                     acc[t] = mfma16(B.lo, Ah, acc[t]);
                     acc[t] = mfma16(B.hi, Al, acc[t]);
+#else
+                    asm volatile("" :: "v"(Al));
+#endif
                 } else {
                     acc[t] = mfma16(Ah, B.hi, acc[t]);
+#ifndef SGN_X3_ABLATE_MFMA3  // timing experiment only: one product instead of three (wrong results)
                     acc[t] = mfma16(Ah, B.lo, acc[t]);
                     acc[t] = mfma16(Al, B.hi, acc[t]);
+#else
+                    asm volatile("" :: "v"(Al));
+#endif
                 }
                 constexpr int NS = NF / SGN_X3_SPREAD_DIV > 0 ? NF / SGN_X3_SPREAD_DIV : 1;
                 if constexpr (F < NS) {
                     static_for<(F + 1) * PW / NS - F * PW / NS>([&](auto jj) {
-                        dma_piece<Net, NN, F * PW / NS + decltype(jj)::value, NW16>(wb, dnext, w, lane, lz);
+                        dma_piece<Net, NN, F * PW / NS + decltype(jj)::value, NWv>(wb, dnext, w, lane, lz);
                     });
                 }
                 mid(std::integral_constant<int, (C * ly.kc + KK) * TP + t>{});
@@ -519,10 +553,12 @@ __global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
 }
 
 // ---- per-neighbour rows (16x16) -------------------------------------------------------------
-constexpr int WG16_SAMPLES = NW16 * 2;            // 16 samples = 128 rows per workgroup tile
-constexpr int YT16_OFF = Y_LDS_OFF + N_Y32 * 4;  // [unit r][20] 2^s3 b3 (t = 0..15) then [r][20] 2^-s3 alpha w
+constexpr int WG16_SAMPLES = NWR * 2;            // halves (16 rows, 2 per wave) per workgroup tile
+constexpr int TPBR = NWR * 64;
+constexpr int YR_OFF = NSLOT * SPR * PAIR;        // the row kernel's fp32 section, after its ring
+constexpr int YT16_OFF = YR_OFF + N_Y32 * 4;      // [unit r][20] 2^s3 b3 (t = 0..15) then [r][20] 2^-s3 alpha w
 constexpr int ROWS16_LDS = YT16_OFF + 2 * 16 * 20 * 4;
-static_assert(ROWS16_LDS <= 163840, "LDS budget (16x16 rows)");
+static_assert(ROWS16_LDS * (8 / NWR) <= 163840, "LDS budget (16x16 rows, 8 / NWR workgroups per CU)");
 
 // row r's point record, its sample position and view direction (+ the caller's pers
 // coordinates on the compatibility path)
@@ -582,8 +618,8 @@ __device__ __forceinline__ Rec16<PERS> load_rec16(const AggArgs &a, const RowIdx
 struct VmL3P0 {
     static constexpr int vm(int c) { return c == 1 ? REC16_LOADS + 1 : 0; }
 };
-struct VmL0 {
-    static constexpr int vm(int) { return 16; }
+struct VmL0 {  // the P loads follow only the DMA of block1.0's first chunk
+    static constexpr int vm(int c) { return c == 0 ? 16 : 0; }
 };
 
 // ---- paired samples: k_rows16's 8-row halves ----------------------------------------------------
@@ -855,7 +891,7 @@ __device__ __forceinline__ XcdTiles xcd_tiles(int ntiles) {
 // SAVE (base viewmlp, training): the pre-activations of block1.0 / 1.2 / 3.0 go to a.z1 / z2 / z3 as
 // the next layer converts them (chain_k)
 template <int KB, bool PERS, bool SAVE = false>
-__global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
+__global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
     using Net = std::conditional_t<(KB > 0), NetR16SG<KB>, NetR16>;
     constexpr int LB = 2, L2 = KB ? 3 : 2, L3 = KB ? 4 : 3;
     constexpr int NBP = KB > 8 ? KB - 8 : 0;  // BPNet k-steps (32 channels each)
@@ -869,12 +905,12 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     const float *proj = (const float *)a.proj;
     {
         const float *src = (const float *)((const char *)a.blob + OFF16_F32);
-        float *dst = (float *)(lds + Y_LDS_OFF);
-        for (int i = threadIdx.x; i < N_Y32; i += TPB16) dst[i] = src[i];
+        float *dst = (float *)(lds + YR_OFF);
+        for (int i = threadIdx.x; i < N_Y32; i += TPBR) dst[i] = src[i];
         {
             // row stride 20 floats: the 16 lanes' 16-B reads of one column quad hit disjoint banks
             float *yt = (float *)(lds + YT16_OFF);
-            for (int i = threadIdx.x; i < 512; i += TPB16) {
+            for (int i = threadIdx.x; i < 512; i += TPBR) {
                 const int which = i >> 8, u = i & 255, t = u >> 4, rr = u & 15;
                 yt[which * 320 + rr * 20 + t] = src[(which ? Y_WA : Y_B3) + 16 * t + rr];
             }
@@ -882,7 +918,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     }
     __syncthreads();
     int slot = 0;
-    dma_chunk<Net, 0, NW16>(wb, lds, w, lane, 0);
+    dma_chunk<Net, 0, NWR>(wb, lds, w, lane, 0);
     // The next tile's chain, prefetched inside the current tile so each step lands under MFMAs:
     // row-table entry (block1.2), neighbour / ray index (block3.0), point record + sample position
     // and the P row (block3.2).  First tile: here.
@@ -906,7 +942,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     f32x4 accA[16], accB[16];
     load_p(nx.pid, pick<(KB > 0)>(accB, accA));  // SG: where the tile loop copies it from
 #ifdef SGN_X3_TIMING
-    TStamp tsv{blockIdx.x < TD_BLOCKS && a.tdbg ? a.tdbg + ((int64_t)blockIdx.x * NW16 + w) * TD_EV : nullptr, 0};
+    TStamp tsv{blockIdx.x < TD_BLOCKS && a.tdbg ? a.tdbg + ((int64_t)blockIdx.x * NWR + w) * TD_EV : nullptr, 0};
     TStamp *ts = &tsv;
     // in-kernel clock (MI355X_MICROARCH.md 'DVFS give-back' item 6): s_memtime and s_memrealtime
     // (100 MHz) around the tile loop, in the last four words of the wave's stamp area
@@ -922,7 +958,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
 
     // epilogue pieces (LDS reads through the tile's opaque base)
     auto epi_begin = [&](Epi16 &e, const char *ldsi, float wgt, int nA, int nB, int2 ce, bool ok) {
-        const float inv3 = ((const float *)(ldsi + Y_LDS_OFF))[Y_INV + 3];
+        const float inv3 = ((const float *)(ldsi + YR_OFF))[Y_INV + 3];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const float wi = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, wgt)));
@@ -968,7 +1004,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
     auto epi_end = [&](Epi16 &e, const char *ldsi, int nA, int nB, int s_ix) {
         // alpha: row logits summed over the 16 lanes (units) of the group, softplus(x + b - 1), blended
         // over the segment's rows like f_s
-        const float ba = ((const float *)(ldsi + Y_LDS_OFF))[Y_BA];
+        const float ba = ((const float *)(ldsi + YR_OFF))[Y_BA];
         const float sc3 = SGN_X3_B3FOLD ? 1.f / e.inv3 : 1.f;  // 2^s3, exact
         float xr[4];
 #pragma unroll
@@ -1005,7 +1041,7 @@ __global__ __launch_bounds__(TPB16, 1) void k_rows16(AggArgs a) {
         int lz = 0;
         asm volatile("" : "+s"(lz));
         char *ldsi = lds + lz;
-        const float *Yl = (const float *)(ldsi + Y_LDS_OFF);
+        const float *Yl = (const float *)(ldsi + YR_OFF);
         const int hslot = base + w * 2 + sc;  // this lane's half (the LDS ring slot is `slot`)
         const int nslot = tile + xt.step < xt.end ? hslot + xt.step * WG16_SAMPLES : nslots;  // next tile's half
         X3T();  // tile start
@@ -1355,9 +1391,11 @@ struct ColorArgs {
 // 1 and 2 chain lazily as in k_rows16 (k-step s converts tiles 2 s, 2 s + 1 of the previous layer).
 // The output layer (128 -> 3) and the sigmoid are per-lane FMAs over the 32 units a lane holds
 // plus two cross-group shuffles.
-constexpr int COL16_LDS = Y_LDS_OFF + N_Y32 * 4;
+constexpr int YC_OFF = NSLOT * SPC * PAIR, TPBC = NWC * 64;
+constexpr int COL16_LDS = YC_OFF + N_Y32 * 4;
+static_assert(COL16_LDS * (8 / NWC) <= 163840, "LDS budget (colour, 8 / NWC workgroups per CU)");
 
-__global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
+__global__ __launch_bounds__(TPBC, 8 / NWC) void k_color16(ColorArgs a) {
     __shared__ __attribute__((aligned(16))) char lds[COL16_LDS];
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4, r = lane & 15;
@@ -1367,12 +1405,12 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
     const WBlob wb = make_blob(a.blob, BLOB_BYTES_ALL);
     {
         const float *src = (const float *)((const char *)a.blob + OFF16_F32);
-        float *dst = (float *)(lds + Y_LDS_OFF);
-        for (int i = threadIdx.x; i < N_Y32; i += TPB16) dst[i] = src[i];
+        float *dst = (float *)(lds + YC_OFF);
+        for (int i = threadIdx.x; i < N_Y32; i += TPBC) dst[i] = src[i];
     }
     __syncthreads();
     int slot = 0;
-    dma_chunk<NetColor16, 0, NW16>(wb, lds, w, lane, 0);
+    dma_chunk<NetColor16, 0, NWC>(wb, lds, w, lane, 0);
     // The tile's f_s rows and sample ids, then its ray ids, then its ray directions: the next tile's
     // rows and sample ids go out in colour 1, its ray ids in colour 2 and its directions in its own
     // colour 0 (needed by colour 0's last k-step), each step one chunk after the load it depends on,
@@ -1395,13 +1433,13 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) vd[c] = a.raydir[(int64_t)rn * 3 + c];
     };
-    load_rows(a.item0 + blockIdx.x * (16 * NW16) + w * 16 + r);
+    load_rows(a.item0 + blockIdx.x * (16 * NWC) + w * 16 + r);
     load_ray();
-    for (int base = a.item0 + blockIdx.x * (16 * NW16); base < end; base += gridDim.x * (16 * NW16)) {
+    for (int base = a.item0 + blockIdx.x * (16 * NWC); base < end; base += gridDim.x * (16 * NWC)) {
         int lz = 0;
         asm volatile("" : "+s"(lz));
         char *ldsi = lds + lz;
-        const float *Yl = (const float *)(ldsi + Y_LDS_OFF);
+        const float *Yl = (const float *)(ldsi + YC_OFF);
         const int item = base + w * 16 + r;
         const bool sval = item < end;
         const int s = sn;
@@ -1452,10 +1490,14 @@ __global__ __launch_bounds__(TPB16, 1) void k_color16(ColorArgs a) {
         const float inv4 = Yl[Y_INV + 4], inv5 = Yl[Y_INV + 5], inv6 = Yl[Y_INV + 6];
         // colour 0 consumed fr: the next tile's rows go out after colour 1's boundary (land under it)
         run_layer16<NetColor16, 1>(wb, ldsi, slot, w, lane, lz, c1, [&](auto k) { return chain(c0, inv4, k); },
-                                   [&](auto) { load_rows(item + gridDim.x * (16 * NW16)); });
+                                   [&](auto c) {
+                                       if constexpr (decltype(c)::value == 0) load_rows(item + gridDim.x * (16 * NWC));
+                                   });
         bias(c0, Y_CB2);
         run_layer16<NetColor16, 2>(wb, ldsi, slot, w, lane, lz, c0, [&](auto k) { return chain(c1, inv5, k); },
-                                   [&](auto) { load_ray(); });  // the next tile's ray ids
+                                   [&](auto c) {
+                                       if constexpr (decltype(c)::value == 0) load_ray();  // the next tile's ray ids
+                                   });
         // output layer: units 16 t + 4 g + i of this lane, summed over the 4 lane groups (the four
         // weights of a (t, c) as one 16-B LDS read: this file is built without SLP vectorisation)
         float o[3] = {0.f, 0.f, 0.f};
@@ -1682,8 +1724,8 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
                                                                                       : x3::k_rows16<11, true>)
                                      : (ksb == 0 ? x3::k_rows16<0, false> : ksb == KS_HID ? x3::k_rows16<8, false>
                                                                                         : x3::k_rows16<11, false>);
-            const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES;
-            hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < 256 ? wg16 : 256)), dim3(x3::TPB16), 0, st, a);
+            const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES, wmax = 256 * (8 / x3::NWR);
+            hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < wmax ? wg16 : wmax)), dim3(x3::TPBR), 0, st, a);
         }
 #ifdef SGN_X3_TIMING
         if ((stages & 1) && i0 == 0)
@@ -1695,8 +1737,8 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
             }
 #endif
         if (stages & 2) {
-            const int64_t wgc = (n + 16 * x3::NW16 - 1) / (16 * x3::NW16);
-            hipLaunchKernelGGL(x3::k_color16, dim3((unsigned)(wgc < 256 ? wgc : 256)), dim3(x3::TPB16), 0, st, c);
+            const int64_t wgc = (n + 16 * x3::NWC - 1) / (16 * x3::NWC), wcmax = 256 * (8 / x3::NWC);
+            hipLaunchKernelGGL(x3::k_color16, dim3((unsigned)(wgc < wcmax ? wgc : wcmax)), dim3(x3::TPBC), 0, st, c);
         }
     }
     SGN_CHECK_HIP(hipGetLastError());
