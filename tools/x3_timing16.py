@@ -1,15 +1,23 @@
 """SGN_X3_TIMING dump of k_rows16 (8 waves): median cycles per phase of a work tile.
-Usage: python tools/x3_timing16.py <dump>"""
+Usage: python tools/x3_timing16.py <dump> [waves per workgroup: 4 (default) or 8]"""
 import sys
 
 import numpy as np
 
-TB, NW, EV = 8, 8, 2048
+EV = 2048
+RW = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+TB, NW = (8, 8) if RW == 8 else (16, 4)   # the stamp buffer holds 64 waves (mlp_x3.hip TD_BLOCKS x NW16)
 d = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(TB, NW, EV).astype(np.int64)
-labels = ["tile start -> gather + PE", "-> L0 chunk entered", "L0 (32 pairs) + P add", "L1C0 (32)", "L1C1", "L1C2",
-          "L1C3", "L2C0 (32)", "L2C1", "L2C2", "L2C3", "L2C4 (16)", "L3C0 (32)", "L3C1", "L3C2", "L3C3 -> MFMAs issued",
-          "-> block3.2 epilogue done", "f_s + alpha -> tile end", "loop back -> tile start"]
-pairs = [0, 0, 32, 32, 32, 32, 32, 32, 32, 32, 32, 16, 32, 32, 32, 32, 0, 0, 0]
+if RW == 8:   # 32-pair chunks: L0 1, L1 4, L2 4 + 1 of 16, L3 4
+    ch = [("L0", 32)] + [(f"L1C{c}", 32) for c in range(4)] + [(f"L2C{c}", 32 if c < 4 else 16) for c in range(5)] + \
+         [(f"L3C{c}", 32) for c in range(4)]
+else:         # 16-pair chunks: L0 2, L1 8, L2 9, L3 2 passes x 4
+    ch = [(f"L0C{c}", 16) for c in range(2)] + [(f"L1C{c}", 16) for c in range(8)] + [(f"L2C{c}", 16) for c in range(9)] + \
+         [(f"L3P{c // 4}C{c % 4}", 16) for c in range(8)]
+labels = ["tile start -> gather + PE", "-> L0 chunk entered"] + [n for n, _ in ch[:-1]] + \
+         [ch[-1][0] + " -> MFMAs issued", "-> block3.2 epilogue done", "f_s + alpha -> tile end",
+                                 "loop back -> tile start"]
+pairs = [0, 0] + [p for _, p in ch] + [0, 0, 0]
 M = len(labels)
 rows = []
 clocks = []
@@ -26,6 +34,7 @@ for b in range(TB):
         rows.append(np.diff(s[: nt * M + 1])[: nt * M].reshape(nt, M)[1:])
 a = np.concatenate(rows)
 med = np.median(a, axis=0)
+labels = labels[:len(pairs)]
 ideal = sum(pairs) * 48 * 2  # 3 MFMAs x 16 cycles per pair, two waves share a SIMD
 print(f"tiles {a.shape[0]}; median cycles per tile {med.sum():.0f} (MFMA-only ideal per SIMD {ideal}, {ideal / med.sum():.1%})")
 for i in range(M):
