@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 6
+#define SGN_ABI_VERSION 7
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -369,6 +369,32 @@ int sgn_composite(const sgn_composite_params *cp, const float *d_campos, const f
 int sgn_ray_march_dense(const float *d_ray_dist, const uint8_t *d_valid, const float *d_feat, int64_t R,
                         int32_t SR, const float *bg, float *d_rgb, float *d_opacity, float *d_acc_t,
                         float *d_blendw, float *d_bgT, sgn_stream_t stream);
+
+/* ---- training loss stage (forward + backward) ----------------------------
+ * Replaces the torch autograd of ray_dist + ray_march + fill_invalid and the training losses:
+ *   models/neural_points_volumetric_model.py:569-577, models/rendering/diff_ray_marching.py:509-555,
+ *   models/base_rendering_model.py:534-664 (ray_masked_coarse_raycolor; ray_miss / coarse logged),
+ *   models/mvs_points_volumetric_model.py:607-614 (zero_one_loss on conf_coefficient). */
+typedef struct {
+    int32_t SR, K;
+    float vsize_z;             /* vsize[2] */
+    int32_t raydist_mode_unit;
+    float bg[3];
+    float zero_one_weight;     /* 1e-4 (train_ft) */
+    float zero_one_eps;        /* 1e-3 */
+} sgn_loss_params;
+
+size_t sgn_loss_workspace_bytes(int64_t R, int32_t SR);
+/* d_feat float4[S] per sample (alpha, r, g, b; zeros for samples without neighbours) in; per ray
+ * d_out_rgb float[R*3] (bg for rays without a valid sample) and d_out_mask int8[R]; d_losses
+ * float[8] (device): ray_masked_coarse_raycolor, conf_coefficient (zero-one), ray_miss_coarse_raycolor,
+ * coarse_raycolor, then the gradient scales; d_dfeat float4[S] = d total / d feat of every sample of
+ * the rays (written); d_dconf float[N] += d total / d conf (atomics).  total = d_losses[0] + 3e-6 +
+ * zero_one_weight * d_losses[1].  No host synchronisation. */
+int sgn_loss_train(const sgn_loss_params *lp, const float *d_campos, const float *d_camrotc2w, int64_t R,
+                   const sgn_query_out *q, const float *d_feat, const float *d_gt, const float *d_conf,
+                   float *d_out_rgb, int8_t *d_out_mask, float *d_losses, float *d_dfeat, float *d_dconf,
+                   void *d_workspace, size_t workspace_bytes, sgn_stream_t stream);
 
 /* ---- misc -------------------------------------------------------------- */
 int sgn_abi_version(void);

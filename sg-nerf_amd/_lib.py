@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -60,6 +60,11 @@ class PointGrads(ctypes.Structure):
 
 class CompositeParams(ctypes.Structure):
     _fields_ = [("SR", c_i32), ("vsize_z", c_f32), ("raydist_mode_unit", c_i32), ("bg", c_f32 * 3)]
+
+
+class LossParams(ctypes.Structure):
+    _fields_ = [("SR", c_i32), ("K", c_i32), ("vsize_z", c_f32), ("raydist_mode_unit", c_i32), ("bg", c_f32 * 3),
+                ("zero_one_weight", c_f32), ("zero_one_eps", c_f32)]
 
 
 # name -> (restype, argtypes); every symbol include/sgn_hip.h declares.
@@ -124,6 +129,9 @@ SIGNATURES = {
     "sgn_mlp_pack_index_f32": (c_i32, [c_i32, c_i32, c_i32, ctypes.POINTER(c_i32), c_i64]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
                               c_i32, ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_loss_workspace_bytes": (c_sz, [c_i64, c_i32]),
+    "sgn_loss_train": (c_i32, [ctypes.POINTER(LossParams), c_vp, c_vp, c_i64, ctypes.POINTER(QueryOut), c_vp, c_vp,
+                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "sgn_ray_march_dense": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, ctypes.POINTER(c_f32), c_vp, c_vp, c_vp,
                                     c_vp, c_vp, c_vp]),
 }

@@ -109,7 +109,40 @@ class _SavedLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gz):
         x, w = ctx.saved_tensors
-        return gz @ w, gz.t() @ x, gz.sum(0), None
+        return gz @ w, _dw_rows(gz, x), gz.sum(0), None
+
+
+DW_CHUNK_F32 = 1024
+
+
+class _LinearRows(torch.autograd.Function):
+    """F.linear whose weight gradient is the split-K _dw_rows (same fp32 math, other grid)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, w = ctx.saved_tensors
+        return gz @ w, _dw_rows(gz, x), gz.sum(0)
+
+
+def _dw_rows(gz, x, chunk=DW_CHUNK_F32):
+    """gz^T x over the row dimension (fp32): the rows in `chunk`-row batches through one batched
+    GEMM, the partials summed (a [256 x C] output of a plain GEMM with K = tens of thousands of rows
+    occupies a handful of CUs), a ragged tail of rows as one more GEMM."""
+    rows = gz.shape[0]
+    nb = rows // chunk
+    if nb <= 1:
+        return gz.t() @ x
+    body = nb * chunk
+    g = torch.bmm(gz[:body].reshape(nb, chunk, gz.shape[1]).transpose(1, 2),
+                  x[:body].reshape(nb, chunk, x.shape[1])).sum(0)
+    if body < rows:
+        g = g + gz[body:].t() @ x[body:]
+    return g
 
 
 def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, samp_locw, pidx, saved=None):
@@ -155,7 +188,7 @@ def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, 
     sd = torch.index_select(points.points_dir, 0, fm)
     ov = ori_v[:, None, :].expand(S, K, 3).reshape(-1, 3)[m]
     h = torch.cat([h, torch.index_select(points.points_color, 0, fm), sd - ov, torch.sum(sd * ov, dim=-1, keepdim=True)], dim=-1)
-    h = lr_(mlp.f("block3.2", lr_(lin("block3.0", h, 2))))
+    h = lr_(_LinearRows.apply(lr_(lin("block3.0", h, 2)), mlp.w("block3.2"), mlp.b("block3.2")))
     alpha = F.softplus(mlp.f("alpha_branch.0", h) - 1)
     hk = torch.zeros(S * K, h.shape[-1], device=h.device, dtype=h.dtype).masked_scatter(m[:, None], h)
     ak = torch.zeros(S * K, 1, device=h.device, dtype=h.dtype).masked_scatter(m[:, None], alpha)

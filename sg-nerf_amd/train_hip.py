@@ -36,6 +36,7 @@ from . import _lib
 from .opts import HotPathOpts
 from .train import (PointParams, _allreduce_buckets, _allreduce_point_rows, _pe, composite_losses, gather_counts,
                     touched_rows)
+from .loss_hip import LossStage
 from .weights import BPNET, LAYERS, layers_for, strip_prefix
 
 N_F32 = 2056
@@ -345,6 +346,10 @@ class HipTrainer:
         self._cap = 0
         # the colour/composite/loss stage as one replayed HIP graph (SGN_TRAIN_GRAPH=0: eager)
         self.use_graph = os.environ.get("SGN_TRAIN_GRAPH", "1") != "0"
+        # the losses and their gradients on the HIP loss stage (loss.hip; SGN_HIP_LOSS=0: torch autograd
+        # of train.composite_losses, the restatement it is tested against)
+        self.hip_loss = os.environ.get("SGN_HIP_LOSS", "1") != "0"
+        self.loss_stage = LossStage(self.device)
         self._graphs = {}        # (capacity bucket, buffers) -> captured loss stage, LRU order
         self.graph_captures = 0
         self._flat_maps = {}
@@ -495,7 +500,11 @@ class HipTrainer:
             validS[samp] = True
             qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
                   "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
-            total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, campos, rot, raydir, gt, o)
+            if self.hip_loss:
+                total, parts, full, ray_mask = self.loss_stage(self.points, qo, featS, campos, rot, gt, o, R)
+            else:
+                total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, campos, rot, raydir,
+                                                                gt, o)
             total.backward()
             if n > 0:
                 dfs = fs_t.grad.contiguous()
@@ -581,8 +590,11 @@ class HipTrainer:
         self.last_query = qd   # the step's sample-major query (tests rerun fp32 autograd on it)
         feat, _, mask = aggregate(P, self.mlp, campos.reshape(1, 3), rot, raydir, qd["samp_ray"], qd["samp_locw"],
                                   qd["pidx"], saved=self._z32)
-        total, parts, full, ray_mask = composite_losses(P, qd, feat, mask.sum(-1) > 0, campos, rot, raydir,
-                                                        gt.reshape(-1, 3).to(dev, torch.float32), o)
+        if self.hip_loss:
+            total, parts, full, ray_mask = self.loss_stage(P, qo, feat, campos, rot, gt, o, R)
+        else:
+            total, parts, full, ray_mask = composite_losses(P, qd, feat, mask.sum(-1) > 0, campos, rot, raydir,
+                                                            gt.reshape(-1, 3).to(dev, torch.float32), o)
         total.backward()
         self.allreduce_grads([self.mlp.flat])
         if dp:
@@ -620,8 +632,12 @@ class HipTrainer:
         validS = torch.zeros(Sc + 1, dtype=torch.bool, device=dev).index_put((samp,), st["true"])[:Sc]
         qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:Sc],
               "samp_locw": q.samp_locw[:Sc * 3].view(Sc, 3), "pidx": q.pidx[:Sc * o.K].view(Sc, o.K)}
-        total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, st["campos"], st["rot"],
-                                                        st["raydir"], st["gt"], o, s_count=q.counters[0])
+        if self.hip_loss:
+            total, parts, full, ray_mask = self.loss_stage(self.points, st["qabi"], featS, st["campos"], st["rot"],
+                                                           st["gt"], o, R)
+        else:
+            total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, st["campos"], st["rot"],
+                                                            st["raydir"], st["gt"], o, s_count=q.counters[0])
         total.backward()
         with torch.no_grad():
             fl.grad[c0:c1].add_(cw.grad)
@@ -649,7 +665,7 @@ class HipTrainer:
             self.graph_captures += 1
             if len(self._graphs) >= GRAPH_CACHE:
                 self._graphs.pop(next(iter(self._graphs)))
-            st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "ar": torch.arange(Sc, device=dev),
+            st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "qabi": q.abi(), "ar": torch.arange(Sc, device=dev),
                   "true": torch.ones((), dtype=torch.bool, device=dev),
                   "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
                   "campos": campos.clone(), "rot": rot.clone(),
