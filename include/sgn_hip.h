@@ -239,6 +239,11 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
 int sgn_aggregate_check_f32(const void *d_workspace, size_t workspace_bytes, sgn_stream_t stream);
 size_t sgn_aggregate_flag_offset_f32(size_t workspace_bytes);
 
+/* sgn_point_project_f32 for the points d_idx[0 .. *d_count) only (int32 indices < n_points; the
+ * count is a device int64): a training step re-projects the rows its rays touch after each weight
+ * update instead of all N.  The other points' P rows and records are left as they are. */
+int sgn_point_project_f32_subset(const sgn_point_tables *pt, const void *d_packed, const int32_t *d_idx,
+                                 const int64_t *d_count, void *d_proj, sgn_stream_t stream);
 /* fp32-faithful training forward (SURVEY §8 f1 at the reference's arithmetic): stage 1 of
  * sgn_aggregate_f32 for the base viewmlp that also writes the pre-activations of block1.0, block1.2
  * and block3.0 (2^-s (W x + b), before LeakyReLU) as fp32 [S_capacity * 8][256] at row s * 8 + k

@@ -118,6 +118,7 @@ SIGNATURES = {
     "sgn_mlp_pack_f32_host": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp]),
     "sgn_point_proj_bytes_f32": (c_sz, [c_i64]),
     "sgn_point_project_f32": (c_i32, [ctypes.POINTER(PointTables), c_vp, c_vp, c_vp]),
+    "sgn_point_project_f32_subset": (c_i32, [ctypes.POINTER(PointTables), c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_aggregate_workspace_bytes_f32": (c_sz, [c_i64]),
     "sgn_aggregate_f32": (c_i32, [c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),

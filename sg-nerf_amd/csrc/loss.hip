@@ -11,11 +11,11 @@
 //                     the dense [R'', SR, K] neighbour tensor of point_aggregators.py:951-958, empty
 //                     entries reading conf at the clamped index 0, neural_points.py:956-967)
 // Three launches, no host synchronisation (graph-capturable):
-//   k_loss_fwd     one thread per ray: composite, per-slot (T, e, dist) kept in the workspace,
+//   k_loss_fwd     8 lanes per ray: composite, per-slot (T, e, dist) kept in the workspace,
 //                  block partial sums of the loss terms (fixed order)
 //   k_loss_reduce  one workgroup: the partials in block order -> the four losses and the
 //                  gradient scales (the valid-ray count is only known here)
-//   k_loss_bwd     one thread per ray: reverse pass over the slots -> d feat per sample;
+//   k_loss_bwd     8 lanes per ray: reverse pass over the slots -> d feat per sample;
 //                  zero-one gradients added into d conf (atomics; a ray's empty entries as one add)
 #include "sgn_common.h"
 
@@ -23,6 +23,8 @@ namespace sgn {
 namespace {
 
 constexpr int LOSS_TPB = 256;
+constexpr int LPR = 8;  // lanes per ray: the slot walk runs on all 8 (same values), the SR x K zero-one
+                        // entries are split over them by neighbour k
 constexpr int LOSS_NSUM = 5;  // masked se, missed se, all se, zero-one sum, valid rays
 
 struct LossArgs {
@@ -59,7 +61,7 @@ __device__ __forceinline__ void zero_one(float cd, float eps, float &term, float
 // Per ray forward: slot s of the ray (s < ns: sample soff + s; later slots are padding at the
 // origin's depth) closes slot s - 1's interval (running cummax of pers z).
 template <bool STORE>
-__device__ void ray_forward(const LossArgs &a, int64_t r, float (&col)[3], float &T, bool &any_valid) {
+__device__ void ray_forward(const LossArgs &a, int64_t r, bool store, float (&col)[3], float &T, bool &any_valid) {
     const int ns = a.ray_ns[r], off = a.ray_soff[r], SR = a.SR;
     const float z0 = pers_z(a.campos, a.rot, 0.f, 0.f, 0.f);
     float *ws = a.slot_ws + r * (int64_t)SR * 3;
@@ -81,7 +83,7 @@ __device__ void ray_forward(const LossArgs &a, int64_t r, float (&col)[3], float
         col[0] += pf.y * wgt;
         col[1] += pf.z * wgt;
         col[2] += pf.w * wgt;
-        if (STORE) {
+        if (STORE && store) {
             ws[3 * slot + 0] = T;
             ws[3 * slot + 1] = e;
             ws[3 * slot + 2] = dist;
@@ -122,34 +124,39 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
 
 __global__ __launch_bounds__(LOSS_TPB) void k_loss_fwd(LossArgs a) {
     __shared__ float red[LOSS_TPB / 64];
-    const int64_t r = (int64_t)blockIdx.x * LOSS_TPB + threadIdx.x;
+    const int64_t r = ((int64_t)blockIdx.x * LOSS_TPB + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
     float v[LOSS_NSUM] = {0.f, 0.f, 0.f, 0.f, 0.f};
     if (r < a.R) {
         float col[3], T;
         bool any;
-        ray_forward<true>(a, r, col, T, any);
+        ray_forward<true>(a, r, sub == 0, col, T, any);
         const float bg[3] = {a.bg0, a.bg1, a.bg2};
         float se = 0.f;
         for (int c = 0; c < 3; ++c) {
             const float full = any ? col[c] + bg[c] * T : bg[c];
-            a.out_rgb[r * 3 + c] = full;
+            if (sub == 0) a.out_rgb[r * 3 + c] = full;
             const float d = full - a.gt[r * 3 + c];
             se += d * d;
         }
-        a.out_mask[r] = any ? 1 : 0;
-        v[0] = any ? se : 0.f;
-        v[1] = any ? 0.f : se;
-        v[2] = se;
-        v[4] = any ? 1.f : 0.f;
-        if (any) {  // zero-one terms over the ray's SR x K entries
+        if (sub == 0) {
+            a.out_mask[r] = any ? 1 : 0;
+            v[0] = any ? se : 0.f;
+            v[1] = any ? 0.f : se;
+            v[2] = se;
+            v[4] = any ? 1.f : 0.f;
+        }
+        if (any) {  // zero-one terms over the ray's SR x K entries, neighbour k = sub, sub + 8, ..
             const int ns = a.ray_ns[r], off = a.ray_soff[r];
+            const int nv = ns < a.SR ? ns : a.SR;
             float t0, d0;
             zero_one(a.conf[0], a.zo_eps, t0, d0);
             float zs = 0.f;
-            int n_empty = (a.SR - (ns < a.SR ? ns : a.SR)) * a.K;
-            for (int s = 0; s < ns && s < a.SR; ++s)
-                for (int k = 0; k < a.K; ++k) {
-                    const int p = a.pidx[(int64_t)(off + s) * a.K + k];
+            int n_empty = 0;
+            for (int k = sub; k < a.K; k += LPR) {
+                n_empty += a.SR - nv;
+                for (int s2 = 0; s2 < nv; ++s2) {
+                    const int p = a.pidx[(int64_t)(off + s2) * a.K + k];
                     if (p < 0) {
                         ++n_empty;
                         continue;
@@ -158,6 +165,7 @@ __global__ __launch_bounds__(LOSS_TPB) void k_loss_fwd(LossArgs a) {
                     zero_one(a.conf[p], a.zo_eps, t, d);
                     zs += t;
                 }
+            }
             v[3] = zs + (float)n_empty * t0;
         }
     }
@@ -190,47 +198,52 @@ __global__ __launch_bounds__(LOSS_TPB) void k_loss_reduce(LossArgs a, int nblock
 }
 
 __global__ __launch_bounds__(LOSS_TPB) void k_loss_bwd(LossArgs a) {
-    const int64_t r = (int64_t)blockIdx.x * LOSS_TPB + threadIdx.x;
+    const int64_t r = ((int64_t)blockIdx.x * LOSS_TPB + threadIdx.x) / LPR;
+    const int sub = threadIdx.x % LPR;
     if (r >= a.R) return;
     const int ns = a.ray_ns[r], off = a.ray_soff[r], SR = a.SR;
     const int nv = ns < SR ? ns : SR;
     if (!a.out_mask[r]) {  // fill_invalid: the background colour carries no gradient
-        for (int s = 0; s < nv; ++s) *(float4 *)(a.dfeat + (int64_t)(off + s) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s = sub; s < nv; s += LPR)
+            *(float4 *)(a.dfeat + (int64_t)(off + s) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
     }
-    const float gs = a.sums[4];
-    float g[3];
-    for (int c = 0; c < 3; ++c) g[c] = gs * (a.out_rgb[r * 3 + c] - a.gt[r * 3 + c]);
-    const float *ws = a.slot_ws + r * (int64_t)SR * 3;
-    // T after every slot (the padding slots' factors are exactly 1): recomputed from the last slot
-    float Tend = 1.f;
-    if (nv > 0) {
-        const float Tl = ws[3 * (nv - 1)], el = ws[3 * (nv - 1) + 1];
-        Tend = Tl * (1.f - (1.f - el) + 1e-10f);
+    if (sub == 0) {  // reverse pass over the slots (one lane of the ray)
+        const float gs = a.sums[4];
+        float g[3];
+        for (int c = 0; c < 3; ++c) g[c] = gs * (a.out_rgb[r * 3 + c] - a.gt[r * 3 + c]);
+        const float *ws = a.slot_ws + r * (int64_t)SR * 3;
+        // T after every slot (the padding slots' factors are exactly 1): from the last slot
+        float Tend = 1.f;
+        if (nv > 0) {
+            const float Tl = ws[3 * (nv - 1)], el = ws[3 * (nv - 1) + 1];
+            Tend = Tl * (1.f - (1.f - el) + 1e-10f);
+        }
+        // U = sum over later slots of g . c_i o_i T_i + g . bg T_end (d L / d a_s times a_s), from the end
+        float U = (g[0] * a.bg0 + g[1] * a.bg1 + g[2] * a.bg2) * Tend;
+        for (int s = nv - 1; s >= 0; --s) {
+            const int64_t id = off + s;
+            const float T = ws[3 * s], e = ws[3 * s + 1], dist = ws[3 * s + 2];
+            const float4 f = *(const float4 *)(a.feat + id * 4);
+            const float o = 1.f - e;
+            const float gc = g[0] * f.y + g[1] * f.z + g[2] * f.w;
+            const float av = 1.f - o + 1e-10f;
+            const float dO = gc * T - U / av;               // d L / d o_s
+            const bool v = a.samp_nnb[id] > 0;
+            const float dsig = dO * e * dist;              // o = 1 - exp(-sigma dist)
+            const float w = o * T;
+            *(float4 *)(a.dfeat + id * 4) = make_float4(v ? dsig : 0.f, g[0] * w, g[1] * w, g[2] * w);
+            U += gc * w;
+        }
     }
-    // U = d L / d T-suffix: sum over later slots of g . c_i o_i T_i + g . bg T_end, built from the end
-    float U = (g[0] * a.bg0 + g[1] * a.bg1 + g[2] * a.bg2) * Tend;
-    for (int s = nv - 1; s >= 0; --s) {
-        const int64_t id = off + s;
-        const float T = ws[3 * s], e = ws[3 * s + 1], dist = ws[3 * s + 2];
-        const float4 f = *(const float4 *)(a.feat + id * 4);
-        const float o = 1.f - e;
-        const float gc = g[0] * f.y + g[1] * f.z + g[2] * f.w;
-        const float av = 1.f - o + 1e-10f;
-        const float dO = gc * T - U / av;               // d L / d o_s
-        const bool v = a.samp_nnb[id] > 0;
-        const float dsig = dO * e * dist;              // o = 1 - exp(-sigma dist)
-        const float w = o * T;
-        *(float4 *)(a.dfeat + id * 4) = make_float4(v ? dsig : 0.f, g[0] * w, g[1] * w, g[2] * w);
-        U += gc * w;
-    }
-    // zero-one gradients
+    // zero-one gradients, neighbour k = sub, sub + 8, ..; the empty entries all read conf[0]
     const float gz = a.sums[5];
     float t0, d0;
     zero_one(a.conf[0], a.zo_eps, t0, d0);
-    int n_empty = (SR - nv) * a.K;
-    for (int s = 0; s < nv; ++s)
-        for (int k = 0; k < a.K; ++k) {
+    int n_empty = 0;
+    for (int k = sub; k < a.K; k += LPR) {
+        n_empty += SR - nv;
+        for (int s = 0; s < nv; ++s) {
             const int p = a.pidx[(int64_t)(off + s) * a.K + k];
             if (p < 0) {
                 ++n_empty;
@@ -240,6 +253,7 @@ __global__ __launch_bounds__(LOSS_TPB) void k_loss_bwd(LossArgs a) {
             zero_one(a.conf[p], a.zo_eps, t, d);
             if (d != 0.f) atomicAdd(a.dconf + p, gz * d);
         }
+    }
     if (n_empty > 0 && d0 != 0.f) atomicAdd(a.dconf, gz * d0 * (float)n_empty);
 }
 
@@ -250,7 +264,7 @@ extern "C" {
 
 size_t sgn_loss_workspace_bytes(int64_t R, int32_t SR) {
     if (R < 0 || SR <= 0) return 0;
-    const int64_t nb = (R + sgn::LOSS_TPB - 1) / sgn::LOSS_TPB;
+    const int64_t nb = (R * sgn::LPR + sgn::LOSS_TPB - 1) / sgn::LOSS_TPB;
     return (size_t)(R * SR * 3 * 4 + (nb + 1) * sgn::LOSS_NSUM * 4 + 64);
 }
 
@@ -268,7 +282,7 @@ int sgn_loss_train(const sgn_loss_params *lp, const float *d_campos, const float
     SGN_REQUIRE(((uintptr_t)d_feat & 15) == 0 && ((uintptr_t)d_dfeat & 15) == 0 && ((uintptr_t)d_workspace & 15) == 0,
                 "16-byte alignment required");
     hipStream_t st = as_stream(stream);
-    const int64_t nb = (R + LOSS_TPB - 1) / LOSS_TPB;
+    const int64_t nb = (R * LPR + LOSS_TPB - 1) / LOSS_TPB;
     LossArgs a{};
     a.campos = d_campos; a.rot = d_camrotc2w;
     a.ray_ns = q->ray_ns; a.ray_soff = q->ray_soff; a.samp_nnb = q->samp_nnb; a.pidx = q->pidx;

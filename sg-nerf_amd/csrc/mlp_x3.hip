@@ -478,6 +478,8 @@ struct Proj16Args {
     float *proj;
     const float *xyz, *color, *dir, *conf;
     float *rec;  // [n][16] packed point records (AggArgs::rec), after P in the projection buffer
+    const int32_t *idx;    // optional: project only points idx[0 .. *n_dev) (a training step's touched rows)
+    const int64_t *n_dev;  // device count of idx (<= n)
 };
 constexpr int REC16_FLOATS = 16;
 constexpr int Y_LDS_OFF = NSLOT * SLOT;
@@ -496,13 +498,15 @@ __global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
     __syncthreads();
     int slot = 0;
     dma_chunk<NetProj16, 0, NW16>(wb, lds, w, lane, 0);
-    const int64_t ntile = (a.n + 16 * NW16 - 1) / (16 * NW16);
+    const int64_t n = a.idx ? min(*a.n_dev, a.n) : a.n;
+    const int64_t ntile = (n + 16 * NW16 - 1) / (16 * NW16);
     for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
         int lz = 0;
         asm volatile("" : "+s"(lz));
         const float *Yl = (const float *)(lds + lz + Y_LDS_OFF);
-        const int64_t p = tile * (16 * NW16) + w * 16 + (lane & 15);
-        const bool ok = p < a.n;
+        const int64_t j = tile * (16 * NW16) + w * 16 + (lane & 15);
+        const bool ok = j < n;
+        const int64_t p = a.idx ? (ok ? (int64_t)a.idx[j] : 0) : j;
         // lane group g owns features 8 g .. 8 g + 7: k-step 0 slot j = feat[8 g + j]; k-step S >= 1
         // slot j = PE channel q = 8 (S - 1) + j of those features (feature 8 g + q / 6, frequency
         // (q % 6) / 2, sin / cos for even / odd q) -- col_proj16 maps it to the reference column
@@ -1597,6 +1601,25 @@ int sgn_mlp_pack_f32_host(int32_t bpnet_layers, int32_t bpnet_dim, const float *
     return 0;
 }
 
+int sgn_point_project_f32_subset(const sgn_point_tables *pt, const void *d_packed, const int32_t *d_idx,
+                                 const int64_t *d_count, void *d_proj, sgn_stream_t stream) {
+    using namespace sgn;
+    SGN_REQUIRE(pt && d_packed && d_proj && d_idx && d_count, "null argument");
+    SGN_REQUIRE(pt->n_points >= 0 && (pt->n_points == 0 || pt->embedding), "embedding required");
+    SGN_REQUIRE(((uintptr_t)d_proj & 15) == 0 && ((uintptr_t)pt->embedding & 15) == 0, "16-byte alignment required");
+    if (pt->n_points == 0) return 0;
+    SGN_REQUIRE(pt->xyz && pt->color && pt->dir && pt->conf, "point tables (xyz, color, dir, conf) required");
+    float *rec = (float *)((char *)d_proj + (size_t)pt->n_points * x3::PROJ_BYTES_PER_POINT);
+    x3::Proj16Args a{pt->embedding, pt->n_points, d_packed, (float *)d_proj, pt->xyz, pt->color, pt->dir,
+                     pt->conf, rec, d_idx, d_count};
+    // persistent grid over the device count (a training step touches ~50 k of 1.2 M points)
+    const int64_t tiles = (pt->n_points + 16 * x3::NW16 - 1) / (16 * x3::NW16);
+    hipLaunchKernelGGL(x3::k_point_proj16, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB16), 0,
+                       as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
 size_t sgn_point_proj_bytes_f32(int64_t n_points) {
     // P rows, then the packed 64-B point records
     return (size_t)(n_points > 0 ? n_points : 0) * (sgn::x3::PROJ_BYTES_PER_POINT + sgn::x3::REC16_FLOATS * 4);
@@ -1611,7 +1634,7 @@ int sgn_point_project_f32(const sgn_point_tables *pt, const void *d_packed, void
     SGN_REQUIRE(pt->xyz && pt->color && pt->dir && pt->conf, "point tables (xyz, color, dir, conf) required");
     float *rec = (float *)((char *)d_proj + (size_t)pt->n_points * x3::PROJ_BYTES_PER_POINT);
     x3::Proj16Args a{pt->embedding, pt->n_points, d_packed, (float *)d_proj, pt->xyz, pt->color, pt->dir,
-                     pt->conf, rec};
+                     pt->conf, rec, nullptr, nullptr};
     const int64_t tiles = (pt->n_points + 16 * x3::NW16 - 1) / (16 * x3::NW16);
     hipLaunchKernelGGL(x3::k_point_proj16, dim3((unsigned)(tiles < 256 ? tiles : 256)), dim3(x3::TPB16), 0,
                        as_stream(stream), a);

@@ -26,6 +26,7 @@ takes a query result (sample-major) so the same code runs on CPU with the oracle
 the parity tests.
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -112,7 +113,7 @@ class _SavedLinear(torch.autograd.Function):
         return gz @ w, _dw_rows(gz, x), gz.sum(0), None
 
 
-DW_CHUNK_F32 = 1024
+DW_CHUNK_F32 = int(os.environ.get("SGN_DW_CHUNK_F32", "4096"))  # rows per split-K batch (0: one plain GEMM)
 
 
 class _LinearRows(torch.autograd.Function):
@@ -134,7 +135,7 @@ def _dw_rows(gz, x, chunk=DW_CHUNK_F32):
     GEMM, the partials summed (a [256 x C] output of a plain GEMM with K = tens of thousands of rows
     occupies a handful of CUs), a ragged tail of rows as one more GEMM."""
     rows = gz.shape[0]
-    nb = rows // chunk
+    nb = rows // chunk if chunk > 0 else 0
     if nb <= 1:
         return gz.t() @ x
     body = nb * chunk
