@@ -414,6 +414,24 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
     return res
 
 
+def _query_counter(query_ms, key, path=os.path.join(ROOT, "profiles", "traffic_query_latest.json")):
+    """Counter bytes per launch of k_knn27 / k_march (profiles/traffic_query_latest.json, written from
+    the PMC summary of the same workload) and their rate over this run's query-stage time."""
+    try:
+        tj = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if tj.get("workload_key") != key:
+        return None
+    ks = tj.get("kernels", {})
+    b = sum(v["bytes_per_launch"] for v in ks.values())
+    return {"bytes_per_frame": b, "GBps_over_query_stage": b / (query_ms * 1e-3) / 1e9,
+            "frac_of_hbm_peak": b / (query_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+            "per_kernel": {k: {"bytes_per_launch": v["bytes_per_launch"], "l2_hit_rate": v.get("l2_hit_rate"),
+                               "counter_GBps_at_profiled_duration": v.get("counter_GBps")} for k, v in ks.items()},
+            "source": tj.get("source")}
+
+
 def main():
     args = parse()
     lego = args.scene == "lego"
@@ -514,6 +532,9 @@ def main():
             "effective_GBps_no_reuse_credit": h["q_bytes"] / (stage_ms["query"] * 1e-3) / 1e9,
             "hbm_peak_GBps": PEAK_HBM_GBS,
             "bytes_per_frame_no_reuse_credit": h["q_bytes"],
+            # HBM bytes of the query kernels from the PMC passes of the same workload (traffic file),
+            # over this run's query-stage time, beside the no-reuse model
+            "counter": _query_counter(stage_ms["query"], f"{args.h}x{args.w}x{args.sr}"),
         },
         "roofline_proj": {
             "kernel": ("k_point_proj16" if x3 else "k_point_proj") + " (block1.0 point inputs, all points, once per frame)",

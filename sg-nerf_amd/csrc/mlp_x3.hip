@@ -746,14 +746,17 @@ __global__ __launch_bounds__(PAIR_TPB) void k_pair_slots(const int32_t *__restri
     }
 }
 
-// the lane's row of slot `slot` (half of the wave), row kk of the half: rows table -> pidx index v
+// a row-table entry s * 8 + k -> the pidx index s * K + k of that neighbour
+__device__ __forceinline__ int64_t pidx_of(const AggArgs &a, int v) { return (int64_t)(v >> 3) * a.K + (v & 7); }
+
+// the lane's row of slot `slot` (half of the wave), row kk of the half: rows table -> pidx index
 __device__ __forceinline__ RowIdx row_index16(const AggArgs &a, int slot, int nslots, int kk) {
     RowIdx x;
     const int v = slot < nslots ? a.rows[(int64_t)slot * 8 + kk] : -1;
     x.sval = v >= 0;
     x.s = x.sval ? v >> 3 : 0;
     x.a = (v & 7) == kk;  // B rows sit nA rows after their k
-    x.pid = x.sval ? a.pidx[v] : -1;
+    x.pid = x.sval ? a.pidx[pidx_of(a, v)] : -1;
     x.ray = x.sval ? a.samp_ray[x.s] : 0;
     return x;
 }
@@ -1058,9 +1061,9 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         const bool waveB = (mrowB & 0xFFFFull) != 0;  // wave-uniform: a B sample in either half
         const Row16 rw = row_math16<PERS>(cam, rc, m, ix.a, sc ? nA1 : nA0, waveB);
         // SAVE: the row's pidx index s * 8 + k (from the slot's row table), -1 for rows without a neighbour
-        const int vrow = SAVE && ix.sval && m ? a.rows[(int64_t)hslot * 8 + kk] : -1;
+        const int64_t vrow = SAVE && ix.sval && m ? pidx_of(a, a.rows[(int64_t)hslot * 8 + kk]) : -1;
         if ((a.blend || a.wnorm) && ix.sval) {  // optional outputs: the row's pidx index from the table
-            const int v = a.rows[(int64_t)hslot * 8 + kk];
+            const int64_t v = pidx_of(a, a.rows[(int64_t)hslot * 8 + kk]);
             if (a.blend && g == 0) a.blend[v] = rw.wgt;
             if (a.wnorm && g == 1) a.wnorm[v] = rw.wn;
         }
@@ -1151,7 +1154,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
                 nx.sval = v_next >= 0;
                 nx.s = nx.sval ? v_next >> 3 : 0;
                 nx.a = (v_next & 7) == kk;
-                nx.pid = nx.sval ? a.pidx[v_next] : -1;
+                nx.pid = nx.sval ? a.pidx[pidx_of(a, v_next)] : -1;
                 nx.ray = nx.sval ? a.samp_ray[nx.s] : 0;
             }
         }, ts);
@@ -1675,7 +1678,7 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
     SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
     SGN_REQUIRE(bpnet_dim == 0 || (d_bpnet && ((uintptr_t)d_bpnet & 15) == 0),
                 "bpnet_dim > 0 needs the 16-byte aligned fp32 BPNet point embedding");
-    SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
+    SGN_REQUIRE(K >= 1 && K <= 8, "the fp32 MFMA aggregator takes K = 1 .. 8 neighbours per sample");
     SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir, "camera (campos, camrotc2w, raydir) required");
     SGN_REQUIRE((pt->pers == nullptr) == (pt->samp_pers == nullptr), "pers and samp_pers go together");
     SGN_REQUIRE(S_capacity >= 0 && S_capacity < (1 << 30), "S_capacity out of range");
@@ -1697,6 +1700,7 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
     a.pers = pt->pers; a.samp_pers = pt->samp_pers;
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
+    a.K = K;
     a.blob = d_packed; a.blob_bytes = x3::blob_bytes_sg(ksb);
     a.bpnet32 = d_bpnet;
     a.proj = (const _Float16 *)d_point_proj;  // fp32 P table (k_rows16 reads it as float)
@@ -1715,8 +1719,8 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
     const int32_t pair = !(pe && pe[0] == '0');
     if (stages & 1) {
         // a paired half writes only its samples' valid rows: the optional per-slot outputs start at 0
-        if (d_out_blend) SGN_CHECK_HIP(hipMemsetAsync(d_out_blend, 0, (size_t)S_capacity * 8 * 4, st));
-        if (d_out_wnorm) SGN_CHECK_HIP(hipMemsetAsync(d_out_wnorm, 0, (size_t)S_capacity * 8 * 4, st));
+        if (d_out_blend) SGN_CHECK_HIP(hipMemsetAsync(d_out_blend, 0, (size_t)S_capacity * K * 4, st));
+        if (d_out_wnorm) SGN_CHECK_HIP(hipMemsetAsync(d_out_wnorm, 0, (size_t)S_capacity * K * 4, st));
     }
     // the fp16-range flag covers the samples of this call's colour stage (cleared with its first chunk)
     if (stages & 2) SGN_CHECK_HIP(hipMemsetAsync(tail + 1, 0, 4, st));

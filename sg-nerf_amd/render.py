@@ -91,7 +91,7 @@ class HipRenderer:
             cap = max(R * SR, 1)
             dev = self.device
             self.feat = torch.empty(cap, 4, dtype=torch.float32, device=dev)
-            self.blend = torch.empty(cap, 8, dtype=torch.float32, device=dev)
+            self.blend = torch.empty(cap, self.opts.K, dtype=torch.float32, device=dev)
             L = _lib.lib()
             nb = int(L.sgn_aggregate_workspace_bytes_f32(cap) if self.f32 else L.sgn_aggregate_workspace_bytes(cap))
             self.agg_ws = torch.empty(nb, dtype=torch.uint8, device=dev)
@@ -157,7 +157,7 @@ class HipRenderer:
         R = raydir.shape[0]
         self._buffers(R)
         if want_weights and self.wnorm is None:
-            self.wnorm = torch.empty(self._cap[1], 8, dtype=torch.float32, device=self.device)
+            self.wnorm = torch.empty(self._cap[1], o.K, dtype=torch.float32, device=self.device)
             self.blendw = torch.empty(max(self._cap[0], 1), o.SR, dtype=torch.float32, device=self.device)
         if want_weights:
             self.wnorm.zero_()

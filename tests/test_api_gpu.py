@@ -150,6 +150,37 @@ def test_point_aggregator_shuffled_mask(name, prec):
     np.testing.assert_allclose(weight[0].cpu().numpy(), want_w, atol=1e-5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("kk", [5, 3])
+@pytest.mark.parametrize("name", ["patch", "opq_patch"])
+def test_point_aggregator_fewer_neighbours(name, kk):
+    """PointAggregator with K < 8 (the reference's aggregator takes any K, point_aggregators.py:868-959):
+    the golden case's first kk neighbour slots, f32 against fp32 agg_ref.aggregate on the same kk
+    neighbours (decoded features 1e-5 relative above 1, weights as the K = 8 test)."""
+    import agg_ref
+    pts, mlp, case = _load(name)
+    agg = PointAggregator(mlp, HotPathOpts(SR=int(case["SR"]), K=kk, precision="f32"), DEV)
+    args = _gathered(pts, case)
+    R, SR, K = case["sample_pidx"].shape
+    for k, v in list(args.items()):
+        if torch.is_tensor(v) and v.dim() >= 4 and v.shape[1:4] == (R, SR, K):
+            args[k] = v[:, :, :, :kk].contiguous()
+    dec, valid, weight, conf = agg(**args)
+    pidx = torch.from_numpy(case["sample_pidx"][:, :, :kk].reshape(-1, kk).astype(np.int64))
+    rd = torch.from_numpy(case["raydir"][case["ray_mask"].astype(bool)].astype(np.float32))
+    samp_ray = torch.arange(R).repeat_interleave(SR)
+    locw = torch.from_numpy(case["sample_loc_w"].reshape(-1, 3).astype(np.float32))
+    tp = {k: torch.from_numpy(v) for k, v in pts.items()}
+    with torch.no_grad():
+        feat, w_ref = agg_ref.aggregate(tp, mlp, torch.from_numpy(case["campos"].astype(np.float32)),
+                                        torch.from_numpy(case["camrotc2w"].astype(np.float32)), rd, samp_ray, locw,
+                                        pidx)
+    ref = feat.reshape(R, SR, 4).numpy()
+    np.testing.assert_array_equal(valid[0].cpu().numpy(), (pidx >= 0).any(-1).reshape(R, SR).numpy())
+    err = (np.abs(dec[0].cpu().numpy() - ref) / np.maximum(1.0, np.abs(ref))).max()
+    print(f"{name} K={kk}: PointAggregator max |decoded - agg_ref| / max(1, |ref|) = {err:.3e}")
+    assert err <= F32_TOL
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_ray_march_matches_reference(name):
     _, _, case = _load(name)

@@ -115,6 +115,35 @@ def test_render_matches_oracle_room(SR, seed, yaw, alpha_bias, prec):
     assert int(mask.sum()) > 0.5 * mask.numel()
 
 
+@pytest.mark.parametrize("K,alpha_bias", [(4, 0.0), (4, 150.0), (1, 0.0)])
+def test_render_matches_oracle_room_small_k(K, alpha_bias):
+    """K < 8 neighbours per sample (PointAggregator takes any K, point_aggregators.py:868-959; the
+    query supports 1 / 4 / 8 / 16) on the fp32 path: rows of a sample are its K slots, pidx
+    index s * K + k.  Same bars as K = 8, plus the per-slot blend weights against the oracle's."""
+    pc = small_room(300_000, seed=5)
+    o = HotPathOpts(SR=32, K=K, precision="f32")
+    mlp = init_mlp(5, bias_std=0.01)
+    mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + alpha_bias
+    view = make_view(48, 64, yaw=60.0, pitch=-8.0)
+    pts = dict(xyz=pc.xyz, embedding=pc.embedding, color=pc.color, dir=pc.dir, conf=pc.conf)
+    r, out = _render(pts, mlp, view, o)
+    hy = hyper_for(pc, o)
+    q = oq.OracleGrid(pc.xyz, hy, o).query(view.campos, view.raydir, r.querier.depth_table(0.1, 8.0, 0)[0].cpu().numpy())
+    assert q["pidx"].shape[-1] == K
+    tp = {k: torch.from_numpy(v) for k, v in pts.items()}
+    with torch.no_grad():
+        full, mask, fd, opacity, bg_t = agg_ref.render(tp, mlp, torch.from_numpy(view.campos),
+                                                       torch.from_numpy(view.camrotc2w), torch.from_numpy(view.raydir),
+                                                       q, o.SR)
+    np.testing.assert_array_equal(out.ray_mask.cpu().numpy().astype(bool), mask.numpy())
+    err = np.abs(out.rgb.cpu().numpy() - full.numpy()).max()
+    dense = _dense_feat(out, view.raydir.shape[0], o.SR)[0]
+    ferr = (np.abs(dense - fd.numpy()) / np.maximum(1.0, np.abs(fd.numpy()))).max()
+    print(f"room K={K} alpha_bias={alpha_bias} [f32]: max |rgb - oracle| = {err:.3e}, max feature error {ferr:.3e}")
+    assert err <= F32_TOL and ferr <= F32_TOL
+    assert int(mask.sum()) > 0.5 * mask.numel()
+
+
 @pytest.mark.parametrize("theta,alpha_bias", [(30.0, 0.0), (200.0, 150.0)])
 def test_render_matches_oracle_lego(theta, alpha_bias):
     """BASELINE config 4 at test size: the NeRF-synthetic camera model
