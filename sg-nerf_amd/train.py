@@ -196,10 +196,11 @@ def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, 
     fs = torch.sum(hk.view(S, K, -1) * w[..., None], dim=1)
     a_s = torch.sum(ak.view(S, K, 1) * w[..., None], dim=1)
     c = torch.cat([fs, vpe], dim=-1)
-    c = lr_(mlp.f("color_branch.0", c))
-    c = lr_(mlp.f("color_branch.2", c))
-    c = lr_(mlp.f("color_branch.4", c))
-    c = torch.sigmoid(mlp.f("color_branch.6", c)) * (1 + 2 * 0.001) - 0.001
+    lin_r = lambda name, t: _LinearRows.apply(t, mlp.w(name), mlp.b(name))  # noqa: E731  (split-K dW)
+    c = lr_(lin_r("color_branch.0", c))
+    c = lr_(lin_r("color_branch.2", c))
+    c = lr_(lin_r("color_branch.4", c))
+    c = torch.sigmoid(lin_r("color_branch.6", c)) * (1 + 2 * 0.001) - 0.001
     feat = torch.cat([a_s, c], dim=-1) * valid[:, None]
     return feat, conf_coef, mask
 

@@ -34,8 +34,8 @@ import torch.nn.functional as F
 
 from . import _lib
 from .opts import HotPathOpts
-from .train import (PointParams, _allreduce_buckets, _allreduce_point_rows, _pe, composite_losses, gather_counts,
-                    touched_rows)
+from .train import (PointParams, _LinearRows, _allreduce_buckets, _allreduce_point_rows, _pe, composite_losses,
+                    gather_counts, touched_rows)
 from .loss_hip import LossStage
 from .weights import BPNET, LAYERS, layers_for, strip_prefix
 
@@ -432,7 +432,7 @@ class HipTrainer:
                 off, o, i = m.slices[name]
                 w = src[off - base:off - base + o * i].view(o, i)
                 b = src[off - base + o * i:off - base + o * i + o]
-            c = F.linear(c, w, b)
+            c = _LinearRows.apply(c, w, b)   # F.linear with a split-K weight gradient (K = the samples)
             if name != "color_branch.6":
                 c = F.leaky_relu(c, 0.01)
         return torch.sigmoid(c) * (1 + 2 * 0.001) - 0.001
