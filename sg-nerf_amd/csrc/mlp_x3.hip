@@ -220,12 +220,80 @@ __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int
 template <class Net, int N, int NWv = NW16>
 constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NWv - 1) / NWv; }
 
+// ---- counted weight ring (SGN_X3_RING, the row kernel): 4 slots, no workgroup barrier ------------
+// Chunk n of the stream (n counts across tiles) lives in slot n % 4; its pieces are issued during chunk
+// n - 2 (two ahead).  Per slot two LDS counters: FULL (+1 per wave once its pieces of the slot's
+// current chunk have landed, signalled at that wave's entry of the chunk before) and FREE (+1 per
+// wave once it has read the slot's chunk).  Entering chunk n waits for FULL = NW (u + 1) (u = n / 4,
+// the slot's fill count) and, before the chunk's pieces of n + 2 go into slot (n + 2) % 4, for that
+// slot's previous chunk n - 2 to be FREE on every wave -- so the waves of a workgroup may drift apart
+// by one chunk instead of meeting at every boundary.  Every wait is bounded (a wave that has spun
+// 2^14 times moves on and sets the error word, so a protocol bug can only produce wrong results,
+// never a hang).
+struct RingState {
+    int slot;          // slot of the chunk being entered
+    uint32_t n;        // its stream position
+    uint32_t *cnt;     // LDS: FULL[4] then FREE[4]
+};
+constexpr int RING_SLOTS = 4;
+__device__ __forceinline__ int cur_slot(int s) { return s; }
+__device__ __forceinline__ int cur_slot(const RingState &r) { return r.slot; }
+__device__ __forceinline__ int dma_slot(int s) { return s ^ 1; }
+__device__ __forceinline__ int dma_slot(const RingState &r) { return (r.slot + 2) & (RING_SLOTS - 1); }
+template <class T>
+struct RingAhead {
+    static constexpr int value = 1;  // chunks the DMA runs ahead of the reads
+};
+template <>
+struct RingAhead<RingState> {
+    static constexpr int value = 2;
+};
+__device__ __forceinline__ void ring_wait(uint32_t *c, uint32_t target, uint32_t *err) {
+    for (int it = 0; it < (1 << 14); ++it) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (v >= target) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (err) *err = 1u;
+}
+__device__ __forceinline__ void ring_add(uint32_t *c, int lane) {
+    if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void chunk_exit(int &s, int) { s ^= 1; }
+template <int NWv>
+__device__ __forceinline__ void chunk_exit_ring(RingState &r, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
+    ring_add(r.cnt + RING_SLOTS + r.slot, lane);
+    r.slot = (r.slot + 1) & (RING_SLOTS - 1);
+    ++r.n;
+}
+
 // chunk boundary: this wave's DMAs of chunk N landed, LDS reads drained, barrier; then chunk N+1
 // goes into the slot every wave finished reading one chunk ago (its pieces are spread over the
 // chunk's MFMAs by run_layer16)
 // VM: vector-memory operations this wave is guaranteed to have issued after its last DMA piece of
 // the chunk being entered (loads placed at the end of the previous chunk, stores): they may stay in
 // flight across the boundary (vmcnt retires in order, so the DMA has landed once at most VM remain)
+// counted ring: this wave's pieces of chunk n + 1 (issued during n - 1) landed -> FULL of its slot;
+// wait for chunk n FULL on every wave and for slot (n + 2) % 4 (chunk n - 2) FREE on every wave
+template <class Net, int N, int NWv = NW16, int VM = 0>
+__device__ __forceinline__ void chunk_enter(const WBlob &, char *, RingState &r, int, int lane, int,
+                                            TStamp *ts = nullptr) {
+    static_assert(VM >= 0 && VM < 64, "vmcnt range");
+    if constexpr (VM == 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+        __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
+    ring_add(r.cnt + ((r.slot + 1) & (RING_SLOTS - 1)), lane);
+    uint32_t *err = r.cnt + 2 * RING_SLOTS;
+    ring_wait(r.cnt + r.slot, (uint32_t)NWv * (r.n / RING_SLOTS + 1), err);
+    if (r.n >= 2) ring_wait(r.cnt + RING_SLOTS + ((r.slot + 2) & (RING_SLOTS - 1)), (uint32_t)NWv * ((r.n - 2) / RING_SLOTS + 1), err);
+#ifdef SGN_X3_TIMING
+    if (ts) (*ts)(lane);
+#else
+    (void)ts;
+#endif
+}
 template <class Net, int N, int NWv = NW16, int VM = 0>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz,
                                             TStamp *ts = nullptr) {
@@ -325,10 +393,14 @@ static_assert(N_Y32 % 4 == 0, "fp32 section in 16-B units");
 // of one chunk boundary no longer holds the other workgroup's wave of the SIMD: while one runs its
 // tile transition or epilogue VALU, the other's MFMAs keep the matrix pipe busy); or 8 waves with a
 // 2 x 64-KiB ring (one workgroup per CU, every wave in step)
-#ifndef SGN_X3_RW
-#define SGN_X3_RW 4
+#ifndef SGN_X3_RING
+#define SGN_X3_RING 0   // 1: 8 waves sharing a counted 4-slot ring of 16-pair chunks (RingState), no barrier
 #endif
-constexpr int NWR = SGN_X3_RW, SPR = NWR == 4 ? 16 : 32;  // row waves, ring slot pairs
+#ifndef SGN_X3_RW
+#define SGN_X3_RW (SGN_X3_RING ? 8 : 4)
+#endif
+constexpr int NWR = SGN_X3_RW, SPR = (NWR == 4 || SGN_X3_RING) ? 16 : 32;  // row waves, ring slot pairs
+constexpr int NSLR = SGN_X3_RING ? RING_SLOTS : NSLOT;                    // row ring slots
 static_assert(NWR == 4 || NWR == 8, "row workgroup: 4 or 8 waves");
 constexpr int KCR = SPR / 16;                             // k-steps of 16 tiles per chunk
 constexpr XL L3_16 = SGN_X3_SPLIT3 ? XL{8, 8, 2, 2 * KCR, OFF16_W3} : XL{8, 16, 1, KCR, OFF16_W3};
@@ -361,7 +433,7 @@ struct NetColor16 {
     static constexpr int NL = 3;
     static constexpr XL L[NL] = {{9, 8, 1, KCC, OFF16_C0}, {4, 8, 1, KCC, OFF16_C1}, {4, 8, 1, KCC, OFF16_C2}};
 };
-static_assert(NWR == 4 ? Sched<NetR16>::total() == 27 : Sched<NetR16>::total() == 14 && Sched<NetR16>::pairs(9) == 16,
+static_assert(SPR == 16 ? Sched<NetR16>::total() == 27 : Sched<NetR16>::total() == 14 && Sched<NetR16>::pairs(9) == 16,
               "16x16 row stream");
 static_assert(NWC == 4 ? Sched<NetColor16>::total() == 9 && Sched<NetColor16>::pairs(4) == 8
                        : Sched<NetColor16>::total() == 5 && Sched<NetColor16>::pairs(2) == 8, "16x16 colour stream");
@@ -375,9 +447,9 @@ __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
 // are the A operand (acc[t] holds D[row 4g+i][unit 16t + (l & 15)]).
 // mid(integral_constant F) runs after pair F's MFMAs of every chunk (F counted over the layer: k-step
 // K, tile t -> F = K TP + t), so per-pair VALU work of another stage can ride between the MFMAs.
-template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, class InFn, class PostFn = NoHook,
-          class EndFn = NoHook, class MidFn = NoHook>
-__device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz,
+template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, class SlotT, class InFn,
+          class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>
+__device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &slot, int w, int lane, int lz,
                                             f32x4 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{},
                                             TStamp *ts = nullptr, EndFn &&end = EndFn{}, MidFn &&mid = MidFn{}) {
     constexpr XL ly = Net::L[L];
@@ -385,13 +457,13 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slo
     static_assert((TP == 16 || TP == 8) && P < ly.np, "passes of 16 or 8 output tiles");
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
-        constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
+        constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + RingAhead<SlotT>::value) % Sched<Net>::total();
         constexpr int NWv = Net::NW, SLOTv = Net::SP * PAIR;
         static_assert(nk(ly, C) * TP <= Net::SP, "chunk larger than a ring slot");
         chunk_enter<Net, N, NWv, Vm::vm(C)>(wb, lds, slot, w, lane, lz, ts);
         post(cc);
-        const char *sl = lds + slot * SLOTv;
-        char *dnext = lds + (slot ^ 1) * SLOTv;
+        const char *sl = lds + cur_slot(slot) * SLOTv;
+        char *dnext = lds + dma_slot(slot) * SLOTv;
         constexpr int NF = nk(ly, C) * TP;
         constexpr int PW = dma_pieces<Net, NN, NWv>();
         auto frag = [&](int f, int part) { return *(const h8 *)(sl + (2 * f + part) * 1024 + lane * 16); };
@@ -449,7 +521,10 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, int &slo
         });
         __builtin_amdgcn_sched_barrier(0);
         end(cc);  // after every DMA piece of the chunk: loads here may stay in flight one boundary
-        slot ^= 1;
+        if constexpr (RingAhead<SlotT>::value == 2)
+            chunk_exit_ring<NWv>(slot, lane);
+        else
+            chunk_exit(slot, lane);
         __builtin_amdgcn_sched_barrier(0);
     });
 }
@@ -559,9 +634,10 @@ __global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
 // ---- per-neighbour rows (16x16) -------------------------------------------------------------
 constexpr int WG16_SAMPLES = NWR * 2;            // halves (16 rows, 2 per wave) per workgroup tile
 constexpr int TPBR = NWR * 64;
-constexpr int YR_OFF = NSLOT * SPR * PAIR;        // the row kernel's fp32 section, after its ring
+constexpr int YR_OFF = NSLR * SPR * PAIR;         // the row kernel's fp32 section, after its ring
 constexpr int YT16_OFF = YR_OFF + N_Y32 * 4;      // [unit r][20] 2^s3 b3 (t = 0..15) then [r][20] 2^-s3 alpha w
-constexpr int ROWS16_LDS = YT16_OFF + 2 * 16 * 20 * 4;
+constexpr int RINGCNT_OFF = YT16_OFF + 2 * 16 * 20 * 4;  // counted ring: FULL[4], FREE[4], error word
+constexpr int ROWS16_LDS = RINGCNT_OFF + (SGN_X3_RING ? 64 : 0);
 static_assert(ROWS16_LDS * (8 / NWR) <= 163840, "LDS budget (16x16 rows, 8 / NWR workgroups per CU)");
 
 // row r's point record, its sample position and view direction (+ the caller's pers
@@ -914,6 +990,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         const float *src = (const float *)((const char *)a.blob + OFF16_F32);
         float *dst = (float *)(lds + YR_OFF);
         for (int i = threadIdx.x; i < N_Y32; i += TPBR) dst[i] = src[i];
+        if (SGN_X3_RING && threadIdx.x < 16) ((uint32_t *)(lds + RINGCNT_OFF))[threadIdx.x] = 0u;
         {
             // row stride 20 floats: the 16 lanes' 16-B reads of one column quad hit disjoint banks
             float *yt = (float *)(lds + YT16_OFF);
@@ -924,8 +1001,16 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         }
     }
     __syncthreads();
+#if SGN_X3_RING
+    RingState slot{0, 0u, (uint32_t *)(lds + RINGCNT_OFF)};
+    dma_chunk<Net, 0, NWR>(wb, lds, w, lane, 0);
+    dma_chunk<Net, 1, NWR>(wb, lds + SPR * PAIR, w, lane, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ring_add(slot.cnt + 0, lane);  // chunk 0 landed (chunk 1 is signalled at chunk 0's entry)
+#else
     int slot = 0;
     dma_chunk<Net, 0, NWR>(wb, lds, w, lane, 0);
+#endif
     // The next tile's chain, prefetched inside the current tile so each step lands under MFMAs:
     // row-table entry (block1.2), neighbour / ray index (block3.0), point record + sample position
     // and the P row (block3.2).  First tile: here.

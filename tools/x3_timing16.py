@@ -6,9 +6,10 @@ import numpy as np
 
 EV = 2048
 RW = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+RING = len(sys.argv) > 3 and sys.argv[3] == "ring"   # SGN_X3_RING: 8 waves, 16-pair chunks
 TB, NW = (8, 8) if RW == 8 else (16, 4)   # the stamp buffer holds 64 waves (mlp_x3.hip TD_BLOCKS x NW16)
 d = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(TB, NW, EV).astype(np.int64)
-if RW == 8:   # 32-pair chunks: L0 1, L1 4, L2 4 + 1 of 16, L3 4
+if RW == 8 and not RING:   # 32-pair chunks: L0 1, L1 4, L2 4 + 1 of 16, L3 4
     ch = [("L0", 32)] + [(f"L1C{c}", 32) for c in range(4)] + [(f"L2C{c}", 32 if c < 4 else 16) for c in range(5)] + \
          [(f"L3C{c}", 32) for c in range(4)]
 else:         # 16-pair chunks: L0 2, L1 8, L2 9, L3 2 passes x 4

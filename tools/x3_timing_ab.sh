@@ -9,7 +9,7 @@ for v in "$@"; do
     n=$(basename $v .so)
     cp "$v" sg-nerf_amd/libsgn_hip.so
     SGN_X3_TDBG=$PWD/gpurun_out/t_$n.bin timeout -k 10 120 python tools/agg_time.py f32 2 > /dev/null 2>&1 || { echo "FAIL $n"; cp /tmp/base.so sg-nerf_amd/libsgn_hip.so; exit 1; }
-    echo "== $n"; python tools/x3_timing16.py gpurun_out/t_$n.bin
+    echo "== $n"; python tools/x3_timing16.py gpurun_out/t_$n.bin ${TIMING_ARGS:-}
 done
 cp /tmp/base.so sg-nerf_amd/libsgn_hip.so
 echo TIMING_DONE
