@@ -249,6 +249,12 @@ struct RingAhead<RingState> {
     static constexpr int value = 2;
 };
 __device__ __forceinline__ void ring_wait(uint32_t *c, uint32_t target, uint32_t *err) {
+#ifdef SGN_X3_ABLATE_RINGWAIT  // timing experiment only: the counters are read but never waited on
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0xFFFFFFFFu &&
+        err)
+        *err = target;
+    return;
+#endif
     for (int it = 0; it < (1 << 14); ++it) {
         const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (v >= target) return;
