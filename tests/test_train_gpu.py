@@ -244,7 +244,8 @@ def test_model_plugin_training_surface(tmp_path):
     before = m.test()["coarse_raycolor"].clone()
     # reference step: HipTrainer on the same batch, same jitter seed
     tr = HipTrainer(PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV), mlp,
-                    dataclasses.replace(O, is_train=1), DEV)
+                    dataclasses.replace(O, is_train=1), DEV, precision="f32")   # the plugin's default arithmetic
+    assert m.trainer.precision == "f32"
     torch.manual_seed(11)
     parts_ref, _, _ = tr.step(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV))
     torch.manual_seed(11)
