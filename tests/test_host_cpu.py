@@ -80,6 +80,24 @@ def test_argument_errors_are_reported_without_gpu():
     assert rc != 0 and b"256" in L.sgn_last_error()
     rc = L.sgn_colsum_f16(9, xs, 100, 256, fake, fake, None)
     assert rc != 0 and b"count" in L.sgn_last_error()
+    # fp32 aggregator: K = 1 .. 8 (the row table names pidx index s * K + k)
+    rc = L.sgn_aggregate_f32(0, 0, None, fake, ctypes.byref(pt), ctypes.byref(qo), 64, 16, fake, fake, None, None,
+                             fake, 1 << 20, 3, None)
+    assert rc != 0 and b"K = 1 .. 8" in L.sgn_last_error()
+    rc = L.sgn_point_project_f32_subset(ctypes.byref(pt), fake, None, fake, fake, None)
+    assert rc != 0 and b"null" in L.sgn_last_error()
+    # training loss stage: null pointers, SR / K, the workspace size
+    lp = _lib.LossParams()
+    lp.SR, lp.K = 24, 8
+    args = (fake, fake, 64, ctypes.byref(qo), fake, fake, fake, fake, fake, fake, fake, fake)
+    rc = L.sgn_loss_train(ctypes.byref(lp), *args, fake, 16, None)
+    assert rc != 0 and b"workspace" in L.sgn_last_error()
+    assert L.sgn_loss_workspace_bytes(64, 24) >= 64 * 24 * 12
+    rc = L.sgn_loss_train(ctypes.byref(lp), *args, None, 1 << 20, None)
+    assert rc != 0 and b"null" in L.sgn_last_error()
+    lp.K = 0
+    rc = L.sgn_loss_train(ctypes.byref(lp), *args, fake, 1 << 20, None)
+    assert rc != 0 and b"positive" in L.sgn_last_error()
 
 
 # ---- options ------------------------------------------------------------------------
