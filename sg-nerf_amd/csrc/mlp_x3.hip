@@ -111,7 +111,7 @@ __device__ __forceinline__ X3B split8(const float (&v)[8]) {
 // t -> (hi, lo) of x = t * inv (inv a power of two, so x is exact): hi = fp16(x), lo = fp16(x - hi), each
 // half written by one v_fma_mix{lo,hi}_f16 (fp32 FMA, rounded once to fp16): 4 instructions per 2
 // values instead of a multiply each, a pack and the two fma_mix + pack of split8 -- the same bits
-__device__ __forceinline__ X3B split8s(const float (&t)[8], float inv) {
+[[maybe_unused]] __device__ __forceinline__ X3B split8s(const float (&t)[8], float inv) {
     u32x4 hi, lo;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
