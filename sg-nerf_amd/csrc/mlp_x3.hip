@@ -237,18 +237,18 @@ struct RingState {
 };
 constexpr int RING_SLOTS = 4;
 __device__ __forceinline__ int cur_slot(int s) { return s; }
-__device__ __forceinline__ int cur_slot(const RingState &r) { return r.slot; }
+[[maybe_unused]] __device__ __forceinline__ int cur_slot(const RingState &r) { return r.slot; }
 __device__ __forceinline__ int dma_slot(int s) { return s ^ 1; }
-__device__ __forceinline__ int dma_slot(const RingState &r) { return (r.slot + 2) & (RING_SLOTS - 1); }
+[[maybe_unused]] __device__ __forceinline__ int dma_slot(const RingState &r) { return (r.slot + 2) & (RING_SLOTS - 1); }
 template <class T>
 struct RingAhead {
     static constexpr int value = 1;  // chunks the DMA runs ahead of the reads
 };
 template <>
 struct RingAhead<RingState> {
-    static constexpr int value = 2;
+    [[maybe_unused]] static constexpr int value = 2;
 };
-__device__ __forceinline__ void ring_wait(uint32_t *c, uint32_t target, uint32_t *err) {
+[[maybe_unused]] __device__ __forceinline__ void ring_wait(uint32_t *c, uint32_t target, uint32_t *err) {
 #ifdef SGN_X3_ABLATE_RINGWAIT  // timing experiment only: the counters are read but never waited on
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0xFFFFFFFFu &&
         err)
@@ -262,7 +262,7 @@ __device__ __forceinline__ void ring_wait(uint32_t *c, uint32_t target, uint32_t
     }
     if (err) *err = 1u;
 }
-__device__ __forceinline__ void ring_add(uint32_t *c, int lane) {
+[[maybe_unused]] __device__ __forceinline__ void ring_add(uint32_t *c, int lane) {
     if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void chunk_exit(int &s, int) { s ^= 1; }
