@@ -174,6 +174,39 @@ def test_f32_training_matches_fp32_autograd_on_same_query(cfg):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("K", [4, 1])
+def test_f32_training_small_k_matches_fp32_autograd(K):
+    """precision "f32" with K < 8 neighbours per sample (saved pre-activations at pidx index
+    s * K + k): every gradient within GRAD_TOL_F32 of train.Trainer's fp32 autograd on the very
+    samples the HIP query produced."""
+    o = dataclasses_replace(O, K=K)
+    pc, view, _, mlp, gt = _setup(seed=5)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    tr = HipTrainer(points, mlp, o, DEV, precision="f32")
+    parts, full, ray_mask = tr.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV))
+    qd = {k: v.long() if v.dtype == torch.int32 else v for k, v in tr.last_query.items()}
+    assert qd["pidx"].shape[1] == K
+    ref_points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    ref = Trainer(ref_points, mlp, o, DEV)
+    parts_c, full_c, mask_c = ref.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV),
+                                           q=qd)
+    torch.cuda.synchronize()
+    assert torch.equal(ray_mask, mask_c)
+    assert _rel(full, full_c) <= GRAD_TOL_F32
+    g = grads_named(tr)
+    worst = {}
+    for name, *_ in LAYERS:
+        m = ref.mlp.lin[name.replace(".", "_")]
+        worst[name + ".weight"] = _rel(g[name + ".weight"], m.weight.grad)
+        worst[name + ".bias"] = _rel(g[name + ".bias"], m.bias.grad)
+    for k in ("points_embeding", "points_color", "points_dir", "points_conf"):
+        worst[k] = _rel(g[k].reshape(getattr(ref_points, k).grad.shape), getattr(ref_points, k).grad)
+    print(f"K={K}: relative L2 gradient errors (same query):", {k: f"{v:.2e}" for k, v in worst.items()})
+    bad = {k: v for k, v in worst.items() if v > GRAD_TOL_F32}
+    assert not bad, bad
+
+
 def _config5():
     from sgnerf_amd import scene
     pc = scene.synth_room(1_200_000, seed=0)
