@@ -34,18 +34,19 @@ class _HipLoss(torch.autograd.Function):
 
 
 class LossStage:
-    """Reusable device buffers of the loss stage for one (R, SR, capacity) shape."""
+    """The loss stage with its reusable workspace."""
 
     def __init__(self, device):
         self.device = torch.device(device)
         self._key = None
 
-    def _buffers(self, R, SR, S_cap, n_points):
-        key = (R, SR, S_cap, n_points)
-        if key != self._key:
-            d = self.device
-            self.ws = torch.empty(max(int(_lib.lib().sgn_loss_workspace_bytes(R, SR)), 16), dtype=torch.uint8, device=d)
-            self._key = key
+    def _buffers(self, R, SR):
+        """The workspace grows, never moves to a smaller one (a captured graph keeps the pointer it
+        was captured with: HipTrainer gives every captured loss stage its own LossStage)."""
+        need = max(int(_lib.lib().sgn_loss_workspace_bytes(R, SR)), 16)
+        if self._key is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._key = (R, SR)
         return self.ws
 
     def __call__(self, points, q_abi, feat, campos, rot, gt, opts: HotPathOpts, R, bg=(1.0, 1.0, 1.0),
@@ -59,7 +60,7 @@ class LossStage:
         feat = feat.contiguous()
         if feat.shape[0] == 0:   # a batch without samples: one zero row keeps the pointers valid
             feat = torch.cat([feat, feat.new_zeros(1, 4)])
-        ws = self._buffers(R, opts.SR, feat.shape[0], n_points)
+        ws = self._buffers(R, opts.SR)
         campos = campos.reshape(3).to(dev, torch.float32).contiguous()
         rot = rot.reshape(3, 3).to(dev, torch.float32).contiguous()
         gt = gt.reshape(-1, 3).to(dev, torch.float32).contiguous()

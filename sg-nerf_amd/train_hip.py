@@ -645,8 +645,9 @@ class HipTrainer:
         qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:Sc],
               "samp_locw": q.samp_locw[:Sc * 3].view(Sc, 3), "pidx": q.pidx[:Sc * o.K].view(Sc, o.K)}
         if self.hip_loss:
-            total, parts, full, ray_mask = self.loss_stage(self.points, st["qabi"], featS, st["campos"], st["rot"],
-                                                           st["gt"], o, R)
+            # the graph's own loss stage: its workspace lives as long as the captured graph that uses it
+            total, parts, full, ray_mask = st["loss"](self.points, st["qabi"], featS, st["campos"], st["rot"],
+                                                      st["gt"], o, R)
         else:
             total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, st["campos"], st["rot"],
                                                             st["raydir"], st["gt"], o, s_count=q.counters[0])
@@ -677,7 +678,8 @@ class HipTrainer:
             self.graph_captures += 1
             if len(self._graphs) >= GRAPH_CACHE:
                 self._graphs.pop(next(iter(self._graphs)))
-            st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "qabi": q.abi(), "ar": torch.arange(Sc, device=dev),
+            st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "qabi": q.abi(), "loss": LossStage(dev),
+                  "ar": torch.arange(Sc, device=dev),
                   "true": torch.ones((), dtype=torch.bool, device=dev),
                   "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
                   "campos": campos.clone(), "rot": rot.clone(),
