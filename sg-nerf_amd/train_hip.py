@@ -11,8 +11,9 @@ are differentiated by torch on the device (they are small, per sample / per ray)
   query        sgn_query (jittered depths, is_train), indices carry no gradient
   forward      sgn_aggregate_train_fwd: blended features f_s (fp16) and alpha_s per sample,
                per-row layer inputs saved for the backward
-  colour+loss  torch: colour MLP on [f_s | PE(v)], ray_dist + ray_march, ray-masked MSE +
-               zero-one(conf) (train.composite_losses); backward -> d f_s, d alpha_s, colour grads
+  colour+loss  torch: colour MLP on [f_s | PE(v)] (autograd); the HIP loss stage (loss.hip via
+               loss_hip.LossStage): ray_dist + ray_march, ray-masked MSE + zero-one(conf) and their
+               gradients -> d f_s, d alpha_s, colour grads, d conf
   backward     sgn_aggregate_backward: deltas of the 4 row layers, d alpha-logit, point grads
                (embedding via PE(feat), colour, dir, conf through the straight-through clamp)
                with a power-of-two loss scale; dW = delta^T x per layer as fp16 GEMMs with fp32
@@ -22,6 +23,10 @@ are differentiated by torch on the device (they are small, per sample / per ray)
 
 MLP weights live in ONE flat fp32 parameter (LAYERS order), so the MFMA blobs are re-packed on
 the device every step by index gathers (sgn_mlp_pack_index / sgn_train_pack_index).
+
+precision "f32" (the reference's arithmetic): the fp32-faithful row kernel in save mode
+(k_rows16: block1.0 / 1.2 / 3.0 pre-activations per row) after re-projecting the touched points'
+P rows, then train.aggregate(saved=...) and fp32 autograd through the HIP loss stage.
 """
 import ctypes
 import os
