@@ -151,8 +151,9 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None, precision=
            "config": {"workload": f"synth-room, {args.train_rays} random rays per rank per step, SR=24, K=8, "
                                   f"{args.points} neural points, HIP query + "
                                   + ("torch autograd" if args.train_torch else
-                                     "HIP fp32-faithful row-MLP forward (k_rows16 save mode) + fp32 backward" if precision == "f32"
-                                     else "HIP MFMA row-MLP forward/backward + torch colour/composite autograd")
+                                     "HIP fp32-faithful row-MLP forward (k_rows16 save mode) + fp32 backward + HIP loss stage"
+                                     if precision == "f32"
+                                     else "HIP MFMA row-MLP forward/backward + torch colour-MLP autograd + HIP loss stage")
                                   + (" (SG-NeRF variant: semantic-guided kNN, block2_bpnet 352->256)" if args.sg else "")
                                   + " + RCCL all-reduce",
                       "parallelism": f"dp{world}"},

@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 7
+#define SGN_ABI_VERSION 8
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -107,6 +107,13 @@ typedef struct {
     int32_t *ray_ns, *ray_soff, *samp_ray, *samp_d, *samp_nnb, *pidx, *work, *counters;
     float *samp_locw;
 } sgn_query_out;
+
+/* Training-mode depth table (is_train: jittered linear depths), replacing the torch op sequence of
+ * near_far_linear_ray_generation (models/rendering/diff_ray_marching.py:349-393) after its
+ * torch.rand: d_rnd float[R*D] uniform [0, 1) in, d_t float[R*D] segment mid-point depths out
+ * (the reference's middle_point_ts; sgn_query's per_ray_t = 1 table). */
+int sgn_depth_table_jitter(float near, float far, int32_t D, float jitter, int64_t R, const float *d_rnd, float *d_t,
+                           sgn_stream_t stream);
 
 size_t sgn_query_workspace_bytes(int64_t R);
 int sgn_query(const sgn_grid *grid, const sgn_query_params *qp, const float *d_campos,
@@ -347,6 +354,53 @@ int sgn_adam_step(float *d_param, float *d_grad, float *d_exp_avg, float *d_exp_
  * pointers; d_ws: sgn_colsum_workspace_bytes(count) of device scratch. */
 size_t sgn_colsum_workspace_bytes(int32_t count);
 int sgn_colsum_f16(int32_t count, const void *const *d_x, int64_t rows, int32_t cols, float *d_ws, float *d_out,
+                   sgn_stream_t stream);
+/* The same with per-row fp32 weights: d_out[i][c] = sum over r of d_rw[i][r] * d_x[i][r][c] (d_rw: host
+ * array of device pointers, NULL entries = unweighted) -- the alpha branch's weight gradient
+ * dza^T h4 (point_aggregators.py:650-653, nn.Linear(256, 1)) in the bias sums' launch. */
+int sgn_colsum_f16_weighted(int32_t count, const void *const *d_x, const float *const *d_rw, int64_t rows,
+                            int32_t cols, float *d_ws, float *d_out, sgn_stream_t stream);
+
+/* ---- training: segment kernels (one launch for up to 16 segments) --------------------
+ * The gradient epilogue of the training step's weight GEMMs, i.e. the accumulation torch
+ * autograd does into nn.Linear's weight/bias .grad (models/base_rendering_model.py:534-664 ->
+ * loss.backward(); the layers of models/aggregators/point_aggregators.py:620-653, :772-780):
+ * per segment, for j < n with dst[j] >= 0,
+ *   d_grad[dst[j]] += (sum over b < nb of src[b * stride + j]  (+ tail[j] if tail)) / d_scale[0]
+ * src: nb split-K partials (fp32, device); dst: int32 device map from the MFMA storage order to
+ * the flat parameter (-1 = padding); d_scale: device loss scale or NULL (1).  Every dst entry of
+ * a launch must be distinct (no two segments add into the same element).  Up to 16 partials the
+ * sum runs in partial order; beyond, groups of ~16 partials add with float atomics. */
+typedef struct {
+    const float *src;
+    const float *tail;     /* optional [n] partial added after the nb slices (NULL: none) */
+    const int32_t *dst;
+    int64_t n;             /* elements per partial */
+    int64_t stride;        /* elements between partials (>= n) */
+    int32_t nb;            /* partials (>= 1) */
+    int32_t reserved;
+} sgn_grad_segment;
+int sgn_grad_accumulate(int32_t n_seg, const sgn_grad_segment *segs, const float *d_scale, float *d_grad,
+                        sgn_stream_t stream);
+/* Clears n_seg device regions (d_ptr[i]: 16-B aligned, bytes[i] a multiple of 16; host arrays). */
+int sgn_zero_segments(int32_t n_seg, void *const *d_ptr, const int64_t *bytes, sgn_stream_t stream);
+/* Index gathers from one fp32 source (the flat MLP parameter): dst[j] = src[idx[j]], 0 for idx
+ * outside [0, n_src); stored as fp32 or, with fp16 != 0, rounded to fp16 (nearest even) -- the
+ * device re-pack of the MFMA weight blobs each training step. */
+typedef struct {
+    const int32_t *idx;
+    void *dst;
+    int64_t n;
+    int32_t fp16;
+    int32_t reserved;
+} sgn_gather_segment;
+int sgn_gather_segments(int32_t n_seg, const sgn_gather_segment *segs, const float *d_src, int64_t n_src,
+                        sgn_stream_t stream);
+/* The backward's power-of-two loss scale: d_out[0] = 2^-floor(log2(max(max|a|, max|b|, 1e-30)))
+ * over two fp32 device arrays (a NaN propagates), in two launches with no host sync; d_ws:
+ * sgn_pow2_scale_workspace_bytes() of device scratch. */
+size_t sgn_pow2_scale_workspace_bytes(void);
+int sgn_pow2_scale(const float *d_a, int64_t na, const float *d_b, int64_t nb, void *d_ws, float *d_out,
                    sgn_stream_t stream);
 
 /* ---- composite --------------------------------------------------------- */

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -67,6 +67,15 @@ class LossParams(ctypes.Structure):
                 ("zero_one_weight", c_f32), ("zero_one_eps", c_f32)]
 
 
+class GradSegment(ctypes.Structure):
+    _fields_ = [("src", c_vp), ("tail", c_vp), ("dst", c_vp), ("n", c_i64), ("stride", c_i64), ("nb", c_i32),
+                ("reserved", c_i32)]
+
+
+class GatherSegment(ctypes.Structure):
+    _fields_ = [("idx", c_vp), ("dst", c_vp), ("n", c_i64), ("fp16", c_i32), ("reserved", c_i32)]
+
+
 # name -> (restype, argtypes); every symbol include/sgn_hip.h declares.
 SIGNATURES = {
     "sgn_abi_version": (c_i32, []),
@@ -75,6 +84,7 @@ SIGNATURES = {
     "sgn_grid_free": (c_i32, [c_vp]),
     "sgn_grid_get_info": (c_i32, [c_vp, ctypes.POINTER(GridInfo)]),
     "sgn_grid_export": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_depth_table_jitter": (c_i32, [c_f32, c_f32, c_i32, c_f32, c_i64, c_vp, c_vp, c_vp]),
     "sgn_query_workspace_bytes": (c_sz, [c_i64]),
     "sgn_query": (c_i32, [c_vp, ctypes.POINTER(QueryParams), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                           ctypes.POINTER(QueryOut), c_vp, c_sz, c_vp]),
@@ -113,6 +123,13 @@ SIGNATURES = {
                                ctypes.c_double, c_i64, c_i32, c_vp]),
     "sgn_colsum_workspace_bytes": (c_sz, [c_i32]),
     "sgn_colsum_f16": (c_i32, [c_i32, ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp, c_vp]),
+    "sgn_colsum_f16_weighted": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp,
+                                        c_vp]),
+    "sgn_grad_accumulate": (c_i32, [c_i32, ctypes.POINTER(GradSegment), c_vp, c_vp, c_vp]),
+    "sgn_zero_segments": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),
+    "sgn_gather_segments": (c_i32, [c_i32, ctypes.POINTER(GatherSegment), c_vp, c_i64, c_vp]),
+    "sgn_pow2_scale_workspace_bytes": (c_sz, []),
+    "sgn_pow2_scale": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "sgn_mlp_packed_bytes_f32": (c_sz, [c_i32, c_i32]),
     "sgn_mlp_pack_f32": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
     "sgn_mlp_pack_f32_host": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp]),

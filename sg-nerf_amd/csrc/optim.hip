@@ -14,6 +14,11 @@
 // Column sums: db_l = sum over rows of the fp16 delta tile [rows][cols] (fp32 accumulate),
 // in two deterministic passes (fixed row slabs per workgroup, then the slabs in order), all
 // layers of the step in the same two launches.
+//
+// Segment kernels (one launch for up to 16 segments): the weight-gradient epilogue (split-K
+// partials summed, unpermuted from the MFMA storage order, unscaled and added into the flat
+// gradient -- the accumulation autograd does into nn.Linear's .grad), clearing padded tails and
+// the index gathers that re-pack the MFMA weight blobs from the flat parameter.
 #include <algorithm>
 #include <cmath>
 #include <hip/hip_fp16.h>
@@ -72,6 +77,7 @@ constexpr int kColsumSlabs = 512;   // row slabs (workgroups) per matrix
 
 struct ColsumArgs {
     const __half *x[kMaxColsumMats];
+    const float *rw[kMaxColsumMats];   // per-row weights (null: 1)
     int64_t rows, slab;   // rows per slab
     float *ws;            // [count][kColsumSlabs][256]
     float *out;           // [count][256]
@@ -84,15 +90,26 @@ __global__ __launch_bounds__(256) void k_colsum_part(ColsumArgs a) {
     const int64_t r0 = blockIdx.x * a.slab;
     const int64_t r1 = min(r0 + a.slab, a.rows);
     const __half *x = a.x[mat];
+    const float *rw = a.rw[mat];
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int64_t r = r0 + r8; r < r1; r += 8) {
         const uint4 w = *reinterpret_cast<const uint4 *>(x + r * kColsumCols + c8 * 8);
         const __half2 *h = reinterpret_cast<const __half2 *>(&w);
+        if (rw) {
+            const float s = rw[r];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float2 f = __half22float2(h[j]);
-            acc[2 * j] += f.x;
-            acc[2 * j + 1] += f.y;
+            for (int j = 0; j < 4; ++j) {
+                const float2 f = __half22float2(h[j]);
+                acc[2 * j] += f.x * s;
+                acc[2 * j + 1] += f.y * s;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float2 f = __half22float2(h[j]);
+                acc[2 * j] += f.x;
+                acc[2 * j + 1] += f.y;
+            }
         }
     }
     __shared__ float red[8][kColsumCols];
@@ -112,6 +129,147 @@ __global__ __launch_bounds__(256) void k_colsum_final(ColsumArgs a) {
     float s = 0.f;
     for (int b = 0; b < kColsumSlabs; ++b) s += w[b * kColsumCols];
     a.out[mat * kColsumCols + threadIdx.x] = s;
+}
+
+// ---- segment kernels: the step's small gathers / clears / gradient epilogues, one launch each
+// (grid.y = segment).  Replace ~40 per-tensor torch launches of the training step.
+constexpr int kMaxSegs = 16;
+
+struct GradArgs {
+    sgn_grad_segment s[kMaxSegs];
+    const float *scale;   // device loss scale (power of two) or null
+    float *grad;
+};
+
+__device__ __forceinline__ bool grad_seg_vec4(const sgn_grad_segment &g) {
+    return !((g.n | g.stride) & 3) && !(reinterpret_cast<uintptr_t>(g.src) & 15) &&
+           !(reinterpret_cast<uintptr_t>(g.tail) & 15) && !(reinterpret_cast<uintptr_t>(g.dst) & 15);
+}
+
+__device__ __forceinline__ void grad_add(float *p, float v, bool atomic) {
+    if (atomic)
+        atomicAdd(p, v);
+    else
+        *p += v;
+}
+
+// grad[dst[j]] += (sum over b < nb of src[b * stride + j] (+ tail[j])) / scale; dst[j] < 0: skipped.
+// grid (units, segments, partial groups): group z sums its share of the nb partials in order and
+// adds it with a float atomic when there is more than one group (else a plain read-modify-write:
+// the destinations are distinct across all segments -- each reference weight has one stored
+// element).  Four consecutive elements per thread (16-B loads) when the segment allows it.
+__global__ __launch_bounds__(256) void k_grad_accumulate(GradArgs a) {
+    const sgn_grad_segment &g = a.s[blockIdx.y];
+    const int32_t per = (g.nb + (int32_t)gridDim.z - 1) / (int32_t)gridDim.z;
+    const int32_t b0 = (int32_t)blockIdx.z * per, b1 = min(g.nb, b0 + per);
+    if (b0 >= b1) return;
+    const bool atomic = gridDim.z > 1;
+    const bool tail = g.tail && blockIdx.z == 0;
+    const float inv = a.scale ? 1.f / a.scale[0] : 1.f;
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (grad_seg_vec4(g)) {
+        const int64_t j = u * 4;
+        if (j >= g.n) return;
+        const float4 *src = reinterpret_cast<const float4 *>(g.src + j);
+        const int64_t st4 = g.stride / 4;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+        for (int32_t b = b0; b < b1; ++b) {
+            const float4 v = src[(int64_t)b * st4];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        if (tail) {
+            const float4 v = *reinterpret_cast<const float4 *>(g.tail + j);
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        const int4 d = *reinterpret_cast<const int4 *>(g.dst + j);
+        if (d.x >= 0) grad_add(a.grad + d.x, s.x * inv, atomic);
+        if (d.y >= 0) grad_add(a.grad + d.y, s.y * inv, atomic);
+        if (d.z >= 0) grad_add(a.grad + d.z, s.z * inv, atomic);
+        if (d.w >= 0) grad_add(a.grad + d.w, s.w * inv, atomic);
+        return;
+    }
+    if (u >= g.n) return;
+    const int32_t d = g.dst[u];
+    if (d < 0) return;
+    float s = 0.f;
+    for (int32_t b = b0; b < b1; ++b) s += g.src[(int64_t)b * g.stride + u];
+    if (tail) s += g.tail[u];
+    grad_add(a.grad + d, s * inv, atomic);
+}
+
+struct ZeroArgs {
+    uint4 *p[kMaxSegs];
+    int64_t n16[kMaxSegs];
+};
+
+__global__ __launch_bounds__(256) void k_zero_segments(ZeroArgs a) {
+    uint4 *p = a.p[blockIdx.y];
+    const int64_t n = a.n16[blockIdx.y];
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = z;
+}
+
+struct GatherArgs {
+    sgn_gather_segment s[kMaxSegs];
+    const float *src;
+    int64_t n_src;
+};
+
+// dst[j] = idx[j] in [0, n_src) ? src[idx[j]] : 0, stored as fp32 or fp16 (round to nearest even)
+__global__ __launch_bounds__(256) void k_gather_segments(GatherArgs a) {
+    const sgn_gather_segment &g = a.s[blockIdx.y];
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= g.n) return;
+    const int32_t i = g.idx[j];
+    const float v = (i >= 0 && i < a.n_src) ? a.src[i] : 0.f;
+    if (g.fp16)
+        static_cast<__half *>(g.dst)[j] = __float2half_rn(v);
+    else
+        static_cast<float *>(g.dst)[j] = v;
+}
+
+// ---- power-of-two loss scale: 2^-floor(log2(max(max|a|, max|b|, 1e-30))) -----------------
+// max |x| as the max of the sign-cleared bit patterns (NaN > inf > every finite value, so a NaN
+// propagates as torch.amax / torch.maximum would), per-workgroup partials then one workgroup.
+constexpr int kScaleBlocks = 256;
+
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t v) {
+    __shared__ uint32_t red[256];
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    return red[0];
+}
+
+__global__ __launch_bounds__(256) void k_absmax_part(const float *a, int64_t na, const float *b, int64_t nb,
+                                                     uint32_t *ws) {
+    uint32_t m = 0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < na; i += stride)
+        m = max(m, __float_as_uint(a[i]) & 0x7fffffffu);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride)
+        m = max(m, __float_as_uint(b[i]) & 0x7fffffffu);
+    m = block_max_u32(m);
+    if (threadIdx.x == 0) ws[blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(256) void k_pow2_scale(const uint32_t *ws, float *out) {
+    const uint32_t m = block_max_u32(ws[threadIdx.x]);
+    if (threadIdx.x == 0) {
+        const float f = __uint_as_float(m);
+        const float c = (f != f) ? f : fmaxf(f, 1e-30f);   // torch.clamp(min=1e-30) keeps a NaN
+        out[0] = exp2f(-floorf(log2f(c)));
+    }
 }
 
 }  // namespace
@@ -160,6 +318,11 @@ size_t sgn_colsum_workspace_bytes(int32_t count) {
 
 int sgn_colsum_f16(int32_t count, const void *const *d_x, int64_t rows, int32_t cols, float *d_ws, float *d_out,
                    sgn_stream_t stream) {
+    return sgn_colsum_f16_weighted(count, d_x, nullptr, rows, cols, d_ws, d_out, stream);
+}
+
+int sgn_colsum_f16_weighted(int32_t count, const void *const *d_x, const float *const *d_rw, int64_t rows, int32_t cols,
+                            float *d_ws, float *d_out, sgn_stream_t stream) {
     SGN_REQUIRE(count >= 1 && count <= kMaxColsumMats, "sgn_colsum_f16: 1 <= count <= 8");
     SGN_REQUIRE(cols == kColsumCols, "sgn_colsum_f16: cols must be 256");
     SGN_REQUIRE(rows >= 0, "sgn_colsum_f16: rows < 0");
@@ -169,6 +332,7 @@ int sgn_colsum_f16(int32_t count, const void *const *d_x, int64_t rows, int32_t 
         SGN_REQUIRE(d_x[i] != nullptr, "sgn_colsum_f16: null matrix");
         SGN_REQUIRE(!(reinterpret_cast<uintptr_t>(d_x[i]) & 15), "sgn_colsum_f16: matrices must be 16-B aligned");
         a.x[i] = static_cast<const __half *>(d_x[i]);
+        a.rw[i] = d_rw ? d_rw[i] : nullptr;
     }
     a.rows = rows;
     a.slab = (rows + kColsumSlabs - 1) / kColsumSlabs;
@@ -177,6 +341,96 @@ int sgn_colsum_f16(int32_t count, const void *const *d_x, int64_t rows, int32_t 
     hipLaunchKernelGGL(k_colsum_part, dim3(kColsumSlabs, count), dim3(256), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_colsum_final, dim3(count), dim3(256), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_grad_accumulate(int32_t n_seg, const sgn_grad_segment *segs, const float *d_scale, float *d_grad,
+                        sgn_stream_t stream) {
+    SGN_REQUIRE(n_seg >= 0 && n_seg <= kMaxSegs, "sgn_grad_accumulate: 0 <= n_seg <= 16");
+    if (n_seg == 0) return 0;
+    SGN_REQUIRE(segs && d_grad, "sgn_grad_accumulate: null argument");
+    GradArgs a;
+    int64_t umax = 0;
+    int32_t nbmax = 1;
+    for (int i = 0; i < n_seg; ++i) {
+        const sgn_grad_segment &g = segs[i];
+        SGN_REQUIRE(g.n >= 0 && g.nb >= 1 && g.stride >= g.n, "sgn_grad_accumulate: n >= 0, nb >= 1, stride >= n");
+        SGN_REQUIRE(g.n == 0 || (g.src && g.dst), "sgn_grad_accumulate: null segment buffer");
+        a.s[i] = g;
+        // work units as the kernel counts them (grad_seg_vec4)
+        const bool vec = !((g.n | g.stride) & 3) && !(reinterpret_cast<uintptr_t>(g.src) & 15) &&
+                         !(reinterpret_cast<uintptr_t>(g.tail) & 15) && !(reinterpret_cast<uintptr_t>(g.dst) & 15);
+        umax = std::max(umax, vec ? g.n / 4 : g.n);
+        if (g.n > 0) nbmax = std::max(nbmax, g.nb);
+    }
+    if (umax == 0) return 0;
+    SGN_REQUIRE(umax <= (int64_t)256 * 0x7fffffff, "sgn_grad_accumulate: segment too long");
+    a.scale = d_scale;
+    a.grad = d_grad;
+    // partial groups: ~16 partials per group, at most 32 groups (one group: deterministic order)
+    const int groups = std::min(32, std::max(1, (nbmax + 15) / 16));
+    hipLaunchKernelGGL(k_grad_accumulate, dim3((unsigned)((umax + 255) / 256), n_seg, groups), dim3(256), 0,
+                       as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_zero_segments(int32_t n_seg, void *const *d_ptr, const int64_t *bytes, sgn_stream_t stream) {
+    SGN_REQUIRE(n_seg >= 0 && n_seg <= kMaxSegs, "sgn_zero_segments: 0 <= n_seg <= 16");
+    if (n_seg == 0) return 0;
+    SGN_REQUIRE(d_ptr && bytes, "sgn_zero_segments: null argument");
+    ZeroArgs a;
+    int64_t nmax = 0;
+    for (int i = 0; i < n_seg; ++i) {
+        SGN_REQUIRE(bytes[i] >= 0 && bytes[i] % 16 == 0, "sgn_zero_segments: byte counts must be multiples of 16");
+        SGN_REQUIRE(bytes[i] == 0 || (d_ptr[i] && !(reinterpret_cast<uintptr_t>(d_ptr[i]) & 15)),
+                    "sgn_zero_segments: regions must be 16-B aligned");
+        a.p[i] = static_cast<uint4 *>(d_ptr[i]);
+        a.n16[i] = bytes[i] / 16;
+        nmax = std::max(nmax, a.n16[i]);
+    }
+    if (nmax == 0) return 0;
+    const int64_t blocks = std::min<int64_t>((nmax + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_zero_segments, dim3((unsigned)blocks, n_seg), dim3(256), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_gather_segments(int32_t n_seg, const sgn_gather_segment *segs, const float *d_src, int64_t n_src,
+                        sgn_stream_t stream) {
+    SGN_REQUIRE(n_seg >= 0 && n_seg <= kMaxSegs, "sgn_gather_segments: 0 <= n_seg <= 16");
+    if (n_seg == 0) return 0;
+    SGN_REQUIRE(segs && n_src >= 0 && (d_src || n_src == 0), "sgn_gather_segments: null argument");
+    GatherArgs a;
+    int64_t nmax = 0;
+    for (int i = 0; i < n_seg; ++i) {
+        const sgn_gather_segment &g = segs[i];
+        SGN_REQUIRE(g.n >= 0 && (g.n == 0 || (g.idx && g.dst)), "sgn_gather_segments: bad segment");
+        a.s[i] = g;
+        nmax = std::max(nmax, g.n);
+    }
+    if (nmax == 0) return 0;
+    SGN_REQUIRE(nmax <= (int64_t)256 * 0x7fffffff, "sgn_gather_segments: segment too long");
+    a.src = d_src;
+    a.n_src = n_src;
+    hipLaunchKernelGGL(k_gather_segments, dim3((unsigned)((nmax + 255) / 256), n_seg), dim3(256), 0,
+                       as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+size_t sgn_pow2_scale_workspace_bytes(void) { return kScaleBlocks * sizeof(uint32_t); }
+
+int sgn_pow2_scale(const float *d_a, int64_t na, const float *d_b, int64_t nb, void *d_ws, float *d_out,
+                   sgn_stream_t stream) {
+    SGN_REQUIRE(na >= 0 && nb >= 0 && na + nb >= 1, "sgn_pow2_scale: at least one element");
+    SGN_REQUIRE((d_a || na == 0) && (d_b || nb == 0) && d_ws && d_out, "sgn_pow2_scale: null buffer");
+    hipLaunchKernelGGL(k_absmax_part, dim3(kScaleBlocks), dim3(256), 0, as_stream(stream), d_a, na, d_b, nb,
+                       static_cast<uint32_t *>(d_ws));
+    SGN_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_pow2_scale, dim3(1), dim3(256), 0, as_stream(stream), static_cast<const uint32_t *>(d_ws),
+                       d_out);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

@@ -484,10 +484,66 @@ void launch_knn(dim3 grid, hipStream_t st, bool semantic, bool count, bool runs_
                        o->ray_soff, o->samp_ray, o->samp_d, o->counters, o->samp_locw, o->samp_nnb, o->pidx, o->work);
 }
 
+// ---- training-mode depth table (jitter > 0): near_far_linear_ray_generation,
+// diff_ray_marching.py:349-393 -- tvals = linspace(0, 1, D + 1) (torch's two-sided linspace
+// formula), t = near (1 - tvals) + far tvals, seg_i = (t_{i+1} - t_i) (1 + jitter (rnd_i - 0.5)),
+// end = near + [0, cumsum(seg)], mid_i = (end_i + end_{i+1}) / 2.  One wave per ray, the cumsum as
+// a wave scan per 64-segment chunk with the running sum carried across chunks (the torch
+// sequence is ~17 launches over [R, D]).
+__device__ __forceinline__ float linspace01(int i, int steps) {
+    const float step = 1.0f / (float)(steps - 1);
+    const int half = steps / 2;
+    return i < half ? step * (float)i : 1.0f - step * (float)(steps - i - 1);
+}
+
+__global__ __launch_bounds__(256) void k_depth_jitter(float near, float far, int D, float jitter, int64_t R,
+                                                      const float *__restrict__ rnd, float *__restrict__ t) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const float *rr = rnd + r * D;
+    float *tr = t + r * D;
+    float carry = 0.f;   // cumsum of the segments before this chunk
+    for (int c0 = 0; c0 < D; c0 += 64) {
+        const int i = c0 + lane;
+        float seg = 0.f;
+        if (i < D) {
+            const float ta = linspace01(i, D + 1), tb = linspace01(i + 1, D + 1);
+            const float za = near * (1.0f - ta) + far * ta, zb = near * (1.0f - tb) + far * tb;
+            seg = (zb - za) * (1.0f + jitter * (rr[i] - 0.5f));
+        }
+        float inc = seg;   // inclusive scan over the wave, in lane order
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const float v = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += v;
+        }
+        const float cs = carry + inc;                       // cumsum through segment i
+        float prev = __shfl_up(cs, 1, 64);                  // cumsum through segment i - 1
+        if (lane == 0) prev = carry;
+        if (i < D) {
+            const float e0 = (i == 0) ? near : near + prev, e1 = near + cs;
+            tr[i] = (e0 + e1) / 2.0f;
+        }
+        carry = __shfl(cs, 63, 64);
+    }
+}
+
 }  // namespace
 }  // namespace sgn
 
 extern "C" {
+
+int sgn_depth_table_jitter(float near, float far, int32_t D, float jitter, int64_t R, const float *d_rnd, float *d_t,
+                           sgn_stream_t stream) {
+    SGN_REQUIRE(D >= 1 && R >= 0, "sgn_depth_table_jitter: D >= 1, R >= 0");
+    if (R == 0) return 0;
+    SGN_REQUIRE(d_rnd && d_t, "sgn_depth_table_jitter: null buffer");
+    hipLaunchKernelGGL(sgn::k_depth_jitter, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, sgn::as_stream(stream), near, far,
+                       (int)D, jitter, R, d_rnd, d_t);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
 
 size_t sgn_query_workspace_bytes(int64_t R) {
     // [R*SR_MAX int16 slot->depth table] is carved by the caller? no: kept here.

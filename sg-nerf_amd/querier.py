@@ -19,8 +19,19 @@ import torch
 from . import _lib
 from .hyper import grid_hyperparameters, point_extent
 from .opts import HotPathOpts
-from .raygen import depth_table, shared_depth_table
+from .raygen import shared_depth_table
 
+
+
+def depth_table_jitter_hip(near, far, D, jitter, R, device, generator=None):
+    """Training-mode depth table [R, D] (raygen.depth_table with jitter > 0, i.e.
+    near_far_linear_ray_generation, diff_ray_marching.py:349-393): the same torch.rand draw, the
+    rest in one HIP launch (sgn_depth_table_jitter)."""
+    rnd = torch.rand((R, D), device=device, generator=generator)
+    t = torch.empty(R, D, dtype=torch.float32, device=device)
+    _lib.check(_lib.lib().sgn_depth_table_jitter(float(near), float(far), int(D), float(jitter), int(R), _lib.ptr(rnd),
+                                                 _lib.ptr(t), _lib.stream_handle()), "sgn_depth_table_jitter")
+    return t
 
 class HipGrid:
     """Owns one sgn_grid (device memory is released on close/GC)."""
@@ -192,7 +203,7 @@ class LightningFastQuerier:
     def depth_table(self, near, far, R):
         o = self.opts
         if o.is_train > 0:
-            return depth_table(near, far, o.z_depth_dim, jitter=0.3, R=R, device=self.device), 1
+            return depth_table_jitter_hip(near, far, o.z_depth_dim, 0.3, R, self.device), 1
         return shared_depth_table(near, far, o.z_depth_dim, self.device), 0
 
     # -- sample-major fast path ------------------------------------------------------

@@ -39,7 +39,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .opts import HotPathOpts
-from .train import (PointParams, _LinearRows, _allreduce_buckets, _allreduce_point_rows, _pe, composite_losses,
+from .train import (PointParams, _allreduce_buckets, _allreduce_point_rows, _pe, composite_losses,
                     gather_counts, touched_rows)
 from .loss_hip import LossStage
 from .weights import BPNET, LAYERS, layers_for, strip_prefix
@@ -169,9 +169,10 @@ class _Packer:
         self.tbytes = int(L.sgn_train_tblob_bytes())
 
         def imap(fn, name, *args, n):
+            """The layout's index map (flat index + 1, 0 = zero) as flat indices (-1 = zero)."""
             a = (ctypes.c_int32 * n)()
             _lib.check(fn(*args, a, n), name)
-            return torch.frombuffer(bytearray(a), dtype=torch.int32).long().to(device)
+            return (torch.frombuffer(bytearray(a), dtype=torch.int32) - 1).to(device)
         self.i16 = imap(L.sgn_mlp_pack_index, "sgn_mlp_pack_index", 0, n=self.off_f32 // 2)
         self.i32 = imap(L.sgn_mlp_pack_index, "sgn_mlp_pack_index", 1, n=N_F32)
         self.isp = imap(L.sgn_mlp_pack_index, "sgn_mlp_pack_index", 2, n=(self.base - self.off_split) // 2)
@@ -185,16 +186,22 @@ class _Packer:
             self.it = imap(L.sgn_train_pack_index, "sgn_train_pack_index", n=self.tbytes // 2)
         self.blob = torch.zeros(self.total, dtype=torch.uint8, device=device)
         self.tblob = torch.zeros(self.tbytes, dtype=torch.uint8, device=device)
+        # (index map, destination bytes, fp16?) -- every section of both blobs in one gather launch
+        segs = [(self.i16, self.blob[:self.off_f32], 1), (self.i32, self.blob[self.off_f32:self.off_f32 + 4 * N_F32], 0),
+                (self.isp, self.blob[self.off_split:self.base], 1)]
+        if variant != (0, 0):
+            segs += [(self.iwb, self.blob[self.base:self.off_bb], 1), (self.ibb, self.blob[self.off_bb:], 0)]
+        segs.append((self.it, self.tblob, 1))
+        for idx, dst, h in segs:
+            assert dst.numel() == idx.numel() * (2 if h else 4)
+        self._segs = (_lib.GatherSegment * len(segs))(*[_lib.GatherSegment(idx.data_ptr(), dst.data_ptr(), idx.numel(), h, 0)
+                                                       for idx, dst, h in segs])
 
     def pack(self, flat):
-        ext = torch.cat([flat.detach().new_zeros(1), flat.detach()])
-        self.blob[:self.off_f32].view(torch.float16).copy_(ext[self.i16])
-        self.blob[self.off_f32:self.off_f32 + 4 * N_F32].view(torch.float32).copy_(ext[self.i32])
-        self.blob[self.off_split:self.base].view(torch.float16).copy_(ext[self.isp])
-        if self.variant != (0, 0):
-            self.blob[self.base:self.off_bb].view(torch.float16).copy_(ext[self.iwb])
-            self.blob[self.off_bb:].view(torch.float32).copy_(ext[self.ibb])
-        self.tblob.view(torch.float16).copy_(ext[self.it])
+        flat = flat.detach()
+        assert flat.is_contiguous() and flat.dtype == torch.float32
+        _lib.check(_lib.lib().sgn_gather_segments(len(self._segs), self._segs, _lib.ptr(flat), flat.numel(),
+                                                  _lib.stream_handle()), "sgn_gather_segments")
         return self.blob, self.tblob
 
 
@@ -208,18 +215,19 @@ _MM_OUT_DTYPE = None
 _BMM_OUT_DTYPE = None
 
 
-def _gemm_rows_f32(a, b, chunk):
-    """a^T b over the row dimension: a [rows, M], b [rows, N] fp16 -> [M, N] fp32.
+def _gemm_rows_parts(a, b, chunk):
+    """a^T b over the row dimension as split-K partials: a [rows, M], b [rows, N] fp16 ->
+    ([nb, M, N] fp32 partials, [M, N] tail partial or None); their sum is a^T b.
 
-    Split-K: the rows go in `chunk`-row batches through one batched GEMM (a 256 x 288 output
-    alone is ~8 macro tiles, so a plain GEMM would occupy a handful of the 256 CUs and walk
-    K = 160 k rows serially), the batch partials summed in fp32; a ragged tail of rows takes
-    one more plain GEMM.  Every row is summed exactly once whatever `chunk` is."""
+    The rows go in `chunk`-row batches through one batched GEMM (a 256 x 288 output alone is ~8
+    macro tiles, so a plain GEMM would occupy a handful of the 256 CUs and walk K = 160 k rows
+    serially); a ragged tail of rows takes one more plain GEMM.  The partials are summed by the
+    gradient epilogue (sgn_grad_accumulate), not here.  Every row is in exactly one partial."""
     global _BMM_OUT_DTYPE
     rows = a.shape[0]
     nb = rows // chunk if chunk > 0 else 0
     if nb <= 1:
-        return _mm_f32(a.t(), b)
+        return _mm_f32(a.t(), b)[None], None
     body = nb * chunk
     at = a[:body].view(nb, chunk, a.shape[1]).transpose(1, 2)
     bt = b[:body].view(nb, chunk, b.shape[1])
@@ -229,13 +237,9 @@ def _gemm_rows_f32(a, b, chunk):
             _BMM_OUT_DTYPE = True
         except Exception:
             _BMM_OUT_DTYPE = False
-    if _BMM_OUT_DTYPE:
-        G = torch.bmm(at, bt, out_dtype=torch.float32).sum(0)
-    else:
-        G = torch.bmm(at.float(), bt.float()).sum(0)
-    if body < rows:
-        G += _mm_f32(a[body:].t(), b[body:])
-    return G
+    G = torch.bmm(at, bt, out_dtype=torch.float32) if _BMM_OUT_DTYPE else torch.bmm(at.float(), bt.float())
+    tail = _mm_f32(a[body:].t(), b[body:]) if body < rows else None
+    return G.contiguous(), tail
 
 
 # loss-stage graphs: capacity bucket (items / samples) and how many captured graphs are kept
@@ -258,6 +262,53 @@ def _mm_f32(a, b):
     if _MM_OUT_DTYPE:
         return torch.mm(a, b, out_dtype=torch.float32)
     return a.float() @ b.float()
+
+
+def _grad_into(g, dst, parts, tail=None, scale=None):
+    """g[dst[j]] += (sum of the partials [nb, n] (+ tail)) (/ scale): one sgn_grad_accumulate launch."""
+    n = dst.numel()
+    seg = _lib.GradSegment(parts.data_ptr(), tail.data_ptr() if tail is not None else None, dst.data_ptr(), n, n,
+                           parts.numel() // n, 0)
+    _lib.check(_lib.lib().sgn_grad_accumulate(1, ctypes.byref(seg), _lib.ptr(scale), _lib.ptr(g),
+                                              _lib.stream_handle()), "sgn_grad_accumulate")
+
+
+class _LinearInto(torch.autograd.Function):
+    """F.linear (fp32) of a weight / bias held in the flat parameter whose gradients the backward
+    ADDS into the flat gradient (split-K weight partials through sgn_grad_accumulate, the bias sum
+    in place) instead of returning them through autograd -- which would zero-fill a full-size
+    gradient per parameter view, copy the slice in and add it back: six launches per layer."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, g, dst_w, off_b):
+        ctx.save_for_backward(x, w)
+        ctx.g, ctx.dst_w, ctx.off_b = g, dst_w, off_b
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, w = ctx.saved_tensors
+        gz = gz.contiguous()
+        parts, tail = _fp32_rows_parts(gz, x, DW_CHUNK_COLOUR)
+        _grad_into(ctx.g, ctx.dst_w, parts, tail)
+        ctx.g[ctx.off_b:ctx.off_b + w.shape[0]].add_(gz.sum(0))
+        return (gz @ w if ctx.needs_input_grad[0] else None), None, None, None, None, None
+
+
+# rows per split-K batch of the colour layers' fp32 weight gradients
+DW_CHUNK_COLOUR = int(os.environ.get("SGN_DW_CHUNK_COLOUR", "4096"))
+
+
+def _fp32_rows_parts(gz, x, chunk):
+    """gz^T x (fp32) over the rows as split-K partials ([nb, M, N], tail [M, N] or None)."""
+    rows = gz.shape[0]
+    nb = rows // chunk if chunk > 0 else 0
+    if nb <= 1:
+        return (gz.t() @ x)[None].contiguous(), None
+    body = nb * chunk
+    parts = torch.bmm(gz[:body].view(nb, chunk, gz.shape[1]).transpose(1, 2), x[:body].reshape(nb, chunk, x.shape[1]))
+    tail = (gz[body:].t() @ x[body:]).contiguous() if body < rows else None
+    return parts.contiguous(), tail
 
 
 class PointAdam(torch.optim.Adam):
@@ -416,31 +467,32 @@ class HipTrainer:
 
     _COLOUR = ("color_branch.0", "color_branch.2", "color_branch.4", "color_branch.6")
 
-    def _colour_span(self):
-        """[c0, c1): the colour branch's weights and biases, contiguous in the flat parameter."""
-        sl = self.mlp.slices
-        c0 = min(sl[n][0] for n in self._COLOUR)
-        c1 = max(sl[n][0] + sl[n][1] * sl[n][2] + sl[n][1] for n in self._COLOUR)
-        assert c1 - c0 == sum(sl[n][1] * sl[n][2] + sl[n][1] for n in self._COLOUR)
-        return c0, c1
-
-    def _colour(self, fs, v, src=None, base=0):
-        """colour MLP (point_aggregators.py color_branch); weights from the flat parameter, or
-        from `src` = a copy of its [base, base + len) span."""
+    def _colour(self, fs, v):
+        """colour MLP (point_aggregators.py color_branch) on the flat parameter's weights (detached),
+        the weight / bias gradients added straight into the flat gradient (_LinearInto)."""
         m = self.mlp
+        g = m.flat.grad
         vpe = _pe(v, 4, ori=True)[..., 3:]
         c = torch.cat([fs, vpe], dim=-1)
         for name in self._COLOUR:
-            if src is None:
-                w, b = m.w(name), m.b(name)
-            else:
-                off, o, i = m.slices[name]
-                w = src[off - base:off - base + o * i].view(o, i)
-                b = src[off - base + o * i:off - base + o * i + o]
-            c = _LinearRows.apply(c, w, b)   # F.linear with a split-K weight gradient (K = the samples)
+            dst = self._flat_maps.get(("colour", name))
+            off, o, i = m.slices[name]
+            if dst is None:
+                dst = self._flat_maps[("colour", name)] = (off + torch.arange(o * i, device=self.device)).to(torch.int32)
+            c = _LinearInto.apply(c, m.w(name).detach(), m.b(name).detach(), g, dst, off + o * i)
             if name != "color_branch.6":
                 c = F.leaky_relu(c, 0.01)
         return torch.sigmoid(c) * (1 + 2 * 0.001) - 0.001
+
+    def _loss_scale(self, dfs, dal):
+        """2^-floor(log2(max |d|)) of the per-row deltas' inputs, on the device (sgn_pow2_scale)."""
+        L = _lib.lib()
+        if not hasattr(self, "_scale_ws"):
+            self._scale_ws = torch.empty(int(L.sgn_pow2_scale_workspace_bytes()), dtype=torch.uint8, device=self.device)
+        scale = torch.empty(1, dtype=torch.float32, device=self.device)
+        _lib.check(L.sgn_pow2_scale(_lib.ptr(dfs), dfs.numel(), _lib.ptr(dal), dal.numel(), _lib.ptr(self._scale_ws),
+                                    _lib.ptr(scale), _lib.stream_handle()), "sgn_pow2_scale")
+        return scale
 
     # -- one step ------------------------------------------------------------------------
     def backward(self, campos, rot, raydir, near, far, gt, labels=None):
@@ -516,8 +568,7 @@ class HipTrainer:
             if n > 0:
                 dfs = fs_t.grad.contiguous()
                 dal = alpha_t.grad.contiguous()
-                m = torch.maximum(dfs.abs().amax(), dal.abs().amax())
-                scale = torch.exp2(-torch.floor(torch.log2(torch.clamp(m, min=1e-30)))).reshape(1).contiguous()
+                scale = self._loss_scale(dfs, dal)
         # ---- HIP backward of the per-row part -----------------------------------------------
         if n > 0:
             deltas = _lib.AggDeltas(self.d[3].data_ptr(), self.d[2].data_ptr(), self.d[1].data_ptr(),
@@ -632,19 +683,15 @@ class HipTrainer:
         work = q.work[:Nc]
         samp = torch.where(ok_i, work, Sc)      # padding items -> sentinel sample Sc
         samp_c = torch.where(ok_i, work, 0)
-        fs32, al32, cw = st["fs32"], st["al32"], st["cw"]
-        c0, c1 = st["cspan"]
-        fl = self.mlp.flat
+        fs32, al32 = st["fs32"], st["al32"]
         with torch.no_grad():
             fs32.copy_(torch.where(ok_i[:, None], self.fs[:Nc].float(), 0.0))
             al32.copy_(torch.where(ok_i, self.feat[:, 0][samp_c], 0.0))
-            cw.copy_(fl[c0:c1])                 # colour weights as their own leaf: autograd
-            for t in (fs32, al32, cw):          # never touches the full flat parameter
-                t.grad.zero_()
+        fs32.grad = al32.grad = None   # backward assigns fresh (graph-pool) gradients: no clear, no accumulate
         # padding items read sample 0's ray, which is unwritten when the step has no samples:
         # mask the gathered ray index too, so the raydir gather stays in bounds
         v = st["raydir"][torch.where(ok_i, q.samp_ray[:Sc][samp_c], 0)]
-        feat_s = torch.cat([al32[:, None], self._colour(fs32, v, cw, c0)], dim=-1)
+        feat_s = torch.cat([al32[:, None], self._colour(fs32, v)], dim=-1)   # colour grads -> flat.grad
         featS = torch.zeros(Sc + 1, 4, device=dev).index_put((samp,), feat_s)[:Sc]
         validS = torch.zeros(Sc + 1, dtype=torch.bool, device=dev).index_put((samp,), st["true"])[:Sc]
         qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:Sc],
@@ -657,13 +704,11 @@ class HipTrainer:
             total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, st["campos"], st["rot"],
                                                             st["raydir"], st["gt"], o, s_count=q.counters[0])
         total.backward()
-        with torch.no_grad():
-            fl.grad[c0:c1].add_(cw.grad)
         dfs, dal = fs32.grad, al32.grad
-        m = torch.maximum(dfs.abs().amax(), dal.abs().amax())
-        scale = torch.exp2(-torch.floor(torch.log2(torch.clamp(m, min=1e-30)))).reshape(1)
-        return {"total": total.detach(), "parts": parts, "full": full.detach(), "ray_mask": ray_mask,
-                "dfs": dfs, "dal": dal, "scale": scale}
+        scale = self._loss_scale(dfs, dal)
+        names = list(parts)
+        return {"scalars": torch.stack([total.detach()] + [parts[k] for k in names]), "names": names,
+                "full": full.detach(), "ray_mask": ray_mask, "dfs": dfs, "dal": dal, "scale": scale}
 
     def _graph_losses(self, q, campos, rot, raydir, gt, R, S, n):
         """Replay the captured loss stage for this step's capacity bucket (item / sample counts
@@ -689,11 +734,7 @@ class HipTrainer:
                   "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
                   "campos": campos.clone(), "rot": rot.clone(),
                   "fs32": torch.zeros(Nc, 256, device=dev, requires_grad=True),
-                  "al32": torch.zeros(Nc, device=dev, requires_grad=True), "cspan": self._colour_span()}
-            st["cw"] = torch.zeros(st["cspan"][1] - st["cspan"][0], device=dev, requires_grad=True)
-            st["cw"].grad = torch.zeros_like(st["cw"])
-            st["fs32"].grad = torch.zeros_like(st["fs32"])
-            st["al32"].grad = torch.zeros_like(st["al32"])
+                  "al32": torch.zeros(Nc, device=dev, requires_grad=True)}
             keep = [fl.grad.clone(), P.points_conf.grad.clone()]   # warm-up accumulates into them
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
@@ -714,31 +755,61 @@ class HipTrainer:
         st["rot"].copy_(rot)
         st["graph"].replay()
         out = st["out"]
-        return {"total": out["total"].clone(), "parts": {k: v.clone() for k, v in out["parts"].items()},
+        sc = out["scalars"].clone()             # the loss and its parts: one copy out of the graph's buffers
+        return {"total": sc[0], "parts": {k: sc[1 + i] for i, k in enumerate(out["names"])},
                 "full": out["full"].clone(), "ray_mask": out["ray_mask"].clone(),
                 "dfs": out["dfs"], "dal": out["dal"], "scale": out["scale"]}
 
+    def _dst_maps(self, name, x_cols, ix):
+        """int32 maps from the MFMA storage order to the flat parameter for layer `name`: weight
+        [256 stored units][x_cols stored columns] (-1: padding column) and bias [256 stored]."""
+        maps = self._flat_maps.get(name)
+        if maps is None:
+            m, iu = self.mlp, self.inv_chain
+            off, o, i = m.slices[name]
+            fi = (iu[:, None] * x_cols + ix[None, :]).reshape(-1)   # stored index of each reference weight
+            dw = torch.full((o * x_cols,), -1, dtype=torch.int32, device=self.device)
+            dw[fi] = (off + torch.arange(o * i, device=self.device)).to(torch.int32)
+            db = torch.full((o,), -1, dtype=torch.int32, device=self.device)
+            db[iu] = (off + o * i + torch.arange(o, device=self.device)).to(torch.int32)
+            maps = self._flat_maps[name] = (dw, db)
+        return maps
+
     def _weight_grads(self, rows, scale, q=None):
-        """dW_l = delta_l^T x_l (fp16 GEMM, fp32 out), db_l = sum delta_l, unpermuted."""
+        """dW_l = delta_l^T x_l (fp16 GEMM, fp32 split-K partials), db_l = sum delta_l; the partials
+        summed, unscaled and unpermuted into the flat gradient by one sgn_grad_accumulate launch."""
         m = self.mlp
         g = m.flat.grad
-        inv = 1.0 / scale
-        iu = self.inv_chain
+        L = _lib.lib()
+        st = _lib.stream_handle()
         rp = ((rows + 1023) // 1024) * 1024   # rows padded to the split-K batch (buffers are)
         chunk = max(DW_CHUNK, -(-rp // 512))  # at most 512 batches (no ragged tail up to 512 * DW_CHUNK rows)
-        if rp > rows:
-            for t in self.d + [self.x0, self.h1, self.h2, self.h3] + ([self.h2b, self.db] if self.sg else []):
-                t[rows:rp].zero_()             # stale tails must not reach the GEMM (0 * NaN)
-        # db_l = column sums of the delta tiles (+ block2_bpnet's for SG), in one pair of launches
+        if rp > rows:                          # stale tails must not reach the GEMM (0 * NaN): one clear launch
+            tails = [t[rows:rp] for t in self.d + [self.x0, self.h1, self.h2, self.h3]
+                     + ([self.h2b, self.db] if self.sg else [])]
+            _lib.check(L.sgn_zero_segments(len(tails), (ctypes.c_void_p * len(tails))(*(t.data_ptr() for t in tails)),
+                                           (ctypes.c_int64 * len(tails))(*(t.numel() * t.element_size() for t in tails)),
+                                           st),
+                       "sgn_zero_segments")
+        # db_l = column sums of the delta tiles (+ block2_bpnet's for SG) and the alpha branch's
+        # dWa = dza^T h4 (row-weighted column sums), in one pair of launches
         nd = 5 if self.sg else 4
         if not hasattr(self, "_cs_out"):
-            self._cs_ws = torch.empty(int(_lib.lib().sgn_colsum_workspace_bytes(nd)) // 4, dtype=torch.float32,
+            self._cs_ws = torch.empty(int(L.sgn_colsum_workspace_bytes(nd + 1)) // 4, dtype=torch.float32,
                                       device=self.device)
-            self._cs_out = torch.empty(nd, 256, dtype=torch.float32, device=self.device)
-        dl = [self.d[3], self.d[2], self.d[1], self.d[0]] + ([self.db] if self.sg else [])
-        ds = (ctypes.c_void_p * nd)(*(t.data_ptr() for t in dl))
-        _lib.check(_lib.lib().sgn_colsum_f16(nd, ds, rows, 256, _lib.ptr(self._cs_ws), _lib.ptr(self._cs_out),
-                                             _lib.stream_handle()), "sgn_colsum_f16")
+            self._cs_out = torch.empty(nd + 1, 256, dtype=torch.float32, device=self.device)
+        dl = [self.d[3], self.d[2], self.d[1], self.d[0]] + ([self.db] if self.sg else []) + [self.h4]
+        ds = (ctypes.c_void_p * (nd + 1))(*(t.data_ptr() for t in dl))
+        rw = (ctypes.c_void_p * (nd + 1))(*([None] * nd + [self.dza.data_ptr()]))
+        _lib.check(L.sgn_colsum_f16_weighted(nd + 1, ds, rw, rows, 256, _lib.ptr(self._cs_ws), _lib.ptr(self._cs_out),
+                                             st), "sgn_colsum_f16_weighted")
+        segs, keep = [], []
+
+        def add(src, tail, dst):
+            keep.append((src, tail))
+            n = dst.numel()
+            segs.append(_lib.GradSegment(src.data_ptr(), tail.data_ptr() if tail is not None else None,
+                                         dst.data_ptr(), n, n, src.numel() // n, 0))
         if self.sg:
             # block2_bpnet.0: x = [h (chain order) | the row's BPNet embedding (natural order)]
             x = self.h2b[:rp]
@@ -750,31 +821,29 @@ class HipTrainer:
                 bp = self.bpnet16[torch.clamp(pid, min=0)]
                 bp = torch.where((ok & (pid >= 0))[:, None], bp, torch.zeros((), dtype=bp.dtype, device=bp.device))
                 x = torch.cat([x, bp], dim=1)
-            G = _gemm_rows_f32(self.db[:rp], x, chunk)
-            fi = self._flat_maps.get(BPNET)
-            if fi is None:
-                ix = torch.cat([self.inv_chain, 256 + torch.arange(self.variant[1], device=self.device)])
-                fi = (iu[:, None] * x.shape[1] + ix[None, :]).reshape(-1)
-                self._flat_maps[BPNET] = fi
-            m.w(BPNET, g).addcmul_(G.view(-1).index_select(0, fi).view(m.w(BPNET, g).shape), inv)
-            m.b(BPNET, g).addcmul_(self._cs_out[4].index_select(0, iu), inv)
+            ix = torch.cat([self.inv_chain, 256 + torch.arange(self.variant[1], device=self.device)])
+            dw, db = self._dst_maps(BPNET, x.shape[1], ix)
+            add(*_gemm_rows_parts(self.db[:rp], x, chunk), dw)
+            add(self._cs_out[4], None, db)
         for li, (name, d, x, ix) in enumerate((("block3.2", self.d[3], self.h3, self.inv_chain),
                                                ("block3.0", self.d[2], self.h2, self.inv_h2),
                                                ("block1.2", self.d[1], self.h1, self.inv_chain),
                                                ("block1.0", self.d[0], self.x0, self.inv_x0))):
-            dr, xr = d[:rp], x[:rp]
-            G = _gemm_rows_f32(dr, xr, chunk)    # [256 stored][C stored]
-            fi = self._flat_maps.get(name)
-            if fi is None:                       # stored (unit, column) of each reference weight
-                fi = (iu[:, None] * x.shape[1] + ix[None, :]).reshape(-1)
-                self._flat_maps[name] = fi
-            w = m.w(name, g)
-            w.addcmul_(G.view(-1).index_select(0, fi).view(w.shape), inv)   # gather, no scatter
-            m.b(name, g).addcmul_(self._cs_out[li].index_select(0, iu), inv)
+            dw, db = self._dst_maps(name, x.shape[1], ix)
+            add(*_gemm_rows_parts(d[:rp], x[:rp], chunk), dw)    # [256 stored][C stored]
+            add(self._cs_out[li], None, db)
         # alpha branch: dWa = dza^T h4, dba = sum dza
-        ga = _mm_f32(self.dza[:rows].to(torch.float16)[None, :], self.h4[:rows])[0]
-        m.w("alpha_branch.0", g)[0].add_(ga[iu] * inv)
-        m.b("alpha_branch.0", g).add_(self.dza[:rows].sum() * inv)
+        amaps = self._flat_maps.get("alpha_branch.0")
+        if amaps is None:
+            off, o, i = m.slices["alpha_branch.0"]
+            dwa = torch.empty(256, dtype=torch.int32, device=self.device)
+            dwa[self.inv_chain] = (off + torch.arange(256, device=self.device)).to(torch.int32)
+            amaps = self._flat_maps["alpha_branch.0"] = (dwa, torch.full((1,), off + i, dtype=torch.int32,
+                                                                        device=self.device))
+        add(self._cs_out[nd], None, amaps[0])
+        add(self.dza[:rows].sum().reshape(1), None, amaps[1])
+        _lib.check(L.sgn_grad_accumulate(len(segs), (_lib.GradSegment * len(segs))(*segs), _lib.ptr(scale),
+                                         _lib.ptr(g), st), "sgn_grad_accumulate")
 
     def allreduce_grads(self, params):
         _allreduce_buckets([p.grad for p in params if p.grad is not None], self.bucket_elems)

@@ -98,6 +98,24 @@ def test_argument_errors_are_reported_without_gpu():
     lp.K = 0
     rc = L.sgn_loss_train(ctypes.byref(lp), *args, fake, 1 << 20, None)
     assert rc != 0 and b"positive" in L.sgn_last_error()
+    # training segment kernels: segment count, per-segment shapes, alignment
+    gs = (_lib.GradSegment * 17)()
+    rc = L.sgn_grad_accumulate(17, gs, None, fake, None)
+    assert rc != 0 and b"n_seg" in L.sgn_last_error()
+    gs[0] = _lib.GradSegment(16, None, 16, 256, 128, 1, 0)
+    rc = L.sgn_grad_accumulate(1, gs, None, fake, None)
+    assert rc != 0 and b"stride >= n" in L.sgn_last_error()
+    gs[0] = _lib.GradSegment(None, None, 16, 256, 256, 1, 0)
+    rc = L.sgn_grad_accumulate(1, gs, None, fake, None)
+    assert rc != 0 and b"null" in L.sgn_last_error()
+    rc = L.sgn_zero_segments(1, (ctypes.c_void_p * 1)(20), (ctypes.c_int64 * 1)(64), None)
+    assert rc != 0 and b"aligned" in L.sgn_last_error()
+    rc = L.sgn_zero_segments(1, (ctypes.c_void_p * 1)(16), (ctypes.c_int64 * 1)(60), None)
+    assert rc != 0 and b"multiples of 16" in L.sgn_last_error()
+    gt = (_lib.GatherSegment * 1)(_lib.GatherSegment(None, 16, 8, 1, 0))
+    rc = L.sgn_gather_segments(1, gt, fake, 8, None)
+    assert rc != 0 and b"bad segment" in L.sgn_last_error()
+    assert L.sgn_grad_accumulate(0, None, None, None, None) == 0   # nothing to do: no launch
 
 
 # ---- options ------------------------------------------------------------------------

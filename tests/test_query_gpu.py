@@ -108,6 +108,22 @@ def test_query_parity_jittered_rays(room, march, monkeypatch):
     _check(og, g, res, ref, o)
 
 
+@pytest.mark.parametrize("R,D", [(1, 1), (3, 64), (257, 400), (4096, 400)])
+def test_depth_table_jitter_hip_matches_torch(R, D):
+    """sgn_depth_table_jitter against raygen.depth_table (the torch restatement of
+    near_far_linear_ray_generation) on the same torch.rand draw: the cumsum's order differs (wave
+    scan vs torch's scan), so within 4 ulp of far (4.8e-6 at 8.0); strictly increasing per ray."""
+    from sgnerf_amd.querier import depth_table_jitter_hip
+    from sgnerf_amd.raygen import depth_table
+    t = depth_table_jitter_hip(0.1, 8.0, D, 0.3, R, DEV, generator=torch.Generator(DEV).manual_seed(7))
+    ref = depth_table(0.1, 8.0, D, jitter=0.3, R=R, device=DEV, generator=torch.Generator(DEV).manual_seed(7))
+    assert t.shape == ref.shape == (R, D)
+    assert float((t - ref).abs().max()) <= 4.8e-6
+    if D > 1:
+        assert bool((t[:, 1:] > t[:, :-1]).all())
+    assert float(t.min()) > 0.1
+
+
 @pytest.mark.parametrize("seconds", [3, 11])
 def test_query_parity_semantic(room, seconds):
     o = mkopts(semantic_guidance=1)
