@@ -146,7 +146,8 @@ def _dw_rows(gz, x, chunk=DW_CHUNK_F32):
     return g
 
 
-def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, samp_locw, pidx, saved=None):
+def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, samp_locw, pidx, saved=None,
+              rows=None):
     """Differentiable PointAggregator.forward on sample-major neighbours.
     Returns feat [S,4] (alpha, r, g, b; zeros for samples without neighbours), conf_coefficient
     [S,K] (straight-through clamp) and the neighbour mask [S,K].
@@ -154,7 +155,11 @@ def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, 
     saved = (z1, z2, z3): the pre-activations of block1.0, block1.2 and block3.0 per row s * K + k
     ([>= S K, 256] fp32, from sgn_aggregate_train_fwd_f32): those three layers then take their
     forward values from there (_SavedLinear) instead of recomputing them, with the same fp32
-    backward."""
+    backward.
+
+    rows: the valid rows s * K + k in order (torch.nonzero of pidx >= 0), when the caller has them
+    without a host sync (nonzero_static with a device-side count); else computed here (one sync).
+    Every masked selection goes through them (index_select / index_copy, no further syncs)."""
     S, K = pidx.shape
     mask = pidx >= 0
     flat = torch.clamp(pidx, min=0).reshape(-1).long()
@@ -175,24 +180,25 @@ def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, 
     vpe = _pe(v, 4, ori=True)
     ori_v, vpe = vpe[..., :3], vpe[..., 3:]
     m = mask.reshape(-1)
-    fm = flat[m]  # index_select: its backward is an index_add (atomics), not a sort-based index_put
+    if rows is None:
+        rows = torch.nonzero(m).reshape(-1)   # the valid rows s * K + k, in the order of m
+    fm = flat.index_select(0, rows)  # index_select: its backward is an index_add (atomics), not a sort-based index_put
     emb = torch.index_select(points.points_embeding, 0, fm)
-    x = torch.cat([emb, _pe(emb, 3), _pe(dists.reshape(-1, 6)[m], 5)], dim=-1)
+    x = torch.cat([emb, _pe(emb, 3), _pe(dists.reshape(-1, 6).index_select(0, rows), 5)], dim=-1)
     lr_ = lambda t: F.leaky_relu(t, 0.01)  # noqa: E731
     if saved is not None:
-        rows = torch.nonzero(m).reshape(-1)   # the valid rows s * K + k, in the order of m
         zs = [z.index_select(0, rows) for z in saved]
         lin = lambda name, t, zi: _SavedLinear.apply(t, mlp.w(name), mlp.b(name), zs[zi])  # noqa: E731
     else:
         lin = lambda name, t, zi: mlp.f(name, t)  # noqa: E731
     h = lr_(lin("block1.2", lr_(lin("block1.0", x, 0)), 1))
     sd = torch.index_select(points.points_dir, 0, fm)
-    ov = ori_v[:, None, :].expand(S, K, 3).reshape(-1, 3)[m]
+    ov = ori_v[:, None, :].expand(S, K, 3).reshape(-1, 3).index_select(0, rows)
     h = torch.cat([h, torch.index_select(points.points_color, 0, fm), sd - ov, torch.sum(sd * ov, dim=-1, keepdim=True)], dim=-1)
     h = lr_(_LinearRows.apply(lr_(lin("block3.0", h, 2)), mlp.w("block3.2"), mlp.b("block3.2")))
     alpha = F.softplus(mlp.f("alpha_branch.0", h) - 1)
-    hk = torch.zeros(S * K, h.shape[-1], device=h.device, dtype=h.dtype).masked_scatter(m[:, None], h)
-    ak = torch.zeros(S * K, 1, device=h.device, dtype=h.dtype).masked_scatter(m[:, None], alpha)
+    hk = torch.zeros(S * K, h.shape[-1], device=h.device, dtype=h.dtype).index_copy(0, rows, h)
+    ak = torch.zeros(S * K, 1, device=h.device, dtype=h.dtype).index_copy(0, rows, alpha)
     fs = torch.sum(hk.view(S, K, -1) * w[..., None], dim=1)
     a_s = torch.sum(ak.view(S, K, 1) * w[..., None], dim=1)
     c = torch.cat([fs, vpe], dim=-1)
