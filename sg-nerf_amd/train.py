@@ -130,6 +130,39 @@ class _LinearRows(torch.autograd.Function):
         return gz @ w, _dw_rows(gz, x), gz.sum(0)
 
 
+class _LinearSink(torch.autograd.Function):
+    """z = x W^T + b (or the z computed elsewhere, passed in a one-element list) whose weight and
+    bias gradients the backward hands to `sink(gz, x)` -- which adds them into the trainer's flat
+    gradient -- instead of returning them through autograd (autograd through views of a flat
+    parameter zero-fills a full-size gradient per view, copies the slice in and adds it)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, sink, zbox):
+        ctx.save_for_backward(x, w)
+        ctx.sink = sink
+        return zbox[0] if zbox is not None else F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, w = ctx.saved_tensors
+        gz = gz.contiguous()
+        ctx.sink(gz, x)
+        return (gz @ w if ctx.needs_input_grad[0] else None), None, None, None, None
+
+
+def _linear(mlp, name, x, z=None, split=False):
+    """One aggregator layer: through the mlp's gradient sink when it has one (the HIP trainer's flat
+    parameter), else _SavedLinear (z given) / _LinearRows (split-K dW) / nn.Linear."""
+    sink = mlp.grad_sink(name) if hasattr(mlp, "grad_sink") else None
+    if sink is not None:
+        return _LinearSink.apply(x, mlp.w(name).detach(), mlp.b(name).detach(), sink, None if z is None else [z])
+    if z is not None:
+        return _SavedLinear.apply(x, mlp.w(name), mlp.b(name), z)
+    if split:
+        return _LinearRows.apply(x, mlp.w(name), mlp.b(name))
+    return mlp.f(name, x)
+
+
 def _dw_rows(gz, x, chunk=DW_CHUNK_F32):
     """gz^T x over the row dimension (fp32): the rows in `chunk`-row batches through one batched
     GEMM, the partials summed (a [256 x C] output of a plain GEMM with K = tens of thousands of rows
@@ -188,21 +221,21 @@ def aggregate(points: PointParams, mlp: ViewMLP, campos, rot, raydir, samp_ray, 
     lr_ = lambda t: F.leaky_relu(t, 0.01)  # noqa: E731
     if saved is not None:
         zs = [z.index_select(0, rows) for z in saved]
-        lin = lambda name, t, zi: _SavedLinear.apply(t, mlp.w(name), mlp.b(name), zs[zi])  # noqa: E731
+        lin = lambda name, t, zi: _linear(mlp, name, t, z=zs[zi])  # noqa: E731
     else:
-        lin = lambda name, t, zi: mlp.f(name, t)  # noqa: E731
+        lin = lambda name, t, zi: _linear(mlp, name, t)  # noqa: E731
     h = lr_(lin("block1.2", lr_(lin("block1.0", x, 0)), 1))
     sd = torch.index_select(points.points_dir, 0, fm)
     ov = ori_v[:, None, :].expand(S, K, 3).reshape(-1, 3).index_select(0, rows)
     h = torch.cat([h, torch.index_select(points.points_color, 0, fm), sd - ov, torch.sum(sd * ov, dim=-1, keepdim=True)], dim=-1)
-    h = lr_(_LinearRows.apply(lr_(lin("block3.0", h, 2)), mlp.w("block3.2"), mlp.b("block3.2")))
+    h = lr_(_linear(mlp, "block3.2", lr_(lin("block3.0", h, 2)), split=True))
     alpha = F.softplus(mlp.f("alpha_branch.0", h) - 1)
     hk = torch.zeros(S * K, h.shape[-1], device=h.device, dtype=h.dtype).index_copy(0, rows, h)
     ak = torch.zeros(S * K, 1, device=h.device, dtype=h.dtype).index_copy(0, rows, alpha)
     fs = torch.sum(hk.view(S, K, -1) * w[..., None], dim=1)
     a_s = torch.sum(ak.view(S, K, 1) * w[..., None], dim=1)
     c = torch.cat([fs, vpe], dim=-1)
-    lin_r = lambda name, t: _LinearRows.apply(t, mlp.w(name), mlp.b(name))  # noqa: E731  (split-K dW)
+    lin_r = lambda name, t: _linear(mlp, name, t, split=True)  # noqa: E731  (split-K dW)
     c = lr_(lin_r("color_branch.0", c))
     c = lr_(lin_r("color_branch.2", c))
     c = lr_(lin_r("color_branch.4", c))

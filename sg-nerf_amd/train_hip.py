@@ -62,6 +62,7 @@ class FlatMLP(nn.Module):
             self.slices[name] = (off, o, i)
             off += o * i + o
         self.flat = nn.Parameter(torch.cat(parts).to(device))
+        self._dst = {}   # grad_sink: flat-gradient index maps per layer
 
     def w(self, name, t=None):
         off, o, i = self.slices[name]
@@ -73,6 +74,24 @@ class FlatMLP(nn.Module):
 
     def f(self, name, x):
         return F.linear(x, self.w(name), self.b(name))
+
+    def grad_sink(self, name):
+        """For train.aggregate (the fp32 step): a callable adding a layer's dW = gz^T x (split-K
+        partials, one sgn_grad_accumulate launch) and db = sum gz into flat.grad; None for the
+        alpha branch (one output unit: its dW stays an autograd GEMM, not an M = 1 batched GEMM)."""
+        off, o, i = self.slices[name]
+        g = self.flat.grad
+        if g is None or o < 16:
+            return None
+        dst = self._dst.get(name)
+        if dst is None:
+            dst = self._dst[name] = (off + torch.arange(o * i, device=g.device)).to(torch.int32)
+
+        def sink(gz, x):
+            parts, tail = _fp32_rows_parts(gz, x, DW_CHUNK_COLOUR)
+            _grad_into(g, dst, parts, tail)
+            g[off + o * i:off + o * i + o].add_(gz.sum(0))
+        return sink
 
     def state(self):
         out = {}
