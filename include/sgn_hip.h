@@ -396,6 +396,16 @@ typedef struct {
 } sgn_gather_segment;
 int sgn_gather_segments(int32_t n_seg, const sgn_gather_segment *segs, const float *d_src, int64_t n_src,
                         sgn_stream_t stream);
+/* The fp32-faithful blob (sgn_mlp_pack_f32's layout) re-packed on the device from the flat fp32
+ * parameter each training step: per layer l (w_off / w_len: host arrays, the weight span of layer
+ * l in the flat vector, n_layers <= 16) the shift s_l = 14 - e, max |W_l| = f 2^e (frexp); then
+ * the fp16 section (d_code16[j] = flat index | layer << 22 | lo << 26, -1 = zero: hi = fp16(W 2^s),
+ * lo = fp16(W 2^s - hi)) and the fp32 section (d_code32[j] = flat index | layer << 22 | kind << 26,
+ * kinds as the layout's sgn_mlp_pack_index_f32 map).  d_shift: int32[16] device scratch.  Bit-equal
+ * to sgn_mlp_pack_f32 on the same weights. */
+int sgn_pack_scaled_f32(const float *d_flat, int64_t n_flat, int32_t n_layers, const int64_t *w_off,
+                        const int64_t *w_len, const int32_t *d_code16, int64_t n16, const int32_t *d_code32, int64_t n32,
+                        int32_t *d_shift, void *d_out16, float *d_out32, sgn_stream_t stream);
 /* The backward's power-of-two loss scale: d_out[0] = 2^-floor(log2(max(max|a|, max|b|, 1e-30)))
  * over two fp32 device arrays (a NaN propagates), in two launches with no host sync; d_ws:
  * sgn_pow2_scale_workspace_bytes() of device scratch. */

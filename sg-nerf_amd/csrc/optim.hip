@@ -272,6 +272,64 @@ __global__ __launch_bounds__(256) void k_pow2_scale(const uint32_t *ws, float *o
     }
 }
 
+// ---- fp32-faithful blob re-pack from the flat parameter (one shift launch + one pack launch) --
+// per layer l: s_l = 14 - e with max |W_l| = f 2^e (frexp; 0 for an all-zero or non-finite max),
+// then per fp16 fragment element v = W 2^s_l, hi = fp16(v), lo = fp16(v - hi), and the fp32
+// section by kind (mlp_x3.hip Y32Kind: weight, bias, bias 2^s, 2^-s, 1, weight 2^-s_3).
+constexpr int kMaxPackLayers = 16;
+
+struct PackArgs {
+    const float *flat;
+    int64_t woff[kMaxPackLayers], wlen[kMaxPackLayers];
+    const int32_t *code16, *code32;
+    int64_t n16, n32;
+    int32_t *shift;
+    __half *out16;
+    float *out32;
+};
+
+__global__ __launch_bounds__(256) void k_layer_shift(PackArgs a) {
+    const float *w = a.flat + a.woff[blockIdx.x];
+    const int64_t n = a.wlen[blockIdx.x];
+    uint32_t m = 0;
+    for (int64_t i = threadIdx.x; i < n; i += 256) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
+    m = block_max_u32(m);
+    if (threadIdx.x == 0) {
+        const float f = __uint_as_float(m);
+        int e = 0;
+        if (f > 0.f && __builtin_isfinite(f)) frexpf(f, &e);
+        a.shift[blockIdx.x] = (f > 0.f && __builtin_isfinite(f)) ? 14 - e : 0;
+    }
+}
+
+// codes: fp16 element idx | layer << 22 | lo << 26 (-1: zero); fp32 element idx | layer << 22 | kind << 26
+__global__ __launch_bounds__(256) void k_pack_scaled(PackArgs a) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.y == 0) {
+        if (j >= a.n16) return;
+        const int32_t c = a.code16[j];
+        float v = 0.f;
+        if (c >= 0) v = a.flat[c & 0x3fffff] * ldexpf(1.f, a.shift[(c >> 22) & 15]);
+        const __half hi = __float2half_rn(v);
+        a.out16[j] = (c >= 0 && ((c >> 26) & 1)) ? __float2half_rn(v - __half2float(hi)) : hi;
+        return;
+    }
+    if (j >= a.n32) return;
+    const int32_t c = a.code32[j];
+    const int idx = c & 0x3fffff, l = (c >> 22) & 15, k = (c >> 26) & 7;
+    float y = 0.f;
+    switch (k) {
+    case 1: y = a.flat[idx]; break;                                   // YK_W
+    case 2: y = a.flat[idx]; break;                                   // YK_B
+    case 3: y = a.flat[idx] * ldexpf(1.f, a.shift[l]); break;         // YK_BS
+    case 4: y = ldexpf(1.f, -a.shift[l]); break;                      // YK_INV
+    case 5: y = 1.f; break;                                           // YK_ONE
+    case 6: y = a.flat[idx] * ldexpf(1.f, -a.shift[3]); break;        // YK_WINV
+    default: break;                                                   // YK_ZERO
+    }
+    a.out32[j] = y;
+}
+
 }  // namespace
 }  // namespace sgn
 
@@ -416,6 +474,37 @@ int sgn_gather_segments(int32_t n_seg, const sgn_gather_segment *segs, const flo
     a.n_src = n_src;
     hipLaunchKernelGGL(k_gather_segments, dim3((unsigned)((nmax + 255) / 256), n_seg), dim3(256), 0,
                        as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_pack_scaled_f32(const float *d_flat, int64_t n_flat, int32_t n_layers, const int64_t *w_off,
+                        const int64_t *w_len, const int32_t *d_code16, int64_t n16, const int32_t *d_code32, int64_t n32,
+                        int32_t *d_shift, void *d_out16, float *d_out32, sgn_stream_t stream) {
+    SGN_REQUIRE(n_layers >= 1 && n_layers <= kMaxPackLayers, "sgn_pack_scaled_f32: 1 <= n_layers <= 16");
+    SGN_REQUIRE(d_flat && w_off && w_len && d_shift && n16 >= 0 && n32 >= 0, "sgn_pack_scaled_f32: null argument");
+    SGN_REQUIRE(n_flat <= 0x3fffff, "sgn_pack_scaled_f32: flat parameter above 2^22 elements");
+    SGN_REQUIRE((n16 == 0 || (d_code16 && d_out16)) && (n32 == 0 || (d_code32 && d_out32)),
+                "sgn_pack_scaled_f32: null section buffer");
+    PackArgs a;
+    for (int l = 0; l < n_layers; ++l) {
+        SGN_REQUIRE(w_off[l] >= 0 && w_len[l] >= 0 && w_off[l] + w_len[l] <= n_flat,
+                    "sgn_pack_scaled_f32: layer span outside the flat parameter");
+        a.woff[l] = w_off[l];
+        a.wlen[l] = w_len[l];
+    }
+    a.flat = d_flat;
+    a.code16 = d_code16;
+    a.code32 = d_code32;
+    a.n16 = n16;
+    a.n32 = n32;
+    a.shift = d_shift;
+    a.out16 = static_cast<__half *>(d_out16);
+    a.out32 = d_out32;
+    hipLaunchKernelGGL(k_layer_shift, dim3(n_layers), dim3(256), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    const int64_t nmax = std::max<int64_t>(std::max(n16, n32), 1);
+    hipLaunchKernelGGL(k_pack_scaled, dim3((unsigned)((nmax + 255) / 256), 2), dim3(256), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

@@ -148,29 +148,27 @@ class _PackerF32:
         assert bool((e32[uses_w] < wlen[l32[uses_w]]).all() and (e32[uses_b] < blen[l32[uses_b]]).all())
         f16 = woff[l16] + e16
         assert int(f16.max()) < nflat and int(fw32.max()) < nflat and int(fb32.max()) < nflat
-        d = lambda t: t.to(device)  # noqa: E731
-        self.v16, self.lo16, self.l16, self.f16 = d(v16), d((c16 >> 30) & 1 == 1), d(l16), d(f16)
-        self.k32, self.l32, self.fw32, self.fb32 = d(k32), d(l32), d(fw32), d(fb32)
+        assert nflat < (1 << 22) and nl <= 16 and int(k32.max()) <= self.YK_WINV
+        # one int32 code per blob element for sgn_pack_scaled_f32: flat index | layer << 22 | lo / kind << 26
+        code16 = torch.where(v16, f16 | (l16 << 22) | (((c16 >> 30) & 1) << 26), -1)
+        code32 = torch.where(uses_w, fw32, fb32) | (l32 << 22) | (k32 << 26)
+        self.code16 = code16.to(torch.int32).to(device)
+        self.code32 = code32.to(torch.int32).to(device)
+        self.n_layers = nl
+        self.woff = (ctypes.c_int64 * nl)(*[int(a) for a, _ in self.wspan])
+        self.wlen = (ctypes.c_int64 * nl)(*[int(b - a) for a, b in self.wspan])
+        self.shift = torch.zeros(16, dtype=torch.int32, device=device)
         self.blob = torch.zeros(self.total, dtype=torch.uint8, device=device)
+        assert self.n16b == 2 * self.code16.numel() and self.n16b + 4 * self.code32.numel() <= self.total
 
     def pack(self, flat):
+        """Per-layer shifts and both blob sections from the flat parameter: two launches."""
         flat = flat.detach()
-        m = torch.stack([flat[a:b].abs().amax() for a, b in self.wspan])
-        _, e = torch.frexp(m)
-        sh = torch.where((m > 0) & torch.isfinite(m), 14 - e, torch.zeros_like(e)).float()
-        v = torch.where(self.v16, flat[self.f16] * torch.exp2(sh[self.l16]), 0.0)
-        hi = v.half()
-        lo = (v - hi.float()).half()
-        self.blob[:self.n16b].view(torch.float16).copy_(torch.where(self.lo16, lo, hi))
-        k, inv = self.k32, torch.exp2(-sh)
-        y = torch.zeros(k.shape, dtype=torch.float32, device=flat.device)
-        y = torch.where(k == self.YK_W, flat[self.fw32], y)
-        y = torch.where(k == self.YK_B, flat[self.fb32], y)
-        y = torch.where(k == self.YK_BS, flat[self.fb32] * torch.exp2(sh[self.l32]), y)
-        y = torch.where(k == self.YK_INV, inv[self.l32], y)
-        y = torch.where(k == self.YK_ONE, torch.ones_like(y), y)
-        y = torch.where(k == self.YK_WINV, flat[self.fw32] * inv[3], y)
-        self.blob[self.n16b:self.n16b + 4 * y.numel()].view(torch.float32).copy_(y)
+        assert flat.is_contiguous() and flat.dtype == torch.float32
+        _lib.check(_lib.lib().sgn_pack_scaled_f32(
+            _lib.ptr(flat), flat.numel(), self.n_layers, self.woff, self.wlen, _lib.ptr(self.code16), self.code16.numel(),
+            _lib.ptr(self.code32), self.code32.numel(), _lib.ptr(self.shift), _lib.ptr(self.blob[:self.n16b]),
+            _lib.ptr(self.blob[self.n16b:]), _lib.stream_handle()), "sgn_pack_scaled_f32")
         return self.blob
 
 

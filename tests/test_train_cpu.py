@@ -194,17 +194,39 @@ def test_gpu_training_gradients_match_cpu():
 
 
 @pytest.mark.parametrize("seed", [4, 9])
-def test_flat_pack_f32_matches_host_pack(seed):
-    """train_hip._PackerF32 (index gathers from the flat parameter + per-layer shifts, run here on
-    the CPU) against the C packer (pack_blob_x3 into host memory), byte for byte; the layers' weights
-    span several binades so every layer gets its own shift."""
+def test_flat_pack_f32_codes_match_host_pack(seed):
+    """train_hip._PackerF32's per-element codes (what sgn_pack_scaled_f32 decodes on the device),
+    decoded here on the CPU with the kernel's rules, against the C packer (pack_blob_x3 into host
+    memory), byte for byte; the layers' weights span several binades so every layer gets its own
+    shift.  The device kernel itself: tests/test_train_gpu.py::test_device_pack_f32_matches_host_pack."""
     from sgnerf_amd.train_hip import FlatMLP, _PackerF32
     from sgnerf_amd.weights import LAYERS, init_mlp, pack_mlp
     mlp = init_mlp(seed, bias_std=0.05)
     for i, (n, *_) in enumerate(LAYERS):
         mlp[n + ".weight"] = mlp[n + ".weight"] * 2.0 ** (3 - i)
     flat = FlatMLP(mlp, "cpu")
-    blob = _PackerF32("cpu", flat).pack(flat.flat)
+    pk = _PackerF32("cpu", flat)
+    f = flat.flat.detach()
+    sh = torch.zeros(16)
+    for li, (a, b) in enumerate(pk.wspan):
+        m = f[a:b].abs().max()
+        sh[li] = float(14 - int(torch.frexp(m)[1])) if bool(m > 0) and bool(torch.isfinite(m)) else 0.0
+    c = pk.code16.long()
+    ok = c >= 0
+    v = torch.where(ok, f[torch.where(ok, c & 0x3FFFFF, 0)] * torch.exp2(sh[(c >> 22) & 15]), 0.0)
+    hi = v.half()
+    out16 = torch.where(ok & ((c >> 26) & 1 == 1), (v - hi.float()).half(), hi)
+    c = pk.code32.long()
+    idx, l, k = c & 0x3FFFFF, (c >> 22) & 15, c >> 26
+    y = torch.zeros(c.shape)
+    y = torch.where((k == pk.YK_W) | (k == pk.YK_B), f[idx], y)
+    y = torch.where(k == pk.YK_BS, f[idx] * torch.exp2(sh[l]), y)
+    y = torch.where(k == pk.YK_INV, torch.exp2(-sh[l]), y)
+    y = torch.where(k == pk.YK_ONE, torch.ones_like(y), y)
+    y = torch.where(k == pk.YK_WINV, f[idx] * torch.exp2(-sh[3]), y)
+    blob = torch.zeros(pk.total, dtype=torch.uint8)
+    blob[:pk.n16b].view(torch.float16).copy_(out16)
+    blob[pk.n16b:pk.n16b + 4 * y.numel()].view(torch.float32).copy_(y)
     host = pack_mlp(mlp, "cpu", precision="f32")
     assert blob.numel() == host.numel()
     bad = torch.nonzero(blob != host).reshape(-1)
