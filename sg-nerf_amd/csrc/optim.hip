@@ -83,6 +83,28 @@ struct ColsumArgs {
     float *out;           // [count][256]
 };
 
+template <bool W>
+__device__ __forceinline__ void colsum_rows(const __half *x, const float *rw, int64_t r, int64_t r1, int c8,
+                                            float (&acc)[8]) {
+#pragma unroll 2
+    for (; r < r1; r += 8) {
+        const uint4 w = *reinterpret_cast<const uint4 *>(x + r * kColsumCols + c8 * 8);
+        const float s = W ? rw[r] : 1.f;
+        const __half2 *h = reinterpret_cast<const __half2 *>(&w);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float2 f = __half22float2(h[j]);
+            if (W) {
+                acc[2 * j] += f.x * s;
+                acc[2 * j + 1] += f.y * s;
+            } else {
+                acc[2 * j] += f.x;
+                acc[2 * j + 1] += f.y;
+            }
+        }
+    }
+}
+
 // grid (kColsumSlabs, count), 256 threads: 32 lanes x 8 columns cover a row, 8 rows at a time
 __global__ __launch_bounds__(256) void k_colsum_part(ColsumArgs a) {
     const int mat = blockIdx.y;
@@ -92,26 +114,10 @@ __global__ __launch_bounds__(256) void k_colsum_part(ColsumArgs a) {
     const __half *x = a.x[mat];
     const float *rw = a.rw[mat];
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int64_t r = r0 + r8; r < r1; r += 8) {
-        const uint4 w = *reinterpret_cast<const uint4 *>(x + r * kColsumCols + c8 * 8);
-        const __half2 *h = reinterpret_cast<const __half2 *>(&w);
-        if (rw) {
-            const float s = rw[r];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float2 f = __half22float2(h[j]);
-                acc[2 * j] += f.x * s;
-                acc[2 * j + 1] += f.y * s;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float2 f = __half22float2(h[j]);
-                acc[2 * j] += f.x;
-                acc[2 * j + 1] += f.y;
-            }
-        }
-    }
+    if (rw)   // workgroup-uniform: two loops, no branch inside
+        colsum_rows<true>(x, rw, r0 + r8, r1, c8, acc);
+    else
+        colsum_rows<false>(x, rw, r0 + r8, r1, c8, acc);
     __shared__ float red[8][kColsumCols];
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[r8][c8 * 8 + j] = acc[j];
