@@ -406,6 +406,13 @@ int sgn_gather_segments(int32_t n_seg, const sgn_gather_segment *segs, const flo
 int sgn_pack_scaled_f32(const float *d_flat, int64_t n_flat, int32_t n_layers, const int64_t *w_off,
                         const int64_t *w_len, const int32_t *d_code16, int64_t n16, const int32_t *d_code32, int64_t n32,
                         int32_t *d_shift, void *d_out16, float *d_out32, sgn_stream_t stream);
+/* The f16 training step's captured loss stage inputs over its item capacity n_cap: for item
+ * i < d_counters[1] (sgn_query's work-item count) d_fs32[i] = fp32 of d_fs16[i] ([n_cap][256] fp16,
+ * sgn_aggregate_train_fwd's blended features), d_al32[i] = d_feat[work[i]].alpha, d_v[i] = the
+ * direction of the item's ray, d_samp[i] = work[i]; padding items get zeros, ray 0 and s_cap. */
+int sgn_colour_inputs(const int32_t *d_counters, const int32_t *d_work, const int32_t *d_samp_ray, int64_t n_cap,
+                      int64_t s_cap, const void *d_fs16, const float *d_feat, const float *d_raydir, float *d_fs32,
+                      float *d_al32, float *d_v, int32_t *d_samp, sgn_stream_t stream);
 /* The backward's power-of-two loss scale: d_out[0] = 2^-floor(log2(max(max|a|, max|b|, 1e-30)))
  * over two fp32 device arrays (a NaN propagates), in two launches with no host sync; d_ws:
  * sgn_pow2_scale_workspace_bytes() of device scratch. */

@@ -130,6 +130,7 @@ SIGNATURES = {
     "sgn_gather_segments": (c_i32, [c_i32, ctypes.POINTER(GatherSegment), c_vp, c_i64, c_vp]),
     "sgn_pack_scaled_f32": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_vp, c_i64, c_vp,
                                     c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_colour_inputs": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_pow2_scale_workspace_bytes": (c_sz, []),
     "sgn_pow2_scale": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "sgn_mlp_packed_bytes_f32": (c_sz, [c_i32, c_i32]),

@@ -336,6 +336,47 @@ __global__ __launch_bounds__(256) void k_pack_scaled(PackArgs a) {
     a.out32[j] = y;
 }
 
+// ---- the captured loss stage's inputs over the batch's item capacity: item i < counters[1] takes
+// its blended features (fp16 -> fp32), its sample's alpha, its ray's direction and its sample id;
+// padding items zeros, ray 0 and the sentinel sample s_cap.  32 threads per item (8 columns each).
+struct ColourInArgs {
+    const int32_t *counters, *work, *samp_ray;
+    int64_t n_cap, s_cap;
+    const __half *fs16;
+    const float *feat, *raydir;
+    float *fs32, *al32, *v;
+    int32_t *samp;
+};
+
+__global__ __launch_bounds__(256) void k_colour_inputs(ColourInArgs a) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = t >> 5;
+    const int c8 = (int)(t & 31);
+    if (i >= a.n_cap) return;
+    const bool ok = i < (int64_t)a.counters[1];
+    float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+    if (ok) {
+        const uint4 w = *reinterpret_cast<const uint4 *>(a.fs16 + i * 256 + c8 * 8);
+        const __half2 *h = reinterpret_cast<const __half2 *>(&w);
+        const float2 f0 = __half22float2(h[0]), f1 = __half22float2(h[1]), f2 = __half22float2(h[2]),
+                     f3 = __half22float2(h[3]);
+        lo = make_float4(f0.x, f0.y, f1.x, f1.y);
+        hi = make_float4(f2.x, f2.y, f3.x, f3.y);
+    }
+    float4 *o = reinterpret_cast<float4 *>(a.fs32 + i * 256 + c8 * 8);
+    o[0] = lo;
+    o[1] = hi;
+    if (c8 == 0) {
+        const int32_t s = ok ? a.work[i] : 0;
+        const int64_t r = ok ? (int64_t)a.samp_ray[s] : 0;
+        a.al32[i] = ok ? a.feat[(int64_t)s * 4] : 0.f;
+        a.v[i * 3 + 0] = a.raydir[r * 3 + 0];
+        a.v[i * 3 + 1] = a.raydir[r * 3 + 1];
+        a.v[i * 3 + 2] = a.raydir[r * 3 + 2];
+        a.samp[i] = ok ? s : (int32_t)a.s_cap;
+    }
+}
+
 }  // namespace
 }  // namespace sgn
 
@@ -511,6 +552,33 @@ int sgn_pack_scaled_f32(const float *d_flat, int64_t n_flat, int32_t n_layers, c
     SGN_CHECK_HIP(hipGetLastError());
     const int64_t nmax = std::max<int64_t>(std::max(n16, n32), 1);
     hipLaunchKernelGGL(k_pack_scaled, dim3((unsigned)((nmax + 255) / 256), 2), dim3(256), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_colour_inputs(const int32_t *d_counters, const int32_t *d_work, const int32_t *d_samp_ray, int64_t n_cap,
+                      int64_t s_cap, const void *d_fs16, const float *d_feat, const float *d_raydir, float *d_fs32,
+                      float *d_al32, float *d_v, int32_t *d_samp, sgn_stream_t stream) {
+    SGN_REQUIRE(n_cap >= 0 && s_cap >= 0 && s_cap < 0x7fffffff, "sgn_colour_inputs: bad capacity");
+    if (n_cap == 0) return 0;
+    SGN_REQUIRE(d_counters && d_work && d_samp_ray && d_fs16 && d_feat && d_raydir && d_fs32 && d_al32 && d_v && d_samp,
+                "sgn_colour_inputs: null buffer");
+    SGN_REQUIRE(!(reinterpret_cast<uintptr_t>(d_fs16) & 15) && !(reinterpret_cast<uintptr_t>(d_fs32) & 15),
+                "sgn_colour_inputs: feature rows must be 16-B aligned");
+    ColourInArgs a;
+    a.counters = d_counters;
+    a.work = d_work;
+    a.samp_ray = d_samp_ray;
+    a.n_cap = n_cap;
+    a.s_cap = s_cap;
+    a.fs16 = static_cast<const __half *>(d_fs16);
+    a.feat = d_feat;
+    a.raydir = d_raydir;
+    a.fs32 = d_fs32;
+    a.al32 = d_al32;
+    a.v = d_v;
+    a.samp = d_samp;
+    hipLaunchKernelGGL(k_colour_inputs, dim3((unsigned)((n_cap * 32 + 255) / 256)), dim3(256), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

@@ -698,28 +698,23 @@ class HipTrainer:
         o, dev, R = self.opts, self.device, st["R"]
         Sc, Nc = st["Sc"], st["Nc"]             # sample / item capacity of this graph
         q = st["q"]
-        ok_i = st["ar"][:Nc] < q.counters[1]
-        work = q.work[:Nc]
-        samp = torch.where(ok_i, work, Sc)      # padding items -> sentinel sample Sc
-        samp_c = torch.where(ok_i, work, 0)
-        fs32, al32 = st["fs32"], st["al32"]
-        with torch.no_grad():
-            fs32.copy_(torch.where(ok_i[:, None], self.fs[:Nc].float(), 0.0))
-            al32.copy_(torch.where(ok_i, self.feat[:, 0][samp_c], 0.0))
+        fs32, al32, v, samp = st["fs32"], st["al32"], st["v"], st["samp"]
+        # one launch: items past the device count n are padding (zeros, ray 0, sentinel sample Sc)
+        _lib.check(_lib.lib().sgn_colour_inputs(_lib.ptr(q.counters), _lib.ptr(q.work), _lib.ptr(q.samp_ray), Nc, Sc,
+                                                _lib.ptr(self.fs), _lib.ptr(self.feat), _lib.ptr(st["raydir"]),
+                                                _lib.ptr(fs32), _lib.ptr(al32), _lib.ptr(v), _lib.ptr(samp),
+                                                _lib.stream_handle()), "sgn_colour_inputs")
         fs32.grad = al32.grad = None   # backward assigns fresh (graph-pool) gradients: no clear, no accumulate
-        # padding items read sample 0's ray, which is unwritten when the step has no samples:
-        # mask the gathered ray index too, so the raydir gather stays in bounds
-        v = st["raydir"][torch.where(ok_i, q.samp_ray[:Sc][samp_c], 0)]
         feat_s = torch.cat([al32[:, None], self._colour(fs32, v)], dim=-1)   # colour grads -> flat.grad
         featS = torch.zeros(Sc + 1, 4, device=dev).index_put((samp,), feat_s)[:Sc]
-        validS = torch.zeros(Sc + 1, dtype=torch.bool, device=dev).index_put((samp,), st["true"])[:Sc]
-        qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:Sc],
-              "samp_locw": q.samp_locw[:Sc * 3].view(Sc, 3), "pidx": q.pidx[:Sc * o.K].view(Sc, o.K)}
         if self.hip_loss:
             # the graph's own loss stage: its workspace lives as long as the captured graph that uses it
             total, parts, full, ray_mask = st["loss"](self.points, st["qabi"], featS, st["campos"], st["rot"],
                                                       st["gt"], o, R)
         else:
+            validS = torch.zeros(Sc + 1, dtype=torch.bool, device=dev).index_put((samp,), st["true"])[:Sc]
+            qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:Sc],
+                  "samp_locw": q.samp_locw[:Sc * 3].view(Sc, 3), "pidx": q.pidx[:Sc * o.K].view(Sc, o.K)}
             total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, st["campos"], st["rot"],
                                                             st["raydir"], st["gt"], o, s_count=q.counters[0])
         total.backward()
@@ -748,12 +743,12 @@ class HipTrainer:
             if len(self._graphs) >= GRAPH_CACHE:
                 self._graphs.pop(next(iter(self._graphs)))
             st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "qabi": q.abi(), "loss": LossStage(dev),
-                  "ar": torch.arange(Sc, device=dev),
                   "true": torch.ones((), dtype=torch.bool, device=dev),
                   "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
                   "campos": campos.clone(), "rot": rot.clone(),
                   "fs32": torch.zeros(Nc, 256, device=dev, requires_grad=True),
-                  "al32": torch.zeros(Nc, device=dev, requires_grad=True)}
+                  "al32": torch.zeros(Nc, device=dev, requires_grad=True),
+                  "v": torch.zeros(Nc, 3, device=dev), "samp": torch.zeros(Nc, dtype=torch.int32, device=dev)}
             keep = [fl.grad.clone(), P.points_conf.grad.clone()]   # warm-up accumulates into them
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
