@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 8
+#define SGN_ABI_VERSION 9
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -253,9 +253,10 @@ int sgn_point_project_f32_subset(const sgn_point_tables *pt, const void *d_packe
                                  const int64_t *d_count, void *d_proj, sgn_stream_t stream);
 /* fp32-faithful training forward (SURVEY §8 f1 at the reference's arithmetic): stage 1 of
  * sgn_aggregate_f32 for the base viewmlp that also writes the pre-activations of block1.0, block1.2
- * and block3.0 (2^-s (W x + b), before LeakyReLU) as fp32 [S_capacity * 8][256] at row s * 8 + k
- * (the row's pidx index; rows without a neighbour are left unwritten).  The backward through them
- * runs in fp32 (train_hip, f32 mode).
+ * and block3.0 (2^-s (W x + b), before LeakyReLU) as fp32 [S_capacity * K][256] at row s * K + k
+ * (the row's pidx index; rows without a neighbour are left unwritten), or, with d_row_off
+ * (sgn_train_lists), at the compact row d_row_off[s] + k.  The backward through them runs on
+ * sgn_x3_gemm and the row kernels below (train_hip, f32 mode).
  *   sgn_mlp_layout_f32(0 / 1)   : bytes of the blob's fragment section / fp32 entries after it
  *   sgn_mlp_pack_index_f32      : the blob as index maps, for packing it on the device from a flat
  *                                 parameter: which 0 -> per fp16 element (layer << 20 | element)
@@ -263,8 +264,8 @@ int sgn_point_project_f32_subset(const sgn_point_tables *pt, const void *d_packe
  *                                 kind << 26 | layer << 20 | element (kinds: see mlp_x3.hip Y32Kind) */
 int sgn_aggregate_train_fwd_f32(const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q,
                                 int64_t S_capacity, int32_t K, const void *d_packed_mlp, float *d_out_feat,
-                                float *d_z1, float *d_z2, float *d_z3, void *d_workspace, size_t workspace_bytes,
-                                sgn_stream_t stream);
+                                float *d_z1, float *d_z2, float *d_z3, const int32_t *d_row_off, void *d_workspace,
+                                size_t workspace_bytes, sgn_stream_t stream);
 int64_t sgn_mlp_layout_f32(int32_t which);
 int sgn_mlp_pack_index_f32(int32_t bpnet_layers, int32_t bpnet_dim, int32_t which, int32_t *out, int64_t n);
 
@@ -419,6 +420,105 @@ int sgn_colour_inputs(const int32_t *d_counters, const int32_t *d_work, const in
 size_t sgn_pow2_scale_workspace_bytes(void);
 int sgn_pow2_scale(const float *d_a, int64_t na, const float *d_b, int64_t nb, void *d_ws, float *d_out,
                    sgn_stream_t stream);
+
+/* ---- fp32 training step on hand-written kernels (ABI 9) -----------------------------------
+ * The reference's fp32 autograd through PointAggregator / viewmlp and the NeuralPoints gather
+ * (models/aggregators/point_aggregators.py:561-786, :868-959; neural_points.py:942-988; run from
+ * optimize_parameters, base_rendering_model.py:534-664, mvs_points_volumetric_model.py:116-141) as
+ * a fixed launch sequence over COMPACT rows (one per valid (sample, neighbour), sample-major) and
+ * work items (samples with a neighbour, ascending): no host synchronisation, every count read on
+ * the device (d_counts[0] = items, d_counts[1] = rows, from sgn_train_lists).
+ *
+ * sgn_x3_gemm: every nn.Linear product of the step (forward x W^T, backward data dy W, weight
+ * gradient dy^T x) at fp32 accuracy on fp16 MFMA: each fp32 product as three fp16 products of
+ * hi / lo halves (fp32 accumulate), operands scaled by powers of two before the split (weights by
+ * d_shift -- the per-layer shifts sgn_pack_scaled_f32 writes -- deltas by the amax word their
+ * producer wrote).  Operand element (i, k) (i: output row / column index, k: reduction index) is
+ * element (r, c) of a row-major fp32 matrix, r = i, c = k (kmajor 0) or r = k, c = i (kmajor 1);
+ * columns c >= csplit come from p2 (column c - csplit, no activation), c == ones_col reads 1 (the
+ * bias gradient's column), c >= ncols reads 0; act = 1 applies LeakyReLU(0.01) to p's values.
+ *   mode 0 (rows): out[r][n] (n < out_cols) / out2[r][n - out_cols] (n < N) = sum_k A(r, k) B(n, k)
+ *     (+ bias[n]) for r < min(*d_rows, M); out is multiplied by LeakyReLU'(mask[r][n]) when mask is
+ *     given (dz = dh * (z > 0 ? 1 : 0.01)), then LeakyReLU'd when act; *amax_out = max(|out|)
+ *     (atomicMax of the bits; the caller zeroes it).  K = the weight matrix's reduction extent.
+ *   mode 1 (split-K): part[s][m][n] = sum over rows r of split s of A(m, r) B(n, r), rows
+ *     r < min(*d_rows, K) cut into `splits` equal 32-aligned runs (empty runs write zeros). */
+typedef struct {
+    const float *p, *p2;
+    int64_t ld, ld2;
+    int32_t csplit, ncols, ones_col, act, kmajor;
+    const uint32_t *amax;   /* scale source: max |x| bits (or NULL) */
+    const int32_t *shift;   /* or a power-of-two shift (or NULL: no scaling) */
+} sgn_x3_operand;
+typedef struct {
+    sgn_x3_operand a, b;
+    int32_t mode, M, N, K;
+    const int32_t *d_rows;
+    const float *bias;
+    int32_t act;
+    const float *mask;
+    int64_t ldm;
+    float *out;
+    int64_t ldo;
+    int32_t out_cols;
+    float *out2;
+    int64_t ldo2;
+    uint32_t *amax_out, *amax_out2;
+    float *part;
+    int32_t splits;
+} sgn_x3_gemm_args;
+int sgn_x3_gemm(const sgn_x3_gemm_args *g, sgn_stream_t stream);
+
+/* Deterministic work list and compact row offsets after sgn_query: for s < d_counters[0],
+ * d_row_off[s] = sum of samp_nnb over samples < s; d_work = the samples with samp_nnb > 0 in
+ * ascending order (overwrites the query's unordered list: same set, same count); d_feat[s] = 0
+ * (float4[s_cap]); d_counts[0] = items, [1] = rows.  d_ws: sgn_train_lists_workspace_bytes. */
+size_t sgn_train_lists_workspace_bytes(int64_t s_cap);
+int sgn_train_lists(const int32_t *d_counters, const int32_t *d_samp_nnb, int64_t s_cap, int32_t *d_work,
+                    int32_t *d_row_off, float *d_feat, int32_t *d_counts, void *d_ws, sgn_stream_t stream);
+/* Per row j (compact): d_x0[j] fp32[288] = block1.0's input [emb | PE(emb) | PE(dists)] (:594-621)
+ * with 1 in column 284 (bias) and 0 after; d_ext[j] fp32[8] = block3.0's extra inputs [colour |
+ * dir - v | <dir, v>] (:639-652) and 1; d_rw[j] fp32[2] = (normalised weight * clamped conf,
+ * normalised weight).  Per item i: d_vpe[i] fp32[32] = PE(viewdir, 4) (sin | cos, :772-780), 1
+ * in column 24, 0 after. */
+int sgn_train_row_inputs(const sgn_point_tables *pt, const sgn_query_out *q, int32_t K, const int32_t *d_row_off,
+                         const int32_t *d_counts, float *d_x0, float *d_ext, float *d_rw, float *d_vpe,
+                         sgn_stream_t stream);
+/* color_branch.6 + sigmoid * 1.002 - 0.001 (fp32) on the items' last hidden layer d_h3 [items][128]
+ * (d_w6 [3][128], d_b6 [3]): d_feat[work[i]].rgb. */
+int sgn_train_colour_head(const sgn_query_out *q, const int32_t *d_counts, const float *d_h3, const float *d_w6,
+                          const float *d_b6, float *d_feat, sgn_stream_t stream);
+/* Its backward from d_dfeat float4[S] (the loss stage's d feat): d_dy3 [items][128] = d loss / d
+ * color_branch.4's pre-activation, *d_amax = max |dy3|, d_part = color_branch.6's weight / bias
+ * gradient as sgn_train_head_partial_floats(0) floats ([blocks][3][129]). */
+size_t sgn_train_head_partial_floats(int32_t which);
+int sgn_train_colour_head_bwd(const sgn_query_out *q, const int32_t *d_counts, const float *d_h3, const float *d_w6,
+                              const float *d_b6, const float *d_dfeat, float *d_dy3, uint32_t *d_amax, float *d_part,
+                              sgn_stream_t stream);
+/* block3.2's LeakyReLU, the alpha branch and the K-blend backward per row: d_z4_delta4 holds
+ * block3.2's pre-activation [rows][256] and is overwritten with its delta; d_dfs [items][256]
+ * = d loss / d f_s; d_dfeat.x = d loss / d alpha_s; d_rw from sgn_train_row_inputs; d_wa [256],
+ * d_ba [1] alpha_branch.0; d_gconf[N] += d conf (straight-through clamp, :863-865); *d_amax =
+ * max |delta4|; d_part = alpha_branch.0's weight / bias gradient, sgn_train_head_partial_floats(1)
+ * floats ([blocks][257]). */
+int sgn_train_row_head(const sgn_point_tables *pt, const sgn_query_out *q, int32_t K, const int32_t *d_row_off,
+                       const int32_t *d_counts, float *d_z4_delta4, const float *d_dfs, const float *d_dfeat,
+                       const float *d_rw, const float *d_wa, const float *d_ba, float *d_gconf, uint32_t *d_amax,
+                       float *d_part, sgn_stream_t stream);
+/* Point gradients of the rows (atomic adds, like the reference's index_add): d_dx0 [rows][224] =
+ * d loss / d [emb | PE(emb)] -> points_embeding; d_dext [rows][8] -> points_color, points_dir. */
+int sgn_train_row_tail(const sgn_point_tables *pt, const sgn_query_out *q, int32_t K, const int32_t *d_row_off,
+                       const int32_t *d_counts, const float *d_dx0, const float *d_dext, const sgn_point_grads *grads,
+                       sgn_stream_t stream);
+/* Partials -> flat gradient, in a fixed order: per segment, for m < M, c < N,
+ * v = sum over s < splits of part[s][m][c]; dst_w[m * ldw + c] += v (c < n_in), dst_b[m] += v
+ * (c == bias_col).  Up to 16 segments per launch; no two may add into the same element. */
+typedef struct {
+    const float *part;
+    int32_t splits, M, N, n_in, bias_col, ldw;
+    float *dst_w, *dst_b;
+} sgn_partial_segment;
+int sgn_reduce_partials(int32_t n_seg, const sgn_partial_segment *segs, sgn_stream_t stream);
 
 /* ---- composite --------------------------------------------------------- */
 

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -74,6 +74,23 @@ class GradSegment(ctypes.Structure):
 
 class GatherSegment(ctypes.Structure):
     _fields_ = [("idx", c_vp), ("dst", c_vp), ("n", c_i64), ("fp16", c_i32), ("reserved", c_i32)]
+
+
+class X3Operand(ctypes.Structure):
+    _fields_ = [("p", c_vp), ("p2", c_vp), ("ld", c_i64), ("ld2", c_i64), ("csplit", c_i32), ("ncols", c_i32),
+                ("ones_col", c_i32), ("act", c_i32), ("kmajor", c_i32), ("amax", c_vp), ("shift", c_vp)]
+
+
+class X3GemmArgs(ctypes.Structure):
+    _fields_ = [("a", X3Operand), ("b", X3Operand), ("mode", c_i32), ("M", c_i32), ("N", c_i32), ("K", c_i32),
+                ("d_rows", c_vp), ("bias", c_vp), ("act", c_i32), ("mask", c_vp), ("ldm", c_i64), ("out", c_vp),
+                ("ldo", c_i64), ("out_cols", c_i32), ("out2", c_vp), ("ldo2", c_i64), ("amax_out", c_vp),
+                ("amax_out2", c_vp), ("part", c_vp), ("splits", c_i32)]
+
+
+class PartialSegment(ctypes.Structure):
+    _fields_ = [("part", c_vp), ("splits", c_i32), ("M", c_i32), ("N", c_i32), ("n_in", c_i32), ("bias_col", c_i32),
+                ("ldw", c_i32), ("dst_w", c_vp), ("dst_b", c_vp)]
 
 
 # name -> (restype, argtypes); every symbol include/sgn_hip.h declares.
@@ -145,7 +162,21 @@ SIGNATURES = {
     "sgn_aggregate_check_f32": (c_i32, [c_vp, c_sz, c_vp]),
     "sgn_aggregate_flag_offset_f32": (c_sz, [c_sz]),
     "sgn_aggregate_train_fwd_f32": (c_i32, [c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,
-                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "sgn_x3_gemm": (c_i32, [ctypes.POINTER(X3GemmArgs), c_vp]),
+    "sgn_train_lists_workspace_bytes": (c_sz, [c_i64]),
+    "sgn_train_lists": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_train_row_inputs": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp, c_vp,
+                                     c_vp, c_vp, c_vp, c_vp]),
+    "sgn_train_colour_head": (c_i32, [ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_train_head_partial_floats": (c_sz, [c_i32]),
+    "sgn_train_colour_head_bwd": (c_i32, [ctypes.POINTER(QueryOut), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                          c_vp]),
+    "sgn_train_row_head": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp, c_vp,
+                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_train_row_tail": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp, c_vp,
+                                   c_vp, ctypes.POINTER(PointGrads), c_vp]),
+    "sgn_reduce_partials": (c_i32, [c_i32, ctypes.POINTER(PartialSegment), c_vp]),
     "sgn_mlp_layout_f32": (c_i64, [c_i32]),
     "sgn_mlp_pack_index_f32": (c_i32, [c_i32, c_i32, c_i32, ctypes.POINTER(c_i32), c_i64]),
     "sgn_composite": (c_i32, [ctypes.POINTER(CompositeParams), c_vp, c_vp, c_vp, c_i64, c_vp, c_i32,
@@ -174,15 +205,16 @@ def lib():
                 f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(there is no CPU fallback for the hot path)")
         h = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(h, name, None)
-            if fn is None:
-                continue
-            fn.restype = res
-            fn.argtypes = args
         v = h.sgn_abi_version()
         if v != ABI_VERSION:
-            raise SgnError(f"libsgn_hip.so ABI {v} != expected {ABI_VERSION}")
+            raise SgnError(f"libsgn_hip.so ABI {v} != expected {ABI_VERSION}: rebuild it")
+        missing = [name for name in SIGNATURES if getattr(h, name, None) is None]
+        if missing:   # a stale build: fail before any GPU work, not at the first call of a missing symbol
+            raise SgnError(f"libsgn_hip.so lacks {', '.join(missing)}: rebuild it")
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
         _LIB = h
     return _LIB
 

@@ -117,6 +117,8 @@ struct AggArgs {
     // block1.2 and block3.0 (the inputs of the next layer before LeakyReLU), fp32 natural unit order,
     // row s * 8 + k (the row's pidx index); rows without a neighbour are not written
     float *z1, *z2, *z3;
+    // with row_off (sgn_train_lists): the rows are compact instead, row_off[s] + k
+    const int32_t *row_off;
     // neighbours per sample of the query's pidx (fp32 kernels: 1..8; a row-table entry s * 8 + k
     // names pidx index s * K + k)
     int32_t K;

@@ -1151,8 +1151,13 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         const int nA0 = __popc((uint32_t)mrowA & 0xFFu), nA1 = __popc(((uint32_t)mrowA >> 8) & 0xFFu);
         const bool waveB = (mrowB & 0xFFFFull) != 0;  // wave-uniform: a B sample in either half
         const Row16 rw = row_math16<PERS>(cam, rc, m, ix.a, sc ? nA1 : nA0, waveB);
-        // SAVE: the row's pidx index s * 8 + k (from the slot's row table), -1 for rows without a neighbour
-        const int64_t vrow = SAVE && ix.sval && m ? pidx_of(a, a.rows[(int64_t)hslot * 8 + kk]) : -1;
+        // SAVE: the row's pidx index s * K + k (from the slot's row table entry s * 8 + k), or its compact
+        // row row_off[s] + k; -1 for rows without a neighbour
+        int64_t vrow = -1;
+        if (SAVE && ix.sval && m) {
+            const int e = a.rows[(int64_t)hslot * 8 + kk];
+            vrow = a.row_off ? (int64_t)a.row_off[e >> 3] + (e & 7) : pidx_of(a, e);
+        }
         if ((a.blend || a.wnorm) && ix.sval) {  // optional outputs: the row's pidx index from the table
             const int64_t v = pidx_of(a, a.rows[(int64_t)hslot * 8 + kk]);
             if (a.blend && g == 0) a.blend[v] = rw.wgt;
@@ -1760,7 +1765,7 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
                   const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_capacity, int32_t K,
                   const void *d_packed, float *d_out_feat, float *d_out_blend, float *d_out_wnorm,
                   void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream,
-                  float *const *z = nullptr) {
+                  float *const *z = nullptr, const int32_t *row_off = nullptr) {
     using namespace sgn;
     using namespace sgn::mlp;
     SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_workspace && d_point_proj, "null argument");
@@ -1804,6 +1809,7 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
     a.rows = rows; a.slots = slots; a.slot_n = slot_n;
     if (z) {
         a.z1 = z[0]; a.z2 = z[1]; a.z3 = z[2];
+        a.row_off = row_off;
     }
     // SGN_PAIR=0 runs every sample alone in its k_rows16 half (same results, bit for bit; tests)
     const char *pe = getenv("SGN_PAIR");
@@ -1877,15 +1883,15 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
 
 int sgn_aggregate_train_fwd_f32(const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q,
                                 int64_t S_capacity, int32_t K, const void *d_packed, float *d_out_feat,
-                                float *d_z1, float *d_z2, float *d_z3, void *d_workspace, size_t workspace_bytes,
-                                sgn_stream_t stream) {
+                                float *d_z1, float *d_z2, float *d_z3, const int32_t *d_row_off, void *d_workspace,
+                                size_t workspace_bytes, sgn_stream_t stream) {
     SGN_REQUIRE(d_z1 && d_z2 && d_z3 && ((uintptr_t)d_z1 & 15) == 0 && ((uintptr_t)d_z2 & 15) == 0 &&
                     ((uintptr_t)d_z3 & 15) == 0,
                 "16-byte aligned pre-activation buffers z1, z2, z3 required");
     SGN_REQUIRE(pt && pt->pers == nullptr, "the training forward computes the pers coordinates itself");
     float *const z[3] = {d_z1, d_z2, d_z3};
     return aggregate_f32(0, 0, nullptr, d_point_proj, pt, q, S_capacity, K, d_packed, d_out_feat, nullptr, nullptr,
-                         d_workspace, workspace_bytes, 1, stream, z);
+                         d_workspace, workspace_bytes, 1, stream, z, d_row_off);
 }
 
 int sgn_mlp_pack_index_f32(int32_t bpnet_layers, int32_t bpnet_dim, int32_t which, int32_t *out, int64_t n) {

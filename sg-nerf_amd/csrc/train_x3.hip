@@ -1,0 +1,949 @@
+// train_x3.hip -- the fp32 training step's backward (and the colour MLP's training forward) on
+// hand-written gfx950 kernels, at the reference's fp32 arithmetic.
+//
+// The reference differentiates PointAggregator.forward / viewmlp (models/aggregators/
+// point_aggregators.py:868-959, :561-786) and the NeuralPoints gather (models/neural_points/
+// neural_points.py:942-988) with torch autograd in fp32 (optimize_parameters,
+// models/base_rendering_model.py:534-664; models/mvs_points_volumetric_model.py:116-141).  Here the
+// step is a fixed sequence of launches over compact rows (one per valid (sample, neighbour) pair,
+// sample-major) and work items (one per sample with a neighbour, sample order):
+//
+//   k_lists_count / k_lists_write  deterministic work list (samples with a neighbour, ascending) and
+//                                  the compact row offset of every sample (prefix sum of samp_nnb)
+//   k_rows16 (mlp_x3.hip, save)    the forward; z1 / z2 / z3 pre-activations at the compact rows
+//   k_row_inputs                   per row: block1.0's input x0 = [emb | PE(emb) | PE(dists) | 1],
+//                                  block3.0's extra channels [colour | dir - v | <dir, v> | 1], the
+//                                  blend weights (w conf, w)
+//   k_colour_in                    per item: PE(viewdir) | 1 (the colour MLP's 24 extra inputs)
+//   k_x3gemm                       every nn.Linear product: forward (x W^T), backward data
+//                                  (dy W, masked by LeakyReLU' of the saved activation) and weight
+//                                  gradients (dy^T x as split-K partials, bias through a ones column)
+//   k_colour_head / _bwd           color_branch.6 + sigmoid (fp32 FMA), and its backward
+//   k_row_head                     block3.2's LeakyReLU, the alpha branch, the K-blend backward:
+//                                  delta4, d conf through the straight-through clamp, dWa partials
+//   k_row_tail                     d points_embeding through PE(emb), d colour / dir
+//   k_reduce_partials              partials summed in a fixed order into the flat gradient
+//
+// Every GEMM is the 3-product split: x = hi + lo (fp16), w = hi + lo, w x ~ w_hi x_hi + w_hi x_lo +
+// w_lo x_hi on v_mfma_f32_32x32x16_f16 with fp32 accumulation.  Operands are scaled by powers of two
+// before the split so hi stays below 2^14 and lo stays a normal fp16 number: weights by the packer's
+// per-layer shift, deltas by the amax word their producer wrote (max |x| via atomicMax), forward
+// activations not at all (they are inside fp16 range, as the forward kernel requires).  Results are
+// deterministic: no float atomics except the per-point gradients (the reference's index_add).
+#include <cmath>
+#include <vector>
+
+#include "agg_device.h"
+#include "x3_split.h"
+
+namespace sgn {
+namespace {
+namespace tx {
+
+constexpr int TPB = 256;
+constexpr int FRAG = 1024;  // one fragment: 64 lanes x 16 B
+
+// ---- the split-K / rows GEMM ------------------------------------------------------------
+
+struct Opnd {
+    const float *p, *p2;
+    int64_t ld, ld2;
+    int32_t csplit, ncols, ones_col, act, kmajor, nrows, dyn, vec;
+    const uint32_t *amax;
+    const int32_t *shift;
+};
+
+struct GemmK {
+    Opnd A, B;
+    int32_t M, N, K;
+    const int32_t *d_rows;
+    const float *bias;
+    int32_t act;
+    const float *mask;
+    int64_t ldm;
+    float *out;
+    int64_t ldo;
+    int32_t out_cols;
+    float *out2;
+    int64_t ldo2;
+    uint32_t *amax_out, *amax_out2;
+    float *part;
+};
+
+__device__ __forceinline__ int op_shift(const Opnd &o) {
+    if (o.shift) return o.shift[0];
+    if (o.amax) {
+        const float m = __builtin_bit_cast(float, o.amax[0]);
+        if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
+        int e;
+        frexpf(m, &e);  // m < 2^e
+        return 14 - e;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ float lrelu_ref(float x) { return x > 0.f ? x : x * 0.01f; }
+
+// element (i, k .. k + 7) of an operand (i: the M / N index, k: the reduction index); rows past
+// `lim` read as 0.  kmajor 0: matrix row i, columns k..k+7; kmajor 1: rows k..k+7, column i.
+__device__ __forceinline__ void load8(const Opnd &o, int i, int k, int lim, float (&v)[8]) {
+    if (!o.kmajor) {
+        const bool rok = i < lim;
+        const bool s1 = k < o.csplit;
+        const float *src = s1 ? o.p + (int64_t)i * o.ld + k : o.p2 + (int64_t)i * o.ld2 + (k - o.csplit);
+        const bool full = rok && o.vec && k + 8 <= o.ncols && (o.ones_col < k || o.ones_col >= k + 8);
+        if (full) {
+            const f32x4 a = *(const f32x4 *)src, b = *(const f32x4 *)(src + 4);
+            v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+            v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int c = k + e;
+                v[e] = !rok ? 0.f : c == o.ones_col ? 1.f : c < o.ncols ? src[e] : 0.f;
+            }
+        }
+        if (o.act && s1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (k + e != o.ones_col) v[e] = lrelu_ref(v[e]);
+        }
+    } else {
+        if (i == o.ones_col) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = k + e < lim ? 1.f : 0.f;
+        } else if (i < o.ncols) {
+            const bool s1 = i < o.csplit;
+            const float *src = s1 ? o.p + i : o.p2 + (i - o.csplit);
+            const int64_t ld = s1 ? o.ld : o.ld2;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = k + e < lim ? src[(int64_t)(k + e) * ld] : 0.f;
+            if (o.act && s1) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = lrelu_ref(v[e]);
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        }
+    }
+}
+
+// One operand tile of T 32-wide tiles x 32 k per stage: 128 T lane fragments of 8 values, thread
+// tid takes fragments tid, tid + 256, ... (consecutive threads: consecutive i, so the LDS writes of
+// a wave land on consecutive 16-B slots).  LDS fragment (t, s, hl) at ((t * 2 + s) * 2 + hl) * FRAG.
+template <int T>
+struct Stage {
+    static constexpr int NF = (128 * T + TPB - 1) / TPB;
+    float v[NF][8];
+    __device__ __forceinline__ void load(const Opnd &o, int i0, int k0, int lim, int tid) {
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            const int f = tid + TPB * j;
+            if ((128 * T) % TPB == 0 || f < 128 * T) {
+                const int il = f % (32 * T), oc = f / (32 * T);
+                load8(o, i0 + il, k0 + 8 * oc, lim, v[j]);
+            }
+        }
+    }
+    __device__ __forceinline__ void store(char *base, float scale, int tid) const {
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            const int f = tid + TPB * j;
+            if ((128 * T) % TPB == 0 || f < 128 * T) {
+                const int il = f % (32 * T), oc = f / (32 * T);
+                const int t = il >> 5, L = (il & 31) + 32 * (oc & 1), s = oc >> 1;
+                const X3Pair x = split8_scaled(v[j], scale);
+                char *d = base + ((t * 2 + s) * 2) * FRAG + L * 16;
+                *(h8 *)d = x.hi;
+                *(h8 *)(d + FRAG) = x.lo;
+            }
+        }
+    }
+};
+
+// WM x WN 32x32 tiles per wave, GM x GN waves; TNM: split-K partials over rows (else rows mode)
+template <int WM, int WN, int GM, int GN, bool TNM>
+__global__ __launch_bounds__(TPB) void k_x3gemm(GemmK g) {
+    static_assert(GM * GN == 4, "four waves");
+    constexpr int TA = WM * GM, TB = WN * GN, BM = 32 * TA, BN = 32 * TB;
+    constexpr int ABYTES = TA * 4 * FRAG, STAGE = (TA + TB) * 4 * FRAG;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w % GM, wn = w / GM;
+    const int sa = op_shift(g.A), sb = op_shift(g.B);
+    const float fa = ldexpf(1.f, sa), fb = ldexpf(1.f, sb), osc = ldexpf(1.f, -(sa + sb));
+    const int rows_dev = g.d_rows ? *g.d_rows : 0x7fffffff;
+    Stage<TA> stA;
+    Stage<TB> stB;
+
+    auto tile = [&](int m0, int n0, int kbeg, int kend, int limA, int limB, f32x16 (&acc)[WM][WN]) {
+#pragma unroll
+        for (int a = 0; a < WM; ++a)
+#pragma unroll
+            for (int b = 0; b < WN; ++b) acc[a][b] = f32x16{};
+        const int nkb = kend > kbeg ? (kend - kbeg + 31) / 32 : 0;
+        if (nkb == 0) return;
+        stA.load(g.A, m0, kbeg, limA, tid);
+        stB.load(g.B, n0, kbeg, limB, tid);
+        stA.store(lds, fa, tid);
+        stB.store(lds + ABYTES, fb, tid);
+        __syncthreads();
+        for (int kb = 0; kb < nkb; ++kb) {
+            const bool more = kb + 1 < nkb;
+            if (more) {
+                stA.load(g.A, m0, kbeg + 32 * (kb + 1), limA, tid);
+                stB.load(g.B, n0, kbeg + 32 * (kb + 1), limB, tid);
+            }
+            const char *st = lds + (kb & 1) * STAGE;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                h8 ah[WM], al[WM], bh[WN], bl[WN];
+#pragma unroll
+                for (int a = 0; a < WM; ++a) {
+                    const char *p = st + (((wm * WM + a) * 2 + s) * 2) * FRAG + lane * 16;
+                    ah[a] = *(const h8 *)p;
+                    al[a] = *(const h8 *)(p + FRAG);
+                }
+#pragma unroll
+                for (int b = 0; b < WN; ++b) {
+                    const char *p = st + ABYTES + (((wn * WN + b) * 2 + s) * 2) * FRAG + lane * 16;
+                    bh[b] = *(const h8 *)p;
+                    bl[b] = *(const h8 *)(p + FRAG);
+                }
+#pragma unroll
+                for (int a = 0; a < WM; ++a)
+#pragma unroll
+                    for (int b = 0; b < WN; ++b) {
+                        acc[a][b] = mfma32(al[a], bh[b], acc[a][b]);
+                        acc[a][b] = mfma32(ah[a], bl[b], acc[a][b]);
+                        acc[a][b] = mfma32(ah[a], bh[b], acc[a][b]);
+                    }
+            }
+            if (more) {
+                char *nx = lds + ((kb + 1) & 1) * STAGE;
+                stA.store(nx, fa, tid);
+                stB.store(nx + ABYTES, fb, tid);
+            }
+            __syncthreads();
+        }
+    };
+
+    f32x16 acc[WM][WN];
+    if constexpr (TNM) {
+        // C[m][n] = sum over rows r of A(m, r) B(n, r); this workgroup: one (m, n) block, one split
+        const int nb_n = (g.N + BN - 1) / BN;
+        const int m0 = (blockIdx.x / nb_n) * BM, n0 = (blockIdx.x % nb_n) * BN;
+        const int rows = min(rows_dev, g.K);
+        const int splits = gridDim.y;
+        const int per = ((rows + splits - 1) / splits + 31) / 32 * 32;
+        const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+        tile(m0, n0, r0, r1, r1, r1, acc);
+        float *part = g.part + (int64_t)blockIdx.y * g.M * g.N;
+#pragma unroll
+        for (int a = 0; a < WM; ++a)
+#pragma unroll
+            for (int b = 0; b < WN; ++b) {
+                const int n = n0 + (wn * WN + b) * 32 + (lane & 31);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + (wm * WM + a) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    if (m < g.M && n < g.N) part[(int64_t)m * g.N + n] = acc[a][b][r] * osc;
+                }
+            }
+    } else {
+        // Y[r][n] = sum_k A(r, k) B(n, k): persistent over row tiles, blockIdx.x = column block
+        const int rows = min(rows_dev, g.M);
+        const int n0 = blockIdx.x * BN;
+        const int limA = g.A.dyn ? min(rows, g.A.nrows) : g.A.nrows;
+        float am1 = 0.f, am2 = 0.f;
+        for (int rt = blockIdx.y; rt * BM < rows; rt += gridDim.y) {
+            const int m0 = rt * BM;
+            tile(m0, n0, 0, g.K, limA, g.B.nrows, acc);
+#pragma unroll
+            for (int a = 0; a < WM; ++a)
+#pragma unroll
+                for (int b = 0; b < WN; ++b) {
+                    const int n = n0 + (wn * WN + b) * 32 + (lane & 31);
+                    const float bv = g.bias && n < g.N ? g.bias[n] : 0.f;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int row = m0 + (wm * WM + a) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                        if (row >= rows || n >= g.N) continue;
+                        float v = acc[a][b][r] * osc + bv;
+                        if (n < g.out_cols) {
+                            if (g.mask && !(g.mask[(int64_t)row * g.ldm + n] > 0.f)) v *= 0.01f;
+                            if (g.act) v = lrelu_ref(v);
+                            g.out[(int64_t)row * g.ldo + n] = v;
+                            am1 = fmaxf(am1, fabsf(v));
+                        } else {
+                            g.out2[(int64_t)row * g.ldo2 + (n - g.out_cols)] = v;
+                            am2 = fmaxf(am2, fabsf(v));
+                        }
+                    }
+                }
+        }
+        // the producer's amax word for the consumer's operand scale (max |x|, as uint bits)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            am1 = fmaxf(am1, __shfl_xor(am1, o));
+            am2 = fmaxf(am2, __shfl_xor(am2, o));
+        }
+        if (lane == 0) {
+            if (g.amax_out) atomicMax(g.amax_out, __builtin_bit_cast(uint32_t, am1));
+            if (g.amax_out2) atomicMax(g.amax_out2, __builtin_bit_cast(uint32_t, am2));
+        }
+    }
+}
+
+// ---- deterministic work list and compact row offsets ---------------------------------------
+
+constexpr int LIST_PER_BLOCK = 1024;  // samples per block (4 per thread)
+
+// exclusive scan of one int2 per thread over the workgroup, in thread order; returns the total
+__device__ __forceinline__ int2 block_scan2(int2 v, int2 &excl, int2 *sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int2 inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(inc.x, o), y = __shfl_up(inc.y, o);
+        if (lane >= o) {
+            inc.x += x;
+            inc.y += y;
+        }
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    int2 base = make_int2(0, 0), tot = make_int2(0, 0);
+    for (int i = 0; i < TPB / 64; ++i) {
+        if (i < w) {
+            base.x += sh[i].x;
+            base.y += sh[i].y;
+        }
+        tot.x += sh[i].x;
+        tot.y += sh[i].y;
+    }
+    excl = make_int2(base.x + inc.x - v.x, base.y + inc.y - v.y);
+    __syncthreads();
+    return tot;
+}
+
+__device__ __forceinline__ int2 count4(const int32_t *nnb, int s0, int S, int (&n)[4]) {
+    int2 c = make_int2(0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int s = s0 + j;
+        n[j] = s < S ? nnb[s] : 0;
+        c.x += n[j] > 0;
+        c.y += n[j];
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(TPB) void k_lists_count(const int32_t *counters, const int32_t *nnb, int2 *bsum) {
+    __shared__ int2 sh[TPB / 64];
+    const int S = counters[0];
+    int n[4];
+    const int2 c = count4(nnb, blockIdx.x * LIST_PER_BLOCK + threadIdx.x * 4, S, n);
+    int2 ex;
+    const int2 tot = block_scan2(c, ex, sh);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(TPB) void k_lists_write(const int32_t *counters, const int32_t *nnb, const int2 *bsum,
+                                                     int32_t *work, int32_t *row_off, float4 *feat, int32_t *tl) {
+    __shared__ int2 sh[TPB / 64];
+    __shared__ int2 bb[TPB / 64];
+    const int S = counters[0];
+    const int s_blk = blockIdx.x * LIST_PER_BLOCK;
+    // base = sum of the previous blocks' totals (fixed order: per-thread strided sums, then waves)
+    int2 pb = make_int2(0, 0);
+    for (int b = threadIdx.x; b < (int)blockIdx.x; b += TPB) {
+        pb.x += bsum[b].x;
+        pb.y += bsum[b].y;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        pb.x += __shfl_xor(pb.x, o);
+        pb.y += __shfl_xor(pb.y, o);
+    }
+    if ((threadIdx.x & 63) == 0) bb[threadIdx.x >> 6] = pb;
+    __syncthreads();
+    int2 base = make_int2(0, 0);
+    for (int i = 0; i < TPB / 64; ++i) {
+        base.x += bb[i].x;
+        base.y += bb[i].y;
+    }
+    int n[4];
+    const int s0 = s_blk + threadIdx.x * 4;
+    const int2 c = count4(nnb, s0, S, n);
+    int2 ex;
+    const int2 tot = block_scan2(c, ex, sh);
+    int it = base.x + ex.x, ro = base.y + ex.y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int s = s0 + j;
+        if (s < S) {
+            row_off[s] = ro;
+            if (n[j] > 0) work[it++] = s;
+            ro += n[j];
+            feat[s] = make_float4(0.f, 0.f, 0.f, 0.f);  // the forward writes alpha / rgb of items only
+        }
+    }
+    // the block holding the last sample (block 0 when there are none) publishes the totals
+    const int last = S > 0 ? S - 1 : 0;
+    if (threadIdx.x == 0 && last >= s_blk && last < s_blk + LIST_PER_BLOCK) {
+        tl[0] = base.x + tot.x;
+        tl[1] = base.y + tot.y;
+    }
+}
+
+// ---- per-row / per-item kernels (one wave per work item, its rows in turn) ------------------
+
+struct RowArgs {
+    const float *xyz, *emb, *color, *dir, *conf, *campos, *rot, *raydir;
+    const int32_t *counters, *work, *samp_ray, *samp_nnb, *pidx, *row_off, *tl;
+    const float *samp_locw;
+    int32_t K;
+};
+
+__device__ __forceinline__ int n_items(const RowArgs &r) { return r.tl[0]; }
+
+// x0 column c of a row (point_aggregators.py:594-621: [emb | PE(emb, 3) | PE(dists, 5)], then the
+// ones column 284 that carries block1.0's bias gradient, zero padding to 288)
+__device__ __forceinline__ float x0_col(int c, const float *e, const float (&d)[6]) {
+    if (c < 32) return e[c];
+    if (c < 224) {
+        const int m = c - 32, ch = m / 6, f = (m % 6) >> 1;
+        const float a = e[ch] * (float)(1 << f);
+        return (m & 1) ? cosf(a) : sinf(a);
+    }
+    if (c < 284) {
+        const int m = c - 224, dd = m / 10, f = (m % 10) >> 1;
+        const float a = d[dd] * (float)(1 << f);
+        return (m & 1) ? cosf(a) : sinf(a);
+    }
+    return c == 284 ? 1.f : 0.f;
+}
+
+// dists of a row and the sample's linear-kernel weights (point_aggregators.py:494-502, :868-953;
+// the same arithmetic as the forward's gather_row): lane k < K of the wave holds row k's
+__device__ __forceinline__ void row_geometry(const RowArgs &a, const Cam &cam, int s, int pid, float (&d)[6], float &wn,
+                                             float &wgt) {
+    const float lx = a.samp_locw[(int64_t)s * 3], ly = a.samp_locw[(int64_t)s * 3 + 1], lz = a.samp_locw[(int64_t)s * 3 + 2];
+    const bool m = pid >= 0;
+    float px = 0.f, py = 0.f, pz = 0.f, cf = 0.f;
+    if (m) {
+        px = a.xyz[(int64_t)pid * 3]; py = a.xyz[(int64_t)pid * 3 + 1]; pz = a.xyz[(int64_t)pid * 3 + 2];
+        cf = a.conf[pid];
+    }
+    const float dwx = __fsub_rn(px, lx), dwy = __fsub_rn(py, ly), dwz = __fsub_rn(pz, lz);
+    float xp = 0.f, yp = 0.f, zp = 0.f, xl, yl, zl;
+    if (m) cam.pers(px, py, pz, xp, yp, zp);
+    cam.pers(lx, ly, lz, xl, yl, zl);
+    d[0] = m ? dwx : 0.f; d[1] = m ? dwy : 0.f; d[2] = m ? dwz : 0.f;
+    d[3] = m ? __fsub_rn(__fmul_rn(xp, zp), __fmul_rn(xl, zl)) : 0.f;
+    d[4] = m ? __fsub_rn(__fmul_rn(yp, zp), __fmul_rn(yl, zl)) : 0.f;
+    d[5] = m ? __fsub_rn(zp, zl) : 0.f;
+    float w = 0.f;
+    if (m) {
+        const float n2 = __fadd_rn(__fadd_rn(__fmul_rn(dwx, dwx), __fmul_rn(dwy, dwy)), __fmul_rn(dwz, dwz));
+        w = 1.f / fmaxf(sqrtf(n2), 1e-6f);
+    }
+    wn = w;
+    wgt = cf;
+}
+
+__global__ __launch_bounds__(TPB) void k_row_inputs(RowArgs a, float *x0, float *ext, float2 *rw) {
+    const int lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TPB / 64);
+    const Cam cam = load_cam(a.campos, a.rot);
+    const int n = n_items(a);
+    for (int it = wv; it < n; it += nw) {
+        const int s = a.work[it];
+        const int nnb = a.samp_nnb[s], ro = a.row_off[s];
+        const int ray = a.samp_ray[s];
+        // lanes k < K: row k's geometry and weight; normalised over the sample's rows
+        const int kl = lane < a.K ? lane : 0;
+        const int pidl = lane < nnb ? a.pidx[(int64_t)s * a.K + kl] : -1;
+        float dl[6], w, cf;
+        row_geometry(a, cam, s, pidl, dl, w, cf);
+        float wsum = w;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) wsum += __shfl_xor(wsum, o);  // lanes 0..7 (K <= 8)
+        wsum = __shfl(wsum, 0);
+        const float wn = w / fmaxf(wsum, 1e-8f);
+        const float wgt = wn * fminf(fmaxf(cf, 1e-4f), 1.f);
+        if (lane < nnb) rw[ro + lane] = make_float2(wgt, wn);
+        const float vx = a.raydir[(int64_t)ray * 3], vy = a.raydir[(int64_t)ray * 3 + 1], vz = a.raydir[(int64_t)ray * 3 + 2];
+        for (int k = 0; k < nnb; ++k) {
+            const int pid = __shfl(pidl, k);
+            float d[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) d[q] = __shfl(dl[q], k);
+            const float *e = a.emb + (int64_t)pid * 32;
+            float *xr = x0 + (int64_t)(ro + k) * 288;
+            f32x4 v4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v4[q] = x0_col(4 * lane + q, e, d);
+            *(f32x4 *)(xr + 4 * lane) = v4;
+            if (lane < 8) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v4[q] = x0_col(256 + 4 * lane + q, e, d);
+                *(f32x4 *)(xr + 256 + 4 * lane) = v4;
+            }
+            if (lane < 8) {  // block3.0's extra channels (:639-652) + the ones column of its bias
+                float u;
+                const int64_t pb = (int64_t)pid * 3;
+                if (lane < 3) u = a.color[pb + lane];
+                else if (lane < 6) u = __fsub_rn(a.dir[pb + lane - 3], lane == 3 ? vx : lane == 4 ? vy : vz);
+                else if (lane == 6)
+                    u = __fadd_rn(__fadd_rn(__fmul_rn(a.dir[pb], vx), __fmul_rn(a.dir[pb + 1], vy)), __fmul_rn(a.dir[pb + 2], vz));
+                else u = 1.f;
+                ext[(int64_t)(ro + k) * 8 + lane] = u;
+            }
+        }
+    }
+}
+
+// PE(viewdir) for the colour MLP (point_aggregators.py:772-780: positional_encoding(v, 4, ori=True)
+// without the raw v): [sin(v_c 2^f) (c-major) | cos(...)], then the ones column 24, zero to 32
+__global__ __launch_bounds__(TPB) void k_colour_in(RowArgs a, float *vpe) {
+    const int n = n_items(a);
+    for (int64_t t = blockIdx.x * (int64_t)TPB + threadIdx.x; t < (int64_t)n * 32; t += (int64_t)gridDim.x * TPB) {
+        const int it = (int)(t >> 5), j = (int)(t & 31);
+        float v = 0.f;
+        if (j < 24) {
+            const int ray = a.samp_ray[a.work[it]];
+            const int jj = j < 12 ? j : j - 12, c = jj >> 2, f = jj & 3;
+            const float x = a.raydir[(int64_t)ray * 3 + c] * (float)(1 << f);
+            v = j < 12 ? sinf(x) : cosf(x);
+        } else if (j == 24) {
+            v = 1.f;
+        }
+        vpe[t] = v;
+    }
+}
+
+// wave-wide sum
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+// color_branch.6 (128 -> 3) + sigmoid * (1 + 2e-3) - 1e-3 in fp32; rgb into feat[s].yzw
+__global__ __launch_bounds__(TPB) void k_colour_head(RowArgs a, const float *h3, const float *w6, const float *b6,
+                                                     float4 *feat) {
+    const int lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TPB / 64);
+    const int n = n_items(a);
+    for (int it = wv; it < n; it += nw) {
+        const float2 h = *(const float2 *)(h3 + (int64_t)it * 128 + 2 * lane);
+        float y[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) y[c] = wave_sum(h.x * w6[c * 128 + 2 * lane] + h.y * w6[c * 128 + 2 * lane + 1]) + b6[c];
+        if (lane == 0) {
+            const int s = a.work[it];
+            float4 f = feat[s];
+            f.y = 1.f / (1.f + expf(-y[0])) * 1.002f - 0.001f;
+            f.z = 1.f / (1.f + expf(-y[1])) * 1.002f - 0.001f;
+            f.w = 1.f / (1.f + expf(-y[2])) * 1.002f - 0.001f;
+            feat[s] = f;
+        }
+    }
+}
+
+constexpr int HEAD_BLOCKS = 256;
+
+// backward of k_colour_head: dy4 = d rgb 1.002 sig (1 - sig); dy3 = (W6^T dy4) LReLU'(h3); the
+// weight / bias gradient of color_branch.6 as one fixed-order partial per workgroup
+// ([HEAD_BLOCKS][3][129]: 128 weights then the bias)
+__global__ __launch_bounds__(TPB) void k_colour_head_bwd(RowArgs a, const float *h3, const float *w6, const float *b6,
+                                                         const float4 *dfeat, float *dy3, uint32_t *amax, float *part) {
+    __shared__ float sh[TPB / 64][3][130];
+    const int lane = threadIdx.x & 63, wl = threadIdx.x >> 6;
+    const int wv = blockIdx.x * (TPB / 64) + wl, nw = gridDim.x * (TPB / 64);
+    const int n = n_items(a);
+    float gw[3][2] = {}, gb[3] = {}, am = 0.f;
+    for (int it = wv; it < n; it += nw) {
+        const float2 h = *(const float2 *)(h3 + (int64_t)it * 128 + 2 * lane);
+        const float4 df = dfeat[a.work[it]];
+        const float dr[3] = {df.y, df.z, df.w};
+        float dy[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float y = wave_sum(h.x * w6[c * 128 + 2 * lane] + h.y * w6[c * 128 + 2 * lane + 1]) + b6[c];
+            const float sg = 1.f / (1.f + expf(-y));
+            dy[c] = dr[c] * 1.002f * (sg * (1.f - sg));
+            gw[c][0] += dy[c] * h.x;
+            gw[c][1] += dy[c] * h.y;
+            gb[c] += dy[c];
+        }
+        float d0 = dy[0] * w6[2 * lane] + dy[1] * w6[128 + 2 * lane] + dy[2] * w6[256 + 2 * lane];
+        float d1 = dy[0] * w6[2 * lane + 1] + dy[1] * w6[128 + 2 * lane + 1] + dy[2] * w6[256 + 2 * lane + 1];
+        d0 = h.x > 0.f ? d0 : d0 * 0.01f;
+        d1 = h.y > 0.f ? d1 : d1 * 0.01f;
+        *(float2 *)(dy3 + (int64_t)it * 128 + 2 * lane) = make_float2(d0, d1);
+        am = fmaxf(am, fmaxf(fabsf(d0), fabsf(d1)));
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        sh[wl][c][2 * lane] = gw[c][0];
+        sh[wl][c][2 * lane + 1] = gw[c][1];
+        if (lane == 0) sh[wl][c][128] = gb[c];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < 3 * 129; j += TPB) {
+        const int c = j / 129, u = j % 129;
+        float v = 0.f;
+        for (int q = 0; q < TPB / 64; ++q) v += sh[q][c][u];
+        part[(int64_t)blockIdx.x * 3 * 129 + j] = v;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
+    if (lane == 0) atomicMax(amax, __builtin_bit_cast(uint32_t, am));
+}
+
+__device__ __forceinline__ float softplus_ref(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+// block3.2's output and everything between it and the blended feature (point_aggregators.py:
+// 640-653, :743-770): h4 = LReLU(z4); alpha = softplus(wa h4 + ba - 1); f_s = sum_k w_k h4_k,
+// alpha_s = sum_k w_k alpha_k.  Backward per row: dza = w dalpha_s sigmoid(za - 1);
+// d w = <h4, d f_s> + alpha dalpha_s (-> d conf = d w * w_norm through the straight-through clamp);
+// delta4 = (w d f_s + dza wa) LReLU'(z4) (in place over z4).  dWa / dba partial per workgroup
+// ([HEAD_BLOCKS][257]).
+__global__ __launch_bounds__(TPB) void k_row_head(RowArgs a, float *z4d4, const float *dfs, const float4 *dfeat,
+                                                  const float2 *rw, const float *wa, const float *ba, float *g_conf,
+                                                  uint32_t *amax, float *part) {
+    __shared__ float sh[TPB / 64][260];
+    const int lane = threadIdx.x & 63, wl = threadIdx.x >> 6;
+    const int wv = blockIdx.x * (TPB / 64) + wl, nw = gridDim.x * (TPB / 64);
+    const int n = n_items(a);
+    const f32x4 wa4 = *(const f32x4 *)(wa + 4 * lane);
+    const float bav = ba[0];
+    f32x4 gw = {0.f, 0.f, 0.f, 0.f};
+    float gb = 0.f, am = 0.f;
+    for (int it = wv; it < n; it += nw) {
+        const int s = a.work[it];
+        const int nnb = a.samp_nnb[s], ro = a.row_off[s];
+        const float das = dfeat[s].x;
+        const f32x4 df = *(const f32x4 *)(dfs + (int64_t)it * 256 + 4 * lane);
+        for (int k = 0; k < nnb; ++k) {
+            const int64_t j = ro + k;
+            f32x4 z = *(const f32x4 *)(z4d4 + j * 256 + 4 * lane);
+            f32x4 h;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) h[q] = lrelu_ref(z[q]);
+            const float za = wave_sum(wa4[0] * h[0] + wa4[1] * h[1] + wa4[2] * h[2] + wa4[3] * h[3]) + bav;
+            const float dot = wave_sum(h[0] * df[0] + h[1] * df[1] + h[2] * df[2] + h[3] * df[3]);
+            const float x = za - 1.f;
+            const float al = softplus_ref(x), sg = x > 20.f ? 1.f : 1.f / (1.f + expf(-x));
+            const float2 ww = rw[j];
+            const float dza = ww.x * das * sg;
+            const float dw = dot + al * das;
+            f32x4 d;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float t = ww.x * df[q] + dza * wa4[q];
+                d[q] = z[q] > 0.f ? t : t * 0.01f;
+                am = fmaxf(am, fabsf(d[q]));
+                gw[q] += dza * h[q];
+            }
+            gb += dza;
+            *(f32x4 *)(z4d4 + j * 256 + 4 * lane) = d;
+            if (lane == 0) {
+                const int pid = a.pidx[(int64_t)s * a.K + k];
+                atomicAdd(g_conf + pid, dw * ww.y);
+            }
+        }
+    }
+    *(f32x4 *)&sh[wl][4 * lane] = gw;
+    if (lane == 0) sh[wl][256] = gb;
+    __syncthreads();
+    for (int j = threadIdx.x; j < 257; j += TPB) {
+        float v = 0.f;
+        for (int q = 0; q < TPB / 64; ++q) v += sh[q][j];
+        part[(int64_t)blockIdx.x * 257 + j] = v;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
+    if (lane == 0) atomicMax(amax, __builtin_bit_cast(uint32_t, am));
+}
+
+// the point gradients of a row: d emb through [emb | PE(emb)] (networks.py:175-192) from block1.0's
+// input gradient dx0 [rows][224]; d colour, d dir from block3.0's extra-channel gradient dext
+// [rows][8] (d (dir - v) + v d <dir, v>)
+__global__ __launch_bounds__(TPB) void k_row_tail(RowArgs a, const float *dx0, const float *dext, float *g_emb,
+                                                  float *g_color, float *g_dir) {
+    const int lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TPB / 64);
+    const int n = n_items(a);
+    for (int it = wv; it < n; it += nw) {
+        const int s = a.work[it];
+        const int nnb = a.samp_nnb[s], ro = a.row_off[s];
+        const int ray = a.samp_ray[s];
+        for (int k = 0; k < nnb; ++k) {
+            const int64_t j = ro + k;
+            const int pid = a.pidx[(int64_t)s * a.K + k];
+            if (lane < 32) {
+                const float *g = dx0 + j * 224;
+                const float e = a.emb[(int64_t)pid * 32 + lane];
+                float de = g[lane];
+#pragma unroll
+                for (int f = 0; f < 3; ++f) {
+                    const float sc = (float)(1 << f), x = e * sc;
+                    const int c = 32 + 2 * (3 * lane + f);
+                    de += g[c] * cosf(x) * sc - g[c + 1] * sinf(x) * sc;
+                }
+                atomicAdd(g_emb + (int64_t)pid * 32 + lane, de);
+            } else if (lane < 38) {
+                const int c = lane - 32;
+                const float *g = dext + j * 8;
+                if (c < 3) {
+                    atomicAdd(g_color + (int64_t)pid * 3 + c, g[c]);
+                } else {
+                    const float v = a.raydir[(int64_t)ray * 3 + c - 3];
+                    atomicAdd(g_dir + (int64_t)pid * 3 + c - 3, g[c] + g[6] * v);
+                }
+            }
+        }
+    }
+}
+
+// ---- partials -> flat gradient ---------------------------------------------------------------
+
+struct RedSeg {
+    const float *part;
+    int32_t splits, M, N, n_in, bias_col, ldw;
+    float *dst_w, *dst_b;
+};
+constexpr int MAX_RED = 16;
+struct RedArgs {
+    RedSeg s[MAX_RED];
+    int64_t start[MAX_RED + 1];
+    int32_t n_seg;
+};
+
+__global__ __launch_bounds__(TPB) void k_reduce_partials(RedArgs r) {
+    const int64_t t = blockIdx.x * (int64_t)TPB + threadIdx.x;
+    if (t >= r.start[r.n_seg]) return;
+    int q = 0;
+    while (q + 1 < r.n_seg && t >= r.start[q + 1]) ++q;
+    const RedSeg &s = r.s[q];
+    const int64_t e = t - r.start[q];
+    const int m = (int)(e / s.N), c = (int)(e % s.N);
+    const int64_t stride = (int64_t)s.M * s.N;
+    float v = 0.f;
+    for (int i = 0; i < s.splits; ++i) v += s.part[i * stride + e];
+    if (c < s.n_in) s.dst_w[(int64_t)m * s.ldw + c] += v;
+    else if (c == s.bias_col) s.dst_b[m] += v;
+}
+
+}  // namespace tx
+}  // namespace
+}  // namespace sgn
+
+extern "C" {
+
+int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(ga, "null argument");
+    const sgn_x3_gemm_args &g = *ga;
+    SGN_REQUIRE(g.mode == 0 || g.mode == 1, "mode: 0 rows, 1 split-K partials");
+    SGN_REQUIRE(g.M >= 0 && g.N > 0 && g.K >= 0, "bad extents");
+    SGN_REQUIRE(g.a.p && g.b.p, "null operand");
+    auto conv = [](const sgn_x3_operand &o, int dyn, int nrows, Opnd &d) -> int {
+        if ((o.csplit < o.ncols) && (!o.p2 || o.csplit % 8 != 0)) return -1;
+        if (o.amax && o.shift) return -1;
+        d.p = o.p; d.p2 = o.p2; d.ld = o.ld; d.ld2 = o.ld2;
+        d.csplit = o.csplit < o.ncols ? o.csplit : 0x7fffffff;
+        d.ncols = o.ncols; d.ones_col = o.ones_col; d.act = o.act; d.kmajor = o.kmajor;
+        d.nrows = nrows; d.dyn = dyn; d.amax = o.amax; d.shift = o.shift;
+        const bool al1 = ((uintptr_t)o.p & 15) == 0 && o.ld % 4 == 0;
+        const bool al2 = !o.p2 || (((uintptr_t)o.p2 & 15) == 0 && o.ld2 % 4 == 0);
+        d.vec = !o.kmajor && al1 && al2;
+        return 0;
+    };
+    GemmK k{};
+    // the data rows: mode 0 = A's rows (M, device count); mode 1 = the reduction (K, device count)
+    SGN_REQUIRE(conv(g.a, 1, g.mode == 0 ? g.M : g.K, k.A) == 0, "operand a: bad column split or scale source");
+    SGN_REQUIRE(conv(g.b, g.mode == 1, g.mode == 0 ? (g.b.kmajor ? g.K : g.N) : g.K, k.B) == 0,
+                "operand b: bad column split or scale source");
+    if (g.mode == 0) {
+        SGN_REQUIRE(!g.a.kmajor, "mode 0: operand a is row-major [rows][K]");
+        SGN_REQUIRE(g.out && g.out_cols > 0 && (g.out_cols >= g.N || g.out2), "mode 0: out (and out2 past out_cols)");
+        // B's "rows": kmajor 0 -> its i = n < N; kmajor 1 -> its k < K
+        k.B.nrows = g.b.kmajor ? g.K : g.N;
+    } else {
+        SGN_REQUIRE(g.a.kmajor && g.b.kmajor, "mode 1: both operands [rows][...] (kmajor)");
+        SGN_REQUIRE(g.part && g.splits >= 1 && g.splits <= 4096, "mode 1: partials and 1..4096 splits");
+    }
+    k.M = g.M; k.N = g.N; k.K = g.K;
+    k.d_rows = g.d_rows;
+    k.bias = g.bias; k.act = g.act; k.mask = g.mask; k.ldm = g.ldm;
+    k.out = g.out; k.ldo = g.ldo; k.out_cols = g.out_cols < g.N ? g.out_cols : g.N;
+    k.out2 = g.out2; k.ldo2 = g.ldo2; k.amax_out = g.amax_out; k.amax_out2 = g.amax_out2;
+    k.part = g.part;
+    hipStream_t st = as_stream(stream);
+    if (g.mode == 0) {
+        if (g.M == 0) return 0;
+        // column block: 128 wide unless 96 covers N with less padding
+        const bool w96 = ((g.N + 95) / 96) * 96 < ((g.N + 127) / 128) * 128;
+        const int BN = w96 ? 96 : 128, BM = 128;
+        const int nb = (g.N + BN - 1) / BN;
+        const int tiles = (g.M + BM - 1) / BM;
+        int gy = 1024 / nb;
+        gy = gy < 1 ? 1 : gy > tiles ? tiles : gy;
+        if (w96) hipLaunchKernelGGL((k_x3gemm<1, 3, 4, 1, false>), dim3(nb, gy), dim3(TPB), 0, st, k);
+        else hipLaunchKernelGGL((k_x3gemm<2, 2, 2, 2, false>), dim3(nb, gy), dim3(TPB), 0, st, k);
+    } else {
+        const int BM = g.M > 128 ? 256 : 128;
+        const int BN = g.N <= 32 ? 32 : 96;
+        const int nbm = (g.M + BM - 1) / BM, nbn = (g.N + BN - 1) / BN;
+        const dim3 grid(nbm * nbn, g.splits);
+        if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3gemm<2, 3, 4, 1, true>), grid, dim3(TPB), 0, st, k);
+        else if (BM == 256) hipLaunchKernelGGL((k_x3gemm<2, 1, 4, 1, true>), grid, dim3(TPB), 0, st, k);
+        else if (BN == 96) hipLaunchKernelGGL((k_x3gemm<1, 3, 4, 1, true>), grid, dim3(TPB), 0, st, k);
+        else hipLaunchKernelGGL((k_x3gemm<1, 1, 4, 1, true>), grid, dim3(TPB), 0, st, k);
+    }
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_train_lists(const int32_t *d_counters, const int32_t *d_samp_nnb, int64_t s_cap, int32_t *d_work,
+                    int32_t *d_row_off, float *d_feat, int32_t *d_counts, void *d_ws, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(d_counters && d_samp_nnb && d_work && d_row_off && d_feat && d_counts && d_ws, "null argument");
+    SGN_REQUIRE(s_cap >= 1 && s_cap < (1 << 30), "s_cap out of range");
+    const int nb = (int)((s_cap + LIST_PER_BLOCK - 1) / LIST_PER_BLOCK);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_lists_count, dim3(nb), dim3(TPB), 0, st, d_counters, d_samp_nnb, (int2 *)d_ws);
+    hipLaunchKernelGGL(k_lists_write, dim3(nb), dim3(TPB), 0, st, d_counters, d_samp_nnb, (const int2 *)d_ws, d_work,
+                       d_row_off, (float4 *)d_feat, d_counts);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+size_t sgn_train_lists_workspace_bytes(int64_t s_cap) {
+    return (size_t)((s_cap + sgn::tx::LIST_PER_BLOCK - 1) / sgn::tx::LIST_PER_BLOCK + 1) * 8;
+}
+
+namespace {
+sgn::tx::RowArgs row_args(const sgn_point_tables *pt, const sgn_query_out *q, int32_t K, const int32_t *row_off,
+                          const int32_t *counts) {
+    sgn::tx::RowArgs a{};
+    a.xyz = pt->xyz; a.emb = pt->embedding; a.color = pt->color; a.dir = pt->dir; a.conf = pt->conf;
+    a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
+    a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.samp_nnb = q->samp_nnb; a.pidx = q->pidx;
+    a.samp_locw = q->samp_locw; a.row_off = row_off; a.tl = counts; a.K = K;
+    return a;
+}
+constexpr int ROW_GRID = 1024;
+}  // namespace
+
+int sgn_train_row_inputs(const sgn_point_tables *pt, const sgn_query_out *q, int32_t K, const int32_t *d_row_off,
+                         const int32_t *d_counts, float *d_x0, float *d_ext, float *d_rw, float *d_vpe,
+                         sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(pt && q && d_row_off && d_counts && d_x0 && d_ext && d_rw && d_vpe, "null argument");
+    SGN_REQUIRE(K >= 1 && K <= 8, "K = 1 .. 8");
+    SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
+    SGN_REQUIRE(((uintptr_t)d_x0 & 15) == 0 && ((uintptr_t)d_rw & 7) == 0, "aligned x0 / rw required");
+    const RowArgs a = row_args(pt, q, K, d_row_off, d_counts);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_row_inputs, dim3(ROW_GRID), dim3(TPB), 0, st, a, d_x0, d_ext, (float2 *)d_rw);
+    hipLaunchKernelGGL(k_colour_in, dim3(ROW_GRID), dim3(TPB), 0, st, a, d_vpe);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_train_colour_head(const sgn_query_out *q, const int32_t *d_counts, const float *d_h3, const float *d_w6,
+                          const float *d_b6, float *d_feat, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(q && d_counts && d_h3 && d_w6 && d_b6 && d_feat, "null argument");
+    SGN_REQUIRE(((uintptr_t)d_h3 & 7) == 0, "aligned h3 required");
+    RowArgs a{};
+    a.work = q->work; a.tl = d_counts;
+    hipLaunchKernelGGL(k_colour_head, dim3(ROW_GRID), dim3(TPB), 0, as_stream(stream), a, d_h3, d_w6, d_b6,
+                       (float4 *)d_feat);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+size_t sgn_train_head_partial_floats(int32_t which) {
+    return (size_t)sgn::tx::HEAD_BLOCKS * (which == 0 ? 3 * 129 : 257);
+}
+
+int sgn_train_colour_head_bwd(const sgn_query_out *q, const int32_t *d_counts, const float *d_h3, const float *d_w6,
+                              const float *d_b6, const float *d_dfeat, float *d_dy3, uint32_t *d_amax, float *d_part,
+                              sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(q && d_counts && d_h3 && d_w6 && d_b6 && d_dfeat && d_dy3 && d_amax && d_part, "null argument");
+    RowArgs a{};
+    a.work = q->work; a.tl = d_counts;
+    hipLaunchKernelGGL(k_colour_head_bwd, dim3(HEAD_BLOCKS), dim3(TPB), 0, as_stream(stream), a, d_h3, d_w6, d_b6,
+                       (const float4 *)d_dfeat, d_dy3, d_amax, d_part);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_train_row_head(const sgn_point_tables *pt, const sgn_query_out *q, int32_t K, const int32_t *d_row_off,
+                       const int32_t *d_counts, float *d_z4_delta4, const float *d_dfs, const float *d_dfeat,
+                       const float *d_rw, const float *d_wa, const float *d_ba, float *d_gconf, uint32_t *d_amax,
+                       float *d_part, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(pt && q && d_row_off && d_counts && d_z4_delta4 && d_dfs && d_dfeat && d_rw && d_wa && d_ba && d_gconf &&
+                    d_amax && d_part,
+                "null argument");
+    SGN_REQUIRE(K >= 1 && K <= 8, "K = 1 .. 8");
+    const RowArgs a = row_args(pt, q, K, d_row_off, d_counts);
+    hipLaunchKernelGGL(k_row_head, dim3(HEAD_BLOCKS), dim3(TPB), 0, as_stream(stream), a, d_z4_delta4, d_dfs,
+                       (const float4 *)d_dfeat, (const float2 *)d_rw, d_wa, d_ba, d_gconf, d_amax, d_part);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_train_row_tail(const sgn_point_tables *pt, const sgn_query_out *q, int32_t K, const int32_t *d_row_off,
+                       const int32_t *d_counts, const float *d_dx0, const float *d_dext, const sgn_point_grads *grads,
+                       sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(pt && q && d_row_off && d_counts && d_dx0 && d_dext && grads, "null argument");
+    SGN_REQUIRE(grads->embedding && grads->color && grads->dir, "null gradient outputs");
+    SGN_REQUIRE(K >= 1 && K <= 8, "K = 1 .. 8");
+    const RowArgs a = row_args(pt, q, K, d_row_off, d_counts);
+    hipLaunchKernelGGL(k_row_tail, dim3(ROW_GRID), dim3(TPB), 0, as_stream(stream), a, d_dx0, d_dext, grads->embedding,
+                       grads->color, grads->dir);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_reduce_partials(int32_t n_seg, const sgn_partial_segment *segs, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(segs && n_seg >= 1 && n_seg <= MAX_RED, "1..16 segments");
+    RedArgs r{};
+    r.n_seg = n_seg;
+    r.start[0] = 0;
+    for (int i = 0; i < n_seg; ++i) {
+        const sgn_partial_segment &s = segs[i];
+        SGN_REQUIRE(s.part && s.splits >= 1 && s.M >= 1 && s.N >= 1 && s.dst_w, "bad segment");
+        SGN_REQUIRE(s.n_in <= s.N && (s.bias_col < 0 || (s.bias_col < s.N && s.dst_b)), "bad segment columns");
+        r.s[i] = RedSeg{s.part, s.splits, s.M, s.N, s.n_in, s.bias_col, s.ldw, s.dst_w, s.dst_b};
+        r.start[i + 1] = r.start[i] + (int64_t)s.M * s.N;
+    }
+    const int64_t blocks = (r.start[n_seg] + TPB - 1) / TPB;
+    hipLaunchKernelGGL(k_reduce_partials, dim3((unsigned)blocks), dim3(TPB), 0, as_stream(stream), r);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

@@ -612,7 +612,76 @@ class HipTrainer:
         return parts, full.detach(), ray_mask
 
     # -- fp32-faithful step ---------------------------------------------------------------------
+    def _loss_params(self):
+        o = self.opts
+        lp = _lib.LossParams()
+        lp.SR, lp.K = o.SR, o.K
+        lp.vsize_z, lp.raydist_mode_unit = float(o.vsize[2]), int(o.raydist_mode_unit)
+        for i in range(3):
+            lp.bg[i] = 1.0
+        lp.zero_one_weight, lp.zero_one_eps = 1e-4, 1e-3   # train_ft: zero_one weight 1e-4, epsilon 1e-3
+        return lp
+
     def _backward_f32(self, campos, rot, raydir, near, far, gt, labels=None):
+        """The reference's fp32 step on hand-written kernels (train_f32.F32Step): query, forward,
+        colour MLP, losses and the whole backward as HIP launches with the counts on the device (no
+        host sync on one GPU; under DP one for the touched-row counts).  SGN_F32_TORCH=1: the earlier
+        step (HIP forward, torch fp32 autograd backward), kept for A/B."""
+        if os.environ.get("SGN_F32_TORCH", "0") == "1":
+            return self._backward_f32_torch(campos, rot, raydir, near, far, gt, labels)
+        from .train_f32 import F32Step
+        o = self.opts
+        dev = self.device
+        campos = campos.reshape(3).to(dev, torch.float32).contiguous()
+        rot = rot.reshape(3, 3).to(dev, torch.float32).contiguous()
+        raydir = raydir.reshape(-1, 3).to(dev, torch.float32).contiguous()
+        gt = gt.reshape(-1, 3).to(dev, torch.float32).contiguous()
+        R = raydir.shape[0]
+        q = self._query(campos, raydir, near, far, labels)
+        blob = self.packer32.pack(self.mlp.flat)
+        for p in self.point_params + [self.mlp.flat]:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            elif not (self._pts_grad_clean and p is not self.mlp.flat):
+                p.grad.zero_()
+        self._pts_grad_clean = False
+        L = _lib.lib()
+        st = _lib.stream_handle()
+        pt = self._tables(campos, rot, raydir)
+        P = self.points
+        npts = P.xyz.shape[0]
+        nproj = int(L.sgn_point_proj_bytes_f32(npts))
+        if getattr(self, "_proj32", None) is None or self._proj32.numel() < nproj:
+            self._proj32 = torch.empty(max(nproj, 16), dtype=torch.uint8, device=dev)
+        dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        t_idx = t_cnt = None
+        if dp or self.proj_subset:
+            t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, npts)
+        if self.proj_subset:
+            _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(t_idx.to(torch.int32)),
+                                                      _lib.ptr(t_cnt), _lib.ptr(self._proj32), st),
+                       "sgn_point_project_f32_subset")
+        else:
+            _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(self._proj32), st),
+                       "sgn_point_project_f32")
+        step = getattr(self, "_f32step", None)
+        key = (R, q.work.data_ptr(), q.pidx.data_ptr(), self.mlp.flat.data_ptr(), self.mlp.flat.grad.data_ptr())
+        if step is None or step.key != key:
+            step = self._f32step = F32Step(self, q, R)
+            step.key = key
+        losses, full, mask = step.run(pt, self._proj32, blob, campos, rot, gt, self._loss_params())
+        self._last_q, self._last_qd = q, None
+        total = losses[0] + 3e-6 + 1e-4 * losses[1]
+        parts = {"ray_masked_coarse_raycolor": losses[0], "ray_miss_coarse_raycolor": losses[2],
+                 "coarse_raycolor": losses[3], "conf_coefficient": losses[1]}
+        self.allreduce_grads([self.mlp.flat])
+        if dp:
+            t_counts = [int(x) for x in gather_counts(t_cnt).tolist()]
+            _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
+        parts["total"] = total
+        return parts, full, mask.bool()
+
+    def _backward_f32_torch(self, campos, rot, raydir, near, far, gt, labels=None):
         """The reference's fp32 step: HIP query, the fp32-faithful row MLP on the HIP kernels
         (k_point_proj16 + k_pair_slots + k_rows16 save mode: block1.0 / 1.2 / 3.0 pre-activations per
         row), then train.aggregate(saved=...) (those three layers take their forward values from the
@@ -663,7 +732,7 @@ class HipTrainer:
         qo = q.abi()
         _lib.check(L.sgn_aggregate_train_fwd_f32(_lib.ptr(self._proj32), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
                                                  _lib.ptr(blob), _lib.ptr(self._feat32), _lib.ptr(self._z32[0]),
-                                                 _lib.ptr(self._z32[1]), _lib.ptr(self._z32[2]), _lib.ptr(self._ws32),
+                                                 _lib.ptr(self._z32[1]), _lib.ptr(self._z32[2]), None, _lib.ptr(self._ws32),
                                                  self._ws32.numel(), st), "sgn_aggregate_train_fwd_f32")
         # valid rows (sum of the samples' neighbour counts) on the device, fetched with S
         nnb = q.samp_nnb[:cap]
@@ -673,7 +742,7 @@ class HipTrainer:
         S, n_rows, *t_counts = (int(x) for x in sync.tolist())   # one host sync per step
         qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
               "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
-        self.last_query = qd   # the step's sample-major query (tests rerun fp32 autograd on it)
+        self._last_qd = qd   # the step's sample-major query (tests rerun fp32 autograd on it)
         rows = torch.nonzero_static(qd["pidx"].reshape(-1) >= 0, size=n_rows).reshape(-1)   # no second sync
         feat, _, mask = aggregate(P, self.mlp, campos.reshape(1, 3), rot, raydir, qd["samp_ray"], qd["samp_locw"],
                                   qd["pidx"], saved=self._z32, rows=rows)
@@ -688,6 +757,17 @@ class HipTrainer:
             _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
         parts["total"] = total.detach()
         return parts, full.detach(), ray_mask
+
+    @property
+    def last_query(self):
+        """The last fp32 step's sample-major query as a dict (ray_ns, ray_soff, samp_ray, samp_locw,
+        pidx): tests rerun fp32 autograd on the very samples the step used.  Reads S (host sync)."""
+        if getattr(self, "_last_qd", None) is not None:
+            return self._last_qd
+        q, o = self._last_q, self.opts
+        R, S = q.R, int(q.counters[0].item())
+        return {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
+                "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
 
     # -- graph-captured loss stage -----------------------------------------------------------
     def _loss_body(self, st):
