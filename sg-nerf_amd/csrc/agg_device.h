@@ -103,7 +103,6 @@ struct AggArgs {
     _Float16 *sh3;    // [rows][256] block3.2 inputs (chain order)
     _Float16 *sh2b;   // [rows][256] block2_bpnet inputs h (chain order; SG save mode, where sh2 then
                       // holds block3.0's inputs [block2_bpnet output | colour, dir - v, <dir, v>])
-    unsigned long long *tdbg;  // timing builds only (SGN_X3_TIMING): per-wave clock stamps
     // packed point records of the fp32 16x16 kernels (k_point_proj16 writes them beside P):
     // 64 B per point = {x, y, z, conf}, {r, g, b, 0}, {dx, dy, dz, 0}, {0}; one cache line per row
     const float *rec;
@@ -207,10 +206,6 @@ __device__ __forceinline__ float l0_channel(const float (&feat)[16], const float
 
 template <int K0>
 __device__ __forceinline__ h8 l0_step(const float (&feat)[16], const float (&dist)[3]) {
-#ifdef SGN_ABLATE_PE  // timing experiment only: raw features instead of encodings (wrong results)
-    return pack8(feat[(8 * K0) & 15], feat[(8 * K0 + 1) & 15], feat[(8 * K0 + 2) & 15], feat[(8 * K0 + 3) & 15],
-                 feat[(8 * K0 + 4) & 15], feat[(8 * K0 + 5) & 15], dist[K0 % 3], feat[(8 * K0 + 7) & 15]);
-#endif
     return pack8(l0_channel<8 * K0 + 0>(feat, dist), l0_channel<8 * K0 + 1>(feat, dist),
                  l0_channel<8 * K0 + 2>(feat, dist), l0_channel<8 * K0 + 3>(feat, dist),
                  l0_channel<8 * K0 + 4>(feat, dist), l0_channel<8 * K0 + 5>(feat, dist),
@@ -272,11 +267,7 @@ __device__ __forceinline__ RowIdx row_index(const AggArgs &a, int item, int end,
     RowIdx x;
     x.sval = item < end;
     x.s = x.sval ? a.work[item] : 0;
-#ifdef SGN_DEBUG_FAST_GATHER  // timing experiment only: no dependent index load, L2-resident records
-    x.pid = x.sval ? ((item * 8 + (lane & 7)) & 1023) : -1;
-#else
     x.pid = x.sval ? a.pidx[(int64_t)x.s * 8 + (lane & 7)] : -1;
-#endif
     x.ray = x.sval ? a.samp_ray[x.s] : 0;  // no sample id to follow without a work item
     return x;
 }

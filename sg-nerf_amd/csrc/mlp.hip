@@ -43,17 +43,8 @@ namespace {
 constexpr int ROWS_TPB = 512;
 constexpr int WG_WAVES = ROWS_TPB / 64;
 constexpr int WG_SAMPLES = WG_WAVES * 4;  // 32
-#ifndef SGN_CHUNK_FRAGS
-#define SGN_CHUNK_FRAGS 32
-#endif
-constexpr int CHUNK_FRAGS = SGN_CHUNK_FRAGS;  // fragments per LDS chunk (k-steps x tiles of a pass)
-#ifndef SGN_FRAG_PD
-#define SGN_FRAG_PD 3
-#endif
-#ifndef SGN_SCHED_PIN
-#define SGN_SCHED_PIN 1
-#endif
-constexpr int FRAG_PD = SGN_FRAG_PD;  // weight fragments in flight per wave (LDS -> VGPR queue)
+constexpr int CHUNK_FRAGS = 32;  // fragments per LDS chunk (k-steps x tiles of a pass)
+constexpr int FRAG_PD = 3;  // weight fragments in flight per wave (LDS -> VGPR queue)
 // output tiles per pass: layer 0 runs all 8 tiles in one pass (its inputs are generated on
 // the fly and never stored), the chained layers run two passes of 4 (their input fragments
 // stay in registers, the accumulators of 8 tiles would not fit beside them)
@@ -61,71 +52,20 @@ __host__ __device__ constexpr int layer_tp(int L) { return L == 0 ? 8 : 4; }
 __host__ __device__ constexpr int layer_np(int L) { return 8 / layer_tp(L); }
 // block3.0 (17 k-steps: 256 chained + the colour/dir channels) goes in chunks of 9 + 8 k-steps
 // instead of 8 + 8 + 1: a 4-fragment tail chunk cost a whole boundary (~2.3 k cycles for 4
-// MFMAs per wave, tools/tdbg.py)
-#ifndef SGN_KC2
-#define SGN_KC2 9
-#endif
-__host__ __device__ constexpr int layer_kc(int L) { return L == 2 ? SGN_KC2 : CHUNK_FRAGS / layer_tp(L); }
-constexpr int MAX_CHUNK_FRAGS = SGN_KC2 * 4 > CHUNK_FRAGS ? SGN_KC2 * 4 : CHUNK_FRAGS;
+// MFMAs per wave, measured with clock stamps in round 2)
+__host__ __device__ constexpr int layer_kc(int L) { return L == 2 ? 9 : CHUNK_FRAGS / layer_tp(L); }
+constexpr int MAX_CHUNK_FRAGS = 9 * 4 > CHUNK_FRAGS ? 9 * 4 : CHUNK_FRAGS;
 constexpr int SLOT_BYTES = MAX_CHUNK_FRAGS * (int)FRAG;
-// LAG > 0: waves WG_WAVES/2.. (followers, one per SIMD) run LAG chunks behind waves 0..
-// (leaders, one per SIMD), so on every SIMD one wave's VALU epilogue overlaps the other's
-// MFMAs instead of both stalling the matrix pipe at once.  The leaders issue every LDS-DMA;
-// the ring keeps LAG extra slots for the followers.
-#ifndef SGN_LAG
-#define SGN_LAG 0
-#endif
-constexpr int LAG = SGN_LAG;
-// SGN_DMA_HALF: only waves 0..3 issue the weight LDS-DMAs (and wait vmcnt(0) at chunk boundaries);
-// waves 4..7 never wait on memory at a boundary, so they issue the workgroup's mid-tile global
-// stores (their own and, through LDS, those of waves 0..3): a store's ~2.5 us acknowledgement
-// otherwise stalls the issuing wave's next boundary.
-#ifndef SGN_NT_GATHER
-#define SGN_NT_GATHER 0
-#endif
-#ifndef SGN_STAGGER
-#define SGN_STAGGER 1
-#endif
-#ifndef SGN_DMA_HALF
-#define SGN_DMA_HALF 0
-#endif
-constexpr int N_DMA_WAVES = (LAG || SGN_DMA_HALF) ? WG_WAVES / 2 : WG_WAVES;
-constexpr int PF_N = CHUNK_FRAGS / N_DMA_WAVES;  // LDS-DMA instructions per issuing wave per chunk
-constexpr int PF_MAX = (MAX_CHUNK_FRAGS + N_DMA_WAVES - 1) / N_DMA_WAVES;
-#ifndef SGN_DIST
-#define SGN_DIST 1  // measured: 1 chunk in flight beats 2 by 12 % (k_agg_rows 13.65 -> 11.97 ms, same box)
-#endif
-constexpr int DIST = SGN_DIST;                // chunks in flight ahead of the one being consumed
-constexpr int NSLOT = DIST + LAG + 1;         // ring slots (the DMA target was read LAG+1 chunks ago)
+constexpr int PF_MAX = (MAX_CHUNK_FRAGS + WG_WAVES - 1) / WG_WAVES;  // LDS-DMA pieces per wave per chunk (max)
+constexpr int NSLOT = 2;  // ring slots: the next chunk in flight while the current one is read (two
+                          // in flight measured 12 % slower: k_agg_rows 13.65 vs 11.97 ms, same box)
 constexpr int LDS_F32_OFF = NSLOT * SLOT_BYTES;
-constexpr int STAGE_OFF = LDS_F32_OFF + (int)(N_F32 + HID) * 4;  // + block2_bpnet bias (SG)
-constexpr int STAGE_BYTES = N_DMA_WAVES < WG_WAVES ? WG_WAVES * 1024 : 0;  // block3.2 pass-0 features, per wave
-// SGN_FS_WIDE: blended features leave through a per-wave LDS transpose as one 16-B store per
-// lane and block3.2 pass (full 128-B lines) instead of eight 2-B scattered stores
-#ifndef SGN_FS_WIDE
-#define SGN_FS_WIDE 1
-#endif
-constexpr int FSW_OFF = STAGE_OFF + STAGE_BYTES;
-constexpr int FSW_BYTES = SGN_FS_WIDE ? WG_WAVES * 1024 : 0;  // [wave][4 samples][128 units] fp16
+// blended features leave through a per-wave LDS transpose as one 16-B store per lane and
+// block3.2 pass (full 128-B lines) instead of eight 2-B scattered stores
+constexpr int FSW_OFF = LDS_F32_OFF + (int)(N_F32 + HID) * 4;  // after the fp32 section + block2_bpnet bias (SG)
+constexpr int FSW_BYTES = WG_WAVES * 1024;  // [wave][4 samples][128 units] fp16
 constexpr int LDS_BYTES = FSW_OFF + FSW_BYTES;
 static_assert(CHUNK_FRAGS % WG_WAVES == 0, "chunk must split evenly over the waves");
-#ifdef SGN_TIMING
-// Timing build only: every chunk boundary of the first TDBG_BLOCKS workgroups writes the wave's
-// clock (s_memtime) to g_tdbg[(block * 8 + wave) * TDBG_EV + seq]; seq lives in LDS after the
-// kernel's own bytes (non-SG variants).
-constexpr int TDBG_BLOCKS = 4, TDBG_EV = 512;
-__device__ unsigned long long *g_tdbg;
-#endif
-#ifdef SGN_TIMING
-__device__ __forceinline__ void tmark(char *lds, int w, int lane) {
-    int *seq = (int *)(lds + LDS_BYTES) + w;
-    const int n = *seq;
-    if (lane == 0) {
-        if (blockIdx.x < TDBG_BLOCKS && n < TDBG_EV) g_tdbg[((int64_t)blockIdx.x * 8 + w) * TDBG_EV + n] = clock64();
-        *seq = n + 1;
-    }
-}
-#endif
 
 
 // Layers of the row stream: 0 block1.0, 1 block1.2, 2 block3.0, 3 block3.2, 4 block2_bpnet.0
@@ -178,68 +118,40 @@ __host__ __device__ constexpr int chunk_P(int KSB, int n) {
 __host__ __device__ constexpr int chunk_C(int KSB, int n) {
     return (n - chunk_base(KSB, chunk_L(KSB, n))) % pass_chunks(KSB, chunk_L(KSB, n));
 }
-static_assert(CHUNK_FRAGS != 32 || SGN_KC2 != 9 || n_chunks(0) == 5 + 2 * (2 + 2 + 2), "base stream");
-static_assert(CHUNK_FRAGS != 32 || SGN_KC2 != 9 ||
-                  (chunk_L(ks_bp(BP_DIM), 9) == 4 && chunk_L(ks_bp(BP_DIM), 8) == 1 &&
+static_assert(n_chunks(0) == 5 + 2 * (2 + 2 + 2), "base stream");
+static_assert((chunk_L(ks_bp(BP_DIM), 9) == 4 && chunk_L(ks_bp(BP_DIM), 8) == 1 &&
                    chunk_L(ks_bp(BP_DIM), 15) == 2 && n_chunks(ks_bp(BP_DIM)) == 23),
               "SG stream order");
-static_assert(CHUNK_FRAGS != 32 || SGN_KC2 != 9 || (n_chunks(256) == 1 + 2 * (2 + 2 + 2) && chunk_L(256, 1) == 1),
+static_assert((n_chunks(256) == 1 + 2 * (2 + 2 + 2) && chunk_L(256, 1) == 1),
               "split stream");
 
 // Issue the LDS-DMA of stream chunk N into LDS slot `dst`: each wave moves fragments
-// w + WG_WAVES*j (1 KiB, lane-linear) with buffer_load ... lds.  With DIST > 1 (counted
-// vmcnt below) every chunk is full and each wave issues exactly PF_N DMAs; with DIST = 1 the
-// boundary waits for vmcnt(0) and a wave issues only the fragments of the chunk it owns.
+// w + WG_WAVES*j (1 KiB, lane-linear) with buffer_load ... lds; the boundary waits for vmcnt(0).
 template <int KSB, int N>
 __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int lane, int lz) {
     constexpr int L = chunk_L(KSB, N), P = chunk_P(KSB, N), C = chunk_C(KSB, N);
     constexpr int nf = chunk_nk(KSB, L, C) * layer_tp(L);
-    static_assert(DIST == 1 || MAX_CHUNK_FRAGS == CHUNK_FRAGS, "counted vmcnt needs equal chunk slots");
     static_for<PF_MAX>([&](auto jj) {
         constexpr int J = decltype(jj)::value;
-        // DIST > 1: always PF_N DMAs (short chunks re-load their last fragment into spare slot space)
-        if constexpr (DIST > 1 ? J < PF_N : N_DMA_WAVES * J < nf) {
-            const int i = w + N_DMA_WAVES * J;
-            if (DIST > 1 || N_DMA_WAVES * (J + 1) <= nf || i < nf) {  // wave-uniform
-                const int src = min(i, nf - 1);
+        if constexpr (WG_WAVES * J < nf) {
+            const int i = w + WG_WAVES * J;
+            if (WG_WAVES * (J + 1) <= nf || i < nf) {  // wave-uniform
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     wb.rsrc, (__attribute__((address_space(3))) void *)(dst + i * (int)FRAG), 16,
-                    lane * 16, chunk_off(KSB, L, P, C) + (uint32_t)(src * (int)FRAG + lz), 0, 0);
+                    lane * 16, chunk_off(KSB, L, P, C) + (uint32_t)(i * (int)FRAG + lz), 0, 0);
             }
         }
     });
 }
 
-// Chunk boundary: wait for this wave's DMAs of the chunk about to be read (all but the
-// DIST-1 younger chunks' PF_N each), drain LDS reads, barrier; then start the DMA that is
-// DIST chunks ahead into the slot read one chunk ago.
+// Chunk boundary: wait for this wave's DMAs of the chunk about to be read, drain LDS reads,
+// barrier; then start the next chunk's DMA into the slot read one chunk ago.
 template <int KSB, int N>
 __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int &slot, int w, int lane, int lz) {
-#ifdef SGN_ABLATE_STREAM  // timing experiment only: no weight stream, no barriers (wrong results)
-    return;
-#endif
-    constexpr int younger = (DIST - 1) * PF_N;  // DMAs issued after this chunk's
-    static_assert(younger == 0 || younger == 4 || younger == 8, "add the vmcnt immediate");
-    const bool issuer = w < N_DMA_WAVES;  // wave-uniform
-#ifndef SGN_ABLATE_VMWAIT  // timing experiment only: boundaries do not wait for the DMA (wrong results)
-    if (issuer) {
-        if constexpr (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if constexpr (younger == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    }
-#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifndef SGN_ABLATE_BARRIER  // timing experiment only: no workgroup barrier at boundaries (wrong results)
     __builtin_amdgcn_s_barrier();
-#endif
-#ifdef SGN_TIMING
-    tmark(lds, w, lane);
-#endif
-    if (issuer) {
-        int tgt = slot + DIST;
-        tgt = tgt >= NSLOT ? tgt - NSLOT : tgt;
-        dma_chunk<KSB, (N + DIST) % n_chunks(KSB)>(wb, lds + tgt * SLOT_BYTES, w, lane, lz);
-    }
+    dma_chunk<KSB, (N + 1) % n_chunks(KSB)>(wb, lds + (slot ^ 1) * SLOT_BYTES, w, lane, lz);
 }
 
 // One pass of a layer, k-outer: acc[t] = bias + sum_k W[TP*P+t][k] * in(k), chunk by chunk.
@@ -284,9 +196,7 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
         h8 fr[PD];
 #pragma unroll
         for (int f = 0; f < PD; ++f) fr[f] = frag(f);
-#if SGN_SCHED_PIN
         __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);  // PD LDS reads in flight first
-#endif
         static_for<chunk_nk(KSB, L, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
             const h8 B = in(std::integral_constant<int, C * KC + KK>{});
@@ -295,10 +205,8 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
                 const h8 A = fr[F % PD];
                 if constexpr (F + PD < NF) fr[F % PD] = frag(F + PD);
                 acc[t] = TRANS ? mfma32(B, A, acc[t]) : mfma32(A, B, acc[t]);
-#if SGN_SCHED_PIN
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // then one LDS read
-#endif
             });
         });
         slot = slot + 1 == NSLOT ? 0 : slot + 1;
@@ -313,20 +221,11 @@ __device__ __forceinline__ void run_pass(const WBlob &wb, char *lds, int &slot, 
 // P[pid] of this lane's row -> 16 B fragments in accumulator order (layout: run_split_l0)
 __device__ __forceinline__ void load_proj(const _Float16 *proj, int pid, int lane, h8 (&pv)[16]) {
     const int h = lane >> 5;
-#ifdef SGN_ABLATE_PROJ  // timing experiment only: P of point 0 for every row (wrong results)
-    const h8 *src = (const h8 *)proj;
-#else
     const h8 *src = (const h8 *)(proj + (int64_t)(pid < 0 ? 0 : pid) * HID);
-#endif
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-#if SGN_NT_GATHER  // streaming hint: keep the weight stream resident in L2 (timing option)
-        pv[2 * t] = __builtin_nontemporal_load(src + (2 * t + h) * 2);
-        pv[2 * t + 1] = __builtin_nontemporal_load(src + (2 * t + h) * 2 + 1);
-#else
         pv[2 * t] = src[(2 * t + h) * 2];
         pv[2 * t + 1] = src[(2 * t + h) * 2 + 1];
-#endif
     }
 }
 
@@ -350,9 +249,7 @@ __device__ __forceinline__ void run_split_l0(const WBlob &wb, char *lds, int &sl
     h8 fr[PD];
 #pragma unroll
     for (int f = 0; f < PD; ++f) fr[f] = frag(fidx(f));
-#if SGN_SCHED_PIN
     __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
-#endif
     static_for<4>([&](auto pp) {
         constexpr int P = decltype(pp)::value;
 #pragma unroll
@@ -369,10 +266,8 @@ __device__ __forceinline__ void run_split_l0(const WBlob &wb, char *lds, int &sl
             const h8 A = fr[N % PD];
             if constexpr (N + PD < NF) fr[N % PD] = frag(fidx(N + PD));
             acc[T] = mfma32(A, B[K], acc[T]);
-#if SGN_SCHED_PIN
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-#endif
         });
     });
     slot = slot + 1 == NSLOT ? 0 : slot + 1;
@@ -387,18 +282,9 @@ __device__ __forceinline__ void chain_out(const f32x16 (&acc)[TP], h8 (&out)[16]
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
             const int t = TP * P + tt, r = 8 * s2;
-#if defined(SGN_ABLATE_ACT)  // timing experiment only: no activation (wrong results)
-            out[2 * t + s2] = pack8(acc[tt][r + 0], acc[tt][r + 1], acc[tt][r + 2], acc[tt][r + 3], acc[tt][r + 4],
-                                    acc[tt][r + 5], acc[tt][r + 6], acc[tt][r + 7]);
-#elif SGN_LRELU_F32
-            out[2 * t + s2] = pack8(lrelu_max(acc[tt][r + 0]), lrelu_max(acc[tt][r + 1]), lrelu_max(acc[tt][r + 2]),
-                                    lrelu_max(acc[tt][r + 3]), lrelu_max(acc[tt][r + 4]), lrelu_max(acc[tt][r + 5]),
-                                    lrelu_max(acc[tt][r + 6]), lrelu_max(acc[tt][r + 7]));
-#else
             const u32x4 u = {lrelu_pk(acc[tt][r + 0], acc[tt][r + 1]), lrelu_pk(acc[tt][r + 2], acc[tt][r + 3]),
                              lrelu_pk(acc[tt][r + 4], acc[tt][r + 5]), lrelu_pk(acc[tt][r + 6], acc[tt][r + 7])};
             out[2 * t + s2] = __builtin_bit_cast(h8, u);
-#endif
         }
 }
 
@@ -408,12 +294,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     constexpr bool SPLIT = vsplit(V);
     static_assert(!(SPLIT && SAVE), "the training save mode runs the unsplit block1.0");
     constexpr int NBP = KSB > KS_HID ? KSB - KS_HID : 0;  // BPNet k-steps (SG, predict_semantic = 1)
-#ifdef SGN_TIMING
-    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES + WG_WAVES * NBP * (int)FRAG + 64];
-    if (threadIdx.x < 8) ((int *)(lds + LDS_BYTES))[threadIdx.x] = 0;
-#else
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES + WG_WAVES * NBP * (int)FRAG];
-#endif
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, kk = lane & 7, q = (lane & 31) >> 3;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -421,11 +302,6 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     const int end = min(nwork, a.item0 + a.n_items);
     const Cam cam = load_cam(a.campos, a.rot);
     const WBlob wb = make_blob(a.blob, a.blob_bytes);
-#if defined(SGN_PRIO_HI)  // (timing option, measured neutral with DIST = 1) static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-    if (w >= WG_WAVES / 2) __builtin_amdgcn_s_setprio(1);
-#elif defined(SGN_PRIO_LO)
-    if (w < WG_WAVES / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     const __amdgpu_buffer_rsrc_t bp_rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.bpnet, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t fs_rsrc =
@@ -441,23 +317,13 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     }
     __syncthreads();  // parameters visible before the first tile's bias reads
     int slot = 0;
-    // stream prologue: chunks 0..DIST-1 in flight (chunk_enter<n> issues chunk n+DIST)
-    if (w < N_DMA_WAVES) {
-        static_for<DIST>([&](auto nn) {
-            constexpr int N0 = decltype(nn)::value;
-            dma_chunk<V, N0>(wb, lds + N0 * SLOT_BYTES, w, lane, 0);
-        });
-    } else if (LAG) {
-        // followers start LAG chunk intervals late (the leaders add LAG barriers at the end)
-        for (int i = 0; i < LAG; ++i) __builtin_amdgcn_s_barrier();
-    }
-#if SGN_STAGGER
+    // stream prologue: chunk 0 in flight (chunk_enter<n> issues chunk n + 1)
+    dma_chunk<V, 0>(wb, lds, w, lane, 0);
     // Phase stagger: every workgroup runs identical tiles, so without it all CUs gather their
     // tiles' point records (~150 KB per CU) in the same microseconds and the chip-wide burst
     // (~38 MB of random reads) sets the tile-start latency.  Eight start phases, one per
     // group of CUs on every XCD (workgroups go round-robin over the 8 XCDs), ~1/8 tile apart.
     for (int i = (blockIdx.x >> 3) & 7; i > 0; --i) __builtin_amdgcn_s_sleep(127);
-#endif
     // index chain of this wave's rows, one work tile ahead (issued mid-tile, see block1.2)
     RowIdx nx = row_index(a, a.item0 + blockIdx.x * WG_SAMPLES + w * 4 + q, end, lane);
     asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));  // waited for here (once), see block3.0
@@ -472,38 +338,19 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
     uint32_t pf0[4], pf1[4];
     // stores as wave ww; drop = true sends them out of the buffer's range (discarded by the
     // hardware) so the wave-role choice below needs no branch (a branch here costs ~20 spills)
-    auto flush_fs = [&](const uint32_t (&pv)[4], int pbase, int P, int ww, bool drop = false) {
-#if SGN_FS_WIDE
-        if constexpr (FSW_BYTES > 0) {
-            // lane (unit jl, half h) holds samples h (lo) and h + 2 (hi) of tiles 4P + tt
-            _Float16 *st = (_Float16 *)(lds + FSW_OFF + w * 1024);
+    auto flush_fs = [&](const uint32_t (&pv)[4], int pbase, int P, int ww) {
+        // lane (unit jl, half h) holds samples h (lo) and h + 2 (hi) of tiles 4P + tt
+        _Float16 *st = (_Float16 *)(lds + FSW_OFF + w * 1024);
 #pragma unroll
-            for (int tt = 0; tt < 4; ++tt) {
-                st[h * 128 + 32 * tt + jl] = __builtin_bit_cast(_Float16, (unsigned short)(pv[tt] & 0xffff));
-                st[(h + 2) * 128 + 32 * tt + jl] = __builtin_bit_cast(_Float16, (unsigned short)(pv[tt] >> 16));
-            }
-            // lane L: sample L >> 4, units 8 (L & 15) .. +7 of the pass (16 B)
-            const u32x4 v = *(const u32x4 *)(st + (lane >> 4) * 128 + 8 * (lane & 15));
-            const int it = pbase + ww * 4 + (lane >> 4);
-            const uint32_t off = (it < end && !drop) ? (uint32_t)((it - a.item0) * HID + 128 * P + 8 * (lane & 15)) * 2
-                                                     : 0xFFFF0000u;
-            __builtin_amdgcn_raw_buffer_store_b128(v, fs_rsrc, off, 0, 0);
-            return;
+        for (int tt = 0; tt < 4; ++tt) {
+            st[h * 128 + 32 * tt + jl] = __builtin_bit_cast(_Float16, (unsigned short)(pv[tt] & 0xffff));
+            st[(h + 2) * 128 + 32 * tt + jl] = __builtin_bit_cast(_Float16, (unsigned short)(pv[tt] >> 16));
         }
-#endif
-#pragma unroll
-        for (int k2 = 0; k2 < 2; ++k2) {
-            const int it = pbase + ww * 4 + h + 2 * k2;
-            const uint32_t off = (it < end && !drop) ? (uint32_t)((it - a.item0) * HID + jl) * 2 : 0xFFFF0000u;
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt)  // tile offset in the instruction's immediate
-#ifndef SGN_ABLATE_FS  // timing experiment only: no blended-feature stores (wrong results)
-                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(pv[tt] >> (16 * k2)), fs_rsrc, off,
-                                                      64 * (4 * P + tt), SGN_NT_GATHER ? 2 : 0);
-#else
-                (void)off;
-#endif
-        }
+        // lane L: sample L >> 4, units 8 (L & 15) .. +7 of the pass (16 B)
+        const u32x4 v = *(const u32x4 *)(st + (lane >> 4) * 128 + 8 * (lane & 15));
+        const int it = pbase + ww * 4 + (lane >> 4);
+        const uint32_t off = it < end ? (uint32_t)((it - a.item0) * HID + 128 * P + 8 * (lane & 15)) * 2 : 0xFFFF0000u;
+        __builtin_amdgcn_raw_buffer_store_b128(v, fs_rsrc, off, 0, 0);
     };
 
     for (int base = a.item0 + blockIdx.x * WG_SAMPLES; base < end; base += gridDim.x * WG_SAMPLES) {
@@ -515,13 +362,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         const int item = base + w * 4 + q;
         float feat[16], dist[3];
         h8 ext;
-#ifdef SGN_TIMING
-        tmark(ldsi, w, lane);  // tile start (after the loop back-edge)
-#endif
         const RowIn ri = gather_row<!SPLIT>(a, cam, nx, lane, feat, dist, ext);
-#ifdef SGN_TIMING
-        tmark(ldsi, w, lane);  // gather issued (and its uses that the compiler placed before this)
-#endif
         const int nitem = item + gridDim.x * WG_SAMPLES;
 
         const int64_t srow0 = (int64_t)(base + w * 4 - a.item0) * 8;  // first saved row of this wave (SAVE)
@@ -585,7 +426,6 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
                 if constexpr (K < 16) return actB[K];
                 else return *(const h8 *)(bpl + (K - 16) * (int)FRAG + lane * 16);
             };
-            if (w >= N_DMA_WAVES) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own BPNet LDS-DMA landed
             run_pass<V, 4, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
             chain_out<4, 0>(acc, actA);
             run_pass<V, 4, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_BB, acc, inBP);
@@ -663,32 +503,12 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         auto inA3 = [&](auto k) { return out3[decltype(k)::value]; };
         run_pass<V, 3, 0, true>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3);
         l3_epilogue(std::integral_constant<int, 0>{});
-        const bool dma_wave = w < N_DMA_WAVES;
-        if constexpr (STAGE_BYTES > 0) {
-            // pass-0 features: non-DMA waves store their own now; DMA waves leave theirs in LDS for
-            // wave w + 4, which stores them after block3.2 pass 1 (two barriers later)
-            uint32_t *stage = (uint32_t *)(ldsi + STAGE_OFF) + w * 256 + lane;
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) stage[tt * 64] = pf0[tt];
-            flush_fs(pf0, base, 0, w, dma_wave);
-        } else {
-            flush_fs(pf0, base, 0, w);
-        }
+        flush_fs(pf0, base, 0, w);
         run_pass<V, 3, 1, true, false, layer_nch(V, 3) - 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B3, acc, inA3, [&]() {
             if constexpr (SPLIT) load_proj(a.proj, nx.pid, lane, pnext);  // next tile's P (its last chunk)
         });
-        if constexpr (STAGE_BYTES > 0) {
-            const uint32_t *pstage = (const uint32_t *)(ldsi + STAGE_OFF) + (w ^ N_DMA_WAVES) * 256 + lane;
-            uint32_t pv[4];
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) pv[tt] = pstage[tt * 64];
-            flush_fs(pv, base, 0, w ^ N_DMA_WAVES, dma_wave);
-        }
         l3_epilogue(std::integral_constant<int, 1>{});
         flush_fs(pf1, base, 1, w);
-#ifdef SGN_TIMING
-        tmark(ldsi, w, lane);  // block3.2 pass-1 epilogue done
-#endif
         // alpha: reduce the 16 row partials over the 32 lanes (units) of each half,
         // reduce-scatter style; lane j ends with row index i = 8 b1 + 4 b2 + 2 b3 + b4 (b = bits of j)
         float bq[8];
@@ -722,9 +542,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         const float alpha_s = dpp_sum8(ri.wgt * alpha_row);
         if (ri.sval && kk == 0 && h == 0) a.feat[(int64_t)ri.s * 4 + 0] = alpha_s;
     }
-    if (LAG && w < N_DMA_WAVES)
-        for (int i = 0; i < LAG; ++i) __builtin_amdgcn_s_barrier();  // match the followers' late start
-    // the stream ran DIST chunks ahead: let those LDS-DMAs land before the workgroup retires
+    // the stream ran one chunk ahead: let those LDS-DMAs land before the workgroup retires
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 struct ColorArgs {
@@ -1174,33 +992,12 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
         dim3 g1((unsigned)(wg < 256 ? wg : 256));
         if (stages & 1) {
             constexpr int SP = 256;  // split block1.0 (per-point projection given)
-#if SGN_LAG || defined(SGN_KB16)  // timing builds with a bigger ring: the SG BPNet LDS staging does not fit
-            constexpr int KB = KS_HID;
-#else
             constexpr int KB = ks_bp(BP_DIM);
-#endif
             auto kern = d_point_proj ? (ksb == 0 ? k_agg_rows<SP> : ksb == KS_HID ? k_agg_rows<KS_HID + SP>
                                                                                 : k_agg_rows<KB + SP>)
                                      : (ksb == 0 ? k_agg_rows<0> : ksb == KS_HID ? k_agg_rows<KS_HID>
                                                                                 : k_agg_rows<KB>);
-#ifdef SGN_TIMING
-            static unsigned long long *tbuf = nullptr;
-            const size_t tn = (size_t)TDBG_BLOCKS * 8 * TDBG_EV;
-            if (!tbuf) {
-                SGN_CHECK_HIP(hipMalloc(&tbuf, tn * 8));
-                SGN_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tdbg), &tbuf, sizeof(tbuf)));
-            }
-            SGN_CHECK_HIP(hipMemsetAsync(tbuf, 0, tn * 8, st));
-#endif
             hipLaunchKernelGGL(kern, g1, dim3(ROWS_TPB), 0, st, a);
-#ifdef SGN_TIMING
-            if (const char *path = getenv("SGN_TDBG")) {
-                std::vector<unsigned long long> h(tn);
-                SGN_CHECK_HIP(hipMemcpyAsync(h.data(), tbuf, tn * 8, hipMemcpyDeviceToHost, st));
-                SGN_CHECK_HIP(hipStreamSynchronize(st));
-                if (FILE *f = fopen(path, "wb")) { fwrite(h.data(), 8, tn, f); fclose(f); }
-            }
-#endif
         }
         int64_t wg2 = (n + 32 * (COL_TPB / 64) - 1) / (32 * (COL_TPB / 64));  // 32 samples per wave
         dim3 g2((unsigned)(wg2 < 256 ? wg2 : 256));  // persistent: colour weights loaded once per CU

@@ -46,16 +46,7 @@ constexpr int PAIR = 2048;        // hi fragment (1 KiB) then lo fragment (1 KiB
 constexpr int SLOT_PAIRS = 32;
 constexpr int SLOT = SLOT_PAIRS * PAIR;  // 64 KiB
 constexpr int NSLOT = 2;
-#ifndef SGN_X3_PD
-#define SGN_X3_PD 2
-#endif
-#ifndef SGN_X3_PIN
-#define SGN_X3_PIN 1
-#endif
-#ifndef SGN_X3_SPREAD_DIV
-#define SGN_X3_SPREAD_DIV 2  // DMA pieces spread over the first NF / DIV pairs of a chunk
-#endif
-constexpr int PD = SGN_X3_PD;     // fragment pairs in flight per wave (LDS -> VGPR queue)
+constexpr int PD = 2;     // fragment pairs in flight per wave (LDS -> VGPR queue)
 constexpr size_t PROJ_BYTES_PER_POINT = HID * 4;  // P row: fp32 [256], natural unit order
 struct XL {
     int ks, tp, np, kc;
@@ -83,15 +74,11 @@ struct X3B {
     h8 hi, lo;
 };
 
-#ifndef SGN_X3_MIX
-#define SGN_X3_MIX 1  // x - fp32(hi) as one v_fma_mix_f32 reading the packed fp16 hi
-#endif
 // x -> (hi, lo): hi = fp16(x), lo = fp16(x - hi) (the difference is exact in fp32)
 __device__ __forceinline__ X3B split8(const float (&v)[8]) {
     X3B r;
     r.hi = pack8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
     float d[8];
-#if SGN_X3_MIX
     const u32x4 hp = __builtin_bit_cast(u32x4, r.hi);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -100,96 +87,36 @@ __device__ __forceinline__ X3B split8(const float (&v)[8]) {
         asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
             : "=v"(d[2 * q + 1]) : "v"(hp[q]), "v"(v[2 * q + 1]));
     }
-#else
-#pragma unroll
-    for (int e = 0; e < 8; ++e) d[e] = v[e] - (float)r.hi[e];
-#endif
     r.lo = pack8(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
     return r;
 }
 
-// t -> (hi, lo) of x = t * inv (inv a power of two, so x is exact): hi = fp16(x), lo = fp16(x - hi), each
-// half written by one v_fma_mix{lo,hi}_f16 (fp32 FMA, rounded once to fp16): 4 instructions per 2
-// values instead of a multiply each, a pack and the two fma_mix + pack of split8 -- the same bits
-[[maybe_unused]] __device__ __forceinline__ X3B split8s(const float (&t)[8], float inv) {
-    u32x4 hi, lo;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t h, l;
-        asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(t[2 * q]), "v"(inv));
-        asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(t[2 * q + 1]), "v"(inv));
-        asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(t[2 * q]), "v"(inv), "v"(h));
-        asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-            : "+v"(l) : "v"(t[2 * q + 1]), "v"(inv), "v"(h));
-        hi[q] = h;
-        lo[q] = l;
-    }
-    return X3B{__builtin_bit_cast(h8, hi), __builtin_bit_cast(h8, lo)};
-}
 // LeakyReLU(0.01) exactly as the reference (x, or fp32(0.01 x) below zero): max(x, 0.01 x) as one
 // v_max_f32 in inline asm -- fmaxf on an MFMA result makes the compiler canonicalise the operand with
 // an extra v_max_f32 x, x, x first (IEEE mode); NaN / inf still propagate (the fp16-range guard)
-#ifndef SGN_X3_LRELU_ASM
-#define SGN_X3_LRELU_ASM 1
-#endif
 __device__ __forceinline__ float lrelu_x3(float a) {
-#if SGN_X3_LRELU_ASM
     float r;
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(0.01f * a));
     return r;
-#else
-    return fmaxf(a, 0.01f * a);
-#endif
 }
-#ifndef SGN_X3_MIXCHAIN
-#define SGN_X3_MIXCHAIN 0
-#endif
-// LeakyReLU(2^-s a) as the next layer's (hi, lo) fragment: LeakyReLU commutes with the exact
-// power-of-two scaling, so the scale rides in the fp16 conversion (split8s)
+// LeakyReLU(2^-s a) as the next layer's (hi, lo) fragment (LeakyReLU commutes with the exact
+// power-of-two scaling)
 __device__ __forceinline__ X3B lrelu_split8(const float (&a)[8], float inv) {
     float v[8];
-#if SGN_X3_MIXCHAIN
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = lrelu_x3(a[j]);
-    return split8s(v, inv);
-#else
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const float y = a[j] * inv;
         v[j] = fmaxf(y, 0.01f * y);
     }
     return split8(v);
-#endif
 }
-
-// Timing build (SGN_X3_TIMING): wave w of the first TD_BLOCKS workgroups stamps the clock at the
-// kernel's phase points into tdbg[(block * NW16 + w) * TD_EV + seq] (tools/x3_timing16.py reads it).
-[[maybe_unused]] constexpr int TD_BLOCKS = 8, TD_EV = 2048;
-struct TStamp {
-    unsigned long long *buf;
-    int seq;
-    __device__ __forceinline__ void operator()(int lane) {
-#ifdef SGN_X3_TIMING
-        if (buf && lane == 0 && seq < TD_EV - 4) buf[seq] = clock64();
-        ++seq;
-#else
-        (void)lane;
-#endif
-    }
-};
 
 // one 1-KiB LDS-DMA piece of wave w: 16 B per lane from blob byte offset soff + w * 1024 + lane * 16 into
 // LDS dst + w * 1024 (+ lane * 16).  The constant part of the offset is made opaque at its use, so the
 // compiler materialises it right there (one s_mov) instead of hoisting ~70 per-tile offsets into
 // SGPRs that then spill into VGPR lanes.
 __device__ __forceinline__ void lds_dma_1k(const WBlob &wb, char *dst, int w, int lane, uint32_t soff) {
-#ifdef SGN_X3_ABLATE_DMA  // timing experiment only: no weight stream (wrong results)
-    return;
-#endif
-#ifndef SGN_X3_DMAOPQ
-#define SGN_X3_DMAOPQ 1
-#endif
-    if (SGN_X3_DMAOPQ) asm volatile("" : "+s"(soff));
+    asm volatile("" : "+s"(soff));
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)(dst + w * 1024), 16,
                                              lane * 16 + w * 1024, soff, 0, 0);
 }
@@ -220,59 +147,9 @@ __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int
 template <class Net, int N, int NWv = NW16>
 constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NWv - 1) / NWv; }
 
-// ---- counted weight ring (SGN_X3_RING, the row kernel): 4 slots, no workgroup barrier ------------
-// Chunk n of the stream (n counts across tiles) lives in slot n % 4; its pieces are issued during chunk
-// n - 2 (two ahead).  Per slot two LDS counters: FULL (+1 per wave once its pieces of the slot's
-// current chunk have landed, signalled at that wave's entry of the chunk before) and FREE (+1 per
-// wave once it has read the slot's chunk).  Entering chunk n waits for FULL = NW (u + 1) (u = n / 4,
-// the slot's fill count) and, before the chunk's pieces of n + 2 go into slot (n + 2) % 4, for that
-// slot's previous chunk n - 2 to be FREE on every wave -- so the waves of a workgroup may drift apart
-// by one chunk instead of meeting at every boundary.  Every wait is bounded (a wave that has spun
-// 2^14 times moves on and sets the error word, so a protocol bug can only produce wrong results,
-// never a hang).
-struct RingState {
-    int slot;          // slot of the chunk being entered
-    uint32_t n;        // its stream position
-    uint32_t *cnt;     // LDS: FULL[4] then FREE[4]
-};
-constexpr int RING_SLOTS = 4;
 __device__ __forceinline__ int cur_slot(int s) { return s; }
-[[maybe_unused]] __device__ __forceinline__ int cur_slot(const RingState &r) { return r.slot; }
 __device__ __forceinline__ int dma_slot(int s) { return s ^ 1; }
-[[maybe_unused]] __device__ __forceinline__ int dma_slot(const RingState &r) { return (r.slot + 2) & (RING_SLOTS - 1); }
-template <class T>
-struct RingAhead {
-    static constexpr int value = 1;  // chunks the DMA runs ahead of the reads
-};
-template <>
-struct RingAhead<RingState> {
-    [[maybe_unused]] static constexpr int value = 2;
-};
-[[maybe_unused]] __device__ __forceinline__ void ring_wait(uint32_t *c, uint32_t target, uint32_t *err) {
-#ifdef SGN_X3_ABLATE_RINGWAIT  // timing experiment only: the counters are read but never waited on
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0xFFFFFFFFu &&
-        err)
-        *err = target;
-    return;
-#endif
-    for (int it = 0; it < (1 << 14); ++it) {
-        const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (v >= target) return;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    if (err) *err = 1u;
-}
-[[maybe_unused]] __device__ __forceinline__ void ring_add(uint32_t *c, int lane) {
-    if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 __device__ __forceinline__ void chunk_exit(int &s, int) { s ^= 1; }
-template <int NWv>
-__device__ __forceinline__ void chunk_exit_ring(RingState &r, int lane) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
-    ring_add(r.cnt + RING_SLOTS + r.slot, lane);
-    r.slot = (r.slot + 1) & (RING_SLOTS - 1);
-    ++r.n;
-}
 
 // chunk boundary: this wave's DMAs of chunk N landed, LDS reads drained, barrier; then chunk N+1
 // goes into the slot every wave finished reading one chunk ago (its pieces are spread over the
@@ -280,30 +157,8 @@ __device__ __forceinline__ void chunk_exit_ring(RingState &r, int lane) {
 // VM: vector-memory operations this wave is guaranteed to have issued after its last DMA piece of
 // the chunk being entered (loads placed at the end of the previous chunk, stores): they may stay in
 // flight across the boundary (vmcnt retires in order, so the DMA has landed once at most VM remain)
-// counted ring: this wave's pieces of chunk n + 1 (issued during n - 1) landed -> FULL of its slot;
-// wait for chunk n FULL on every wave and for slot (n + 2) % 4 (chunk n - 2) FREE on every wave
 template <class Net, int N, int NWv = NW16, int VM = 0>
-__device__ __forceinline__ void chunk_enter(const WBlob &, char *, RingState &r, int, int lane, int,
-                                            TStamp *ts = nullptr) {
-    static_assert(VM >= 0 && VM < 64, "vmcnt range");
-    if constexpr (VM == 0)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else
-        __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
-    ring_add(r.cnt + ((r.slot + 1) & (RING_SLOTS - 1)), lane);
-    uint32_t *err = r.cnt + 2 * RING_SLOTS;
-    ring_wait(r.cnt + r.slot, (uint32_t)NWv * (r.n / RING_SLOTS + 1), err);
-    if (r.n >= 2) ring_wait(r.cnt + RING_SLOTS + ((r.slot + 2) & (RING_SLOTS - 1)), (uint32_t)NWv * ((r.n - 2) / RING_SLOTS + 1), err);
-#ifdef SGN_X3_TIMING
-    if (ts) (*ts)(lane);
-#else
-    (void)ts;
-#endif
-}
-template <class Net, int N, int NWv = NW16, int VM = 0>
-__device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot, int w, int lane, int lz,
-                                            TStamp *ts = nullptr) {
-#ifndef SGN_X3_ABLATE_BARRIER  // timing experiment only: no boundary waits / barrier (wrong results)
+__device__ __forceinline__ void chunk_enter(const WBlob &, char *, int, int, int, int) {
     static_assert(VM >= 0 && VM < 64, "vmcnt range");
     if constexpr (VM == 0)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -311,12 +166,6 @@ __device__ __forceinline__ void chunk_enter(const WBlob &wb, char *lds, int slot
         __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-#endif
-#ifdef SGN_X3_TIMING
-    if (ts) (*ts)(lane);
-#else
-    (void)ts;
-#endif
 }
 
 struct NoHook {
@@ -389,27 +238,17 @@ constexpr size_t BLOB_BYTES_ALL = OFF16_F32 + (size_t)N_Y32 * 4;
 __host__ __device__ constexpr size_t blob_bytes_sg(int) { return BLOB_BYTES_ALL; }
 static_assert(N_Y32 % 4 == 0, "fp32 section in 16-B units");
 
-// block3.2 in two passes of 8 output tiles (SGN_X3_SPLIT3): pass 0 converts the input once and keeps it
+// block3.2 in two passes of 8 output tiles: pass 0 converts the input once and keeps it
 // as (hi, lo) fragments, and the epilogue (K-blend, alpha) of its 8 tiles runs between pass 1's MFMAs
-#ifndef SGN_X3_SPLIT3
-#define SGN_X3_SPLIT3 1
-#endif
-// Row kernel workgroup (SGN_X3_RW waves): 4 waves (one per SIMD) with a 2 x 32-KiB ring, so two
+// Row kernel workgroup (4 waves): 4 waves (one per SIMD) with a 2 x 32-KiB ring, so two
 // workgroups share a CU and their waves pair up on each SIMD without a common barrier (the barrier
 // of one chunk boundary no longer holds the other workgroup's wave of the SIMD: while one runs its
-// tile transition or epilogue VALU, the other's MFMAs keep the matrix pipe busy); or 8 waves with a
-// 2 x 64-KiB ring (one workgroup per CU, every wave in step)
-#ifndef SGN_X3_RING
-#define SGN_X3_RING 0   // 1: 8 waves sharing a counted 4-slot ring of 16-pair chunks (RingState), no barrier
-#endif
-#ifndef SGN_X3_RW
-#define SGN_X3_RW (SGN_X3_RING ? 8 : 4)
-#endif
-constexpr int NWR = SGN_X3_RW, SPR = (NWR == 4 || SGN_X3_RING) ? 16 : 32;  // row waves, ring slot pairs
-constexpr int NSLR = SGN_X3_RING ? RING_SLOTS : NSLOT;                    // row ring slots
+// tile transition or epilogue VALU, the other's MFMAs keep the matrix pipe busy)
+constexpr int NWR = 4, SPR = NWR == 4 ? 16 : 32;  // row waves, ring slot pairs
+constexpr int NSLR = NSLOT;                       // row ring slots
 static_assert(NWR == 4 || NWR == 8, "row workgroup: 4 or 8 waves");
 constexpr int KCR = SPR / 16;                             // k-steps of 16 tiles per chunk
-constexpr XL L3_16 = SGN_X3_SPLIT3 ? XL{8, 8, 2, 2 * KCR, OFF16_W3} : XL{8, 16, 1, KCR, OFF16_W3};
+constexpr XL L3_16 = XL{8, 8, 2, 2 * KCR, OFF16_W3};
 struct NetR16 {
     static constexpr int NW = NWR, SP = SPR;  // waves sharing the ring, fragment pairs per ring slot
     static constexpr int NL = 4;
@@ -428,11 +267,8 @@ struct NetProj16 {
     static constexpr int NL = 1;
     static constexpr XL L[NL] = {{7, 16, 1, 2, OFF16_W0A}};
 };
-// colour kernel workgroup (SGN_X3_CW waves), as the row kernel's
-#ifndef SGN_X3_CW
-#define SGN_X3_CW 8
-#endif
-constexpr int NWC = SGN_X3_CW, SPC = NWC == 4 ? 16 : 32, KCC = SPC / 8;
+// colour kernel workgroup (8 waves), as the row kernel's
+constexpr int NWC = 8, SPC = NWC == 4 ? 16 : 32, KCC = SPC / 8;
 static_assert(NWC == 4 || NWC == 8, "colour workgroup: 4 or 8 waves");
 struct NetColor16 {
     static constexpr int NW = NWC, SP = SPC;
@@ -457,16 +293,16 @@ template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, cl
           class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>
 __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &slot, int w, int lane, int lz,
                                             f32x4 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{},
-                                            TStamp *ts = nullptr, EndFn &&end = EndFn{}, MidFn &&mid = MidFn{}) {
+                                            EndFn &&end = EndFn{}, MidFn &&mid = MidFn{}) {
     constexpr XL ly = Net::L[L];
     constexpr int TP = ly.tp;
     static_assert((TP == 16 || TP == 8) && P < ly.np, "passes of 16 or 8 output tiles");
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
-        constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + RingAhead<SlotT>::value) % Sched<Net>::total();
+        constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
         constexpr int NWv = Net::NW, SLOTv = Net::SP * PAIR;
         static_assert(nk(ly, C) * TP <= Net::SP, "chunk larger than a ring slot");
-        chunk_enter<Net, N, NWv, Vm::vm(C)>(wb, lds, slot, w, lane, lz, ts);
+        chunk_enter<Net, N, NWv, Vm::vm(C)>(wb, lds, slot, w, lane, lz);
         post(cc);
         const char *sl = lds + cur_slot(slot) * SLOTv;
         char *dnext = lds + dma_slot(slot) * SLOTv;
@@ -479,9 +315,7 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &s
             fh[f] = frag(f, 0);
             fl[f] = frag(f, 1);
         }
-#if SGN_X3_PIN
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
-#endif
         static_for<nk(ly, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
             const X3B B = in(std::integral_constant<int, C * ly.kc + KK>{});
@@ -494,43 +328,30 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &s
                 }
                 if constexpr (TRANS) {
                     acc[t] = mfma16(B.hi, Ah, acc[t]);
-#ifndef SGN_X3_ABLATE_MFMA3
                     acc[t] = mfma16(B.lo, Ah, acc[t]);
                     acc[t] = mfma16(B.hi, Al, acc[t]);
-#else
-                    asm volatile("" :: "v"(Al));
-#endif
                 } else {
                     acc[t] = mfma16(Ah, B.hi, acc[t]);
-#ifndef SGN_X3_ABLATE_MFMA3  // timing experiment only: one product instead of three (wrong results)
                     acc[t] = mfma16(Ah, B.lo, acc[t]);
                     acc[t] = mfma16(Al, B.hi, acc[t]);
-#else
-                    asm volatile("" :: "v"(Al));
-#endif
                 }
-                constexpr int NS = NF / SGN_X3_SPREAD_DIV > 0 ? NF / SGN_X3_SPREAD_DIV : 1;
+                constexpr int NS = NF / 2 > 0 ? NF / 2 : 1;
                 if constexpr (F < NS) {
                     static_for<(F + 1) * PW / NS - F * PW / NS>([&](auto jj) {
                         dma_piece<Net, NN, F * PW / NS + decltype(jj)::value, NWv>(wb, dnext, w, lane, lz);
                     });
                 }
                 mid(std::integral_constant<int, (C * ly.kc + KK) * TP + t>{});
-#if SGN_X3_PIN
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-#endif
             });
         });
         __builtin_amdgcn_sched_barrier(0);
         end(cc);  // after every DMA piece of the chunk: loads here may stay in flight one boundary
-        if constexpr (RingAhead<SlotT>::value == 2)
-            chunk_exit_ring<NWv>(slot, lane);
-        else
-            chunk_exit(slot, lane);
+        chunk_exit(slot, lane);
         __builtin_amdgcn_sched_barrier(0);
     });
 }
@@ -642,8 +463,7 @@ constexpr int WG16_SAMPLES = NWR * 2;            // halves (16 rows, 2 per wave)
 constexpr int TPBR = NWR * 64;
 constexpr int YR_OFF = NSLR * SPR * PAIR;         // the row kernel's fp32 section, after its ring
 constexpr int YT16_OFF = YR_OFF + N_Y32 * 4;      // [unit r][20] 2^s3 b3 (t = 0..15) then [r][20] 2^-s3 alpha w
-constexpr int RINGCNT_OFF = YT16_OFF + 2 * 16 * 20 * 4;  // counted ring: FULL[4], FREE[4], error word
-constexpr int ROWS16_LDS = RINGCNT_OFF + (SGN_X3_RING ? 64 : 0);
+constexpr int ROWS16_LDS = YT16_OFF + 2 * 16 * 20 * 4;
 static_assert(ROWS16_LDS * (8 / NWR) <= 163840, "LDS budget (16x16 rows, 8 / NWR workgroups per CU)");
 
 // row r's point record, its sample position and view direction (+ the caller's pers
@@ -942,12 +762,6 @@ __device__ __forceinline__ X3B pe_dists16_k(const PeRow &r) {
 }
 
 // block3.2 epilogue of a tile (K-blend -> f_s, alpha), per lane: rows 4 g + i of half g >> 1
-#ifndef SGN_X3_B3FOLD
-#define SGN_X3_B3FOLD 0  // block3.2's bias in its accumulator init, 2^-s3 folded into the blend / alpha weights
-#endif
-#ifndef SGN_X3_STORE1
-#define SGN_X3_STORE1 0  // 1: each f_s value stored as it is blended (else per 4 under one branch)
-#endif
 struct Epi16 {
     float wsa[4], wsb[4];   // the rows' blend weights split by segment (A: positions < nA, B: the rest),
                             // times 2^-s3 (block3.2's accumulators hold 2^s3 (W x + b))
@@ -958,23 +772,12 @@ struct Epi16 {
     float inv3;
 };
 
-// a workgroup's tiles under the XCD-aware order: tiles first, first + step, ... < end
-struct XcdTiles {
+// a workgroup's tiles: first, first + step, ... < end (grid-stride; an XCD-contiguous order measured
+// within +-1 %)
+struct Tiles {
     int first, end, step;
 };
-__device__ __forceinline__ XcdTiles xcd_tiles(int ntiles) {
-#ifndef SGN_X3_XCD
-#define SGN_X3_XCD 0
-#endif
-    const int nx = SGN_X3_XCD && gridDim.x % 8 == 0 ? 8 : 1;  // only when the grid covers the XCDs evenly
-    const int per = gridDim.x / nx, x = blockIdx.x % nx, j = blockIdx.x / nx;
-    const int len = (ntiles + nx - 1) / nx, r0 = x * len;
-    XcdTiles t;
-    t.first = r0 + j;
-    t.end = min(ntiles, r0 + len);
-    t.step = per;
-    return t;
-}
+__device__ __forceinline__ Tiles grid_tiles(int ntiles) { return Tiles{(int)blockIdx.x, ntiles, (int)gridDim.x}; }
 
 // KB: k-steps of block2_bpnet.0 in 16x16 steps (0: base viewmlp; 8: bpnet_dim 0; 11: dim 96)
 // SAVE (base viewmlp, training): the pre-activations of block1.0 / 1.2 / 3.0 go to a.z1 / z2 / z3 as
@@ -996,7 +799,6 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         const float *src = (const float *)((const char *)a.blob + OFF16_F32);
         float *dst = (float *)(lds + YR_OFF);
         for (int i = threadIdx.x; i < N_Y32; i += TPBR) dst[i] = src[i];
-        if (SGN_X3_RING && threadIdx.x < 16) ((uint32_t *)(lds + RINGCNT_OFF))[threadIdx.x] = 0u;
         {
             // row stride 20 floats: the 16 lanes' 16-B reads of one column quad hit disjoint banks
             float *yt = (float *)(lds + YT16_OFF);
@@ -1007,24 +809,12 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         }
     }
     __syncthreads();
-#if SGN_X3_RING
-    RingState slot{0, 0u, (uint32_t *)(lds + RINGCNT_OFF)};
-    dma_chunk<Net, 0, NWR>(wb, lds, w, lane, 0);
-    dma_chunk<Net, 1, NWR>(wb, lds + SPR * PAIR, w, lane, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ring_add(slot.cnt + 0, lane);  // chunk 0 landed (chunk 1 is signalled at chunk 0's entry)
-#else
     int slot = 0;
     dma_chunk<Net, 0, NWR>(wb, lds, w, lane, 0);
-#endif
     // The next tile's chain, prefetched inside the current tile so each step lands under MFMAs:
     // row-table entry (block1.2), neighbour / ray index (block3.0), point record + sample position
     // and the P row (block3.2).  First tile: here.
-    // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one),
-    // so XCD x = b % 8 walks its own contiguous eighth of the tiles.  Neighbouring tiles hold samples of
-    // neighbouring rays, which gather largely the same points: their P rows and records then meet in
-    // that XCD's L2 instead of being fetched from HBM by all eight.
-    const XcdTiles xt = xcd_tiles((nslots + WG16_SAMPLES - 1) / WG16_SAMPLES);
+    const Tiles xt = grid_tiles((nslots + WG16_SAMPLES - 1) / WG16_SAMPLES);
     RowIdx nx = row_index16(a, xt.first * WG16_SAMPLES + w * 2 + sc, nslots, kk);
     Rec16<PERS> rnext = load_rec16<PERS>(a, nx);
     // P row of point pid into `dst`: natural unit order, tile t of lane group g at 16 t + 4 g, so the
@@ -1039,20 +829,6 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
     // block3.2 epilogue and the tile transition without extra registers
     f32x4 accA[16], accB[16];
     load_p(nx.pid, pick<(KB > 0)>(accB, accA));  // SG: where the tile loop copies it from
-#ifdef SGN_X3_TIMING
-    TStamp tsv{blockIdx.x < TD_BLOCKS && a.tdbg ? a.tdbg + ((int64_t)blockIdx.x * NWR + w) * TD_EV : nullptr, 0};
-    TStamp *ts = &tsv;
-    // in-kernel clock (MI355X_MICROARCH.md 'DVFS give-back' item 6): s_memtime and s_memrealtime
-    // (100 MHz) around the tile loop, in the last four words of the wave's stamp area
-    if (tsv.buf && lane == 0) {
-        tsv.buf[TD_EV - 4] = __builtin_amdgcn_s_memtime();
-        tsv.buf[TD_EV - 3] = __builtin_amdgcn_s_memrealtime();
-    }
-#define X3T() tsv(lane)
-#else
-    TStamp *ts = nullptr;
-#define X3T()
-#endif
 
     // epilogue pieces (LDS reads through the tile's opaque base)
     auto epi_begin = [&](Epi16 &e, const char *ldsi, float wgt, int nA, int nB, int2 ce, bool ok) {
@@ -1061,7 +837,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         for (int i = 0; i < 4; ++i) {
             const float wi = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute((4 * g + i) * 4, __builtin_bit_cast(int, wgt)));
             const bool inA = 4 * (g & 1) + i < nA;
-            const float ws = SGN_X3_B3FOLD ? wi * inv3 : wi;
+            const float ws = wi;
             e.wsa[i] = inA ? ws : 0.f;
             e.wsb[i] = inA ? 0.f : ws;
             e.ap[i] = 0.f;
@@ -1077,9 +853,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         float fa = 0.f, fb = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const float hv = SGN_X3_B3FOLD ? lrelu_x3(ac[T][i])
-                                           : lrelu_x3(__builtin_fmaf(ac[T][i], e.inv3,
-                                                                     ((const float *)(ldsi + YT16_OFF))[r * 20 + T]));
+            const float hv = lrelu_x3(__builtin_fmaf(ac[T][i], e.inv3, ((const float *)(ldsi + YT16_OFF))[r * 20 + T]));
             e.ap[i] = __builtin_fmaf(wau, hv, e.ap[i]);
             fa = __builtin_fmaf(e.wsa[i], hv, fa);
             fb = __builtin_fmaf(e.wsb[i], hv, fb);
@@ -1090,9 +864,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         // unchanged, the other group's chain is 0)
         permlane16_swap(fa, fb);
         e.fsv[T & 3] = fa + fb;
-        if constexpr (SGN_X3_STORE1) {
-            if (e.fs_have) e.fs_dst[16 * T] = e.fsv[T & 3];
-        } else if constexpr ((T & 3) == 3) {  // 16 lanes write 64 contiguous bytes of the work item's row, per 4
+        if constexpr ((T & 3) == 3) {  // 16 lanes write 64 contiguous bytes of the work item's row, per 4
             if (e.fs_have) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) e.fs_dst[16 * (T - 3 + u)] = e.fsv[u];
@@ -1103,7 +875,6 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         // alpha: row logits summed over the 16 lanes (units) of the group, softplus(x + b - 1), blended
         // over the segment's rows like f_s
         const float ba = ((const float *)(ldsi + YR_OFF))[Y_BA];
-        const float sc3 = SGN_X3_B3FOLD ? 1.f / e.inv3 : 1.f;  // 2^s3, exact
         float xr[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1123,9 +894,9 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
                               __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(spi, 0xFF, 0xF, 0xF, true))};
         float asa = 0.f, asb = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {  // the rows' weights: 2^s3 (2^-s3 w), exact
-            asa = __builtin_fmaf(e.wsa[i] * sc3, sp4[i], asa);
-            asb = __builtin_fmaf(e.wsb[i] * sc3, sp4[i], asb);
+        for (int i = 0; i < 4; ++i) {  // the rows' weights
+            asa = __builtin_fmaf(e.wsa[i], sp4[i], asa);
+            asb = __builtin_fmaf(e.wsb[i], sp4[i], asb);
         }
         permlane16_swap(asa, asb);
         const float as = asa + asb;  // even groups: A's alpha, odd groups: B's
@@ -1142,7 +913,6 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         const float *Yl = (const float *)(ldsi + YR_OFF);
         const int hslot = base + w * 2 + sc;  // this lane's half (the LDS ring slot is `slot`)
         const int nslot = tile + xt.step < xt.end ? hslot + xt.step * WG16_SAMPLES : nslots;  // next tile's half
-        X3T();  // tile start
         const RowIdx ix = nx;
         const bool m = ix.pid >= 0;
         const Rec16<PERS> rc = rnext;
@@ -1199,14 +969,13 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         };
         {   // block1.0: W0b PE(dists) on MFMA, + P[pid] (W0a [feat | PE(feat)] + b0, k_point_proj16)
             const PeRow pr = pe_row16(rw.d, g);
-            X3T();  // gather (PE inside block1.0's k-loop)
             if constexpr (KB > 0) {  // SG: five layers, the P array alternates -- copy it back
 #pragma unroll
                 for (int t = 0; t < 16; ++t) accA[t] = accB[t];
             }
             run_layer16<Net, 0, false, VmL0>(wb, ldsi, slot, w, lane, lz, accA,
                                              [&](auto k) { return pe_dists16_k<decltype(k)::value>(pr); },
-                                             NoHook{}, ts);
+                                             NoHook{});
         }
         // block1.2: 256 -> 256 (input: block1.0 accumulators)
         const float inv0 = Yl[Y_INV + 0], inv1 = Yl[Y_INV + 1], inv2 = Yl[Y_INV + 2], inv7 = Yl[Y_INV + 7];
@@ -1216,7 +985,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
                             [&](auto c) {
                                 if constexpr (decltype(c)::value == 0)
                                     v_next = nslot < nslots ? a.rows[(int64_t)nslot * 8 + kk] : -1;
-                            }, ts);
+                            });
         if constexpr (KB > 0) {
             // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256; the row's fp32 embedding
             // (channels 32 m + 8 g .. +7 for k-step 8 + m) gathered and split here
@@ -1234,7 +1003,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
             run_layer16<Net, LB>(wb, ldsi, slot, w, lane, lz, accA, [&](auto k) {
                 constexpr int K = decltype(k)::value;
                 if constexpr (K < 8) return chain_k(accB, inv1, k); else return bpv[K - 8];
-            }, NoHook{}, ts);
+            }, NoHook{});
         }
         // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input: block1.2 or block2_bpnet)
         auto &in2 = pick<(KB > 0)>(accA, accB);
@@ -1253,18 +1022,11 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
                 nx.pid = nx.sval ? a.pidx[pidx_of(a, v_next)] : -1;
                 nx.ray = nx.sval ? a.samp_ray[nx.s] : 0;
             }
-        }, ts);
+        });
         // block3.2: 256 -> 256 transposed: acc[t][i] = h[row 4 g + i][unit 16 t + (l & 15)]
         auto &acc = in2;  // block3.0's input is dead: its registers take block3.2's accumulators
-        {   // start at the bias (2^s3 b3[16 t + r], the transposed LDS copy: 4 x 16 B per lane)
-            const float *ytb = (const float *)(ldsi + YT16_OFF) + r * 20;
 #pragma unroll
-            for (int t4 = 0; t4 < 4; ++t4) {
-                const f32x4 b = *(const f32x4 *)(ytb + 4 * t4);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) acc[4 * t4 + u] = SGN_X3_B3FOLD ? f32x4{b[u], b[u], b[u], b[u]} : f32x4{};
-            }
-        }
+        for (int t = 0; t < 16; ++t) acc[t] = f32x4{};  // the bias joins in the epilogue (epi_step)
         // the next tile's record (and this tile's slot entry for the epilogue: half g >> 1's
         // {A item | nA << 28, B item | nB << 28, ..}) go out at the end of block3.2's first chunk, after
         // the chunk's DMA pieces, so they stay in flight across one boundary (VmL3)
@@ -1279,7 +1041,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
             }
         };
         Epi16 e;
-        if constexpr (SGN_X3_SPLIT3) {
+        {
             // pass 0 (output tiles 0..7) converts block3.0's output once into (hi, lo) fragments (in the
             // registers it frees) and pass 1 (tiles 8..15) reuses them; pass 1 carries the epilogue of
             // pass 0's tiles, output tile T after k-step T (one per 8 MFMA pairs)
@@ -1290,22 +1052,16 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
                 constexpr int K = decltype(k)::value;
                 in3[K] = chain_k(acc2, inv2, k, a.z3);
                 return in3[K];
-            }, NoHook{}, ts, first_chunk_loads);
+            }, NoHook{}, first_chunk_loads);
             epi_begin(e, ldsi, rw.wgt, nA, nB, ce, eslot < nslots);
             run_layer16<Net, L3, true, VmZero, 1>(wb, ldsi, slot, w, lane, lz, acc1,
-                                                  [&](auto k) { return in3[decltype(k)::value]; }, NoHook{}, ts,
+                                                  [&](auto k) { return in3[decltype(k)::value]; }, NoHook{},
                                                   NoHook{}, [&](auto f) {
                                                       constexpr int F = decltype(f)::value;
                                                       if constexpr ((F & 7) == 7)
                                                           epi_step(e, ldsi, acc, std::integral_constant<int, F / 8>{});
                                                   });
-        } else {
-            run_layer16<Net, L3, true, VmL3P0>(wb, ldsi, slot, w, lane, lz, acc,
-                                               [&](auto k) { return chain_k(acc2, inv2, k, a.z3); }, NoHook{}, ts,
-                                               first_chunk_loads);
-            epi_begin(e, ldsi, rw.wgt, nA, nB, ce, eslot < nslots);
         }
-        X3T();  // block3.2 MFMAs issued
         // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads
         // from the compiler's wait tracking, which would otherwise wait for the epilogue's stores
         asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
@@ -1318,25 +1074,16 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         {   // the rest of the epilogue; the next tile's P rows (see accA) go out first, into block3.2's
             // consumed input registers, and land under it
             const float *psrc = proj + (int64_t)(nx.pid < 0 ? 0 : nx.pid) * HID + 4 * g;
-            constexpr int NE = SGN_X3_SPLIT3 ? 8 : 16, PPE = 16 / NE;  // epilogue steps left, P loads per step
+            constexpr int NE = 8, PPE = 16 / NE;  // epilogue steps left, P loads per step
             static_for<NE>([&](auto tc) {  // the loads spread between the steps (a burst stalls the issue)
                 constexpr int J = decltype(tc)::value;
 #pragma unroll
                 for (int u = 0; u < PPE; ++u) acc2[PPE * J + u] = *(const f32x4 *)(psrc + 16 * (PPE * J + u));
                 epi_step(e, ldsi, acc, std::integral_constant<int, (16 - NE) + J>{});
             });
-            X3T();  // block3.2 epilogue (K-blend, alpha partials)
             epi_end(e, ldsi, nA, nB, ix.s);
         }
-        X3T();  // tile end
     }
-#ifdef SGN_X3_TIMING
-    if (tsv.buf && lane == 0) {
-        tsv.buf[TD_EV - 2] = __builtin_amdgcn_s_memtime();
-        tsv.buf[TD_EV - 1] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-#undef X3T
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -1404,9 +1151,8 @@ void layout_blob16(int ksb, int bpnet_dim, Pairs &&pairs, F32 &&f32) {
         f32(Y_B0 + u, YK_BS, 0, u);
         f32(Y_B1 + u, YK_BS, 1, u);
         f32(Y_B2 + u, YK_BS, 2, u);
-        // block3.2's accumulator init and the alpha weights on 2^s3-scaled activations (SGN_X3_B3FOLD)
-        f32(Y_B3 + u, SGN_X3_B3FOLD ? YK_BS : YK_B, 3, u);
-        f32(Y_WA + u, SGN_X3_B3FOLD ? YK_WINV : YK_W, 4, u);  // YK_WINV: w 2^-s of layer 3
+        f32(Y_B3 + u, YK_B, 3, u);  // block3.2's bias, added in the row kernel's epilogue
+        f32(Y_WA + u, YK_W, 4, u);
     }
     f32(Y_BA, YK_B, 4, 0);
     const int li[7] = {0, 1, 2, 3, 5, 6, 7};
@@ -1821,13 +1567,6 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
     }
     // the fp16-range flag covers the samples of this call's colour stage (cleared with its first chunk)
     if (stages & 2) SGN_CHECK_HIP(hipMemsetAsync(tail + 1, 0, 4, st));
-#ifdef SGN_X3_TIMING
-    static unsigned long long *tbuf = nullptr;
-    const size_t tn = (size_t)x3::TD_BLOCKS * x3::NW16 * x3::TD_EV;
-    if (!tbuf) SGN_CHECK_HIP(hipMalloc(&tbuf, tn * 8));
-    SGN_CHECK_HIP(hipMemsetAsync(tbuf, 0, tn * 8, st));
-    a.tdbg = tbuf;
-#endif
     x3::ColorArgs c{q->counters, q->work, q->samp_ray, pt->raydir, d_packed, (const float *)d_workspace, d_out_feat,
                     tail + 1, 0, 0};
     for (int64_t i0 = 0; i0 < S_capacity; i0 += chunk) {
@@ -1851,15 +1590,6 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
             const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES, wmax = 256 * (8 / x3::NWR);
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < wmax ? wg16 : wmax)), dim3(x3::TPBR), 0, st, a);
         }
-#ifdef SGN_X3_TIMING
-        if ((stages & 1) && i0 == 0)
-            if (const char *path = getenv("SGN_X3_TDBG")) {
-                std::vector<unsigned long long> hb(tn);
-                SGN_CHECK_HIP(hipMemcpyAsync(hb.data(), tbuf, tn * 8, hipMemcpyDeviceToHost, st));
-                SGN_CHECK_HIP(hipStreamSynchronize(st));
-                if (FILE *f = fopen(path, "wb")) { fwrite(hb.data(), 8, tn, f); fclose(f); }
-            }
-#endif
         if (stages & 2) {
             const int64_t wgc = (n + 16 * x3::NWC - 1) / (16 * x3::NWC), wcmax = 256 * (8 / x3::NWC);
             hipLaunchKernelGGL(x3::k_color16, dim3((unsigned)(wgc < wcmax ? wgc : wcmax)), dim3(x3::TPBC), 0, st, c);

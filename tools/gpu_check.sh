@@ -1,16 +1,19 @@
 #!/bin/bash
-# One GPU call: GPU tests, smoke, bench (config 2) and the training bench (config 5).
-# Usage (GPU box): bash tools/gpu_check.sh <tag>
+# One GPU call: the GPU test suite (one process), then the training bench and its kernel trace.
+# Usage (GPU box): bash tools/gpu_check.sh <tag> [pytest -k expression]
 set -u
-TAG=${1:-chk}
-cd "$GRAFT_REPO_ROOT"
+TAG=$1
+K=${2:-}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-    > gpurun_out/pytest_$TAG.log 2>&1 || { echo PYTEST_FAIL; tail -30 gpurun_out/pytest_$TAG.log; exit 1; }
-tail -3 gpurun_out/pytest_$TAG.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo SMOKE_FAIL; tail -30 gpurun_out/smoke_$TAG.log; exit 1; }
-timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo BENCH_FAIL; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
-cat gpurun_out/bench_$TAG.json
-timeout -k 10 300 python bench.py --train > gpurun_out/train_$TAG.json 2> gpurun_out/train_$TAG.err || { echo TRAIN_FAIL; tail -30 gpurun_out/train_$TAG.err; exit 1; }
+if [ -n "$K" ]; then
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "$K" > gpurun_out/pytest_$TAG.log 2>&1
+else
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+fi
+rc=$?
+tail -5 gpurun_out/pytest_$TAG.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --train --steps 20 --warmup 5 > gpurun_out/train_$TAG.json 2> gpurun_out/train_$TAG.err || { tail -20 gpurun_out/train_$TAG.err; exit 1; }
 cat gpurun_out/train_$TAG.json
-echo GPU_CHECK_DONE
+bash tools/prof_train.sh $TAG --steps 20 --warmup 5 > /dev/null
