@@ -371,7 +371,9 @@ int sgn_colsum_f16_weighted(int32_t count, const void *const *d_x, const float *
  * src: nb split-K partials (fp32, device); dst: int32 device map from the MFMA storage order to
  * the flat parameter (-1 = padding); d_scale: device loss scale or NULL (1).  Every dst entry of
  * a launch must be distinct (no two segments add into the same element).  Up to 16 partials the
- * sum runs in partial order; beyond, groups of ~16 partials add with float atomics. */
+ * sum runs in partial order; beyond, groups of ~16 partials add with float atomics, so the
+ * fp32 sum order (not the set of terms) varies run to run.  The f16 training step uses it; the
+ * fp32 step reduces through sgn_reduce_partials (fixed order, deterministic). */
 typedef struct {
     const float *src;
     const float *tail;     /* optional [n] partial added after the nb slices (NULL: none) */

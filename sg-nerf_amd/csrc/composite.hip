@@ -40,6 +40,8 @@ __device__ __forceinline__ float pers_z(const float *campos, const float *rot, f
 // stores it as coalesced 16-B writes.  The LDS per workgroup (16.9 KiB) does not grow with SR, so
 // a CU holds 9 such waves at any SR (a whole-row [64][SR + 1] staging took 66 KiB at SR 128).
 constexpr int COMP_RAYS = 64, COMP_CW = 32, COMP_LD = COMP_CW + 1;
+// one wave per workgroup: the chunk loop's barriers stage the wave's own rows only
+static_assert(COMP_RAYS == 64, "k_composite: one wave64 per workgroup");
 
 // chunk [c0, c0 + cw) of the wave's 64 x SR block (row stride SR) from st [64][COMP_LD]
 __device__ __forceinline__ void store_chunk(float *dst, const float *st, int SR, int c0, int cw, int nrows,
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(COMP_RAYS) void k_composite(CompArgs a) {
         any_valid |= v;
     };
     if (last >= 0) step(0);
-    for (c0 = 0; c0 < SR; c0 += COMP_CW) {  // wave-uniform: every lane walks every chunk
+    for (c0 = 0; c0 < SR; c0 += COMP_CW) {  // wave-uniform trip count (see the exit below)
         const int cw = SR - c0 < COMP_CW ? SR - c0 : COMP_CW;
         if (want_o)
             for (int c = 0; c < cw; ++c) so[c] = 0.f;
@@ -127,7 +129,9 @@ __global__ __launch_bounds__(COMP_RAYS) void k_composite(CompArgs a) {
         if (want_o) store_chunk(a.out_opacity + r0 * SR, st[0], SR, c0, cw, nrows, lane);
         if (want_b) store_chunk(a.out_blendw + r0 * SR, st[1], SR, c0, cw, nrows, lane);
         __syncthreads();
-        if (!want_o && !want_b && c0 + cw > last) break;  // nothing staged: stop after the ray's slots
+        // nothing staged: stop once every lane's slots are done (a wave-uniform exit: the loop body holds
+        // barriers; the extra iterations of lanes already past their last slot are no-ops)
+        if (!want_o && !want_b && __all(c0 + cw > last)) break;
     }
     if (live) {
         a.out_mask[r] = any_valid ? 1 : 0;

@@ -521,6 +521,9 @@ __device__ __forceinline__ Rec16<PERS> load_rec16(const AggArgs &a, const RowIdx
 // tile's record (REC16_LOADS loads) and this tile's slot entry (1), the youngest; after block3.2 come the
 // next tile's 16 P loads (and the epilogue's f_s stores, masked per segment, so not counted), all
 // younger than block1.0's DMA
+// The save mode (training) waits vmcnt(0) at every boundary instead: its z stores inside the k-loops
+// let these counts pass with a weight LDS-DMA piece still in flight (a few samples a frame read stale
+// block3.2 weights, run to run; tools/f32_repeat.py)
 struct VmL3P0 {
     static constexpr int vm(int c) { return c == 1 ? REC16_LOADS + 1 : 0; }
 };
@@ -973,7 +976,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
 #pragma unroll
                 for (int t = 0; t < 16; ++t) accA[t] = accB[t];
             }
-            run_layer16<Net, 0, false, VmL0>(wb, ldsi, slot, w, lane, lz, accA,
+            run_layer16<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0>>(wb, ldsi, slot, w, lane, lz, accA,
                                              [&](auto k) { return pe_dists16_k<decltype(k)::value>(pr); },
                                              NoHook{});
         }
@@ -1048,7 +1051,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
             X3B in3[8];
             auto &acc0 = reinterpret_cast<f32x4(&)[8]>(acc[0]);
             auto &acc1 = reinterpret_cast<f32x4(&)[8]>(acc[8]);
-            run_layer16<Net, L3, true, VmL3P0, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) {
+            run_layer16<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0>, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) {
                 constexpr int K = decltype(k)::value;
                 in3[K] = chain_k(acc2, inv2, k, a.z3);
                 return in3[K];

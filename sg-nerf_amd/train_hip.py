@@ -734,16 +734,17 @@ class HipTrainer:
                                                  _lib.ptr(blob), _lib.ptr(self._feat32), _lib.ptr(self._z32[0]),
                                                  _lib.ptr(self._z32[1]), _lib.ptr(self._z32[2]), None, _lib.ptr(self._ws32),
                                                  self._ws32.numel(), st), "sgn_aggregate_train_fwd_f32")
-        # valid rows (sum of the samples' neighbour counts) on the device, fetched with S
-        nnb = q.samp_nnb[:cap]
-        n_rows = torch.where(torch.arange(cap, device=dev) < q.counters[0], nnb, 0).sum().reshape(1)
+        # valid rows on the device, fetched with S: counted from the same mask nonzero_static selects
+        # (a count from samp_nnb could disagree with pidx and pad with -1 or drop rows)
+        vmask = (q.pidx[:cap * o.K] >= 0) & (torch.arange(cap * o.K, device=dev) < q.counters[0] * o.K)
+        n_rows = vmask.sum().reshape(1)
         sync = torch.cat([q.counters[:1].to(torch.int64), n_rows.to(torch.int64)]
                          + ([gather_counts(t_cnt)] if dp else []))
         S, n_rows, *t_counts = (int(x) for x in sync.tolist())   # one host sync per step
         qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
               "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
         self._last_qd = qd   # the step's sample-major query (tests rerun fp32 autograd on it)
-        rows = torch.nonzero_static(qd["pidx"].reshape(-1) >= 0, size=n_rows).reshape(-1)   # no second sync
+        rows = torch.nonzero_static(vmask[:S * o.K], size=n_rows).reshape(-1)   # no second sync
         feat, _, mask = aggregate(P, self.mlp, campos.reshape(1, 3), rot, raydir, qd["samp_ray"], qd["samp_locw"],
                                   qd["pidx"], saved=self._z32, rows=rows)
         if self.hip_loss:

@@ -456,6 +456,62 @@ def test_graph_step_without_hits():
     assert tr._graphs, "the graph path did not run"
 
 
+def test_f32_step_without_hits():
+    """The fp32 step (every count on the device) on a batch whose rays all miss: background colour,
+    zero masked loss, every gradient exactly zero, finite parameters after the update."""
+    pc, view, qd, mlp, gt = _setup(seed=3)
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    campos = d(view.campos) + 100.0
+    points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    tr = HipTrainer(points, mlp, O, DEV, precision="f32")
+    for _ in range(2):
+        parts, full, mask = tr.backward(campos, d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV))
+        torch.cuda.synchronize()
+        assert not bool(mask.any())
+        assert torch.equal(full.cpu(), torch.ones_like(full.cpu()))
+        assert float(parts["ray_masked_coarse_raycolor"]) == 0.0
+        for k, g in grads_named(tr).items():
+            assert float(g.abs().max()) == 0.0, k
+        tr.apply()
+        assert all(torch.isfinite(getattr(points, k)).all() for k in ("points_embeding", "points_conf"))
+
+
+def test_colour_inputs_kernel_matches_torch():
+    """sgn_colour_inputs (the f16 step's captured colour-stage inputs) element by element against the
+    torch construction it replaced: items < counters[1] get fp32 f_s, the sample's alpha, its ray's
+    direction and the sample id; padding items zeros, ray 0's direction and the sentinel s_cap."""
+    from sgnerf_amd import _lib
+    g = torch.Generator().manual_seed(7)
+    n_cap, s_cap, n, R = 300, 500, 217, 64
+    work = torch.randperm(s_cap, generator=g)[:n_cap].to(torch.int32)
+    samp_ray = torch.randint(0, R, (s_cap,), generator=g, dtype=torch.int32)
+    fs16 = torch.randn(n_cap, 256, generator=g).half()
+    feat = torch.randn(s_cap, 4, generator=g)
+    raydir = torch.randn(R, 3, generator=g)
+    counters = torch.tensor([s_cap, n, 0, 0], dtype=torch.int32)
+    dv = {k: v.to(DEV) for k, v in dict(work=work, samp_ray=samp_ray, fs16=fs16, feat=feat, raydir=raydir,
+                                         counters=counters).items()}
+    fs32 = torch.full((n_cap, 256), float("nan"), device=DEV)
+    al32 = torch.full((n_cap,), float("nan"), device=DEV)
+    v = torch.full((n_cap, 3), float("nan"), device=DEV)
+    samp = torch.full((n_cap,), -7, dtype=torch.int32, device=DEV)
+    p = _lib.ptr
+    _lib.check(_lib.lib().sgn_colour_inputs(p(dv["counters"]), p(dv["work"]), p(dv["samp_ray"]), n_cap, s_cap,
+                                            p(dv["fs16"]), p(dv["feat"]), p(dv["raydir"]), p(fs32), p(al32), p(v),
+                                            p(samp), _lib.stream_handle()), "sgn_colour_inputs")
+    torch.cuda.synchronize()
+    ok = torch.arange(n_cap) < n
+    wk = work.long()
+    exp_fs = torch.where(ok[:, None], fs16.float(), torch.zeros(()))
+    exp_al = torch.where(ok, feat[wk, 0], torch.zeros(()))
+    exp_v = torch.where(ok[:, None], raydir[samp_ray[wk].long()], raydir[0].expand(n_cap, 3))
+    exp_samp = torch.where(ok, work, torch.full((), s_cap, dtype=torch.int32))
+    assert torch.equal(fs32.cpu(), exp_fs)
+    assert torch.equal(al32.cpu(), exp_al)
+    assert torch.equal(v.cpu(), exp_v)
+    assert torch.equal(samp.cpu(), exp_samp)
+
+
 def test_model_ranks_frames_by_ray_miss_loss(tmp_path):
     """optimize_parameters -> update_rank_ray_miss (neural_points_volumetric_model.py:328-330,
     mvs_points_volumetric_model.py:157-176) on real steps: the logged ray-miss loss is the
