@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--w", type=int, default=800)
     ap.add_argument("--sr", type=int, default=None, help="samples per ray (default 64 room, 128 lego)")
     ap.add_argument("--points", type=int, default=None, help="neural points (default 1.2M room, 300k lego)")
-    ap.add_argument("--scene", choices=["room", "lego", "dense"], default="room",
+    ap.add_argument("--scene", choices=["room", "lego", "dense", "spiral"], default="room",
                     help="room: BASELINE config 2 (headline); lego: config 4 (NeRF-synthetic camera, SR 128)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
@@ -93,8 +93,6 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None, precision=
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
     precision = args.train_precision if precision is None else precision
-    if args.sg and precision == "f32":
-        precision = "f16"    # the SG variant trains at fp16 operands (HipTrainer)
     from sgnerf_amd.train import PointParams, Trainer
     from sgnerf_amd.train_hip import HipTrainer
     sg = dict(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1) if args.sg else {}
@@ -151,11 +149,13 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None, precision=
            "config": {"workload": f"synth-room, {args.train_rays} random rays per rank per step, SR=24, K=8, "
                                   f"{args.points} neural points, HIP query + "
                                   + ("torch autograd" if args.train_torch else
-                                     "HIP fp32-faithful row-MLP forward (k_rows16 save mode) + fp32 backward + HIP loss stage"
+                                     "fp32 forward + backward on hand-written HIP kernels (k_rows16 save mode, split-fp16 "
+                                     "MFMA GEMMs k_x3rows / k_x3tn, HIP loss stage), fused Adam"
                                      if precision == "f32"
                                      else "HIP MFMA row-MLP forward/backward + torch colour-MLP autograd + HIP loss stage")
                                   + (" (SG-NeRF variant: semantic-guided kNN, block2_bpnet 352->256)" if args.sg else "")
-                                  + " + RCCL all-reduce",
+                                  + (" + RCCL all-reduce of the gradients" if world > 1 else
+                                     ", one GPU (no gradient exchange)"),
                       "parallelism": f"dp{world}"},
            "final_loss": float(torch.stack(losses).mean().item()),
            "graph_captures": int(getattr(tr, "graph_captures", 0))}   # loss-stage captures, warm-up included
@@ -189,6 +189,13 @@ def _ray_labels(dev, o, pc, campos, raydir, near, far):
 def lego_pose_view(i, h, w, n_poses=120):
     """Config 4: the render_vid-style orbit of load_blender.py:51-56 (theta 0..360, phi -30, r 4)."""
     return scene.lego_view(360.0 * (i % n_poses) / n_poses, h, w, focal=1111.1111 * w / 800)
+
+
+def spiral_pose_view(i, h, w, n_poses=120):
+    """Config 3: the render_vid spiral (sgnerf_amd.render_vid.spiral_views: yaw 0->360 deg, pitch
+    10 sin(2 pi i / n) deg, camera at the room centre)."""
+    yaw, pitch = scene.spiral_yaw_pitch(i % n_poses, n_poses)
+    return scene.room_view(h, w, yaw=yaw, pitch=pitch, campos=(2.0, 2.0, 1.5))
 
 
 def pose_view(i, h, w, n_poses=120):
@@ -273,6 +280,7 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
     sg = dict(shading_feature_mlp_layer2_bpnet=1, predict_semantic=1, semantic_guidance=1) if args.sg else {}
     o = HotPathOpts(SR=args.sr, precision=precision, **sg)
     dense = args.scene == "dense"
+    spiral = args.scene == "spiral"
     pc = (scene.lego_standin(args.points, seed=0) if lego else
           scene.dense_cube(args.points, seed=0) if dense else scene.synth_room(args.points, seed=0))
     if args.sg:
@@ -282,7 +290,8 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
     r = HipRenderer(PointTables.from_cloud(pc, dev), mlp, o, dev)
     n_frames = warmup + steps
     poses = [(s * world + rank) for s in range(n_frames)]
-    views = [(lego_pose_view if lego else dense_pose_view if dense else pose_view)(p, args.h, args.w) for p in poses]
+    views = [(lego_pose_view if lego else dense_pose_view if dense else spiral_pose_view if spiral else pose_view)(
+        p, args.h, args.w) for p in poses]
     rays = [torch.from_numpy(v.raydir).to(dev) for v in views]
     cams = [(torch.from_numpy(v.campos).to(dev), torch.from_numpy(v.camrotc2w).to(dev)) for v in views]
     R = args.h * args.w
@@ -413,6 +422,31 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
     res.update(n_nb=float(np.mean(n_nb)), n_smp=float(np.mean(n_smp)), n_samples=float(np.mean(n_samples)),
                q_bytes=float(np.mean(q_bytes)))
     return res
+
+
+def extra_render(args, world, rank, dev, dist, scene_name, sr, points, steps, warmup, label, sg=False):
+    """One more frame workload at the headline's arithmetic, as an extra key of the bench line:
+    rate, stage times, the row kernel's MFMA roofline fraction and the occupancy."""
+    x3 = args.precision == "f32"
+    a = argparse.Namespace(**{**vars(args), "scene": scene_name, "sr": sr, "points": points, "sg": sg})
+    e = render_run(a, args.precision, world, rank, dev, dist, steps, warmup, scene_name == "lego")
+    R = args.h * args.w
+    flop_nb = FLOP_PER_ROW_SPLIT + (2 * 352 * 256 if sg else 0)
+    peak = PEAK_X3_TFLOPS if x3 else PEAK_F16_TFLOPS
+    st = e["stages_ms"]
+    achieved = flop_nb * e["n_nb"] / (st["agg_rows"] * 1e-3) / 1e12
+    out = {"value": e["value"], "unit": "rays/s", "ms_per_frame": e["ms_per_frame"], "steps": steps,
+           "warmup": warmup, "n_gpus": world, "dtype": "f32 (3xf16 split MFMA, fp32 accumulate)" if x3 else "f16",
+           "workload": f"{label}; {args.h}x{args.w} rays x SR={sr}, K=8",
+           "stages_ms": st,
+           "roofline": {"kernel": ("k_rows16" if x3 else "k_agg_rows") + (" (SG, + block2_bpnet.0)" if sg else ""),
+                        "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                        "frac": achieved / peak, "flop_per_valid_row": flop_nb, "avg_launch_ms": st["agg_rows"]},
+           "occupancy": {"samples_per_ray": e["n_samples"] / R, "valid_samples_per_ray": e["n_smp"] / R,
+                         "valid_neighbours_per_ray": e["n_nb"] / R}}
+    del e
+    torch.cuda.empty_cache()
+    return out
 
 
 def _query_counter(query_ms, key, path=os.path.join(ROOT, "profiles", "traffic_query_latest.json")):
@@ -582,6 +616,20 @@ def main():
             "roofline_frac": flop_nb * e["n_nb"] / (e["stages_ms"]["agg_rows"] * 1e-3) / 1e12 / peak}
         del e
         torch.cuda.empty_cache()
+        # BASELINE config 4 (lego stand-in, SR 128), the SG-NeRF variant on the config-2 frame and
+        # config 3 (the 120-frame render_vid spiral, SR 24) on this job's GPUs, at the headline's arithmetic
+        res["lego"] = extra_render(args, world, rank, dev, dist, scene_name="lego", sr=128, points=300_000, steps=4,
+                                   warmup=1, label="BASELINE config 4: synth-lego stand-in, Blender orbit, "
+                                                   "near 2 far 6, 300k points")
+        res["sg"] = extra_render(args, world, rank, dev, dist, scene_name="room", sr=args.sr, points=args.points,
+                                 steps=4, warmup=1, sg=True,
+                                 label="config-2 frame with the SG-NeRF variant: semantic-guided kNN (20 labels), "
+                                       "block2_bpnet 352->256")
+        n3 = -(-120 // world)
+        res[f"config3_{world}gpu"] = extra_render(
+            args, world, rank, dev, dist, scene_name="spiral", sr=24, points=1_200_000, steps=n3, warmup=1,
+            label=f"BASELINE config 3: 120-frame render_vid spiral (camera at the room centre, SR 24), "
+                  f"frame-sharded over {world} GPU(s), {n3} frames per rank")
         keys = ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "final_loss", "graph_captures", "config")
         res["train_config5"] = {k: tr[k] for k in keys}
         if tr16 is not None:

@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 9
+#define SGN_ABI_VERSION 10
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -266,6 +266,14 @@ int sgn_aggregate_train_fwd_f32(const void *d_point_proj, const sgn_point_tables
                                 int64_t S_capacity, int32_t K, const void *d_packed_mlp, float *d_out_feat,
                                 float *d_z1, float *d_z2, float *d_z3, const int32_t *d_row_off, void *d_workspace,
                                 size_t workspace_bytes, sgn_stream_t stream);
+/* The same for SG-NeRF's block2_bpnet.0 (point_aggregators.py:345-354, :629-636; bpnet_layers 1,
+ * bpnet_dim 0 or 96 with d_bpnet the fp32 [N][96] BPNet embedding): d_z2 gets block1.2's
+ * pre-activations, d_zb block2_bpnet.0's (block3.0's input).  d_packed_mlp: the SG fp32 blob. */
+int sgn_aggregate_train_fwd_f32_sg(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
+                                   const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q,
+                                   int64_t S_capacity, int32_t K, const void *d_packed_mlp, float *d_out_feat,
+                                   float *d_z1, float *d_z2, float *d_zb, float *d_z3, const int32_t *d_row_off,
+                                   void *d_workspace, size_t workspace_bytes, sgn_stream_t stream);
 int64_t sgn_mlp_layout_f32(int32_t which);
 int sgn_mlp_pack_index_f32(int32_t bpnet_layers, int32_t bpnet_dim, int32_t which, int32_t *out, int64_t n);
 
@@ -423,7 +431,7 @@ size_t sgn_pow2_scale_workspace_bytes(void);
 int sgn_pow2_scale(const float *d_a, int64_t na, const float *d_b, int64_t nb, void *d_ws, float *d_out,
                    sgn_stream_t stream);
 
-/* ---- fp32 training step on hand-written kernels (ABI 9) -----------------------------------
+/* ---- fp32 training step on hand-written kernels (ABI 9; SG entries ABI 10) -----------------------------------
  * The reference's fp32 autograd through PointAggregator / viewmlp and the NeuralPoints gather
  * (models/aggregators/point_aggregators.py:561-786, :868-959; neural_points.py:942-988; run from
  * optimize_parameters, base_rendering_model.py:534-664, mvs_points_volumetric_model.py:116-141) as
@@ -486,6 +494,11 @@ int sgn_train_lists(const int32_t *d_counters, const int32_t *d_samp_nnb, int64_
 int sgn_train_row_inputs(const sgn_point_tables *pt, const sgn_query_out *q, int32_t K, const int32_t *d_row_off,
                          const int32_t *d_counts, float *d_x0, float *d_ext, float *d_rw, float *d_vpe,
                          sgn_stream_t stream);
+/* Per compact row j (sample s, neighbour k): d_dst[j][0..dim) = d_src[pidx[s K + k]][0..dim) --
+ * SG's BPNet embedding rows, block2_bpnet.0's second input, for its weight gradient (dim % 4 == 0,
+ * 16-B aligned tables). */
+int sgn_train_row_gather(const sgn_query_out *q, int32_t K, const int32_t *d_row_off, const int32_t *d_counts,
+                         const float *d_src, int32_t dim, float *d_dst, sgn_stream_t stream);
 /* color_branch.6 + sigmoid * 1.002 - 0.001 (fp32) on the items' last hidden layer d_h3 [items][128]
  * (d_w6 [3][128], d_b6 [3]): d_feat[work[i]].rgb. */
 int sgn_train_colour_head(const sgn_query_out *q, const int32_t *d_counts, const float *d_h3, const float *d_w6,

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -163,6 +163,10 @@ SIGNATURES = {
     "sgn_aggregate_flag_offset_f32": (c_sz, [c_sz]),
     "sgn_aggregate_train_fwd_f32": (c_i32, [c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,
                                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "sgn_aggregate_train_fwd_f32_sg": (c_i32, [c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(PointTables),
+                                               ctypes.POINTER(QueryOut), c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                               c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "sgn_train_row_gather": (c_i32, [ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "sgn_x3_gemm": (c_i32, [ctypes.POINTER(X3GemmArgs), c_vp]),
     "sgn_train_lists_workspace_bytes": (c_sz, [c_i64]),
     "sgn_train_lists": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -114,8 +114,9 @@ struct AggArgs {
     const int32_t *slot_n;
     // fp32-faithful training forward (k_rows16 save mode): the pre-activations 2^-s acc of block1.0,
     // block1.2 and block3.0 (the inputs of the next layer before LeakyReLU), fp32 natural unit order,
-    // row s * 8 + k (the row's pidx index); rows without a neighbour are not written
-    float *z1, *z2, *z3;
+    // row s * 8 + k (the row's pidx index); rows without a neighbour are not written.  SG: zb is
+    // block2_bpnet.0's (block3.0's input), z2 stays block1.2's
+    float *z1, *z2, *z3, *zb;
     // with row_off (sgn_train_lists): the rows are compact instead, row_off[s] + k
     const int32_t *row_off;
     // neighbours per sample of the query's pidx (fp32 kernels: 1..8; a row-table entry s * 8 + k

@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "agg_device.h"
+#include "x3_split.h"
 
 namespace sgn {
 namespace {
@@ -177,30 +178,6 @@ struct VmZero {
     static constexpr int vm(int) { return 0; }
 };
 
-
-// sin and cos of x (fp32, within ~1 ulp): quadrant q = rint(x 2/pi), r = x - q pi/2 in double
-// (exact to far below fp32 resolution for |x| < 2^20), cephes' minimax polynomials on
-// [-pi/4, pi/4]; |x| >= 2^20 (never met by the encodings' arguments) takes the library sincosf.
-__device__ __forceinline__ void sincos_acc_fast(float x, float &s, float &c) {  // |x| < 2^20
-    const float qf = __builtin_rintf(x * 0.63661977236758134f);
-    const float r = (float)__builtin_fma((double)qf, -1.5707963267948966, (double)x);
-    const float z = r * r;
-    const float sp = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
-                                                   -1.6666654611e-1f), z * r, r);
-    const float cp = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
-                                                   4.166664568298827e-2f), z * z, __builtin_fmaf(-0.5f, z, 1.f));
-    const int q = (int)qf;
-    const float s0 = (q & 1) ? cp : sp, c0 = (q & 1) ? sp : cp;
-    s = (q & 2) ? -s0 : s0;
-    c = ((q + 1) & 2) ? -c0 : c0;
-}
-__device__ __forceinline__ void sincos_acc(float x, float &s, float &c) {
-    if (__builtin_expect(__builtin_fabsf(x) >= 1048576.f, 0)) {
-        sincosf(x, &s, &c);
-        return;
-    }
-    sincos_acc_fast(x, s, c);
-}
 
 // accurate sin/cos of x 2^F (the scaling is exact; torch.sin on the product, networks.py:186)
 template <int F>
@@ -783,8 +760,8 @@ struct Tiles {
 __device__ __forceinline__ Tiles grid_tiles(int ntiles) { return Tiles{(int)blockIdx.x, ntiles, (int)gridDim.x}; }
 
 // KB: k-steps of block2_bpnet.0 in 16x16 steps (0: base viewmlp; 8: bpnet_dim 0; 11: dim 96)
-// SAVE (base viewmlp, training): the pre-activations of block1.0 / 1.2 / 3.0 go to a.z1 / z2 / z3 as
-// the next layer converts them (chain_k)
+// SAVE (training): the pre-activations of block1.0 / 1.2 / 3.0 go to a.z1 / z2 / z3 as the next
+// layer converts them (chain_k); SG: block2_bpnet.0's to a.zb
 template <int KB, bool PERS, bool SAVE = false>
 __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
     using Net = std::conditional_t<(KB > 0), NetR16SG<KB>, NetR16>;
@@ -1005,7 +982,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
             bias_init(accA, Y_BB);
             run_layer16<Net, LB>(wb, ldsi, slot, w, lane, lz, accA, [&](auto k) {
                 constexpr int K = decltype(k)::value;
-                if constexpr (K < 8) return chain_k(accB, inv1, k); else return bpv[K - 8];
+                if constexpr (K < 8) return chain_k(accB, inv1, k, a.z2); else return bpv[K - 8];
             }, NoHook{});
         }
         // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input: block1.2 or block2_bpnet)
@@ -1015,7 +992,7 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
         bias_init(acc2, Y_B2);
         run_layer16<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {
             constexpr int K = decltype(k)::value;
-            if constexpr (K < 8) return chain_k(in2, inv_in2, k, a.z2); else return ext;
+            if constexpr (K < 8) return chain_k(in2, inv_in2, k, KB > 0 ? a.zb : a.z2); else return ext;
         }, [&](auto c) {
             constexpr int C = decltype(c)::value;
             if constexpr (C == 0) {  // v_next landed at the previous boundaries
@@ -1557,7 +1534,7 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
     int32_t *slot_n = tail;
     a.rows = rows; a.slots = slots; a.slot_n = slot_n;
     if (z) {
-        a.z1 = z[0]; a.z2 = z[1]; a.z3 = z[2];
+        a.z1 = z[0]; a.z2 = z[1]; a.z3 = z[2]; a.zb = z[3];
         a.row_off = row_off;
     }
     // SGN_PAIR=0 runs every sample alone in its k_rows16 half (same results, bit for bit; tests)
@@ -1585,7 +1562,8 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
             hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)(pb < 1024 ? pb : 1024)),
                                dim3(x3::PAIR_TPB), 0, st, q->counters, q->work, q->samp_nnb, (int32_t)i0, (int32_t)n,
                                pair, rows, slots, slot_n);
-            auto kern = z ? x3::k_rows16<0, false, true>
+            auto kern = z ? (ksb == 0 ? x3::k_rows16<0, false, true> : ksb == KS_HID ? x3::k_rows16<8, false, true>
+                                                                                  : x3::k_rows16<11, false, true>)
                           : pt->pers ? (ksb == 0 ? x3::k_rows16<0, true> : ksb == KS_HID ? x3::k_rows16<8, true>
                                                                                       : x3::k_rows16<11, true>)
                                      : (ksb == 0 ? x3::k_rows16<0, false> : ksb == KS_HID ? x3::k_rows16<8, false>
@@ -1622,9 +1600,24 @@ int sgn_aggregate_train_fwd_f32(const void *d_point_proj, const sgn_point_tables
                     ((uintptr_t)d_z3 & 15) == 0,
                 "16-byte aligned pre-activation buffers z1, z2, z3 required");
     SGN_REQUIRE(pt && pt->pers == nullptr, "the training forward computes the pers coordinates itself");
-    float *const z[3] = {d_z1, d_z2, d_z3};
+    float *const z[4] = {d_z1, d_z2, d_z3, nullptr};
     return aggregate_f32(0, 0, nullptr, d_point_proj, pt, q, S_capacity, K, d_packed, d_out_feat, nullptr, nullptr,
                          d_workspace, workspace_bytes, 1, stream, z, d_row_off);
+}
+
+int sgn_aggregate_train_fwd_f32_sg(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
+                                   const void *d_point_proj, const sgn_point_tables *pt, const sgn_query_out *q,
+                                   int64_t S_capacity, int32_t K, const void *d_packed, float *d_out_feat, float *d_z1,
+                                   float *d_z2, float *d_zb, float *d_z3, const int32_t *d_row_off, void *d_workspace,
+                                   size_t workspace_bytes, sgn_stream_t stream) {
+    SGN_REQUIRE(bpnet_layers == 1, "the SG training forward has one block2_bpnet layer");
+    SGN_REQUIRE(d_z1 && d_z2 && d_zb && d_z3 && ((uintptr_t)d_z1 & 15) == 0 && ((uintptr_t)d_z2 & 15) == 0 &&
+                    ((uintptr_t)d_zb & 15) == 0 && ((uintptr_t)d_z3 & 15) == 0,
+                "16-byte aligned pre-activation buffers z1, z2, zb, z3 required");
+    SGN_REQUIRE(pt && pt->pers == nullptr, "the training forward computes the pers coordinates itself");
+    float *const z[4] = {d_z1, d_z2, d_z3, d_zb};
+    return aggregate_f32(bpnet_layers, bpnet_dim, d_bpnet, d_point_proj, pt, q, S_capacity, K, d_packed, d_out_feat,
+                         nullptr, nullptr, d_workspace, workspace_bytes, 1, stream, z, d_row_off);
 }
 
 int sgn_mlp_pack_index_f32(int32_t bpnet_layers, int32_t bpnet_dim, int32_t which, int32_t *out, int64_t n) {

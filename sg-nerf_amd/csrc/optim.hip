@@ -294,14 +294,29 @@ struct PackArgs {
     float *out32;
 };
 
-__global__ __launch_bounds__(256) void k_layer_shift(PackArgs a) {
+// one 1024-thread workgroup per layer; four independent max chains per thread keep several loads
+// in flight (the largest layer, block1.2 / block3.0, is ~73k weights)
+constexpr int SHIFT_TPB = 1024;
+__global__ __launch_bounds__(SHIFT_TPB) void k_layer_shift(PackArgs a) {
+    __shared__ uint32_t red[SHIFT_TPB / 64];
     const float *w = a.flat + a.woff[blockIdx.x];
     const int64_t n = a.wlen[blockIdx.x];
-    uint32_t m = 0;
-    for (int64_t i = threadIdx.x; i < n; i += 256) m = max(m, __float_as_uint(w[i]) & 0x7fffffffu);
-    m = block_max_u32(m);
+    uint32_t m[4] = {0u, 0u, 0u, 0u};
+    int64_t i = threadIdx.x;
+    for (; i + 3 * SHIFT_TPB < n; i += 4 * SHIFT_TPB) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] = max(m[q], __float_as_uint(w[i + q * SHIFT_TPB]) & 0x7fffffffu);
+    }
+    for (; i < n; i += SHIFT_TPB) m[0] = max(m[0], __float_as_uint(w[i]) & 0x7fffffffu);
+    uint32_t v = max(max(m[0], m[1]), max(m[2], m[3]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
     if (threadIdx.x == 0) {
-        const float f = __uint_as_float(m);
+        uint32_t mm = 0;
+        for (int q = 0; q < SHIFT_TPB / 64; ++q) mm = max(mm, red[q]);
+        const float f = __uint_as_float(mm);
         int e = 0;
         if (f > 0.f && __builtin_isfinite(f)) frexpf(f, &e);
         a.shift[blockIdx.x] = (f > 0.f && __builtin_isfinite(f)) ? 14 - e : 0;
@@ -548,7 +563,7 @@ int sgn_pack_scaled_f32(const float *d_flat, int64_t n_flat, int32_t n_layers, c
     a.shift = d_shift;
     a.out16 = static_cast<__half *>(d_out16);
     a.out32 = d_out32;
-    hipLaunchKernelGGL(k_layer_shift, dim3(n_layers), dim3(256), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(k_layer_shift, dim3(n_layers), dim3(SHIFT_TPB), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     const int64_t nmax = std::max<int64_t>(std::max(n16, n32), 1);
     hipLaunchKernelGGL(k_pack_scaled, dim3((unsigned)((nmax + 255) / 256), 2), dim3(256), 0, as_stream(stream), a);

@@ -10,14 +10,16 @@
 //
 //   k_lists_count / k_lists_write  deterministic work list (samples with a neighbour, ascending) and
 //                                  the compact row offset of every sample (prefix sum of samp_nnb)
-//   k_rows16 (mlp_x3.hip, save)    the forward; z1 / z2 / z3 pre-activations at the compact rows
+//   k_rows16 (mlp_x3.hip, save)    the forward; z1 / z2 / z3 (SG: + zb) pre-activations at the rows
 //   k_row_inputs                   per row: block1.0's input x0 = [emb | PE(emb) | PE(dists) | 1],
 //                                  block3.0's extra channels [colour | dir - v | <dir, v> | 1], the
-//                                  blend weights (w conf, w)
-//   k_colour_in                    per item: PE(viewdir) | 1 (the colour MLP's 24 extra inputs)
-//   k_x3gemm                       every nn.Linear product: forward (x W^T), backward data
-//                                  (dy W, masked by LeakyReLU' of the saved activation) and weight
-//                                  gradients (dy^T x as split-K partials, bias through a ones column)
+//                                  blend weights (w conf, w); per item PE(viewdir) | 1 (the colour
+//                                  MLP's 24 extra inputs)
+//   k_row_gather                   SG: the rows' BPNet embedding (block2_bpnet.0's second input)
+//   k_x3rows / k_x3tn              every nn.Linear product: rows mode = forward (x W^T) and backward
+//                                  data (dy W, masked by LeakyReLU' of the saved activation), the
+//                                  weight block resident in LDS; split-K mode = weight gradients
+//                                  (dy^T x as fixed-order partials, bias through a ones column)
 //   k_colour_head / _bwd           color_branch.6 + sigmoid (fp32 FMA), and its backward
 //   k_row_head                     block3.2's LeakyReLU, the alpha branch, the K-blend backward:
 //                                  delta4, d conf through the straight-through clamp, dWa partials
@@ -129,171 +131,305 @@ __device__ __forceinline__ void load8(const Opnd &o, int i, int k, int lim, floa
     }
 }
 
-// One operand tile of T 32-wide tiles x 32 k per stage: 128 T lane fragments of 8 values, thread
-// tid takes fragments tid, tid + 256, ... (consecutive threads: consecutive i, so the LDS writes of
-// a wave land on consecutive 16-B slots).  LDS fragment (t, s, hl) at ((t * 2 + s) * 2 + hl) * FRAG.
-template <int T>
-struct Stage {
-    static constexpr int NF = (128 * T + TPB - 1) / TPB;
-    float v[NF][8];
-    __device__ __forceinline__ void load(const Opnd &o, int i0, int k0, int lim, int tid) {
+// ---- split-K mode: C[m][n] = sum over rows r of A(m, r) B(n, r) ---------------------------------
+// Both operands are row-major [rows][cols] (kmajor).  A stage is 32 rows; thread t of an operand loads
+// 4 consecutive columns (a quad) of 8 consecutive rows (an octet) as 8 float4, which transpose in
+// registers into the lane fragments of those 4 columns (8 k values each).  Stages are loaded two ahead
+// into registers, converted into LDS (two buffers), then 2 k-steps of MFMAs: 4 waves split M, each
+// wave WM x WN 32x32 tiles.
+template <int Q>  // column quads of the operand's block
+struct QStage {
+    float4 v[8];
+    __device__ __forceinline__ void load(const Opnd &o, int c0, int r0, int lim, int tid) {
+        if (tid >= 4 * Q) return;
+        const int q = tid % Q, oc = tid / Q;
+        const int c = c0 + 4 * q, r = r0 + 8 * oc;
+        const bool s1 = c < o.csplit;
+        const float *src = s1 ? o.p + c : o.p2 + (c - o.csplit);
+        const int64_t ld = s1 ? o.ld : o.ld2;
+        const bool full = o.vec && c + 4 <= o.ncols && (o.ones_col < c || o.ones_col >= c + 4);
+        if (full) {
 #pragma unroll
-        for (int j = 0; j < NF; ++j) {
-            const int f = tid + TPB * j;
-            if ((128 * T) % TPB == 0 || f < 128 * T) {
-                const int il = f % (32 * T), oc = f / (32 * T);
-                load8(o, i0 + il, k0 + 8 * oc, lim, v[j]);
+            for (int e = 0; e < 8; ++e)
+                v[e] = r + e < lim ? *(const float4 *)(src + (int64_t)(r + e) * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (o.act && s1) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    v[e] = make_float4(lrelu_ref(v[e].x), lrelu_ref(v[e].y), lrelu_ref(v[e].z), lrelu_ref(v[e].w));
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float x[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int cc = c + j;
+                    float u = 0.f;
+                    if (r + e < lim) {
+                        if (cc == o.ones_col) u = 1.f;
+                        else if (cc < o.ncols) {
+                            const bool t1 = cc < o.csplit;
+                            u = t1 ? o.p[(int64_t)(r + e) * o.ld + cc] : o.p2[(int64_t)(r + e) * o.ld2 + (cc - o.csplit)];
+                            if (o.act && t1) u = lrelu_ref(u);
+                        }
+                    }
+                    x[j] = u;
+                }
+                v[e] = make_float4(x[0], x[1], x[2], x[3]);
             }
         }
     }
+    // lane fragments (column 4 q + j, octet oc) -> LDS ((tile * 2 + kstep) * 2 + hi/lo) * FRAG + L * 16
     __device__ __forceinline__ void store(char *base, float scale, int tid) const {
+        if (tid >= 4 * Q) return;
+        const int q = tid % Q, oc = tid / Q;
 #pragma unroll
-        for (int j = 0; j < NF; ++j) {
-            const int f = tid + TPB * j;
-            if ((128 * T) % TPB == 0 || f < 128 * T) {
-                const int il = f % (32 * T), oc = f / (32 * T);
-                const int t = il >> 5, L = (il & 31) + 32 * (oc & 1), s = oc >> 1;
-                const X3Pair x = split8_scaled(v[j], scale);
-                char *d = base + ((t * 2 + s) * 2) * FRAG + L * 16;
-                *(h8 *)d = x.hi;
-                *(h8 *)(d + FRAG) = x.lo;
-            }
+        for (int j = 0; j < 4; ++j) {
+            float x[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = j == 0 ? v[e].x : j == 1 ? v[e].y : j == 2 ? v[e].z : v[e].w;
+            const int m = 4 * q + j;
+            const int t = m >> 5, L = (m & 31) + 32 * (oc & 1), s = oc >> 1;
+            const X3Pair p = split8_scaled(x, scale);
+            char *d = base + ((t * 2 + s) * 2) * FRAG + L * 16;
+            *(h8 *)d = p.hi;
+            *(h8 *)(d + FRAG) = p.lo;
         }
     }
 };
 
-// WM x WN 32x32 tiles per wave, GM x GN waves; TNM: split-K partials over rows (else rows mode)
-template <int WM, int WN, int GM, int GN, bool TNM>
-__global__ __launch_bounds__(TPB) void k_x3gemm(GemmK g) {
-    static_assert(GM * GN == 4, "four waves");
-    constexpr int TA = WM * GM, TB = WN * GN, BM = 32 * TA, BN = 32 * TB;
+template <int WM, int WN>
+__global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
+    constexpr int TA = 4 * WM, TB = WN, BM = 32 * TA, BN = 32 * TB;
     constexpr int ABYTES = TA * 4 * FRAG, STAGE = (TA + TB) * 4 * FRAG;
+    static_assert(BM / 4 * 4 <= TPB && BN / 4 * 4 <= TPB, "one quad-octet per thread");
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w % GM, wn = w / GM;
     const int sa = op_shift(g.A), sb = op_shift(g.B);
     const float fa = ldexpf(1.f, sa), fb = ldexpf(1.f, sb), osc = ldexpf(1.f, -(sa + sb));
-    const int rows_dev = g.d_rows ? *g.d_rows : 0x7fffffff;
-    Stage<TA> stA;
-    Stage<TB> stB;
-
-    auto tile = [&](int m0, int n0, int kbeg, int kend, int limA, int limB, f32x16 (&acc)[WM][WN]) {
+    const int nb_n = (g.N + BN - 1) / BN;
+    const int m0 = (blockIdx.x / nb_n) * BM, n0 = (blockIdx.x % nb_n) * BN;
+    const int rows = min(g.d_rows ? *g.d_rows : 0x7fffffff, g.K);
+    const int per = ((rows + (int)gridDim.y - 1) / (int)gridDim.y + 31) / 32 * 32;
+    const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+    const int nkb = r1 > r0 ? (r1 - r0 + 31) / 32 : 0;
+    f32x16 acc[WM][WN];
 #pragma unroll
-        for (int a = 0; a < WM; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-            for (int b = 0; b < WN; ++b) acc[a][b] = f32x16{};
-        const int nkb = kend > kbeg ? (kend - kbeg + 31) / 32 : 0;
-        if (nkb == 0) return;
-        stA.load(g.A, m0, kbeg, limA, tid);
-        stB.load(g.B, n0, kbeg, limB, tid);
-        stA.store(lds, fa, tid);
-        stB.store(lds + ABYTES, fb, tid);
-        __syncthreads();
-        for (int kb = 0; kb < nkb; ++kb) {
-            const bool more = kb + 1 < nkb;
-            if (more) {
-                stA.load(g.A, m0, kbeg + 32 * (kb + 1), limA, tid);
-                stB.load(g.B, n0, kbeg + 32 * (kb + 1), limB, tid);
+        for (int b = 0; b < WN; ++b) acc[a][b] = f32x16{};
+    QStage<BM / 4> a0, a1;
+    QStage<BN / 4> b0, b1;
+    auto compute = [&](const char *st) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            h8 ah[WM], al[WM];
+#pragma unroll
+            for (int a = 0; a < WM; ++a) {
+                const char *p = st + (((w * WM + a) * 2 + s) * 2) * FRAG + lane * 16;
+                ah[a] = *(const h8 *)p;
+                al[a] = *(const h8 *)(p + FRAG);
             }
-            const char *st = lds + (kb & 1) * STAGE;
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                h8 ah[WM], al[WM], bh[WN], bl[WN];
+            for (int b = 0; b < WN; ++b) {
+                const char *p = st + ABYTES + ((b * 2 + s) * 2) * FRAG + lane * 16;
+                const h8 bh = *(const h8 *)p, bl = *(const h8 *)(p + FRAG);
 #pragma unroll
                 for (int a = 0; a < WM; ++a) {
-                    const char *p = st + (((wm * WM + a) * 2 + s) * 2) * FRAG + lane * 16;
-                    ah[a] = *(const h8 *)p;
-                    al[a] = *(const h8 *)(p + FRAG);
+                    acc[a][b] = mfma32(al[a], bh, acc[a][b]);
+                    acc[a][b] = mfma32(ah[a], bl, acc[a][b]);
+                    acc[a][b] = mfma32(ah[a], bh, acc[a][b]);
                 }
-#pragma unroll
-                for (int b = 0; b < WN; ++b) {
-                    const char *p = st + ABYTES + (((wn * WN + b) * 2 + s) * 2) * FRAG + lane * 16;
-                    bh[b] = *(const h8 *)p;
-                    bl[b] = *(const h8 *)(p + FRAG);
-                }
-#pragma unroll
-                for (int a = 0; a < WM; ++a)
-#pragma unroll
-                    for (int b = 0; b < WN; ++b) {
-                        acc[a][b] = mfma32(al[a], bh[b], acc[a][b]);
-                        acc[a][b] = mfma32(ah[a], bl[b], acc[a][b]);
-                        acc[a][b] = mfma32(ah[a], bh[b], acc[a][b]);
-                    }
             }
-            if (more) {
-                char *nx = lds + ((kb + 1) & 1) * STAGE;
-                stA.store(nx, fa, tid);
-                stB.store(nx + ABYTES, fb, tid);
+        }
+    };
+    if (nkb > 0) {
+        a0.load(g.A, m0, r0, r1, tid);
+        b0.load(g.B, n0, r0, r1, tid);
+        if (nkb > 1) {
+            a1.load(g.A, m0, r0 + 32, r1, tid);
+            b1.load(g.B, n0, r0 + 32, r1, tid);
+        }
+        a0.store(lds, fa, tid);
+        b0.store(lds + ABYTES, fb, tid);
+        __syncthreads();
+        // two stages per trip, so the register sets keep static names: stage kb in LDS buffer kb & 1,
+        // stage kb + 1 in registers, stage kb + 2 loading
+        for (int kb = 0; kb < nkb; kb += 2) {
+            if (kb + 2 < nkb) {
+                a0.load(g.A, m0, r0 + 32 * (kb + 2), r1, tid);
+                b0.load(g.B, n0, r0 + 32 * (kb + 2), r1, tid);
+            }
+            compute(lds);
+            if (kb + 1 < nkb) {
+                a1.store(lds + STAGE, fa, tid);
+                b1.store(lds + STAGE + ABYTES, fb, tid);
+            }
+            __syncthreads();
+            if (kb + 1 >= nkb) break;
+            if (kb + 3 < nkb) {
+                a1.load(g.A, m0, r0 + 32 * (kb + 3), r1, tid);
+                b1.load(g.B, n0, r0 + 32 * (kb + 3), r1, tid);
+            }
+            compute(lds + STAGE);
+            if (kb + 2 < nkb) {
+                a0.store(lds, fa, tid);
+                b0.store(lds + ABYTES, fb, tid);
             }
             __syncthreads();
         }
-    };
+    }
+    float *part = g.part + (int64_t)blockIdx.y * g.M * g.N;
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+        for (int b = 0; b < WN; ++b) {
+            const int n = n0 + b * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + (w * WM + a) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (m < g.M && n < g.N) part[(int64_t)m * g.N + n] = acc[a][b][r] * osc;
+            }
+        }
+}
 
-    f32x16 acc[WM][WN];
-    if constexpr (TNM) {
-        // C[m][n] = sum over rows r of A(m, r) B(n, r); this workgroup: one (m, n) block, one split
-        const int nb_n = (g.N + BN - 1) / BN;
-        const int m0 = (blockIdx.x / nb_n) * BM, n0 = (blockIdx.x % nb_n) * BN;
-        const int rows = min(rows_dev, g.K);
-        const int splits = gridDim.y;
-        const int per = ((rows + splits - 1) / splits + 31) / 32 * 32;
-        const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
-        tile(m0, n0, r0, r1, r1, r1, acc);
-        float *part = g.part + (int64_t)blockIdx.y * g.M * g.N;
+// ---- rows mode, weights resident ----------------------------------------------------------------
+// Y[r][n] = sum_k A(r, k) B(n, k) for the 32 WN columns of block blockIdx.x: the workgroup converts
+// that block of B (KS k-steps of 16 x WN tiles of 32, hi / lo fp16 fragments, 2 KiB per (k-step,
+// tile)) into LDS once, then walks row tiles of 128 rows (one 32-row MFMA tile per wave) with the A
+// fragments loaded straight into registers: lane l holds row l & 31, k = 16 s + 8 (l >> 5) .. + 7 of
+// every k-step s, and the next tile's k-step s is loaded as soon as this tile's has been converted,
+// so a whole tile of MFMAs hides it.  One workgroup per CU (the weight block is up to 144 KiB).
+constexpr int RT_ROWS = 128;
+
+// the A operand of the rows mode: row-major, 16-B aligned rows, columns in whole octets (host-checked)
+struct ARow {
+    const float *r1, *r2;  // this lane's row in source 1 / 2 (null past the rows)
+    int csplit, ncols, act;
+    __device__ __forceinline__ void load(int k, float (&v)[8]) const {
+        const bool s1 = k < csplit;
+        const float *src = s1 ? r1 + k : r2 + (k - csplit);
+        if (r1 && k < ncols) {
+            const f32x4 x = *(const f32x4 *)src, y = *(const f32x4 *)(src + 4);
+            v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+            v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
+            if (act && s1) {
 #pragma unroll
-        for (int a = 0; a < WM; ++a)
+                for (int e = 0; e < 8; ++e) v[e] = lrelu_ref(v[e]);
+            }
+        } else {
 #pragma unroll
-            for (int b = 0; b < WN; ++b) {
-                const int n = n0 + (wn * WN + b) * 32 + (lane & 31);
+            for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        }
+    }
+};
+__device__ __forceinline__ ARow arow(const Opnd &o, int row, int lim) {
+    ARow a;
+    const bool ok = row < lim;
+    a.r1 = ok ? o.p + (int64_t)row * o.ld : nullptr;
+    a.r2 = ok && o.p2 ? o.p2 + (int64_t)row * o.ld2 : a.r1;
+    a.csplit = o.csplit;
+    a.ncols = o.ncols;
+    a.act = o.act;
+    return a;
+}
+
+template <int KS, int WN>
+__global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
+    __shared__ __attribute__((aligned(16))) char lds[KS * WN * 2 * FRAG];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int sa = op_shift(g.A), sb = op_shift(g.B);
+    const float fa = ldexpf(1.f, sa), fb = ldexpf(1.f, sb), osc = ldexpf(1.f, -(sa + sb));
+    const int rows = min(g.d_rows ? *g.d_rows : 0x7fffffff, g.M);
+    const int limA = min(rows, g.A.nrows);
+    const int n0 = blockIdx.x * (32 * WN);
+    const int L = lane & 31, hk = lane >> 5;
+    // the first tile's A loads go out before the weight staging
+    float a[KS][8];
+    int rt = blockIdx.y;
+    {
+        const ARow ar = arow(g.A, rt * RT_ROWS + 32 * w + L, limA);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) ar.load(16 * s + 8 * hk, a[s]);
+    }
+    // weights: lane fragment f = (k-step s, tile t, lane) -> ((s WN + t) 2 + hi/lo) FRAG + lane 16
+    for (int f = tid; f < KS * WN * 64; f += TPB) {
+        const int fl = f & 63, t = (f >> 6) % WN, s = f / (64 * WN);
+        float v[8];
+        load8(g.B, n0 + 32 * t + (fl & 31), 16 * s + 8 * (fl >> 5), g.B.nrows, v);
+        const X3Pair x = split8_scaled(v, fb);
+        char *d = lds + ((s * WN + t) * 2) * FRAG + fl * 16;
+        *(h8 *)d = x.hi;
+        *(h8 *)(d + FRAG) = x.lo;
+    }
+    __syncthreads();
+    float am1 = 0.f, am2 = 0.f;
+    for (; rt * RT_ROWS < rows; rt += gridDim.y) {
+        const int m0 = rt * RT_ROWS + 32 * w;
+        const ARow an = arow(g.A, (rt + gridDim.y) * RT_ROWS + 32 * w + L, limA);
+        f32x16 acc[WN];
+#pragma unroll
+        for (int t = 0; t < WN; ++t) acc[t] = f32x16{};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const X3Pair x = split8_scaled(a[s], fa);
+            an.load(16 * s + 8 * hk, a[s]);  // the next tile's k-step s
+            const char *p = lds + (s * WN * 2) * FRAG + lane * 16;
+#pragma unroll
+            for (int t = 0; t < WN; ++t) {
+                const h8 bh = *(const h8 *)(p + (2 * t) * FRAG), bl = *(const h8 *)(p + (2 * t + 1) * FRAG);
+                acc[t] = mfma32(x.lo, bh, acc[t]);
+                acc[t] = mfma32(x.hi, bl, acc[t]);
+                acc[t] = mfma32(x.hi, bh, acc[t]);
+            }
+        }
+        // epilogue: every mask value of the tile is loaded before any is used (one wait, not 16 per tile)
+        float mk[WN][16];
+        if (g.mask) {
+#pragma unroll
+            for (int t = 0; t < WN; ++t) {
+                const int n = n0 + 32 * t + L;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + (wm * WM + a) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    if (m < g.M && n < g.N) part[(int64_t)m * g.N + n] = acc[a][b][r] * osc;
+                    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+                    mk[t][r] = row < rows && n < g.out_cols ? g.mask[(int64_t)row * g.ldm + n] : 1.f;
                 }
             }
-    } else {
-        // Y[r][n] = sum_k A(r, k) B(n, k): persistent over row tiles, blockIdx.x = column block
-        const int rows = min(rows_dev, g.M);
-        const int n0 = blockIdx.x * BN;
-        const int limA = g.A.dyn ? min(rows, g.A.nrows) : g.A.nrows;
-        float am1 = 0.f, am2 = 0.f;
-        for (int rt = blockIdx.y; rt * BM < rows; rt += gridDim.y) {
-            const int m0 = rt * BM;
-            tile(m0, n0, 0, g.K, limA, g.B.nrows, acc);
+        }
 #pragma unroll
-            for (int a = 0; a < WM; ++a)
+        for (int t = 0; t < WN; ++t) {
+            const int n = n0 + 32 * t + L;
+            const float bv = g.bias && n < g.N ? g.bias[n] : 0.f;
+            const bool o1 = n < g.out_cols, o2 = !o1 && n < g.N;
+            float *d1 = g.out + n, *d2 = g.out2 + (n - g.out_cols);
 #pragma unroll
-                for (int b = 0; b < WN; ++b) {
-                    const int n = n0 + (wn * WN + b) * 32 + (lane & 31);
-                    const float bv = g.bias && n < g.N ? g.bias[n] : 0.f;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int row = m0 + (wm * WM + a) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                        if (row >= rows || n >= g.N) continue;
-                        float v = acc[a][b][r] * osc + bv;
-                        if (n < g.out_cols) {
-                            if (g.mask && !(g.mask[(int64_t)row * g.ldm + n] > 0.f)) v *= 0.01f;
-                            if (g.act) v = lrelu_ref(v);
-                            g.out[(int64_t)row * g.ldo + n] = v;
-                            am1 = fmaxf(am1, fabsf(v));
-                        } else {
-                            g.out2[(int64_t)row * g.ldo2 + (n - g.out_cols)] = v;
-                            am2 = fmaxf(am2, fabsf(v));
-                        }
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+                float v = acc[t][r] * osc + bv;
+                if (g.mask && !(mk[t][r] > 0.f)) v *= 0.01f;
+                if (o1) {
+                    if (g.act) v = lrelu_ref(v);
+                    if (row < rows) {
+                        d1[(int64_t)row * g.ldo] = v;
+                        am1 = fmaxf(am1, fabsf(v));
                     }
+                } else if (o2 && row < rows) {
+                    d2[(int64_t)row * g.ldo2] = v;
+                    am2 = fmaxf(am2, fabsf(v));
                 }
+            }
         }
-        // the producer's amax word for the consumer's operand scale (max |x|, as uint bits)
+    }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            am1 = fmaxf(am1, __shfl_xor(am1, o));
-            am2 = fmaxf(am2, __shfl_xor(am2, o));
-        }
-        if (lane == 0) {
-            if (g.amax_out) atomicMax(g.amax_out, __builtin_bit_cast(uint32_t, am1));
-            if (g.amax_out2) atomicMax(g.amax_out2, __builtin_bit_cast(uint32_t, am2));
-        }
+    for (int o = 32; o > 0; o >>= 1) {
+        am1 = fmaxf(am1, __shfl_xor(am1, o));
+        am2 = fmaxf(am2, __shfl_xor(am2, o));
+    }
+    if (lane == 0) {
+        if (g.amax_out) atomicMax(g.amax_out, __builtin_bit_cast(uint32_t, am1));
+        if (g.amax_out2) atomicMax(g.amax_out2, __builtin_bit_cast(uint32_t, am2));
     }
 }
 
@@ -410,21 +546,30 @@ struct RowArgs {
 
 __device__ __forceinline__ int n_items(const RowArgs &r) { return r.tl[0]; }
 
-// x0 column c of a row (point_aggregators.py:594-621: [emb | PE(emb, 3) | PE(dists, 5)], then the
-// ones column 284 that carries block1.0's bias gradient, zero padding to 288)
-__device__ __forceinline__ float x0_col(int c, const float *e, const float (&d)[6]) {
-    if (c < 32) return e[c];
-    if (c < 224) {
-        const int m = c - 32, ch = m / 6, f = (m % 6) >> 1;
-        const float a = e[ch] * (float)(1 << f);
-        return (m & 1) ? cosf(a) : sinf(a);
+// x0 columns c0..c0+3 (c0 % 4 == 0) of a row (point_aggregators.py:594-621: [emb | PE(emb, 3) |
+// PE(dists, 5)], then the ones column 284 that carries block1.0's bias gradient, zero padding to
+// 288).  PE columns come in (sin, cos) pairs of one argument: pair p of PE(emb) is channel p / 3 at
+// frequency 2^(p % 3), of PE(dists) channel p / 5 at 2^(p % 5) (networks.py:175-192)
+__device__ __forceinline__ f32x4 x0_quad(int c0, const float *e, const float (&d)[6]) {
+    f32x4 v;
+    if (c0 < 32) return *(const f32x4 *)(e + c0);
+    if (c0 >= 284) {
+        v[0] = 1.f; v[1] = v[2] = v[3] = 0.f;
+        return v;
     }
-    if (c < 284) {
-        const int m = c - 224, dd = m / 10, f = (m % 10) >> 1;
-        const float a = d[dd] * (float)(1 << f);
-        return (m & 1) ? cosf(a) : sinf(a);
+    const bool pe_emb = c0 < 224;
+    const int p0 = (c0 - (pe_emb ? 32 : 224)) >> 1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int p = p0 + h;
+        const int ch = pe_emb ? p / 3 : p / 5, f = pe_emb ? p % 3 : p % 5;
+        const float base = pe_emb ? e[ch] : d[ch];
+        float sn, cs;
+        sincos_acc(base * (float)(1 << f), sn, cs);
+        v[2 * h] = sn;
+        v[2 * h + 1] = cs;
     }
-    return c == 284 ? 1.f : 0.f;
+    return v;
 }
 
 // dists of a row and the sample's linear-kernel weights (point_aggregators.py:494-502, :868-953;
@@ -455,7 +600,11 @@ __device__ __forceinline__ void row_geometry(const RowArgs &a, const Cam &cam, i
     wgt = cf;
 }
 
-__global__ __launch_bounds__(TPB) void k_row_inputs(RowArgs a, float *x0, float *ext, float2 *rw) {
+// x0 as 72 quads + ext as 2 quads per row: the item's rows x quads are one flat task list over the
+// wave's lanes (row geometry from lane k by a lane-indexed shuffle)
+constexpr int X0_QUADS = 72, ROW_QUADS = 74;
+
+__global__ __launch_bounds__(TPB) void k_row_inputs(RowArgs a, float *x0, float *ext, float2 *rw, float *vpe) {
     const int lane = threadIdx.x & 63;
     const int wv = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TPB / 64);
     const Cam cam = load_cam(a.campos, a.rot);
@@ -477,52 +626,61 @@ __global__ __launch_bounds__(TPB) void k_row_inputs(RowArgs a, float *x0, float 
         const float wgt = wn * fminf(fmaxf(cf, 1e-4f), 1.f);
         if (lane < nnb) rw[ro + lane] = make_float2(wgt, wn);
         const float vx = a.raydir[(int64_t)ray * 3], vy = a.raydir[(int64_t)ray * 3 + 1], vz = a.raydir[(int64_t)ray * 3 + 2];
-        for (int k = 0; k < nnb; ++k) {
+        if (lane < 32) {  // the item's PE(viewdir) for the colour MLP (:772-780), ones column 24
+            float v = lane == 24 ? 1.f : 0.f;
+            if (lane < 24) {
+                const int jj = lane < 12 ? lane : lane - 12, c = jj >> 2, f = jj & 3;
+                float sn, cs;
+                sincos_acc((c == 0 ? vx : c == 1 ? vy : vz) * (float)(1 << f), sn, cs);
+                v = lane < 12 ? sn : cs;
+            }
+            vpe[(int64_t)it * 32 + lane] = v;
+        }
+        const int ntask = nnb * ROW_QUADS;
+        for (int t0 = 0; t0 < ntask; t0 += 64) {  // wave-uniform trip count: the shuffles see every lane
+            const int t = t0 + lane;
+            const bool act = t < ntask;
+            const int k = act ? t / ROW_QUADS : 0, q = t - k * ROW_QUADS;
             const int pid = __shfl(pidl, k);
             float d[6];
 #pragma unroll
-            for (int q = 0; q < 6; ++q) d[q] = __shfl(dl[q], k);
-            const float *e = a.emb + (int64_t)pid * 32;
-            float *xr = x0 + (int64_t)(ro + k) * 288;
-            f32x4 v4;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v4[q] = x0_col(4 * lane + q, e, d);
-            *(f32x4 *)(xr + 4 * lane) = v4;
-            if (lane < 8) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v4[q] = x0_col(256 + 4 * lane + q, e, d);
-                *(f32x4 *)(xr + 256 + 4 * lane) = v4;
-            }
-            if (lane < 8) {  // block3.0's extra channels (:639-652) + the ones column of its bias
-                float u;
-                const int64_t pb = (int64_t)pid * 3;
-                if (lane < 3) u = a.color[pb + lane];
-                else if (lane < 6) u = __fsub_rn(a.dir[pb + lane - 3], lane == 3 ? vx : lane == 4 ? vy : vz);
-                else if (lane == 6)
-                    u = __fadd_rn(__fadd_rn(__fmul_rn(a.dir[pb], vx), __fmul_rn(a.dir[pb + 1], vy)), __fmul_rn(a.dir[pb + 2], vz));
-                else u = 1.f;
-                ext[(int64_t)(ro + k) * 8 + lane] = u;
+            for (int c = 0; c < 6; ++c) d[c] = __shfl(dl[c], k);
+            if (!act) continue;
+            const int64_t row = ro + k;
+            const int64_t pb = (int64_t)pid * 3;
+            if (q < X0_QUADS) {
+                *(f32x4 *)(x0 + row * 288 + 4 * q) = x0_quad(4 * q, a.emb + (int64_t)pid * 32, d);
+            } else if (q == X0_QUADS) {  // block3.0's extra channels (:639-652): colour, dir - v
+                f32x4 u;
+                u[0] = a.color[pb]; u[1] = a.color[pb + 1]; u[2] = a.color[pb + 2];
+                u[3] = __fsub_rn(a.dir[pb], vx);
+                *(f32x4 *)(ext + row * 8) = u;
+            } else {  // dir - v, <dir, v>, and the ones column of block3.0's bias
+                const float d0 = a.dir[pb], d1 = a.dir[pb + 1], d2 = a.dir[pb + 2];
+                f32x4 u;
+                u[0] = __fsub_rn(d1, vy);
+                u[1] = __fsub_rn(d2, vz);
+                u[2] = __fadd_rn(__fadd_rn(__fmul_rn(d0, vx), __fmul_rn(d1, vy)), __fmul_rn(d2, vz));
+                u[3] = 1.f;
+                *(f32x4 *)(ext + row * 8 + 4) = u;
             }
         }
     }
 }
 
-// PE(viewdir) for the colour MLP (point_aggregators.py:772-780: positional_encoding(v, 4, ori=True)
-// without the raw v): [sin(v_c 2^f) (c-major) | cos(...)], then the ones column 24, zero to 32
-__global__ __launch_bounds__(TPB) void k_colour_in(RowArgs a, float *vpe) {
-    const int n = n_items(a);
-    for (int64_t t = blockIdx.x * (int64_t)TPB + threadIdx.x; t < (int64_t)n * 32; t += (int64_t)gridDim.x * TPB) {
-        const int it = (int)(t >> 5), j = (int)(t & 31);
-        float v = 0.f;
-        if (j < 24) {
-            const int ray = a.samp_ray[a.work[it]];
-            const int jj = j < 12 ? j : j - 12, c = jj >> 2, f = jj & 3;
-            const float x = a.raydir[(int64_t)ray * 3 + c] * (float)(1 << f);
-            v = j < 12 ? sinf(x) : cosf(x);
-        } else if (j == 24) {
-            v = 1.f;
+// d_dst[row] = d_src[pid of the row] (dim floats, as quads): the item's rows x quads as one flat list
+__global__ __launch_bounds__(TPB) void k_row_gather(RowArgs a, const float *src, int dim, float *dst) {
+    const int lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TPB / 64);
+    const int n = n_items(a), nq = dim >> 2;
+    for (int it = wv; it < n; it += nw) {
+        const int s = a.work[it];
+        const int nnb = a.samp_nnb[s], ro = a.row_off[s];
+        for (int t = lane; t < nnb * nq; t += 64) {
+            const int k = t / nq, q = t - k * nq;
+            const int pid = a.pidx[(int64_t)s * a.K + k];
+            *(f32x4 *)(dst + (int64_t)(ro + k) * dim + 4 * q) = *(const f32x4 *)(src + (int64_t)pid * dim + 4 * q);
         }
-        vpe[t] = v;
     }
 }
 
@@ -614,6 +772,29 @@ __device__ __forceinline__ float softplus_ref(float x) { return x > 20.f ? x : l
 // d w = <h4, d f_s> + alpha dalpha_s (-> d conf = d w * w_norm through the straight-through clamp);
 // delta4 = (w d f_s + dza wa) LReLU'(z4) (in place over z4).  dWa / dba partial per workgroup
 // ([HEAD_BLOCKS][257]).
+// 16 wave-wide sums at once, reduce-scatter style (17 cross-lane moves instead of 96): on return,
+// the sum of v[j] over the wave sits in lane 4 j of v[0] (fixed order, deterministic)
+__device__ __forceinline__ void wave_sum16(float (&v)[16], int lane) {
+#pragma unroll
+    for (int h = 8; h >= 1; h >>= 1) {  // exchange distance 32, 16, 8, 4 halves the live values
+        const int o = 4 * h;
+        const bool up = lane & o;
+#pragma unroll
+        for (int i = 0; i < h; ++i) {
+            const float send = up ? v[i] : v[i + h];
+            const float keep = up ? v[i + h] : v[i];
+            v[i] = keep + __shfl_xor(send, o);
+        }
+    }
+    v[0] += __shfl_xor(v[0], 2);
+    v[0] += __shfl_xor(v[0], 1);
+}
+__device__ __forceinline__ float lane_value(float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+
+constexpr int MAX_K = 8;
+
 __global__ __launch_bounds__(TPB) void k_row_head(RowArgs a, float *z4d4, const float *dfs, const float4 *dfeat,
                                                   const float2 *rw, const float *wa, const float *ba, float *g_conf,
                                                   uint32_t *amax, float *part) {
@@ -630,34 +811,53 @@ __global__ __launch_bounds__(TPB) void k_row_head(RowArgs a, float *z4d4, const 
         const int nnb = a.samp_nnb[s], ro = a.row_off[s];
         const float das = dfeat[s].x;
         const f32x4 df = *(const f32x4 *)(dfs + (int64_t)it * 256 + 4 * lane);
-        for (int k = 0; k < nnb; ++k) {
-            const int64_t j = ro + k;
-            f32x4 z = *(const f32x4 *)(z4d4 + j * 256 + 4 * lane);
-            f32x4 h;
+        // all rows' z4 in flight at once, then their two dot products in one batched reduction
+        f32x4 z[MAX_K];
+        float red[16];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) h[q] = lrelu_ref(z[q]);
-            const float za = wave_sum(wa4[0] * h[0] + wa4[1] * h[1] + wa4[2] * h[2] + wa4[3] * h[3]) + bav;
-            const float dot = wave_sum(h[0] * df[0] + h[1] * df[1] + h[2] * df[2] + h[3] * df[3]);
+        for (int k = 0; k < MAX_K; ++k) {
+            z[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (k < nnb) z[k] = *(const f32x4 *)(z4d4 + (int64_t)(ro + k) * 256 + 4 * lane);
+        }
+        const float2 wwl = lane < nnb ? rw[ro + lane] : make_float2(0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < MAX_K; ++k) {
+            float pa = 0.f, pd = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float h = lrelu_ref(z[k][q]);
+                pa += wa4[q] * h;
+                pd += h * df[q];
+            }
+            red[k] = pa;
+            red[MAX_K + k] = pd;
+        }
+        wave_sum16(red, lane);
+        float gc = 0.f;
+#pragma unroll
+        for (int k = 0; k < MAX_K; ++k) {
+            if (k >= nnb) break;
+            const float za = lane_value(red[0], 4 * k) + bav;
+            const float dot = lane_value(red[0], 4 * (MAX_K + k));
             const float x = za - 1.f;
             const float al = softplus_ref(x), sg = x > 20.f ? 1.f : 1.f / (1.f + expf(-x));
-            const float2 ww = rw[j];
-            const float dza = ww.x * das * sg;
+            const float wk = lane_value(wwl.x, k), wnk = lane_value(wwl.y, k);
+            const float dza = wk * das * sg;
             const float dw = dot + al * das;
             f32x4 d;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float t = ww.x * df[q] + dza * wa4[q];
-                d[q] = z[q] > 0.f ? t : t * 0.01f;
+                const float h = lrelu_ref(z[k][q]);
+                const float t = wk * df[q] + dza * wa4[q];
+                d[q] = z[k][q] > 0.f ? t : t * 0.01f;
                 am = fmaxf(am, fabsf(d[q]));
-                gw[q] += dza * h[q];
+                gw[q] += dza * h;
             }
             gb += dza;
-            *(f32x4 *)(z4d4 + j * 256 + 4 * lane) = d;
-            if (lane == 0) {
-                const int pid = a.pidx[(int64_t)s * a.K + k];
-                atomicAdd(g_conf + pid, dw * ww.y);
-            }
+            *(f32x4 *)(z4d4 + (int64_t)(ro + k) * 256 + 4 * lane) = d;
+            if (lane == k) gc = dw * wnk;
         }
+        if (lane < nnb) atomicAdd(g_conf + a.pidx[(int64_t)s * a.K + lane], gc);
     }
     *(f32x4 *)&sh[wl][4 * lane] = gw;
     if (lane == 0) sh[wl][256] = gb;
@@ -675,6 +875,10 @@ __global__ __launch_bounds__(TPB) void k_row_head(RowArgs a, float *z4d4, const 
 // the point gradients of a row: d emb through [emb | PE(emb)] (networks.py:175-192) from block1.0's
 // input gradient dx0 [rows][224]; d colour, d dir from block3.0's extra-channel gradient dext
 // [rows][8] (d (dir - v) + v d <dir, v>)
+// tasks per row: 32 embedding channels, then colour (3) and dir (3); the item's rows x tasks are
+// one flat list over the wave's lanes
+constexpr int TAIL_TASKS = 38;
+
 __global__ __launch_bounds__(TPB) void k_row_tail(RowArgs a, const float *dx0, const float *dext, float *g_emb,
                                                   float *g_color, float *g_dir) {
     const int lane = threadIdx.x & 63;
@@ -684,28 +888,32 @@ __global__ __launch_bounds__(TPB) void k_row_tail(RowArgs a, const float *dx0, c
         const int s = a.work[it];
         const int nnb = a.samp_nnb[s], ro = a.row_off[s];
         const int ray = a.samp_ray[s];
-        for (int k = 0; k < nnb; ++k) {
+        const int ntask = nnb * TAIL_TASKS;
+        for (int t = lane; t < ntask; t += 64) {
+            const int k = t / TAIL_TASKS, c = t - k * TAIL_TASKS;
             const int64_t j = ro + k;
             const int pid = a.pidx[(int64_t)s * a.K + k];
-            if (lane < 32) {
+            if (c < 32) {
                 const float *g = dx0 + j * 224;
-                const float e = a.emb[(int64_t)pid * 32 + lane];
-                float de = g[lane];
+                const float e = a.emb[(int64_t)pid * 32 + c];
+                float de = g[c];
 #pragma unroll
                 for (int f = 0; f < 3; ++f) {
-                    const float sc = (float)(1 << f), x = e * sc;
-                    const int c = 32 + 2 * (3 * lane + f);
-                    de += g[c] * cosf(x) * sc - g[c + 1] * sinf(x) * sc;
+                    const float sc = (float)(1 << f);
+                    float sn, cs;
+                    sincos_acc(e * sc, sn, cs);
+                    const int col = 32 + 2 * (3 * c + f);
+                    de += g[col] * cs * sc - g[col + 1] * sn * sc;
                 }
-                atomicAdd(g_emb + (int64_t)pid * 32 + lane, de);
-            } else if (lane < 38) {
-                const int c = lane - 32;
+                atomicAdd(g_emb + (int64_t)pid * 32 + c, de);
+            } else {
+                const int u = c - 32;
                 const float *g = dext + j * 8;
-                if (c < 3) {
-                    atomicAdd(g_color + (int64_t)pid * 3 + c, g[c]);
+                if (u < 3) {
+                    atomicAdd(g_color + (int64_t)pid * 3 + u, g[u]);
                 } else {
-                    const float v = a.raydir[(int64_t)ray * 3 + c - 3];
-                    atomicAdd(g_dir + (int64_t)pid * 3 + c - 3, g[c] + g[6] * v);
+                    const float v = a.raydir[(int64_t)ray * 3 + u - 3];
+                    atomicAdd(g_dir + (int64_t)pid * 3 + u - 3, g[u] + g[6] * v);
                 }
             }
         }
@@ -735,8 +943,20 @@ __global__ __launch_bounds__(TPB) void k_reduce_partials(RedArgs r) {
     const int64_t e = t - r.start[q];
     const int m = (int)(e / s.N), c = (int)(e % s.N);
     const int64_t stride = (int64_t)s.M * s.N;
-    float v = 0.f;
-    for (int i = 0; i < s.splits; ++i) v += s.part[i * stride + e];
+    // four interleaved chains (fixed order: split i into chain i % 4, chains summed pairwise)
+    const float *p = s.part + e;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    int i = 0;
+    for (; i + 3 < s.splits; i += 4) {
+        v0 += p[i * stride];
+        v1 += p[(i + 1) * stride];
+        v2 += p[(i + 2) * stride];
+        v3 += p[(i + 3) * stride];
+    }
+    if (i < s.splits) v0 += p[i * stride];
+    if (i + 1 < s.splits) v1 += p[(i + 1) * stride];
+    if (i + 2 < s.splits) v2 += p[(i + 2) * stride];
+    const float v = (v0 + v1) + (v2 + v3);
     if (c < s.n_in) s.dst_w[(int64_t)m * s.ldw + c] += v;
     else if (c == s.bias_col) s.dst_b[m] += v;
 }
@@ -764,7 +984,7 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
         d.nrows = nrows; d.dyn = dyn; d.amax = o.amax; d.shift = o.shift;
         const bool al1 = ((uintptr_t)o.p & 15) == 0 && o.ld % 4 == 0;
         const bool al2 = !o.p2 || (((uintptr_t)o.p2 & 15) == 0 && o.ld2 % 4 == 0);
-        d.vec = !o.kmajor && al1 && al2;
+        d.vec = al1 && al2;
         return 0;
     };
     GemmK k{};
@@ -790,24 +1010,40 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
     hipStream_t st = as_stream(stream);
     if (g.mode == 0) {
         if (g.M == 0) return 0;
-        // column block: 128 wide unless 96 covers N with less padding
+        SGN_REQUIRE(g.K <= 288, "mode 0: K <= 288 (the weight block lives in LDS)");
+        SGN_REQUIRE(k.A.vec && g.a.ncols % 8 == 0 && g.a.ones_col < 0 && (g.a.csplit >= g.a.ncols || g.a.csplit % 8 == 0),
+                    "mode 0: operand a needs 16-B aligned rows (ld % 4 == 0), ncols % 8 == 0, no ones column");
+        // column block: 128 wide unless 96 covers N with less padding; one workgroup per CU
         const bool w96 = ((g.N + 95) / 96) * 96 < ((g.N + 127) / 128) * 128;
-        const int BN = w96 ? 96 : 128, BM = 128;
+        const int BN = w96 ? 96 : 128;
         const int nb = (g.N + BN - 1) / BN;
-        const int tiles = (g.M + BM - 1) / BM;
-        int gy = 1024 / nb;
+        const int tiles = (g.M + RT_ROWS - 1) / RT_ROWS;
+        int gy = 256 / nb;
         gy = gy < 1 ? 1 : gy > tiles ? tiles : gy;
-        if (w96) hipLaunchKernelGGL((k_x3gemm<1, 3, 4, 1, false>), dim3(nb, gy), dim3(TPB), 0, st, k);
-        else hipLaunchKernelGGL((k_x3gemm<2, 2, 2, 2, false>), dim3(nb, gy), dim3(TPB), 0, st, k);
+        const int ks = (g.K + 15) / 16;
+        const dim3 grid(nb, gy);
+        if (ks <= 8) {
+            if (w96) hipLaunchKernelGGL((k_x3rows<8, 3>), grid, dim3(TPB), 0, st, k);
+            else hipLaunchKernelGGL((k_x3rows<8, 4>), grid, dim3(TPB), 0, st, k);
+        } else if (ks <= 16) {
+            if (w96) hipLaunchKernelGGL((k_x3rows<16, 3>), grid, dim3(TPB), 0, st, k);
+            else hipLaunchKernelGGL((k_x3rows<16, 4>), grid, dim3(TPB), 0, st, k);
+        } else {
+            if (w96) hipLaunchKernelGGL((k_x3rows<18, 3>), grid, dim3(TPB), 0, st, k);
+            else hipLaunchKernelGGL((k_x3rows<18, 4>), grid, dim3(TPB), 0, st, k);
+        }
     } else {
+        // M block 256 (or 128 for M <= 128); N block 96, 160 (M <= 128: the colour layers' 129
+        // columns in one block) or 32 (narrow N)
         const int BM = g.M > 128 ? 256 : 128;
-        const int BN = g.N <= 32 ? 32 : 96;
+        const int BN = g.N <= 32 ? 32 : (BM == 128 && g.N <= 160) ? 160 : 96;
         const int nbm = (g.M + BM - 1) / BM, nbn = (g.N + BN - 1) / BN;
         const dim3 grid(nbm * nbn, g.splits);
-        if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3gemm<2, 3, 4, 1, true>), grid, dim3(TPB), 0, st, k);
-        else if (BM == 256) hipLaunchKernelGGL((k_x3gemm<2, 1, 4, 1, true>), grid, dim3(TPB), 0, st, k);
-        else if (BN == 96) hipLaunchKernelGGL((k_x3gemm<1, 3, 4, 1, true>), grid, dim3(TPB), 0, st, k);
-        else hipLaunchKernelGGL((k_x3gemm<1, 1, 4, 1, true>), grid, dim3(TPB), 0, st, k);
+        if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3tn<2, 3>), grid, dim3(TPB), 0, st, k);
+        else if (BM == 256) hipLaunchKernelGGL((k_x3tn<2, 1>), grid, dim3(TPB), 0, st, k);
+        else if (BN == 160) hipLaunchKernelGGL((k_x3tn<1, 5>), grid, dim3(TPB), 0, st, k);
+        else if (BN == 96) hipLaunchKernelGGL((k_x3tn<1, 3>), grid, dim3(TPB), 0, st, k);
+        else hipLaunchKernelGGL((k_x3tn<1, 1>), grid, dim3(TPB), 0, st, k);
     }
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
@@ -856,8 +1092,22 @@ int sgn_train_row_inputs(const sgn_point_tables *pt, const sgn_query_out *q, int
     SGN_REQUIRE(((uintptr_t)d_x0 & 15) == 0 && ((uintptr_t)d_rw & 7) == 0, "aligned x0 / rw required");
     const RowArgs a = row_args(pt, q, K, d_row_off, d_counts);
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(k_row_inputs, dim3(ROW_GRID), dim3(TPB), 0, st, a, d_x0, d_ext, (float2 *)d_rw);
-    hipLaunchKernelGGL(k_colour_in, dim3(ROW_GRID), dim3(TPB), 0, st, a, d_vpe);
+    hipLaunchKernelGGL(k_row_inputs, dim3(ROW_GRID), dim3(TPB), 0, st, a, d_x0, d_ext, (float2 *)d_rw, d_vpe);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_train_row_gather(const sgn_query_out *q, int32_t K, const int32_t *d_row_off, const int32_t *d_counts,
+                         const float *d_src, int32_t dim, float *d_dst, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::tx;
+    SGN_REQUIRE(q && d_row_off && d_counts && d_src && d_dst, "null argument");
+    SGN_REQUIRE(K >= 1 && K <= 8, "K = 1 .. 8");
+    SGN_REQUIRE(dim > 0 && dim % 4 == 0 && ((uintptr_t)d_src & 15) == 0 && ((uintptr_t)d_dst & 15) == 0,
+                "dim % 4 == 0 and 16-B aligned tables");
+    RowArgs a{};
+    a.work = q->work; a.samp_nnb = q->samp_nnb; a.pidx = q->pidx; a.row_off = d_row_off; a.tl = d_counts; a.K = K;
+    hipLaunchKernelGGL(k_row_gather, dim3(ROW_GRID), dim3(TPB), 0, as_stream(stream), a, d_src, dim, d_dst);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

@@ -2,7 +2,8 @@
 //
 // x = hi + lo with hi = fp16(x), lo = fp16(x - hi); a product w x is then carried as
 // w_hi x_hi + w_hi x_lo + w_lo x_hi in fp32 MFMA accumulators (22 significant bits per factor,
-// the dropped w_lo x_lo term <= 2^-22 |w x|).  Included inside sgn::{anonymous}.
+// the dropped w_lo x_lo term <= 2^-22 |w x|).  Also the accurate sin / cos of the positional
+// encodings (networks.py:175-192 uses torch.sin / torch.cos in fp32).
 #pragma once
 #include "agg_device.h"
 
@@ -29,6 +30,30 @@ __device__ __forceinline__ X3Pair split8_scaled(const float (&t)[8], float scale
         lo[q] = l;
     }
     return X3Pair{__builtin_bit_cast(h8, hi), __builtin_bit_cast(h8, lo)};
+}
+
+// sin and cos of x (fp32, within ~1 ulp): quadrant q = rint(x 2/pi), r = x - q pi/2 in double
+// (exact to far below fp32 resolution for |x| < 2^20), cephes' minimax polynomials on
+// [-pi/4, pi/4]; |x| >= 2^20 (never met by the encodings' arguments) takes the library sincosf.
+__device__ __forceinline__ void sincos_acc_fast(float x, float &s, float &c) {  // |x| < 2^20
+    const float qf = __builtin_rintf(x * 0.63661977236758134f);
+    const float r = (float)__builtin_fma((double)qf, -1.5707963267948966, (double)x);
+    const float z = r * r;
+    const float sp = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z,
+                                                   -1.6666654611e-1f), z * r, r);
+    const float cp = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                                                   4.166664568298827e-2f), z * z, __builtin_fmaf(-0.5f, z, 1.f));
+    const int q = (int)qf;
+    const float s0 = (q & 1) ? cp : sp, c0 = (q & 1) ? sp : cp;
+    s = (q & 2) ? -s0 : s0;
+    c = ((q + 1) & 2) ? -c0 : c0;
+}
+__device__ __forceinline__ void sincos_acc(float x, float &s, float &c) {
+    if (__builtin_expect(__builtin_fabsf(x) >= 1048576.f, 0)) {
+        sincosf(x, &s, &c);
+        return;
+    }
+    sincos_acc_fast(x, s, c);
 }
 
 }  // namespace

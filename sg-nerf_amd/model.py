@@ -156,9 +156,9 @@ class HipPointsVolumetricModel:
             # built by setup() / the first optimize_parameters once it is there
             self.trainer = None
             return
-        # the step at the model's arithmetic: precision "f32" (the reference's) trains the base viewmlp
-        # through the fp32-faithful forward and an fp32 backward; the SG variant trains at fp16 operands
-        prec = "f16" if (self.opts.precision == "f16" or tuple(self.opts.bpnet_variant) != (0, 0)) else "f32"
+        # the step at the model's arithmetic: precision "f32" (the reference's) trains through the
+        # fp32-faithful forward and the fp32 backward (base viewmlp and SG's block2_bpnet alike)
+        prec = "f16" if self.opts.precision == "f16" else "f32"
         self.trainer = HipTrainer(params, self.net_ray_marching.renderer.mlp_state,
                                   dataclasses.replace(self.opts, is_train=1), self.device,
                                   lr=g("lr", 5e-4), plr=g("plr", 2e-3), lr_decay_exp=g("lr_decay_exp", 0.1),

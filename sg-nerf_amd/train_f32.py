@@ -9,14 +9,15 @@ as one captured graph:
 
   sgn_train_lists            deterministic work list + compact row offsets (prefix sums)
   sgn_aggregate_train_fwd_f32  k_pair_slots + k_rows16 (save mode): alpha_s, f_s, z1 / z2 / z3 rows
+                             (SG: _sg, + block2_bpnet.0's zb)
   sgn_train_row_inputs       x0 = [emb | PE(emb) | PE(dists) | 1], extra channels, blend weights,
-                             PE(viewdir)
+                             PE(viewdir); SG: sgn_train_row_gather, the rows' BPNet embedding
   colour forward             3 x sgn_x3_gemm (x W^T + b, LeakyReLU) + sgn_train_colour_head (rgb)
   sgn_loss_train             ray_dist + ray_march + losses and d feat, d conf (zero-one)
   colour backward            sgn_train_colour_head_bwd, 3 x dy W (masked), 3 x dy^T x (split-K)
   row backward               z4 = LReLU(z3) W3^T + b3; sgn_train_row_head (alpha, K-blend, delta4,
-                             d conf); 4 x delta W (masked); sgn_train_row_tail (d emb / colour / dir);
-                             4 x delta^T x (split-K)
+                             d conf); 4 x delta W (masked; SG 5); sgn_train_row_tail (d emb /
+                             colour / dir); 4 x delta^T x (split-K; SG 5)
   sgn_reduce_partials        every weight / bias gradient into the flat gradient, fixed order
 
 Rows r are the valid (sample, neighbour) pairs, sample-major (sample s owns rows
@@ -28,9 +29,10 @@ import torch
 
 from . import _lib
 
-# split-K partials of the weight-gradient GEMMs (rows / items cut into this many 32-aligned runs)
-SPLITS_ROWS = 128
-SPLITS_ITEMS = 64
+# split-K partials of the weight-gradient GEMMs (rows / items cut into this many 32-aligned runs;
+# 84 x 3 column blocks = one workgroup per CU for the row layers)
+SPLITS_ROWS = 84
+SPLITS_ITEMS = 128
 
 
 def _addr(t, elem_off=0):
@@ -74,12 +76,14 @@ class F32Step:
     workspace.  `run` issues the step's launches on the current stream."""
 
     # amax words (max |x| of a delta tensor, written by its producer, read by its consumers)
-    A_DY3, A_DY2, A_DY1, A_D4, A_D3, A_D2, A_D1 = range(7)
+    A_DY3, A_DY2, A_DY1, A_D4, A_D3, A_D2, A_D1, A_DB = range(8)
 
     def __init__(self, trainer, q, R):
         L = _lib.lib()
         o = trainer.opts
         self.trainer, self.R, self.K = trainer, R, o.K
+        # SG-NeRF's block2_bpnet.0 between block1.2 and block3.0 (point_aggregators.py:345-354)
+        self.sg, self.D = trainer.sg, trainer.variant[1]
         dev = trainer.device
         self.cap = cap = max(R * o.SR, 1)
         self.rows_cap = rows = cap * o.K
@@ -92,6 +96,10 @@ class F32Step:
         self.lists_ws = torch.empty(int(L.sgn_train_lists_workspace_bytes(cap)), dtype=torch.uint8, device=dev)
         self.feat = torch.zeros(cap, 4, **f32)
         self.z = [torch.empty(rows, 256, **f32) for _ in range(4)]     # z1, z2, z3, z4 -> delta4
+        if self.sg:   # block2_bpnet.0's pre-activation and delta, the rows' BPNet embedding
+            self.zb = torch.empty(rows, 256, **f32)
+            self.db = torch.empty(rows, 256, **f32)
+            self.bprow = torch.empty(rows, self.D, **f32) if self.D else None
         self.ws32 = torch.empty(int(L.sgn_aggregate_workspace_bytes_f32(cap)), dtype=torch.uint8, device=dev)
         self.fs = self.ws32[:cap * 256 * 4].view(torch.float32).view(cap, 256)   # k_rows16's blended features
         self.x0 = torch.empty(rows, 288, **f32)
@@ -110,7 +118,8 @@ class F32Step:
         self.full = torch.empty(max(R, 1), 3, **f32)
         self.mask = torch.empty(max(R, 1), dtype=torch.int8, device=dev)
         self.loss_ws = torch.empty(max(int(L.sgn_loss_workspace_bytes(R, o.SR)), 16), dtype=torch.uint8, device=dev)
-        self.part_rows = [torch.empty(SPLITS_ROWS, 256, n, **f32) for n in (257, 264, 257, 285)]
+        self.part_rows = [torch.empty(SPLITS_ROWS, 256, n, **f32)
+                          for n in (257, 264, 257, 285) + ((257 + self.D,) if self.sg else ())]
         self.part_col = [torch.empty(SPLITS_ITEMS, 128, n, **f32) for n in (129, 129, 281)]
         self.part_c6 = torch.empty(int(L.sgn_train_head_partial_floats(0)), **f32)
         self.part_a = torch.empty(int(L.sgn_train_head_partial_floats(1)), **f32)
@@ -186,9 +195,19 @@ class F32Step:
         G.append(("d3", _rows_gemm(_operand(z4, 256, 256, 0, amax=amax[self.A_D4]), _operand(w, i_, i_, 1, shift=S("block3.2")),
                                    rc, 256, 256, n_rows, d3, 256, mask=z3, ldm=256, amax_out=amax[self.A_D3])))
         w, o_, i_ = W("block3.0")
-        G.append(("d2", _rows_gemm(_operand(d3, 256, 256, 0, amax=amax[self.A_D3]), _operand(w, i_, i_, 1, shift=S("block3.0")),
-                                   rc, 263, 256, n_rows, d2, 256, mask=z2, ldm=256, out_cols=256,
-                                   out2=_addr(self.dext), ldo2=8, amax_out=amax[self.A_D2])))
+        if self.sg:   # block3.0's input is block2_bpnet.0's output: its delta, then block1.2's
+            db, zb = _addr(self.db), _addr(self.zb)
+            G.append(("db", _rows_gemm(_operand(d3, 256, 256, 0, amax=amax[self.A_D3]),
+                                       _operand(w, i_, i_, 1, shift=S("block3.0")), rc, 263, 256, n_rows, db, 256, mask=zb,
+                                       ldm=256, out_cols=256, out2=_addr(self.dext), ldo2=8, amax_out=amax[self.A_DB])))
+            w, o_, i_ = W("block2_bpnet.0")
+            G.append(("d2", _rows_gemm(_operand(db, 256, 256, 0, amax=amax[self.A_DB]),
+                                       _operand(w, i_, 256, 1, shift=S("block2_bpnet.0")), rc, 256, 256, n_rows, d2, 256,
+                                       mask=z2, ldm=256, amax_out=amax[self.A_D2])))
+        else:
+            G.append(("d2", _rows_gemm(_operand(d3, 256, 256, 0, amax=amax[self.A_D3]),
+                                       _operand(w, i_, i_, 1, shift=S("block3.0")), rc, 263, 256, n_rows, d2, 256, mask=z2,
+                                       ldm=256, out_cols=256, out2=_addr(self.dext), ldo2=8, amax_out=amax[self.A_D2])))
         w, o_, i_ = W("block1.2")
         G.append(("d1", _rows_gemm(_operand(d2, 256, 256, 0, amax=amax[self.A_D2]), _operand(w, i_, i_, 1, shift=S("block1.2")),
                                    rc, 256, 256, n_rows, d1, 256, mask=z1, ldm=256, amax_out=amax[self.A_D1])))
@@ -202,12 +221,18 @@ class F32Step:
             _splitk_gemm(_operand(z4, 256, 256, 1, amax=amax[self.A_D4]), _operand(z3, 256, 256, 1, ones_col=256, act=1),
                          256, 257, rc, n_rows, _addr(pr[0]), SPLITS_ROWS),
             _splitk_gemm(_operand(d3, 256, 256, 1, amax=amax[self.A_D3]),
-                         _operand(z2, 256, 264, 1, p2=_addr(self.ext), ld2=8, csplit=256, act=1), 256, 264, rc, n_rows,
-                         _addr(pr[1]), SPLITS_ROWS),
+                         _operand(_addr(self.zb) if self.sg else z2, 256, 264, 1, p2=_addr(self.ext), ld2=8, csplit=256,
+                                  act=1), 256, 264, rc, n_rows, _addr(pr[1]), SPLITS_ROWS),
             _splitk_gemm(_operand(d2, 256, 256, 1, amax=amax[self.A_D2]), _operand(z1, 256, 256, 1, ones_col=256, act=1),
                          256, 257, rc, n_rows, _addr(pr[2]), SPLITS_ROWS),
             _splitk_gemm(_operand(d1, 256, 256, 1, amax=amax[self.A_D1]), _operand(_addr(self.x0), 288, 285, 1),
                          256, 285, rc, n_rows, _addr(pr[3]), SPLITS_ROWS)]
+        if self.sg:   # block2_bpnet.0: delta_b^T [LReLU(z2) | BPNet embedding | 1]
+            D = self.D
+            xb = (_operand(z2, 256, 256 + D, 1, p2=_addr(self.bprow), ld2=D, csplit=256, ones_col=256 + D, act=1) if D
+                  else _operand(z2, 256, 256, 1, ones_col=256, act=1))
+            self.g_row_dw.append(_splitk_gemm(_operand(_addr(self.db), 256, 256, 1, amax=amax[self.A_DB]), xb, 256, 257 + D,
+                                              rc, n_rows, _addr(pr[4]), SPLITS_ROWS))
         # ---- partials -> flat gradient ----------------------------------------------------------
         segs = []
 
@@ -227,6 +252,8 @@ class F32Step:
         seg(_addr(pr[1]), SPLITS_ROWS, 256, 264, "block3.0", 263, 263)
         seg(_addr(pr[2]), SPLITS_ROWS, 256, 257, "block1.2", 256, 256)
         seg(_addr(pr[3]), SPLITS_ROWS, 256, 285, "block1.0", 284, 284)
+        if self.sg:
+            seg(_addr(pr[4]), SPLITS_ROWS, 256, 257 + self.D, "block2_bpnet.0", 256 + self.D, 256 + self.D)
         self.segs = (_lib.PartialSegment * len(segs))(*segs)
         self.n_seg = len(segs)
         self.w6, self.b6 = W("color_branch.6")[0], Bv("color_branch.6")
@@ -251,11 +278,20 @@ class F32Step:
         self.amax.zero_()
         ck(L.sgn_train_lists(p(self.q.counters), p(self.q.samp_nnb), cap, p(self.q.work), p(self.row_off), p(self.feat),
                              p(self.counts), p(self.lists_ws), st), "sgn_train_lists")
-        ck(L.sgn_aggregate_train_fwd_f32(p(proj), ctypes.byref(pt), ctypes.byref(qo), cap, K, p(blob), p(self.feat),
-                                         p(self.z[0]), p(self.z[1]), p(self.z[2]), p(self.row_off), p(self.ws32),
-                                         self.ws32.numel(), st), "sgn_aggregate_train_fwd_f32")
+        if self.sg:
+            ck(L.sgn_aggregate_train_fwd_f32_sg(1, self.D, p(tr.bpnet32) if self.D else None, p(proj), ctypes.byref(pt),
+                                                ctypes.byref(qo), cap, K, p(blob), p(self.feat), p(self.z[0]),
+                                                p(self.z[1]), p(self.zb), p(self.z[2]), p(self.row_off), p(self.ws32),
+                                                self.ws32.numel(), st), "sgn_aggregate_train_fwd_f32_sg")
+        else:
+            ck(L.sgn_aggregate_train_fwd_f32(p(proj), ctypes.byref(pt), ctypes.byref(qo), cap, K, p(blob), p(self.feat),
+                                             p(self.z[0]), p(self.z[1]), p(self.z[2]), p(self.row_off), p(self.ws32),
+                                             self.ws32.numel(), st), "sgn_aggregate_train_fwd_f32")
         ck(L.sgn_train_row_inputs(ctypes.byref(pt), ctypes.byref(qo), K, p(self.row_off), p(self.counts), p(self.x0),
                                   p(self.ext), p(self.rw), p(self.vpe), st), "sgn_train_row_inputs")
+        if self.D:
+            ck(L.sgn_train_row_gather(ctypes.byref(qo), K, p(self.row_off), p(self.counts), p(tr.bpnet32), self.D,
+                                      p(self.bprow), st), "sgn_train_row_gather")
         for _, gs in self.g_colour_fwd:
             gemm(gs)
         ck(L.sgn_train_colour_head(ctypes.byref(qo), p(self.counts), p(self.h[2]), self.w6, self.b6, p(self.feat), st),

@@ -370,21 +370,19 @@ class HipTrainer:
         """bpnet: the SG variant's BPNet point embedding [N, 96] (fp32, detached: it is an input,
         neural_points.py:662), needed when opts select block2_bpnet with predict_semantic = 1.
         precision "f16": the fp16-operand HIP forward + backward (k_agg_rows save mode, k_agg_bwd);
-        "f32" (base viewmlp): the reference's fp32 arithmetic -- the HIP fp32-faithful row kernel
-        (k_rows16, 3 fp16 MFMA products per fp32 product) saves the row MLP's pre-activations and the
-        backward runs in fp32 through them (train.aggregate(saved=...), fp32 GEMMs)."""
+        "f32" (base viewmlp and SG): the reference's fp32 arithmetic -- the HIP fp32-faithful row
+        kernel (k_rows16, 3 fp16 MFMA products per fp32 product) saves the row MLP's pre-activations
+        and the backward runs through them on the same split-fp16 GEMMs (train_f32.F32Step)."""
         self.device = torch.device(device)
         self.opts = opts.check_supported()
         self.variant = tuple(opts.bpnet_variant)
         self.sg = self.variant != (0, 0)
         if precision not in ("f16", "f32"):
             raise ValueError("precision: 'f16' or 'f32'")
-        if precision == "f32" and self.sg:
-            raise NotImplementedError("f32 training covers the base viewmlp (the SG variant trains at f16)")
         self.precision = precision
         self.points = points
         self.mlp = FlatMLP(mlp_state, self.device, layers_for(*self.variant))
-        self.bpnet16 = None
+        self.bpnet16 = self.bpnet32 = None
         if self.variant[1]:
             if bpnet is None:
                 raise ValueError("block2_bpnet with predict_semantic = 1 needs the BPNet point embedding")
@@ -392,6 +390,8 @@ class HipTrainer:
             self.bpnet16 = torch.empty(e.shape, dtype=torch.float16, device=self.device)
             _lib.check(_lib.lib().sgn_bpnet_pack(_lib.ptr(e), e.shape[0], e.shape[1], _lib.ptr(self.bpnet16),
                                                  _lib.stream_handle()), "sgn_bpnet_pack")
+            if precision == "f32":   # the fp32 kernels read the embedding as it is
+                self.bpnet32 = e
         self.point_params = [points.points_embeding, points.points_color, points.points_dir, points.points_conf]
         # the reference's two Adam groups (mvs_points_volumetric_model.py:100-108); fused: one
         # kernel per group for the dense 47 M-element point update instead of the foreach chain
@@ -628,6 +628,8 @@ class HipTrainer:
         host sync on one GPU; under DP one for the touched-row counts).  SGN_F32_TORCH=1: the earlier
         step (HIP forward, torch fp32 autograd backward), kept for A/B."""
         if os.environ.get("SGN_F32_TORCH", "0") == "1":
+            if self.sg:
+                raise NotImplementedError("SGN_F32_TORCH=1 (the torch-autograd A/B step) covers the base viewmlp")
             return self._backward_f32_torch(campos, rot, raydir, near, far, gt, labels)
         from .train_f32 import F32Step
         o = self.opts

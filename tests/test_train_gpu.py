@@ -690,8 +690,75 @@ def test_hip_sg_training_gradients_match_oracle(dim, seed):
         worst[k] = _rel(v.cpu().reshape(ref.shape), ref)
     print(f"SG dim {dim} relative L2 gradient errors:", {k: f"{v:.2e}" for k, v in worst.items()})
     assert "block2_bpnet.0.weight" in worst
-    # the SG variant trains at fp16 operands (HipTrainer refuses precision "f32" for it): the f16 bars
+    # precision "f16" (the default): the f16 bars; "f32": test_hip_sg_f32_training_gradients_match_fp32_autograd
     bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("dim,seed", [(96, 3), (0, 5)])
+def test_hip_sg_f32_training_gradients_match_fp32_autograd(dim, seed):
+    """SG-NeRF's block2_bpnet at precision "f32" (train_f32.F32Step with block2_bpnet.0 between
+    block1.2 and block3.0): one backward against fp32 autograd through oracle/agg_ref.py's SG
+    aggregator, on the GPU, over the very samples the HIP query produced (last_query): the
+    colour, the loss and every gradient (block2_bpnet.0 and the points included) within
+    GRAD_TOL_F32."""
+    import math
+
+    import agg_ref
+    from test_train_cpu import O as O_BASE
+    pc, view, _, mlp, gt = _setup(seed=seed)
+    n = pc.xyz.shape[0]
+    g = torch.Generator().manual_seed(11)
+    bound = math.sqrt(6.0 / (256 + dim + 256)) * 0.5
+    mlp = dict(mlp)
+    mlp["block2_bpnet.0.weight"] = (torch.rand(256, 256 + dim, generator=g) * 2 - 1) * bound
+    mlp["block2_bpnet.0.bias"] = torch.randn(256, generator=g) * 0.01
+    bp = (torch.rand(n, dim, generator=g) - 0.5) if dim else None
+    o = dataclasses_replace(O_BASE, shading_feature_mlp_layer2_bpnet=1, predict_semantic=1 if dim else 0,
+                            semantic_guidance=1 if dim else 0)
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    tr = HipTrainer(points, mlp, o, DEV, bpnet=bp, precision="f32")
+    R = view.raydir.shape[0]
+    labels = (torch.zeros(n, dtype=torch.int32), torch.ones(R, dtype=torch.int32), 10) if dim else None
+    parts, full, mask = tr.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV), labels)
+    torch.cuda.synchronize()
+    hg = grads_named(tr)
+    qd = {k: v.long() if v.dtype == torch.int32 else v for k, v in tr.last_query.items()}
+    pts = {k: torch.from_numpy(getattr(pc, k)).to(DEV).requires_grad_(k != "xyz")
+           for k in ("xyz", "embedding", "color", "dir", "conf")}
+    if dim:
+        pts["bpnet"] = bp.to(DEV)
+    m = {k: v.to(DEV).requires_grad_(True) for k, v in mlp.items()}
+    campos, rot, raydir = d(view.campos), d(view.camrotc2w), d(view.raydir)
+    feat, _ = agg_ref.aggregate(pts, m, campos, rot, raydir, qd["samp_ray"], qd["samp_locw"], qd["pidx"])
+    nnb = (qd["pidx"] >= 0).sum(-1)
+    fd, vd, ld = agg_ref.densify(R, O_BASE.SR, qd["ray_ns"], qd["samp_ray"], qd["samp_locw"], feat, nnb)
+    color, _, _ = agg_ref.composite(fd, vd, ld, rot, campos)
+    ray_mask = vd.any(-1)
+    gtd = gt.to(DEV)
+    l_col = torch.mean((color[ray_mask] - gtd[ray_mask]) ** 2)
+    S = qd["samp_ray"].shape[0]
+    slot = torch.arange(S, device=DEV) - qd["ray_soff"][qd["samp_ray"]]
+    pd = torch.full((R, O_BASE.SR, O_BASE.K), -1, dtype=torch.long, device=DEV)
+    pd[qd["samp_ray"], slot] = qd["pidx"]
+    cd = pts["conf"][torch.clamp(pd[ray_mask], min=0).reshape(-1), 0]
+    val = torch.clamp(torch.clamp(cd, 1e-4, 1.0), 1e-3, 1 - 1e-3)
+    l_zo = torch.mean(torch.log(val) + torch.log(1 - val))
+    total = l_col + 3e-6 + 1e-4 * l_zo
+    total.backward()
+    torch.cuda.synchronize()
+    assert torch.equal(mask, ray_mask)
+    assert _rel(full[ray_mask], color[ray_mask].detach()) <= GRAD_TOL_F32
+    assert abs(float(parts["total"]) - float(total)) <= GRAD_TOL_F32 * abs(float(total))
+    names = {"points_embeding": "embedding", "points_color": "color", "points_dir": "dir", "points_conf": "conf"}
+    worst = {}
+    for k, v in hg.items():
+        ref = pts[names[k]].grad if k in names else m[k].grad
+        worst[k] = _rel(v.reshape(ref.shape), ref)
+    print(f"SG f32 dim {dim} relative L2 gradient errors (same query):", {k: f"{v:.2e}" for k, v in worst.items()})
+    assert "block2_bpnet.0.weight" in worst
+    bad = {k: v for k, v in worst.items() if v > GRAD_TOL_F32}
     assert not bad, bad
 
 
@@ -731,7 +798,7 @@ def test_model_plugin_sg_training(tmp_path):
     m.set_input(inputs)
     before = m.test()["coarse_raycolor"].clone()
     tr = HipTrainer(PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV), mlp,
-                    dataclasses.replace(O, is_train=1, **sg), DEV, bpnet=bp)
+                    dataclasses.replace(O, is_train=1, **sg), DEV, bpnet=bp, precision=m.trainer.precision)
     torch.manual_seed(11)
     parts_ref, _, _ = tr.step(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV),
                               labels=(lab, torch.zeros(R, dtype=torch.int32), None))
