@@ -88,7 +88,7 @@ def aggregate(points, mlp, campos, rot, raydir, samp_ray, samp_locw, pidx):
     conf_coef = torch.clamp(conf[..., 0], 0.0001, 1)
     weight = weight * conf_coef
     ray_valid = torch.any(mask, dim=-1)
-    v = raydir.reshape(-1, 3)[samp_ray.long()] @ torch.eye(3)
+    v = raydir.reshape(-1, 3)[samp_ray.long()] @ torch.eye(3, device=raydir.device)
     vpe = positional_encoding(v, 4, ori=True)
     ori_v, vpe = vpe[..., :3], vpe[..., 3:]
     # viewmlp :594-653 on the valid (sample, neighbour) rows
@@ -111,10 +111,10 @@ def aggregate(points, mlp, campos, rot, raydir, samp_ray, samp_locw, pidx):
     f = _lrelu(_lin(mlp, "block3.2", _lrelu(_lin(mlp, "block3.0", f))))
     # alpha + K-blend :743-770
     alpha = F.softplus(_lin(mlp, "alpha_branch.0", f) - 1)
-    ah = torch.zeros(S * K, 1)
+    ah = torch.zeros(S * K, 1, device=pidx.device)
     ah[m] = alpha
     alpha = torch.sum(ah.view(S, K, 1) * weight[..., None], dim=-2)[ray_valid]
-    fh = torch.zeros(S * K, f.shape[-1])
+    fh = torch.zeros(S * K, f.shape[-1], device=pidx.device)
     fh[m] = f
     fs = torch.sum(fh.view(S, K, -1) * weight[..., None], dim=-2)[ray_valid]
     c = torch.cat([fs, vpe[ray_valid]], dim=-1)
@@ -122,7 +122,7 @@ def aggregate(points, mlp, campos, rot, raydir, samp_ray, samp_locw, pidx):
     c = _lrelu(_lin(mlp, "color_branch.2", c))
     c = _lrelu(_lin(mlp, "color_branch.4", c))
     c = torch.sigmoid(_lin(mlp, "color_branch.6", c)) * (1 + 2 * 0.001) - 0.001
-    out = torch.zeros(S, 4)
+    out = torch.zeros(S, 4, device=pidx.device)
     out[ray_valid] = torch.cat([alpha, c], dim=-1)
     return out, weight
 
@@ -135,7 +135,7 @@ def composite(feat_dense, valid_dense, loc_w_dense, rot, campos, vsize_z=0.008, 
     loc = w2pers_samples(loc_w_dense[None], rot.reshape(1, 3, 3), campos.reshape(1, 3))
     ray_dist = torch.cummax(loc[..., 2], dim=-1)[0]
     ray_dist = torch.cat([ray_dist[..., 1:] - ray_dist[..., :-1],
-                          torch.full((ray_dist.shape[0], ray_dist.shape[1], 1), vsize_z)], dim=-1)
+                          torch.full((ray_dist.shape[0], ray_dist.shape[1], 1), vsize_z, device=loc.device)], dim=-1)
     m = ray_dist < 1e-8
     if raydist_mode_unit > 0:
         m = torch.logical_or(m, ray_dist > 2 * vsize_z)
@@ -148,9 +148,9 @@ def composite(feat_dense, valid_dense, loc_w_dense, rot, campos, vsize_z=0.008, 
     opacity = 1 - torch.exp(-sigma * ray_dist)
     acc = torch.cumprod(1. - opacity + 1e-10, dim=-1)
     bg_t = acc[:, :, [-1]]
-    acc = torch.cat([torch.ones(opacity.shape[0:2] + (1,)), acc[:, :, :-1]], dim=-1)
+    acc = torch.cat([torch.ones(opacity.shape[0:2] + (1,), device=acc.device), acc[:, :, :-1]], dim=-1)
     w = (opacity * acc)[..., None]
-    color = torch.sum(point_color * w, dim=-2) + torch.as_tensor(bg, dtype=torch.float32).view(1, 1, 3) * bg_t
+    color = torch.sum(point_color * w, dim=-2) + torch.as_tensor(bg, dtype=torch.float32, device=bg_t.device).view(1, 1, 3) * bg_t
     return color[0], opacity[0], bg_t[0, :, 0]
 
 
@@ -158,10 +158,11 @@ def densify(R, SR, ray_ns, samp_ray, samp_locw, feat, nnb):
     """sample-major -> dense [R, SR] (feat, valid, loc_w)."""
     S = samp_ray.shape[0]
     soff = torch.cumsum(ray_ns, 0) - ray_ns
-    slot = torch.arange(S) - soff[samp_ray.long()]
-    fd = torch.zeros(R, SR, 4)
-    vd = torch.zeros(R, SR, dtype=torch.bool)
-    ld = torch.zeros(R, SR, 3)
+    dev = feat.device
+    slot = torch.arange(S, device=dev) - soff[samp_ray.long()]
+    fd = torch.zeros(R, SR, 4, device=dev)
+    vd = torch.zeros(R, SR, dtype=torch.bool, device=dev)
+    ld = torch.zeros(R, SR, 3, device=dev)
     fd[samp_ray.long(), slot] = feat
     vd[samp_ray.long(), slot] = nnb > 0
     ld[samp_ray.long(), slot] = samp_locw

@@ -261,19 +261,27 @@ __device__ __forceinline__ f32x4 mfma16(h8 a, h8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// One layer, k-outer over all 16 output tiles: acc[t] += W[t] in(k), three MFMAs per
-// (k-step, tile), next chunk's LDS-DMA pieces spread over the first pairs.  TRANS: activations
-// are the A operand (acc[t] holds D[row 4g+i][unit 16t + (l & 15)]).
+// the B fragments of one k-step for NS row sets of 16 rows each
+template <int NS>
+struct X3S {
+    X3B b[NS];
+};
+
+// One layer, k-outer over all output tiles of pass P: acc[s][AOFF + t] += W[t] in(k).b[s], three MFMAs
+// per (k-step, tile, row set), next chunk's LDS-DMA pieces spread over the first pairs.  Each weight
+// fragment pair read from LDS feeds 3 NS MFMAs.  TRANS: activations are the A operand (acc[s][t]
+// holds D[row 4g+i][unit 16t + (l & 15)]).
 // mid(integral_constant F) runs after pair F's MFMAs of every chunk (F counted over the layer: k-step
 // K, tile t -> F = K TP + t), so per-pair VALU work of another stage can ride between the MFMAs.
-template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, class SlotT, class InFn,
-          class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>
-__device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &slot, int w, int lane, int lz,
-                                            f32x4 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{},
-                                            EndFn &&end = EndFn{}, MidFn &&mid = MidFn{}) {
+template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, int AOFF = 0, int NS, int NA,
+          class SlotT, class InFn, class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>
+__device__ __forceinline__ void run_layer_ns(const WBlob &wb, char *lds, SlotT &slot, int w, int lane, int lz,
+                                             f32x4 (&acc)[NS][NA], InFn &&in, PostFn &&post = PostFn{},
+                                             EndFn &&end = EndFn{}, MidFn &&mid = MidFn{}) {
     constexpr XL ly = Net::L[L];
     constexpr int TP = ly.tp;
     static_assert((TP == 16 || TP == 8) && P < ly.np, "passes of 16 or 8 output tiles");
+    static_assert(AOFF + TP <= NA, "accumulator view");
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
         constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
@@ -295,7 +303,7 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &s
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
         static_for<nk(ly, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
-            const X3B B = in(std::integral_constant<int, C * ly.kc + KK>{});
+            const X3S<NS> B = in(std::integral_constant<int, C * ly.kc + KK>{});
             static_for<TP>([&](auto tt) {
                 constexpr int t = decltype(tt)::value, F = KK * TP + t;
                 const h8 Ah = fh[F % PD], Al = fl[F % PD];
@@ -303,27 +311,38 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &s
                     fh[F % PD] = frag(F + PD, 0);
                     fl[F % PD] = frag(F + PD, 1);
                 }
-                if constexpr (TRANS) {
-                    acc[t] = mfma16(B.hi, Ah, acc[t]);
-                    acc[t] = mfma16(B.lo, Ah, acc[t]);
-                    acc[t] = mfma16(B.hi, Al, acc[t]);
-                } else {
-                    acc[t] = mfma16(Ah, B.hi, acc[t]);
-                    acc[t] = mfma16(Ah, B.lo, acc[t]);
-                    acc[t] = mfma16(Al, B.hi, acc[t]);
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    f32x4 &c = acc[s][AOFF + t];
+                    if constexpr (TRANS) {
+                        c = mfma16(B.b[s].hi, Ah, c);
+                        c = mfma16(B.b[s].lo, Ah, c);
+                        c = mfma16(B.b[s].hi, Al, c);
+                    } else {
+                        c = mfma16(Ah, B.b[s].hi, c);
+                        c = mfma16(Ah, B.b[s].lo, c);
+                        c = mfma16(Al, B.b[s].hi, c);
+                    }
                 }
-                constexpr int NS = NF / 2 > 0 ? NF / 2 : 1;
-                if constexpr (F < NS) {
-                    static_for<(F + 1) * PW / NS - F * PW / NS>([&](auto jj) {
-                        dma_piece<Net, NN, F * PW / NS + decltype(jj)::value, NWv>(wb, dnext, w, lane, lz);
+                constexpr int NSP = NF / 2 > 0 ? NF / 2 : 1;
+                if constexpr (F < NSP) {
+                    static_for<(F + 1) * PW / NSP - F * PW / NSP>([&](auto jj) {
+                        dma_piece<Net, NN, F * PW / NSP + decltype(jj)::value, NWv>(wb, dnext, w, lane, lz);
                     });
                 }
                 mid(std::integral_constant<int, (C * ly.kc + KK) * TP + t>{});
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if constexpr (NS == 1) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                } else {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 3 * NS / 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 3 * NS - 3 * NS / 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
             });
         });
         __builtin_amdgcn_sched_barrier(0);
@@ -331,6 +350,17 @@ __device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &s
         chunk_exit(slot, lane);
         __builtin_amdgcn_sched_barrier(0);
     });
+}
+
+// one row set (16 rows / units of the accumulators): the layer loop above with NS = 1
+template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, class SlotT, class InFn,
+          class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>
+__device__ __forceinline__ void run_layer16(const WBlob &wb, char *lds, SlotT &slot, int w, int lane, int lz,
+                                            f32x4 (&acc)[Net::L[L].tp], InFn &&in, PostFn &&post = PostFn{},
+                                            EndFn &&end = EndFn{}, MidFn &&mid = MidFn{}) {
+    constexpr int TP = Net::L[L].tp;
+    run_layer_ns<Net, L, TRANS, Vm, P, 0>(wb, lds, slot, w, lane, lz, reinterpret_cast<f32x4(&)[1][TP]>(acc),
+                                          [&](auto k) { return X3S<1>{{in(k)}}; }, post, end, mid);
 }
 
 // LeakyReLU(2^-s acc + add) of 16 tiles -> the next layer's 8 k-step B fragments (hi/lo)
@@ -490,22 +520,20 @@ __device__ __forceinline__ Rec16<PERS> load_rec16(const AggArgs &a, const RowIdx
     r.cf = m ? q0[3] : 0.f;
     return r;
 }
-// vmcnt allowances of k_rows16's boundaries (chunk_enter VM): block3.2 ends chunk 0 with the next
-// tile's record (REC16_LOADS loads, the youngest); after block3.2 come the next tile's 16 P loads
-// (and the epilogue's f_s stores, masked per segment, so not counted), all younger than block1.0's
-// DMA
-// vmcnt allowances of k_rows16's boundaries (chunk_enter VM): block3.2 ends its first chunk with the next
-// tile's record (REC16_LOADS loads) and this tile's slot entry (1), the youngest; after block3.2 come the
-// next tile's 16 P loads (and the epilogue's f_s stores, masked per segment, so not counted), all
-// younger than block1.0's DMA
+// vmcnt allowances of k_rows16's boundaries (chunk_enter VM), per row set of the wave: block3.2 ends its
+// first chunk with the next tile's record (REC16_LOADS loads) and this tile's slot entry (1), the
+// youngest; after block3.2 come the next tile's 16 P loads (and the epilogue's f_s stores, masked per
+// segment, so not counted), all younger than block1.0's DMA
 // The save mode (training) waits vmcnt(0) at every boundary instead: its z stores inside the k-loops
 // let these counts pass with a weight LDS-DMA piece still in flight (a few samples a frame read stale
 // block3.2 weights, run to run; tools/f32_repeat.py)
+template <int NS>
 struct VmL3P0 {
-    static constexpr int vm(int c) { return c == 1 ? REC16_LOADS + 1 : 0; }
+    static constexpr int vm(int c) { return c == 1 ? NS * (REC16_LOADS + 1) : 0; }
 };
+template <int NS>
 struct VmL0 {  // the P loads follow only the DMA of block1.0's first chunk
-    static constexpr int vm(int c) { return c == 0 ? 16 : 0; }
+    static constexpr int vm(int c) { return c == 0 ? 16 * NS : 0; }
 };
 
 // ---- paired samples: k_rows16's 8-row halves ----------------------------------------------------
@@ -762,16 +790,20 @@ __device__ __forceinline__ Tiles grid_tiles(int ntiles) { return Tiles{(int)bloc
 // KB: k-steps of block2_bpnet.0 in 16x16 steps (0: base viewmlp; 8: bpnet_dim 0; 11: dim 96)
 // SAVE (training): the pre-activations of block1.0 / 1.2 / 3.0 go to a.z1 / z2 / z3 as the next
 // layer converts them (chain_k); SG: block2_bpnet.0's to a.zb
-template <int KB, bool PERS, bool SAVE = false>
-__global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
+// NS: row sets of 16 rows per wave.  NS = 2: 32 rows per wave, each LDS weight fragment pair feeds
+// six MFMAs (half the LDS reads and weight DMA per MFMA of NS = 1), one workgroup per CU and one
+// wave per SIMD (the accumulators of two layers, 256 registers, sit in AGPRs)
+template <int KB, bool PERS, bool SAVE = false, int NS = 1>
+__global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs a) {
     using Net = std::conditional_t<(KB > 0), NetR16SG<KB>, NetR16>;
     constexpr int LB = 2, L2 = KB ? 3 : 2, L3 = KB ? 4 : 3;
     constexpr int NBP = KB > 8 ? KB - 8 : 0;  // BPNet k-steps (32 channels each)
+    constexpr int WGS = WG16_SAMPLES * NS;    // halves per workgroup tile
     __shared__ __attribute__((aligned(16))) char lds[ROWS16_LDS];
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4, r = lane & 15, kk = lane & 7, sc = r >> 3;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nslots = a.slot_n[0];  // paired halves (k_pair_slots), 2 per wave and tile
+    const int nslots = a.slot_n[0];  // paired halves (k_pair_slots), 2 per row set and tile
     const Cam cam = load_cam(a.campos, a.rot);
     const WBlob wb = make_blob(a.blob, BLOB_BYTES_ALL);
     const float *proj = (const float *)a.proj;
@@ -793,10 +825,15 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
     dma_chunk<Net, 0, NWR>(wb, lds, w, lane, 0);
     // The next tile's chain, prefetched inside the current tile so each step lands under MFMAs:
     // row-table entry (block1.2), neighbour / ray index (block3.0), point record + sample position
-    // and the P row (block3.2).  First tile: here.
-    const Tiles xt = grid_tiles((nslots + WG16_SAMPLES - 1) / WG16_SAMPLES);
-    RowIdx nx = row_index16(a, xt.first * WG16_SAMPLES + w * 2 + sc, nslots, kk);
-    Rec16<PERS> rnext = load_rec16<PERS>(a, nx);
+    // and the P row (block3.2).  First tile: here.  Row set q of wave w: halves w 2 NS + 2 q (+ sc).
+    const Tiles xt = grid_tiles((nslots + WGS - 1) / WGS);
+    RowIdx nx[NS];
+    Rec16<PERS> rnext[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        nx[q] = row_index16(a, xt.first * WGS + w * 2 * NS + 2 * q + sc, nslots, kk);
+        rnext[q] = load_rec16<PERS>(a, nx[q]);
+    }
     // P row of point pid into `dst`: natural unit order, tile t of lane group g at 16 t + 4 g, so the
     // 4 lanes of a row read one contiguous 64 B per load instruction
     auto load_p = [&](int pid, f32x4 (&dst)[16]) {
@@ -807,8 +844,9 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
     // accA: block1.0's accumulators start at P[pid]; the next tile's P is loaded into the array
     // block3.0 accumulated in (dead once block3.2 has consumed it), so it lands during the
     // block3.2 epilogue and the tile transition without extra registers
-    f32x4 accA[16], accB[16];
-    load_p(nx.pid, pick<(KB > 0)>(accB, accA));  // SG: where the tile loop copies it from
+    f32x4 accA[NS][16], accB[NS][16];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) load_p(nx[q].pid, pick<(KB > 0)>(accB[q], accA[q]));  // SG: where the tile loop copies it from
 
     // epilogue pieces (LDS reads through the tile's opaque base)
     auto epi_begin = [&](Epi16 &e, const char *ldsi, float wgt, int nA, int nB, int2 ce, bool ok) {
@@ -886,57 +924,69 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
     };
 
     for (int tile = xt.first; tile < xt.end; tile += xt.step) {
-        const int base = tile * WG16_SAMPLES;
+        const int base = tile * WGS;
         int lz = 0;
         asm volatile("" : "+s"(lz));
         char *ldsi = lds + lz;
         const float *Yl = (const float *)(ldsi + YR_OFF);
-        const int hslot = base + w * 2 + sc;  // this lane's half (the LDS ring slot is `slot`)
-        const int nslot = tile + xt.step < xt.end ? hslot + xt.step * WG16_SAMPLES : nslots;  // next tile's half
-        const RowIdx ix = nx;
-        const bool m = ix.pid >= 0;
-        const Rec16<PERS> rc = rnext;
-        // rows of the two segments (lane group 0 = rows 0..15): bits 8 h .. 8 h + 7 are half h's
-        const uint64_t mrowA = __ballot(ix.sval && ix.a), mrowB = __ballot(ix.sval && !ix.a);
-        const int nA0 = __popc((uint32_t)mrowA & 0xFFu), nA1 = __popc(((uint32_t)mrowA >> 8) & 0xFFu);
-        const bool waveB = (mrowB & 0xFFFFull) != 0;  // wave-uniform: a B sample in either half
-        const Row16 rw = row_math16<PERS>(cam, rc, m, ix.a, sc ? nA1 : nA0, waveB);
-        // SAVE: the row's pidx index s * K + k (from the slot's row table entry s * 8 + k), or its compact
-        // row row_off[s] + k; -1 for rows without a neighbour
-        int64_t vrow = -1;
-        if (SAVE && ix.sval && m) {
-            const int e = a.rows[(int64_t)hslot * 8 + kk];
-            vrow = a.row_off ? (int64_t)a.row_off[e >> 3] + (e & 7) : pidx_of(a, e);
-        }
-        if ((a.blend || a.wnorm) && ix.sval) {  // optional outputs: the row's pidx index from the table
-            const int64_t v = pidx_of(a, a.rows[(int64_t)hslot * 8 + kk]);
-            if (a.blend && g == 0) a.blend[v] = rw.wgt;
-            if (a.wnorm && g == 1) a.wnorm[v] = rw.wn;
-        }
-        X3B ext;
-        {   // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane group 0
-            const bool e = g == 0 && m;
-            float u[8];
-            u[0] = e ? rc.col[0] : 0.f; u[1] = e ? rc.col[1] : 0.f; u[2] = e ? rc.col[2] : 0.f;
-            u[3] = e ? __fsub_rn(rc.dir[0], rc.v[0]) : 0.f;
-            u[4] = e ? __fsub_rn(rc.dir[1], rc.v[1]) : 0.f;
-            u[5] = e ? __fsub_rn(rc.dir[2], rc.v[2]) : 0.f;
-            u[6] = e ? __fadd_rn(__fadd_rn(__fmul_rn(rc.dir[0], rc.v[0]), __fmul_rn(rc.dir[1], rc.v[1])),
-                                 __fmul_rn(rc.dir[2], rc.v[2])) : 0.f;
-            u[7] = 0.f;
-            ext = split8(u);
+        RowIdx ix[NS];
+        Row16 rw[NS];
+        int nslot[NS], nA[NS], nB[NS];
+        uint64_t mrowA[NS], mrowB[NS];
+        int64_t vrow[NS];
+        X3B ext[NS];
+        const int hsh = 8 * (g >> 1);  // half g >> 1's row bits
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int hslot = base + w * 2 * NS + 2 * q + sc;  // this lane's half (the LDS ring slot is `slot`)
+            nslot[q] = tile + xt.step < xt.end ? hslot + xt.step * WGS : nslots;  // next tile's half
+            ix[q] = nx[q];
+            const bool m = ix[q].pid >= 0;
+            const Rec16<PERS> rc = rnext[q];
+            // rows of the two segments (lane group 0 = rows 0..15): bits 8 h .. 8 h + 7 are half h's
+            mrowA[q] = __ballot(ix[q].sval && ix[q].a);
+            mrowB[q] = __ballot(ix[q].sval && !ix[q].a);
+            const int nA0 = __popc((uint32_t)mrowA[q] & 0xFFu), nA1 = __popc(((uint32_t)mrowA[q] >> 8) & 0xFFu);
+            const bool waveB = (mrowB[q] & 0xFFFFull) != 0;  // wave-uniform: a B sample in either half
+            rw[q] = row_math16<PERS>(cam, rc, m, ix[q].a, sc ? nA1 : nA0, waveB);
+            nA[q] = __popcll((mrowA[q] >> hsh) & 0xFFull);
+            nB[q] = __popcll((mrowB[q] >> hsh) & 0xFFull);
+            // SAVE: the row's pidx index s * K + k (from the slot's row table entry s * 8 + k), or its
+            // compact row row_off[s] + k; -1 for rows without a neighbour
+            vrow[q] = -1;
+            if (SAVE && ix[q].sval && m) {
+                const int e = a.rows[(int64_t)hslot * 8 + kk];
+                vrow[q] = a.row_off ? (int64_t)a.row_off[e >> 3] + (e & 7) : pidx_of(a, e);
+            }
+            if ((a.blend || a.wnorm) && ix[q].sval) {  // optional outputs: the row's pidx index from the table
+                const int64_t v = pidx_of(a, a.rows[(int64_t)hslot * 8 + kk]);
+                if (a.blend && g == 0) a.blend[v] = rw[q].wgt;
+                if (a.wnorm && g == 1) a.wnorm[v] = rw[q].wn;
+            }
+            {   // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane group 0
+                const bool e = g == 0 && m;
+                float u[8];
+                u[0] = e ? rc.col[0] : 0.f; u[1] = e ? rc.col[1] : 0.f; u[2] = e ? rc.col[2] : 0.f;
+                u[3] = e ? __fsub_rn(rc.dir[0], rc.v[0]) : 0.f;
+                u[4] = e ? __fsub_rn(rc.dir[1], rc.v[1]) : 0.f;
+                u[5] = e ? __fsub_rn(rc.dir[2], rc.v[2]) : 0.f;
+                u[6] = e ? __fadd_rn(__fadd_rn(__fmul_rn(rc.dir[0], rc.v[0]), __fmul_rn(rc.dir[1], rc.v[1])),
+                                     __fmul_rn(rc.dir[2], rc.v[2])) : 0.f;
+                u[7] = 0.f;
+                ext[q] = split8(u);
+            }
         }
         // Each layer's epilogue (LeakyReLU + hi/lo split of its accumulators) runs lazily inside the
         // next layer's k-loop: k-step k converts tiles 2k, 2k+1 only, so the VALU work overlaps the
         // MFMAs in flight instead of idling the matrix pipe between layers.
-        auto chain_k = [&](const f32x4 (&ac)[16], float inv, auto kc, float *zsave = nullptr) {
+        auto chain_k = [&](int q, const f32x4 (&ac)[16], float inv, auto kc, float *zsave = nullptr) {
             constexpr int S = decltype(kc)::value;
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = ac[2 * S + (j >> 2)][j & 3];
             if constexpr (SAVE) {  // units 16 t + 4 g .. + 3 of tiles t = 2 S, 2 S + 1
-                if (zsave && vrow >= 0) {
-                    float *zr = zsave + (int64_t)vrow * HID + 4 * g;
+                if (zsave && vrow[q] >= 0) {
+                    float *zr = zsave + vrow[q] * HID + 4 * g;
                     *(f32x4 *)(zr + 32 * S) = f32x4{v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv};
                     *(f32x4 *)(zr + 32 * S + 16) = f32x4{v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv};
                 }
@@ -948,120 +998,181 @@ __global__ __launch_bounds__(TPBR, 8 / NWR) void k_rows16(AggArgs a) {
             for (int t = 0; t < 16; ++t) ac[t] = *(const f32x4 *)(Yl + yb + 16 * t + 4 * g);
         };
         {   // block1.0: W0b PE(dists) on MFMA, + P[pid] (W0a [feat | PE(feat)] + b0, k_point_proj16)
-            const PeRow pr = pe_row16(rw.d, g);
-            if constexpr (KB > 0) {  // SG: five layers, the P array alternates -- copy it back
+            PeRow pr[NS];
 #pragma unroll
-                for (int t = 0; t < 16; ++t) accA[t] = accB[t];
+            for (int q = 0; q < NS; ++q) {
+                pr[q] = pe_row16(rw[q].d, g);
+                if constexpr (KB > 0) {  // SG: five layers, the P array alternates -- copy it back
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) accA[q][t] = accB[q][t];
+                }
             }
-            run_layer16<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0>>(wb, ldsi, slot, w, lane, lz, accA,
-                                             [&](auto k) { return pe_dists16_k<decltype(k)::value>(pr); },
-                                             NoHook{});
+            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>>(
+                wb, ldsi, slot, w, lane, lz, accA, [&](auto k) {
+                    X3S<NS> o;
+#pragma unroll
+                    for (int q = 0; q < NS; ++q) o.b[q] = pe_dists16_k<decltype(k)::value>(pr[q]);
+                    return o;
+                }, NoHook{});
         }
         // block1.2: 256 -> 256 (input: block1.0 accumulators)
         const float inv0 = Yl[Y_INV + 0], inv1 = Yl[Y_INV + 1], inv2 = Yl[Y_INV + 2], inv7 = Yl[Y_INV + 7];
-        bias_init(accB, Y_B1);
-        int v_next = -1;
-        run_layer16<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) { return chain_k(accA, inv0, k, a.z1); },
-                            [&](auto c) {
-                                if constexpr (decltype(c)::value == 0)
-                                    v_next = nslot < nslots ? a.rows[(int64_t)nslot * 8 + kk] : -1;
-                            });
+#pragma unroll
+        for (int q = 0; q < NS; ++q) bias_init(accB[q], Y_B1);
+        int v_next[NS];
+        run_layer_ns<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {
+            X3S<NS> o;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) o.b[q] = chain_k(q, accA[q], inv0, k, a.z1);
+            return o;
+        }, [&](auto c) {
+            if constexpr (decltype(c)::value == 0) {
+#pragma unroll
+                for (int q = 0; q < NS; ++q) v_next[q] = nslot[q] < nslots ? a.rows[(int64_t)nslot[q] * 8 + kk] : -1;
+            }
+        });
         if constexpr (KB > 0) {
             // block2_bpnet.0 (SG): [h 256 | BPNet embedding] -> 256; the row's fp32 embedding
             // (channels 32 m + 8 g .. +7 for k-step 8 + m) gathered and split here
-            X3B bpv[NBP > 0 ? NBP : 1];
+            X3B bpv[NS][NBP > 0 ? NBP : 1];
             if constexpr (NBP > 0) {
-                const float *src = a.bpnet32 + (int64_t)(m ? ix.pid : 0) * (NBP * 32) + 8 * g;
 #pragma unroll
-                for (int q = 0; q < NBP; ++q) {
-                    const f32x4 u0 = *(const f32x4 *)(src + 32 * q), u1 = *(const f32x4 *)(src + 32 * q + 4);
-                    const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-                    bpv[q] = split8(v);
+                for (int q = 0; q < NS; ++q) {
+                    const float *src = a.bpnet32 + (int64_t)(ix[q].pid >= 0 ? ix[q].pid : 0) * (NBP * 32) + 8 * g;
+#pragma unroll
+                    for (int j = 0; j < NBP; ++j) {
+                        const f32x4 u0 = *(const f32x4 *)(src + 32 * j), u1 = *(const f32x4 *)(src + 32 * j + 4);
+                        const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+                        bpv[q][j] = split8(v);
+                    }
                 }
             }
-            bias_init(accA, Y_BB);
-            run_layer16<Net, LB>(wb, ldsi, slot, w, lane, lz, accA, [&](auto k) {
+#pragma unroll
+            for (int q = 0; q < NS; ++q) bias_init(accA[q], Y_BB);
+            run_layer_ns<Net, LB>(wb, ldsi, slot, w, lane, lz, accA, [&](auto k) {
                 constexpr int K = decltype(k)::value;
-                if constexpr (K < 8) return chain_k(accB, inv1, k, a.z2); else return bpv[K - 8];
+                X3S<NS> o;
+#pragma unroll
+                for (int q = 0; q < NS; ++q) {
+                    if constexpr (K < 8) o.b[q] = chain_k(q, accB[q], inv1, k, a.z2);
+                    else o.b[q] = bpv[q][K - 8];
+                }
+                return o;
             }, NoHook{});
         }
         // block3.0: [h 256 | colour, dir - v, <dir, v>] -> 256 (input: block1.2 or block2_bpnet)
         auto &in2 = pick<(KB > 0)>(accA, accB);
         auto &acc2 = pick<(KB > 0)>(accB, accA);
         const float inv_in2 = KB > 0 ? inv7 : inv1;
-        bias_init(acc2, Y_B2);
-        run_layer16<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) bias_init(acc2[q], Y_B2);
+        run_layer_ns<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {
             constexpr int K = decltype(k)::value;
-            if constexpr (K < 8) return chain_k(in2, inv_in2, k, KB > 0 ? a.zb : a.z2); else return ext;
+            X3S<NS> o;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+                if constexpr (K < 8) o.b[q] = chain_k(q, in2[q], inv_in2, k, KB > 0 ? a.zb : a.z2);
+                else o.b[q] = ext[q];
+            }
+            return o;
         }, [&](auto c) {
             constexpr int C = decltype(c)::value;
             if constexpr (C == 0) {  // v_next landed at the previous boundaries
-                nx.sval = v_next >= 0;
-                nx.s = nx.sval ? v_next >> 3 : 0;
-                nx.a = (v_next & 7) == kk;
-                nx.pid = nx.sval ? a.pidx[pidx_of(a, v_next)] : -1;
-                nx.ray = nx.sval ? a.samp_ray[nx.s] : 0;
+#pragma unroll
+                for (int q = 0; q < NS; ++q) {
+                    nx[q].sval = v_next[q] >= 0;
+                    nx[q].s = nx[q].sval ? v_next[q] >> 3 : 0;
+                    nx[q].a = (v_next[q] & 7) == kk;
+                    nx[q].pid = nx[q].sval ? a.pidx[pidx_of(a, v_next[q])] : -1;
+                    nx[q].ray = nx[q].sval ? a.samp_ray[nx[q].s] : 0;
+                }
             }
         });
         // block3.2: 256 -> 256 transposed: acc[t][i] = h[row 4 g + i][unit 16 t + (l & 15)]
         auto &acc = in2;  // block3.0's input is dead: its registers take block3.2's accumulators
 #pragma unroll
-        for (int t = 0; t < 16; ++t) acc[t] = f32x4{};  // the bias joins in the epilogue (epi_step)
+        for (int q = 0; q < NS; ++q)
+#pragma unroll
+            for (int t = 0; t < 16; ++t) acc[q][t] = f32x4{};  // the bias joins in the epilogue (epi_step)
         // the next tile's record (and this tile's slot entry for the epilogue: half g >> 1's
         // {A item | nA << 28, B item | nB << 28, ..}) go out at the end of block3.2's first chunk, after
-        // the chunk's DMA pieces, so they stay in flight across one boundary (VmL3)
-        int2 ce = make_int2(0, 0);
-        const int eslot = base + w * 2 + (g >> 1);
-        const int hsh = 8 * (g >> 1);  // half g >> 1's row bits
-        const int nA = __popcll((mrowA >> hsh) & 0xFFull), nB = __popcll((mrowB >> hsh) & 0xFFull);
+        // the chunk's DMA pieces, so they stay in flight across one boundary (VmL3P0)
+        int2 ce[NS];
+        int eslot[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            ce[q] = make_int2(0, 0);
+            eslot[q] = base + w * 2 * NS + 2 * q + (g >> 1);
+        }
         auto first_chunk_loads = [&](auto c) {
             if constexpr (decltype(c)::value == 0) {
-                rnext = load_rec16<PERS>(a, nx);
-                ce = *(const int2 *)(a.slots + (eslot < nslots ? eslot : 0));
+#pragma unroll
+                for (int q = 0; q < NS; ++q) {
+                    rnext[q] = load_rec16<PERS>(a, nx[q]);
+                    ce[q] = *(const int2 *)(a.slots + (eslot[q] < nslots ? eslot[q] : 0));
+                }
             }
         };
-        Epi16 e;
+        Epi16 e[NS];
         {
             // pass 0 (output tiles 0..7) converts block3.0's output once into (hi, lo) fragments (in the
             // registers it frees) and pass 1 (tiles 8..15) reuses them; pass 1 carries the epilogue of
             // pass 0's tiles, output tile T after k-step T (one per 8 MFMA pairs)
-            X3B in3[8];
-            auto &acc0 = reinterpret_cast<f32x4(&)[8]>(acc[0]);
-            auto &acc1 = reinterpret_cast<f32x4(&)[8]>(acc[8]);
-            run_layer16<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0>, 0>(wb, ldsi, slot, w, lane, lz, acc0, [&](auto k) {
-                constexpr int K = decltype(k)::value;
-                in3[K] = chain_k(acc2, inv2, k, a.z3);
-                return in3[K];
-            }, NoHook{}, first_chunk_loads);
-            epi_begin(e, ldsi, rw.wgt, nA, nB, ce, eslot < nslots);
-            run_layer16<Net, L3, true, VmZero, 1>(wb, ldsi, slot, w, lane, lz, acc1,
-                                                  [&](auto k) { return in3[decltype(k)::value]; }, NoHook{},
-                                                  NoHook{}, [&](auto f) {
-                                                      constexpr int F = decltype(f)::value;
-                                                      if constexpr ((F & 7) == 7)
-                                                          epi_step(e, ldsi, acc, std::integral_constant<int, F / 8>{});
-                                                  });
+            X3B in3[NS][8];
+            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(
+                wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
+                    constexpr int K = decltype(k)::value;
+                    X3S<NS> o;
+#pragma unroll
+                    for (int q = 0; q < NS; ++q) {
+                        in3[q][K] = chain_k(q, acc2[q], inv2, k, a.z3);
+                        o.b[q] = in3[q][K];
+                    }
+                    return o;
+                }, NoHook{}, first_chunk_loads);
+#pragma unroll
+            for (int q = 0; q < NS; ++q) epi_begin(e[q], ldsi, rw[q].wgt, nA[q], nB[q], ce[q], eslot[q] < nslots);
+            run_layer_ns<Net, L3, true, VmZero, 1, 8>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
+                X3S<NS> o;
+#pragma unroll
+                for (int q = 0; q < NS; ++q) o.b[q] = in3[q][decltype(k)::value];
+                return o;
+            }, NoHook{}, NoHook{}, [&](auto f) {
+                constexpr int F = decltype(f)::value;
+                if constexpr ((F & 7) == 7) {
+#pragma unroll
+                    for (int q = 0; q < NS; ++q) epi_step(e[q], ldsi, acc[q], std::integral_constant<int, F / 8>{});
+                }
+            });
         }
         // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads
         // from the compiler's wait tracking, which would otherwise wait for the epilogue's stores
-        asm volatile("" : "+v"(nx.s), "+v"(nx.pid), "+v"(nx.ray));
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            asm volatile("" : "+v"(rnext.p[c]), "+v"(rnext.col[c]), "+v"(rnext.dir[c]), "+v"(rnext.l[c]), "+v"(rnext.v[c]));
-            if constexpr (PERS) asm volatile("" : "+v"(rnext.pp[c]), "+v"(rnext.pl[c]));
+        for (int q = 0; q < NS; ++q) {
+            asm volatile("" : "+v"(nx[q].s), "+v"(nx[q].pid), "+v"(nx[q].ray));
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                asm volatile("" : "+v"(rnext[q].p[c]), "+v"(rnext[q].col[c]), "+v"(rnext[q].dir[c]), "+v"(rnext[q].l[c]),
+                             "+v"(rnext[q].v[c]));
+                if constexpr (PERS) asm volatile("" : "+v"(rnext[q].pp[c]), "+v"(rnext[q].pl[c]));
+            }
+            asm volatile("" : "+v"(rnext[q].cf));
         }
-        asm volatile("" : "+v"(rnext.cf));
         {   // the rest of the epilogue; the next tile's P rows (see accA) go out first, into block3.2's
             // consumed input registers, and land under it
-            const float *psrc = proj + (int64_t)(nx.pid < 0 ? 0 : nx.pid) * HID + 4 * g;
-            constexpr int NE = 8, PPE = 16 / NE;  // epilogue steps left, P loads per step
+            constexpr int NE = 8, PPE = 16 / NE;  // epilogue steps left, P loads per step and row set
             static_for<NE>([&](auto tc) {  // the loads spread between the steps (a burst stalls the issue)
                 constexpr int J = decltype(tc)::value;
 #pragma unroll
-                for (int u = 0; u < PPE; ++u) acc2[PPE * J + u] = *(const f32x4 *)(psrc + 16 * (PPE * J + u));
-                epi_step(e, ldsi, acc, std::integral_constant<int, (16 - NE) + J>{});
+                for (int q = 0; q < NS; ++q) {
+                    const float *psrc = proj + (int64_t)(nx[q].pid < 0 ? 0 : nx[q].pid) * HID + 4 * g;
+#pragma unroll
+                    for (int u = 0; u < PPE; ++u) acc2[q][PPE * J + u] = *(const f32x4 *)(psrc + 16 * (PPE * J + u));
+                    epi_step(e[q], ldsi, acc[q], std::integral_constant<int, (16 - NE) + J>{});
+                }
             });
-            epi_end(e, ldsi, nA, nB, ix.s);
+#pragma unroll
+            for (int q = 0; q < NS; ++q) epi_end(e[q], ldsi, nA[q], nB[q], ix[q].s);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1568,7 +1679,12 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
                                                                                       : x3::k_rows16<11, true>)
                                      : (ksb == 0 ? x3::k_rows16<0, false> : ksb == KS_HID ? x3::k_rows16<8, false>
                                                                                         : x3::k_rows16<11, false>);
-            const int64_t wg16 = (n + x3::WG16_SAMPLES - 1) / x3::WG16_SAMPLES, wmax = 256 * (8 / x3::NWR);
+            // A/B (temporary): SGN_ROWS_NS=2 runs the 32-rows-per-wave form of the base kernel
+            const char *nse = getenv("SGN_ROWS_NS");
+            const int ns = (nse && nse[0] == '2' && !z && !pt->pers && ksb == 0) ? 2 : 1;
+            if (ns == 2) kern = x3::k_rows16<0, false, false, 2>;
+            const int64_t wg16 = (n + x3::WG16_SAMPLES * ns - 1) / (x3::WG16_SAMPLES * ns),
+                          wmax = ns == 1 ? 256 * (8 / x3::NWR) : 256;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < wmax ? wg16 : wmax)), dim3(x3::TPBR), 0, st, a);
         }
         if (stages & 2) {
