@@ -10,7 +10,8 @@ import os
 
 import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds to the same runtime
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
+# SGN_HIP_LIB: another build of the same ABI (same-box A/B of kernel variants, tools/ab_lib.sh)
+LIB_PATH = os.environ.get("SGN_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
 ABI_VERSION = 10
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,

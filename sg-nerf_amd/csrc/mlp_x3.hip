@@ -77,27 +77,17 @@ struct X3B {
 
 // x -> (hi, lo): hi = fp16(x), lo = fp16(x - hi) (the difference is exact in fp32)
 __device__ __forceinline__ X3B split8(const float (&v)[8]) {
-    X3B r;
-    r.hi = pack8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
-    float d[8];
-    const u32x4 hp = __builtin_bit_cast(u32x4, r.hi);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        // d = hi * -1.0 + x with hi read as the low / high fp16 half of the packed word
-        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d[2 * q]) : "v"(hp[q]), "v"(v[2 * q]));
-        asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
-            : "=v"(d[2 * q + 1]) : "v"(hp[q]), "v"(v[2 * q + 1]));
-    }
-    r.lo = pack8(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
-    return r;
+    const X3Pair p = split8_unit(v);
+    return X3B{p.hi, p.lo};
 }
 
 // LeakyReLU(0.01) exactly as the reference (x, or fp32(0.01 x) below zero): max(x, 0.01 x) as one
-// v_max_f32 in inline asm -- fmaxf on an MFMA result makes the compiler canonicalise the operand with
-// an extra v_max_f32 x, x, x first (IEEE mode); NaN / inf still propagate (the fp16-range guard)
+// v_max_f32 in inline asm -- fmaxf on an MFMA result makes the compiler canonicalise the operand with an
+// extra v_max_f32 x, x, x first (IEEE mode); NaN / inf still propagate (the fp16-range guard).  The asm
+// writes into the register of 0.01 x ("+v", tied; see split8_unit for why)
 __device__ __forceinline__ float lrelu_x3(float a) {
-    float r;
-    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(0.01f * a));
+    float r = 0.01f * a;
+    asm("v_max_f32 %0, %1, %0" : "+v"(r) : "v"(a));
     return r;
 }
 // LeakyReLU(2^-s a) as the next layer's (hi, lo) fragment (LeakyReLU commutes with the exact
@@ -105,10 +95,7 @@ __device__ __forceinline__ float lrelu_x3(float a) {
 __device__ __forceinline__ X3B lrelu_split8(const float (&a)[8], float inv) {
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float y = a[j] * inv;
-        v[j] = fmaxf(y, 0.01f * y);
-    }
+    for (int j = 0; j < 8; ++j) v[j] = lrelu_x3(a[j] * inv);
     return split8(v);
 }
 
@@ -221,23 +208,26 @@ static_assert(N_Y32 % 4 == 0, "fp32 section in 16-B units");
 // workgroups share a CU and their waves pair up on each SIMD without a common barrier (the barrier
 // of one chunk boundary no longer holds the other workgroup's wave of the SIMD: while one runs its
 // tile transition or epilogue VALU, the other's MFMAs keep the matrix pipe busy)
-constexpr int NWR = 4, SPR = NWR == 4 ? 16 : 32;  // row waves, ring slot pairs
+constexpr int NWR = 4;                            // row waves
 constexpr int NSLR = NSLOT;                       // row ring slots
-static_assert(NWR == 4 || NWR == 8, "row workgroup: 4 or 8 waves");
-constexpr int KCR = SPR / 16;                             // k-steps of 16 tiles per chunk
-constexpr XL L3_16 = XL{8, 8, 2, 2 * KCR, OFF16_W3};
-struct NetR16 {
-    static constexpr int NW = NWR, SP = SPR;  // waves sharing the ring, fragment pairs per ring slot
+static_assert(NWR == 4, "row workgroup: 4 waves");
+// ring slot of SP fragment pairs: 16 (NS = 1, two workgroups per CU) or 32 (NS = 2, one per CU);
+// KC = SP / 16 k-steps of 16 tiles per chunk
+template <int SP_>
+struct NetR16T {
+    static constexpr int NW = NWR, SP = SP_;  // waves sharing the ring, fragment pairs per ring slot
+    static constexpr int KC = SP_ / 16;
     static constexpr int NL = 4;
-    static constexpr XL L[NL] = {{2, 16, 1, KCR, OFF16_W0B}, {8, 16, 1, KCR, OFF16_W1}, {9, 16, 1, KCR, OFF16_W2},
-                                 L3_16};
+    static constexpr XL L[NL] = {{2, 16, 1, KC, OFF16_W0B}, {8, 16, 1, KC, OFF16_W1}, {9, 16, 1, KC, OFF16_W2},
+                                 {8, 8, 2, 2 * KC, OFF16_W3}};
 };
-template <int KB>
-struct NetR16SG {
-    static constexpr int NW = NWR, SP = SPR;
+template <int KB, int SP_>
+struct NetR16SGT {
+    static constexpr int NW = NWR, SP = SP_;
+    static constexpr int KC = SP_ / 16;
     static constexpr int NL = 5;
-    static constexpr XL L[NL] = {{2, 16, 1, KCR, OFF16_W0B}, {8, 16, 1, KCR, OFF16_W1}, {KB, 16, 1, KCR, OFF16_WB},
-                                 {9, 16, 1, KCR, OFF16_W2}, L3_16};
+    static constexpr XL L[NL] = {{2, 16, 1, KC, OFF16_W0B}, {8, 16, 1, KC, OFF16_W1}, {KB, 16, 1, KC, OFF16_WB},
+                                 {9, 16, 1, KC, OFF16_W2}, {8, 8, 2, 2 * KC, OFF16_W3}};
 };
 struct NetProj16 {
     static constexpr int NW = NW16, SP = SLOT_PAIRS;
@@ -252,8 +242,8 @@ struct NetColor16 {
     static constexpr int NL = 3;
     static constexpr XL L[NL] = {{9, 8, 1, KCC, OFF16_C0}, {4, 8, 1, KCC, OFF16_C1}, {4, 8, 1, KCC, OFF16_C2}};
 };
-static_assert(SPR == 16 ? Sched<NetR16>::total() == 27 : Sched<NetR16>::total() == 14 && Sched<NetR16>::pairs(9) == 16,
-              "16x16 row stream");
+static_assert(Sched<NetR16T<16>>::total() == 27 && Sched<NetR16T<32>>::total() == 14 &&
+                  Sched<NetR16T<32>>::pairs(9) == 16, "16x16 row stream");
 static_assert(NWC == 4 ? Sched<NetColor16>::total() == 9 && Sched<NetColor16>::pairs(4) == 8
                        : Sched<NetColor16>::total() == 5 && Sched<NetColor16>::pairs(2) == 8, "16x16 colour stream");
 
@@ -303,6 +293,9 @@ __device__ __forceinline__ void run_layer_ns(const WBlob &wb, char *lds, SlotT &
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
         static_for<nk(ly, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
+            // NS = 2 (one wave per SIMD, ~480 registers): a k-step's input conversion stays inside its
+            // k-step, so the B fragments of two k-steps are never live together
+            if constexpr (NS > 1 && KK > 0) __builtin_amdgcn_sched_barrier(0);
             const X3S<NS> B = in(std::integral_constant<int, C * ly.kc + KK>{});
             static_for<TP>([&](auto tt) {
                 constexpr int t = decltype(tt)::value, F = KK * TP + t;
@@ -468,10 +461,16 @@ __global__ __launch_bounds__(TPB16, 1) void k_point_proj16(Proj16Args a) {
 // ---- per-neighbour rows (16x16) -------------------------------------------------------------
 constexpr int WG16_SAMPLES = NWR * 2;            // halves (16 rows, 2 per wave) per workgroup tile
 constexpr int TPBR = NWR * 64;
-constexpr int YR_OFF = NSLR * SPR * PAIR;         // the row kernel's fp32 section, after its ring
-constexpr int YT16_OFF = YR_OFF + N_Y32 * 4;      // [unit r][20] 2^s3 b3 (t = 0..15) then [r][20] 2^-s3 alpha w
-constexpr int ROWS16_LDS = YT16_OFF + 2 * 16 * 20 * 4;
-static_assert(ROWS16_LDS * (8 / NWR) <= 163840, "LDS budget (16x16 rows, 8 / NWR workgroups per CU)");
+// the row kernel's LDS: ring (NSLR slots of SP pairs), fp32 section, then [unit r][20] 2^s3 b3
+// (t = 0..15) and [r][20] 2^-s3 alpha w
+__host__ __device__ constexpr int yr_off(int sp) { return NSLR * sp * PAIR; }
+__host__ __device__ constexpr int yt16_off(int sp) { return yr_off(sp) + N_Y32 * 4; }
+__host__ __device__ constexpr int rows16_lds(int sp) { return yt16_off(sp) + 2 * 16 * 20 * 4; }
+// NS = 2: block3.2's converted input of row set 1 (8 k-steps of (hi, lo) fragments per wave) waits
+// for its second pass in LDS, not in 64 registers
+constexpr int IN3_BYTES = NWR * 8 * 2 * 1024;
+__host__ __device__ constexpr int rows16_lds_ns(int sp, int ns) { return rows16_lds(sp) + (ns > 1 ? IN3_BYTES : 0); }
+static_assert(2 * rows16_lds(16) <= 163840 && rows16_lds_ns(16, 2) <= 163840, "LDS budget (16x16 rows)");
 
 // row r's point record, its sample position and view direction (+ the caller's pers
 // coordinates on the compatibility path)
@@ -793,9 +792,10 @@ __device__ __forceinline__ Tiles grid_tiles(int ntiles) { return Tiles{(int)bloc
 // NS: row sets of 16 rows per wave.  NS = 2: 32 rows per wave, each LDS weight fragment pair feeds
 // six MFMAs (half the LDS reads and weight DMA per MFMA of NS = 1), one workgroup per CU and one
 // wave per SIMD (the accumulators of two layers, 256 registers, sit in AGPRs)
-template <int KB, bool PERS, bool SAVE = false, int NS = 1>
+template <int KB, bool PERS, bool SAVE = false, int NS = 1, int SP = 16>
 __global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs a) {
-    using Net = std::conditional_t<(KB > 0), NetR16SG<KB>, NetR16>;
+    using Net = std::conditional_t<(KB > 0), NetR16SGT<KB, SP>, NetR16T<SP>>;
+    constexpr int YR_OFF = yr_off(SP), YT16_OFF = yt16_off(SP), IN3_OFF = rows16_lds(SP), ROWS16_LDS = rows16_lds_ns(SP, NS);
     constexpr int LB = 2, L2 = KB ? 3 : 2, L3 = KB ? 4 : 3;
     constexpr int NBP = KB > 8 ? KB - 8 : 0;  // BPNet k-steps (32 channels each)
     constexpr int WGS = WG16_SAMPLES * NS;    // halves per workgroup tile
@@ -1118,24 +1118,36 @@ __global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs 
             // pass 0 (output tiles 0..7) converts block3.0's output once into (hi, lo) fragments (in the
             // registers it frees) and pass 1 (tiles 8..15) reuses them; pass 1 carries the epilogue of
             // pass 0's tiles, output tile T after k-step T (one per 8 MFMA pairs)
-            X3B in3[NS][8];
+            // set 0 keeps its fragments in registers; set 1 (NS = 2) parks them in this wave's LDS area
+            // and pass 1 reads each one k-step ahead
+            X3B in3[8];
+            char *park = ldsi + IN3_OFF + w * (8 * 2 * 1024) + lane * 16;
             run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(
                 wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
                     constexpr int K = decltype(k)::value;
                     X3S<NS> o;
 #pragma unroll
-                    for (int q = 0; q < NS; ++q) {
-                        in3[q][K] = chain_k(q, acc2[q], inv2, k, a.z3);
-                        o.b[q] = in3[q][K];
+                    for (int q = 0; q < NS; ++q) o.b[q] = chain_k(q, acc2[q], inv2, k, a.z3);
+                    in3[K] = o.b[0];
+                    if constexpr (NS > 1) {
+                        *(h8 *)(park + (2 * K) * 1024) = o.b[1].hi;
+                        *(h8 *)(park + (2 * K + 1) * 1024) = o.b[1].lo;
                     }
                     return o;
                 }, NoHook{}, first_chunk_loads);
 #pragma unroll
             for (int q = 0; q < NS; ++q) epi_begin(e[q], ldsi, rw[q].wgt, nA[q], nB[q], ce[q], eslot[q] < nslots);
+            X3B pk{};
+            if constexpr (NS > 1) pk = X3B{*(const h8 *)park, *(const h8 *)(park + 1024)};
             run_layer_ns<Net, L3, true, VmZero, 1, 8>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
+                constexpr int K = decltype(k)::value;
                 X3S<NS> o;
-#pragma unroll
-                for (int q = 0; q < NS; ++q) o.b[q] = in3[q][decltype(k)::value];
+                o.b[0] = in3[K];
+                if constexpr (NS > 1) {
+                    o.b[1] = pk;
+                    if constexpr (K + 1 < 8)
+                        pk = X3B{*(const h8 *)(park + (2 * K + 2) * 1024), *(const h8 *)(park + (2 * K + 3) * 1024)};
+                }
                 return o;
             }, NoHook{}, NoHook{}, [&](auto f) {
                 constexpr int F = decltype(f)::value;
@@ -1236,7 +1248,7 @@ void layout_blob16(int ksb, int bpnet_dim, Pairs &&pairs, F32 &&f32) {
     pairs(OFF16_W0B, 0, 256, 284, 2, col_l0b16, 16, 1);
     pairs(OFF16_W1, 1, 256, 256, 8, col_chain16, 16, 1);
     pairs(OFF16_W2, 2, 256, 263, 9, col_l2_16, 16, 1);
-    pairs(OFF16_W3, 3, 256, 256, 8, col_chain16, 16, L3_16.np);
+    pairs(OFF16_W3, 3, 256, 256, 8, col_chain16, 16, 2);  // block3.2 in two passes of 8 tiles
     pairs(OFF16_W0A, 0, 256, 284, 7, col_proj16, 16, 1);
     for (int u = 0; u < HID; ++u) {
         f32(Y_B0 + u, YK_BS, 0, u);
@@ -1679,10 +1691,11 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
                                                                                       : x3::k_rows16<11, true>)
                                      : (ksb == 0 ? x3::k_rows16<0, false> : ksb == KS_HID ? x3::k_rows16<8, false>
                                                                                         : x3::k_rows16<11, false>);
-            // A/B (temporary): SGN_ROWS_NS=2 runs the 32-rows-per-wave form of the base kernel
-            const char *nse = getenv("SGN_ROWS_NS");
-            const int ns = (nse && nse[0] == '2' && !z && !pt->pers && ksb == 0) ? 2 : 1;
-            if (ns == 2) kern = x3::k_rows16<0, false, false, 2>;
+            // the base viewmlp's inference rows: 32 rows per wave (NS = 2; 0.95x the time of NS = 1 at
+            // config 2, profiles/r04_v3_*); the save mode, SG and the caller-pers path keep NS = 1
+            // (NS = 2 spills there)
+            const int ns = (!z && !pt->pers && ksb == 0) ? 2 : 1;
+            if (ns == 2) kern = x3::k_rows16<0, false, false, 2, 16>;
             const int64_t wg16 = (n + x3::WG16_SAMPLES * ns - 1) / (x3::WG16_SAMPLES * ns),
                           wmax = ns == 1 ? 256 * (8 / x3::NWR) : 256;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < wmax ? wg16 : wmax)), dim3(x3::TPBR), 0, st, a);

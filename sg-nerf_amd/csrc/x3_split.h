@@ -14,22 +14,45 @@ struct X3Pair {
     h8 hi, lo;
 };
 
-// (t * scale) -> (hi, lo) for a power-of-two `scale` (so t * scale is exact): each fp16 half is one
-// v_fma_mix{lo,hi}_f16 (an fp32 FMA rounded once to fp16), 4 instructions per 2 values
+// (t * scale) -> (hi, lo) for a power-of-two `scale` (so t * scale is exact): hi = fp16(t scale),
+// lo = fp16(t scale - hi) -- the difference is exact in fp32, so each half is rounded once.  Written as
+// plain fmas with an fp16 source, so the compiler selects one v_fma_mix{lo,hi}_f16 per half and, unlike
+// for inline asm, inserts the wait states a VALU write needs after an MFMA that still reads the same
+// registers (inline-asm VALU next to MFMAs raced: a wrong, run-to-run different accumulation).  The
+// constants the fmas must keep (the -0 addend, which also keeps the sign of a zero; the unit scale) are
+// hidden from the compiler by empty asm statements (no instruction), or it folds the fmas into
+// multiply / subtract / convert chains.
 __device__ __forceinline__ X3Pair split8_scaled(const float (&t)[8], float scale) {
-    u32x4 hi, lo;
+    float nz = -0.f;
+    asm volatile("" : "+v"(nz));
+    X3Pair r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r.hi[j] = (_Float16)__builtin_fmaf(t[j], scale, nz);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r.lo[j] = (_Float16)__builtin_fmaf(t[j], scale, -(float)r.hi[j]);
+    return r;
+}
+// x -> (hi, lo) without scaling: v_cvt_pk_f16_f32 for hi and lo, and the difference x - hi as one
+// v_fma_mix_f32 per value reading hi's fp16 half in place (the compiler forms a convert and a
+// subtract instead).  The asm writes only into x's own register ("+v", tied): that register's last
+// writer is a compiler-visible instruction, which already waited out any MFMA still reading it, so
+// the asm needs no hazard wait states of its own (an asm VALU writing a fresh register can land on
+// a register an in-flight MFMA still reads as its accumulator input -- the hazard recognizer does not
+// see inline asm).
+__device__ __forceinline__ X3Pair split8_unit(const float (&v)[8]) {
+    X3Pair r;
+    r.hi = pack8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+    const u32x4 hp = __builtin_bit_cast(u32x4, r.hi);
+    float d[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        uint32_t h, l;
-        asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(t[2 * q]), "v"(scale));
-        asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(t[2 * q + 1]), "v"(scale));
-        asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(t[2 * q]), "v"(scale), "v"(h));
-        asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-            : "+v"(l) : "v"(t[2 * q + 1]), "v"(scale), "v"(h));
-        hi[q] = h;
-        lo[q] = l;
+        d[2 * q] = v[2 * q];
+        d[2 * q + 1] = v[2 * q + 1];
+        asm("v_fma_mix_f32 %0, %1, -1.0, %0 op_sel_hi:[1,0,0]" : "+v"(d[2 * q]) : "v"(hp[q]));
+        asm("v_fma_mix_f32 %0, %1, -1.0, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(d[2 * q + 1]) : "v"(hp[q]));
     }
-    return X3Pair{__builtin_bit_cast(h8, hi), __builtin_bit_cast(h8, lo)};
+    r.lo = pack8(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+    return r;
 }
 
 // sin and cos of x (fp32, within ~1 ulp): quadrant q = rint(x 2/pi), r = x - q pi/2 in double
