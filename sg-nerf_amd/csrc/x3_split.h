@@ -14,23 +14,25 @@ struct X3Pair {
     h8 hi, lo;
 };
 
-// (t * scale) -> (hi, lo) for a power-of-two `scale` (so t * scale is exact): hi = fp16(t scale),
-// lo = fp16(t scale - hi) -- the difference is exact in fp32, so each half is rounded once.  Written as
-// plain fmas with an fp16 source, so the compiler selects one v_fma_mix{lo,hi}_f16 per half and, unlike
-// for inline asm, inserts the wait states a VALU write needs after an MFMA that still reads the same
-// registers (inline-asm VALU next to MFMAs raced: a wrong, run-to-run different accumulation).  The
-// constants the fmas must keep (the -0 addend, which also keeps the sign of a zero; the unit scale) are
-// hidden from the compiler by empty asm statements (no instruction), or it folds the fmas into
-// multiply / subtract / convert chains.
+// (t * scale) -> (hi, lo) for a power-of-two `scale` (so t * scale is exact): each fp16 half is one
+// v_fma_mix{lo,hi}_f16 (an fp32 FMA rounded once to fp16), 4 instructions per 2 values.  Inline asm
+// (the compiler turns the same fmas into multiply / move / convert chains), so its hazard wait states
+// are not inserted: use it only where no MFMA accumulates in VGPRs the outputs could land on (the
+// training GEMMs keep their accumulators in AGPRs; tools/asm_hazards.py checks the built code)
 __device__ __forceinline__ X3Pair split8_scaled(const float (&t)[8], float scale) {
-    float nz = -0.f;
-    asm volatile("" : "+v"(nz));
-    X3Pair r;
+    u32x4 hi, lo;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r.hi[j] = (_Float16)__builtin_fmaf(t[j], scale, nz);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r.lo[j] = (_Float16)__builtin_fmaf(t[j], scale, -(float)r.hi[j]);
-    return r;
+    for (int q = 0; q < 4; ++q) {
+        uint32_t h, l;
+        asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(t[2 * q]), "v"(scale));
+        asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(t[2 * q + 1]), "v"(scale));
+        asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(t[2 * q]), "v"(scale), "v"(h));
+        asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+            : "+v"(l) : "v"(t[2 * q + 1]), "v"(scale), "v"(h));
+        hi[q] = h;
+        lo[q] = l;
+    }
+    return X3Pair{__builtin_bit_cast(h8, hi), __builtin_bit_cast(h8, lo)};
 }
 // x -> (hi, lo) without scaling: v_cvt_pk_f16_f32 for hi and lo, and the difference x - hi as one
 // v_fma_mix_f32 per value reading hi's fp16 half in place (the compiler forms a convert and a

@@ -1,0 +1,47 @@
+"""Scan a gfx950 assembly listing (hipcc -save-temps) for inline-asm VALU instructions that write a
+register an MFMA wrote or reads as its accumulator input (srcC), or read an MFMA's result, within the
+previous 16 instructions (with no compiler-visible write of that register in between): the hazard recognizer
+does not see inline asm, so such a write may land while the MFMA still reads its accumulator input.
+Usage: python tools/asm_hazards.py <file.s>   (prints the candidates and their count)"""
+import re, sys
+def regs(tok):
+    tok = tok.strip().lstrip('-').strip('|')
+    m = re.match(r'([va])\[(\d+):(\d+)\]', tok)
+    if m: return {(m.group(1), i) for i in range(int(m.group(2)), int(m.group(3)) + 1)}
+    m = re.match(r'([va])(\d+)$', tok)
+    if m: return {(m.group(1), int(m.group(2)))}
+    return set()
+lines = open(sys.argv[1]).read().split('\n')
+inasm = False
+hist = []  # recent instructions: (kind, dst, srcs)
+found = 0
+for ln in lines:
+    s = ln.strip()
+    if s.startswith(';;#ASMSTART'): inasm = True; continue
+    if s.startswith(';;#ASMEND'): inasm = False; continue
+    if not s or s.startswith(';') or s.endswith(':') or s.startswith('.'): continue
+    parts = s.split(None, 1)
+    op = parts[0]; ops = [o for o in (parts[1].split(',') if len(parts) > 1 else [])]
+    dst = regs(ops[0]) if ops else set()
+    if op.startswith('v_mfma'):
+        # the accumulator input (srcC) is read over the MFMA's passes; srcA / srcB are latched at issue
+        srcs = regs(ops[3]) if len(ops) > 3 else set()
+    else:
+        srcs = set().union(*[regs(o) for o in ops[1:]]) if len(ops) > 1 else set()
+    if inasm and op.startswith('v_') and not op.startswith('v_mfma'):
+        # look back for an MFMA reading / writing the asm's destination with no compiler-visible write of
+        # it in between (such a write already waited out the MFMA: the hazard recognizer saw it)
+        for dist, (k, d2, s2, txt) in enumerate(reversed(hist[-16:])):
+            if k == 'other' and not txt.startswith('asm:') and dst & d2:
+                break
+            if k == 'mfma' and (dst & s2 or dst & d2 or srcs & d2):  # WAR / WAW, or RAW of the MFMA's result
+                found += 1
+                if found <= 12:
+                    print(f'asm {s!r} {dist+1} instrs after {txt!r}')
+                break
+    kind = 'mfma' if op.startswith('v_mfma') else 'other'
+    nw = 0
+    if op == 's_nop': nw = int(ops[0]) + 1 if ops else 1
+    hist.append((kind, dst, srcs, ('asm:' if inasm else '') + s))
+    for _ in range(nw - 1): hist.append(('nop', set(), set(), 's_nop'))
+print('hazard candidates:', found)
