@@ -466,11 +466,7 @@ constexpr int TPBR = NWR * 64;
 __host__ __device__ constexpr int yr_off(int sp) { return NSLR * sp * PAIR; }
 __host__ __device__ constexpr int yt16_off(int sp) { return yr_off(sp) + N_Y32 * 4; }
 __host__ __device__ constexpr int rows16_lds(int sp) { return yt16_off(sp) + 2 * 16 * 20 * 4; }
-// NS = 2: block3.2's converted input of row set 1 (8 k-steps of (hi, lo) fragments per wave) waits
-// for its second pass in LDS, not in 64 registers
-constexpr int IN3_BYTES = NWR * 8 * 2 * 1024;
-__host__ __device__ constexpr int rows16_lds_ns(int sp, int ns) { return rows16_lds(sp) + (ns > 1 ? IN3_BYTES : 0); }
-static_assert(2 * rows16_lds(16) <= 163840 && rows16_lds_ns(16, 2) <= 163840, "LDS budget (16x16 rows)");
+static_assert(2 * rows16_lds(16) <= 163840, "LDS budget (16x16 rows)");
 
 // row r's point record, its sample position and view direction (+ the caller's pers
 // coordinates on the compatibility path)
@@ -795,7 +791,7 @@ __device__ __forceinline__ Tiles grid_tiles(int ntiles) { return Tiles{(int)bloc
 template <int KB, bool PERS, bool SAVE = false, int NS = 1, int SP = 16>
 __global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs a) {
     using Net = std::conditional_t<(KB > 0), NetR16SGT<KB, SP>, NetR16T<SP>>;
-    constexpr int YR_OFF = yr_off(SP), YT16_OFF = yt16_off(SP), IN3_OFF = rows16_lds(SP), ROWS16_LDS = rows16_lds_ns(SP, NS);
+    constexpr int YR_OFF = yr_off(SP), YT16_OFF = yt16_off(SP), ROWS16_LDS = rows16_lds(SP);
     constexpr int LB = 2, L2 = KB ? 3 : 2, L3 = KB ? 4 : 3;
     constexpr int NBP = KB > 8 ? KB - 8 : 0;  // BPNet k-steps (32 channels each)
     constexpr int WGS = WG16_SAMPLES * NS;    // halves per workgroup tile
@@ -1118,36 +1114,24 @@ __global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs 
             // pass 0 (output tiles 0..7) converts block3.0's output once into (hi, lo) fragments (in the
             // registers it frees) and pass 1 (tiles 8..15) reuses them; pass 1 carries the epilogue of
             // pass 0's tiles, output tile T after k-step T (one per 8 MFMA pairs)
-            // set 0 keeps its fragments in registers; set 1 (NS = 2) parks them in this wave's LDS area
-            // and pass 1 reads each one k-step ahead
-            X3B in3[8];
-            char *park = ldsi + IN3_OFF + w * (8 * 2 * 1024) + lane * 16;
+            X3B in3[NS][8];
             run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(
                 wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
                     constexpr int K = decltype(k)::value;
                     X3S<NS> o;
 #pragma unroll
-                    for (int q = 0; q < NS; ++q) o.b[q] = chain_k(q, acc2[q], inv2, k, a.z3);
-                    in3[K] = o.b[0];
-                    if constexpr (NS > 1) {
-                        *(h8 *)(park + (2 * K) * 1024) = o.b[1].hi;
-                        *(h8 *)(park + (2 * K + 1) * 1024) = o.b[1].lo;
+                    for (int q = 0; q < NS; ++q) {
+                        in3[q][K] = chain_k(q, acc2[q], inv2, k, a.z3);
+                        o.b[q] = in3[q][K];
                     }
                     return o;
                 }, NoHook{}, first_chunk_loads);
 #pragma unroll
             for (int q = 0; q < NS; ++q) epi_begin(e[q], ldsi, rw[q].wgt, nA[q], nB[q], ce[q], eslot[q] < nslots);
-            X3B pk{};
-            if constexpr (NS > 1) pk = X3B{*(const h8 *)park, *(const h8 *)(park + 1024)};
             run_layer_ns<Net, L3, true, VmZero, 1, 8>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
-                constexpr int K = decltype(k)::value;
                 X3S<NS> o;
-                o.b[0] = in3[K];
-                if constexpr (NS > 1) {
-                    o.b[1] = pk;
-                    if constexpr (K + 1 < 8)
-                        pk = X3B{*(const h8 *)(park + (2 * K + 2) * 1024), *(const h8 *)(park + (2 * K + 3) * 1024)};
-                }
+#pragma unroll
+                for (int q = 0; q < NS; ++q) o.b[q] = in3[q][decltype(k)::value];
                 return o;
             }, NoHook{}, NoHook{}, [&](auto f) {
                 constexpr int F = decltype(f)::value;
