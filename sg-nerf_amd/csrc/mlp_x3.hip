@@ -1669,17 +1669,15 @@ int aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet,
             hipLaunchKernelGGL(x3::k_pair_slots, dim3((unsigned)(pb < 1024 ? pb : 1024)),
                                dim3(x3::PAIR_TPB), 0, st, q->counters, q->work, q->samp_nnb, (int32_t)i0, (int32_t)n,
                                pair, rows, slots, slot_n);
+            // inference rows: 32 rows per wave (NS = 2; 0.94x the time of NS = 1 at config 2,
+            // profiles/r04_v2_bench_rows_ns*.json); the save mode (training) keeps NS = 1
+            const int ns = z ? 1 : 2;
             auto kern = z ? (ksb == 0 ? x3::k_rows16<0, false, true> : ksb == KS_HID ? x3::k_rows16<8, false, true>
                                                                                   : x3::k_rows16<11, false, true>)
-                          : pt->pers ? (ksb == 0 ? x3::k_rows16<0, true> : ksb == KS_HID ? x3::k_rows16<8, true>
-                                                                                      : x3::k_rows16<11, true>)
-                                     : (ksb == 0 ? x3::k_rows16<0, false> : ksb == KS_HID ? x3::k_rows16<8, false>
-                                                                                        : x3::k_rows16<11, false>);
-            // the base viewmlp's inference rows: 32 rows per wave (NS = 2; 0.95x the time of NS = 1 at
-            // config 2, profiles/r04_v3_*); the save mode, SG and the caller-pers path keep NS = 1
-            // (NS = 2 spills there)
-            const int ns = (!z && !pt->pers && ksb == 0) ? 2 : 1;
-            if (ns == 2) kern = x3::k_rows16<0, false, false, 2, 16>;
+                          : pt->pers ? (ksb == 0 ? x3::k_rows16<0, true, false, 2> : ksb == KS_HID ? x3::k_rows16<8, true, false, 2>
+                                                                                      : x3::k_rows16<11, true, false, 2>)
+                                     : (ksb == 0 ? x3::k_rows16<0, false, false, 2> : ksb == KS_HID ? x3::k_rows16<8, false, false, 2>
+                                                                                        : x3::k_rows16<11, false, false, 2>);
             const int64_t wg16 = (n + x3::WG16_SAMPLES * ns - 1) / (x3::WG16_SAMPLES * ns),
                           wmax = ns == 1 ? 256 * (8 / x3::NWR) : 256;
             hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < wmax ? wg16 : wmax)), dim3(x3::TPBR), 0, st, a);
