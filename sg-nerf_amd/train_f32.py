@@ -318,3 +318,139 @@ class F32Step:
             gemm(gs)
         ck(L.sgn_reduce_partials(self.n_seg, self.segs, st), "sgn_reduce_partials")
         return self.losses, self.full[:self.R], self.mask[:self.R]
+
+
+class ColourStep:
+    """The colour MLP, the losses and their backward for the f16 training step on the same hand-written
+    kernels as F32Step (precision "f16" only changes the row MLP): items are the query's work-list
+    positions (k_agg_rows' f_s rows), `cap` of them at most, the device count at q.counters[1].
+    Per step: PE(viewdir), 3 x sgn_x3_gemm forward + sgn_train_colour_head (rgb into feat), sgn_loss_train,
+    the colour backward (head, 2 masked dy W, d f_s = dy1 W0[:, :256]), the three weight gradients as
+    split-K partials and one sgn_reduce_partials into the flat gradient.  No autograd, no host sync: it
+    runs inside the f16 step's captured graph."""
+
+    A_DY3, A_DY2, A_DY1 = range(3)
+
+    def __init__(self, trainer, q, cap, fs32, vdir, feat, R):
+        L = _lib.lib()
+        self.trainer, self.q, self.cap, self.R = trainer, q, max(cap, 1), R
+        self.qo = q.abi()
+        dev = trainer.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        cap = self.cap
+        self.fs32, self.vdir, self.feat = fs32, vdir, feat
+        self.vpe = torch.zeros(cap, 32, **f32)
+        self.vpe[:, 24] = 1.0                      # the ones column (colour 0's bias)
+        self.freq = torch.tensor([1.0, 2.0, 4.0, 8.0], **f32)
+        self.h = [torch.empty(cap, 128, **f32) for _ in range(3)]
+        self.dy = [torch.empty(cap, 128, **f32) for _ in range(3)]
+        self.dfs = torch.empty(cap, 256, **f32)
+        self.amax = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.dfeat = torch.zeros(feat.shape[0] + 1, 4, **f32)   # + the padding items' zero row
+        self.losses = torch.zeros(8, **f32)
+        self.full = torch.empty(max(R, 1), 3, **f32)
+        self.mask = torch.empty(max(R, 1), dtype=torch.int8, device=dev)
+        self.loss_ws = torch.empty(max(int(L.sgn_loss_workspace_bytes(R, trainer.opts.SR)), 16), dtype=torch.uint8,
+                                   device=dev)
+        self.part_col = [torch.empty(SPLITS_ITEMS, 128, n, **f32) for n in (129, 129, 281)]
+        self.part_c6 = torch.empty(int(L.sgn_train_head_partial_floats(0)), **f32)
+        self._build()
+
+    def _build(self):
+        tr = self.trainer
+        m, flat, shift = tr.mlp, tr.mlp.flat, tr.packer32.shift
+        g = flat.grad
+        layer_ix = {name: i for i, (name, *_) in enumerate(m.layers)}
+
+        def W(name):
+            off, o, i = m.slices[name]
+            return _addr(flat, off), o, i
+
+        def Bv(name):
+            off, o, i = m.slices[name]
+            return _addr(flat, off + o * i)
+
+        def S(name):
+            return _addr(shift, layer_ix[name])
+
+        amax = [_addr(self.amax, i) for i in range(4)]
+        n_items = _addr(self.q.counters, 1)         # the work-list length
+        cap = self.cap
+        h1, h2, h3 = (_addr(t) for t in self.h)
+        dy1, dy2, dy3 = (_addr(t) for t in self.dy)
+        fs, vpe = _addr(self.fs32), _addr(self.vpe)
+        w, o_, i_ = W("color_branch.0")
+        G = [_rows_gemm(_operand(fs, 256, 280, 0, p2=vpe, ld2=32, csplit=256), _operand(w, i_, i_, 0, shift=S("color_branch.0")),
+                        cap, o_, i_, n_items, h1, 128, bias=Bv("color_branch.0"), act=1)]
+        for name, x, y in (("color_branch.2", h1, h2), ("color_branch.4", h2, h3)):
+            w, o_, i_ = W(name)
+            G.append(_rows_gemm(_operand(x, 128, 128, 0), _operand(w, i_, i_, 0, shift=S(name)), cap, o_, i_, n_items,
+                                y, 128, bias=Bv(name), act=1))
+        self.g_fwd = G
+        G = []
+        for name, dyi, mk, dyo, ai, ao in (("color_branch.4", dy3, h2, dy2, self.A_DY3, self.A_DY2),
+                                           ("color_branch.2", dy2, h1, dy1, self.A_DY2, self.A_DY1)):
+            w, o_, i_ = W(name)
+            G.append(_rows_gemm(_operand(dyi, 128, 128, 0, amax=amax[ai]), _operand(w, i_, i_, 1, shift=S(name)), cap, i_, o_,
+                                n_items, dyo, 128, mask=mk, ldm=128, amax_out=amax[ao]))
+        w, o_, i_ = W("color_branch.0")
+        G.append(_rows_gemm(_operand(dy1, 128, 128, 0, amax=amax[self.A_DY1]), _operand(w, i_, 256, 1, shift=S("color_branch.0")),
+                            cap, 256, o_, n_items, _addr(self.dfs), 256))
+        pc = self.part_col
+        G.append(_splitk_gemm(_operand(dy3, 128, 128, 1, amax=amax[self.A_DY3]), _operand(h2, 128, 128, 1, ones_col=128),
+                              128, 129, cap, n_items, _addr(pc[0]), SPLITS_ITEMS))
+        G.append(_splitk_gemm(_operand(dy2, 128, 128, 1, amax=amax[self.A_DY2]), _operand(h1, 128, 128, 1, ones_col=128),
+                              128, 129, cap, n_items, _addr(pc[1]), SPLITS_ITEMS))
+        G.append(_splitk_gemm(_operand(dy1, 128, 128, 1, amax=amax[self.A_DY1]),
+                              _operand(fs, 256, 281, 1, p2=vpe, ld2=32, csplit=256), 128, 281, cap, n_items, _addr(pc[2]),
+                              SPLITS_ITEMS))
+        self.g_bwd = G
+        segs = []
+
+        def seg(part, splits, M, N, name, n_in, bias_col):
+            off, o_, i_ = m.slices[name]
+            s = _lib.PartialSegment()
+            s.part, s.splits, s.M, s.N, s.n_in, s.bias_col, s.ldw = part, splits, M, N, n_in, bias_col, i_
+            s.dst_w, s.dst_b = _addr(g, off), _addr(g, off + o_ * i_)
+            segs.append(s)
+        seg(_addr(pc[0]), SPLITS_ITEMS, 128, 129, "color_branch.4", 128, 128)
+        seg(_addr(pc[1]), SPLITS_ITEMS, 128, 129, "color_branch.2", 128, 128)
+        seg(_addr(pc[2]), SPLITS_ITEMS, 128, 281, "color_branch.0", 280, 280)
+        seg(_addr(self.part_c6), self.part_c6.numel() // (3 * 129), 3, 129, "color_branch.6", 128, 128)
+        self.segs = (_lib.PartialSegment * len(segs))(*segs)
+        self.n_seg = len(segs)
+        self.w6, self.b6 = W("color_branch.6")[0], Bv("color_branch.6")
+
+    def run(self, campos, rot, gt, lp):
+        """Colour forward into feat[.].yzw, the losses, the colour backward: returns the loss vector
+        (sgn_loss_train's 8 floats), full [R, 3], mask [R] (int8), d f_s [cap, 256] and d feat [S, 4]
+        (alpha's gradient in .x); the colour weight gradients are added into flat.grad, the zero-one
+        gradients into points_conf.grad."""
+        L = _lib.lib()
+        st = _lib.stream_handle()
+        ck, p = _lib.check, _lib.ptr
+        tr, qo = self.trainer, self.qo
+        P = tr.points
+        cnt = ctypes.c_void_p(_addr(self.q.counters, 1))
+        # PE(viewdir) ori=True without the raw v (point_aggregators.py:772-780): sin | cos of v 2^f
+        v = self.vdir
+        x = (v[:, :, None] * self.freq).reshape(-1, 12)
+        self.vpe[:, :12] = torch.sin(x)
+        self.vpe[:, 12:24] = torch.cos(x)
+        self.amax.zero_()
+        for gs in self.g_fwd:
+            ck(L.sgn_x3_gemm(ctypes.byref(gs), st), "sgn_x3_gemm")
+        ck(L.sgn_train_colour_head(ctypes.byref(qo), cnt, p(self.h[2]), self.w6, self.b6, p(self.feat), st),
+           "sgn_train_colour_head")
+        ck(L.sgn_loss_train(ctypes.byref(lp), p(campos), p(rot), self.R, ctypes.byref(qo), p(self.feat), p(gt),
+                            p(P.points_conf), p(self.full), p(self.mask), p(self.losses), p(self.dfeat),
+                            p(P.points_conf.grad), p(self.loss_ws), self.loss_ws.numel(), st), "sgn_loss_train")
+        # d f_s of the padding items stays 0: the f16 backward's loss scale is the max over all cap rows
+        self.dfs.zero_()
+        ck(L.sgn_train_colour_head_bwd(ctypes.byref(qo), cnt, p(self.h[2]), self.w6, self.b6, p(self.dfeat), p(self.dy[2]),
+                                       ctypes.c_void_p(_addr(self.amax, self.A_DY3)), p(self.part_c6), st),
+           "sgn_train_colour_head_bwd")
+        for gs in self.g_bwd:
+            ck(L.sgn_x3_gemm(ctypes.byref(gs), st), "sgn_x3_gemm")
+        ck(L.sgn_reduce_partials(self.n_seg, self.segs, st), "sgn_reduce_partials")
+        return self.losses, self.full[:self.R], self.mask[:self.R], self.dfs, self.dfeat

@@ -408,7 +408,12 @@ class HipTrainer:
         self.bucket_elems = bucket_mb * (1 << 20) // 4
         self.querier = querier
         self.packer = _Packer(self.device, self.variant)
-        self.packer32 = _PackerF32(self.device, self.mlp, self.variant) if precision == "f32" else None
+        # the fp32-faithful blob (f32 step) and, for both precisions, the per-layer weight shifts the
+        # split-fp16 GEMMs of the colour MLP read
+        self.packer32 = _PackerF32(self.device, self.mlp, self.variant)
+        # the f16 step's colour MLP + losses + backward on hand-written kernels inside the captured graph
+        # (train_f32.ColourStep; SGN_HIP_COLOUR=0: torch autograd of the colour MLP, the earlier stage)
+        self.hip_colour = os.environ.get("SGN_HIP_COLOUR", "1") != "0"
         # stored column p -> reference index; inverses: reference index -> stored column
         self.map_chain = _colmap(0, 256, self.device)
         self.map_x0 = _colmap(1, 288, self.device)
@@ -550,6 +555,9 @@ class HipTrainer:
         st = _lib.stream_handle()
         pt = self._tables(campos, rot, raydir)
         qo = q.abi()
+        if graph and self.hip_colour:
+            self.packer32.pack(self.mlp.flat)   # the colour GEMMs' weight shifts
+            self.feat.zero_()                    # samples without neighbours keep zero features
         saved = _lib.AggSaved(self.x0.data_ptr(), self.h1.data_ptr(), self.h2.data_ptr(), self.h3.data_ptr())
         if n > 0 and self.sg:
             _lib.check(L.sgn_aggregate_train_fwd_sg(*self.variant, _lib.ptr(self.bpnet16), ctypes.byref(pt),
@@ -787,6 +795,14 @@ class HipTrainer:
                                                 _lib.ptr(self.fs), _lib.ptr(self.feat), _lib.ptr(st["raydir"]),
                                                 _lib.ptr(fs32), _lib.ptr(al32), _lib.ptr(v), _lib.ptr(samp),
                                                 _lib.stream_handle()), "sgn_colour_inputs")
+        if "col" in st:   # hand-written colour MLP, losses and backward (train_f32.ColourStep)
+            losses, full, mask, dfs, dfeat = st["col"].run(st["campos"], st["rot"], st["gt"], self._loss_params())
+            dal = dfeat[samp.long(), 0]          # per item (padding: the zero row Sc)
+            scale = self._loss_scale(dfs, dal)
+            total = losses[0] + 3e-6 + 1e-4 * losses[1]
+            names = ["ray_masked_coarse_raycolor", "ray_miss_coarse_raycolor", "coarse_raycolor", "conf_coefficient"]
+            return {"scalars": torch.stack([total, losses[0], losses[2], losses[3], losses[1]]), "names": names,
+                    "full": full, "ray_mask": mask.bool(), "dfs": dfs, "dal": dal, "scale": scale}
         fs32.grad = al32.grad = None   # backward assigns fresh (graph-pool) gradients: no clear, no accumulate
         feat_s = torch.cat([al32[:, None], self._colour(fs32, v)], dim=-1)   # colour grads -> flat.grad
         featS = torch.zeros(Sc + 1, 4, device=dev).index_put((samp,), feat_s)[:Sc]
@@ -832,6 +848,9 @@ class HipTrainer:
                   "fs32": torch.zeros(Nc, 256, device=dev, requires_grad=True),
                   "al32": torch.zeros(Nc, device=dev, requires_grad=True),
                   "v": torch.zeros(Nc, 3, device=dev), "samp": torch.zeros(Nc, dtype=torch.int32, device=dev)}
+            if self.hip_colour and self.hip_loss:
+                from .train_f32 import ColourStep
+                st["col"] = ColourStep(self, q, Nc, st["fs32"], st["v"], self.feat, R)
             keep = [fl.grad.clone(), P.points_conf.grad.clone()]   # warm-up accumulates into them
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
