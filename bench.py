@@ -150,9 +150,10 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None, precision=
                                   f"{args.points} neural points, HIP query + "
                                   + ("torch autograd" if args.train_torch else
                                      "fp32 forward + backward on hand-written HIP kernels (k_rows16 save mode, split-fp16 "
-                                     "MFMA GEMMs k_x3rows / k_x3tn, HIP loss stage), fused Adam"
+                                     "MFMA GEMMs k_x3rows / k_x3tn, HIP loss stage), HIP Adam"
                                      if precision == "f32"
-                                     else "HIP MFMA row-MLP forward/backward + torch colour-MLP autograd + HIP loss stage")
+                                     else "HIP MFMA row-MLP forward/backward (fp16 operands) + colour MLP and losses "
+                                          "on the split-fp16 GEMMs and HIP loss stage in one captured graph, fused Adam")
                                   + (" (SG-NeRF variant: semantic-guided kNN, block2_bpnet 352->256)" if args.sg else "")
                                   + (" + RCCL all-reduce of the gradients" if world > 1 else
                                      ", one GPU (no gradient exchange)"),

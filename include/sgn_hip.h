@@ -430,6 +430,16 @@ int sgn_colour_inputs(const int32_t *d_counters, const int32_t *d_work, const in
 size_t sgn_pow2_scale_workspace_bytes(void);
 int sgn_pow2_scale(const float *d_a, int64_t na, const float *d_b, int64_t nb, void *d_ws, float *d_out,
                    sgn_stream_t stream);
+/* The distinct points a training step's rays touch, on the device: point 0 (the conf read of empty
+ * neighbour slots, train.composite_losses) and every neighbour d_pidx[e] >= 0, e < d_counters[0] * K
+ * (sgn_query's sample count; s_cap bounds it).  Appends them to d_idx (int32 [n_points]) in no
+ * particular order and writes their count to d_count2[step & 1]; d_count2[(step + 1) & 1] is
+ * cleared for the next step.  d_stamp: int32 [n_points], -1 once at allocation, then owned by the
+ * caller's step counter (step >= 0, increasing).  Replaces the torch touched_rows mask / scan /
+ * scatter (train.py) on the single-GPU fp32 step's projection subset (sgn_point_project_f32_subset);
+ * the neighbours come from the reference's query (neural_points.py:942-988). */
+int sgn_touched_points(const int32_t *d_pidx, const int32_t *d_counters, int64_t s_cap, int32_t K, int64_t n_points,
+                       int32_t step, int32_t *d_stamp, int32_t *d_idx, int64_t *d_count2, sgn_stream_t stream);
 
 /* ---- fp32 training step on hand-written kernels (ABI 9; SG entries ABI 10) -----------------------------------
  * The reference's fp32 autograd through PointAggregator / viewmlp and the NeuralPoints gather

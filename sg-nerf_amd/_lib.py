@@ -151,6 +151,7 @@ SIGNATURES = {
     "sgn_colour_inputs": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_pow2_scale_workspace_bytes": (c_sz, []),
     "sgn_pow2_scale": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "sgn_touched_points": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "sgn_mlp_packed_bytes_f32": (c_sz, [c_i32, c_i32]),
     "sgn_mlp_pack_f32": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
     "sgn_mlp_pack_f32_host": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp]),

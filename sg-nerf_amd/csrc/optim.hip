@@ -392,6 +392,43 @@ __global__ __launch_bounds__(256) void k_colour_inputs(ColourInArgs a) {
     }
 }
 
+// The distinct points a training step touches: point 0 (the conf read of empty neighbour slots),
+// then every neighbour pidx[e] >= 0 of the first S = counters[0] samples.  stamp[p] == step marks
+// a point already listed this step (the first lane to swap the stamp in owns it), so the table is
+// never cleared; a wave appends its fresh points with one atomic on the count.  The list order
+// follows the atomics (the consumers are order-free); its contents are deterministic.
+__global__ void __launch_bounds__(256) k_touched_points(const int32_t *__restrict__ pidx,
+                                                        const int32_t *__restrict__ counters, int64_t cap_slots,
+                                                        int32_t K, int64_t n_points, int32_t step, int32_t *stamp,
+                                                        int32_t *__restrict__ idx, unsigned long long *cnt,
+                                                        unsigned long long *cnt_next) {
+    int64_t n = (int64_t)counters[0] * K;
+    n = (n < cap_slots ? n : cap_slots) + 1;   // virtual slot 0 is point 0
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;   // the other step parity's count
+    const int lane = threadIdx.x & 63;
+    for (int64_t v0 = (int64_t)blockIdx.x * blockDim.x; v0 < n; v0 += stride) {
+        const int64_t v = v0 + threadIdx.x;
+        int32_t p = -1;
+        bool fresh = false;
+        if (v < n) {
+            p = v == 0 ? 0 : pidx[v - 1];
+            if (p >= 0 && p < n_points && stamp[p] != step)
+                fresh = atomicExch(&stamp[p], step) != step;
+        }
+        const uint64_t m = __ballot(fresh);
+        if (m == 0) continue;
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        int base = 0;
+        if (lane == leader) base = (int)atomicAdd(cnt, (unsigned long long)__popcll(m));
+        base = __shfl(base, leader);
+        if (fresh) {
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            idx[base + below] = p;
+        }
+    }
+}
+
 }  // namespace
 }  // namespace sgn
 
@@ -594,6 +631,20 @@ int sgn_colour_inputs(const int32_t *d_counters, const int32_t *d_work, const in
     a.v = d_v;
     a.samp = d_samp;
     hipLaunchKernelGGL(k_colour_inputs, dim3((unsigned)((n_cap * 32 + 255) / 256)), dim3(256), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+int sgn_touched_points(const int32_t *d_pidx, const int32_t *d_counters, int64_t s_cap, int32_t K, int64_t n_points,
+                       int32_t step, int32_t *d_stamp, int32_t *d_idx, int64_t *d_count2, sgn_stream_t stream) {
+    SGN_REQUIRE(s_cap >= 0 && K >= 1 && n_points >= 1 && step >= 0, "sgn_touched_points: bad size");
+    SGN_REQUIRE(d_pidx && d_counters && d_stamp && d_idx && d_count2, "sgn_touched_points: null buffer");
+    const int64_t slots = s_cap * K + 1;
+    int64_t blocks = (slots + 255) / 256;
+    blocks = blocks < 2048 ? blocks : 2048;
+    auto *c = reinterpret_cast<unsigned long long *>(d_count2);
+    hipLaunchKernelGGL(k_touched_points, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), d_pidx, d_counters,
+                       s_cap * K, K, n_points, step, d_stamp, d_idx, c + (step & 1), c + ((step + 1) & 1));
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

@@ -395,13 +395,16 @@ class HipTrainer:
         self.point_params = [points.points_embeding, points.points_color, points.points_dir, points.points_conf]
         # the reference's two Adam groups (mvs_points_volumetric_model.py:100-108); fused: one
         # kernel per group for the dense 47 M-element point update instead of the foreach chain
+        # kernel per group (sgn_adam_step, which also clears the gradient for the next step) instead
+        # of the foreach chain; the MLP group's flat 0.35 M elements the same way
         fused = self.device.type == "cuda"
-        self.opt_net = torch.optim.Adam([self.mlp.flat], lr=lr, betas=(0.9, 0.999), fused=fused)
         if fused:
+            self.opt_net = PointAdam([self.mlp.flat], lr=lr, betas=(0.9, 0.999))
             self.opt_pts = PointAdam(self.point_params, lr=plr, betas=(0.9, 0.999))
         else:
+            self.opt_net = torch.optim.Adam([self.mlp.flat], lr=lr, betas=(0.9, 0.999))
             self.opt_pts = torch.optim.Adam(self.point_params, lr=plr, betas=(0.9, 0.999))
-        self._pts_grad_clean = False  # PointAdam left the point gradients zeroed
+        self._grads_clean = False  # the optimizers left every gradient zeroed
         self.base_lr = (lr, plr)
         self.decay = (lr_decay_exp, lr_decay_iters)
         self.step_count = 0
@@ -516,6 +519,25 @@ class HipTrainer:
                                     _lib.ptr(scale), _lib.stream_handle()), "sgn_pow2_scale")
         return scale
 
+    def _touched(self, q, npts):
+        """The step's touched points (sgn_touched_points: an int32 list in no particular order and
+        its device count), for the single-GPU projection subset; no host sync, one launch."""
+        dev = self.device
+        if getattr(self, "_stamp_n", -1) != npts:
+            self._stamp = torch.full((npts,), -1, dtype=torch.int32, device=dev)
+            self._tlist = torch.empty(npts, dtype=torch.int32, device=dev)
+            self._tcount = torch.zeros(2, dtype=torch.int64, device=dev)
+            self._stamp_n, self._tstep = npts, 0
+        step = self._tstep
+        self._tstep = (step + 1) & 0x7fffffff
+        if self._tstep == 0:   # the stamp table outlived 2^31 steps: start it again
+            self._stamp_n = -1
+        K = self.opts.K
+        _lib.check(_lib.lib().sgn_touched_points(_lib.ptr(q.pidx), _lib.ptr(q.counters), q.pidx.numel() // K, K, npts,
+                                                 step, _lib.ptr(self._stamp), _lib.ptr(self._tlist),
+                                                 _lib.ptr(self._tcount), _lib.stream_handle()), "sgn_touched_points")
+        return self._tlist, self._tcount[step & 1]
+
     # -- one step ------------------------------------------------------------------------
     def backward(self, campos, rot, raydir, near, far, gt, labels=None):
         """Forward + backward + gradient all-reduce (no parameter update).  labels: (point_labels,
@@ -536,9 +558,9 @@ class HipTrainer:
         for p in self.point_params + [self.mlp.flat]:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-            elif not (self._pts_grad_clean and p is not self.mlp.flat):
+            elif not self._grads_clean:
                 p.grad.zero_()
-        self._pts_grad_clean = False
+        self._grads_clean = False
         dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         if dp:   # the point rows this rank's step can touch, and every rank's count, ride the same sync
             t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, self.points.xyz.shape[0])
@@ -652,9 +674,9 @@ class HipTrainer:
         for p in self.point_params + [self.mlp.flat]:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-            elif not (self._pts_grad_clean and p is not self.mlp.flat):
+            elif not self._grads_clean:
                 p.grad.zero_()
-        self._pts_grad_clean = False
+        self._grads_clean = False
         L = _lib.lib()
         st = _lib.stream_handle()
         pt = self._tables(campos, rot, raydir)
@@ -665,11 +687,12 @@ class HipTrainer:
             self._proj32 = torch.empty(max(nproj, 16), dtype=torch.uint8, device=dev)
         dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         t_idx = t_cnt = None
-        if dp or self.proj_subset:
+        if dp:
             t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, npts)
         if self.proj_subset:
-            _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(t_idx.to(torch.int32)),
-                                                      _lib.ptr(t_cnt), _lib.ptr(self._proj32), st),
+            idx32, cnt = self._touched(q, npts) if not dp else (t_idx.to(torch.int32), t_cnt)
+            _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(idx32),
+                                                      _lib.ptr(cnt), _lib.ptr(self._proj32), st),
                        "sgn_point_project_f32_subset")
         else:
             _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(self._proj32), st),
@@ -708,9 +731,9 @@ class HipTrainer:
         for p in self.point_params + [self.mlp.flat]:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-            elif not (self._pts_grad_clean and p is not self.mlp.flat):
+            elif not self._grads_clean:
                 p.grad.zero_()
-        self._pts_grad_clean = False
+        self._grads_clean = False
         L = _lib.lib()
         st = _lib.stream_handle()
         pt = self._tables(campos, rot, raydir)
@@ -721,14 +744,14 @@ class HipTrainer:
             self._proj32 = torch.empty(max(nproj, 16), dtype=torch.uint8, device=dev)
         dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         t_idx = t_cnt = None
-        if dp or self.proj_subset:   # the point rows this step's rays touch (device-side, no sync)
+        if dp:   # the point rows this step's rays touch, sorted for the sparse exchange (device-side, no sync)
             t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, npts)
         if self.proj_subset:
             # P and the packed records of the touched points only (~50 k of 1.2 M for a 4096-ray batch):
             # the rows read no other point, and the weights change every step
-            idx32 = t_idx.to(torch.int32)
+            idx32, cnt = self._touched(q, npts) if not dp else (t_idx.to(torch.int32), t_cnt)
             _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(idx32),
-                                                      _lib.ptr(t_cnt), _lib.ptr(self._proj32), st),
+                                                      _lib.ptr(cnt), _lib.ptr(self._proj32), st),
                        "sgn_point_project_f32_subset")
         else:
             _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(self._proj32), st),
@@ -975,7 +998,7 @@ class HipTrainer:
         self._set_lr()
         self.opt_net.step()
         self.opt_pts.step()
-        self._pts_grad_clean = isinstance(self.opt_pts, PointAdam) and self.opt_pts.zero_grad_in_step
+        self._grads_clean = all(isinstance(o, PointAdam) and o.zero_grad_in_step for o in (self.opt_net, self.opt_pts))
         self.step_count += 1
 
     def step(self, campos, rot, raydir, near, far, gt, labels=None):
