@@ -395,6 +395,11 @@ int sgn_grad_accumulate(int32_t n_seg, const sgn_grad_segment *segs, const float
                         sgn_stream_t stream);
 /* Clears n_seg device regions (d_ptr[i]: 16-B aligned, bytes[i] a multiple of 16; host arrays). */
 int sgn_zero_segments(int32_t n_seg, void *const *d_ptr, const int64_t *bytes, sgn_stream_t stream);
+/* Copies n_seg device regions in one launch: d_dst[i] = d_src[i] (bytes[i] bytes; d_src[i] null:
+ * zeros), any alignment (16-B units where both ends and the length allow).  Host arrays.  The
+ * training step's graph inputs / outputs and clears, instead of one copy or fill per tensor. */
+int sgn_copy_segments(int32_t n_seg, const void *const *d_src, void *const *d_dst, const int64_t *bytes,
+                      sgn_stream_t stream);
 /* Index gathers from one fp32 source (the flat MLP parameter): dst[j] = src[idx[j]], 0 for idx
  * outside [0, n_src); stored as fp32 or, with fp16 != 0, rounded to fp16 (nearest even) -- the
  * device re-pack of the MFMA weight blobs each training step. */
@@ -420,10 +425,12 @@ int sgn_pack_scaled_f32(const float *d_flat, int64_t n_flat, int32_t n_layers, c
 /* The f16 training step's captured loss stage inputs over its item capacity n_cap: for item
  * i < d_counters[1] (sgn_query's work-item count) d_fs32[i] = fp32 of d_fs16[i] ([n_cap][256] fp16,
  * sgn_aggregate_train_fwd's blended features), d_al32[i] = d_feat[work[i]].alpha, d_v[i] = the
- * direction of the item's ray, d_samp[i] = work[i]; padding items get zeros, ray 0 and s_cap. */
+ * direction of the item's ray, d_samp[i] = work[i]; padding items get zeros, ray 0 and s_cap.
+ * d_vpe (or NULL): [n_cap][32] the colour MLP's PE(viewdir) (sin | cos of v 2^f, f < 4, per
+ * component; point_aggregators.py:772-780), 1 in column 24 (colour 0's bias column), zeros after. */
 int sgn_colour_inputs(const int32_t *d_counters, const int32_t *d_work, const int32_t *d_samp_ray, int64_t n_cap,
                       int64_t s_cap, const void *d_fs16, const float *d_feat, const float *d_raydir, float *d_fs32,
-                      float *d_al32, float *d_v, int32_t *d_samp, sgn_stream_t stream);
+                      float *d_al32, float *d_v, int32_t *d_samp, float *d_vpe, sgn_stream_t stream);
 /* The backward's power-of-two loss scale: d_out[0] = 2^-floor(log2(max(max|a|, max|b|, 1e-30)))
  * over two fp32 device arrays (a NaN propagates), in two launches with no host sync; d_ws:
  * sgn_pow2_scale_workspace_bytes() of device scratch. */
@@ -486,6 +493,8 @@ typedef struct {
     uint32_t *amax_out, *amax_out2;
     float *part;
     int32_t splits;
+    int32_t products;   /* 3 (or 0): hi/lo products, fp32 accuracy; 1: the hi halves only (fp16 operands,
+                           the f16 training step's colour MLP; colour-layer shapes only) */
 } sgn_x3_gemm_args;
 int sgn_x3_gemm(const sgn_x3_gemm_args *g, sgn_stream_t stream);
 

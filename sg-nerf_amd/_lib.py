@@ -86,7 +86,7 @@ class X3GemmArgs(ctypes.Structure):
     _fields_ = [("a", X3Operand), ("b", X3Operand), ("mode", c_i32), ("M", c_i32), ("N", c_i32), ("K", c_i32),
                 ("d_rows", c_vp), ("bias", c_vp), ("act", c_i32), ("mask", c_vp), ("ldm", c_i64), ("out", c_vp),
                 ("ldo", c_i64), ("out_cols", c_i32), ("out2", c_vp), ("ldo2", c_i64), ("amax_out", c_vp),
-                ("amax_out2", c_vp), ("part", c_vp), ("splits", c_i32)]
+                ("amax_out2", c_vp), ("part", c_vp), ("splits", c_i32), ("products", c_i32)]
 
 
 class PartialSegment(ctypes.Structure):
@@ -145,10 +145,12 @@ SIGNATURES = {
                                         c_vp]),
     "sgn_grad_accumulate": (c_i32, [c_i32, ctypes.POINTER(GradSegment), c_vp, c_vp, c_vp]),
     "sgn_zero_segments": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),
+    "sgn_copy_segments": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),
     "sgn_gather_segments": (c_i32, [c_i32, ctypes.POINTER(GatherSegment), c_vp, c_i64, c_vp]),
     "sgn_pack_scaled_f32": (c_i32, [c_vp, c_i64, c_i32, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_vp, c_i64, c_vp,
                                     c_i64, c_vp, c_vp, c_vp, c_vp]),
-    "sgn_colour_inputs": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "sgn_colour_inputs": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp]),
     "sgn_pow2_scale_workspace_bytes": (c_sz, []),
     "sgn_pow2_scale": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "sgn_touched_points": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
@@ -229,6 +231,18 @@ def check(rc, what):
     if rc != 0:
         msg = lib().sgn_last_error()
         raise SgnError(f"{what} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def copy_segments(pairs, stream=None):
+    """One sgn_copy_segments launch: pairs of (src tensor or None = clear, dst tensor), byte counts
+    from dst (the source must hold at least as many bytes)."""
+    n = len(pairs)
+    src = (c_vp * n)(*[None if s is None else s.data_ptr() for s, _ in pairs])
+    dst = (c_vp * n)(*[d.data_ptr() for _, d in pairs])
+    nb = (c_i64 * n)(*[d.numel() * d.element_size() for _, d in pairs])
+    for s, d in pairs:
+        assert d.is_contiguous() and (s is None or (s.is_contiguous() and s.numel() * s.element_size() >= d.numel() * d.element_size()))
+    check(lib().sgn_copy_segments(n, src, dst, nb, stream_handle() if stream is None else stream), "sgn_copy_segments")
 
 
 def ptr(t):

@@ -7,8 +7,9 @@
 //   m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // The point group is ~47 M fp32 elements per step (embedding 32 + colour 3 + dir 3 + conf 1
-// per point): pure HBM streaming, 16 B read + 12 B written per element (+4 B when the kernel
-// also clears the gradient for the next step, which replaces a separate fill pass).
+// per point): pure HBM streaming, 16 B read + 12 B written per element (+4 B for the elements
+// whose gradient is non-zero when the kernel also clears the gradient for the next step, which
+// replaces a separate fill pass).
 // One thread per float4, every access a 16-B vector load/store.
 //
 // Column sums: db_l = sum over rows of the fp16 delta tile [rows][cols] (fp32 accumulate),
@@ -57,7 +58,10 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         reinterpret_cast<float4 *>(a.p)[i] = p;
         reinterpret_cast<float4 *>(a.m)[i] = m;
         reinterpret_cast<float4 *>(a.v)[i] = v;
-        if (a.zero_grad) reinterpret_cast<float4 *>(a.g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        // most rows' gradients are already zero (a step touches ~50 k of 1.2 M points): store only
+        // the others, 4 of the 32 B per element skipped for the untouched rows
+        if (a.zero_grad && (g.x != 0.f || g.y != 0.f || g.z != 0.f || g.w != 0.f))
+            reinterpret_cast<float4 *>(a.g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // ragged tail (n % 4 elements), first workgroup only
     if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
@@ -222,6 +226,31 @@ __global__ __launch_bounds__(256) void k_zero_segments(ZeroArgs a) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = z;
 }
 
+struct CopyArgs {
+    const char *src[kMaxSegs];   // null: clear
+    char *dst[kMaxSegs];
+    int64_t bytes[kMaxSegs];
+};
+
+// dst = src (or zeros) per segment, in 16-B, 4-B or single-byte units as the segment's alignment allows
+__global__ __launch_bounds__(256) void k_copy_segments(CopyArgs a) {
+    const int sg = blockIdx.y;
+    const char *src = a.src[sg];
+    char *dst = a.dst[sg];
+    const int64_t n = a.bytes[sg];
+    const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x, st = (int64_t)gridDim.x * 256;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | (uintptr_t)n;
+    if (!(al & 15)) {
+        for (int64_t i = t0; i < n / 16; i += st)
+            reinterpret_cast<uint4 *>(dst)[i] = src ? reinterpret_cast<const uint4 *>(src)[i] : make_uint4(0u, 0u, 0u, 0u);
+    } else if (!(al & 3)) {
+        for (int64_t i = t0; i < n / 4; i += st)
+            reinterpret_cast<uint32_t *>(dst)[i] = src ? reinterpret_cast<const uint32_t *>(src)[i] : 0u;
+    } else {
+        for (int64_t i = t0; i < n; i += st) dst[i] = src ? src[i] : (char)0;
+    }
+}
+
 struct GatherArgs {
     sgn_gather_segment s[kMaxSegs];
     const float *src;
@@ -361,6 +390,7 @@ struct ColourInArgs {
     const float *feat, *raydir;
     float *fs32, *al32, *v;
     int32_t *samp;
+    float *vpe;   // [n_cap][32] PE(viewdir) | 1 | 0 or null
 };
 
 __global__ __launch_bounds__(256) void k_colour_inputs(ColourInArgs a) {
@@ -389,6 +419,18 @@ __global__ __launch_bounds__(256) void k_colour_inputs(ColourInArgs a) {
         a.v[i * 3 + 1] = a.raydir[r * 3 + 1];
         a.v[i * 3 + 2] = a.raydir[r * 3 + 2];
         a.samp[i] = ok ? s : (int32_t)a.s_cap;
+    }
+    if (a.vpe) {   // PE(viewdir), ori=True without the raw v (point_aggregators.py:772-780): sin | cos of v 2^f
+        float x = c8 == 24 ? 1.f : 0.f;
+        if (c8 < 24) {
+            const int jj = c8 < 12 ? c8 : c8 - 12, c = jj >> 2, f = jj & 3;
+            const int32_t s = ok ? a.work[i] : 0;
+            const int64_t r = ok ? (int64_t)a.samp_ray[s] : 0;
+            float sn, cs;
+            sincosf(a.raydir[r * 3 + c] * (float)(1 << f), &sn, &cs);
+            x = c8 < 12 ? sn : cs;
+        }
+        a.vpe[i * 32 + c8] = x;
     }
 }
 
@@ -554,6 +596,28 @@ int sgn_zero_segments(int32_t n_seg, void *const *d_ptr, const int64_t *bytes, s
     return 0;
 }
 
+int sgn_copy_segments(int32_t n_seg, const void *const *d_src, void *const *d_dst, const int64_t *bytes,
+                      sgn_stream_t stream) {
+    SGN_REQUIRE(n_seg >= 0 && n_seg <= kMaxSegs, "sgn_copy_segments: 0 <= n_seg <= 16");
+    if (n_seg == 0) return 0;
+    SGN_REQUIRE(d_src && d_dst && bytes, "sgn_copy_segments: null argument");
+    CopyArgs a;
+    int64_t nmax = 0;
+    for (int i = 0; i < n_seg; ++i) {
+        SGN_REQUIRE(bytes[i] >= 0 && (bytes[i] == 0 || d_dst[i]), "sgn_copy_segments: bad segment");
+        a.src[i] = static_cast<const char *>(d_src[i]);
+        a.dst[i] = static_cast<char *>(d_dst[i]);
+        a.bytes[i] = bytes[i];
+        const uintptr_t al = reinterpret_cast<uintptr_t>(d_src[i]) | reinterpret_cast<uintptr_t>(d_dst[i]) | (uintptr_t)bytes[i];
+        nmax = std::max(nmax, (al & 15) == 0 ? bytes[i] / 16 : (al & 3) == 0 ? bytes[i] / 4 : bytes[i]);
+    }
+    if (nmax == 0) return 0;
+    const int64_t blocks = std::min<int64_t>((nmax + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_copy_segments, dim3((unsigned)blocks, n_seg), dim3(256), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
 int sgn_gather_segments(int32_t n_seg, const sgn_gather_segment *segs, const float *d_src, int64_t n_src,
                         sgn_stream_t stream) {
     SGN_REQUIRE(n_seg >= 0 && n_seg <= kMaxSegs, "sgn_gather_segments: 0 <= n_seg <= 16");
@@ -610,7 +674,7 @@ int sgn_pack_scaled_f32(const float *d_flat, int64_t n_flat, int32_t n_layers, c
 
 int sgn_colour_inputs(const int32_t *d_counters, const int32_t *d_work, const int32_t *d_samp_ray, int64_t n_cap,
                       int64_t s_cap, const void *d_fs16, const float *d_feat, const float *d_raydir, float *d_fs32,
-                      float *d_al32, float *d_v, int32_t *d_samp, sgn_stream_t stream) {
+                      float *d_al32, float *d_v, int32_t *d_samp, float *d_vpe, sgn_stream_t stream) {
     SGN_REQUIRE(n_cap >= 0 && s_cap >= 0 && s_cap < 0x7fffffff, "sgn_colour_inputs: bad capacity");
     if (n_cap == 0) return 0;
     SGN_REQUIRE(d_counters && d_work && d_samp_ray && d_fs16 && d_feat && d_raydir && d_fs32 && d_al32 && d_v && d_samp,
@@ -630,6 +694,7 @@ int sgn_colour_inputs(const int32_t *d_counters, const int32_t *d_work, const in
     a.al32 = d_al32;
     a.v = d_v;
     a.samp = d_samp;
+    a.vpe = d_vpe;
     hipLaunchKernelGGL(k_colour_inputs, dim3((unsigned)((n_cap * 32 + 255) / 256)), dim3(256), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;

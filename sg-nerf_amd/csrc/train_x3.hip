@@ -180,6 +180,7 @@ struct QStage {
         }
     }
     // lane fragments (column 4 q + j, octet oc) -> LDS ((tile * 2 + kstep) * 2 + hi/lo) * FRAG + L * 16
+    template <bool P1 = false>
     __device__ __forceinline__ void store(char *base, float scale, int tid) const {
         if (tid >= 4 * Q) return;
         const int q = tid % Q, oc = tid / Q;
@@ -193,12 +194,13 @@ struct QStage {
             const X3Pair p = split8_scaled(x, scale);
             char *d = base + ((t * 2 + s) * 2) * FRAG + L * 16;
             *(h8 *)d = p.hi;
-            *(h8 *)(d + FRAG) = p.lo;
+            if (!P1) *(h8 *)(d + FRAG) = p.lo;
         }
     }
 };
 
-template <int WM, int WN>
+// P1: the hi halves only (one fp16 product per fp32 product: the f16 training step's accuracy)
+template <int WM, int WN, bool P1 = false>
 __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
     constexpr int TA = 4 * WM, TB = WN, BM = 32 * TA, BN = 32 * TB;
     constexpr int ABYTES = TA * 4 * FRAG, STAGE = (TA + TB) * 4 * FRAG;
@@ -237,8 +239,10 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
                 const h8 bh = *(const h8 *)p, bl = *(const h8 *)(p + FRAG);
 #pragma unroll
                 for (int a = 0; a < WM; ++a) {
-                    acc[a][b] = mfma32(al[a], bh, acc[a][b]);
-                    acc[a][b] = mfma32(ah[a], bl, acc[a][b]);
+                    if (!P1) {
+                        acc[a][b] = mfma32(al[a], bh, acc[a][b]);
+                        acc[a][b] = mfma32(ah[a], bl, acc[a][b]);
+                    }
                     acc[a][b] = mfma32(ah[a], bh, acc[a][b]);
                 }
             }
@@ -251,8 +255,8 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
             a1.load(g.A, m0, r0 + 32, r1, tid);
             b1.load(g.B, n0, r0 + 32, r1, tid);
         }
-        a0.store(lds, fa, tid);
-        b0.store(lds + ABYTES, fb, tid);
+        a0.template store<P1>(lds, fa, tid);
+        b0.template store<P1>(lds + ABYTES, fb, tid);
         __syncthreads();
         // two stages per trip, so the register sets keep static names: stage kb in LDS buffer kb & 1,
         // stage kb + 1 in registers, stage kb + 2 loading
@@ -263,8 +267,8 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
             }
             compute(lds);
             if (kb + 1 < nkb) {
-                a1.store(lds + STAGE, fa, tid);
-                b1.store(lds + STAGE + ABYTES, fb, tid);
+                a1.template store<P1>(lds + STAGE, fa, tid);
+                b1.template store<P1>(lds + STAGE + ABYTES, fb, tid);
             }
             __syncthreads();
             if (kb + 1 >= nkb) break;
@@ -274,8 +278,8 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
             }
             compute(lds + STAGE);
             if (kb + 2 < nkb) {
-                a0.store(lds, fa, tid);
-                b0.store(lds + ABYTES, fb, tid);
+                a0.template store<P1>(lds, fa, tid);
+                b0.template store<P1>(lds + ABYTES, fb, tid);
             }
             __syncthreads();
         }
@@ -335,7 +339,7 @@ __device__ __forceinline__ ARow arow(const Opnd &o, int row, int lim) {
     return a;
 }
 
-template <int KS, int WN>
+template <int KS, int WN, bool P1 = false>
 __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
     __shared__ __attribute__((aligned(16))) char lds[KS * WN * 2 * FRAG];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
         const X3Pair x = split8_scaled(v, fb);
         char *d = lds + ((s * WN + t) * 2) * FRAG + fl * 16;
         *(h8 *)d = x.hi;
-        *(h8 *)(d + FRAG) = x.lo;
+        if (!P1) *(h8 *)(d + FRAG) = x.lo;
     }
     __syncthreads();
     float am1 = 0.f, am2 = 0.f;
@@ -379,9 +383,12 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
             const char *p = lds + (s * WN * 2) * FRAG + lane * 16;
 #pragma unroll
             for (int t = 0; t < WN; ++t) {
-                const h8 bh = *(const h8 *)(p + (2 * t) * FRAG), bl = *(const h8 *)(p + (2 * t + 1) * FRAG);
-                acc[t] = mfma32(x.lo, bh, acc[t]);
-                acc[t] = mfma32(x.hi, bl, acc[t]);
+                const h8 bh = *(const h8 *)(p + (2 * t) * FRAG);
+                if (!P1) {
+                    const h8 bl = *(const h8 *)(p + (2 * t + 1) * FRAG);
+                    acc[t] = mfma32(x.lo, bh, acc[t]);
+                    acc[t] = mfma32(x.hi, bl, acc[t]);
+                }
                 acc[t] = mfma32(x.hi, bh, acc[t]);
             }
         }
@@ -1007,6 +1014,8 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
     k.out = g.out; k.ldo = g.ldo; k.out_cols = g.out_cols < g.N ? g.out_cols : g.N;
     k.out2 = g.out2; k.ldo2 = g.ldo2; k.amax_out = g.amax_out; k.amax_out2 = g.amax_out2;
     k.part = g.part;
+    SGN_REQUIRE(g.products == 0 || g.products == 1 || g.products == 3, "products: 3 (0) or 1");
+    const bool p1 = g.products == 1;
     hipStream_t st = as_stream(stream);
     if (g.mode == 0) {
         if (g.M == 0) return 0;
@@ -1022,7 +1031,11 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
         gy = gy < 1 ? 1 : gy > tiles ? tiles : gy;
         const int ks = (g.K + 15) / 16;
         const dim3 grid(nb, gy);
-        if (ks <= 8) {
+        if (p1) {
+            SGN_REQUIRE(!w96 && ks != 16 && ks <= 18, "products 1: the colour layers' shapes (K <= 128 or 272..288, N > 96)");
+            if (ks <= 8) hipLaunchKernelGGL((k_x3rows<8, 4, true>), grid, dim3(TPB), 0, st, k);
+            else hipLaunchKernelGGL((k_x3rows<18, 4, true>), grid, dim3(TPB), 0, st, k);
+        } else if (ks <= 8) {
             if (w96) hipLaunchKernelGGL((k_x3rows<8, 3>), grid, dim3(TPB), 0, st, k);
             else hipLaunchKernelGGL((k_x3rows<8, 4>), grid, dim3(TPB), 0, st, k);
         } else if (ks <= 16) {
@@ -1039,7 +1052,11 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
         const int BN = g.N <= 32 ? 32 : (BM == 128 && g.N <= 160) ? 160 : 96;
         const int nbm = (g.M + BM - 1) / BM, nbn = (g.N + BN - 1) / BN;
         const dim3 grid(nbm * nbn, g.splits);
-        if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3tn<2, 3>), grid, dim3(TPB), 0, st, k);
+        if (p1) {
+            SGN_REQUIRE(BM == 128 && (BN == 160 || BN == 96), "products 1: the colour layers' shapes (M <= 128, N > 32)");
+            if (BN == 160) hipLaunchKernelGGL((k_x3tn<1, 5, true>), grid, dim3(TPB), 0, st, k);
+            else hipLaunchKernelGGL((k_x3tn<1, 3, true>), grid, dim3(TPB), 0, st, k);
+        } else if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3tn<2, 3>), grid, dim3(TPB), 0, st, k);
         else if (BM == 256) hipLaunchKernelGGL((k_x3tn<2, 1>), grid, dim3(TPB), 0, st, k);
         else if (BN == 160) hipLaunchKernelGGL((k_x3tn<1, 5>), grid, dim3(TPB), 0, st, k);
         else if (BN == 96) hipLaunchKernelGGL((k_x3tn<1, 3>), grid, dim3(TPB), 0, st, k);

@@ -324,24 +324,28 @@ class ColourStep:
     """The colour MLP, the losses and their backward for the f16 training step on the same hand-written
     kernels as F32Step (precision "f16" only changes the row MLP): items are the query's work-list
     positions (k_agg_rows' f_s rows), `cap` of them at most, the device count at q.counters[1].
-    Per step: PE(viewdir), 3 x sgn_x3_gemm forward + sgn_train_colour_head (rgb into feat), sgn_loss_train,
-    the colour backward (head, 2 masked dy W, d f_s = dy1 W0[:, :256]), the three weight gradients as
+    Per step (PE(viewdir) arrives from sgn_colour_inputs): 3 x sgn_x3_gemm forward + sgn_train_colour_head
+    (rgb into feat), sgn_loss_train,
+    the colour backward (head, 2 masked dy W, d f_s = dy1 W0[:, :256]; one fp16 product per multiply-add,
+    the step's delta precision), the three weight gradients as
     split-K partials and one sgn_reduce_partials into the flat gradient.  No autograd, no host sync: it
     runs inside the f16 step's captured graph."""
 
     A_DY3, A_DY2, A_DY1 = range(3)
 
-    def __init__(self, trainer, q, cap, fs32, vdir, feat, R):
+    def __init__(self, trainer, q, cap, fs32, vdir, feat, R, products=1):
+        """products: of the backward GEMMs, 1 (the f16 step's delta precision: one fp16 product per
+        multiply-add) or 3 (split-fp16 at fp32 accuracy); the forward keeps 3, so the rendered colour and
+        the losses are the eager fp32 colour MLP's."""
         L = _lib.lib()
         self.trainer, self.q, self.cap, self.R = trainer, q, max(cap, 1), R
+        self.products = products
         self.qo = q.abi()
         dev = trainer.device
         f32 = dict(dtype=torch.float32, device=dev)
         cap = self.cap
         self.fs32, self.vdir, self.feat = fs32, vdir, feat
-        self.vpe = torch.zeros(cap, 32, **f32)
-        self.vpe[:, 24] = 1.0                      # the ones column (colour 0's bias)
-        self.freq = torch.tensor([1.0, 2.0, 4.0, 8.0], **f32)
+        self.vpe = torch.zeros(cap, 32, **f32)     # sgn_colour_inputs: PE(viewdir), the ones column 24, zeros
         self.h = [torch.empty(cap, 128, **f32) for _ in range(3)]
         self.dy = [torch.empty(cap, 128, **f32) for _ in range(3)]
         self.dfs = torch.empty(cap, 256, **f32)
@@ -405,6 +409,8 @@ class ColourStep:
                               _operand(fs, 256, 281, 1, p2=vpe, ld2=32, csplit=256), 128, 281, cap, n_items, _addr(pc[2]),
                               SPLITS_ITEMS))
         self.g_bwd = G
+        for gs in self.g_bwd:
+            gs.products = self.products
         segs = []
 
         def seg(part, splits, M, N, name, n_in, bias_col):
@@ -432,11 +438,7 @@ class ColourStep:
         tr, qo = self.trainer, self.qo
         P = tr.points
         cnt = ctypes.c_void_p(_addr(self.q.counters, 1))
-        # PE(viewdir) ori=True without the raw v (point_aggregators.py:772-780): sin | cos of v 2^f
-        v = self.vdir
-        x = (v[:, :, None] * self.freq).reshape(-1, 12)
-        self.vpe[:, :12] = torch.sin(x)
-        self.vpe[:, 12:24] = torch.cos(x)
+        # self.vpe (PE(viewdir) | 1 | 0) was written by sgn_colour_inputs with the items' other inputs
         self.amax.zero_()
         for gs in self.g_fwd:
             ck(L.sgn_x3_gemm(ctypes.byref(gs), st), "sgn_x3_gemm")

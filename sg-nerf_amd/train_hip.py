@@ -817,6 +817,7 @@ class HipTrainer:
         _lib.check(_lib.lib().sgn_colour_inputs(_lib.ptr(q.counters), _lib.ptr(q.work), _lib.ptr(q.samp_ray), Nc, Sc,
                                                 _lib.ptr(self.fs), _lib.ptr(self.feat), _lib.ptr(st["raydir"]),
                                                 _lib.ptr(fs32), _lib.ptr(al32), _lib.ptr(v), _lib.ptr(samp),
+                                                _lib.ptr(st["col"].vpe) if "col" in st else None,
                                                 _lib.stream_handle()), "sgn_colour_inputs")
         if "col" in st:   # hand-written colour MLP, losses and backward (train_f32.ColourStep)
             losses, full, mask, dfs, dfeat = st["col"].run(st["campos"], st["rot"], st["gt"], self._loss_params())
@@ -825,7 +826,7 @@ class HipTrainer:
             total = losses[0] + 3e-6 + 1e-4 * losses[1]
             names = ["ray_masked_coarse_raycolor", "ray_miss_coarse_raycolor", "coarse_raycolor", "conf_coefficient"]
             return {"scalars": torch.stack([total, losses[0], losses[2], losses[3], losses[1]]), "names": names,
-                    "full": full, "ray_mask": mask.bool(), "dfs": dfs, "dal": dal, "scale": scale}
+                    "full": full, "ray_mask": mask, "dfs": dfs, "dal": dal, "scale": scale}
         fs32.grad = al32.grad = None   # backward assigns fresh (graph-pool) gradients: no clear, no accumulate
         feat_s = torch.cat([al32[:, None], self._colour(fs32, v)], dim=-1)   # colour grads -> flat.grad
         featS = torch.zeros(Sc + 1, 4, device=dev).index_put((samp,), feat_s)[:Sc]
@@ -888,15 +889,23 @@ class HipTrainer:
             P.points_conf.grad.copy_(keep[1])
             st["graph"] = g
             self._graphs[key] = st
-        st["raydir"].copy_(raydir)
-        st["gt"].copy_(gt.reshape(-1, 3))
-        st["campos"].copy_(campos)
-        st["rot"].copy_(rot)
+        g3 = gt.reshape(-1, 3)
+        if g3.dtype != torch.float32 or g3.device != dev or not g3.is_contiguous():
+            g3 = g3.to(dev, torch.float32).contiguous()
+        # the step's inputs into the graph's static buffers: one launch
+        _lib.copy_segments([(raydir, st["raydir"]), (g3, st["gt"]), (campos, st["campos"]), (rot, st["rot"])])
         st["graph"].replay()
         out = st["out"]
-        sc = out["scalars"].clone()             # the loss and its parts: one copy out of the graph's buffers
+        # the loss, its parts, the rendered colour and the ray mask out of the graph's buffers: one
+        # launch into one fresh allocation (the caller may keep them across steps)
+        nsc = out["scalars"].numel()
+        o_full = 8 * (-(-nsc // 8))
+        buf = torch.empty(o_full + 3 * R + -(-R // 4), dtype=torch.float32, device=dev)
+        sc, full = buf[:nsc], buf[o_full:o_full + 3 * R].view(R, 3)
+        ray_mask = buf[o_full + 3 * R:].view(torch.bool)[:R]
+        _lib.copy_segments([(out["scalars"], sc), (out["full"], full), (out["ray_mask"], ray_mask)])
         return {"total": sc[0], "parts": {k: sc[1 + i] for i, k in enumerate(out["names"])},
-                "full": out["full"].clone(), "ray_mask": out["ray_mask"].clone(),
+                "full": full, "ray_mask": ray_mask,
                 "dfs": out["dfs"], "dal": out["dal"], "scale": out["scale"]}
 
     def _dst_maps(self, name, x_cols, ix):

@@ -116,7 +116,7 @@ def test_argument_errors_are_reported_without_gpu():
     rc = L.sgn_gather_segments(1, gt, fake, 8, None)
     assert rc != 0 and b"bad segment" in L.sgn_last_error()
     assert L.sgn_grad_accumulate(0, None, None, None, None) == 0   # nothing to do: no launch
-    rc = L.sgn_colour_inputs(fake, fake, fake, 16, 64, ctypes.c_void_p(24), fake, fake, fake, fake, fake, fake, None)
+    rc = L.sgn_colour_inputs(fake, fake, fake, 16, 64, ctypes.c_void_p(24), fake, fake, fake, fake, fake, fake, None, None)
     assert rc != 0 and b"aligned" in L.sgn_last_error()
     rc = L.sgn_pack_scaled_f32(fake, 100, 17, None, None, fake, 8, fake, 8, fake, fake, fake, None)
     assert rc != 0 and b"n_layers" in L.sgn_last_error()

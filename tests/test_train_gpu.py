@@ -426,7 +426,10 @@ def test_graph_captured_step_matches_eager_step():
     assert abs(le[0] - lg[0]) <= 1e-5 * abs(le[0])
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-3 * abs(a)
-    assert max(ge_err.values()) <= 2e-4, ge_err       # measured <= 8.5e-5 (points_embeding)
+    # the graph path's colour backward multiplies in fp16 (ColourStep products=1, the step's delta
+    # precision) where the eager path's torch autograd runs fp32: measured 7.2e-4 (block3.2), every
+    # tensor far inside the f16 step's bars against fp32 autograd (GRAD_TOL_MLP / GRAD_TOL_POINTS)
+    assert max(ge_err.values()) <= 2e-3, ge_err
     assert max(pe_err.values()) <= UPDATE_TOL, (pe_err, ee_err)
 
 
@@ -495,10 +498,11 @@ def test_colour_inputs_kernel_matches_torch():
     al32 = torch.full((n_cap,), float("nan"), device=DEV)
     v = torch.full((n_cap, 3), float("nan"), device=DEV)
     samp = torch.full((n_cap,), -7, dtype=torch.int32, device=DEV)
+    vpe = torch.full((n_cap, 32), float("nan"), device=DEV)
     p = _lib.ptr
     _lib.check(_lib.lib().sgn_colour_inputs(p(dv["counters"]), p(dv["work"]), p(dv["samp_ray"]), n_cap, s_cap,
                                             p(dv["fs16"]), p(dv["feat"]), p(dv["raydir"]), p(fs32), p(al32), p(v),
-                                            p(samp), _lib.stream_handle()), "sgn_colour_inputs")
+                                            p(samp), p(vpe), _lib.stream_handle()), "sgn_colour_inputs")
     torch.cuda.synchronize()
     ok = torch.arange(n_cap) < n
     wk = work.long()
@@ -510,6 +514,26 @@ def test_colour_inputs_kernel_matches_torch():
     assert torch.equal(al32.cpu(), exp_al)
     assert torch.equal(v.cpu(), exp_v)
     assert torch.equal(samp.cpu(), exp_samp)
+    # PE(viewdir) as the torch construction it replaced (sin | cos of v 2^f), the ones column, zeros
+    x = (exp_v[:, :, None] * torch.tensor([1.0, 2.0, 4.0, 8.0])).reshape(-1, 12)
+    exp_vpe = torch.cat([torch.sin(x), torch.cos(x), torch.ones(n_cap, 1), torch.zeros(n_cap, 7)], dim=1)
+    torch.testing.assert_close(vpe.cpu(), exp_vpe, rtol=0, atol=2e-6)
+
+
+def test_copy_segments_kernel():
+    """sgn_copy_segments: 16-B, 4-B and byte-granular segments (odd offsets and lengths) and a
+    clear (null source) in one launch; bytes outside each destination untouched."""
+    g = torch.Generator().manual_seed(5)
+    src = torch.randint(0, 255, (4096,), generator=g, dtype=torch.uint8).to(DEV)
+    dst = torch.full((4096,), 7, dtype=torch.uint8, device=DEV)
+    spans = [(0, 64, 1024), (4, 1200, 36), (3, 2001, 13), (None, 3000, 100)]   # (src off, dst off, bytes)
+    _lib.copy_segments([(None if so is None else src[so:so + n], dst[do:do + n]) for so, do, n in spans])
+    torch.cuda.synchronize()
+    exp = torch.full((4096,), 7, dtype=torch.uint8)
+    s = src.cpu()
+    for so, do, n in spans:
+        exp[do:do + n] = 0 if so is None else s[so:so + n]
+    assert torch.equal(dst.cpu(), exp)
 
 
 def test_touched_points_kernel_matches_torch():
