@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 10
+#define SGN_ABI_VERSION 11
 
 /* ---- grid ------------------------------------------------------------- */
 
