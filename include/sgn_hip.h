@@ -357,6 +357,11 @@ int sgn_train_pack_index_sg(int32_t bpnet_dim, int32_t *out, int64_t n);
  * step's zero_grad).  All buffers 16-B aligned. */
 int sgn_adam_step(float *d_param, float *d_grad, float *d_exp_avg, float *d_exp_avg_sq, int64_t n, double lr,
                   double beta1, double beta2, double eps, int64_t step, int32_t zero_grad, sgn_stream_t stream);
+/* The same update for n_t <= 8 tensors of one parameter group (host arrays of device pointers and
+ * element counts; one lr / step for all) in one launch. */
+int sgn_adam_step_multi(int32_t n_t, float *const *d_param, float *const *d_grad, float *const *d_exp_avg,
+                        float *const *d_exp_avg_sq, const int64_t *n, double lr, double beta1, double beta2, double eps,
+                        int64_t step, int32_t zero_grad, sgn_stream_t stream);
 /* d_out[i][c] = sum over r < rows of d_x[i][r][c] (fp16 in, fp32 out, deterministic order),
  * for count <= 8 matrices [rows][256] (the bias gradients db = sum of the deltas,
  * torch.sum(d, 0) in the reference's autograd of nn.Linear).  d_x: host array of device

@@ -139,6 +139,9 @@ SIGNATURES = {
     "sgn_train_pack_index_sg": (c_i32, [c_i32, ctypes.POINTER(c_i32), c_i64]),
     "sgn_adam_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                ctypes.c_double, c_i64, c_i32, c_vp]),
+    "sgn_adam_step_multi": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
+                                     ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_double, c_i64, c_i32, c_vp]),
     "sgn_colsum_workspace_bytes": (c_sz, [c_i32]),
     "sgn_colsum_f16": (c_i32, [c_i32, ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp, c_vp]),
     "sgn_colsum_f16_weighted": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp,

@@ -29,9 +29,13 @@
 namespace sgn {
 namespace {
 
+constexpr int kMaxAdamTensors = 8;
+
 struct AdamArgs {
-    float *p, *g, *m, *v;
-    int64_t n;
+    float *p[kMaxAdamTensors], *g[kMaxAdamTensors], *m[kMaxAdamTensors], *v[kMaxAdamTensors];
+    int64_t n[kMaxAdamTensors];
+    int64_t off4[kMaxAdamTensors + 1];   // prefix sums of the tensors' whole float4 counts
+    int nt;
     float b1, b2, omb1, omb2, step_size, bc2_sqrt, eps;
     int zero_grad;
 };
@@ -43,35 +47,73 @@ __device__ __forceinline__ void adam1(float &p, float &g, float &m, float &v, co
     p -= a.step_size * m / denom;
 }
 
+// float4 number i of the group's concatenated tensors -> (tensor, float4 index in it)
+__device__ __forceinline__ int adam_tensor(const AdamArgs &a, int64_t i) {
+    int t = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxAdamTensors; ++k) t += (k < a.nt && i >= a.off4[k]);
+    return t;
+}
+
+struct Adam4 {
+    float4 p, g, m, v;
+    int t;
+    int64_t j;
+};
+
+__device__ __forceinline__ void adam_load(const AdamArgs &a, int64_t i, Adam4 &x) {
+    x.t = adam_tensor(a, i);
+    x.j = i - a.off4[x.t];
+    x.p = reinterpret_cast<const float4 *>(a.p[x.t])[x.j];
+    x.g = reinterpret_cast<const float4 *>(a.g[x.t])[x.j];
+    x.m = reinterpret_cast<const float4 *>(a.m[x.t])[x.j];
+    x.v = reinterpret_cast<const float4 *>(a.v[x.t])[x.j];
+}
+
+__device__ __forceinline__ void adam_store(const AdamArgs &a, Adam4 &x) {
+    const bool gz = x.g.x != 0.f || x.g.y != 0.f || x.g.z != 0.f || x.g.w != 0.f;
+    adam1(x.p.x, x.g.x, x.m.x, x.v.x, a);
+    adam1(x.p.y, x.g.y, x.m.y, x.v.y, a);
+    adam1(x.p.z, x.g.z, x.m.z, x.v.z, a);
+    adam1(x.p.w, x.g.w, x.m.w, x.v.w, a);
+    reinterpret_cast<float4 *>(a.p[x.t])[x.j] = x.p;
+    reinterpret_cast<float4 *>(a.m[x.t])[x.j] = x.m;
+    reinterpret_cast<float4 *>(a.v[x.t])[x.j] = x.v;
+    // most rows' gradients are already zero (a step touches ~50 k of 1.2 M points): store only
+    // the others, 4 of the 32 B per element skipped for the untouched rows
+    if (a.zero_grad && gz) reinterpret_cast<float4 *>(a.g[x.t])[x.j] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// one launch per parameter group: every tensor's float4s as one range, two per thread per trip
+// (both loaded before either is computed: 128 B in flight per thread)
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
-    const int64_t n4 = a.n >> 2;
+    const int64_t n4 = a.off4[a.nt];
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
-        float4 p = reinterpret_cast<const float4 *>(a.p)[i];
-        float4 g = reinterpret_cast<const float4 *>(a.g)[i];
-        float4 m = reinterpret_cast<const float4 *>(a.m)[i];
-        float4 v = reinterpret_cast<const float4 *>(a.v)[i];
-        adam1(p.x, g.x, m.x, v.x, a);
-        adam1(p.y, g.y, m.y, v.y, a);
-        adam1(p.z, g.z, m.z, v.z, a);
-        adam1(p.w, g.w, m.w, v.w, a);
-        reinterpret_cast<float4 *>(a.p)[i] = p;
-        reinterpret_cast<float4 *>(a.m)[i] = m;
-        reinterpret_cast<float4 *>(a.v)[i] = v;
-        // most rows' gradients are already zero (a step touches ~50 k of 1.2 M points): store only
-        // the others, 4 of the 32 B per element skipped for the untouched rows
-        if (a.zero_grad && (g.x != 0.f || g.y != 0.f || g.z != 0.f || g.w != 0.f))
-            reinterpret_cast<float4 *>(a.g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (; i + stride < n4; i += 2 * stride) {
+        Adam4 x, y;
+        adam_load(a, i, x);
+        adam_load(a, i + stride, y);
+        adam_store(a, x);
+        adam_store(a, y);
     }
-    // ragged tail (n % 4 elements), first workgroup only
-    if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
-        const int64_t j = (n4 << 2) + threadIdx.x;
-        float p = a.p[j], g = a.g[j], m = a.m[j], v = a.v[j];
-        adam1(p, g, m, v, a);
-        a.p[j] = p;
-        a.m[j] = m;
-        a.v[j] = v;
-        if (a.zero_grad) a.g[j] = 0.f;
+    if (i < n4) {
+        Adam4 x;
+        adam_load(a, i, x);
+        adam_store(a, x);
+    }
+    // ragged tails (n % 4 elements of each tensor), first workgroup only
+    if (blockIdx.x == 0) {
+        for (int t = 0; t < a.nt; ++t) {
+            if (threadIdx.x >= (a.n[t] & 3)) continue;
+            const int64_t j = ((a.n[t] >> 2) << 2) + threadIdx.x;
+            float p = a.p[t][j], g = a.g[t][j], m = a.m[t][j], v = a.v[t][j];
+            adam1(p, g, m, v, a);
+            a.p[t][j] = p;
+            a.m[t][j] = m;
+            a.v[t][j] = v;
+            if (a.zero_grad) a.g[t][j] = 0.f;
+        }
     }
 }
 
@@ -478,20 +520,30 @@ using namespace sgn;
 
 extern "C" {
 
-int sgn_adam_step(float *d_param, float *d_grad, float *d_exp_avg, float *d_exp_avg_sq, int64_t n, double lr,
-                  double beta1, double beta2, double eps, int64_t step, int32_t zero_grad, sgn_stream_t stream) {
-    SGN_REQUIRE(n >= 0 && step >= 1, "sgn_adam_step: n >= 0 and step >= 1 required");
-    if (n == 0) return 0;
-    SGN_REQUIRE(d_param && d_grad && d_exp_avg && d_exp_avg_sq, "sgn_adam_step: null buffer");
-    for (const void *q : {(const void *)d_param, (const void *)d_grad, (const void *)d_exp_avg,
-                          (const void *)d_exp_avg_sq})
-        SGN_REQUIRE(!(reinterpret_cast<uintptr_t>(q) & 15), "sgn_adam_step: buffers must be 16-B aligned");
+int sgn_adam_step_multi(int32_t n_t, float *const *d_param, float *const *d_grad, float *const *d_exp_avg,
+                        float *const *d_exp_avg_sq, const int64_t *n, double lr, double beta1, double beta2, double eps,
+                        int64_t step, int32_t zero_grad, sgn_stream_t stream) {
+    SGN_REQUIRE(n_t >= 0 && n_t <= kMaxAdamTensors, "sgn_adam_step_multi: 0 <= n_t <= 8");
+    SGN_REQUIRE(step >= 1, "sgn_adam_step: step >= 1 required");
+    if (n_t == 0) return 0;
+    SGN_REQUIRE(d_param && d_grad && d_exp_avg && d_exp_avg_sq && n, "sgn_adam_step_multi: null argument");
     AdamArgs a;
-    a.p = d_param;
-    a.g = d_grad;
-    a.m = d_exp_avg;
-    a.v = d_exp_avg_sq;
-    a.n = n;
+    a.nt = n_t;
+    a.off4[0] = 0;
+    for (int t = 0; t < n_t; ++t) {
+        SGN_REQUIRE(n[t] >= 0, "sgn_adam_step: n >= 0 required");
+        SGN_REQUIRE(n[t] == 0 || (d_param[t] && d_grad[t] && d_exp_avg[t] && d_exp_avg_sq[t]),
+                    "sgn_adam_step: null buffer");
+        for (const void *q : {(const void *)d_param[t], (const void *)d_grad[t], (const void *)d_exp_avg[t],
+                              (const void *)d_exp_avg_sq[t]})
+            SGN_REQUIRE(!(reinterpret_cast<uintptr_t>(q) & 15), "sgn_adam_step: buffers must be 16-B aligned");
+        a.p[t] = d_param[t];
+        a.g[t] = d_grad[t];
+        a.m[t] = d_exp_avg[t];
+        a.v[t] = d_exp_avg_sq[t];
+        a.n[t] = n[t];
+        a.off4[t + 1] = a.off4[t] + (n[t] >> 2);
+    }
     // host-side scalars in double and rounded once to fp32, as torch does with its Python
     // float hyper-parameters (1 - beta2 = 0.001, not 1 - 0.999f)
     a.b1 = (float)beta1;
@@ -504,11 +556,20 @@ int sgn_adam_step(float *d_param, float *d_grad, float *d_exp_avg, float *d_exp_
     a.bc2_sqrt = (float)std::sqrt(bc2);
     a.eps = (float)eps;
     a.zero_grad = zero_grad ? 1 : 0;
-    const int64_t n4 = n >> 2;
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 256 * 32));
+    const int64_t n4 = a.off4[n_t];
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n4 + 511) / 512, 256 * 16));
     hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
+}
+
+int sgn_adam_step(float *d_param, float *d_grad, float *d_exp_avg, float *d_exp_avg_sq, int64_t n, double lr,
+                  double beta1, double beta2, double eps, int64_t step, int32_t zero_grad, sgn_stream_t stream) {
+    SGN_REQUIRE(n >= 0 && step >= 1, "sgn_adam_step: n >= 0 and step >= 1 required");
+    if (n == 0) return 0;
+    SGN_REQUIRE(d_param && d_grad && d_exp_avg && d_exp_avg_sq, "sgn_adam_step: null buffer");
+    return sgn_adam_step_multi(1, &d_param, &d_grad, &d_exp_avg, &d_exp_avg_sq, &n, lr, beta1, beta2, eps, step,
+                               zero_grad, stream);
 }
 
 size_t sgn_colsum_workspace_bytes(int32_t count) {

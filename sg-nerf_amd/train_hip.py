@@ -330,8 +330,9 @@ def _fp32_rows_parts(gz, x, chunk):
 
 class PointAdam(torch.optim.Adam):
     """torch.optim.Adam (same param_groups, state keys and state_dict) whose step is one
-    sgn_adam_step launch per tensor; with zero_grad the launch also clears the gradient, so
-    the next step skips its fill pass.  For the dense ~47 M-element point group."""
+    sgn_adam_step_multi launch per parameter group; with zero_grad the launch also clears the
+    gradients, so the next step skips their fill pass.  For the dense ~47 M-element point group
+    and the MLP's flat parameter."""
 
     def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, zero_grad=True):
         super().__init__(params, lr=lr, betas=betas, eps=eps)
@@ -339,11 +340,13 @@ class PointAdam(torch.optim.Adam):
 
     @torch.no_grad()
     def step(self, closure=None):
+        """One sgn_adam_step_multi launch per parameter group (tensors sharing a step count)."""
         assert closure is None
         L = _lib.lib()
         st = _lib.stream_handle()
         for g in self.param_groups:
             b1, b2 = g["betas"]
+            by_step = {}
             for p in g["params"]:
                 if p.grad is None:
                     continue
@@ -354,10 +357,17 @@ class PointAdam(torch.optim.Adam):
                     s["exp_avg"] = torch.zeros_like(p)
                     s["exp_avg_sq"] = torch.zeros_like(p)
                 s["step"] += 1
-                _lib.check(L.sgn_adam_step(_lib.ptr(p), _lib.ptr(p.grad), _lib.ptr(s["exp_avg"]),
-                                           _lib.ptr(s["exp_avg_sq"]), p.numel(), float(g["lr"]), b1, b2,
-                                           float(g["eps"]), int(s["step"].item()), int(self.zero_grad_in_step),
-                                           st), "sgn_adam_step")
+                by_step.setdefault(int(s["step"].item()), []).append(p)
+            for step, ps in by_step.items():
+                for i in range(0, len(ps), 8):
+                    chunk = ps[i:i + 8]
+                    n = len(chunk)
+                    arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
+                    _lib.check(L.sgn_adam_step_multi(
+                        n, arr(chunk), arr([p.grad for p in chunk]), arr([self.state[p]["exp_avg"] for p in chunk]),
+                        arr([self.state[p]["exp_avg_sq"] for p in chunk]), (ctypes.c_int64 * n)(*[p.numel() for p in chunk]),
+                        float(g["lr"]), b1, b2, float(g["eps"]), step, int(self.zero_grad_in_step), st),
+                        "sgn_adam_step_multi")
         return None
 
 

@@ -327,33 +327,37 @@ def test_model_plugin_training_surface(tmp_path):
     assert m.test()["coarse_raycolor"].shape == before.shape
 
 
-@pytest.mark.parametrize("n", [4096, 1003, 3])
-def test_point_adam_matches_torch_adam(n):
-    """PointAdam (sgn_adam_step) against torch.optim.Adam (fp32, single-tensor) over three
-    steps with changing gradients and a decayed lr: parameters and both moments within fp32
-    rounding; the gradient is cleared by the step when zero_grad is on."""
+@pytest.mark.parametrize("sizes", [(4096,), (1003,), (3,), (38_401, 3_601, 7, 1_200)])
+def test_point_adam_matches_torch_adam(sizes):
+    """PointAdam (sgn_adam_step_multi: one launch per group) against torch.optim.Adam (fp32,
+    single-tensor) over three steps with changing gradients and a decayed lr: parameters and
+    both moments within fp32 rounding, for one tensor and for a group of ragged tensors (n % 4
+    tails, float4 ranges crossing tensors); the gradient is cleared by the step when zero_grad
+    is on."""
     from sgnerf_amd.train_hip import PointAdam
-    g = torch.Generator().manual_seed(n)
-    p0 = torch.randn(n, generator=g)
-    a = torch.nn.Parameter(p0.clone().to(DEV))
-    b = torch.nn.Parameter(p0.clone().to(DEV))
-    oa = PointAdam([a], lr=2e-3, betas=(0.9, 0.999))
-    ob = torch.optim.Adam([b], lr=2e-3, betas=(0.9, 0.999), foreach=False)
+    g = torch.Generator().manual_seed(sum(sizes))
+    p0 = [torch.randn(n, generator=g) for n in sizes]
+    a = [torch.nn.Parameter(x.clone().to(DEV)) for x in p0]
+    b = [torch.nn.Parameter(x.clone().to(DEV)) for x in p0]
+    oa = PointAdam(a, lr=2e-3, betas=(0.9, 0.999))
+    ob = torch.optim.Adam(b, lr=2e-3, betas=(0.9, 0.999), foreach=False)
     for it in range(3):
-        gr = (torch.randn(n, generator=g) * 10 ** (it - 1)).to(DEV)
-        gr[::7] = 0.0                                    # untouched points still decay
-        a.grad = gr.clone()
-        b.grad = gr.clone()
+        for x, y, n in zip(a, b, sizes):
+            gr = (torch.randn(n, generator=g) * 10 ** (it - 1)).to(DEV)
+            gr[::7] = 0.0                                    # untouched points still decay
+            x.grad = gr.clone()
+            y.grad = gr.clone()
         for o in (oa, ob):
             o.param_groups[0]["lr"] = 2e-3 * 0.9 ** it
         oa.step()
         ob.step()
-        assert torch.count_nonzero(a.grad) == 0
-        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
-        for k in ("exp_avg", "exp_avg_sq"):
-            ref = ob.state[b][k]   # atol: fp32 rounding at the tensor's scale (m cancels to ~0)
-            torch.testing.assert_close(oa.state[a][k], ref, rtol=1e-6, atol=1e-6 * float(ref.abs().max()))
-    assert float(oa.state[a]["step"]) == 3.0
+        for x, y in zip(a, b):
+            assert torch.count_nonzero(x.grad) == 0
+            torch.testing.assert_close(x, y, rtol=1e-6, atol=1e-7)
+            for k in ("exp_avg", "exp_avg_sq"):
+                ref = ob.state[y][k]   # atol: fp32 rounding at the tensor's scale (m cancels to ~0)
+                torch.testing.assert_close(oa.state[x][k], ref, rtol=1e-6, atol=1e-6 * float(ref.abs().max()))
+    assert all(float(oa.state[x]["step"]) == 3.0 for x in a)
 
 
 @pytest.mark.parametrize("rows", [0, 1, 777, 165_000])

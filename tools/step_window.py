@@ -1,6 +1,6 @@
 """Steady-state per-step view of a training kernel trace (rocprofv3 --kernel-trace, csv): the steps
-are cut at their last Adam launch (5 k_adam launches per step: the MLP group and the four point
-tensors), the last `n` steps averaged -- no setup, grid build or graph capture in the numbers.
+are cut at their first launch (k_depth_jitter, the query's jittered depth table: one per step), the
+last `n` complete steps averaged -- no setup, grid build or graph capture in the numbers.
 Usage: python tools/step_window.py <run_kernel_trace.csv> [n=20] [top=30]"""
 import collections
 import csv
@@ -10,9 +10,10 @@ import sys
 kt = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
-ad = [i for i, r in enumerate(kt) if "k_adam" in r["Kernel_Name"]]
-ends = [ad[i] for i in range(4, len(ad), 5)]
-pairs = list(zip(ends[-n - 1:-1], ends[-n:]))
+starts = [i for i, r in enumerate(kt) if "k_depth_jitter" in r["Kernel_Name"]]
+last = max(i for i, r in enumerate(kt) if "k_adam" in r["Kernel_Name"])
+cuts = [i - 1 for i in starts] + [last]   # window (a, b]: from a step's first launch to the next's
+pairs = list(zip(cuts[:-1], cuts[1:]))[-n:]
 tot = collections.Counter()
 calls = collections.Counter()
 wall = busy = hip = 0
