@@ -70,7 +70,26 @@ struct GemmK {
     int64_t ldo2;
     uint32_t *amax_out, *amax_out2;
     float *part;
+    int32_t splits;   // split-K mode: row runs; rows mode: row-tile strides (the grid is splits x blocks, 1-D)
 };
+
+// 1-D block id -> (output column block, split / row-tile start).  Blocks b and b + 8 run on one XCD
+// (its own L2), so the column blocks of a split go to the same XCD: they read the same rows of the
+// shared operand at about the same time, and the second and third reads hit that L2, not HBM.
+// Splits past the last multiple of 8 keep the plain order (correct, no sharing).
+__device__ __forceinline__ void tn_block(int nblk, int splits, int &blk, int &split) {
+    const int b = blockIdx.x;
+    const int q = splits / 8, base = 8 * nblk * q;
+    if (b < base) {
+        const int xcd = b & 7, k = b >> 3;
+        blk = k % nblk;
+        split = (k / nblk) * 8 + xcd;
+    } else {
+        const int t = b - base;
+        blk = t % nblk;
+        split = 8 * q + t / nblk;
+    }
+}
 
 __device__ __forceinline__ int op_shift(const Opnd &o) {
     if (o.shift) return o.shift[0];
@@ -210,11 +229,13 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int sa = op_shift(g.A), sb = op_shift(g.B);
     const float fa = ldexpf(1.f, sa), fb = ldexpf(1.f, sb), osc = ldexpf(1.f, -(sa + sb));
-    const int nb_n = (g.N + BN - 1) / BN;
-    const int m0 = (blockIdx.x / nb_n) * BM, n0 = (blockIdx.x % nb_n) * BN;
+    const int nb_n = (g.N + BN - 1) / BN, nb_m = (g.M + BM - 1) / BM;
+    int blk, split;
+    tn_block(nb_m * nb_n, g.splits, blk, split);
+    const int m0 = (blk / nb_n) * BM, n0 = (blk % nb_n) * BN;
     const int rows = min(g.d_rows ? *g.d_rows : 0x7fffffff, g.K);
-    const int per = ((rows + (int)gridDim.y - 1) / (int)gridDim.y + 31) / 32 * 32;
-    const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+    const int per = ((rows + g.splits - 1) / g.splits + 31) / 32 * 32;
+    const int r0 = split * per, r1 = min(rows, r0 + per);
     const int nkb = r1 > r0 ? (r1 - r0 + 31) / 32 : 0;
     f32x16 acc[WM][WN];
 #pragma unroll
@@ -284,7 +305,7 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
             __syncthreads();
         }
     }
-    float *part = g.part + (int64_t)blockIdx.y * g.M * g.N;
+    float *part = g.part + (int64_t)split * g.M * g.N;
 #pragma unroll
     for (int a = 0; a < WM; ++a)
 #pragma unroll
@@ -348,11 +369,13 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
     const float fa = ldexpf(1.f, sa), fb = ldexpf(1.f, sb), osc = ldexpf(1.f, -(sa + sb));
     const int rows = min(g.d_rows ? *g.d_rows : 0x7fffffff, g.M);
     const int limA = min(rows, g.A.nrows);
-    const int n0 = blockIdx.x * (32 * WN);
+    int nblk, rt;
+    tn_block((g.N + 32 * WN - 1) / (32 * WN), g.splits, nblk, rt);
+    const int gy = g.splits;
+    const int n0 = nblk * (32 * WN);
     const int L = lane & 31, hk = lane >> 5;
     // the first tile's A loads go out before the weight staging
     float a[KS][8];
-    int rt = blockIdx.y;
     {
         const ARow ar = arow(g.A, rt * RT_ROWS + 32 * w + L, limA);
 #pragma unroll
@@ -370,9 +393,9 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
     }
     __syncthreads();
     float am1 = 0.f, am2 = 0.f;
-    for (; rt * RT_ROWS < rows; rt += gridDim.y) {
+    for (; rt * RT_ROWS < rows; rt += gy) {
         const int m0 = rt * RT_ROWS + 32 * w;
-        const ARow an = arow(g.A, (rt + gridDim.y) * RT_ROWS + 32 * w + L, limA);
+        const ARow an = arow(g.A, (rt + gy) * RT_ROWS + 32 * w + L, limA);
         f32x16 acc[WN];
 #pragma unroll
         for (int t = 0; t < WN; ++t) acc[t] = f32x16{};
@@ -1030,7 +1053,8 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
         int gy = 256 / nb;
         gy = gy < 1 ? 1 : gy > tiles ? tiles : gy;
         const int ks = (g.K + 15) / 16;
-        const dim3 grid(nb, gy);
+        k.splits = gy;
+        const dim3 grid(nb * gy);
         if (p1) {
             SGN_REQUIRE(!w96 && ks != 16 && ks <= 18, "products 1: the colour layers' shapes (K <= 128 or 272..288, N > 96)");
             if (ks <= 8) hipLaunchKernelGGL((k_x3rows<8, 4, true>), grid, dim3(TPB), 0, st, k);
@@ -1051,7 +1075,8 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
         const int BM = g.M > 128 ? 256 : 128;
         const int BN = g.N <= 32 ? 32 : (BM == 128 && g.N <= 160) ? 160 : 96;
         const int nbm = (g.M + BM - 1) / BM, nbn = (g.N + BN - 1) / BN;
-        const dim3 grid(nbm * nbn, g.splits);
+        k.splits = g.splits;
+        const dim3 grid(nbm * nbn * g.splits);
         if (p1) {
             SGN_REQUIRE(BM == 128 && (BN == 160 || BN == 96), "products 1: the colour layers' shapes (M <= 128, N > 32)");
             if (BN == 160) hipLaunchKernelGGL((k_x3tn<1, 5, true>), grid, dim3(TPB), 0, st, k);
