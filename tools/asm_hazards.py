@@ -2,6 +2,7 @@
 register an MFMA wrote or reads as its accumulator input (srcC), or read an MFMA's result, within the
 previous 16 instructions (with no compiler-visible write of that register in between): the hazard recognizer
 does not see inline asm, so such a write may land while the MFMA still reads its accumulator input.
+Also an MFMA reading an operand an inline-asm VALU wrote fewer than 2 wait states before.
 Usage: python tools/asm_hazards.py <file.s>   (prints the candidates and their count)"""
 import re, sys
 def regs(tok):
@@ -39,6 +40,20 @@ for ln in lines:
                 if found <= 12:
                     print(f'asm {s!r} {dist+1} instrs after {txt!r}')
                 break
+    if op.startswith('v_mfma'):
+        # RAW: an MFMA reading (srcA / srcB / srcC) a register an inline-asm VALU wrote fewer than 2 wait
+        # states before (the hazard recognizer does not pad asm writes; the MFMA would read a stale value)
+        ab = set().union(*[regs(o) for o in ops[1:4]]) if len(ops) > 3 else set()
+        states = 0
+        for k, d2, s2, txt in reversed(hist[-4:]):
+            if states >= 2:
+                break
+            if txt.startswith('asm:v_') and not txt.startswith('asm:v_mfma') and ab & d2:
+                found += 1
+                if found <= 12:
+                    print(f'mfma {s!r} reads asm {txt!r} after {states} wait states')
+                break
+            states += 1
     kind = 'mfma' if op.startswith('v_mfma') else 'other'
     nw = 0
     if op == 's_nop': nw = int(ops[0]) + 1 if ops else 1
