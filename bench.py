@@ -153,7 +153,7 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None, precision=
                                      "MFMA GEMMs k_x3rows / k_x3tn, HIP loss stage), HIP Adam"
                                      if precision == "f32"
                                      else "HIP MFMA row-MLP forward/backward (fp16 operands) + colour MLP and losses "
-                                          "on the split-fp16 GEMMs and HIP loss stage in one captured graph, fused Adam")
+                                          "on the split-fp16 GEMMs and HIP loss stage in one captured graph, HIP Adam")
                                   + (" (SG-NeRF variant: semantic-guided kNN, block2_bpnet 352->256)" if args.sg else "")
                                   + (" + RCCL all-reduce of the gradients" if world > 1 else
                                      ", one GPU (no gradient exchange)"),
