@@ -264,7 +264,7 @@ GRAPH_BUCKET = int(os.environ.get("SGN_GRAPH_BUCKET", "8192"))
 GRAPH_CACHE = 8
 
 # rows per split-K batch of the weight-gradient GEMMs (SGN_DW_CHUNK overrides, for sweeps)
-DW_CHUNK = int(os.environ.get("SGN_DW_CHUNK", "1024"))
+DW_CHUNK = int(os.environ.get("SGN_DW_CHUNK", "2048"))
 
 
 def _mm_f32(a, b):
