@@ -24,15 +24,17 @@ Rows r are the valid (sample, neighbour) pairs, sample-major (sample s owns rows
 row_off[s] .. row_off[s] + samp_nnb[s]); items are the samples with a neighbour, ascending.
 """
 import ctypes
+import os
 
 import torch
 
 from . import _lib
 
 # split-K partials of the weight-gradient GEMMs (rows / items cut into this many 32-aligned runs;
-# 84 x 3 column blocks = one workgroup per CU for the row layers)
-SPLITS_ROWS = 84
-SPLITS_ITEMS = 128
+# 84 x 3 column blocks = one workgroup per CU for the row layers).  SGN_SPLITS_ROWS / _ITEMS
+# override them for sweeps (tools/splits_sweep.sh).
+SPLITS_ROWS = int(os.environ.get("SGN_SPLITS_ROWS", "84"))
+SPLITS_ITEMS = int(os.environ.get("SGN_SPLITS_ITEMS", "128"))
 
 
 def _addr(t, elem_off=0):
