@@ -290,7 +290,9 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
     mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0  # opaque surfaces, as a trained scene
     r = HipRenderer(PointTables.from_cloud(pc, dev), mlp, o, dev)
     n_frames = warmup + steps
-    poses = [(s * world + rank) for s in range(n_frames)]
+    # timed frame j renders pose j * N + rank whatever --warmup is (the warm-up frames take poses from
+    # the other end of the spiral), so runs with different warm-up counts time the same frames
+    poses = [(-1 - s * world - rank) % 120 for s in range(warmup)] + [(s * world + rank) for s in range(steps)]
     views = [(lego_pose_view if lego else dense_pose_view if dense else spiral_pose_view if spiral else pose_view)(
         p, args.h, args.w) for p in poses]
     rays = [torch.from_numpy(v.raydir).to(dev) for v in views]

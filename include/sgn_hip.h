@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 11
+#define SGN_ABI_VERSION 12
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -229,6 +229,10 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
  *                             decoded features (an activation outside fp16 range); 0 otherwise
  *   sgn_aggregate_flag_offset_f32 : byte offset of that int32 flag inside the workspace (for a
  *                             caller that reads it asynchronously, e.g. one frame later)
+ *   sgn_aggregate_fs_offset_f32 (ABI 12) : byte offset inside the workspace of the blended features
+ *                             f_s that stage 1 leaves for stage 2 -- fp32 [S_capacity][256], item i's
+ *                             row at offset + 1024 i (a training step reads them) -- or -1 when a
+ *                             workspace of workspace_bytes does not hold every item's row
  *   sgn_mlp_pack_f32_host   : sgn_mlp_pack_f32 into host memory (no device call; checkers)
  * 16-byte aligned device buffers. */
 size_t sgn_mlp_packed_bytes_f32(int32_t bpnet_layers, int32_t bpnet_dim);
@@ -245,6 +249,7 @@ int sgn_aggregate_f32(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bp
                       void *d_workspace, size_t workspace_bytes, int32_t stages, sgn_stream_t stream);
 int sgn_aggregate_check_f32(const void *d_workspace, size_t workspace_bytes, sgn_stream_t stream);
 size_t sgn_aggregate_flag_offset_f32(size_t workspace_bytes);
+int64_t sgn_aggregate_fs_offset_f32(size_t workspace_bytes, int64_t S_capacity);
 
 /* sgn_point_project_f32 for the points d_idx[0 .. *d_count) only (int32 indices < n_points; the
  * count is a device int64): a training step re-projects the rows its rays touch after each weight
@@ -446,7 +451,8 @@ int sgn_pow2_scale(const float *d_a, int64_t na, const float *d_b, int64_t nb, v
  * neighbour slots, train.composite_losses) and every neighbour d_pidx[e] >= 0, e < d_counters[0] * K
  * (sgn_query's sample count; s_cap bounds it).  Appends them to d_idx (int32 [n_points]) in no
  * particular order and writes their count to d_count2[step & 1]; d_count2[(step + 1) & 1] is
- * cleared for the next step.  d_stamp: int32 [n_points], -1 once at allocation, then owned by the
+ * cleared for the next step; d_count2[2] (ABI 12) accumulates the neighbour indices >= n_points met
+ * (a query / point-table mismatch: such a point is never projected), so a caller can assert it is 0.  d_stamp: int32 [n_points], -1 once at allocation, then owned by the
  * caller's step counter (step >= 0, increasing).  Replaces the torch touched_rows mask / scan /
  * scatter (train.py) on the single-GPU fp32 step's projection subset (sgn_point_project_f32_subset);
  * the neighbours come from the reference's query (neural_points.py:942-988). */

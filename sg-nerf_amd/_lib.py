@@ -12,7 +12,7 @@ import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds 
 
 # SGN_HIP_LIB: another build of the same ABI (same-box A/B of kernel variants, tools/ab_lib.sh)
 LIB_PATH = os.environ.get("SGN_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -168,6 +168,7 @@ SIGNATURES = {
                                   c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
     "sgn_aggregate_check_f32": (c_i32, [c_vp, c_sz, c_vp]),
     "sgn_aggregate_flag_offset_f32": (c_sz, [c_sz]),
+    "sgn_aggregate_fs_offset_f32": (c_i64, [c_sz, c_i64]),
     "sgn_aggregate_train_fwd_f32": (c_i32, [c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,
                                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "sgn_aggregate_train_fwd_f32_sg": (c_i32, [c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(PointTables),

@@ -1764,6 +1764,13 @@ int sgn_aggregate_check_f32(const void *d_workspace, size_t workspace_bytes, sgn
     return 0;
 }
 
+int64_t sgn_aggregate_fs_offset_f32(size_t workspace_bytes, int64_t S_capacity) {
+    // aggregate_f32 keeps item i's f_s at d_workspace + i * 1 KiB when the workspace holds every item
+    // (`full`), else it reuses the first rows chunk by chunk
+    const int64_t ws_items = workspace_bytes > (size_t)WS_TAIL ? (int64_t)((workspace_bytes - WS_TAIL) / WS_PER_ITEM) : 0;
+    return S_capacity >= 0 && ws_items >= 32 && ws_items >= S_capacity ? 0 : -1;
+}
+
 size_t sgn_aggregate_flag_offset_f32(size_t workspace_bytes) {
     const int64_t ws_items = workspace_bytes > (size_t)WS_TAIL ? (int64_t)((workspace_bytes - WS_TAIL) / WS_PER_ITEM) : 0;
     return (size_t)(ws_items * WS_PER_ITEM + 4);

@@ -485,7 +485,7 @@ __global__ void __launch_bounds__(256) k_touched_points(const int32_t *__restric
                                                         const int32_t *__restrict__ counters, int64_t cap_slots,
                                                         int32_t K, int64_t n_points, int32_t step, int32_t *stamp,
                                                         int32_t *__restrict__ idx, unsigned long long *cnt,
-                                                        unsigned long long *cnt_next) {
+                                                        unsigned long long *cnt_next, unsigned long long *n_bad) {
     int64_t n = (int64_t)counters[0] * K;
     n = (n < cap_slots ? n : cap_slots) + 1;   // virtual slot 0 is point 0
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -497,6 +497,7 @@ __global__ void __launch_bounds__(256) k_touched_points(const int32_t *__restric
         bool fresh = false;
         if (v < n) {
             p = v == 0 ? 0 : pidx[v - 1];
+            if (p >= n_points) atomicAdd(n_bad, 1ull);   // never expected: reported, not projected
             if (p >= 0 && p < n_points && stamp[p] != step)
                 fresh = atomicExch(&stamp[p], step) != step;
         }
@@ -770,7 +771,7 @@ int sgn_touched_points(const int32_t *d_pidx, const int32_t *d_counters, int64_t
     blocks = blocks < 2048 ? blocks : 2048;
     auto *c = reinterpret_cast<unsigned long long *>(d_count2);
     hipLaunchKernelGGL(k_touched_points, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), d_pidx, d_counters,
-                       s_cap * K, K, n_points, step, d_stamp, d_idx, c + (step & 1), c + ((step + 1) & 1));
+                       s_cap * K, K, n_points, step, d_stamp, d_idx, c + (step & 1), c + ((step + 1) & 1), c + 2);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

@@ -103,7 +103,10 @@ class F32Step:
             self.db = torch.empty(rows, 256, **f32)
             self.bprow = torch.empty(rows, self.D, **f32) if self.D else None
         self.ws32 = torch.empty(int(L.sgn_aggregate_workspace_bytes_f32(cap)), dtype=torch.uint8, device=dev)
-        self.fs = self.ws32[:cap * 256 * 4].view(torch.float32).view(cap, 256)   # k_rows16's blended features
+        # k_rows16's blended features: fp32 [cap][256] inside the workspace (the ABI names where)
+        fs_off = int(L.sgn_aggregate_fs_offset_f32(self.ws32.numel(), cap))
+        assert fs_off >= 0, "the aggregate workspace must hold every item's f_s row"
+        self.fs = self.ws32[fs_off:fs_off + cap * 256 * 4].view(torch.float32).view(cap, 256)
         self.x0 = torch.empty(rows, 288, **f32)
         self.ext = torch.empty(rows, 8, **f32)
         self.rw = torch.empty(rows, 2, **f32)

@@ -30,7 +30,6 @@ P rows, then train.aggregate(saved=...) and fp32 autograd through the HIP loss s
 """
 import ctypes
 import os
-import math
 
 import torch
 import torch.nn as nn
@@ -39,8 +38,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .opts import HotPathOpts
-from .train import (PointParams, _allreduce_buckets, _allreduce_point_rows, _pe, composite_losses,
-                    gather_counts, touched_rows)
+from .train import PointParams, _allreduce_buckets, _allreduce_point_rows, _pe, gather_counts, touched_rows
 from .loss_hip import LossStage
 from .weights import BPNET, LAYERS, layers_for, strip_prefix
 
@@ -424,9 +422,6 @@ class HipTrainer:
         # the fp32-faithful blob (f32 step) and, for both precisions, the per-layer weight shifts the
         # split-fp16 GEMMs of the colour MLP read
         self.packer32 = _PackerF32(self.device, self.mlp, self.variant)
-        # the f16 step's colour MLP + losses + backward on hand-written kernels inside the captured graph
-        # (train_f32.ColourStep; SGN_HIP_COLOUR=0: torch autograd of the colour MLP, the earlier stage)
-        self.hip_colour = os.environ.get("SGN_HIP_COLOUR", "1") != "0"
         # stored column p -> reference index; inverses: reference index -> stored column
         self.map_chain = _colmap(0, 256, self.device)
         self.map_x0 = _colmap(1, 288, self.device)
@@ -435,14 +430,11 @@ class HipTrainer:
         self.inv_x0 = self._inverse(self.map_x0, 284)
         self.inv_h2 = self._inverse(self.map_h2, 263)
         self._cap = 0
-        # the colour/composite/loss stage as one replayed HIP graph (SGN_TRAIN_GRAPH=0: eager)
-        self.use_graph = os.environ.get("SGN_TRAIN_GRAPH", "1") != "0"
-        # the losses and their gradients on the HIP loss stage (loss.hip; SGN_HIP_LOSS=0: torch autograd
-        # of train.composite_losses, the restatement it is tested against)
-        self.hip_loss = os.environ.get("SGN_HIP_LOSS", "1") != "0"
+        # the f16 step's colour MLP, losses and their backward (train_f32.ColourStep on the HIP loss
+        # stage) as one replayed HIP graph; use_graph = False runs the same stage eagerly (torch autograd
+        # of the colour MLP into the HIP loss stage), the graph's parity reference in the tests
+        self.use_graph = True
         self.loss_stage = LossStage(self.device)
-        # f32 step: re-project only the points the step's rays touch (SGN_PROJ_SUBSET=0: all points)
-        self.proj_subset = os.environ.get("SGN_PROJ_SUBSET", "1") != "0"
         self._graphs = {}        # (capacity bucket, buffers) -> captured loss stage, LRU order
         self.graph_captures = 0
         self._flat_maps = {}
@@ -536,7 +528,7 @@ class HipTrainer:
         if getattr(self, "_stamp_n", -1) != npts:
             self._stamp = torch.full((npts,), -1, dtype=torch.int32, device=dev)
             self._tlist = torch.empty(npts, dtype=torch.int32, device=dev)
-            self._tcount = torch.zeros(2, dtype=torch.int64, device=dev)
+            self._tcount = torch.zeros(3, dtype=torch.int64, device=dev)   # [2]: out-of-range ids met
             self._stamp_n, self._tstep = npts, 0
         step = self._tstep
         self._tstep = (step + 1) & 0x7fffffff
@@ -587,7 +579,7 @@ class HipTrainer:
         st = _lib.stream_handle()
         pt = self._tables(campos, rot, raydir)
         qo = q.abi()
-        if graph and self.hip_colour:
+        if graph:
             self.packer32.pack(self.mlp.flat)   # the colour GEMMs' weight shifts
             self.feat.zero_()                    # samples without neighbours keep zero features
         saved = _lib.AggSaved(self.x0.data_ptr(), self.h1.data_ptr(), self.h2.data_ptr(), self.h3.data_ptr())
@@ -616,11 +608,7 @@ class HipTrainer:
             validS[samp] = True
             qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
                   "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
-            if self.hip_loss:
-                total, parts, full, ray_mask = self.loss_stage(self.points, qo, featS, campos, rot, gt, o, R)
-            else:
-                total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, campos, rot, raydir,
-                                                                gt, o)
+            total, parts, full, ray_mask = self.loss_stage(self.points, qo, featS, campos, rot, gt, o, R)
             total.backward()
             if n > 0:
                 dfs = fs_t.grad.contiguous()
@@ -665,12 +653,9 @@ class HipTrainer:
     def _backward_f32(self, campos, rot, raydir, near, far, gt, labels=None):
         """The reference's fp32 step on hand-written kernels (train_f32.F32Step): query, forward,
         colour MLP, losses and the whole backward as HIP launches with the counts on the device (no
-        host sync on one GPU; under DP one for the touched-row counts).  SGN_F32_TORCH=1: the earlier
-        step (HIP forward, torch fp32 autograd backward), kept for A/B."""
-        if os.environ.get("SGN_F32_TORCH", "0") == "1":
-            if self.sg:
-                raise NotImplementedError("SGN_F32_TORCH=1 (the torch-autograd A/B step) covers the base viewmlp")
-            return self._backward_f32_torch(campos, rot, raydir, near, far, gt, labels)
+        host sync on one GPU; under DP one for the touched-row counts).  The block1.0 projection P is
+        recomputed for the points the step's rays touch only (~50 k of 1.2 M for a 4096-ray batch: the
+        rows read no other point, and the weights change every step)."""
         from .train_f32 import F32Step
         o = self.opts
         dev = self.device
@@ -699,115 +684,38 @@ class HipTrainer:
         t_idx = t_cnt = None
         if dp:
             t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, npts)
-        if self.proj_subset:
-            idx32, cnt = self._touched(q, npts) if not dp else (t_idx.to(torch.int32), t_cnt)
-            _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(idx32),
-                                                      _lib.ptr(cnt), _lib.ptr(self._proj32), st),
-                       "sgn_point_project_f32_subset")
-        else:
-            _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(self._proj32), st),
-                       "sgn_point_project_f32")
+        idx32, cnt = self._touched(q, npts) if not dp else (t_idx.to(torch.int32), t_cnt)
+        _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(idx32),
+                                                  _lib.ptr(cnt), _lib.ptr(self._proj32), st),
+                   "sgn_point_project_f32_subset")
         step = getattr(self, "_f32step", None)
         key = (R, q.work.data_ptr(), q.pidx.data_ptr(), self.mlp.flat.data_ptr(), self.mlp.flat.grad.data_ptr())
         if step is None or step.key != key:
             step = self._f32step = F32Step(self, q, R)
             step.key = key
         losses, full, mask = step.run(pt, self._proj32, blob, campos, rot, gt, self._loss_params())
-        self._last_q, self._last_qd = q, None
-        total = losses[0] + 3e-6 + 1e-4 * losses[1]
-        parts = {"ray_masked_coarse_raycolor": losses[0], "ray_miss_coarse_raycolor": losses[2],
-                 "coarse_raycolor": losses[3], "conf_coefficient": losses[1]}
+        self._last_q = q
+        # the step's buffers are reused by the next step: the losses, the colour and the mask out into
+        # one fresh allocation (one launch), as the f16 step's graph outputs
+        nl = losses.numel()
+        buf = torch.empty(nl + 3 * R + -(-R // 4), dtype=torch.float32, device=dev)
+        lo, full_o = buf[:nl], buf[nl:nl + 3 * R].view(R, 3)
+        mask_o = buf[nl + 3 * R:].view(torch.int8)[:R]
+        _lib.copy_segments([(losses, lo), (full, full_o), (mask, mask_o)])
+        total = lo[0] + 3e-6 + 1e-4 * lo[1]
+        parts = {"ray_masked_coarse_raycolor": lo[0], "ray_miss_coarse_raycolor": lo[2],
+                 "coarse_raycolor": lo[3], "conf_coefficient": lo[1]}
         self.allreduce_grads([self.mlp.flat])
         if dp:
             t_counts = [int(x) for x in gather_counts(t_cnt).tolist()]
             _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
         parts["total"] = total
-        return parts, full, mask.bool()
-
-    def _backward_f32_torch(self, campos, rot, raydir, near, far, gt, labels=None):
-        """The reference's fp32 step: HIP query, the fp32-faithful row MLP on the HIP kernels
-        (k_point_proj16 + k_pair_slots + k_rows16 save mode: block1.0 / 1.2 / 3.0 pre-activations per
-        row), then train.aggregate(saved=...) (those three layers take their forward values from the
-        kernel; block3.2, alpha, K-blend, colour in fp32 torch) -> composite_losses -> fp32 autograd."""
-        from .train import aggregate
-        o = self.opts
-        dev = self.device
-        campos = campos.reshape(3).to(dev, torch.float32).contiguous()
-        rot = rot.reshape(3, 3).to(dev, torch.float32).contiguous()
-        raydir = raydir.reshape(-1, 3).to(dev, torch.float32).contiguous()
-        R = raydir.shape[0]
-        q = self._query(campos, raydir, near, far, labels)
-        blob = self.packer32.pack(self.mlp.flat)
-        for p in self.point_params + [self.mlp.flat]:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            elif not self._grads_clean:
-                p.grad.zero_()
-        self._grads_clean = False
-        L = _lib.lib()
-        st = _lib.stream_handle()
-        pt = self._tables(campos, rot, raydir)
-        P = self.points
-        npts = P.xyz.shape[0]
-        nproj = int(L.sgn_point_proj_bytes_f32(npts))
-        if getattr(self, "_proj32", None) is None or self._proj32.numel() < nproj:
-            self._proj32 = torch.empty(max(nproj, 16), dtype=torch.uint8, device=dev)
-        dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-        t_idx = t_cnt = None
-        if dp:   # the point rows this step's rays touch, sorted for the sparse exchange (device-side, no sync)
-            t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, npts)
-        if self.proj_subset:
-            # P and the packed records of the touched points only (~50 k of 1.2 M for a 4096-ray batch):
-            # the rows read no other point, and the weights change every step
-            idx32, cnt = self._touched(q, npts) if not dp else (t_idx.to(torch.int32), t_cnt)
-            _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(idx32),
-                                                      _lib.ptr(cnt), _lib.ptr(self._proj32), st),
-                       "sgn_point_project_f32_subset")
-        else:
-            _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(self._proj32), st),
-                       "sgn_point_project_f32")
-        cap = max(R * o.SR, 1)
-        if getattr(self, "_cap32", 0) < cap:
-            self._z32 = [torch.zeros(cap * o.K, 256, dtype=torch.float32, device=dev) for _ in range(3)]
-            self._ws32 = torch.empty(int(L.sgn_aggregate_workspace_bytes_f32(cap)), dtype=torch.uint8, device=dev)
-            self._feat32 = torch.empty(cap, 4, dtype=torch.float32, device=dev)
-            self._cap32 = cap
-        qo = q.abi()
-        _lib.check(L.sgn_aggregate_train_fwd_f32(_lib.ptr(self._proj32), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
-                                                 _lib.ptr(blob), _lib.ptr(self._feat32), _lib.ptr(self._z32[0]),
-                                                 _lib.ptr(self._z32[1]), _lib.ptr(self._z32[2]), None, _lib.ptr(self._ws32),
-                                                 self._ws32.numel(), st), "sgn_aggregate_train_fwd_f32")
-        # valid rows on the device, fetched with S: counted from the same mask nonzero_static selects
-        # (a count from samp_nnb could disagree with pidx and pad with -1 or drop rows)
-        vmask = (q.pidx[:cap * o.K] >= 0) & (torch.arange(cap * o.K, device=dev) < q.counters[0] * o.K)
-        n_rows = vmask.sum().reshape(1)
-        sync = torch.cat([q.counters[:1].to(torch.int64), n_rows.to(torch.int64)]
-                         + ([gather_counts(t_cnt)] if dp else []))
-        S, n_rows, *t_counts = (int(x) for x in sync.tolist())   # one host sync per step
-        qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
-              "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
-        self._last_qd = qd   # the step's sample-major query (tests rerun fp32 autograd on it)
-        rows = torch.nonzero_static(vmask[:S * o.K], size=n_rows).reshape(-1)   # no second sync
-        feat, _, mask = aggregate(P, self.mlp, campos.reshape(1, 3), rot, raydir, qd["samp_ray"], qd["samp_locw"],
-                                  qd["pidx"], saved=self._z32, rows=rows)
-        if self.hip_loss:
-            total, parts, full, ray_mask = self.loss_stage(P, qo, feat, campos, rot, gt, o, R)
-        else:
-            total, parts, full, ray_mask = composite_losses(P, qd, feat, mask.sum(-1) > 0, campos, rot, raydir,
-                                                            gt.reshape(-1, 3).to(dev, torch.float32), o)
-        total.backward()
-        self.allreduce_grads([self.mlp.flat])
-        if dp:
-            _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
-        parts["total"] = total.detach()
-        return parts, full.detach(), ray_mask
+        return parts, full_o, mask_o.bool()
 
     @property
     def last_query(self):
         """The last fp32 step's sample-major query as a dict (ray_ns, ray_soff, samp_ray, samp_locw,
         pidx): tests rerun fp32 autograd on the very samples the step used.  Reads S (host sync)."""
-        if getattr(self, "_last_qd", None) is not None:
-            return self._last_qd
         q, o = self._last_q, self.opts
         R, S = q.R, int(q.counters[0].item())
         return {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
@@ -815,10 +723,10 @@ class HipTrainer:
 
     # -- graph-captured loss stage -----------------------------------------------------------
     def _loss_body(self, st):
-        """Colour MLP + composite + losses + their autograd over the batch's full sample capacity
-        (R * SR entries, static shapes, no host sync): items past the device count n and samples
-        past S are padding, zeroed on input and routed to sentinel rows, so the gradients equal
-        the eager path's.  Runs inside a HIP graph capture (and its warm-up)."""
+        """Colour MLP + composite + losses + their backward on the hand-written kernels over the batch's
+        full sample capacity (R * SR entries, static shapes, no host sync): items past the device count
+        n and samples past S are padding, zeroed on input and routed to sentinel rows, so the gradients
+        equal the eager path's.  Runs inside a HIP graph capture (and its warm-up)."""
         o, dev, R = self.opts, self.device, st["R"]
         Sc, Nc = st["Sc"], st["Nc"]             # sample / item capacity of this graph
         q = st["q"]
@@ -827,35 +735,16 @@ class HipTrainer:
         _lib.check(_lib.lib().sgn_colour_inputs(_lib.ptr(q.counters), _lib.ptr(q.work), _lib.ptr(q.samp_ray), Nc, Sc,
                                                 _lib.ptr(self.fs), _lib.ptr(self.feat), _lib.ptr(st["raydir"]),
                                                 _lib.ptr(fs32), _lib.ptr(al32), _lib.ptr(v), _lib.ptr(samp),
-                                                _lib.ptr(st["col"].vpe) if "col" in st else None,
+                                                _lib.ptr(st["col"].vpe),
                                                 _lib.stream_handle()), "sgn_colour_inputs")
-        if "col" in st:   # hand-written colour MLP, losses and backward (train_f32.ColourStep)
-            losses, full, mask, dfs, dfeat = st["col"].run(st["campos"], st["rot"], st["gt"], self._loss_params())
-            dal = dfeat[samp.long(), 0]          # per item (padding: the zero row Sc)
-            scale = self._loss_scale(dfs, dal)
-            total = losses[0] + 3e-6 + 1e-4 * losses[1]
-            names = ["ray_masked_coarse_raycolor", "ray_miss_coarse_raycolor", "coarse_raycolor", "conf_coefficient"]
-            return {"scalars": torch.stack([total, losses[0], losses[2], losses[3], losses[1]]), "names": names,
-                    "full": full, "ray_mask": mask, "dfs": dfs, "dal": dal, "scale": scale}
-        fs32.grad = al32.grad = None   # backward assigns fresh (graph-pool) gradients: no clear, no accumulate
-        feat_s = torch.cat([al32[:, None], self._colour(fs32, v)], dim=-1)   # colour grads -> flat.grad
-        featS = torch.zeros(Sc + 1, 4, device=dev).index_put((samp,), feat_s)[:Sc]
-        if self.hip_loss:
-            # the graph's own loss stage: its workspace lives as long as the captured graph that uses it
-            total, parts, full, ray_mask = st["loss"](self.points, st["qabi"], featS, st["campos"], st["rot"],
-                                                      st["gt"], o, R)
-        else:
-            validS = torch.zeros(Sc + 1, dtype=torch.bool, device=dev).index_put((samp,), st["true"])[:Sc]
-            qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:Sc],
-                  "samp_locw": q.samp_locw[:Sc * 3].view(Sc, 3), "pidx": q.pidx[:Sc * o.K].view(Sc, o.K)}
-            total, parts, full, ray_mask = composite_losses(self.points, qd, featS, validS, st["campos"], st["rot"],
-                                                            st["raydir"], st["gt"], o, s_count=q.counters[0])
-        total.backward()
-        dfs, dal = fs32.grad, al32.grad
+        # hand-written colour MLP, losses and backward (train_f32.ColourStep)
+        losses, full, mask, dfs, dfeat = st["col"].run(st["campos"], st["rot"], st["gt"], self._loss_params())
+        dal = dfeat[samp.long(), 0]          # per item (padding: the zero row Sc)
         scale = self._loss_scale(dfs, dal)
-        names = list(parts)
-        return {"scalars": torch.stack([total.detach()] + [parts[k] for k in names]), "names": names,
-                "full": full.detach(), "ray_mask": ray_mask, "dfs": dfs, "dal": dal, "scale": scale}
+        total = losses[0] + 3e-6 + 1e-4 * losses[1]
+        names = ["ray_masked_coarse_raycolor", "ray_miss_coarse_raycolor", "coarse_raycolor", "conf_coefficient"]
+        return {"scalars": torch.stack([total, losses[0], losses[2], losses[3], losses[1]]), "names": names,
+                "full": full, "ray_mask": mask, "dfs": dfs, "dal": dal, "scale": scale}
 
     def _graph_losses(self, q, campos, rot, raydir, gt, R, S, n):
         """Replay the captured loss stage for this step's capacity bucket (item / sample counts
@@ -875,16 +764,13 @@ class HipTrainer:
             self.graph_captures += 1
             if len(self._graphs) >= GRAPH_CACHE:
                 self._graphs.pop(next(iter(self._graphs)))
-            st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "qabi": q.abi(), "loss": LossStage(dev),
-                  "true": torch.ones((), dtype=torch.bool, device=dev),
+            st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "qabi": q.abi(),
                   "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
                   "campos": campos.clone(), "rot": rot.clone(),
-                  "fs32": torch.zeros(Nc, 256, device=dev, requires_grad=True),
-                  "al32": torch.zeros(Nc, device=dev, requires_grad=True),
+                  "fs32": torch.zeros(Nc, 256, device=dev), "al32": torch.zeros(Nc, device=dev),
                   "v": torch.zeros(Nc, 3, device=dev), "samp": torch.zeros(Nc, dtype=torch.int32, device=dev)}
-            if self.hip_colour and self.hip_loss:
-                from .train_f32 import ColourStep
-                st["col"] = ColourStep(self, q, Nc, st["fs32"], st["v"], self.feat, R)
+            from .train_f32 import ColourStep
+            st["col"] = ColourStep(self, q, Nc, st["fs32"], st["v"], self.feat, R)
             keep = [fl.grad.clone(), P.points_conf.grad.clone()]   # warm-up accumulates into them
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))

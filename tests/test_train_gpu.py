@@ -544,13 +544,14 @@ def test_touched_points_kernel_matches_torch():
     """sgn_touched_points (the single-GPU fp32 step's projection subset) against train.touched_rows
     over consecutive steps on one stamp table: the same set of points (point 0 always, -1 slots
     and samples >= S skipped, duplicates listed once), each step's count in its parity slot and
-    the other slot cleared; S = 0 lists point 0 alone."""
+    the other slot cleared; S = 0 lists point 0 alone.  Neighbour ids >= n_points are never
+    listed and are counted in the third word (a query / point-table mismatch must not pass silently)."""
     from sgnerf_amd.train import touched_rows
     g = torch.Generator().manual_seed(11)
     n_points, K, s_cap = 5000, 8, 3000
     stamp = torch.full((n_points,), -1, dtype=torch.int32, device=DEV)
     lst = torch.full((n_points,), -9, dtype=torch.int32, device=DEV)
-    cnt = torch.full((2,), 0, dtype=torch.int64, device=DEV)
+    cnt = torch.full((3,), 0, dtype=torch.int64, device=DEV)
     p = _lib.ptr
     for step, S in enumerate([2500, 3000, 0, 1777]):
         pidx = torch.randint(-1, n_points, (s_cap * K,), generator=g, dtype=torch.int32)
@@ -566,10 +567,20 @@ def test_touched_points_kernel_matches_torch():
         c = int(c)
         assert int(cnt[step & 1]) == c
         assert int(cnt[(step + 1) & 1]) == 0
+        assert int(cnt[2]) == 0
         got = torch.sort(lst[:c].cpu().long()).values
         assert torch.equal(got, idx[:c])
         if S == 0:
             assert c == 1 and int(lst[0]) == 0
+    # a planted out-of-range id (inside the S samples) is counted, never listed
+    pidx = torch.zeros(s_cap * K, dtype=torch.int32)
+    pidx[3] = n_points + 5
+    counters = torch.tensor([10, 0, 0, 0], dtype=torch.int32)
+    dp_, dc = pidx.to(DEV), counters.to(DEV)
+    _lib.check(_lib.lib().sgn_touched_points(p(dp_), p(dc), s_cap, K, n_points, 4, p(stamp), p(lst), p(cnt),
+                                             _lib.stream_handle()), "sgn_touched_points")
+    torch.cuda.synchronize()
+    assert int(cnt[2]) == 1 and int(cnt[0]) == 1 and int(lst[0]) == 0
 
 
 def test_model_ranks_frames_by_ray_miss_loss(tmp_path):

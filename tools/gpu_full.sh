@@ -25,5 +25,5 @@ for k in ("f16_mode", "lego", "sg", "config3_1gpu", "stress_dense", "train_confi
 print("cpu", d.get("cpu_baseline", {}).get("value"))
 PY
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
-    python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err || { echo PROF_FAIL; tail gpurun_out/prof_$TAG.err; exit 1; }
+    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err || { echo PROF_FAIL; tail gpurun_out/prof_$TAG.err; exit 1; }
 echo FULL_DONE
