@@ -123,14 +123,23 @@ __device__ __forceinline__ void dma_chunk(const WBlob &wb, char *dst, int w, int
     });
 }
 
-// piece J (of this wave's ceil(2 pairs / NWv)) of chunk N
+// piece J (of this wave's PW = ceil(2 pairs / NWv)) of chunk N: wave w moves the contiguous pieces
+// w PW .. w PW + PW - 1, so four consecutive pieces share one soffset / M0 and the instruction offset
+// (0 .. 3 KiB, applied to the blob address and the LDS address alike) steps through them: one s_mov pair per
+// four pieces instead of per piece (the initial dma_chunk keeps the interleaved assignment)
 template <class Net, int N, int J, int NWv = NW16>
 __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int lane, int) {
     using S = Sched<Net>;
     constexpr int nf = 2 * S::pairs(N);
-    const int i = w + NWv * J;
-    if (NWv * (J + 1) <= nf || i < nf)  // wave-uniform
-        lds_dma_1k(wb, dst + NWv * J * 1024, w, lane, S::off(N) + (uint32_t)(NWv * J * 1024));
+    constexpr int PW = (nf + NWv - 1) / NWv;
+    const int i = w * PW + J;
+    if (nf % NWv == 0 || i < nf) {  // wave-uniform
+        uint32_t soff = S::off(N) + (uint32_t)((J & ~3) * 1024);
+        asm volatile("" : "+s"(soff));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc,
+                                                 (__attribute__((address_space(3))) void *)(dst + (w * PW + (J & ~3)) * 1024),
+                                                 16, lane * 16 + w * PW * 1024, soff, (J & 3) * 1024, 0);
+    }
 }
 template <class Net, int N, int NWv = NW16>
 constexpr int dma_pieces() { return (2 * Sched<Net>::pairs(N) + NWv - 1) / NWv; }
@@ -263,8 +272,12 @@ struct X3S {
 // holds D[row 4g+i][unit 16t + (l & 15)]).
 // mid(integral_constant F) runs after pair F's MFMAs of every chunk (F counted over the layer: k-step
 // K, tile t -> F = K TP + t), so per-pair VALU work of another stage can ride between the MFMAs.
-template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, int AOFF = 0, int NS, int NA,
-          class SlotT, class InFn, class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>
+// PIPE: k-step K + 1's input (in) is converted halfway through k-step K's MFMAs (k-step 0's before the
+// layer's first chunk boundary), so a chunk's MFMAs start right after its boundary instead of behind the
+// conversion VALU.  Per pair the lo fragment (read after hi) feeds the first MFMA, so one lgkmcnt wait
+// covers both fragments.
+template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, int AOFF = 0, bool PIPE = false,
+          int NS, int NA, class SlotT, class InFn, class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>
 __device__ __forceinline__ void run_layer_ns(const WBlob &wb, char *lds, SlotT &slot, int w, int lane, int lz,
                                              f32x4 (&acc)[NS][NA], InFn &&in, PostFn &&post = PostFn{},
                                              EndFn &&end = EndFn{}, MidFn &&mid = MidFn{}) {
@@ -272,6 +285,8 @@ __device__ __forceinline__ void run_layer_ns(const WBlob &wb, char *lds, SlotT &
     constexpr int TP = ly.tp;
     static_assert((TP == 16 || TP == 8) && P < ly.np, "passes of 16 or 8 output tiles");
     static_assert(AOFF + TP <= NA, "accumulator view");
+    X3S<NS> Bn;
+    if constexpr (PIPE) Bn = in(std::integral_constant<int, 0>{});
     static_for<nch(ly)>([&](auto cc) {
         constexpr int C = decltype(cc)::value;
         constexpr int N = Sched<Net>::idx(L, P, C), NN = (N + 1) % Sched<Net>::total();
@@ -293,10 +308,13 @@ __device__ __forceinline__ void run_layer_ns(const WBlob &wb, char *lds, SlotT &
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);
         static_for<nk(ly, C)>([&](auto kk) {
             constexpr int KK = decltype(kk)::value;
-            // NS = 2 (one wave per SIMD, ~480 registers): a k-step's input conversion stays inside its
-            // k-step, so the B fragments of two k-steps are never live together
-            if constexpr (NS > 1 && KK > 0) __builtin_amdgcn_sched_barrier(0);
-            const X3S<NS> B = in(std::integral_constant<int, C * ly.kc + KK>{});
+            // NS = 2 without PIPE (the save mode): a k-step's input conversion stays inside its k-step, so
+            // the B fragments of two k-steps are never live together
+            constexpr int KS = C * ly.kc + KK;
+            if constexpr (NS > 1 && KK > 0 && !PIPE) __builtin_amdgcn_sched_barrier(0);
+            X3S<NS> B;
+            if constexpr (PIPE) B = Bn;
+            else B = in(std::integral_constant<int, KS>{});
             static_for<TP>([&](auto tt) {
                 constexpr int t = decltype(tt)::value, F = KK * TP + t;
                 const h8 Ah = fh[F % PD], Al = fl[F % PD];
@@ -308,13 +326,13 @@ __device__ __forceinline__ void run_layer_ns(const WBlob &wb, char *lds, SlotT &
                 for (int s = 0; s < NS; ++s) {
                     f32x4 &c = acc[s][AOFF + t];
                     if constexpr (TRANS) {
-                        c = mfma16(B.b[s].hi, Ah, c);
-                        c = mfma16(B.b[s].lo, Ah, c);
                         c = mfma16(B.b[s].hi, Al, c);
+                        c = mfma16(B.b[s].lo, Ah, c);
+                        c = mfma16(B.b[s].hi, Ah, c);
                     } else {
-                        c = mfma16(Ah, B.b[s].hi, c);
-                        c = mfma16(Ah, B.b[s].lo, c);
                         c = mfma16(Al, B.b[s].hi, c);
+                        c = mfma16(Ah, B.b[s].lo, c);
+                        c = mfma16(Ah, B.b[s].hi, c);
                     }
                 }
                 constexpr int NSP = NF / 2 > 0 ? NF / 2 : 1;
@@ -324,6 +342,9 @@ __device__ __forceinline__ void run_layer_ns(const WBlob &wb, char *lds, SlotT &
                     });
                 }
                 mid(std::integral_constant<int, (C * ly.kc + KK) * TP + t>{});
+                // (the clamped index keeps the discarded instantiation of the last k-step in range)
+                if constexpr (PIPE && t == TP / 2 - 1 && KS + 1 < ly.ks)
+                    Bn = in(std::integral_constant<int, (KS + 1 < ly.ks ? KS + 1 : KS)>{});
                 if constexpr (NS == 1) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -1003,7 +1024,7 @@ __global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs 
                     for (int t = 0; t < 16; ++t) accA[q][t] = accB[q][t];
                 }
             }
-            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>>(
+            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>, 0, 0, !SAVE>(
                 wb, ldsi, slot, w, lane, lz, accA, [&](auto k) {
                     X3S<NS> o;
 #pragma unroll
@@ -1016,7 +1037,7 @@ __global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs 
 #pragma unroll
         for (int q = 0; q < NS; ++q) bias_init(accB[q], Y_B1);
         int v_next[NS];
-        run_layer_ns<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {
+        run_layer_ns<Net, 1, false, VmZero, 0, 0, !SAVE>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {
             X3S<NS> o;
 #pragma unroll
             for (int q = 0; q < NS; ++q) o.b[q] = chain_k(q, accA[q], inv0, k, a.z1);
@@ -1062,7 +1083,7 @@ __global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs 
         const float inv_in2 = KB > 0 ? inv7 : inv1;
 #pragma unroll
         for (int q = 0; q < NS; ++q) bias_init(acc2[q], Y_B2);
-        run_layer_ns<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {
+        run_layer_ns<Net, L2, false, VmZero, 0, 0, !SAVE>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {
             constexpr int K = decltype(k)::value;
             X3S<NS> o;
 #pragma unroll
@@ -1115,7 +1136,7 @@ __global__ __launch_bounds__(TPBR, NS == 1 ? 8 / NWR : 1) void k_rows16(AggArgs 
             // registers it frees) and pass 1 (tiles 8..15) reuses them; pass 1 carries the epilogue of
             // pass 0's tiles, output tile T after k-step T (one per 8 MFMA pairs)
             X3B in3[NS][8];
-            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(
+            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0, !SAVE>(
                 wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
                     constexpr int K = decltype(k)::value;
                     X3S<NS> o;

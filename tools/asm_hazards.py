@@ -46,12 +46,17 @@ def scan(text):
         else:
             srcs = set().union(*[_regs(o) for o in ops[1:]]) if len(ops) > 1 else set()
         if inasm and op.startswith('v_') and not op.startswith('v_mfma'):
-            # look back for an MFMA reading / writing the asm's destination with no compiler-visible write
-            # of it in between (such a write already waited out the MFMA: the hazard recognizer saw it)
+            # look back for an MFMA reading / writing the asm's destination, or writing a register the asm
+            # reads, with no compiler-visible write of that register in between (such a write already waited
+            # out the MFMA: the hazard recognizer saw it, and the asm then reads / overwrites that write)
+            wd, rs = set(dst), set(srcs)
             for dist, (k, d2, s2, txt) in enumerate(reversed(hist[-16:])):
-                if k == 'other' and not txt.startswith('asm:') and dst & d2:
-                    break
-                if k == 'mfma' and (dst & s2 or dst & d2 or srcs & d2):  # WAR / WAW, or RAW of the MFMA's result
+                if k == 'other' and not txt.startswith('asm:'):
+                    wd -= d2
+                    rs -= d2
+                    if not wd and not rs:
+                        break
+                if k == 'mfma' and (wd & s2 or wd & d2 or rs & d2):  # WAR / WAW, or RAW of the MFMA's result
                     found.append(f'asm {s!r} {dist + 1} instrs after {txt!r}')
                     break
         if op.startswith('v_mfma'):

@@ -27,5 +27,5 @@ for r in rs:
 for k, v in by.items():
     print(f"{k:14s} rows " + " ".join(f"{r['agg_rows']:.3f}" for r in v) + "  colour " + " ".join(f"{r['agg_color']:.3f}" for r in v))
 PY
-for f in gpurun_out/tdbg_${TAG}_*.bin; do [ -f "$f" ] && python tools/x3_timing_ns2.py $f; done
+for f in gpurun_out/tdbg_${TAG}_*.bin; do [ -f "$f" ] || continue; case $f in *timing2*) python tools/x3_timing2.py $f;; *) python tools/x3_timing_ns2.py $f;; esac; done
 echo VAB_DONE

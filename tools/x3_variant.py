@@ -45,6 +45,25 @@ __device__ __forceinline__ void tstamp(int n) {
 '''
 
 
+TDUMP = '''            // the dump is of the SGN_X3_TDBG_LAUNCH-th (default 6th) inference row launch
+            static int tlaunch = 0;
+            const char *tpath = getenv("SGN_X3_TDBG");
+            const char *tl = getenv("SGN_X3_TDBG_LAUNCH");
+            const int tgt = tl ? atoi(tl) : 6;
+            const bool tme = tpath && !z && ns == 2 && ksb == 0 && i0 == 0 && ++tlaunch == tgt;
+            void *tptr = nullptr;
+            const size_t tn = sizeof(x3::g_tdbg);
+            SGN_CHECK_HIP(hipGetSymbolAddress(&tptr, HIP_SYMBOL(x3::g_tdbg)));
+            if (tme) SGN_CHECK_HIP(hipMemsetAsync(tptr, 0, tn, st));
+            hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < wmax ? wg16 : wmax)), dim3(x3::TPBR), 0, st, a);
+            if (tme) {
+                std::vector<unsigned long long> hb(tn / 8);
+                SGN_CHECK_HIP(hipMemcpyAsync(hb.data(), tptr, tn, hipMemcpyDeviceToHost, st));
+                SGN_CHECK_HIP(hipStreamSynchronize(st));
+                if (FILE *f = fopen(tpath, "wb")) { fwrite(hb.data(), 8, tn / 8, f); fclose(f); }
+            }'''
+
+
 def patch(s, p):
     if p == "timing":
         s = rep(s, "__device__ __forceinline__ int cur_slot(int s) { return s; }",
@@ -83,24 +102,131 @@ def patch(s, p):
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }''')
+        s = patch(s, "tdump")
+    elif p == "timing2":
+        # light stamps: 8 per tile at the layer boundaries of k_rows16<0, false, false, 2> (no chunk stamps)
+        s = rep(s, "__device__ __forceinline__ int cur_slot(int s) { return s; }", r'''
+constexpr int TD_BLOCKS = 8, TD_W = 4, TD_EV = 2048, TD_PER = 8;
+__device__ unsigned long long g_tdbg[TD_BLOCKS * TD_W * TD_EV];
+__device__ __forceinline__ void tst(bool on, int w, int it, int n) {
+    if (on && it < (TD_EV - 4) / TD_PER)
+        g_tdbg[(blockIdx.x * TD_W + w) * TD_EV + it * TD_PER + n] = __builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ int cur_slot(int s) { return s; }''')
+        s = rep(s, '''    for (int tile = xt.first; tile < xt.end; tile += xt.step) {
+        const int base = tile * WGS;''', '''    const bool tdo = !SAVE && KB == 0 && NS == 2 && blockIdx.x < TD_BLOCKS && lane == 0;
+    if (tdo) {
+        g_tdbg[(blockIdx.x * TD_W + w) * TD_EV + TD_EV - 4] = __builtin_amdgcn_s_memtime();
+        g_tdbg[(blockIdx.x * TD_W + w) * TD_EV + TD_EV - 3] = __builtin_amdgcn_s_memrealtime();
+    }
+    int tit = -1;
+    for (int tile = xt.first; tile < xt.end; tile += xt.step) {
+        ++tit;
+        tst(tdo, w, tit, 0);
+        const int base = tile * WGS;''')
+        s = rep(s, "            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>>(",
+                "            tst(tdo, w, tit, 1);\n            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>>(")
+        s = rep(s, "        run_layer_ns<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {",
+                "        tst(tdo, w, tit, 2);\n        run_layer_ns<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {")
+        s = rep(s, "        run_layer_ns<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {",
+                "        tst(tdo, w, tit, 3);\n        run_layer_ns<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {")
+        s = rep(s, "            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(",
+                "            tst(tdo, w, tit, 4);\n            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(")
+        s = rep(s, "            run_layer_ns<Net, L3, true, VmZero, 1, 8>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {",
+                "            tst(tdo, w, tit, 5);\n            run_layer_ns<Net, L3, true, VmZero, 1, 8>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {")
+        s = rep(s, "        // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads",
+                "        tst(tdo, w, tit, 6);\n        // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads")
+        s = rep(s, '''            for (int q = 0; q < NS; ++q) epi_end(e[q], ldsi, nA[q], nB[q], ix[q].s);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}''', '''            for (int q = 0; q < NS; ++q) epi_end(e[q], ldsi, nA[q], nB[q], ix[q].s);
+        }
+        tst(tdo, w, tit, 7);
+    }
+    if (tdo) {
+        g_tdbg[(blockIdx.x * TD_W + w) * TD_EV + TD_EV - 2] = __builtin_amdgcn_s_memtime();
+        g_tdbg[(blockIdx.x * TD_W + w) * TD_EV + TD_EV - 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}''')
+        s = patch(s, "tdump")
+    elif p == "tdump":
         s = rep(s, '''            hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < wmax ? wg16 : wmax)), dim3(x3::TPBR), 0, st, a);''',
-                '''            // the dump is of the SGN_X3_TDBG_LAUNCH-th (default 6th) inference row launch
-            static int tlaunch = 0;
-            const char *tpath = getenv("SGN_X3_TDBG");
-            const char *tl = getenv("SGN_X3_TDBG_LAUNCH");
-            const int tgt = tl ? atoi(tl) : 6;
-            const bool tme = tpath && !z && ns == 2 && ksb == 0 && i0 == 0 && ++tlaunch == tgt;
-            void *tptr = nullptr;
-            const size_t tn = sizeof(x3::g_tdbg);
-            SGN_CHECK_HIP(hipGetSymbolAddress(&tptr, HIP_SYMBOL(x3::g_tdbg)));
-            if (tme) SGN_CHECK_HIP(hipMemsetAsync(tptr, 0, tn, st));
-            hipLaunchKernelGGL(kern, dim3((unsigned)(wg16 < wmax ? wg16 : wmax)), dim3(x3::TPBR), 0, st, a);
-            if (tme) {
-                std::vector<unsigned long long> hb(tn / 8);
-                SGN_CHECK_HIP(hipMemcpyAsync(hb.data(), tptr, tn, hipMemcpyDeviceToHost, st));
-                SGN_CHECK_HIP(hipStreamSynchronize(st));
-                if (FILE *f = fopen(tpath, "wb")) { fwrite(hb.data(), 8, tn / 8, f); fclose(f); }
-            }''')
+                TDUMP)
+    elif p == "v_wait":
+        # one lgkmcnt wait per fragment pair: the lo fragment (loaded after hi) is used first
+        s = rep(s, '''                    if constexpr (TRANS) {
+                        c = mfma16(B.b[s].hi, Ah, c);
+                        c = mfma16(B.b[s].lo, Ah, c);
+                        c = mfma16(B.b[s].hi, Al, c);
+                    } else {
+                        c = mfma16(Ah, B.b[s].hi, c);
+                        c = mfma16(Ah, B.b[s].lo, c);
+                        c = mfma16(Al, B.b[s].hi, c);
+                    }''', '''                    if constexpr (TRANS) {
+                        c = mfma16(B.b[s].hi, Al, c);
+                        c = mfma16(B.b[s].lo, Ah, c);
+                        c = mfma16(B.b[s].hi, Ah, c);
+                    } else {
+                        c = mfma16(Al, B.b[s].hi, c);
+                        c = mfma16(Ah, B.b[s].lo, c);
+                        c = mfma16(Ah, B.b[s].hi, c);
+                    }''')
+    elif p == "v_dma":
+        # contiguous pieces per wave: wave w moves pieces w PW .. w PW + PW - 1 of a chunk; four consecutive
+        # pieces share one soffset / M0, the instruction offset (0..3 KiB) steps through them
+        s = rep(s, '''template <class Net, int N, int J, int NWv = NW16>
+__device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int lane, int) {
+    using S = Sched<Net>;
+    constexpr int nf = 2 * S::pairs(N);
+    const int i = w + NWv * J;
+    if (NWv * (J + 1) <= nf || i < nf)  // wave-uniform
+        lds_dma_1k(wb, dst + NWv * J * 1024, w, lane, S::off(N) + (uint32_t)(NWv * J * 1024));
+}''', '''template <class Net, int N, int J, int NWv = NW16>
+__device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int lane, int) {
+    using S = Sched<Net>;
+    constexpr int nf = 2 * S::pairs(N);
+    constexpr int PW = (nf + NWv - 1) / NWv;
+    const int i = w * PW + J;
+    if (nf % NWv == 0 || i < nf) {  // wave-uniform
+        uint32_t soff = S::off(N) + (uint32_t)((J & ~3) * 1024);
+        asm volatile("" : "+s"(soff));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc,
+                                                 (__attribute__((address_space(3))) void *)(dst + (w * PW + (J & ~3)) * 1024),
+                                                 16, lane * 16 + w * PW * 1024, soff, (J & 3) * 1024, 0);
+    }
+}''')
+    elif p == "v_pipe":
+        # block3.2 pass 0: k-step K + 1's input converted in the middle of k-step K's MFMAs (its fragments are
+        # kept for pass 1 anyway, so both being live costs no registers)
+        s = rep(s, '''template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, int AOFF = 0, int NS, int NA,
+          class SlotT, class InFn, class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>''',
+                '''template <class Net, int L, bool TRANS = false, class Vm = VmZero, int P = 0, int AOFF = 0, bool PIPE = false,
+          int NS, int NA, class SlotT, class InFn, class PostFn = NoHook, class EndFn = NoHook, class MidFn = NoHook>''')
+        s = rep(s, '''    static_assert(AOFF + TP <= NA, "accumulator view");
+    static_for<nch(ly)>([&](auto cc) {''', '''    static_assert(AOFF + TP <= NA, "accumulator view");
+    X3S<NS> Bn;
+    if constexpr (PIPE) Bn = in(std::integral_constant<int, 0>{});
+    static_for<nch(ly)>([&](auto cc) {''')
+        s = rep(s, '''            if constexpr (NS > 1 && KK > 0) __builtin_amdgcn_sched_barrier(0);
+            const X3S<NS> B = in(std::integral_constant<int, C * ly.kc + KK>{});''', '''            constexpr int KS = C * ly.kc + KK;
+            if constexpr (NS > 1 && KK > 0 && !PIPE) __builtin_amdgcn_sched_barrier(0);
+            X3S<NS> B;
+            if constexpr (PIPE) B = Bn;
+            else B = in(std::integral_constant<int, KS>{});''')
+        s = rep(s, '''                mid(std::integral_constant<int, (C * ly.kc + KK) * TP + t>{});''', '''                mid(std::integral_constant<int, (C * ly.kc + KK) * TP + t>{});
+                if constexpr (PIPE && t == TP / 2 - 1 && KS + 1 < ly.ks) Bn = in(std::integral_constant<int, KS + 1>{});''')
+        s = rep(s, '''            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(''',
+                '''            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0, !SAVE>(''')
+    elif p == "v_pipeall":
+        # (after v_pipe) every row-kernel layer converts k-step K + 1's input during k-step K's MFMAs
+        s = rep(s, "            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>>(",
+                "            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>, 0, 0, !SAVE>(")
+        s = rep(s, "        run_layer_ns<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {",
+                "        run_layer_ns<Net, 1, false, VmZero, 0, 0, !SAVE>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {")
+        s = rep(s, "        run_layer_ns<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {",
+                "        run_layer_ns<Net, L2, false, VmZero, 0, 0, !SAVE>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {")
     elif p == "abl_dma":
         s = rep(s, '''    asm volatile("" : "+s"(soff));
     __builtin_amdgcn_raw_ptr_buffer_load_lds(''', '''    return;
@@ -153,6 +279,53 @@ def patch(s, p):
     return s
 
 
+def patch_tx(s, p):
+    """patches of train_x3.hip (the fp32 training GEMMs)"""
+    if p == "tx_rows2":
+        # backward-data / forward rows GEMMs at K 256 / 288: 64-column weight blocks (64 KiB of LDS), two
+        # workgroups per CU (two waves per SIMD hide each other's load / store latency)
+        s = rep(s, '''template <int KS, int WN, bool P1 = false>
+__global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {''', '''template <int KS, int WN, bool P1 = false, int OCC = 1>
+__global__ __launch_bounds__(TPB, OCC) void k_x3rows(GemmK g) {''')
+        s = rep(s, '''        const bool w96 = ((g.N + 95) / 96) * 96 < ((g.N + 127) / 128) * 128;
+        const int BN = w96 ? 96 : 128;''', '''        const bool w96 = ((g.N + 95) / 96) * 96 < ((g.N + 127) / 128) * 128;
+        const bool occ2 = !p1 && (g.K + 15) / 16 > 8;
+        const int BN = occ2 ? 64 : w96 ? 96 : 128;''')
+        s = rep(s, '''        int gy = 256 / nb;''', '''        int gy = (occ2 ? 512 : 256) / nb;''')
+        s = rep(s, '''        } else if (ks <= 16) {
+            if (w96) hipLaunchKernelGGL((k_x3rows<16, 3>), grid, dim3(TPB), 0, st, k);
+            else hipLaunchKernelGGL((k_x3rows<16, 4>), grid, dim3(TPB), 0, st, k);
+        } else {
+            if (w96) hipLaunchKernelGGL((k_x3rows<18, 3>), grid, dim3(TPB), 0, st, k);
+            else hipLaunchKernelGGL((k_x3rows<18, 4>), grid, dim3(TPB), 0, st, k);
+        }''', '''        } else if (ks <= 16) {
+            hipLaunchKernelGGL((k_x3rows<16, 2, false, 2>), grid, dim3(TPB), 0, st, k);
+        } else {
+            hipLaunchKernelGGL((k_x3rows<18, 2, false, 2>), grid, dim3(TPB), 0, st, k);
+        }''')
+    elif p == "tx_tn2":
+        # weight gradients at M 256: 256 x 64 blocks, two workgroups per CU (80 KiB of LDS each)
+        s = rep(s, '''template <int WM, int WN, bool P1 = false>
+__global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {''', '''template <int WM, int WN, bool P1 = false, int OCC = 1>
+__global__ __launch_bounds__(TPB, OCC) void k_x3tn(GemmK g) {''')
+        s = rep(s, '''        const int BN = g.N <= 32 ? 32 : (BM == 128 && g.N <= 160) ? 160 : 96;''',
+                '''        const int BN = g.N <= 32 ? 32 : (BM == 128 && g.N <= 160) ? 160 : BM == 256 ? 64 : 96;''')
+        s = rep(s, '''        } else if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3tn<2, 3>), grid, dim3(TPB), 0, st, k);''',
+                '''        } else if (BM == 256 && BN == 64) hipLaunchKernelGGL((k_x3tn<2, 2, false, 2>), grid, dim3(TPB), 0, st, k);''')
+    elif p == "tx_tn3":
+        # weight gradients at M 256: 128 x 96 blocks, two workgroups per CU (56 KiB of LDS each)
+        s = rep(s, '''template <int WM, int WN, bool P1 = false>
+__global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {''', '''template <int WM, int WN, bool P1 = false, int OCC = 1>
+__global__ __launch_bounds__(TPB, OCC) void k_x3tn(GemmK g) {''')
+        s = rep(s, '''        const int BM = g.M > 128 ? 256 : 128;''', '''        const int BM = 128;''')
+        s = rep(s, '''        else if (BN == 96) hipLaunchKernelGGL((k_x3tn<1, 3>), grid, dim3(TPB), 0, st, k);''',
+                '''        else if (BN == 96 && g.M > 128) hipLaunchKernelGGL((k_x3tn<1, 3, false, 2>), grid, dim3(TPB), 0, st, k);
+        else if (BN == 96) hipLaunchKernelGGL((k_x3tn<1, 3>), grid, dim3(TPB), 0, st, k);''')
+    else:
+        return None
+    return s
+
+
 def main():
     name, patches = sys.argv[1], sys.argv[2:]
     subprocess.check_call(["make", "-s", "-C", CSRC, "-j8"])
@@ -162,20 +335,34 @@ def main():
     shutil.copytree(CSRC, work, ignore=shutil.ignore_patterns("build"))
     os.symlink(os.path.join(ROOT, "include"), os.path.join(top, "include"))
     src = open(os.path.join(work, "mlp_x3.hip")).read()
+    tsrc = open(os.path.join(work, "train_x3.hip")).read()
     for p in patches:
-        src = patch(src, p)
+        t = patch_tx(tsrc, p)
+        if t is not None:
+            tsrc = t
+        else:
+            src = patch(src, p)
     open(os.path.join(work, "mlp_x3.hip"), "w").write(src)
+    open(os.path.join(work, "train_x3.hip"), "w").write(tsrc)
+    txp = [q for q in patches if q.startswith("tx_")]
+    xp = [q for q in patches if not q.startswith("tx_")]
+    targets = (["mlp_x3"] if xp else []) + (["train_x3"] if txp else [])
     out_dir = os.path.join(ROOT, "build", "variants")
     os.makedirs(out_dir, exist_ok=True)
     hipcc = "/opt/rocm/bin/hipcc"
     fl = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-munsafe-fp-atomics",
           "-fno-slp-vectorize", "-I" + os.path.join(ROOT, "include")]
-    obj = os.path.join(work, "mlp_x3.o")
-    subprocess.check_call([hipcc, *fl, "-c", os.path.join(work, "mlp_x3.hip"), "-o", obj])
+    new_objs = []
+    for t in targets:
+        obj = os.path.join(work, t + ".o")
+        extra = ["-fno-slp-vectorize"] if t == "mlp_x3" else []
+        subprocess.check_call([hipcc, *[f for f in fl if f != "-fno-slp-vectorize"], *extra, "-save-temps=obj", "-c",
+                               os.path.join(work, t + ".hip"), "-o", obj])
+        new_objs.append(obj)
     objs = [os.path.join(CSRC, "build", f) for f in sorted(os.listdir(os.path.join(CSRC, "build")))
-            if f.endswith(".o") and f != "mlp_x3.o"]
+            if f.endswith(".o") and f[:-2] not in targets]
     so = os.path.join(out_dir, name + ".so")
-    subprocess.check_call([hipcc, "--offload-arch=gfx950", "-shared", "-Wl,-rpath,/opt/rocm/lib", "-o", so, *objs, obj])
+    subprocess.check_call([hipcc, "--offload-arch=gfx950", "-shared", "-Wl,-rpath,/opt/rocm/lib", "-o", so, *objs, *new_objs])
     print(so)
 
 
