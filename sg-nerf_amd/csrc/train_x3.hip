@@ -105,95 +105,113 @@ __device__ __forceinline__ int op_shift(const Opnd &o) {
 
 __device__ __forceinline__ float lrelu_ref(float x) { return x > 0.f ? x : x * 0.01f; }
 
-// element (i, k .. k + 7) of an operand (i: the M / N index, k: the reduction index); rows past
-// `lim` read as 0.  kmajor 0: matrix row i, columns k..k+7; kmajor 1: rows k..k+7, column i.
-__device__ __forceinline__ void load8(const Opnd &o, int i, int k, int lim, float (&v)[8]) {
-    if (!o.kmajor) {
-        const bool rok = i < lim;
-        const bool s1 = k < o.csplit;
-        const float *src = s1 ? o.p + (int64_t)i * o.ld + k : o.p2 + (int64_t)i * o.ld2 + (k - o.csplit);
-        const bool full = rok && o.vec && k + 8 <= o.ncols && (o.ones_col < k || o.ones_col >= k + 8);
-        if (full) {
-            const f32x4 a = *(const f32x4 *)src, b = *(const f32x4 *)(src + 4);
-            v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
-            v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int c = k + e;
-                v[e] = !rok ? 0.f : c == o.ones_col ? 1.f : c < o.ncols ? src[e] : 0.f;
-            }
-        }
-        if (o.act && s1) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                if (k + e != o.ones_col) v[e] = lrelu_ref(v[e]);
-        }
-    } else {
-        if (i == o.ones_col) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = k + e < lim ? 1.f : 0.f;
-        } else if (i < o.ncols) {
-            const bool s1 = i < o.csplit;
-            const float *src = s1 ? o.p + i : o.p2 + (i - o.csplit);
-            const int64_t ld = s1 ? o.ld : o.ld2;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = k + e < lim ? src[(int64_t)(k + e) * ld] : 0.f;
-            if (o.act && s1) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = lrelu_ref(v[e]);
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = 0.f;
-        }
-    }
-}
-
 // ---- split-K mode: C[m][n] = sum over rows r of A(m, r) B(n, r) ---------------------------------
 // Both operands are row-major [rows][cols] (kmajor).  A stage is 32 rows; thread t of an operand loads
 // 4 consecutive columns (a quad) of 8 consecutive rows (an octet) as 8 float4, which transpose in
 // registers into the lane fragments of those 4 columns (8 k values each).  Stages are loaded two ahead
 // into registers, converted into LDS (two buffers), then 2 k-steps of MFMAs: 4 waves split M, each
 // wave WM x WN 32x32 tiles.
+// Buffer view of an operand's rows [0, rows): loads past them return 0 (the hardware range check),
+// stores past them are dropped -- no per-row branches in the loops.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void *p, int64_t ld, int64_t rows) {
+    int64_t bytes = rows * ld * 4;
+    bytes = bytes < 0 ? 0 : bytes > 0x7fffffff ? 0x7fffffff : bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+constexpr uint32_t OOB = 0x80000000u;  // a byte offset past every operand buffer: loads 0, stores dropped
+
+__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// A split-K operand's two sources as buffers over the split's rows [0, r1) (p2: the columns >= csplit)
+struct OpRs {
+    __amdgpu_buffer_rsrc_t r1, r2;
+};
+__device__ __forceinline__ OpRs op_rsrc(const Opnd &o, int r1) {
+    return OpRs{rows_rsrc(o.p, o.ld, r1), rows_rsrc(o.p2 ? o.p2 : o.p, o.p2 ? o.ld2 : o.ld, r1)};
+}
+
+// element (i, k .. k + 7) of an operand (i: the M / N index, k: the reduction index, a multiple of 8)
+// through its buffers over the matrix rows [0, lim) (rows past them read 0): kmajor 0: matrix row i,
+// columns k..k+7; kmajor 1: rows k..k+7, column i.  Both sources are read and one selected per lane (the
+// weight staging of the rows mode, once per workgroup), no branches.
+__device__ __forceinline__ void load8(const Opnd &o, const OpRs &rs, int i, int k, int lim, float (&v)[8]) {
+    if (!o.kmajor) {
+        const bool s1 = k < o.csplit;  // csplit % 8 == 0: the octet has one source
+        const int64_t rb1 = (int64_t)i * o.ld, rb2 = (int64_t)i * (o.p2 ? o.ld2 : o.ld);
+        const uint32_t a1 = s1 ? (uint32_t)((rb1 + k) * 4) : OOB, a2 = s1 ? OOB : (uint32_t)((rb2 + k - o.csplit) * 4);
+        const float4 x1 = ld4(rs.r1, a1), y1 = ld4(rs.r1, a1 + 16), x2 = ld4(rs.r2, a2), y2 = ld4(rs.r2, a2 + 16);
+        const float4 x = s1 ? x1 : x2, y = s1 ? y1 : y2;
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+        const bool rok = i < lim;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int c = k + e;
+            float u = c == o.ones_col ? (rok ? 1.f : 0.f) : c < o.ncols ? v[e] : 0.f;
+            if (o.act && s1 && c != o.ones_col) u = lrelu_ref(u);
+            v[e] = u;
+        }
+    } else {
+        const bool s1 = i < o.csplit;
+        const int c2 = s1 ? 0 : i - o.csplit;
+        const bool cok = i < o.ncols && i != o.ones_col;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int r = k + e;
+            const uint32_t a1 = s1 ? (uint32_t)(((int64_t)r * o.ld + i) * 4) : OOB;
+            const uint32_t a2 = s1 ? OOB : (uint32_t)(((int64_t)r * (o.p2 ? o.ld2 : o.ld) + c2) * 4);
+            const float x1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs.r1, a1, 0, 0));
+            const float x2 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs.r2, a2, 0, 0));
+            float u = i == o.ones_col ? (r < lim ? 1.f : 0.f) : cok ? (s1 ? x1 : x2) : 0.f;
+            if (o.act && s1 && cok) u = lrelu_ref(u);
+            v[e] = u;
+        }
+    }
+}
+
 template <int Q>  // column quads of the operand's block
 struct QStage {
     float4 v[8];
-    __device__ __forceinline__ void load(const Opnd &o, int c0, int r0, int lim, int tid) {
+    // thread t loads the column quad c0 + 4 (t % Q) of rows r0 + 8 (t / Q) .. + 7 as 8 float4 (rows past the
+    // split's end read 0 through the buffer range).  Lanes whose quad is special (a column past ncols, the
+    // ones column) patch it only in waves that hold one (wave-uniform branch); LeakyReLU on p's columns.
+    __device__ __forceinline__ void load(const Opnd &o, const OpRs &rs, int c0, int r0, int rend, int tid) {
         if (tid >= 4 * Q) return;
         const int q = tid % Q, oc = tid / Q;
         const int c = c0 + 4 * q, r = r0 + 8 * oc;
         const bool s1 = c < o.csplit;
-        const float *src = s1 ? o.p + c : o.p2 + (c - o.csplit);
+        const int cc = s1 ? c : c - o.csplit;
         const int64_t ld = s1 ? o.ld : o.ld2;
-        const bool full = o.vec && c + 4 <= o.ncols && (o.ones_col < c || o.ones_col >= c + 4);
-        if (full) {
+        const bool cin = c < o.ncols;
+        const uint32_t step = (uint32_t)(ld * 4);
+        uint32_t off = (uint32_t)(((int64_t)r * ld + (cin ? cc : 0)) * 4);
+        const bool mixed = __ballot(!s1) != 0 && o.p2;   // wave-uniform: a p2 quad in this wave
+        if (!mixed) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-                v[e] = r + e < lim ? *(const float4 *)(src + (int64_t)(r + e) * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
-            if (o.act && s1) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    v[e] = make_float4(lrelu_ref(v[e].x), lrelu_ref(v[e].y), lrelu_ref(v[e].z), lrelu_ref(v[e].w));
-            }
+            for (int e = 0; e < 8; ++e) v[e] = ld4(rs.r1, off + e * step);
         } else {
+            const uint32_t o1 = s1 ? off : OOB, o2 = s1 ? OOB : off;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                float x[4];
+                const float4 a = ld4(rs.r1, o1 + e * step), b = ld4(rs.r2, o2 + e * step);
+                v[e] = s1 ? a : b;
+            }
+        }
+        if (o.act && s1) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int cc = c + j;
-                    float u = 0.f;
-                    if (r + e < lim) {
-                        if (cc == o.ones_col) u = 1.f;
-                        else if (cc < o.ncols) {
-                            const bool t1 = cc < o.csplit;
-                            u = t1 ? o.p[(int64_t)(r + e) * o.ld + cc] : o.p2[(int64_t)(r + e) * o.ld2 + (cc - o.csplit)];
-                            if (o.act && t1) u = lrelu_ref(u);
-                        }
-                    }
-                    x[j] = u;
-                }
+            for (int e = 0; e < 8; ++e)
+                v[e] = make_float4(lrelu_ref(v[e].x), lrelu_ref(v[e].y), lrelu_ref(v[e].z), lrelu_ref(v[e].w));
+        }
+        const bool spec = c + 4 > o.ncols || (o.ones_col >= c && o.ones_col < c + 4);
+        if (__ballot(spec) != 0) {   // wave-uniform
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const bool rok = r + e < rend;
+                float x[4] = {v[e].x, v[e].y, v[e].z, v[e].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) x[j] = c + j == o.ones_col ? (rok ? 1.f : 0.f) : c + j < o.ncols ? x[j] : 0.f;
                 v[e] = make_float4(x[0], x[1], x[2], x[3]);
             }
         }
@@ -237,6 +255,7 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
     const int per = ((rows + g.splits - 1) / g.splits + 31) / 32 * 32;
     const int r0 = split * per, r1 = min(rows, r0 + per);
     const int nkb = r1 > r0 ? (r1 - r0 + 31) / 32 : 0;
+    const OpRs ra = op_rsrc(g.A, r1), rb = op_rsrc(g.B, r1);
     f32x16 acc[WM][WN];
 #pragma unroll
     for (int a = 0; a < WM; ++a)
@@ -270,11 +289,11 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
         }
     };
     if (nkb > 0) {
-        a0.load(g.A, m0, r0, r1, tid);
-        b0.load(g.B, n0, r0, r1, tid);
+        a0.load(g.A, ra, m0, r0, r1, tid);
+        b0.load(g.B, rb, n0, r0, r1, tid);
         if (nkb > 1) {
-            a1.load(g.A, m0, r0 + 32, r1, tid);
-            b1.load(g.B, n0, r0 + 32, r1, tid);
+            a1.load(g.A, ra, m0, r0 + 32, r1, tid);
+            b1.load(g.B, rb, n0, r0 + 32, r1, tid);
         }
         a0.template store<P1>(lds, fa, tid);
         b0.template store<P1>(lds + ABYTES, fb, tid);
@@ -283,8 +302,8 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
         // stage kb + 1 in registers, stage kb + 2 loading
         for (int kb = 0; kb < nkb; kb += 2) {
             if (kb + 2 < nkb) {
-                a0.load(g.A, m0, r0 + 32 * (kb + 2), r1, tid);
-                b0.load(g.B, n0, r0 + 32 * (kb + 2), r1, tid);
+                a0.load(g.A, ra, m0, r0 + 32 * (kb + 2), r1, tid);
+                b0.load(g.B, rb, n0, r0 + 32 * (kb + 2), r1, tid);
             }
             compute(lds);
             if (kb + 1 < nkb) {
@@ -294,8 +313,8 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
             __syncthreads();
             if (kb + 1 >= nkb) break;
             if (kb + 3 < nkb) {
-                a1.load(g.A, m0, r0 + 32 * (kb + 3), r1, tid);
-                b1.load(g.B, n0, r0 + 32 * (kb + 3), r1, tid);
+                a1.load(g.A, ra, m0, r0 + 32 * (kb + 3), r1, tid);
+                b1.load(g.B, rb, n0, r0 + 32 * (kb + 3), r1, tid);
             }
             compute(lds + STAGE);
             if (kb + 2 < nkb) {
@@ -305,7 +324,8 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
             __syncthreads();
         }
     }
-    float *part = g.part + (int64_t)split * g.M * g.N;
+    // this split's partial [M][N] through a buffer: elements outside it are dropped, not branched around
+    const __amdgpu_buffer_rsrc_t pr = rows_rsrc(g.part + (int64_t)split * g.M * g.N, g.N, g.M);
 #pragma unroll
     for (int a = 0; a < WM; ++a)
 #pragma unroll
@@ -314,7 +334,8 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + (w * WM + a) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (m < g.M && n < g.N) part[(int64_t)m * g.N + n] = acc[a][b][r] * osc;
+                const uint32_t off = n < g.N ? (uint32_t)((m * g.N + n) * 4) : OOB;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[a][b][r] * osc), pr, off, 0, 0);
             }
         }
 }
@@ -328,32 +349,32 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
 // so a whole tile of MFMAs hides it.  One workgroup per CU (the weight block is up to 144 KiB).
 constexpr int RT_ROWS = 128;
 
-// the A operand of the rows mode: row-major, 16-B aligned rows, columns in whole octets (host-checked)
+// the A operand of the rows mode: row-major, 16-B aligned rows, columns in whole octets, the column
+// split at a multiple of 16 (host-checked), read through buffers over the valid rows (rows past them
+// read 0): lane's row offset in each source; k-step kb's source choice is wave-uniform
 struct ARow {
-    const float *r1, *r2;  // this lane's row in source 1 / 2 (null past the rows)
+    __amdgpu_buffer_rsrc_t r1, r2;
+    uint32_t o1, o2;
     int csplit, ncols, act;
-    __device__ __forceinline__ void load(int k, float (&v)[8]) const {
-        const bool s1 = k < csplit;
-        const float *src = s1 ? r1 + k : r2 + (k - csplit);
-        if (r1 && k < ncols) {
-            const f32x4 x = *(const f32x4 *)src, y = *(const f32x4 *)(src + 4);
-            v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
-            v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
-            if (act && s1) {
+    __device__ __forceinline__ void load(int kb, int hk, float (&v)[8]) const {
+        const int k = kb + 8 * hk;
+        const bool s1 = kb < csplit;  // wave-uniform
+        const uint32_t off = k >= ncols ? OOB : s1 ? o1 + (uint32_t)k * 4 : o2 + (uint32_t)(k - csplit) * 4;
+        const float4 x = ld4(s1 ? r1 : r2, off), y = ld4(s1 ? r1 : r2, off + 16);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+        if (act && s1) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = lrelu_ref(v[e]);
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = 0.f;
+            for (int e = 0; e < 8; ++e) v[e] = lrelu_ref(v[e]);
         }
     }
 };
-__device__ __forceinline__ ARow arow(const Opnd &o, int row, int lim) {
+__device__ __forceinline__ ARow arow(const Opnd &o, const OpRs &rs, int row) {
     ARow a;
-    const bool ok = row < lim;
-    a.r1 = ok ? o.p + (int64_t)row * o.ld : nullptr;
-    a.r2 = ok && o.p2 ? o.p2 + (int64_t)row * o.ld2 : a.r1;
+    a.r1 = rs.r1;
+    a.r2 = rs.r2;
+    a.o1 = (uint32_t)((int64_t)row * o.ld * 4);
+    a.o2 = o.p2 ? (uint32_t)((int64_t)row * o.ld2 * 4) : a.o1;
     a.csplit = o.csplit;
     a.ncols = o.ncols;
     a.act = o.act;
@@ -375,17 +396,19 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
     const int n0 = nblk * (32 * WN);
     const int L = lane & 31, hk = lane >> 5;
     // the first tile's A loads go out before the weight staging
+    const OpRs rsA = op_rsrc(g.A, limA);
     float a[KS][8];
     {
-        const ARow ar = arow(g.A, rt * RT_ROWS + 32 * w + L, limA);
+        const ARow ar = arow(g.A, rsA, rt * RT_ROWS + 32 * w + L);
 #pragma unroll
-        for (int s = 0; s < KS; ++s) ar.load(16 * s + 8 * hk, a[s]);
+        for (int s = 0; s < KS; ++s) ar.load(16 * s, hk, a[s]);
     }
     // weights: lane fragment f = (k-step s, tile t, lane) -> ((s WN + t) 2 + hi/lo) FRAG + lane 16
+    const OpRs rsB = op_rsrc(g.B, g.B.nrows);
     for (int f = tid; f < KS * WN * 64; f += TPB) {
         const int fl = f & 63, t = (f >> 6) % WN, s = f / (64 * WN);
         float v[8];
-        load8(g.B, n0 + 32 * t + (fl & 31), 16 * s + 8 * (fl >> 5), g.B.nrows, v);
+        load8(g.B, rsB, n0 + 32 * t + (fl & 31), 16 * s + 8 * (fl >> 5), g.B.nrows, v);
         const X3Pair x = split8_scaled(v, fb);
         char *d = lds + ((s * WN + t) * 2) * FRAG + fl * 16;
         *(h8 *)d = x.hi;
@@ -393,16 +416,21 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
     }
     __syncthreads();
     float am1 = 0.f, am2 = 0.f;
+    // outputs, mask and bias through buffers over the valid rows / columns (no per-value branches)
+    const __amdgpu_buffer_rsrc_t ro1 = rows_rsrc(g.out, g.ldo, rows);
+    const __amdgpu_buffer_rsrc_t ro2 = rows_rsrc(g.out2 ? g.out2 : g.out, g.out2 ? g.ldo2 : g.ldo, g.out2 ? rows : 0);
+    const __amdgpu_buffer_rsrc_t rmk = rows_rsrc(g.mask ? g.mask : g.out, g.ldm, g.mask ? rows : 0);
+    const __amdgpu_buffer_rsrc_t rbs = rows_rsrc(g.bias ? g.bias : g.out, 1, g.bias ? g.N : 0);
     for (; rt * RT_ROWS < rows; rt += gy) {
         const int m0 = rt * RT_ROWS + 32 * w;
-        const ARow an = arow(g.A, (rt + gy) * RT_ROWS + 32 * w + L, limA);
+        const ARow an = arow(g.A, rsA, (rt + gy) * RT_ROWS + 32 * w + L);
         f32x16 acc[WN];
 #pragma unroll
         for (int t = 0; t < WN; ++t) acc[t] = f32x16{};
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const X3Pair x = split8_scaled(a[s], fa);
-            an.load(16 * s + 8 * hk, a[s]);  // the next tile's k-step s
+            an.load(16 * s, hk, a[s]);  // the next tile's k-step s
             const char *p = lds + (s * WN * 2) * FRAG + lane * 16;
 #pragma unroll
             for (int t = 0; t < WN; ++t) {
@@ -417,40 +445,47 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
         }
         // epilogue: every mask value of the tile is loaded before any is used (one wait, not 16 per tile)
         float mk[WN][16];
-        if (g.mask) {
+        if (g.mask) {   // (rows past the valid ones and columns past out_cols read 0: only out's columns are masked)
 #pragma unroll
             for (int t = 0; t < WN; ++t) {
                 const int n = n0 + 32 * t + L;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                    mk[t][r] = row < rows && n < g.out_cols ? g.mask[(int64_t)row * g.ldm + n] : 1.f;
+                    const uint32_t off = n < g.out_cols ? (uint32_t)(((int64_t)row * g.ldm + n) * 4) : OOB;
+                    mk[t][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rmk, off, 0, 0));
                 }
             }
         }
+        auto epilogue = [&](auto o2c) {  // o2c: the launch writes out2 (kernel-uniform, one branch per tile)
+            constexpr bool O2 = decltype(o2c)::value;
 #pragma unroll
-        for (int t = 0; t < WN; ++t) {
-            const int n = n0 + 32 * t + L;
-            const float bv = g.bias && n < g.N ? g.bias[n] : 0.f;
-            const bool o1 = n < g.out_cols, o2 = !o1 && n < g.N;
-            float *d1 = g.out + n, *d2 = g.out2 + (n - g.out_cols);
+            for (int t = 0; t < WN; ++t) {
+                const int n = n0 + 32 * t + L;
+                const float bv =
+                    __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbs, n < g.N ? (uint32_t)n * 4 : OOB, 0, 0));
+                const bool o1 = n < g.out_cols, o2 = !o1 && n < g.N;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                float v = acc[t][r] * osc + bv;
-                if (g.mask && !(mk[t][r] > 0.f)) v *= 0.01f;
-                if (o1) {
-                    if (g.act) v = lrelu_ref(v);
-                    if (row < rows) {
-                        d1[(int64_t)row * g.ldo] = v;
-                        am1 = fmaxf(am1, fabsf(v));
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+                    const bool rok = row < rows;
+                    float v = acc[t][r] * osc + bv;
+                    if (g.mask && o1 && !(mk[t][r] > 0.f)) v *= 0.01f;
+                    const float v1 = g.act ? lrelu_ref(v) : v;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v1), ro1,
+                                                          o1 ? (uint32_t)(((int64_t)row * g.ldo + n) * 4) : OOB, 0, 0);
+                    am1 = fmaxf(am1, o1 && rok ? fabsf(v1) : 0.f);
+                    if constexpr (O2) {
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __builtin_bit_cast(uint32_t, v), ro2,
+                            o2 ? (uint32_t)(((int64_t)row * g.ldo2 + n - g.out_cols) * 4) : OOB, 0, 0);
+                        am2 = fmaxf(am2, o2 && rok ? fabsf(v) : 0.f);
                     }
-                } else if (o2 && row < rows) {
-                    d2[(int64_t)row * g.ldo2] = v;
-                    am2 = fmaxf(am2, fabsf(v));
                 }
             }
-        }
+        };
+        if (g.out2) epilogue(std::true_type{});
+        else epilogue(std::false_type{});
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1029,6 +1064,9 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
         k.B.nrows = g.b.kmajor ? g.K : g.N;
     } else {
         SGN_REQUIRE(g.a.kmajor && g.b.kmajor, "mode 1: both operands [rows][...] (kmajor)");
+        SGN_REQUIRE(k.A.vec && k.B.vec && (g.a.csplit >= g.a.ncols || g.a.csplit % 4 == 0) &&
+                        (g.b.csplit >= g.b.ncols || g.b.csplit % 4 == 0),
+                    "mode 1: 16-B aligned rows (ld % 4 == 0) and column splits at a multiple of 4");
         SGN_REQUIRE(g.part && g.splits >= 1 && g.splits <= 4096, "mode 1: partials and 1..4096 splits");
     }
     k.M = g.M; k.N = g.N; k.K = g.K;
@@ -1043,8 +1081,9 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
     if (g.mode == 0) {
         if (g.M == 0) return 0;
         SGN_REQUIRE(g.K <= 288, "mode 0: K <= 288 (the weight block lives in LDS)");
-        SGN_REQUIRE(k.A.vec && g.a.ncols % 8 == 0 && g.a.ones_col < 0 && (g.a.csplit >= g.a.ncols || g.a.csplit % 8 == 0),
-                    "mode 0: operand a needs 16-B aligned rows (ld % 4 == 0), ncols % 8 == 0, no ones column");
+        SGN_REQUIRE(k.A.vec && g.a.ncols % 8 == 0 && g.a.ones_col < 0 && (g.a.csplit >= g.a.ncols || g.a.csplit % 16 == 0),
+                    "mode 0: operand a needs 16-B aligned rows (ld % 4 == 0), ncols % 8 == 0, a column split at a multiple "
+                    "of 16, no ones column");
         // column block: 128 wide unless 96 covers N with less padding; one workgroup per CU
         const bool w96 = ((g.N + 95) / 96) * 96 < ((g.N + 127) / 128) * 128;
         const int BN = w96 ? 96 : 128;

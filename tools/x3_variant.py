@@ -124,14 +124,11 @@ __device__ __forceinline__ int cur_slot(int s) { return s; }''')
         ++tit;
         tst(tdo, w, tit, 0);
         const int base = tile * WGS;''')
-        s = rep(s, "            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>>(",
-                "            tst(tdo, w, tit, 1);\n            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>>(")
-        s = rep(s, "        run_layer_ns<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {",
-                "        tst(tdo, w, tit, 2);\n        run_layer_ns<Net, 1>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {")
-        s = rep(s, "        run_layer_ns<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {",
-                "        tst(tdo, w, tit, 3);\n        run_layer_ns<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {")
-        s = rep(s, "            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(",
-                "            tst(tdo, w, tit, 4);\n            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(")
+        for a, b in (("            run_layer_ns<Net, 0, false, std::conditional_t<SAVE, VmZero, VmL0<NS>>, 0, 0, !SAVE>(", 1),
+                     ("        run_layer_ns<Net, 1, false, VmZero, 0, 0, !SAVE>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {", 2),
+                     ("        run_layer_ns<Net, L2, false, VmZero, 0, 0, !SAVE>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {", 3),
+                     ("            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0, !SAVE>(", 4)):
+            s = rep(s, a, " " * (len(a) - len(a.lstrip())) + f"tst(tdo, w, tit, {b});\n" + a)
         s = rep(s, "            run_layer_ns<Net, L3, true, VmZero, 1, 8>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {",
                 "            tst(tdo, w, tit, 5);\n            run_layer_ns<Net, L3, true, VmZero, 1, 8>(wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {")
         s = rep(s, "        // everything prefetched has landed (the chunk boundaries waited vmcnt(0)): hide the loads",
@@ -227,6 +224,58 @@ __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int
                 "        run_layer_ns<Net, 1, false, VmZero, 0, 0, !SAVE>(wb, ldsi, slot, w, lane, lz, accB, [&](auto k) {")
         s = rep(s, "        run_layer_ns<Net, L2>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {",
                 "        run_layer_ns<Net, L2, false, VmZero, 0, 0, !SAVE>(wb, ldsi, slot, w, lane, lz, acc2, [&](auto k) {")
+    elif p == "v_mix":
+        # LeakyReLU on the raw accumulator (asm max into the tied 0.01 a) and the 2^-s scale folded into
+        # the compiler's v_fma_mix{lo,hi}_f16 hi / lo conversion: 4 VALU per value instead of 5, same bits
+        s = rep(s, '''__device__ __forceinline__ X3B lrelu_split8(const float (&a)[8], float inv) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = lrelu_x3(a[j] * inv);
+    return split8(v);
+}''', '''__device__ __forceinline__ X3B lrelu_split8(const float (&a)[8], float inv) {
+    float l[8];
+    _Float16 h[8], o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) l[j] = lrelu_x3(a[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = (_Float16)__builtin_fmaf(l[j], inv, 0.f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (_Float16)__builtin_fmaf(l[j], inv, -(float)h[j]);
+    return X3B{h8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]}, h8{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]}};
+}''')
+    elif p == "v_epic":
+        # the epilogue's per-lane constants (block3.2 bias and alpha weight of unit 16 T + r, T = 0..15) read
+        # into registers once per tile (8 ds_read_b128, one wait) instead of one LDS read + wait per step
+        s = rep(s, '''    float inv3;
+};''', '''    float inv3;
+};
+struct EpiC {
+    float b[16], wa[16];
+};''')
+        s = rep(s, '''    auto epi_step = [&](Epi16 &e, const char *ldsi, const f32x4 (&ac)[16], auto tc) {
+        constexpr int T = decltype(tc)::value;
+        const float wau = ((const float *)(ldsi + YT16_OFF))[320 + r * 20 + T];  // 2^-s3 alpha weight''',
+                '''    EpiC ec;
+    auto epi_consts = [&](const char *ldsi) {
+        const f32x4 *yb = (const f32x4 *)(ldsi + YT16_OFF + r * 80), *yw = (const f32x4 *)(ldsi + YT16_OFF + 1280 + r * 80);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f32x4 u = yb[j], v = yw[j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ec.b[4 * j + i] = u[i];
+                ec.wa[4 * j + i] = v[i];
+            }
+        }
+    };
+    auto epi_step = [&](Epi16 &e, const char *ldsi, const f32x4 (&ac)[16], auto tc) {
+        constexpr int T = decltype(tc)::value;
+        const float wau = ec.wa[T];  // 2^-s3 alpha weight''')
+        s = rep(s, '''            const float hv = lrelu_x3(__builtin_fmaf(ac[T][i], e.inv3, ((const float *)(ldsi + YT16_OFF))[r * 20 + T]));''',
+                '''            const float hv = lrelu_x3(__builtin_fmaf(ac[T][i], e.inv3, ec.b[T]));''')
+        s = rep(s, '''            for (int q = 0; q < NS; ++q) epi_begin(e[q], ldsi, rw[q].wgt, nA[q], nB[q], ce[q], eslot[q] < nslots);''',
+                '''            for (int q = 0; q < NS; ++q) epi_begin(e[q], ldsi, rw[q].wgt, nA[q], nB[q], ce[q], eslot[q] < nslots);
+            epi_consts(ldsi);''')
     elif p == "abl_dma":
         s = rep(s, '''    asm volatile("" : "+s"(soff));
     __builtin_amdgcn_raw_ptr_buffer_load_lds(''', '''    return;
