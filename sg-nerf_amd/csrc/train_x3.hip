@@ -340,6 +340,174 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
         }
 }
 
+// ---- split-K weight gradients of the row layers (M = 256), LDS-DMA staged ------------------------
+// part[split][m][n] = sum over the split's rows r of A(m, r) B(n, r): A = a delta [rows][256] (no column
+// split, ones column or activation), B = the layer input ([rows][<= ld], column split, ones column and
+// LeakyReLU as k_x3tn).  The raw fp32 rows of A (all 256 columns) and of B's 96-column block stream into a
+// 3-stage LDS ring by LDS-DMA two stages ahead (rows past the split's end land as zeros through the
+// buffer range check), so no register staging limits how far the loads run ahead.  Every wave reads its
+// MFMA fragments straight from the raw stage (8 rows of one column per lane: two rows per ds_read2st64 /
+// ds_read2), splits them into (hi, lo) in registers (the compiler's v_fma_mix) and runs 36 MFMAs per
+// 32-row stage: waves own 64 rows of M, all 96 columns of the block.
+constexpr int DW_ROWS = 32, DW_BN = 96, DW_NST = 3;
+constexpr int DW_ABYTES = DW_ROWS * 256 * 4;  // 32 KiB
+constexpr int DW_STAGE = DW_ABYTES + DW_ROWS * DW_BN * 4;  // + 12 KiB
+
+// (t * scale) -> (hi, lo) fp16 halves (scale a power of two): v_fma_mix{lo,hi}_f16 the compiler forms itself
+__device__ __forceinline__ X3Pair split8_mix(const float (&t)[8], float scale) {
+    _Float16 h[8], l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = (_Float16)__builtin_fmaf(t[j], scale, 0.f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) l[j] = (_Float16)__builtin_fmaf(t[j], scale, -(float)h[j]);
+    return X3Pair{h8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]}, h8{l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]}};
+}
+
+// 16 B per lane at byte voff (per lane) + soff (uniform) of buffer r into LDS ldsdst + 16 lane
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *ldsdst, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)ldsdst, 16, voff, soff, 0, 0);
+}
+
+__global__ __launch_bounds__(TPB, 1) void k_x3dw(GemmK g) {
+    __shared__ __attribute__((aligned(16))) char lds[DW_NST * DW_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, L = lane & 31, hk = lane >> 5;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int sa = op_shift(g.A), sb = op_shift(g.B);
+    const float fa = ldexpf(1.f, sa), fb = ldexpf(1.f, sb), osc = ldexpf(1.f, -(sa + sb));
+    const int nb_n = (g.N + DW_BN - 1) / DW_BN;
+    int blk, split;
+    tn_block(nb_n, g.splits, blk, split);
+    const int n0 = blk * DW_BN;
+    const int rows = min(g.d_rows ? *g.d_rows : 0x7fffffff, g.K);
+    const int per = ((rows + g.splits - 1) / g.splits + 31) / 32 * 32;
+    const int r0 = split * per, r1 = min(rows, r0 + per);
+    const int nst = r1 > r0 ? (r1 - r0 + DW_ROWS - 1) / DW_ROWS : 0;
+    const OpRs ra = op_rsrc(g.A, r1), rb = op_rsrc(g.B, r1);
+    // B's DMA: chunk ci = 64 j + lane (j = w, w + 4, w + 8) of the dense [32][96] stage, 16 B each: stage row
+    // ci / 24, columns n0 + 4 (ci % 24) .. + 3 from p (columns < csplit) or p2; columns past ncols load 0
+    // per-lane byte offsets relative to the stage's first row (the stage adds a uniform soffset)
+    const uint32_t ald = (uint32_t)(g.A.ld * 4), bld1 = (uint32_t)(g.B.ld * 4),
+                   bld2 = (uint32_t)((g.B.p2 ? g.B.ld2 : g.B.ld) * 4);
+    uint32_t bv1[3], bv2[3];
+    bool bs1[3];
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+        const int ci = 64 * (w + 4 * jj) + lane, rr = ci / 24, c = n0 + 4 * (ci % 24);
+        bs1[jj] = c < g.B.csplit;
+        const bool ok = c < g.B.ncols;
+        bv1[jj] = ok && bs1[jj] ? (uint32_t)rr * bld1 + (uint32_t)(c * 4) : OOB;
+        bv2[jj] = ok && !bs1[jj] ? (uint32_t)rr * bld2 + (uint32_t)((c - g.B.csplit) * 4) : OOB;
+    }
+    const bool bmixed = __ballot(!(bs1[0] && bs1[1] && bs1[2])) != 0;   // wave-uniform: a p2 chunk in this wave
+    const uint32_t av = (uint32_t)(8 * w) * ald + lane * 16;
+    auto issue = [&](int st) {   // the DMA of stage st (rows r0 + 32 st ..) into ring slot st % 3
+        char *slot = lds + (st % DW_NST) * DW_STAGE;
+        const uint32_t rs = (uint32_t)(r0 + DW_ROWS * st);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)   // A: 8 rows per wave, one 1-KiB row per instruction
+            dma16(ra.r1, slot + (8 * w + e) * 1024, av, (rs + e) * ald);
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+            char *dst = slot + DW_ABYTES + (w + 4 * jj) * 1024;
+            if (!bmixed) {
+                dma16(rb.r1, dst, bv1[jj], rs * bld1);
+            } else {   // p and p2 lanes in separate exec-masked instructions
+                if (bs1[jj]) dma16(rb.r1, dst, bv1[jj], rs * bld1);
+                else dma16(rb.r2, dst, bv2[jj], rs * bld2);
+            }
+        }
+    };
+    f32x16 acc[2][3];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) acc[a][b] = f32x16{};
+    // B's per-lane column facts (the fragments' column n0 + 32 b + L): x -> max(x, x m) is LeakyReLU (m = 0.01)
+    // or the identity (m = 1) without a branch (columns past ncols arrived as zeros); the ones column is
+    // patched in its wave only
+    float bm[3];
+    bool bone[3];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        const int c = n0 + 32 * b + L;
+        bone[b] = c == g.B.ones_col;
+        bm[b] = g.B.act && c < g.B.csplit ? 0.01f : 1.f;
+    }
+    const bool bspec = __ballot(bone[0] || bone[1] || bone[2]) != 0;   // wave-uniform
+    if (nst > 0) issue(0);
+    if (nst > 1) issue(1);
+    for (int st = 0; st < nst; ++st) {
+        // stage st's DMA landed (this wave's; stage st + 1's, issued after, may stay in flight), every wave's
+        // too after the barrier, and every wave is done with slot (st - 1) % 3, which stage st + 2 reuses
+        const bool more = st + 1 < nst;
+        if (more) {
+            if (bmixed) __builtin_amdgcn_s_waitcnt((14 & 15) | (7 << 4) | (15 << 8));
+            else __builtin_amdgcn_s_waitcnt((11 & 15) | (7 << 4) | (15 << 8));
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        if (st + 2 < nst) issue(st + 2);
+        const char *slot = lds + (st % DW_NST) * DW_STAGE;
+        const int rs = r0 + DW_ROWS * st;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int rr = 16 * ks + 8 * hk;   // this lane's 8 stage rows rr .. rr + 7
+            X3Pair af[2], bf[3];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const float *src = (const float *)(slot + rr * 1024) + 64 * w + 32 * a + L;
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = src[256 * e];
+                af[a] = split8_mix(v, fa);
+            }
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                const float *src = (const float *)(slot + DW_ABYTES + rr * (DW_BN * 4)) + 32 * b + L;
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = src[DW_BN * e];
+                if (g.B.act) {   // kernel-uniform
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {   // max(x, m x) as one v_max (no canonicalising max of the LDS value)
+                        float t = v[e] * bm[b];
+                        asm("v_max_f32 %0, %1, %0" : "+v"(t) : "v"(v[e]));
+                        v[e] = t;
+                    }
+                }
+                if (bspec) {   // the ones column: 1 on the split's rows
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = bone[b] && rs + rr + e < r1 ? 1.f : v[e];
+                }
+                bf[b] = split8_mix(v, fb);
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    acc[a][b] = mfma32(af[a].lo, bf[b].hi, acc[a][b]);
+                    acc[a][b] = mfma32(af[a].hi, bf[b].lo, acc[a][b]);
+                    acc[a][b] = mfma32(af[a].hi, bf[b].hi, acc[a][b]);
+                }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const __amdgpu_buffer_rsrc_t pr = rows_rsrc(g.part + (int64_t)split * g.M * g.N, g.N, g.M);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const int n = n0 + b * 32 + L;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = 64 * w + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * hk;
+                const uint32_t off = n < g.N ? (uint32_t)((m * g.N + n) * 4) : OOB;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[a][b][r] * osc), pr, off, 0, 0);
+            }
+        }
+}
+
 // ---- rows mode, weights resident ----------------------------------------------------------------
 // Y[r][n] = sum_k A(r, k) B(n, k) for the 32 WN columns of block blockIdx.x: the workgroup converts
 // that block of B (KS k-steps of 16 x WN tiles of 32, hi / lo fp16 fragments, 2 KiB per (k-step,
@@ -1120,6 +1288,9 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
             SGN_REQUIRE(BM == 128 && (BN == 160 || BN == 96), "products 1: the colour layers' shapes (M <= 128, N > 32)");
             if (BN == 160) hipLaunchKernelGGL((k_x3tn<1, 5, true>), grid, dim3(TPB), 0, st, k);
             else hipLaunchKernelGGL((k_x3tn<1, 3, true>), grid, dim3(TPB), 0, st, k);
+        } else if (BM == 256 && BN == 96 && g.M == 256 && !g.a.p2 && g.a.ones_col < 0 && !g.a.act && g.a.ncols >= 256 &&
+                   g.a.ld >= 256) {
+            hipLaunchKernelGGL(k_x3dw, grid, dim3(TPB), 0, st, k);   // the row layers' weight gradients
         } else if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3tn<2, 3>), grid, dim3(TPB), 0, st, k);
         else if (BM == 256) hipLaunchKernelGGL((k_x3tn<2, 1>), grid, dim3(TPB), 0, st, k);
         else if (BN == 160) hipLaunchKernelGGL((k_x3tn<1, 5>), grid, dim3(TPB), 0, st, k);
