@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 12
+#define SGN_ABI_VERSION 13
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -506,8 +506,12 @@ typedef struct {
     int32_t splits;
     int32_t products;   /* 3 (or 0): hi/lo products, fp32 accuracy; 1: the hi halves only (fp16 operands,
                            the f16 training step's colour MLP; colour-layer shapes only) */
+    void *bpack;        /* ABI 13, mode 0: NULL, or a 16-B aligned workspace of sgn_x3_gemm_bpack_bytes(g)
+                           bytes: the weight blocks are split there once per call (one extra launch) and
+                           every workgroup copies its block into LDS by DMA instead of converting it */
 } sgn_x3_gemm_args;
 int sgn_x3_gemm(const sgn_x3_gemm_args *g, sgn_stream_t stream);
+size_t sgn_x3_gemm_bpack_bytes(const sgn_x3_gemm_args *g);   /* ABI 13; 0 unless mode 0 with K <= 288 */
 
 /* Deterministic work list and compact row offsets after sgn_query: for s < d_counters[0],
  * d_row_off[s] = sum of samp_nnb over samples < s; d_work = the samples with samp_nnb > 0 in

@@ -12,7 +12,7 @@ import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds 
 
 # SGN_HIP_LIB: another build of the same ABI (same-box A/B of kernel variants, tools/ab_lib.sh)
 LIB_PATH = os.environ.get("SGN_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -86,7 +86,7 @@ class X3GemmArgs(ctypes.Structure):
     _fields_ = [("a", X3Operand), ("b", X3Operand), ("mode", c_i32), ("M", c_i32), ("N", c_i32), ("K", c_i32),
                 ("d_rows", c_vp), ("bias", c_vp), ("act", c_i32), ("mask", c_vp), ("ldm", c_i64), ("out", c_vp),
                 ("ldo", c_i64), ("out_cols", c_i32), ("out2", c_vp), ("ldo2", c_i64), ("amax_out", c_vp),
-                ("amax_out2", c_vp), ("part", c_vp), ("splits", c_i32), ("products", c_i32)]
+                ("amax_out2", c_vp), ("part", c_vp), ("splits", c_i32), ("products", c_i32), ("bpack", c_vp)]
 
 
 class PartialSegment(ctypes.Structure):
@@ -176,6 +176,7 @@ SIGNATURES = {
                                                c_vp, c_vp, c_vp, c_sz, c_vp]),
     "sgn_train_row_gather": (c_i32, [ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "sgn_x3_gemm": (c_i32, [ctypes.POINTER(X3GemmArgs), c_vp]),
+    "sgn_x3_gemm_bpack_bytes": (c_sz, [ctypes.POINTER(X3GemmArgs)]),
     "sgn_train_lists_workspace_bytes": (c_sz, [c_i64]),
     "sgn_train_lists": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_train_row_inputs": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp, c_vp,

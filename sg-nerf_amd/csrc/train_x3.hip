@@ -33,6 +33,7 @@
 // activations not at all (they are inside fp16 range, as the forward kernel requires).  Results are
 // deterministic: no float atomics except the per-point gradients (the reference's index_add).
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "agg_device.h"
@@ -71,6 +72,7 @@ struct GemmK {
     uint32_t *amax_out, *amax_out2;
     float *part;
     int32_t splits;   // split-K mode: row runs; rows mode: row-tile strides (the grid is splits x blocks, 1-D)
+    char *bpack;      // rows mode: the weight blocks pre-converted by k_x3bpack (or null: each workgroup converts)
 };
 
 // 1-D block id -> (output column block, split / row-tile start).  Blocks b and b + 8 run on one XCD
@@ -104,6 +106,12 @@ __device__ __forceinline__ int op_shift(const Opnd &o) {
 }
 
 __device__ __forceinline__ float lrelu_ref(float x) { return x > 0.f ? x : x * 0.01f; }
+// the same value as max(x, 0.01 x) in two instructions (one v_max: no canonicalising max of a loaded value)
+__device__ __forceinline__ float lrelu_max(float x) {
+    float t = x * 0.01f;
+    asm("v_max_f32 %0, %1, %0" : "+v"(t) : "v"(x));
+    return t;
+}
 
 // ---- split-K mode: C[m][n] = sum over rows r of A(m, r) B(n, r) ---------------------------------
 // Both operands are row-major [rows][cols] (kmajor).  A stage is 32 rows; thread t of an operand loads
@@ -533,7 +541,7 @@ struct ARow {
         v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
         if (act && s1) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = lrelu_ref(v[e]);
+            for (int e = 0; e < 8; ++e) v[e] = lrelu_max(v[e]);
         }
     }
 };
@@ -572,15 +580,25 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
         for (int s = 0; s < KS; ++s) ar.load(16 * s, hk, a[s]);
     }
     // weights: lane fragment f = (k-step s, tile t, lane) -> ((s WN + t) 2 + hi/lo) FRAG + lane 16
-    const OpRs rsB = op_rsrc(g.B, g.B.nrows);
-    for (int f = tid; f < KS * WN * 64; f += TPB) {
-        const int fl = f & 63, t = (f >> 6) % WN, s = f / (64 * WN);
-        float v[8];
-        load8(g.B, rsB, n0 + 32 * t + (fl & 31), 16 * s + 8 * (fl >> 5), g.B.nrows, v);
-        const X3Pair x = split8_scaled(v, fb);
-        char *d = lds + ((s * WN + t) * 2) * FRAG + fl * 16;
-        *(h8 *)d = x.hi;
-        if (!P1) *(h8 *)(d + FRAG) = x.lo;
+    if (g.bpack) {   // the block's image, converted once per launch by k_x3bpack: 1 KiB per wave and instruction
+        constexpr int BYTES = KS * WN * 2 * FRAG;
+        static_assert(BYTES % 4096 == 0, "whole 4-KiB DMA rounds");
+        const __amdgpu_buffer_rsrc_t rp =
+            __builtin_amdgcn_make_buffer_rsrc(g.bpack + (int64_t)nblk * BYTES, (short)0, BYTES, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < BYTES / 4096; ++j) dma16(rp, lds + (4 * j + w) * 1024, lane * 16 + w * 1024, j * 4096);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        const OpRs rsB = op_rsrc(g.B, g.B.nrows);
+        for (int f = tid; f < KS * WN * 64; f += TPB) {
+            const int fl = f & 63, t = (f >> 6) % WN, s = f / (64 * WN);
+            float v[8];
+            load8(g.B, rsB, n0 + 32 * t + (fl & 31), 16 * s + 8 * (fl >> 5), g.B.nrows, v);
+            const X3Pair x = split8_scaled(v, fb);
+            char *d = lds + ((s * WN + t) * 2) * FRAG + fl * 16;
+            *(h8 *)d = x.hi;
+            if (!P1) *(h8 *)(d + FRAG) = x.lo;
+        }
     }
     __syncthreads();
     float am1 = 0.f, am2 = 0.f;
@@ -592,6 +610,21 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
     for (; rt * RT_ROWS < rows; rt += gy) {
         const int m0 = rt * RT_ROWS + 32 * w;
         const ARow an = arow(g.A, rsA, (rt + gy) * RT_ROWS + 32 * w + L);
+        // the tile's mask values go out before its MFMAs (rows past the valid ones and columns past out_cols
+        // read 0: only out's columns are masked)
+        float mk[WN][16];
+        if (g.mask) {
+#pragma unroll
+            for (int t = 0; t < WN; ++t) {
+                const int n = n0 + 32 * t + L;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+                    const uint32_t off = n < g.out_cols ? (uint32_t)(((int64_t)row * g.ldm + n) * 4) : OOB;
+                    mk[t][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rmk, off, 0, 0));
+                }
+            }
+        }
         f32x16 acc[WN];
 #pragma unroll
         for (int t = 0; t < WN; ++t) acc[t] = f32x16{};
@@ -609,20 +642,6 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
                     acc[t] = mfma32(x.hi, bl, acc[t]);
                 }
                 acc[t] = mfma32(x.hi, bh, acc[t]);
-            }
-        }
-        // epilogue: every mask value of the tile is loaded before any is used (one wait, not 16 per tile)
-        float mk[WN][16];
-        if (g.mask) {   // (rows past the valid ones and columns past out_cols read 0: only out's columns are masked)
-#pragma unroll
-            for (int t = 0; t < WN; ++t) {
-                const int n = n0 + 32 * t + L;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                    const uint32_t off = n < g.out_cols ? (uint32_t)(((int64_t)row * g.ldm + n) * 4) : OOB;
-                    mk[t][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rmk, off, 0, 0));
-                }
             }
         }
         auto epilogue = [&](auto o2c) {  // o2c: the launch writes out2 (kernel-uniform, one branch per tile)
@@ -664,6 +683,26 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
         if (g.amax_out) atomicMax(g.amax_out, __builtin_bit_cast(uint32_t, am1));
         if (g.amax_out2) atomicMax(g.amax_out2, __builtin_bit_cast(uint32_t, am2));
     }
+}
+
+// The weight blocks of a rows-mode launch in the LDS image k_x3rows stages: block b at b KS WN 2 FRAG
+// bytes, one thread per lane fragment (the same load8 / split as the in-workgroup conversion).
+template <int KS, int WN, bool P1>
+__global__ __launch_bounds__(TPB) void k_x3bpack(GemmK g) {
+    constexpr int PER = KS * WN * 64;
+    const int f = blockIdx.x * TPB + threadIdx.x;
+    const int nb = (g.N + 32 * WN - 1) / (32 * WN);
+    if (f >= nb * PER) return;
+    const int b = f / PER, fr = f % PER;
+    const int fl = fr & 63, t = (fr >> 6) % WN, s = fr / (64 * WN);
+    const float fb = ldexpf(1.f, op_shift(g.B));
+    const OpRs rsB = op_rsrc(g.B, g.B.nrows);
+    float v[8];
+    load8(g.B, rsB, b * 32 * WN + 32 * t + (fl & 31), 16 * s + 8 * (fl >> 5), g.B.nrows, v);
+    const X3Pair x = split8_scaled(v, fb);
+    char *d = g.bpack + (int64_t)b * (KS * WN * 2 * FRAG) + ((s * WN + t) * 2) * FRAG + fl * 16;
+    *(h8 *)d = x.hi;
+    if (!P1) *(h8 *)(d + FRAG) = x.lo;
 }
 
 // ---- deterministic work list and compact row offsets ---------------------------------------
@@ -1198,7 +1237,26 @@ __global__ __launch_bounds__(TPB) void k_reduce_partials(RedArgs r) {
 }  // namespace
 }  // namespace sgn
 
+namespace {
+// rows mode: column block 128 wide unless 96 covers N with less padding (one workgroup per CU); k-steps
+// of 16 as instantiated (8, 16 or 18)
+void rows_shape(int N, int K, bool &w96, int &ks, int &nb) {
+    w96 = ((N + 95) / 96) * 96 < ((N + 127) / 128) * 128;
+    nb = (N + (w96 ? 96 : 128) - 1) / (w96 ? 96 : 128);
+    const int k16 = (K + 15) / 16;
+    ks = k16 <= 8 ? 8 : k16 <= 16 ? 16 : 18;
+}
+}  // namespace
+
 extern "C" {
+
+size_t sgn_x3_gemm_bpack_bytes(const sgn_x3_gemm_args *g) {
+    if (!g || g->mode != 0 || g->N <= 0 || g->K < 0 || g->K > 288) return 0;
+    bool w96;
+    int ks, nb;
+    rows_shape(g->N, g->K, w96, ks, nb);
+    return (size_t)nb * ks * (w96 ? 3 : 4) * 2 * sgn::tx::FRAG;
+}
 
 int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
     using namespace sgn;
@@ -1252,29 +1310,46 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
         SGN_REQUIRE(k.A.vec && g.a.ncols % 8 == 0 && g.a.ones_col < 0 && (g.a.csplit >= g.a.ncols || g.a.csplit % 16 == 0),
                     "mode 0: operand a needs 16-B aligned rows (ld % 4 == 0), ncols % 8 == 0, a column split at a multiple "
                     "of 16, no ones column");
-        // column block: 128 wide unless 96 covers N with less padding; one workgroup per CU
-        const bool w96 = ((g.N + 95) / 96) * 96 < ((g.N + 127) / 128) * 128;
-        const int BN = w96 ? 96 : 128;
-        const int nb = (g.N + BN - 1) / BN;
+        bool w96;
+        int ks, nb;
+        rows_shape(g.N, g.K, w96, ks, nb);
         const int tiles = (g.M + RT_ROWS - 1) / RT_ROWS;
         int gy = 256 / nb;
         gy = gy < 1 ? 1 : gy > tiles ? tiles : gy;
-        const int ks = (g.K + 15) / 16;
         k.splits = gy;
         const dim3 grid(nb * gy);
+        if (p1) SGN_REQUIRE(!w96 && ks != 16, "products 1: the colour layers' shapes (K <= 128 or 272..288, N > 96)");
+        if (g.bpack) {
+            SGN_REQUIRE(((uintptr_t)g.bpack & 15) == 0, "bpack: 16-B aligned");
+            k.bpack = (char *)g.bpack;
+        }
+        // (KS, WN, P1): the weight conversion (with a workspace) then the row tiles
+        auto launch = [&](auto ks_c, auto wn_c, auto p1_c) {
+            constexpr int KS = decltype(ks_c)::value, WN = decltype(wn_c)::value;
+            constexpr bool P1 = decltype(p1_c)::value;
+            if (k.bpack) {
+                const int nf = nb * KS * WN * 64;
+                hipLaunchKernelGGL((k_x3bpack<KS, WN, P1>), dim3((nf + TPB - 1) / TPB), dim3(TPB), 0, st, k);
+            }
+            hipLaunchKernelGGL((k_x3rows<KS, WN, P1>), grid, dim3(TPB), 0, st, k);
+        };
+        using I8 = std::integral_constant<int, 8>;
+        using I16 = std::integral_constant<int, 16>;
+        using I18 = std::integral_constant<int, 18>;
+        using W3 = std::integral_constant<int, 3>;
+        using W4 = std::integral_constant<int, 4>;
         if (p1) {
-            SGN_REQUIRE(!w96 && ks != 16 && ks <= 18, "products 1: the colour layers' shapes (K <= 128 or 272..288, N > 96)");
-            if (ks <= 8) hipLaunchKernelGGL((k_x3rows<8, 4, true>), grid, dim3(TPB), 0, st, k);
-            else hipLaunchKernelGGL((k_x3rows<18, 4, true>), grid, dim3(TPB), 0, st, k);
+            if (ks <= 8) launch(I8{}, W4{}, std::true_type{});
+            else launch(I18{}, W4{}, std::true_type{});
         } else if (ks <= 8) {
-            if (w96) hipLaunchKernelGGL((k_x3rows<8, 3>), grid, dim3(TPB), 0, st, k);
-            else hipLaunchKernelGGL((k_x3rows<8, 4>), grid, dim3(TPB), 0, st, k);
+            if (w96) launch(I8{}, W3{}, std::false_type{});
+            else launch(I8{}, W4{}, std::false_type{});
         } else if (ks <= 16) {
-            if (w96) hipLaunchKernelGGL((k_x3rows<16, 3>), grid, dim3(TPB), 0, st, k);
-            else hipLaunchKernelGGL((k_x3rows<16, 4>), grid, dim3(TPB), 0, st, k);
+            if (w96) launch(I16{}, W3{}, std::false_type{});
+            else launch(I16{}, W4{}, std::false_type{});
         } else {
-            if (w96) hipLaunchKernelGGL((k_x3rows<18, 3>), grid, dim3(TPB), 0, st, k);
-            else hipLaunchKernelGGL((k_x3rows<18, 4>), grid, dim3(TPB), 0, st, k);
+            if (w96) launch(I18{}, W3{}, std::false_type{});
+            else launch(I18{}, W4{}, std::false_type{});
         }
     } else {
         // M block 256 (or 128 for M <= 128); N block 96, 160 (M <= 128: the colour layers' 129

@@ -72,6 +72,19 @@ def _splitk_gemm(a, b, M, N, K, rows, part, splits):
     return g
 
 
+def _attach_bpack(gemms, device):
+    """One workspace for the rows-mode launches' weight images (sgn_x3_gemm's bpack: the weight blocks are
+    split once per call by a small launch, then DMA'd into every workgroup's LDS).  The launches run in
+    stream order, so they share it.  Returns the buffer (keep it alive with the arguments)."""
+    L = _lib.lib()
+    rows = [g for g in gemms if g.mode == 0]
+    n = max([int(L.sgn_x3_gemm_bpack_bytes(ctypes.byref(g))) for g in rows] + [16])
+    buf = torch.empty(n, dtype=torch.uint8, device=device)
+    for g in rows:
+        g.bpack = buf.data_ptr()
+    return buf
+
+
 class F32Step:
     """Device buffers and pre-built launch arguments of the fp32 step for one batch capacity
     (R rays x SR samples x K neighbours), bound to one trainer's parameters and one query
@@ -264,6 +277,8 @@ class F32Step:
         self.w6, self.b6 = W("color_branch.6")[0], Bv("color_branch.6")
         self.wa, self.ba = W("alpha_branch.0")[0], Bv("alpha_branch.0")
         self.grad_key = (flat.data_ptr(), g.data_ptr())
+        self.bpack = _attach_bpack([gs for _, gs in self.g_colour_fwd + self.g_colour_bwd + self.g_row_bwd] +
+                                   [self.g_z4] + self.g_row_dw, flat.device)
 
     # -- one step ------------------------------------------------------------------------------
     def run(self, pt, proj, blob, campos, rot, gt, lp):
@@ -431,6 +446,7 @@ class ColourStep:
         self.segs = (_lib.PartialSegment * len(segs))(*segs)
         self.n_seg = len(segs)
         self.w6, self.b6 = W("color_branch.6")[0], Bv("color_branch.6")
+        self.bpack = _attach_bpack(self.g_fwd + self.g_bwd, flat.device)
 
     def run(self, campos, rot, gt, lp):
         """Colour forward into feat[.].yzw, the losses, the colour backward: returns the loss vector

@@ -21,6 +21,29 @@ def _gemm(g):
     _lib.check(_lib.lib().sgn_x3_gemm(ctypes.byref(g), _lib.stream_handle()), "sgn_x3_gemm")
 
 
+def _gemm_both(g, outs, amax=None):
+    """sgn_x3_gemm in rows mode with the in-workgroup weight conversion, then with the weight images
+    (bpack, ABI 13) into re-filled outputs: bit-identical results (the same split of the same values)."""
+    _gemm(g)
+    first = [o.clone() for o in outs]
+    am = amax.clone() if amax is not None else None
+    nb = int(_lib.lib().sgn_x3_gemm_bpack_bytes(ctypes.byref(g)))
+    assert nb > 0
+    ws = torch.full((nb // 4 + 4,), float("nan"), device=DEV)
+    g2 = type(g).from_buffer_copy(g)
+    g2.bpack = ws.data_ptr()
+    for o in outs:
+        o.fill_(-5.0)
+    if amax is not None:
+        amax.zero_()
+    _gemm(g2)
+    torch.cuda.synchronize()
+    for a, b in zip(first, outs):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    if amax is not None:
+        assert torch.equal(am, amax)
+
+
 def _rel(x, ref):
     return float((x.double() - ref).abs().max() / ref.abs().max().clamp(min=1e-30))
 
@@ -46,8 +69,9 @@ def test_x3_gemm_rows_mode_matches_float64(scale):
     amax = torch.zeros(2, dtype=torch.int32, device=DEV)
     a = _operand(dy.data_ptr(), K, K, 0, amax=amax_in.data_ptr())
     b = _operand(W.data_ptr(), N, N, 1, shift=shift.data_ptr())
-    _gemm(_rows_gemm(a, b, rows_cap, N, K, nrows.data_ptr(), out.data_ptr(), 256, mask=mask.data_ptr(), ldm=256,
-                     out_cols=256, out2=out2.data_ptr(), ldo2=8, amax_out=amax.data_ptr(), amax_out2=amax[1:].data_ptr()))
+    _gemm_both(_rows_gemm(a, b, rows_cap, N, K, nrows.data_ptr(), out.data_ptr(), 256, mask=mask.data_ptr(), ldm=256,
+                          out_cols=256, out2=out2.data_ptr(), ldo2=8, amax_out=amax.data_ptr(),
+                          amax_out2=amax[1:].data_ptr()), [out, out2], amax)
     torch.cuda.synchronize()
     ref = dy[:rows].double() @ W.double()
     ref1 = torch.where(mask[:rows] > 0, ref[:, :256], ref[:, :256] * 0.01)
@@ -62,9 +86,9 @@ def test_x3_gemm_rows_mode_matches_float64(scale):
     x2 = torch.randn(rows_cap, 32, generator=g).to(DEV)
     sf = torch.tensor([14 - int(torch.frexp(Wf.abs().max().cpu())[1])], dtype=torch.int32, device=DEV)
     y = torch.full((rows_cap, 128), -5.0, device=DEV)
-    _gemm(_rows_gemm(_operand(x1.data_ptr(), 256, 280, 0, p2=x2.data_ptr(), ld2=32, csplit=256, act=1),
-                     _operand(Wf.data_ptr(), 280, 280, 0, shift=sf.data_ptr()), rows_cap, 128, 280, nrows.data_ptr(),
-                     y.data_ptr(), 128, bias=bf.data_ptr(), act=1))
+    _gemm_both(_rows_gemm(_operand(x1.data_ptr(), 256, 280, 0, p2=x2.data_ptr(), ld2=32, csplit=256, act=1),
+                          _operand(Wf.data_ptr(), 280, 280, 0, shift=sf.data_ptr()), rows_cap, 128, 280, nrows.data_ptr(),
+                          y.data_ptr(), 128, bias=bf.data_ptr(), act=1), [y])
     torch.cuda.synchronize()
     xin = torch.cat([_lrelu(x1[:rows].double()), x2[:rows, :24].double()], 1)
     reff = _lrelu(xin @ Wf.double().t() + bf.double())

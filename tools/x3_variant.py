@@ -370,6 +370,32 @@ __global__ __launch_bounds__(TPB, OCC) void k_x3tn(GemmK g) {''')
         s = rep(s, '''        else if (BN == 96) hipLaunchKernelGGL((k_x3tn<1, 3>), grid, dim3(TPB), 0, st, k);''',
                 '''        else if (BN == 96 && g.M > 128) hipLaunchKernelGGL((k_x3tn<1, 3, false, 2>), grid, dim3(TPB), 0, st, k);
         else if (BN == 96) hipLaunchKernelGGL((k_x3tn<1, 3>), grid, dim3(TPB), 0, st, k);''')
+    elif p == "txa_noA":   # k_x3rows ablation: no A loads after the first tile (the split kept)
+        s = rep(s, '''            an.load(16 * s, hk, a[s]);  // the next tile's k-step s''', '''#pragma unroll
+            for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(a[s][e]));''')
+    elif p == "txa_nomask":   # k_x3rows ablation: no mask loads
+        s = rep(s, '''                    mk[t][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rmk, off, 0, 0));''',
+                '''                    mk[t][r] = off == 7u ? 0.f : 1.f;''')
+    elif p == "txa_nostore":   # k_x3rows ablation: no output stores (amax kept)
+        s = rep(s, '''                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v1), ro1,
+                                                          o1 ? (uint32_t)(((int64_t)row * g.ldo + n) * 4) : OOB, 0, 0);''', '')
+    elif p == "txa_nostage":   # k_x3rows ablation: no weight staging loads
+        s = rep(s, '''        load8(g.B, rsB, n0 + 32 * t + (fl & 31), 16 * s + 8 * (fl >> 5), g.B.nrows, v);''',
+                '''#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (float)(fl + e);''')
+    elif p == "txa_nomfma":   # k_x3rows ablation: no MFMAs (operands kept live)
+        s = rep(s, '''                    acc[t] = mfma32(x.lo, bh, acc[t]);
+                    acc[t] = mfma32(x.hi, bl, acc[t]);
+                }
+                acc[t] = mfma32(x.hi, bh, acc[t]);
+            }
+        }
+        // epilogue''', '''                    asm volatile("" :: "v"(x.lo), "v"(bl));
+                }
+                asm volatile("" :: "v"(x.hi), "v"(bh));
+            }
+        }
+        // epilogue''')
     else:
         return None
     return s
@@ -393,8 +419,8 @@ def main():
             src = patch(src, p)
     open(os.path.join(work, "mlp_x3.hip"), "w").write(src)
     open(os.path.join(work, "train_x3.hip"), "w").write(tsrc)
-    txp = [q for q in patches if q.startswith("tx_")]
-    xp = [q for q in patches if not q.startswith("tx_")]
+    txp = [q for q in patches if q.startswith("tx")]
+    xp = [q for q in patches if not q.startswith("tx")]
     targets = (["mlp_x3"] if xp else []) + (["train_x3"] if txp else [])
     out_dir = os.path.join(ROOT, "build", "variants")
     os.makedirs(out_dir, exist_ok=True)
@@ -404,7 +430,7 @@ def main():
     new_objs = []
     for t in targets:
         obj = os.path.join(work, t + ".o")
-        extra = ["-fno-slp-vectorize"] if t == "mlp_x3" else []
+        extra = ["-fno-slp-vectorize"]   # both objects' Makefile flags
         subprocess.check_call([hipcc, *[f for f in fl if f != "-fno-slp-vectorize"], *extra, "-save-temps=obj", "-c",
                                os.path.join(work, t + ".hip"), "-o", obj])
         new_objs.append(obj)
