@@ -351,15 +351,22 @@ __global__ __launch_bounds__(TPB, 1) void k_x3tn(GemmK g) {
 // ---- split-K weight gradients of the row layers (M = 256), LDS-DMA staged ------------------------
 // part[split][m][n] = sum over the split's rows r of A(m, r) B(n, r): A = a delta [rows][256] (no column
 // split, ones column or activation), B = the layer input ([rows][<= ld], column split, ones column and
-// LeakyReLU as k_x3tn).  The raw fp32 rows of A (all 256 columns) and of B's 96-column block stream into a
-// 3-stage LDS ring by LDS-DMA two stages ahead (rows past the split's end land as zeros through the
-// buffer range check), so no register staging limits how far the loads run ahead.  Every wave reads its
-// MFMA fragments straight from the raw stage (8 rows of one column per lane: two rows per ds_read2st64 /
-// ds_read2), splits them into (hi, lo) in registers (the compiler's v_fma_mix) and runs 36 MFMAs per
-// 32-row stage: waves own 64 rows of M, all 96 columns of the block.
+// LeakyReLU as k_x3tn).  The raw fp32 rows of A (all 256 columns) and of B's 96-column block stream into
+// two 3-slot LDS rings by LDS-DMA (rows past the split's end land as zeros through the buffer range
+// check), A two stages ahead of its MFMAs, B three: B's stage is converted one stage ahead, once per
+// workgroup (each wave a quarter: LeakyReLU, the ones column, the (hi, lo) split) into a fragment image
+// the 8 waves share, while A's fragments are read straight from the raw stage by the wave that owns
+// them (8 rows of one column per lane) and split in registers (the compiler's v_fma_mix).  18 MFMAs per
+// 32-row stage and wave: waves own 32 rows of M, all 96 columns of the block; two waves per SIMD hide
+// each other's LDS latencies.
 constexpr int DW_ROWS = 32, DW_BN = 96, DW_NST = 3;
-constexpr int DW_ABYTES = DW_ROWS * 256 * 4;  // 32 KiB
-constexpr int DW_STAGE = DW_ABYTES + DW_ROWS * DW_BN * 4;  // + 12 KiB
+constexpr int DW_ABYTES = DW_ROWS * 256 * 4;       // 32 KiB: a raw A stage
+constexpr int DW_BBYTES = DW_ROWS * DW_BN * 4;     // 12 KiB: a raw B stage
+constexpr int DW_FBYTES = 2 * 3 * 2 * FRAG;        // 12 KiB: a stage's B fragments ((k-step 3 + tile) 2 + hi/lo)
+constexpr int DW_LDS = DW_NST * (DW_ABYTES + DW_BBYTES) + 2 * DW_FBYTES;   // 156 KiB
+constexpr int DW_TPB = 512;   // 8 waves
+
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 
 // (t * scale) -> (hi, lo) fp16 halves (scale a power of two): v_fma_mix{lo,hi}_f16 the compiler forms itself
 __device__ __forceinline__ X3Pair split8_mix(const float (&t)[8], float scale) {
@@ -376,8 +383,20 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *ldsdst, ui
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)ldsdst, 16, voff, soff, 0, 0);
 }
 
-__global__ __launch_bounds__(TPB, 1) void k_x3dw(GemmK g) {
-    __shared__ __attribute__((aligned(16))) char lds[DW_NST * DW_STAGE];
+// this wave's DMAs but the last n issued have landed, its LDS writes are done, then the workgroup barrier
+// (after it every wave's have); the asm's memory clobber keeps the compiler's LDS accesses on their side
+__device__ __forceinline__ void dw_wait_barrier(int n) {
+    if (n == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (n == 7) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (n == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (n == 5) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (n == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__global__ __launch_bounds__(DW_TPB, 1) void k_x3dw(GemmK g) {
+    __shared__ __attribute__((aligned(16))) char lds[DW_LDS];
+    char *const la = lds, *const lb = lds + DW_NST * DW_ABYTES, *const lf = lb + DW_NST * DW_BBYTES;
     const int tid = threadIdx.x, lane = tid & 63, L = lane & 31, hk = lane >> 5;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int sa = op_shift(g.A), sb = op_shift(g.B);
@@ -391,139 +410,175 @@ __global__ __launch_bounds__(TPB, 1) void k_x3dw(GemmK g) {
     const int r0 = split * per, r1 = min(rows, r0 + per);
     const int nst = r1 > r0 ? (r1 - r0 + DW_ROWS - 1) / DW_ROWS : 0;
     const OpRs ra = op_rsrc(g.A, r1), rb = op_rsrc(g.B, r1);
-    // B's DMA: chunk ci = 64 j + lane (j = w, w + 4, w + 8) of the dense [32][96] stage, 16 B each: stage row
+    // B's DMA: chunk ci = 64 j + lane (j = w, w + 8 < 12) of the dense [32][96] stage, 16 B each: stage row
     // ci / 24, columns n0 + 4 (ci % 24) .. + 3 from p (columns < csplit) or p2; columns past ncols load 0
     // per-lane byte offsets relative to the stage's first row (the stage adds a uniform soffset)
     const uint32_t ald = (uint32_t)(g.A.ld * 4), bld1 = (uint32_t)(g.B.ld * 4),
                    bld2 = (uint32_t)((g.B.p2 ? g.B.ld2 : g.B.ld) * 4);
-    uint32_t bv1[3], bv2[3];
-    bool bs1[3];
+    uint32_t bv1[2], bv2[2];
+    bool bs1[2];
+    const bool two = w + 8 < 12;   // wave-uniform: a second chunk
 #pragma unroll
-    for (int jj = 0; jj < 3; ++jj) {
-        const int ci = 64 * (w + 4 * jj) + lane, rr = ci / 24, c = n0 + 4 * (ci % 24);
+    for (int jj = 0; jj < 2; ++jj) {
+        const int ci = 64 * (jj == 0 || two ? w + 8 * jj : w) + lane, rr = ci / 24, c = n0 + 4 * (ci % 24);
         bs1[jj] = c < g.B.csplit;
         const bool ok = c < g.B.ncols;
         bv1[jj] = ok && bs1[jj] ? (uint32_t)rr * bld1 + (uint32_t)(c * 4) : OOB;
         bv2[jj] = ok && !bs1[jj] ? (uint32_t)rr * bld2 + (uint32_t)((c - g.B.csplit) * 4) : OOB;
     }
-    const bool bmixed = __ballot(!(bs1[0] && bs1[1] && bs1[2])) != 0;   // wave-uniform: a p2 chunk in this wave
-    const uint32_t av = (uint32_t)(8 * w) * ald + lane * 16;
-    auto issue = [&](int st) {   // the DMA of stage st (rows r0 + 32 st ..) into ring slot st % 3
-        char *slot = lds + (st % DW_NST) * DW_STAGE;
+    const bool bmixed = __ballot(!(bs1[0] && bs1[1])) != 0;   // wave-uniform: a p2 chunk in this wave
+    // a mixed wave issues a chunk's p lanes and p2 lanes as two exec-masked instructions, each only when
+    // it has a lane (so the in-flight count below is exact)
+    bool any1[2], any2[2];
+    int nbdma = 0;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+        any1[jj] = __ballot(bs1[jj]) != 0;
+        any2[jj] = __ballot(!bs1[jj]) != 0;
+        if (jj == 0 || two) nbdma += bmixed ? (int)any1[jj] + (int)any2[jj] : 1;
+    }
+    const uint32_t av = (uint32_t)(4 * w) * ald + lane * 16;
+    auto issue_a = [&](int st) {   // A rows r0 + 32 st .. into A slot st % 3: 4 rows per wave, a 1-KiB row each
+        char *slot = la + (st % DW_NST) * DW_ABYTES;
         const uint32_t rs = (uint32_t)(r0 + DW_ROWS * st);
 #pragma unroll
-        for (int e = 0; e < 8; ++e)   // A: 8 rows per wave, one 1-KiB row per instruction
-            dma16(ra.r1, slot + (8 * w + e) * 1024, av, (rs + e) * ald);
+        for (int e = 0; e < 4; ++e) dma16(ra.r1, slot + (4 * w + e) * 1024, av, (rs + e) * ald);
+    };
+    auto issue_b = [&](int st) {   // B's block of those rows into B slot st % 3
+        char *slot = lb + (st % DW_NST) * DW_BBYTES;
+        const uint32_t rs = (uint32_t)(r0 + DW_ROWS * st);
 #pragma unroll
-        for (int jj = 0; jj < 3; ++jj) {
-            char *dst = slot + DW_ABYTES + (w + 4 * jj) * 1024;
+        for (int jj = 0; jj < 2; ++jj) {
+            if (jj == 1 && !two) break;
+            char *dst = slot + (w + 8 * jj) * 1024;
             if (!bmixed) {
                 dma16(rb.r1, dst, bv1[jj], rs * bld1);
             } else {   // p and p2 lanes in separate exec-masked instructions
-                if (bs1[jj]) dma16(rb.r1, dst, bv1[jj], rs * bld1);
-                else dma16(rb.r2, dst, bv2[jj], rs * bld2);
+                if (any1[jj] && bs1[jj]) dma16(rb.r1, dst, bv1[jj], rs * bld1);
+                if (any2[jj] && !bs1[jj]) dma16(rb.r2, dst, bv2[jj], rs * bld2);
             }
         }
     };
-    f32x16 acc[2][3];
+    // B's conversion: wave w takes half (w & 1) -- stage rows + 4 .. + 3 -- of the fragments kb = (w >> 1) + 4 j
+    // < 6 (k-step kb / 3, tile kb % 3), j < 2 (waves w and w + 4 share a SIMD: 3 halves per SIMD); lane (L,
+    // hk): column n0 + 32 (kb % 3) + L, rows 16 (kb / 3) + 8 hk + 4 half .. + 3.  x -> max(x, m x) is LeakyReLU (m = 0.01) or the identity (m = 1); columns past ncols
+    // arrived as zeros; the ones column is patched in its wave only.
+    const int half = w & 1;
+    float cm[2];
+    bool cone[2];
+    int crow[2], ccol[2], cimg[2];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) acc[a][b] = f32x16{};
-    // B's per-lane column facts (the fragments' column n0 + 32 b + L): x -> max(x, x m) is LeakyReLU (m = 0.01)
-    // or the identity (m = 1) without a branch (columns past ncols arrived as zeros); the ones column is
-    // patched in its wave only
-    float bm[3];
-    bool bone[3];
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
+    for (int j = 0; j < 2; ++j) {
+        const int kb = min((w >> 1) + 4 * j, 5), ks = kb / 3, b = kb % 3;
         const int c = n0 + 32 * b + L;
-        bone[b] = c == g.B.ones_col;
-        bm[b] = g.B.act && c < g.B.csplit ? 0.01f : 1.f;
+        cone[j] = c == g.B.ones_col;
+        cm[j] = g.B.act && c < g.B.csplit ? 0.01f : 1.f;
+        crow[j] = 16 * ks + 8 * hk + 4 * half;
+        ccol[j] = 32 * b + L;
+        cimg[j] = (kb * 2) * FRAG + lane * 16 + 8 * half;
     }
-    const bool bspec = __ballot(bone[0] || bone[1] || bone[2]) != 0;   // wave-uniform
-    if (nst > 0) issue(0);
-    if (nst > 1) issue(1);
-    for (int st = 0; st < nst; ++st) {
-        // stage st's DMA landed (this wave's; stage st + 1's, issued after, may stay in flight), every wave's
-        // too after the barrier, and every wave is done with slot (st - 1) % 3, which stage st + 2 reuses
-        const bool more = st + 1 < nst;
-        if (more) {
-            if (bmixed) __builtin_amdgcn_s_waitcnt((14 & 15) | (7 << 4) | (15 << 8));
-            else __builtin_amdgcn_s_waitcnt((11 & 15) | (7 << 4) | (15 << 8));
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-        if (st + 2 < nst) issue(st + 2);
-        const char *slot = lds + (st % DW_NST) * DW_STAGE;
+    const bool cspec = __ballot(cone[0] || (two && cone[1])) != 0;   // wave-uniform
+    auto convert = [&](int st) {   // raw B slot st % 3 -> fragment image st & 1
+        const float *src = (const float *)(lb + (st % DW_NST) * DW_BBYTES);
+        char *dst = lf + (st & 1) * DW_FBYTES;
         const int rs = r0 + DW_ROWS * st;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (j == 1 && !two) break;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = src[(crow[j] + e) * DW_BN + ccol[j]];
+            if (g.B.act) {   // kernel-uniform
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {   // max(x, m x) as one v_max (no canonicalising max of the LDS value)
+                    float t = v[e] * cm[j];
+                    asm("v_max_f32 %0, %1, %0" : "+v"(t) : "v"(v[e]));
+                    v[e] = t;
+                }
+            }
+            if (cspec) {   // the ones column: 1 on the split's rows
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = cone[j] && rs + crow[j] + e < r1 ? 1.f : v[e];
+            }
+            _Float16 h[4], l[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h[e] = (_Float16)__builtin_fmaf(v[e], fb, 0.f);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) l[e] = (_Float16)__builtin_fmaf(v[e], fb, -(float)h[e]);
+            *(h4 *)(dst + cimg[j]) = h4{h[0], h[1], h[2], h[3]};
+            *(h4 *)(dst + cimg[j] + FRAG) = h4{l[0], l[1], l[2], l[3]};
+        }
+    };
+    f32x16 acc[3];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) acc[b] = f32x16{};
+    // prologue: B(0) landed and converted; then A(0), B(1), A(1), B(2) in flight -- the loop's DMA groups
+    // are (A(st + 2), B(st + 3)) in that order, so at stage st the last group issued may stay in flight
+    if (nst > 0) {
+        issue_b(0);
+        dw_wait_barrier(0);
+        convert(0);
+        issue_a(0);
+        if (nst > 1) issue_b(1);
+        if (nst > 1) issue_a(1);
+        if (nst > 2) issue_b(2);
+    }
+    for (int st = 0; st < nst; ++st) {
+        // A(st) and B(st + 1) landed (this wave's; the group issued last may stay in flight), every wave's
+        // after the barrier, and every wave is done with stage st - 1 (its A slot, which A(st + 2) reuses,
+        // and its fragment image, which B(st + 1)'s conversion reuses) and has converted B(st)
+        dw_wait_barrier(st + 2 < nst ? 4 + nbdma : st + 1 < nst ? 4 : 0);
+        if (st + 2 < nst) issue_a(st + 2);
+        if (st + 3 < nst) issue_b(st + 3);
+        if (st + 1 < nst) convert(st + 1);
+        const char *slot = la + (st % DW_NST) * DW_ABYTES;
+        const char *fr = lf + (st & 1) * DW_FBYTES + lane * 16;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int rr = 16 * ks + 8 * hk;   // this lane's 8 stage rows rr .. rr + 7
-            X3Pair af[2], bf[3];
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-                const float *src = (const float *)(slot + rr * 1024) + 64 * w + 32 * a + L;
+            X3Pair af, bf[3];
+            {
+                const float *src = (const float *)(slot + rr * 1024) + 32 * w + L;
                 float v[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] = src[256 * e];
-                af[a] = split8_mix(v, fa);
+                af = split8_mix(v, fa);
             }
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
-                const float *src = (const float *)(slot + DW_ABYTES + rr * (DW_BN * 4)) + 32 * b + L;
-                float v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = src[DW_BN * e];
-                if (g.B.act) {   // kernel-uniform
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {   // max(x, m x) as one v_max (no canonicalising max of the LDS value)
-                        float t = v[e] * bm[b];
-                        asm("v_max_f32 %0, %1, %0" : "+v"(t) : "v"(v[e]));
-                        v[e] = t;
-                    }
-                }
-                if (bspec) {   // the ones column: 1 on the split's rows
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] = bone[b] && rs + rr + e < r1 ? 1.f : v[e];
-                }
-                bf[b] = split8_mix(v, fb);
+                bf[b].hi = *(const h8 *)(fr + ((ks * 3 + b) * 2) * FRAG);
+                bf[b].lo = *(const h8 *)(fr + ((ks * 3 + b) * 2 + 1) * FRAG);
             }
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    acc[a][b] = mfma32(af[a].lo, bf[b].hi, acc[a][b]);
-                    acc[a][b] = mfma32(af[a].hi, bf[b].lo, acc[a][b]);
-                    acc[a][b] = mfma32(af[a].hi, bf[b].hi, acc[a][b]);
-                }
+            for (int b = 0; b < 3; ++b) {
+                acc[b] = mfma32(af.lo, bf[b].hi, acc[b]);
+                acc[b] = mfma32(af.hi, bf[b].lo, acc[b]);
+                acc[b] = mfma32(af.hi, bf[b].hi, acc[b]);
+            }
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const __amdgpu_buffer_rsrc_t pr = rows_rsrc(g.part + (int64_t)split * g.M * g.N, g.N, g.M);
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 3; ++b) {
+        const int n = n0 + b * 32 + L;
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            const int n = n0 + b * 32 + L;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = 64 * w + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                const uint32_t off = n < g.N ? (uint32_t)((m * g.N + n) * 4) : OOB;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[a][b][r] * osc), pr, off, 0, 0);
-            }
+        for (int r = 0; r < 16; ++r) {
+            const int m = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * hk;
+            const uint32_t off = n < g.N ? (uint32_t)((m * g.N + n) * 4) : OOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[b][r] * osc), pr, off, 0, 0);
         }
+    }
 }
 
 // ---- rows mode, weights resident ----------------------------------------------------------------
-// Y[r][n] = sum_k A(r, k) B(n, k) for the 32 WN columns of block blockIdx.x: the workgroup converts
-// that block of B (KS k-steps of 16 x WN tiles of 32, hi / lo fp16 fragments, 2 KiB per (k-step,
-// tile)) into LDS once, then walks row tiles of 128 rows (one 32-row MFMA tile per wave) with the A
-// fragments loaded straight into registers: lane l holds row l & 31, k = 16 s + 8 (l >> 5) .. + 7 of
-// every k-step s, and the next tile's k-step s is loaded as soon as this tile's has been converted,
-// so a whole tile of MFMAs hides it.  One workgroup per CU (the weight block is up to 144 KiB).
-constexpr int RT_ROWS = 128;
+// Y[r][n] = sum_k A(r, k) B(n, k) for the 32 WN columns of block blockIdx.x: the workgroup's block of
+// B (KS k-steps of 16 x WN tiles of 32, hi / lo fp16 fragments, 2 KiB per (k-step, tile)) is DMA'd
+// into LDS once (pre-split by k_x3bpack) or converted there, then the workgroup walks row tiles of 256
+// rows (one 32-row MFMA tile per wave) with the A fragments loaded straight into registers: lane l holds
+// row l & 31, k = 16 s + 8 (l >> 5) .. + 7 of k-step s, RT_PD k-steps ahead of the MFMAs.  One
+// workgroup of 8 waves per CU (the weight block is up to 144 KiB): two waves per SIMD, one's epilogue
+// (mask loads, stores) under the other's MFMAs.
+constexpr int RT_W = 8, RT_TPB = 64 * RT_W, RT_ROWS = 32 * RT_W, RT_PD = 4;
 
 // the A operand of the rows mode: row-major, 16-B aligned rows, columns in whole octets, the column
 // split at a multiple of 16 (host-checked), read through buffers over the valid rows (rows past them
@@ -558,7 +613,7 @@ __device__ __forceinline__ ARow arow(const Opnd &o, const OpRs &rs, int row) {
 }
 
 template <int KS, int WN, bool P1 = false>
-__global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
+__global__ __launch_bounds__(RT_TPB, 1) void k_x3rows(GemmK g) {
     __shared__ __attribute__((aligned(16))) char lds[KS * WN * 2 * FRAG];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -571,26 +626,20 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
     const int gy = g.splits;
     const int n0 = nblk * (32 * WN);
     const int L = lane & 31, hk = lane >> 5;
-    // the first tile's A loads go out before the weight staging
     const OpRs rsA = op_rsrc(g.A, limA);
-    float a[KS][8];
-    {
-        const ARow ar = arow(g.A, rsA, rt * RT_ROWS + 32 * w + L);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) ar.load(16 * s, hk, a[s]);
-    }
     // weights: lane fragment f = (k-step s, tile t, lane) -> ((s WN + t) 2 + hi/lo) FRAG + lane 16
     if (g.bpack) {   // the block's image, converted once per launch by k_x3bpack: 1 KiB per wave and instruction
-        constexpr int BYTES = KS * WN * 2 * FRAG;
-        static_assert(BYTES % 4096 == 0, "whole 4-KiB DMA rounds");
+        constexpr int BYTES = KS * WN * 2 * FRAG, NCH = BYTES / 1024;
         const __amdgpu_buffer_rsrc_t rp =
             __builtin_amdgcn_make_buffer_rsrc(g.bpack + (int64_t)nblk * BYTES, (short)0, BYTES, 0x00020000);
 #pragma unroll
-        for (int j = 0; j < BYTES / 4096; ++j) dma16(rp, lds + (4 * j + w) * 1024, lane * 16 + w * 1024, j * 4096);
+        for (int j = 0; j < (NCH + RT_W - 1) / RT_W; ++j)
+            if (NCH % RT_W == 0 || RT_W * j + w < NCH)
+                dma16(rp, lds + (RT_W * j + w) * 1024, lane * 16 + w * 1024, j * (RT_W * 1024));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
         const OpRs rsB = op_rsrc(g.B, g.B.nrows);
-        for (int f = tid; f < KS * WN * 64; f += TPB) {
+        for (int f = tid; f < KS * WN * 64; f += RT_TPB) {
             const int fl = f & 63, t = (f >> 6) % WN, s = f / (64 * WN);
             float v[8];
             load8(g.B, rsB, n0 + 32 * t + (fl & 31), 16 * s + 8 * (fl >> 5), g.B.nrows, v);
@@ -609,9 +658,32 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
     const __amdgpu_buffer_rsrc_t rbs = rows_rsrc(g.bias ? g.bias : g.out, 1, g.bias ? g.N : 0);
     for (; rt * RT_ROWS < rows; rt += gy) {
         const int m0 = rt * RT_ROWS + 32 * w;
-        const ARow an = arow(g.A, rsA, (rt + gy) * RT_ROWS + 32 * w + L);
-        // the tile's mask values go out before its MFMAs (rows past the valid ones and columns past out_cols
-        // read 0: only out's columns are masked)
+        const ARow ar = arow(g.A, rsA, m0 + L);
+        // A: k-steps s .. s + RT_PD - 1 in flight while k-step s's MFMAs run (a ring of RT_PD octets)
+        float a[RT_PD][8];
+#pragma unroll
+        for (int s = 0; s < RT_PD; ++s) ar.load(16 * s, hk, a[s]);
+        f32x16 acc[WN];
+#pragma unroll
+        for (int t = 0; t < WN; ++t) acc[t] = f32x16{};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const X3Pair x = split8_mix(a[s % RT_PD], fa);   // compiler-formed: its hazard recognizer sees it
+            if (s + RT_PD < KS) ar.load(16 * (s + RT_PD), hk, a[s % RT_PD]);
+            const char *p = lds + (s * WN * 2) * FRAG + lane * 16;
+#pragma unroll
+            for (int t = 0; t < WN; ++t) {
+                const h8 bh = *(const h8 *)(p + (2 * t) * FRAG);
+                if (!P1) {
+                    const h8 bl = *(const h8 *)(p + (2 * t + 1) * FRAG);
+                    acc[t] = mfma32(x.lo, bh, acc[t]);
+                    acc[t] = mfma32(x.hi, bl, acc[t]);
+                }
+                acc[t] = mfma32(x.hi, bh, acc[t]);
+            }
+        }
+        // epilogue: every mask value of the tile is loaded before any is used (rows past the valid ones and
+        // columns past out_cols read 0: only out's columns are masked); the other wave of the SIMD hides it
         float mk[WN][16];
         if (g.mask) {
 #pragma unroll
@@ -623,25 +695,6 @@ __global__ __launch_bounds__(TPB, 1) void k_x3rows(GemmK g) {
                     const uint32_t off = n < g.out_cols ? (uint32_t)(((int64_t)row * g.ldm + n) * 4) : OOB;
                     mk[t][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rmk, off, 0, 0));
                 }
-            }
-        }
-        f32x16 acc[WN];
-#pragma unroll
-        for (int t = 0; t < WN; ++t) acc[t] = f32x16{};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const X3Pair x = split8_scaled(a[s], fa);
-            an.load(16 * s, hk, a[s]);  // the next tile's k-step s
-            const char *p = lds + (s * WN * 2) * FRAG + lane * 16;
-#pragma unroll
-            for (int t = 0; t < WN; ++t) {
-                const h8 bh = *(const h8 *)(p + (2 * t) * FRAG);
-                if (!P1) {
-                    const h8 bl = *(const h8 *)(p + (2 * t + 1) * FRAG);
-                    acc[t] = mfma32(x.lo, bh, acc[t]);
-                    acc[t] = mfma32(x.hi, bl, acc[t]);
-                }
-                acc[t] = mfma32(x.hi, bh, acc[t]);
             }
         }
         auto epilogue = [&](auto o2c) {  // o2c: the launch writes out2 (kernel-uniform, one branch per tile)
@@ -1331,7 +1384,7 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
                 const int nf = nb * KS * WN * 64;
                 hipLaunchKernelGGL((k_x3bpack<KS, WN, P1>), dim3((nf + TPB - 1) / TPB), dim3(TPB), 0, st, k);
             }
-            hipLaunchKernelGGL((k_x3rows<KS, WN, P1>), grid, dim3(TPB), 0, st, k);
+            hipLaunchKernelGGL((k_x3rows<KS, WN, P1>), grid, dim3(RT_TPB), 0, st, k);
         };
         using I8 = std::integral_constant<int, 8>;
         using I16 = std::integral_constant<int, 16>;
@@ -1365,7 +1418,7 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
             else hipLaunchKernelGGL((k_x3tn<1, 3, true>), grid, dim3(TPB), 0, st, k);
         } else if (BM == 256 && BN == 96 && g.M == 256 && !g.a.p2 && g.a.ones_col < 0 && !g.a.act && g.a.ncols >= 256 &&
                    g.a.ld >= 256) {
-            hipLaunchKernelGGL(k_x3dw, grid, dim3(TPB), 0, st, k);   // the row layers' weight gradients
+            hipLaunchKernelGGL(k_x3dw, grid, dim3(DW_TPB), 0, st, k);   // the row layers' weight gradients
         } else if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3tn<2, 3>), grid, dim3(TPB), 0, st, k);
         else if (BM == 256) hipLaunchKernelGGL((k_x3tn<2, 1>), grid, dim3(TPB), 0, st, k);
         else if (BN == 160) hipLaunchKernelGGL((k_x3tn<1, 5>), grid, dim3(TPB), 0, st, k);

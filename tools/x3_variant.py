@@ -396,6 +396,33 @@ __global__ __launch_bounds__(TPB, OCC) void k_x3tn(GemmK g) {''')
             }
         }
         // epilogue''')
+    elif p == "dwa_nomfma":   # k_x3dw ablation: no MFMAs (fragments kept live)
+        s = rep(s, """                    acc[a][b] = mfma32(af[a].lo, bf[b].hi, acc[a][b]);
+                    acc[a][b] = mfma32(af[a].hi, bf[b].lo, acc[a][b]);
+                    acc[a][b] = mfma32(af[a].hi, bf[b].hi, acc[a][b]);""",
+                """                    asm volatile("" :: "v"(af[a].lo), "v"(af[a].hi), "v"(bf[b].lo), "v"(bf[b].hi));""")
+    elif p == "dwa_noconv":   # k_x3dw ablation: no B conversion
+        s = rep(s, """        if (st + 1 < nst) convert(st + 1);""", "")
+    elif p == "dwa_noA":   # k_x3dw ablation: no A fragment reads / split (B's fragments reused)
+        s = rep(s, """                af[a] = split8_mix(v, fa);""", """                af[a] = X3Pair{h8{}, h8{}};
+                asm volatile("" :: "v"(v[0]));""")
+        s = rep(s, """                for (int e = 0; e < 8; ++e) v[e] = src[256 * e];""",
+                """                for (int e = 0; e < 1; ++e) v[e] = src[256 * e];""")
+    elif p == "dwa_nodma":   # k_x3dw ablation: no DMA (LDS as it is)
+        s = rep(s, """        for (int e = 0; e < 8; ++e) dma16(ra.r1, slot + (8 * w + e) * 1024, av, (rs + e) * ald);""",
+                """        for (int e = 0; e < 8; ++e) asm volatile("" :: "v"(av));""")
+        s = rep(s, """                dma16(rb.r1, dst, bv1[jj], rs * bld1);
+            } else {""", """                asm volatile("" :: "v"(bv1[jj]));
+            } else {""")
+    elif p == "dwa_nobar":   # k_x3dw ablation: waits without the barrier
+        s = rep(s, """    if (n == 14) asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)\\n\\ts_barrier" ::: "memory");
+    else if (n == 11) asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)\\n\\ts_barrier" ::: "memory");
+    else if (n == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\\n\\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\\n\\ts_barrier" ::: "memory");""",
+                """    if (n == 14) asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
+    else if (n == 11) asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory");
+    else if (n == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");""")
     else:
         return None
     return s
@@ -409,8 +436,8 @@ def main():
     work = os.path.join(top, "pkg", "csrc")      # sgn_common.h includes ../../include/sgn_hip.h
     shutil.copytree(CSRC, work, ignore=shutil.ignore_patterns("build"))
     os.symlink(os.path.join(ROOT, "include"), os.path.join(top, "include"))
-    src = open(os.path.join(work, "mlp_x3.hip")).read()
-    tsrc = open(os.path.join(work, "train_x3.hip")).read()
+    src = src0 = open(os.path.join(work, "mlp_x3.hip")).read()
+    tsrc = tsrc0 = open(os.path.join(work, "train_x3.hip")).read()
     for p in patches:
         t = patch_tx(tsrc, p)
         if t is not None:
@@ -419,9 +446,7 @@ def main():
             src = patch(src, p)
     open(os.path.join(work, "mlp_x3.hip"), "w").write(src)
     open(os.path.join(work, "train_x3.hip"), "w").write(tsrc)
-    txp = [q for q in patches if q.startswith("tx")]
-    xp = [q for q in patches if not q.startswith("tx")]
-    targets = (["mlp_x3"] if xp else []) + (["train_x3"] if txp else [])
+    targets = (["mlp_x3"] if src != src0 else []) + (["train_x3"] if tsrc != tsrc0 else [])
     out_dir = os.path.join(ROOT, "build", "variants")
     os.makedirs(out_dir, exist_ok=True)
     hipcc = "/opt/rocm/bin/hipcc"
