@@ -583,36 +583,38 @@ constexpr int RT_W = 8, RT_TPB = 64 * RT_W, RT_ROWS = 32 * RT_W, RT_PD = 4;
 // the A operand of the rows mode: row-major, 16-B aligned rows, columns in whole octets, the column
 // split at a multiple of 16 (host-checked), read through buffers over the valid rows (rows past them
 // read 0): lane's row offset in each source; k-step kb's source choice is wave-uniform
+template <bool HASP2, bool ACT>   // the operand has a second source (columns >= csplit); LeakyReLU on p's
 struct ARow {
     __amdgpu_buffer_rsrc_t r1, r2;
     uint32_t o1, o2;
-    int csplit, ncols, act;
+    int csplit, ncols;
     __device__ __forceinline__ void load(int kb, int hk, float (&v)[8]) const {
         const int k = kb + 8 * hk;
-        const bool s1 = kb < csplit;  // wave-uniform
+        const bool s1 = !HASP2 || kb < csplit;  // wave-uniform
         const uint32_t off = k >= ncols ? OOB : s1 ? o1 + (uint32_t)k * 4 : o2 + (uint32_t)(k - csplit) * 4;
         const float4 x = ld4(s1 ? r1 : r2, off), y = ld4(s1 ? r1 : r2, off + 16);
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
         v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
-        if (act && s1) {
+        if (ACT && s1) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = lrelu_max(v[e]);
         }
     }
 };
-__device__ __forceinline__ ARow arow(const Opnd &o, const OpRs &rs, int row) {
-    ARow a;
+template <bool HASP2, bool ACT>
+__device__ __forceinline__ ARow<HASP2, ACT> arow(const Opnd &o, const OpRs &rs, int row) {
+    ARow<HASP2, ACT> a;
     a.r1 = rs.r1;
     a.r2 = rs.r2;
     a.o1 = (uint32_t)((int64_t)row * o.ld * 4);
     a.o2 = o.p2 ? (uint32_t)((int64_t)row * o.ld2 * 4) : a.o1;
     a.csplit = o.csplit;
     a.ncols = o.ncols;
-    a.act = o.act;
     return a;
 }
 
-template <int KS, int WN, bool P1 = false>
+// HASP2: operand A has a second source; ACT: LeakyReLU on A; O2: the launch writes out2 (host-dispatched)
+template <int KS, int WN, bool P1, bool HASP2, bool ACT, bool O2>
 __global__ __launch_bounds__(RT_TPB, 1) void k_x3rows(GemmK g) {
     __shared__ __attribute__((aligned(16))) char lds[KS * WN * 2 * FRAG];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -653,12 +655,12 @@ __global__ __launch_bounds__(RT_TPB, 1) void k_x3rows(GemmK g) {
     float am1 = 0.f, am2 = 0.f;
     // outputs, mask and bias through buffers over the valid rows / columns (no per-value branches)
     const __amdgpu_buffer_rsrc_t ro1 = rows_rsrc(g.out, g.ldo, rows);
-    const __amdgpu_buffer_rsrc_t ro2 = rows_rsrc(g.out2 ? g.out2 : g.out, g.out2 ? g.ldo2 : g.ldo, g.out2 ? rows : 0);
+    const __amdgpu_buffer_rsrc_t ro2 = rows_rsrc(O2 ? g.out2 : g.out, O2 ? g.ldo2 : g.ldo, O2 ? rows : 0);
     const __amdgpu_buffer_rsrc_t rmk = rows_rsrc(g.mask ? g.mask : g.out, g.ldm, g.mask ? rows : 0);
     const __amdgpu_buffer_rsrc_t rbs = rows_rsrc(g.bias ? g.bias : g.out, 1, g.bias ? g.N : 0);
     for (; rt * RT_ROWS < rows; rt += gy) {
         const int m0 = rt * RT_ROWS + 32 * w;
-        const ARow ar = arow(g.A, rsA, m0 + L);
+        const ARow<HASP2, ACT> ar = arow<HASP2, ACT>(g.A, rsA, m0 + L);
         // A: k-steps s .. s + RT_PD - 1 in flight while k-step s's MFMAs run (a ring of RT_PD octets)
         float a[RT_PD][8];
 #pragma unroll
@@ -681,50 +683,50 @@ __global__ __launch_bounds__(RT_TPB, 1) void k_x3rows(GemmK g) {
                 }
                 acc[t] = mfma32(x.hi, bh, acc[t]);
             }
+            __builtin_amdgcn_sched_barrier(0);   // k-steps in order: the A ring's registers stay bounded
         }
-        // epilogue: every mask value of the tile is loaded before any is used (rows past the valid ones and
-        // columns past out_cols read 0: only out's columns are masked); the other wave of the SIMD hides it
-        float mk[WN][16];
-        if (g.mask) {
-#pragma unroll
-            for (int t = 0; t < WN; ++t) {
-                const int n = n0 + 32 * t + L;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                    const uint32_t off = n < g.out_cols ? (uint32_t)(((int64_t)row * g.ldm + n) * 4) : OOB;
-                    mk[t][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rmk, off, 0, 0));
-                }
-            }
-        }
-        auto epilogue = [&](auto o2c) {  // o2c: the launch writes out2 (kernel-uniform, one branch per tile)
-            constexpr bool O2 = decltype(o2c)::value;
+        // epilogue per 32-column tile: its 16 mask values loaded before any is used (columns past out_cols read
+        // 0: only out's columns are masked); lane offsets of the tile's first row with the row terms as scalar
+        // offsets; rows past the valid ones read 0 / are dropped by the buffer ranges and, in the one tile that
+        // has them (FULL false), kept out of the amax words; columns past N are 0 (zero B rows, no bias)
+        auto epilogue = [&](auto fullc) {
+            constexpr bool FULL = decltype(fullc)::value;
+            const uint32_t rb = (uint32_t)(m0 + 4 * hk);
 #pragma unroll
             for (int t = 0; t < WN; ++t) {
                 const int n = n0 + 32 * t + L;
                 const float bv =
                     __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbs, n < g.N ? (uint32_t)n * 4 : OOB, 0, 0));
-                const bool o1 = n < g.out_cols, o2 = !o1 && n < g.N;
+                const bool o1 = n < g.out_cols, o2 = O2 && !o1 && n < g.N;
+                const uint32_t b1 = o1 ? (rb * (uint32_t)g.ldo + (uint32_t)n) * 4 : OOB;
+                const uint32_t bm = o1 ? (rb * (uint32_t)g.ldm + (uint32_t)n) * 4 : OOB;
+                const uint32_t b2 = o2 ? (rb * (uint32_t)g.ldo2 + (uint32_t)(n - g.out_cols)) * 4 : OOB;
+                float mk[16];
+                if (g.mask) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const uint32_t rr = (r & 3) + 8 * (r >> 2);
+                        mk[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rmk, bm, rr * (uint32_t)g.ldm * 4, 0));
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-                    const bool rok = row < rows;
+                    const uint32_t rr = (r & 3) + 8 * (r >> 2);
                     float v = acc[t][r] * osc + bv;
-                    if (g.mask && o1 && !(mk[t][r] > 0.f)) v *= 0.01f;
-                    const float v1 = g.act ? lrelu_ref(v) : v;
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v1), ro1,
-                                                          o1 ? (uint32_t)(((int64_t)row * g.ldo + n) * 4) : OOB, 0, 0);
-                    am1 = fmaxf(am1, o1 && rok ? fabsf(v1) : 0.f);
+                    if (g.mask && (!O2 || o1) && !(mk[r] > 0.f)) v *= 0.01f;
+                    const float v1 = g.act ? lrelu_max(v) : v;
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v1), ro1, b1, rr * (uint32_t)g.ldo * 4, 0);
+                    const bool rok = FULL || (int)(rb + rr) < rows;
+                    am1 = fmaxf(am1, (!O2 || o1) && rok ? fabsf(v1) : 0.f);
                     if constexpr (O2) {
-                        __builtin_amdgcn_raw_buffer_store_b32(
-                            __builtin_bit_cast(uint32_t, v), ro2,
-                            o2 ? (uint32_t)(((int64_t)row * g.ldo2 + n - g.out_cols) * 4) : OOB, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ro2, b2,
+                                                              rr * (uint32_t)g.ldo2 * 4, 0);
                         am2 = fmaxf(am2, o2 && rok ? fabsf(v) : 0.f);
                     }
                 }
             }
         };
-        if (g.out2) epilogue(std::true_type{});
+        if (m0 + 32 <= rows) epilogue(std::true_type{});   // wave-uniform
         else epilogue(std::false_type{});
     }
 #pragma unroll
@@ -1377,6 +1379,13 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
             k.bpack = (char *)g.bpack;
         }
         // (KS, WN, P1): the weight conversion (with a workspace) then the row tiles
+        const bool hasp2 = g.a.p2 && g.a.csplit < g.a.ncols, o2 = g.out2 != nullptr, act = g.a.act != 0;
+        if (p1) SGN_REQUIRE(!hasp2 && !o2 && !act, "products 1: one-source operand a without activation, no out2");
+        // 32-bit buffer offsets: every rows-mode operand / output below 2 GiB
+        auto fits = [&](int64_t ld, int64_t cols) { return (int64_t)g.M * ld * 4 + cols * 4 < 0x7fffffff; };
+        SGN_REQUIRE(fits(g.a.ld, 0) && (!hasp2 || fits(g.a.ld2, 0)) && fits(g.ldo, 0) && (!g.mask || fits(g.ldm, 0)) &&
+                        (!o2 || fits(g.ldo2, 0)),
+                    "mode 0: operands and outputs must stay below 2 GiB");
         auto launch = [&](auto ks_c, auto wn_c, auto p1_c) {
             constexpr int KS = decltype(ks_c)::value, WN = decltype(wn_c)::value;
             constexpr bool P1 = decltype(p1_c)::value;
@@ -1384,7 +1393,23 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
                 const int nf = nb * KS * WN * 64;
                 hipLaunchKernelGGL((k_x3bpack<KS, WN, P1>), dim3((nf + TPB - 1) / TPB), dim3(TPB), 0, st, k);
             }
-            hipLaunchKernelGGL((k_x3rows<KS, WN, P1>), grid, dim3(RT_TPB), 0, st, k);
+            if constexpr (P1) {
+                hipLaunchKernelGGL((k_x3rows<KS, WN, P1, false, false, false>), grid, dim3(RT_TPB), 0, st, k);
+            } else {
+                auto go = [&](auto hc, auto ac, auto oc) {
+                    hipLaunchKernelGGL((k_x3rows<KS, WN, P1, decltype(hc)::value, decltype(ac)::value, decltype(oc)::value>),
+                                       grid, dim3(RT_TPB), 0, st, k);
+                };
+                using T = std::true_type;
+                using F = std::false_type;
+                if (hasp2) {
+                    if (act) o2 ? go(T{}, T{}, T{}) : go(T{}, T{}, F{});
+                    else o2 ? go(T{}, F{}, T{}) : go(T{}, F{}, F{});
+                } else {
+                    if (act) o2 ? go(F{}, T{}, T{}) : go(F{}, T{}, F{});
+                    else o2 ? go(F{}, F{}, T{}) : go(F{}, F{}, F{});
+                }
+            }
         };
         using I8 = std::integral_constant<int, 8>;
         using I16 = std::integral_constant<int, 16>;
