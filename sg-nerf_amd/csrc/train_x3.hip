@@ -385,15 +385,17 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *ldsdst, ui
 
 // this wave's DMAs but the last n issued have landed, its LDS writes are done, then the workgroup barrier
 // (after it every wave's have); the asm's memory clobber keeps the compiler's LDS accesses on their side
-__device__ __forceinline__ void dw_wait_barrier(int n) {
-    if (n == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (n == 7) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (n == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (n == 5) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (n == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+// (a wave's last DMA group: A's 4 rows, then 1 or 2 B chunks -- each one or two exec-masked instructions
+// -- so "all but the last 5" is a safe bound for every wave: it may wait for a little more, never less)
+template <int N>
+__device__ __forceinline__ void dw_wait_barrier() {
+    static_assert(N == 5 || N == 4 || N == 0, "");
+    if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+template <bool BACT>   // LeakyReLU on B's p columns
 __global__ __launch_bounds__(DW_TPB, 1) void k_x3dw(GemmK g) {
     __shared__ __attribute__((aligned(16))) char lds[DW_LDS];
     char *const la = lds, *const lb = lds + DW_NST * DW_ABYTES, *const lf = lb + DW_NST * DW_BBYTES;
@@ -427,16 +429,8 @@ __global__ __launch_bounds__(DW_TPB, 1) void k_x3dw(GemmK g) {
         bv2[jj] = ok && !bs1[jj] ? (uint32_t)rr * bld2 + (uint32_t)((c - g.B.csplit) * 4) : OOB;
     }
     const bool bmixed = __ballot(!(bs1[0] && bs1[1])) != 0;   // wave-uniform: a p2 chunk in this wave
-    // a mixed wave issues a chunk's p lanes and p2 lanes as two exec-masked instructions, each only when
-    // it has a lane (so the in-flight count below is exact)
-    bool any1[2], any2[2];
-    int nbdma = 0;
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-        any1[jj] = __ballot(bs1[jj]) != 0;
-        any2[jj] = __ballot(!bs1[jj]) != 0;
-        if (jj == 0 || two) nbdma += bmixed ? (int)any1[jj] + (int)any2[jj] : 1;
-    }
+    // a mixed wave issues a chunk's p lanes and p2 lanes as two exec-masked instructions (at least one of
+    // them has a lane: one or two instructions per chunk)
     const uint32_t av = (uint32_t)(4 * w) * ald + lane * 16;
     auto issue_a = [&](int st) {   // A rows r0 + 32 st .. into A slot st % 3: 4 rows per wave, a 1-KiB row each
         char *slot = la + (st % DW_NST) * DW_ABYTES;
@@ -454,8 +448,8 @@ __global__ __launch_bounds__(DW_TPB, 1) void k_x3dw(GemmK g) {
             if (!bmixed) {
                 dma16(rb.r1, dst, bv1[jj], rs * bld1);
             } else {   // p and p2 lanes in separate exec-masked instructions
-                if (any1[jj] && bs1[jj]) dma16(rb.r1, dst, bv1[jj], rs * bld1);
-                if (any2[jj] && !bs1[jj]) dma16(rb.r2, dst, bv2[jj], rs * bld2);
+                if (bs1[jj]) dma16(rb.r1, dst, bv1[jj], rs * bld1);
+                else dma16(rb.r2, dst, bv2[jj], rs * bld2);
             }
         }
     };
@@ -472,7 +466,7 @@ __global__ __launch_bounds__(DW_TPB, 1) void k_x3dw(GemmK g) {
         const int kb = min((w >> 1) + 4 * j, 5), ks = kb / 3, b = kb % 3;
         const int c = n0 + 32 * b + L;
         cone[j] = c == g.B.ones_col;
-        cm[j] = g.B.act && c < g.B.csplit ? 0.01f : 1.f;
+        cm[j] = c < g.B.csplit ? 0.01f : 1.f;
         crow[j] = 16 * ks + 8 * hk + 4 * half;
         ccol[j] = 32 * b + L;
         cimg[j] = (kb * 2) * FRAG + lane * 16 + 8 * half;
@@ -488,7 +482,7 @@ __global__ __launch_bounds__(DW_TPB, 1) void k_x3dw(GemmK g) {
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = src[(crow[j] + e) * DW_BN + ccol[j]];
-            if (g.B.act) {   // kernel-uniform
+            if (BACT) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {   // max(x, m x) as one v_max (no canonicalising max of the LDS value)
                     float t = v[e] * cm[j];
@@ -516,21 +510,30 @@ __global__ __launch_bounds__(DW_TPB, 1) void k_x3dw(GemmK g) {
     // are (A(st + 2), B(st + 3)) in that order, so at stage st the last group issued may stay in flight
     if (nst > 0) {
         issue_b(0);
-        dw_wait_barrier(0);
+        dw_wait_barrier<0>();
         convert(0);
         issue_a(0);
         if (nst > 1) issue_b(1);
         if (nst > 1) issue_a(1);
         if (nst > 2) issue_b(2);
     }
-    for (int st = 0; st < nst; ++st) {
-        // A(st) and B(st + 1) landed (this wave's; the group issued last may stay in flight), every wave's
-        // after the barrier, and every wave is done with stage st - 1 (its A slot, which A(st + 2) reuses,
-        // and its fragment image, which B(st + 1)'s conversion reuses) and has converted B(st)
-        dw_wait_barrier(st + 2 < nst ? 4 + nbdma : st + 1 < nst ? 4 : 0);
-        if (st + 2 < nst) issue_a(st + 2);
-        if (st + 3 < nst) issue_b(st + 3);
-        if (st + 1 < nst) convert(st + 1);
+    // stage st: A(st) and B(st + 1) landed (this wave's; the group issued last may stay in flight), every
+    // wave's after the barrier, and every wave is done with stage st - 1 (its A slot, which A(st + 2)
+    // reuses, and its fragment image, which B(st + 1)'s conversion reuses) and has converted B(st).
+    // TAIL: one of the last three stages (fewer loads ahead)
+    auto stage = [&](int st, auto tailc) {
+        constexpr bool TAIL = decltype(tailc)::value;
+        if constexpr (!TAIL) {
+            dw_wait_barrier<5>();
+            issue_a(st + 2);
+            issue_b(st + 3);
+            convert(st + 1);
+        } else {
+            if (st + 1 < nst) dw_wait_barrier<4>();
+            else dw_wait_barrier<0>();
+            if (st + 2 < nst) issue_a(st + 2);
+            if (st + 1 < nst) convert(st + 1);
+        }
         const char *slot = la + (st % DW_NST) * DW_ABYTES;
         const char *fr = lf + (st & 1) * DW_FBYTES + lane * 16;
 #pragma unroll
@@ -556,7 +559,10 @@ __global__ __launch_bounds__(DW_TPB, 1) void k_x3dw(GemmK g) {
                 acc[b] = mfma32(af.hi, bf[b].hi, acc[b]);
             }
         }
-    }
+    };
+    int st = 0;
+    for (; st + 3 < nst; ++st) stage(st, std::false_type{});
+    for (; st < nst; ++st) stage(st, std::true_type{});
     const __amdgpu_buffer_rsrc_t pr = rows_rsrc(g.part + (int64_t)split * g.M * g.N, g.N, g.M);
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
@@ -1443,7 +1449,9 @@ int sgn_x3_gemm(const sgn_x3_gemm_args *ga, sgn_stream_t stream) {
             else hipLaunchKernelGGL((k_x3tn<1, 3, true>), grid, dim3(TPB), 0, st, k);
         } else if (BM == 256 && BN == 96 && g.M == 256 && !g.a.p2 && g.a.ones_col < 0 && !g.a.act && g.a.ncols >= 256 &&
                    g.a.ld >= 256) {
-            hipLaunchKernelGGL(k_x3dw, grid, dim3(DW_TPB), 0, st, k);   // the row layers' weight gradients
+            // the row layers' weight gradients
+            if (g.b.act) hipLaunchKernelGGL(k_x3dw<true>, grid, dim3(DW_TPB), 0, st, k);
+            else hipLaunchKernelGGL(k_x3dw<false>, grid, dim3(DW_TPB), 0, st, k);
         } else if (BM == 256 && BN == 96) hipLaunchKernelGGL((k_x3tn<2, 3>), grid, dim3(TPB), 0, st, k);
         else if (BM == 256) hipLaunchKernelGGL((k_x3tn<2, 1>), grid, dim3(TPB), 0, st, k);
         else if (BN == 160) hipLaunchKernelGGL((k_x3tn<1, 5>), grid, dim3(TPB), 0, st, k);
