@@ -226,57 +226,9 @@ def _colmap(which, n, device):
     return torch.frombuffer(bytearray(a), dtype=torch.int32).long().to(device)
 
 
-_MM_OUT_DTYPE = None
-_BMM_OUT_DTYPE = None
-
-
-def _gemm_rows_parts(a, b, chunk):
-    """a^T b over the row dimension as split-K partials: a [rows, M], b [rows, N] fp16 ->
-    ([nb, M, N] fp32 partials, [M, N] tail partial or None); their sum is a^T b.
-
-    The rows go in `chunk`-row batches through one batched GEMM (a 256 x 288 output alone is ~8
-    macro tiles, so a plain GEMM would occupy a handful of the 256 CUs and walk K = 160 k rows
-    serially); a ragged tail of rows takes one more plain GEMM.  The partials are summed by the
-    gradient epilogue (sgn_grad_accumulate), not here.  Every row is in exactly one partial."""
-    global _BMM_OUT_DTYPE
-    rows = a.shape[0]
-    nb = rows // chunk if chunk > 0 else 0
-    if nb <= 1:
-        return _mm_f32(a.t(), b)[None], None
-    body = nb * chunk
-    at = a[:body].view(nb, chunk, a.shape[1]).transpose(1, 2)
-    bt = b[:body].view(nb, chunk, b.shape[1])
-    if _BMM_OUT_DTYPE is None:
-        try:
-            torch.bmm(at[:1, :1, :1], bt[:1, :1, :1], out_dtype=torch.float32)
-            _BMM_OUT_DTYPE = True
-        except Exception:
-            _BMM_OUT_DTYPE = False
-    G = torch.bmm(at, bt, out_dtype=torch.float32) if _BMM_OUT_DTYPE else torch.bmm(at.float(), bt.float())
-    tail = _mm_f32(a[body:].t(), b[body:]) if body < rows else None
-    return G.contiguous(), tail
-
-
 # loss-stage graphs: capacity bucket (items / samples) and how many captured graphs are kept
 GRAPH_BUCKET = int(os.environ.get("SGN_GRAPH_BUCKET", "8192"))
 GRAPH_CACHE = 8
-
-# rows per split-K batch of the weight-gradient GEMMs (SGN_DW_CHUNK overrides, for sweeps)
-DW_CHUNK = int(os.environ.get("SGN_DW_CHUNK", "2048"))
-
-
-def _mm_f32(a, b):
-    """fp16 x fp16 -> fp32 GEMM (hipBLASLt through torch.mm(out_dtype=)); fp32 GEMM otherwise."""
-    global _MM_OUT_DTYPE
-    if _MM_OUT_DTYPE is None:
-        try:
-            torch.mm(a[:1, :1], b[:1, :1], out_dtype=torch.float32)
-            _MM_OUT_DTYPE = True
-        except Exception:
-            _MM_OUT_DTYPE = False
-    if _MM_OUT_DTYPE:
-        return torch.mm(a, b, out_dtype=torch.float32)
-    return a.float() @ b.float()
 
 
 def _grad_into(g, dst, parts, tail=None, scale=None):
@@ -819,22 +771,31 @@ class HipTrainer:
             maps = self._flat_maps[name] = (dw, db)
         return maps
 
+    def _dw_parts(self, name, d, x, rows):
+        """dW = d^T x over the first `rows` rows (fp16 operands, fp32 accumulation) as split-K partials
+        [splits, 256, C] from sgn_f16_weight_grad (rows past `rows` are never read); their sum is dW.
+        One partial buffer per layer: the step's single sgn_grad_accumulate reads them all."""
+        C = x.shape[1]
+        parts = self._dw_bufs.get(name)
+        if parts is None or parts.shape[2] != C:
+            splits = max(1, 256 // -(-C // 128))   # about one workgroup per CU
+            parts = self._dw_bufs[name] = torch.empty(splits, 256, C, dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().sgn_f16_weight_grad(_lib.ptr(d), d.stride(0), _lib.ptr(x), x.stride(0), C, rows,
+                                                  parts.shape[0], _lib.ptr(parts), _lib.stream_handle()),
+                   "sgn_f16_weight_grad")
+        return parts, None
+
     def _weight_grads(self, rows, scale, q=None):
-        """dW_l = delta_l^T x_l (fp16 GEMM, fp32 split-K partials), db_l = sum delta_l; the partials
-        summed, unscaled and unpermuted into the flat gradient by one sgn_grad_accumulate launch."""
+        """dW_l = delta_l^T x_l (sgn_f16_weight_grad: fp16 operands, fp32 split-K partials), db_l = sum
+        delta_l; the partials summed, unscaled and unpermuted into the flat gradient by one
+        sgn_grad_accumulate launch."""
         m = self.mlp
         g = m.flat.grad
         L = _lib.lib()
         st = _lib.stream_handle()
-        rp = ((rows + 1023) // 1024) * 1024   # rows padded to the split-K batch (buffers are)
-        chunk = max(DW_CHUNK, -(-rp // 512))  # at most 512 batches (no ragged tail up to 512 * DW_CHUNK rows)
-        if rp > rows:                          # stale tails must not reach the GEMM (0 * NaN): one clear launch
-            tails = [t[rows:rp] for t in self.d + [self.x0, self.h1, self.h2, self.h3]
-                     + ([self.h2b, self.db] if self.sg else [])]
-            _lib.check(L.sgn_zero_segments(len(tails), (ctypes.c_void_p * len(tails))(*(t.data_ptr() for t in tails)),
-                                           (ctypes.c_int64 * len(tails))(*(t.numel() * t.element_size() for t in tails)),
-                                           st),
-                       "sgn_zero_segments")
+        rp = ((rows + 1023) // 1024) * 1024   # rows padded (the SG embedding gather's view)
+        if not hasattr(self, "_dw_bufs"):
+            self._dw_bufs = {}
         # db_l = column sums of the delta tiles (+ block2_bpnet's for SG) and the alpha branch's
         # dWa = dza^T h4 (row-weighted column sums), in one pair of launches
         nd = 5 if self.sg else 4
@@ -867,14 +828,14 @@ class HipTrainer:
                 x = torch.cat([x, bp], dim=1)
             ix = torch.cat([self.inv_chain, 256 + torch.arange(self.variant[1], device=self.device)])
             dw, db = self._dst_maps(BPNET, x.shape[1], ix)
-            add(*_gemm_rows_parts(self.db[:rp], x, chunk), dw)
+            add(*self._dw_parts(BPNET, self.db, x, rows), dw)
             add(self._cs_out[4], None, db)
         for li, (name, d, x, ix) in enumerate((("block3.2", self.d[3], self.h3, self.inv_chain),
                                                ("block3.0", self.d[2], self.h2, self.inv_h2),
                                                ("block1.2", self.d[1], self.h1, self.inv_chain),
                                                ("block1.0", self.d[0], self.x0, self.inv_x0))):
             dw, db = self._dst_maps(name, x.shape[1], ix)
-            add(*_gemm_rows_parts(d[:rp], x[:rp], chunk), dw)    # [256 stored][C stored]
+            add(*self._dw_parts(name, d, x, rows), dw)    # [256 stored][C stored]
             add(self._cs_out[li], None, db)
         # alpha branch: dWa = dza^T h4, dba = sum dza
         amaps = self._flat_maps.get("alpha_branch.0")
