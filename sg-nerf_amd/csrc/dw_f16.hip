@@ -42,8 +42,23 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *ldsdst, ui
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)ldsdst, 16, voff, soff, 0, 0);
 }
 
-__device__ __forceinline__ s4 tr4(const char *p) {
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4 *)p);
+// The transposed reads as inline asm at an LDS byte address: through the builtin the compiler treats
+// them as possibly aliasing the in-flight LDS-DMA of the later stages and waits for all of it (vmcnt(0))
+// before every stage, which would leave no DMA in flight.  The asm's results are tied to an explicit
+// lgkmcnt wait (lgkm_tie) before any MFMA reads them.
+template <int OFF>
+__device__ __forceinline__ s4 tr4(uint32_t addr) {
+    s4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+    return r;
+}
+// this wave's LDS reads but the last N returned; the registers listed are ordered after the wait
+template <int N>
+__device__ __forceinline__ void lgkm_tie(s4 (&v)[10]) {
+    asm volatile("s_waitcnt lgkmcnt(%10)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+                   "+v"(v[8]), "+v"(v[9])
+                 : "i"(N));
 }
 
 // this wave's DMAs but the last N landed, then the workgroup barrier (every wave's have, after it); the
@@ -117,10 +132,12 @@ __global__ __launch_bounds__(TPB, 1) void k_f16dw(Args g) {
     const int gq = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
     const int trow = 8 * (gq >> 1) + q;
     const int csub = 2 * (gq & 1) + (p >> 1), cbyte = (p & 1) * 8;   // chunk within the tile, byte within it
-    const uint32_t aoff = (uint32_t)(trow * 512 + ((4 * w + csub) ^ (4 * q)) * 16 + cbyte);
+    const uint32_t lbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lds;
+    const uint32_t aoff = lbase + (uint32_t)(trow * 512 + ((4 * w + csub) ^ (4 * q)) * 16 + cbyte);
     uint32_t boff[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) boff[b] = (uint32_t)(ABYTES + trow * 256 + ((4 * b + csub) ^ (4 * q)) * 16 + cbyte);
+    for (int b = 0; b < 4; ++b)
+        boff[b] = lbase + (uint32_t)(ABYTES + trow * 256 + ((4 * b + csub) ^ (4 * q)) * 16 + cbyte);
     f32x16 acc[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[b] = f32x16{};
@@ -137,19 +154,34 @@ __global__ __launch_bounds__(TPB, 1) void k_f16dw(Args g) {
             else if (st + 1 < nst) wait_barrier<3>();
             else wait_barrier<0>();
         }
-        const char *slot = lds + (st % NST) * STAGE;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int ro = (16 * ks) * 512, rob = (16 * ks) * 256;
-            const s4 a0 = tr4(slot + aoff + ro), a1 = tr4(slot + aoff + ro + 4 * 512);
-            const h8 af = __builtin_bit_cast(h8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+        const uint32_t so = (uint32_t)((st % NST) * STAGE);
+        // both k-steps' fragments requested up front (k-step ks: rows 16 ks ..; h = 1: 4 rows further), the
+        // first k-step's MFMAs after its 10 reads returned
+        s4 f[2][10];
+        auto reads = [&](auto ksc) {
+            constexpr int KS = decltype(ksc)::value;
+            f[KS][0] = tr4<KS * 16 * 512>(aoff + so);
+            f[KS][1] = tr4<KS * 16 * 512 + 4 * 512>(aoff + so);
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                const s4 b0 = tr4(slot + boff[b] + rob), b1 = tr4(slot + boff[b] + rob + 4 * 256);
-                const h8 bf = __builtin_bit_cast(h8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+                f[KS][2 + 2 * b] = tr4<KS * 16 * 256>(boff[b] + so);
+                f[KS][3 + 2 * b] = tr4<KS * 16 * 256 + 4 * 256>(boff[b] + so);
+            }
+        };
+        auto mfmas = [&](const s4 (&v)[10]) {
+            const h8 af = __builtin_bit_cast(h8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const h8 bf = __builtin_bit_cast(h8, __builtin_shufflevector(v[2 + 2 * b], v[3 + 2 * b], 0, 1, 2, 3, 4, 5, 6, 7));
                 acc[b] = mfma32(af, bf, acc[b]);
             }
-        }
+        };
+        reads(std::integral_constant<int, 0>{});
+        reads(std::integral_constant<int, 1>{});
+        lgkm_tie<10>(f[0]);
+        mfmas(f[0]);
+        lgkm_tie<0>(f[1]);
+        mfmas(f[1]);
     };
     int st = 0;
     for (; st + 3 < nst; ++st) stage(st, std::false_type{});
