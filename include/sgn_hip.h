@@ -518,9 +518,10 @@ size_t sgn_x3_gemm_bpack_bytes(const sgn_x3_gemm_args *g);   /* ABI 13; 0 unless
  * base_rendering_model.py:534-664): part[s][m][n] = sum over the rows r of run s of d[r][m] x[r][n]
  * (fp32 accumulation of the exact fp16 products) for m < 256, n < ncols, the rows r < n_rows cut into
  * `splits` equal 32-aligned runs (empty runs write zeros); part is fp32 [splits][256][ncols].  d: fp16
- * [n_rows][ldd] (ldd >= 256), x: fp16 [n_rows][ldx], 16-B aligned rows, ncols % 8 == 0. */
+ * [n_rows][ldd] (ldd >= 256), x: fp16 [n_rows][ldx], 16-B aligned rows, ncols % 8 == 0.  part_bias
+ * (or NULL): fp32 [splits][256], the runs' column sums of d (the layer's bias gradient partials). */
 int sgn_f16_weight_grad(const void *d, int64_t ldd, const void *x, int64_t ldx, int32_t ncols, int32_t n_rows,
-                        int32_t splits, float *part, sgn_stream_t stream);
+                        int32_t splits, float *part, float *part_bias, sgn_stream_t stream);
 
 /* Deterministic work list and compact row offsets after sgn_query: for s < d_counters[0],
  * d_row_off[s] = sum of samp_nnb over samples < s; d_work = the samples with samp_nnb > 0 in

@@ -177,7 +177,7 @@ SIGNATURES = {
     "sgn_train_row_gather": (c_i32, [ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "sgn_x3_gemm": (c_i32, [ctypes.POINTER(X3GemmArgs), c_vp]),
     "sgn_x3_gemm_bpack_bytes": (c_sz, [ctypes.POINTER(X3GemmArgs)]),
-    "sgn_f16_weight_grad": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "sgn_f16_weight_grad": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "sgn_train_lists_workspace_bytes": (c_sz, [c_i64]),
     "sgn_train_lists": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_train_row_inputs": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp, c_vp,

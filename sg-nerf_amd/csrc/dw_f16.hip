@@ -36,6 +36,7 @@ struct Args {
     uint32_t ldd2, ldx2;   // row strides in bytes
     int32_t ncols, n_rows, splits;
     float *part;
+    float *part_bias;   // or null: [splits][256] column sums of d (the bias gradient), by the first column block
 };
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *ldsdst, uint32_t voff, uint32_t soff) {
@@ -138,9 +139,14 @@ __global__ __launch_bounds__(TPB, 1) void k_f16dw(Args g) {
 #pragma unroll
     for (int b = 0; b < 4; ++b)
         boff[b] = lbase + (uint32_t)(ABYTES + trow * 256 + ((4 * b + csub) ^ (4 * q)) * 16 + cbyte);
-    f32x16 acc[4];
+    f32x16 acc[4], accb = {};
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[b] = f32x16{};
+    // the bias gradient sum_r d[r][m]: d against an all-ones B fragment, in the first column block's workgroups
+    const bool bias = g.part_bias && blk == 0;   // workgroup-uniform
+    h8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (_Float16)1.f;
     for (int st = 0; st < 3 && st < nst; ++st) issue(st);
     // stage st: this wave's DMAs of stage st landed (those of st + 1, st + 2 may stay in flight), every wave's
     // after the barrier, and every wave is done with stage st - 1, whose slot stage st + 3 reuses
@@ -175,6 +181,7 @@ __global__ __launch_bounds__(TPB, 1) void k_f16dw(Args g) {
                 const h8 bf = __builtin_bit_cast(h8, __builtin_shufflevector(v[2 + 2 * b], v[3 + 2 * b], 0, 1, 2, 3, 4, 5, 6, 7));
                 acc[b] = mfma32(af, bf, acc[b]);
             }
+            if (bias) accb = mfma32(af, ones, accb);
         };
         reads(std::integral_constant<int, 0>{});
         reads(std::integral_constant<int, 1>{});
@@ -190,6 +197,11 @@ __global__ __launch_bounds__(TPB, 1) void k_f16dw(Args g) {
     const int L = lane & 31, hk = lane >> 5;
     const __amdgpu_buffer_rsrc_t pr =
         rsrc((const char *)(g.part + (int64_t)split * 256 * g.ncols), (int64_t)256 * g.ncols * 4);
+    if (bias && L == 0) {   // every column of accb holds the sums: lanes 0 and 32 store theirs
+        float *pb = g.part_bias + (int64_t)split * 256;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pb[32 * w + (r & 3) + 8 * (r >> 2) + 4 * hk] = accb[r];
+    }
     // lane offset of (row 32 w + 4 hk, column n) (past ncols: out of range) plus the register's row term as
     // the scalar offset: no per-store select
     const uint32_t rowb = (uint32_t)g.ncols * 4;
@@ -214,7 +226,7 @@ __global__ __launch_bounds__(TPB, 1) void k_f16dw(Args g) {
 extern "C" {
 
 int sgn_f16_weight_grad(const void *d, int64_t ldd, const void *x, int64_t ldx, int32_t ncols, int32_t n_rows,
-                        int32_t splits, float *part, sgn_stream_t stream) {
+                        int32_t splits, float *part, float *part_bias, sgn_stream_t stream) {
     using namespace sgn;
     SGN_REQUIRE(d && x && part, "null pointer");
     SGN_REQUIRE(ncols > 0 && ncols % 8 == 0 && ldx >= ncols && ldx % 8 == 0 && ldd >= 256 && ldd % 8 == 0,
@@ -232,6 +244,7 @@ int sgn_f16_weight_grad(const void *d, int64_t ldd, const void *x, int64_t ldx, 
     a.n_rows = n_rows;
     a.splits = splits;
     a.part = part;
+    a.part_bias = part_bias;
     const int nb = (ncols + f16dw::BN - 1) / f16dw::BN;
     hipLaunchKernelGGL(f16dw::k_f16dw, dim3(nb * splits), dim3(f16dw::TPB), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());

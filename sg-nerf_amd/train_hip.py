@@ -772,18 +772,20 @@ class HipTrainer:
         return maps
 
     def _dw_parts(self, name, d, x, rows):
-        """dW = d^T x over the first `rows` rows (fp16 operands, fp32 accumulation) as split-K partials
-        [splits, 256, C] from sgn_f16_weight_grad (rows past `rows` are never read); their sum is dW.
-        One partial buffer per layer: the step's single sgn_grad_accumulate reads them all."""
+        """dW = d^T x and db = sum_r d[r] over the first `rows` rows (fp16 operands, fp32 accumulation) as
+        split-K partials ([splits, 256, C], [splits, 256]) from sgn_f16_weight_grad (rows past `rows` are
+        never read).  One pair of buffers per layer: the step's single sgn_grad_accumulate reads them all."""
         C = x.shape[1]
-        parts = self._dw_bufs.get(name)
-        if parts is None or parts.shape[2] != C:
+        bufs = self._dw_bufs.get(name)
+        if bufs is None or bufs[0].shape[2] != C:
             splits = max(1, 256 // -(-C // 128))   # about one workgroup per CU
-            parts = self._dw_bufs[name] = torch.empty(splits, 256, C, dtype=torch.float32, device=self.device)
+            bufs = self._dw_bufs[name] = (torch.empty(splits, 256, C, dtype=torch.float32, device=self.device),
+                                          torch.empty(splits, 256, dtype=torch.float32, device=self.device))
+        parts, pb = bufs
         _lib.check(_lib.lib().sgn_f16_weight_grad(_lib.ptr(d), d.stride(0), _lib.ptr(x), x.stride(0), C, rows,
-                                                  parts.shape[0], _lib.ptr(parts), _lib.stream_handle()),
+                                                  parts.shape[0], _lib.ptr(parts), _lib.ptr(pb), _lib.stream_handle()),
                    "sgn_f16_weight_grad")
-        return parts, None
+        return parts, pb
 
     def _weight_grads(self, rows, scale, q=None):
         """dW_l = delta_l^T x_l (sgn_f16_weight_grad: fp16 operands, fp32 split-K partials), db_l = sum
@@ -796,18 +798,15 @@ class HipTrainer:
         rp = ((rows + 1023) // 1024) * 1024   # rows padded (the SG embedding gather's view)
         if not hasattr(self, "_dw_bufs"):
             self._dw_bufs = {}
-        # db_l = column sums of the delta tiles (+ block2_bpnet's for SG) and the alpha branch's
-        # dWa = dza^T h4 (row-weighted column sums), in one pair of launches
-        nd = 5 if self.sg else 4
+        # the alpha branch's dWa = dza^T h4 (row-weighted column sums); the row layers' bias gradients come
+        # with their weight gradients (sgn_f16_weight_grad's column sums)
         if not hasattr(self, "_cs_out"):
-            self._cs_ws = torch.empty(int(L.sgn_colsum_workspace_bytes(nd + 1)) // 4, dtype=torch.float32,
+            self._cs_ws = torch.empty(int(L.sgn_colsum_workspace_bytes(1)) // 4, dtype=torch.float32,
                                       device=self.device)
-            self._cs_out = torch.empty(nd + 1, 256, dtype=torch.float32, device=self.device)
-        dl = [self.d[3], self.d[2], self.d[1], self.d[0]] + ([self.db] if self.sg else []) + [self.h4]
-        ds = (ctypes.c_void_p * (nd + 1))(*(t.data_ptr() for t in dl))
-        rw = (ctypes.c_void_p * (nd + 1))(*([None] * nd + [self.dza.data_ptr()]))
-        _lib.check(L.sgn_colsum_f16_weighted(nd + 1, ds, rw, rows, 256, _lib.ptr(self._cs_ws), _lib.ptr(self._cs_out),
-                                             st), "sgn_colsum_f16_weighted")
+            self._cs_out = torch.empty(1, 256, dtype=torch.float32, device=self.device)
+        _lib.check(L.sgn_colsum_f16_weighted(1, (ctypes.c_void_p * 1)(self.h4.data_ptr()),
+                                             (ctypes.c_void_p * 1)(self.dza.data_ptr()), rows, 256, _lib.ptr(self._cs_ws),
+                                             _lib.ptr(self._cs_out), st), "sgn_colsum_f16_weighted")
         segs, keep = [], []
 
         def add(src, tail, dst):
@@ -828,15 +827,17 @@ class HipTrainer:
                 x = torch.cat([x, bp], dim=1)
             ix = torch.cat([self.inv_chain, 256 + torch.arange(self.variant[1], device=self.device)])
             dw, db = self._dst_maps(BPNET, x.shape[1], ix)
-            add(*self._dw_parts(BPNET, self.db, x, rows), dw)
-            add(self._cs_out[4], None, db)
+            parts, pb = self._dw_parts(BPNET, self.db, x, rows)
+            add(parts, None, dw)
+            add(pb, None, db)
         for li, (name, d, x, ix) in enumerate((("block3.2", self.d[3], self.h3, self.inv_chain),
                                                ("block3.0", self.d[2], self.h2, self.inv_h2),
                                                ("block1.2", self.d[1], self.h1, self.inv_chain),
                                                ("block1.0", self.d[0], self.x0, self.inv_x0))):
             dw, db = self._dst_maps(name, x.shape[1], ix)
-            add(*self._dw_parts(name, d, x, rows), dw)    # [256 stored][C stored]
-            add(self._cs_out[li], None, db)
+            parts, pb = self._dw_parts(name, d, x, rows)
+            add(parts, None, dw)    # [256 stored][C stored]
+            add(pb, None, db)
         # alpha branch: dWa = dza^T h4, dba = sum dza
         amaps = self._flat_maps.get("alpha_branch.0")
         if amaps is None:
@@ -845,7 +846,7 @@ class HipTrainer:
             dwa[self.inv_chain] = (off + torch.arange(256, device=self.device)).to(torch.int32)
             amaps = self._flat_maps["alpha_branch.0"] = (dwa, torch.full((1,), off + i, dtype=torch.int32,
                                                                         device=self.device))
-        add(self._cs_out[nd], None, amaps[0])
+        add(self._cs_out[0], None, amaps[0])
         add(self.dza[:rows].sum().reshape(1), None, amaps[1])
         _lib.check(L.sgn_grad_accumulate(len(segs), (_lib.GradSegment * len(segs))(*segs), _lib.ptr(scale),
                                          _lib.ptr(g), st), "sgn_grad_accumulate")

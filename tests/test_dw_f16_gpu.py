@@ -1,5 +1,5 @@
 """GPU test of sgn_f16_weight_grad (csrc/dw_f16.hip), the f16 training step's row-layer weight
-gradients: split-K partials of d^T x over fp16 rows against float64 torch on the same fp16 values, at
+and bias gradients: split-K partials of d^T x over fp16 rows against float64 torch on the same fp16 values, at
 the step's column counts (256, 272, 288, SG's 352), ragged row counts and empty runs."""
 import pytest
 import torch
@@ -21,10 +21,15 @@ def test_f16_weight_grad_matches_float64(ncols, rows, splits):
     d[rows:] = float("nan")
     x[rows:] = float("nan")
     part = torch.full((splits, 256, ncols), float("nan"), device=DEV)
+    pb = torch.full((splits, 256), float("nan"), device=DEV)
     _lib.check(_lib.lib().sgn_f16_weight_grad(_lib.ptr(d), 256, _lib.ptr(x), ncols, ncols, rows, splits,
-                                              _lib.ptr(part), _lib.stream_handle()), "sgn_f16_weight_grad")
+                                              _lib.ptr(part), _lib.ptr(pb), _lib.stream_handle()), "sgn_f16_weight_grad")
     torch.cuda.synchronize()
-    assert bool(torch.isfinite(part).all())
+    assert bool(torch.isfinite(part).all()) and bool(torch.isfinite(pb).all())
+    # the bias partials: column sums of d (fp32 accumulation of exact fp16 values)
+    refb = d[:rows].double().sum(0)
+    magb = d[:rows].double().abs().sum(0)
+    assert float(((pb.double().sum(0) - refb).abs() / magb.clamp(min=1e-30)).max()) < 3e-5
     ref = d[:rows].double().t() @ x[:rows].double()
     got = part.double().sum(0)
     if rows == 0:
