@@ -29,6 +29,7 @@ precision "f32" (the reference's arithmetic): the fp32-faithful row kernel in sa
 P rows, then train.aggregate(saved=...) and fp32 autograd through the HIP loss stage.
 """
 import ctypes
+import gc
 import os
 
 import torch
@@ -731,8 +732,18 @@ class HipTrainer:
                     self._loss_body(st)
             torch.cuda.current_stream(dev).wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                st["out"] = self._loss_body(st)
+            # a garbage collection inside the capture would destroy dead objects that hold HIP resources (an
+            # earlier trainer's graphs, streams, events), which invalidates a global-mode capture: collect
+            # them first and keep the collector off until the capture ends
+            gc.collect()
+            gc_on = gc.isenabled()
+            gc.disable()
+            try:
+                with torch.cuda.graph(g):
+                    st["out"] = self._loss_body(st)
+            finally:
+                if gc_on:
+                    gc.enable()
             fl.grad.copy_(keep[0])
             P.points_conf.grad.copy_(keep[1])
             st["graph"] = g
