@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 13
+#define SGN_ABI_VERSION 14
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -379,6 +379,14 @@ int sgn_colsum_f16(int32_t count, const void *const *d_x, int64_t rows, int32_t 
  * dza^T h4 (point_aggregators.py:650-653, nn.Linear(256, 1)) in the bias sums' launch. */
 int sgn_colsum_f16_weighted(int32_t count, const void *const *d_x, const float *const *d_rw, int64_t rows,
                             int32_t cols, float *d_ws, float *d_out, sgn_stream_t stream);
+/* ABI 14: the same sums left as SGN_COLSUM_SLABS fixed row-slab partials in d_ws (one launch, no final
+ * pass), for sgn_grad_accumulate to add: column c of matrix i, slab b at
+ * d_ws[(i * SGN_COLSUM_SLABS + b) * 256 + c]; for weighted matrices the slab's sum of the row weights
+ * (the alpha branch's bias gradient sum(dza), point_aggregators.py:650-653) at
+ * d_ws[count * SGN_COLSUM_SLABS * 256 + i * SGN_COLSUM_SLABS + b]. */
+#define SGN_COLSUM_SLABS 512
+int sgn_colsum_f16_weighted_parts(int32_t count, const void *const *d_x, const float *const *d_rw, int64_t rows,
+                                  int32_t cols, float *d_ws, sgn_stream_t stream);
 
 /* ---- training: segment kernels (one launch for up to 16 segments) --------------------
  * The gradient epilogue of the training step's weight GEMMs, i.e. the accumulation torch

@@ -12,7 +12,8 @@ import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds 
 
 # SGN_HIP_LIB: another build of the same ABI (same-box A/B of kernel variants, tools/ab_lib.sh)
 LIB_PATH = os.environ.get("SGN_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
+COLSUM_SLABS = 512   # SGN_COLSUM_SLABS
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t)
@@ -146,6 +147,8 @@ SIGNATURES = {
     "sgn_colsum_f16": (c_i32, [c_i32, ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp, c_vp]),
     "sgn_colsum_f16_weighted": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp,
                                         c_vp]),
+    "sgn_colsum_f16_weighted_parts": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i64, c_i32, c_vp,
+                                              c_vp]),
     "sgn_grad_accumulate": (c_i32, [c_i32, ctypes.POINTER(GradSegment), c_vp, c_vp, c_vp]),
     "sgn_zero_segments": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),
     "sgn_copy_segments": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_vp]),

@@ -119,23 +119,25 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 
 constexpr int kMaxColsumMats = 8;
 constexpr int kColsumCols = 256;    // columns per tile (the MLP width)
-constexpr int kColsumSlabs = 512;   // row slabs (workgroups) per matrix
+constexpr int kColsumSlabs = SGN_COLSUM_SLABS;   // row slabs (workgroups) per matrix
 
 struct ColsumArgs {
     const __half *x[kMaxColsumMats];
     const float *rw[kMaxColsumMats];   // per-row weights (null: 1)
     int64_t rows, slab;   // rows per slab
-    float *ws;            // [count][kColsumSlabs][256]
-    float *out;           // [count][256]
+    int count;
+    float *ws;            // [count][kColsumSlabs][256], then [count][kColsumSlabs] row-weight sums
+    float *out;           // [count][256] (null: partials only)
 };
 
 template <bool W>
 __device__ __forceinline__ void colsum_rows(const __half *x, const float *rw, int64_t r, int64_t r1, int c8,
-                                            float (&acc)[8]) {
+                                            float (&acc)[8], float &wsum) {
 #pragma unroll 2
     for (; r < r1; r += 8) {
         const uint4 w = *reinterpret_cast<const uint4 *>(x + r * kColsumCols + c8 * 8);
         const float s = W ? rw[r] : 1.f;
+        if (W) wsum += s;
         const __half2 *h = reinterpret_cast<const __half2 *>(&w);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -160,18 +162,27 @@ __global__ __launch_bounds__(256) void k_colsum_part(ColsumArgs a) {
     const __half *x = a.x[mat];
     const float *rw = a.rw[mat];
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float wsum = 0.f;   // this thread's rows' weights (every c8 lane of a row group holds the same)
     if (rw)   // workgroup-uniform: two loops, no branch inside
-        colsum_rows<true>(x, rw, r0 + r8, r1, c8, acc);
+        colsum_rows<true>(x, rw, r0 + r8, r1, c8, acc, wsum);
     else
-        colsum_rows<false>(x, rw, r0 + r8, r1, c8, acc);
+        colsum_rows<false>(x, rw, r0 + r8, r1, c8, acc, wsum);
     __shared__ float red[8][kColsumCols];
+    __shared__ float wred[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[r8][c8 * 8 + j] = acc[j];
+    if (c8 == 0) wred[r8] = wsum;
     __syncthreads();
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += red[k][threadIdx.x];
     a.ws[((int64_t)mat * kColsumSlabs + blockIdx.x) * kColsumCols + threadIdx.x] = s;
+    if (rw && threadIdx.x == 0) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += wred[k];
+        a.ws[(int64_t)a.count * kColsumSlabs * kColsumCols + (int64_t)mat * kColsumSlabs + blockIdx.x] = t;
+    }
 }
 
 // grid (count), 256 threads: the slabs summed in slab order
@@ -186,11 +197,13 @@ __global__ __launch_bounds__(256) void k_colsum_final(ColsumArgs a) {
 // ---- segment kernels: the step's small gathers / clears / gradient epilogues, one launch each
 // (grid.y = segment).  Replace ~40 per-tensor torch launches of the training step.
 constexpr int kMaxSegs = 16;
+constexpr int32_t kGradPer = 32;   // partials per group of k_grad_accumulate (its float atomics)
 
 struct GradArgs {
     sgn_grad_segment s[kMaxSegs];
     const float *scale;   // device loss scale (power of two) or null
     float *grad;
+    int32_t per;          // partials per group (at least kGradPer)
 };
 
 __device__ __forceinline__ bool grad_seg_vec4(const sgn_grad_segment &g) {
@@ -212,7 +225,7 @@ __device__ __forceinline__ void grad_add(float *p, float v, bool atomic) {
 // element).  Four consecutive elements per thread (16-B loads) when the segment allows it.
 __global__ __launch_bounds__(256) void k_grad_accumulate(GradArgs a) {
     const sgn_grad_segment &g = a.s[blockIdx.y];
-    const int32_t per = (g.nb + (int32_t)gridDim.z - 1) / (int32_t)gridDim.z;
+    const int32_t per = max(a.per, (g.nb + (int32_t)gridDim.z - 1) / (int32_t)gridDim.z);
     const int32_t b0 = (int32_t)blockIdx.z * per, b1 = min(g.nb, b0 + per);
     if (b0 >= b1) return;
     const bool atomic = gridDim.z > 1;
@@ -574,7 +587,7 @@ int sgn_adam_step(float *d_param, float *d_grad, float *d_exp_avg, float *d_exp_
 }
 
 size_t sgn_colsum_workspace_bytes(int32_t count) {
-    return (size_t)std::max(count, 0) * kColsumSlabs * kColsumCols * sizeof(float);
+    return (size_t)std::max(count, 0) * kColsumSlabs * (kColsumCols + 1) * sizeof(float);
 }
 
 int sgn_colsum_f16(int32_t count, const void *const *d_x, int64_t rows, int32_t cols, float *d_ws, float *d_out,
@@ -582,12 +595,13 @@ int sgn_colsum_f16(int32_t count, const void *const *d_x, int64_t rows, int32_t 
     return sgn_colsum_f16_weighted(count, d_x, nullptr, rows, cols, d_ws, d_out, stream);
 }
 
-int sgn_colsum_f16_weighted(int32_t count, const void *const *d_x, const float *const *d_rw, int64_t rows, int32_t cols,
-                            float *d_ws, float *d_out, sgn_stream_t stream) {
+namespace {
+int colsum_launch(int32_t count, const void *const *d_x, const float *const *d_rw, int64_t rows, int32_t cols,
+                  float *d_ws, float *d_out, sgn_stream_t stream) {
     SGN_REQUIRE(count >= 1 && count <= kMaxColsumMats, "sgn_colsum_f16: 1 <= count <= 8");
     SGN_REQUIRE(cols == kColsumCols, "sgn_colsum_f16: cols must be 256");
     SGN_REQUIRE(rows >= 0, "sgn_colsum_f16: rows < 0");
-    SGN_REQUIRE(d_x && d_ws && d_out, "sgn_colsum_f16: null buffer");
+    SGN_REQUIRE(d_x && d_ws, "sgn_colsum_f16: null buffer");
     ColsumArgs a;
     for (int i = 0; i < count; ++i) {
         SGN_REQUIRE(d_x[i] != nullptr, "sgn_colsum_f16: null matrix");
@@ -597,13 +611,28 @@ int sgn_colsum_f16_weighted(int32_t count, const void *const *d_x, const float *
     }
     a.rows = rows;
     a.slab = (rows + kColsumSlabs - 1) / kColsumSlabs;
+    a.count = count;
     a.ws = d_ws;
     a.out = d_out;
     hipLaunchKernelGGL(k_colsum_part, dim3(kColsumSlabs, count), dim3(256), 0, as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_colsum_final, dim3(count), dim3(256), 0, as_stream(stream), a);
-    SGN_CHECK_HIP(hipGetLastError());
+    if (d_out) {
+        hipLaunchKernelGGL(k_colsum_final, dim3(count), dim3(256), 0, as_stream(stream), a);
+        SGN_CHECK_HIP(hipGetLastError());
+    }
     return 0;
+}
+}  // namespace
+
+int sgn_colsum_f16_weighted(int32_t count, const void *const *d_x, const float *const *d_rw, int64_t rows, int32_t cols,
+                            float *d_ws, float *d_out, sgn_stream_t stream) {
+    SGN_REQUIRE(d_out, "sgn_colsum_f16: null output");
+    return colsum_launch(count, d_x, d_rw, rows, cols, d_ws, d_out, stream);
+}
+
+int sgn_colsum_f16_weighted_parts(int32_t count, const void *const *d_x, const float *const *d_rw, int64_t rows,
+                                  int32_t cols, float *d_ws, sgn_stream_t stream) {
+    return colsum_launch(count, d_x, d_rw, rows, cols, d_ws, nullptr, stream);
 }
 
 int sgn_grad_accumulate(int32_t n_seg, const sgn_grad_segment *segs, const float *d_scale, float *d_grad,
@@ -629,8 +658,10 @@ int sgn_grad_accumulate(int32_t n_seg, const sgn_grad_segment *segs, const float
     SGN_REQUIRE(umax <= (int64_t)256 * 0x7fffffff, "sgn_grad_accumulate: segment too long");
     a.scale = d_scale;
     a.grad = d_grad;
-    // partial groups: ~16 partials per group, at most 32 groups (one group: deterministic order)
-    const int groups = std::min(32, std::max(1, (nbmax + 15) / 16));
+    // partial groups of at least kGradPer partials each, at most 32 groups (one group: deterministic order);
+    // a segment with fewer partials than the largest uses fewer groups (fewer atomics), the rest exit
+    a.per = kGradPer;
+    const int groups = std::min(32, std::max(1, (nbmax + kGradPer - 1) / kGradPer));
     hipLaunchKernelGGL(k_grad_accumulate, dim3((unsigned)((umax + 255) / 256), n_seg, groups), dim3(256), 0,
                        as_stream(stream), a);
     SGN_CHECK_HIP(hipGetLastError());

@@ -809,15 +809,16 @@ class HipTrainer:
         rp = ((rows + 1023) // 1024) * 1024   # rows padded (the SG embedding gather's view)
         if not hasattr(self, "_dw_bufs"):
             self._dw_bufs = {}
-        # the alpha branch's dWa = dza^T h4 (row-weighted column sums); the row layers' bias gradients come
-        # with their weight gradients (sgn_f16_weight_grad's column sums)
-        if not hasattr(self, "_cs_out"):
+        # the alpha branch's dWa = dza^T h4 and dba = sum dza as row-slab partials (one launch; the final sums
+        # happen in the step's sgn_grad_accumulate); the row layers' bias gradients come with their weight
+        # gradients (sgn_f16_weight_grad's column sums)
+        if not hasattr(self, "_cs_ws"):
             self._cs_ws = torch.empty(int(L.sgn_colsum_workspace_bytes(1)) // 4, dtype=torch.float32,
                                       device=self.device)
-            self._cs_out = torch.empty(1, 256, dtype=torch.float32, device=self.device)
-        _lib.check(L.sgn_colsum_f16_weighted(1, (ctypes.c_void_p * 1)(self.h4.data_ptr()),
-                                             (ctypes.c_void_p * 1)(self.dza.data_ptr()), rows, 256, _lib.ptr(self._cs_ws),
-                                             _lib.ptr(self._cs_out), st), "sgn_colsum_f16_weighted")
+        _lib.check(L.sgn_colsum_f16_weighted_parts(1, (ctypes.c_void_p * 1)(self.h4.data_ptr()),
+                                                   (ctypes.c_void_p * 1)(self.dza.data_ptr()), rows, 256,
+                                                   _lib.ptr(self._cs_ws), st), "sgn_colsum_f16_weighted_parts")
+        ns = _lib.COLSUM_SLABS
         segs, keep = [], []
 
         def add(src, tail, dst):
@@ -857,8 +858,8 @@ class HipTrainer:
             dwa[self.inv_chain] = (off + torch.arange(256, device=self.device)).to(torch.int32)
             amaps = self._flat_maps["alpha_branch.0"] = (dwa, torch.full((1,), off + i, dtype=torch.int32,
                                                                         device=self.device))
-        add(self._cs_out[0], None, amaps[0])
-        add(self.dza[:rows].sum().reshape(1), None, amaps[1])
+        add(self._cs_ws[:ns * 256], None, amaps[0])         # [slabs][256] -> 256
+        add(self._cs_ws[ns * 256:ns * 257], None, amaps[1])  # [slabs] -> 1
         _lib.check(L.sgn_grad_accumulate(len(segs), (_lib.GradSegment * len(segs))(*segs), _lib.ptr(scale),
                                          _lib.ptr(g), st), "sgn_grad_accumulate")
 

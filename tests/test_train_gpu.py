@@ -380,6 +380,42 @@ def test_colsum_matches_torch_sum(rows):
     torch.testing.assert_close(outs[0], ref, rtol=1e-5, atol=1e-5 * max(rows, 1) ** 0.5)
 
 
+@pytest.mark.parametrize("rows", [0, 1, 777, 165_000])
+def test_colsum_weighted_parts(rows):
+    """sgn_colsum_f16_weighted_parts (the alpha branch's dza^T h4 and sum(dza) as row-slab partials):
+    the slabs summed equal a float64 weighted column sum / weight sum, and the weighted launch with a
+    final pass (sgn_colsum_f16_weighted) agrees with the slab sums; rows past `rows` (NaN here) are never
+    read."""
+    L = _lib.lib()
+    ns = _lib.COLSUM_SLABS
+    g = torch.Generator().manual_seed(rows + 5)
+    n = max(rows, 1) + 64
+    xs = [torch.randn(n, 256, generator=g).half() for _ in range(2)]
+    rws = [torch.randn(n, generator=g) for _ in range(2)]
+    for x, w in zip(xs, rws):
+        x[rows:] = float("nan")
+        w[rows:] = float("nan")
+    xd, wd = [x.to(DEV) for x in xs], [w.to(DEV) for w in rws]
+    ws = torch.full((int(L.sgn_colsum_workspace_bytes(2)) // 4,), float("nan"), device=DEV)
+    assert ws.numel() == 2 * ns * 257
+    xp = (ctypes.c_void_p * 2)(*(x.data_ptr() for x in xd))
+    wp = (ctypes.c_void_p * 2)(wd[0].data_ptr(), None)   # the second matrix unweighted
+    _lib.check(L.sgn_colsum_f16_weighted_parts(2, xp, wp, rows, 256, _lib.ptr(ws), _lib.stream_handle()),
+               "sgn_colsum_f16_weighted_parts")
+    cols = ws[:2 * ns * 256].view(2, ns, 256).double().sum(1).cpu()
+    wsum = ws[2 * ns * 256:2 * ns * 256 + ns].double().sum().cpu()
+    r0 = (xs[0][:rows].double() * rws[0][:rows].double()[:, None]).sum(0)
+    r1 = xs[1][:rows].double().sum(0)
+    tol = 1e-5 * max(rows, 1) ** 0.5
+    torch.testing.assert_close(cols[0], r0, rtol=1e-5, atol=tol)
+    torch.testing.assert_close(cols[1], r1, rtol=1e-5, atol=tol)
+    torch.testing.assert_close(wsum, rws[0][:rows].double().sum(), rtol=1e-5, atol=tol)
+    out = torch.empty(2, 256, device=DEV)
+    _lib.check(L.sgn_colsum_f16_weighted(2, xp, wp, rows, 256, _lib.ptr(ws), _lib.ptr(out), _lib.stream_handle()),
+               "sgn_colsum_f16_weighted")
+    torch.testing.assert_close(out.double().cpu(), cols, rtol=1e-5, atol=tol)   # fp32 vs float64 slab sums
+
+
 def test_graph_captured_step_matches_eager_step():
     """The loss stage replayed as a HIP graph over padded capacity (HipTrainer.use_graph) gives
     the eager step's loss, gradients and, over three steps with Adam, parameters: padding items
