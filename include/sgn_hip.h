@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 14
+#define SGN_ABI_VERSION 15
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -322,8 +322,9 @@ int sgn_train_pack_index(int32_t *out, int64_t n);
  * which 0: [256] chain order -> unit, 1: [288] -> block1.0 input, 2: [272] -> block3.0 input. */
 int sgn_train_colmap(int32_t which, int32_t *out, int32_t n);
 /* Backward for n_items work items: d_dfs f32 [n_items][256], d_dalpha f32 [n_items] (d loss
- * w.r.t. the blended features / alpha), d_scale: device scalar loss scale. */
-int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, int32_t n_items,
+ * w.r.t. the blended features / alpha), d_scale: device scalar loss scale.  K (ABI 15): neighbours
+ * per sample of q->pidx, 1 .. 8, as in the forward. */
+int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, int32_t n_items, int32_t K,
                            const void *d_packed_mlp, const void *d_tblob, const sgn_agg_saved *saved,
                            const float *d_dfs, const float *d_dalpha, const float *d_scale,
                            const sgn_agg_deltas *deltas, const sgn_point_grads *grads,
@@ -343,7 +344,8 @@ int sgn_aggregate_train_fwd_sg(int32_t bpnet_layers, int32_t bpnet_dim, const vo
                                const void *d_packed_mlp, float *d_out_feat, void *d_fs, const sgn_agg_saved *saved,
                                void *d_h2b, sgn_stream_t stream);
 int sgn_aggregate_backward_sg(int32_t bpnet_layers, int32_t bpnet_dim, const sgn_point_tables *pt,
-                              const sgn_query_out *q, int32_t n_items, const void *d_packed_mlp, const void *d_tblob,
+                              const sgn_query_out *q, int32_t n_items, int32_t K, const void *d_packed_mlp,
+                              const void *d_tblob,
                               const sgn_agg_saved *saved, const void *d_h2b, const float *d_dfs, const float *d_dalpha,
                               const float *d_scale, const sgn_agg_deltas *deltas, void *d_db,
                               const sgn_point_grads *grads, sgn_stream_t stream);

@@ -12,7 +12,7 @@ import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds 
 
 # SGN_HIP_LIB: another build of the same ABI (same-box A/B of kernel variants, tools/ab_lib.sh)
 LIB_PATH = os.environ.get("SGN_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 COLSUM_SLABS = 512   # SGN_COLSUM_SLABS
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
@@ -127,13 +127,13 @@ SIGNATURES = {
     "sgn_mlp_pack_index": (c_i32, [c_i32, ctypes.POINTER(c_i32), c_i64]),
     "sgn_train_pack_index": (c_i32, [ctypes.POINTER(c_i32), c_i64]),
     "sgn_train_colmap": (c_i32, [c_i32, ctypes.POINTER(c_i32), c_i32]),
-    "sgn_aggregate_backward": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_vp, c_vp,
+    "sgn_aggregate_backward": (c_i32, [ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32, c_i32, c_vp, c_vp,
                                        ctypes.POINTER(AggSaved), c_vp, c_vp, c_vp, ctypes.POINTER(AggDeltas),
                                        ctypes.POINTER(PointGrads), c_vp]),
     "sgn_aggregate_train_fwd_sg": (c_i32, [c_i32, c_i32, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut),
                                            c_i64, c_i32, c_vp, c_vp, c_vp, ctypes.POINTER(AggSaved), c_vp, c_vp]),
     "sgn_aggregate_backward_sg": (c_i32, [c_i32, c_i32, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i32,
-                                          c_vp, c_vp, ctypes.POINTER(AggSaved), c_vp, c_vp, c_vp, c_vp,
+                                          c_i32, c_vp, c_vp, ctypes.POINTER(AggSaved), c_vp, c_vp, c_vp, c_vp,
                                           ctypes.POINTER(AggDeltas), c_vp, ctypes.POINTER(PointGrads), c_vp]),
     "sgn_train_pack_t_sg": (c_i32, [ctypes.POINTER(c_vp), c_i32, c_vp, c_vp]),
     "sgn_mlp_pack_index_sg": (c_i32, [c_i32, c_i32, c_i32, ctypes.POINTER(c_i32), c_i64]),

@@ -119,8 +119,8 @@ struct AggArgs {
     float *z1, *z2, *z3, *zb;
     // with row_off (sgn_train_lists): the rows are compact instead, row_off[s] + k
     const int32_t *row_off;
-    // neighbours per sample of the query's pidx (fp32 kernels: 1..8; a row-table entry s * 8 + k
-    // names pidx index s * K + k)
+    // neighbours per sample of the query's pidx (1..8): a sample's row k < K reads pidx index s * K + k,
+    // rows k >= K are empty (fp32 kernels: a row-table entry s * 8 + k names pidx index s * K + k)
     int32_t K;
 };
 
@@ -268,7 +268,7 @@ __device__ __forceinline__ RowIdx row_index(const AggArgs &a, int item, int end,
     RowIdx x;
     x.sval = item < end;
     x.s = x.sval ? a.work[item] : 0;
-    x.pid = x.sval ? a.pidx[(int64_t)x.s * 8 + (lane & 7)] : -1;
+    x.pid = x.sval && (lane & 7) < a.K ? a.pidx[(int64_t)x.s * a.K + (lane & 7)] : -1;
     x.ray = x.sval ? a.samp_ray[x.s] : 0;  // no sample id to follow without a work item
     return x;
 }
@@ -340,8 +340,8 @@ __device__ __forceinline__ RowIn gather_row_impl(const AggArgs &a, const Cam &ca
     w = w / fmaxf(wsum, 1e-8f);
     ri.wn = w;
     ri.wgt = w * fminf(fmaxf(cf, 1e-4f), 1.f);
-    if (a.blend && ri.sval && h == 0) a.blend[(int64_t)s * 8 + kk] = ri.wgt;
-    if (a.wnorm && ri.sval && h == 1) a.wnorm[(int64_t)s * 8 + kk] = w;
+    if (a.blend && ri.sval && h == 0 && kk < a.K) a.blend[(int64_t)s * a.K + kk] = ri.wgt;
+    if (a.wnorm && ri.sval && h == 1 && kk < a.K) a.wnorm[(int64_t)s * a.K + kk] = w;
     // block3 extra channels: colour, dir - v, <dir, v> (:639-652), lane-half 0 only
     if constexpr (F32EXT) {
         const bool e = h == 0 && m;

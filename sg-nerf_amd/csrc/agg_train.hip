@@ -505,13 +505,14 @@ int sgn_train_colmap(int32_t which, int32_t *out, int32_t n) {
     return 0;
 }
 
-int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, int32_t n_items,
+int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, int32_t n_items, int32_t K,
                            const void *d_packed, const void *d_tblob, const sgn_agg_saved *saved,
                            const float *d_dfs, const float *d_dalpha, const float *d_scale,
                            const sgn_agg_deltas *deltas, const sgn_point_grads *grads, sgn_stream_t stream) {
     using namespace sgn;
     SGN_REQUIRE(pt && q && d_packed && d_tblob && saved && deltas && grads && d_scale, "null argument");
     SGN_REQUIRE(n_items >= 0, "n_items < 0");
+    SGN_REQUIRE(K >= 1 && K <= 8, "the MFMA aggregator takes K = 1 .. 8 neighbours per sample");
     SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
     if (n_items == 0) return 0;
     SGN_REQUIRE(d_dfs && d_dalpha && saved->h1 && saved->h2 && saved->h3, "null saved/input tensors");
@@ -524,6 +525,7 @@ int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, i
     a.pers = nullptr; a.samp_pers = nullptr;
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
+    a.K = K;
     a.blob = d_packed; a.blob_bytes = mlp::TOTAL_BYTES;
     a.blend = nullptr; a.wnorm = nullptr;
     b.tblob = d_tblob;
@@ -542,18 +544,20 @@ int sgn_aggregate_backward(const sgn_point_tables *pt, const sgn_query_out *q, i
 }
 
 int sgn_aggregate_backward_sg(int32_t bpnet_layers, int32_t bpnet_dim, const sgn_point_tables *pt,
-                              const sgn_query_out *q, int32_t n_items, const void *d_packed, const void *d_tblob,
+                              const sgn_query_out *q, int32_t n_items, int32_t K, const void *d_packed,
+                              const void *d_tblob,
                               const sgn_agg_saved *saved, const void *d_h2b, const float *d_dfs, const float *d_dalpha,
                               const float *d_scale, const sgn_agg_deltas *deltas, void *d_db,
                               const sgn_point_grads *grads, sgn_stream_t stream) {
     using namespace sgn;
     if (bpnet_layers == 0)
-        return sgn_aggregate_backward(pt, q, n_items, d_packed, d_tblob, saved, d_dfs, d_dalpha, d_scale, deltas, grads,
-                                      stream);
+        return sgn_aggregate_backward(pt, q, n_items, K, d_packed, d_tblob, saved, d_dfs, d_dalpha, d_scale, deltas,
+                                      grads, stream);
     SGN_REQUIRE(bpnet_layers == 1 && (bpnet_dim == 0 || bpnet_dim == mlp::BP_DIM),
                 "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
     SGN_REQUIRE(pt && q && d_packed && d_tblob && saved && deltas && grads && d_scale && d_h2b && d_db, "null argument");
     SGN_REQUIRE(n_items >= 0, "n_items < 0");
+    SGN_REQUIRE(K >= 1 && K <= 8, "the MFMA aggregator takes K = 1 .. 8 neighbours per sample");
     SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
     if (n_items == 0) return 0;
     SGN_REQUIRE(d_dfs && d_dalpha && saved->h1 && saved->h2 && saved->h3, "null saved/input tensors");
@@ -566,6 +570,7 @@ int sgn_aggregate_backward_sg(int32_t bpnet_layers, int32_t bpnet_dim, const sgn
     a.pers = nullptr; a.samp_pers = nullptr;
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
+    a.K = K;
     a.blob = d_packed; a.blob_bytes = mlp::total_bytes_sg(mlp::ks_bp(bpnet_dim));
     a.blend = nullptr; a.wnorm = nullptr;
     b.tblob = d_tblob;

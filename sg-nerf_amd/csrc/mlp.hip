@@ -446,7 +446,7 @@ __global__ __launch_bounds__(ROWS_TPB, 1) void k_agg_rows(AggArgs a) {
         run_pass<V, 2, 0>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
         nx.sval = nitem < end;
         nx.s = s_next;
-        nx.pid = nx.sval ? a.pidx[(int64_t)s_next * 8 + kk] : -1;
+        nx.pid = nx.sval && kk < a.K ? a.pidx[(int64_t)s_next * a.K + kk] : -1;
         nx.ray = a.samp_ray[s_next];
         chain_out<4, 0>(acc, out3);
         run_pass<V, 2, 1>(wb, ldsi, slot, w, lane, lz, Fl, F_B2, acc, in3f);
@@ -956,7 +956,7 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
     const int ksb = mlp_variant_ksb(bpnet_layers, bpnet_dim);
     SGN_REQUIRE(ksb >= 0, "block2_bpnet: supported are 0 layers, or 1 layer with bpnet_dim 0 or 96");
     SGN_REQUIRE(ksb <= KS_HID || d_bpnet_f16, "bpnet_dim > 0 needs the fp16 BPNet point embedding");
-    SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
+    SGN_REQUIRE(K >= 1 && K <= 8, "the MFMA aggregator takes K = 1 .. 8 neighbours per sample");
     hipStream_t st = as_stream(stream);
     const int64_t ws_items = (int64_t)(workspace_bytes / (HID * sizeof(_Float16)));
     SGN_REQUIRE(ws_items >= 32, "aggregate workspace too small");
@@ -974,6 +974,7 @@ int sgn_aggregate_sg(int32_t bpnet_layers, int32_t bpnet_dim, const void *d_bpne
     SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir, "camera (campos, camrotc2w, raydir) required");
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
+    a.K = K;
     a.blob = P;
     a.blob_bytes = total_bytes_sg(ksb);
     a.bpnet = (const _Float16 *)d_bpnet_f16;
@@ -1014,7 +1015,7 @@ int sgn_aggregate_train_fwd(const sgn_point_tables *pt, const sgn_query_out *q, 
     using namespace sgn::mlp;
     SGN_REQUIRE(pt && q && d_packed && d_out_feat && d_fs && saved, "null argument");
     SGN_REQUIRE(saved->x0 && saved->h1 && saved->h2 && saved->h3, "null saved-activation buffer");
-    SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
+    SGN_REQUIRE(K >= 1 && K <= 8, "the MFMA aggregator takes K = 1 .. 8 neighbours per sample");
     SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
     SGN_REQUIRE(S_capacity >= 0 && S_capacity < (1 << 27), "S_capacity out of range");
     if (S_capacity == 0) return 0;
@@ -1023,6 +1024,7 @@ int sgn_aggregate_train_fwd(const sgn_point_tables *pt, const sgn_query_out *q, 
     a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
+    a.K = K;
     a.blob = d_packed; a.blob_bytes = TOTAL_BYTES;
     a.feat = d_out_feat; a.fs = (_Float16 *)d_fs;
     a.item0 = 0; a.n_items = (int32_t)S_capacity;
@@ -1048,7 +1050,7 @@ int sgn_aggregate_train_fwd_sg(int32_t bpnet_layers, int32_t bpnet_dim, const vo
     SGN_REQUIRE(saved->x0 && saved->h1 && saved->h2 && saved->h3, "null saved-activation buffer");
     SGN_REQUIRE(ksb <= KS_HID || (d_bpnet_f16 && ((uintptr_t)d_bpnet_f16 & 15) == 0),
                 "bpnet_dim > 0 needs the 16-byte aligned fp16 BPNet point embedding");
-    SGN_REQUIRE(K == 8, "the MFMA aggregator is built for K = 8 neighbours");
+    SGN_REQUIRE(K >= 1 && K <= 8, "the MFMA aggregator takes K = 1 .. 8 neighbours per sample");
     SGN_REQUIRE(pt->campos && pt->camrotc2w && pt->raydir && !pt->pers, "camera required, no precomputed pers");
     SGN_REQUIRE(S_capacity >= 0 && S_capacity < (1 << 27), "S_capacity out of range");
     if (S_capacity == 0) return 0;
@@ -1057,6 +1059,7 @@ int sgn_aggregate_train_fwd_sg(int32_t bpnet_layers, int32_t bpnet_dim, const vo
     a.campos = pt->campos; a.rot = pt->camrotc2w; a.raydir = pt->raydir;
     a.counters = q->counters; a.work = q->work; a.samp_ray = q->samp_ray; a.pidx = q->pidx;
     a.samp_locw = q->samp_locw;
+    a.K = K;
     a.blob = d_packed; a.blob_bytes = total_bytes_sg(ksb);
     a.bpnet = (const _Float16 *)d_bpnet_f16;
     a.feat = d_out_feat; a.fs = (_Float16 *)d_fs;

@@ -298,9 +298,8 @@ class PointAggregator:
         dev = self.device
         shp = sample_loc_w.shape[:-1]  # [1, R, SR]
         K = sample_pnt_mask.shape[-1]
-        if not (1 <= K <= 8) or (K != 8 and not self.f32):
-            raise NotImplementedError("the MFMA aggregator takes K = 1 .. 8 neighbours at precision f32, "
-                                      "K = 8 at f16")
+        if not (1 <= K <= 8):
+            raise NotImplementedError("the MFMA aggregator takes K = 1 .. 8 neighbours")
         S = int(torch.tensor(shp).prod().item())
         f = lambda t, c: t.reshape(-1, c).to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
         mask = sample_pnt_mask.reshape(S, K).to(dev).bool()

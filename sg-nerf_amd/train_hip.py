@@ -523,6 +523,7 @@ class HipTrainer:
         else:
             sync = q.counters[:2]
         S, n, *t_counts = (int(x) for x in sync.tolist())  # one host sync per step
+        self._last_q = q
         graph = self.use_graph and dev.type == "cuda"
         if graph:
             self._buffers(R * o.SR, R * o.SR)   # static shapes: every buffer at the batch's capacity
@@ -575,13 +576,13 @@ class HipTrainer:
             grads = _lib.PointGrads(P.points_embeding.grad.data_ptr(), P.points_color.grad.data_ptr(),
                                     P.points_dir.grad.data_ptr(), P.points_conf.grad.data_ptr())
             if self.sg:
-                _lib.check(L.sgn_aggregate_backward_sg(*self.variant, ctypes.byref(pt), ctypes.byref(qo), n,
+                _lib.check(L.sgn_aggregate_backward_sg(*self.variant, ctypes.byref(pt), ctypes.byref(qo), n, o.K,
                                                        _lib.ptr(blob), _lib.ptr(tblob), ctypes.byref(saved),
                                                        _lib.ptr(self.h2b), _lib.ptr(dfs), _lib.ptr(dal),
                                                        _lib.ptr(scale), ctypes.byref(deltas), _lib.ptr(self.db),
                                                        ctypes.byref(grads), st), "sgn_aggregate_backward_sg")
             else:
-                _lib.check(L.sgn_aggregate_backward(ctypes.byref(pt), ctypes.byref(qo), n, _lib.ptr(blob),
+                _lib.check(L.sgn_aggregate_backward(ctypes.byref(pt), ctypes.byref(qo), n, o.K, _lib.ptr(blob),
                                                     _lib.ptr(tblob), ctypes.byref(saved), _lib.ptr(dfs), _lib.ptr(dal),
                                                     _lib.ptr(scale), ctypes.byref(deltas), ctypes.byref(grads), st),
                            "sgn_aggregate_backward")

@@ -58,9 +58,9 @@ def test_argument_errors_are_reported_without_gpu():
     pt, qo = _lib.PointTables(), _lib.QueryOut()
     for f in ("xyz", "embedding", "color", "dir", "conf", "campos", "camrotc2w", "raydir"):
         setattr(pt, f, 16)
-    rc = L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), 64, 4, fake, fake, None, None, fake, 1 << 20, 3, None)
-    assert rc != 0 and b"K = 8" in L.sgn_last_error()
-    with pytest.raises(_lib.SgnError, match="K = 8"):
+    rc = L.sgn_aggregate(ctypes.byref(pt), ctypes.byref(qo), 64, 9, fake, fake, None, None, fake, 1 << 20, 3, None)
+    assert rc != 0 and b"K = 1 .. 8" in L.sgn_last_error()
+    with pytest.raises(_lib.SgnError, match="K = 1 .. 8"):
         _lib.check(rc, "sgn_aggregate")
     cp = _lib.CompositeParams()
     cp.SR = 0

@@ -115,13 +115,16 @@ def test_render_matches_oracle_room(SR, seed, yaw, alpha_bias, prec):
     assert int(mask.sum()) > 0.5 * mask.numel()
 
 
+@pytest.mark.parametrize("prec", ["f32", "f16"])
 @pytest.mark.parametrize("K,alpha_bias", [(4, 0.0), (4, 150.0), (1, 0.0)])
-def test_render_matches_oracle_room_small_k(K, alpha_bias):
+def test_render_matches_oracle_room_small_k(K, alpha_bias, prec):
     """K < 8 neighbours per sample (PointAggregator takes any K, point_aggregators.py:868-959; the
-    query supports 1 / 4 / 8 / 16) on the fp32 path: rows of a sample are its K slots, pidx
-    index s * K + k.  Same bars as K = 8, plus the per-slot blend weights against the oracle's."""
+    query supports 1 / 4 / 8 / 16): a sample's rows k < K read pidx index s * K + k, rows k >= K are
+    empty.  Same bars per precision as K = 8, and the per-slot blend weights (weight * conf) against
+    the oracle's query."""
     pc = small_room(300_000, seed=5)
-    o = HotPathOpts(SR=32, K=K, precision="f32")
+    o = HotPathOpts(SR=32, K=K, precision=prec)
+    rgb_tol, feat_tol = TOL[prec]
     mlp = init_mlp(5, bias_std=0.01)
     mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + alpha_bias
     view = make_view(48, 64, yaw=60.0, pitch=-8.0)
@@ -139,9 +142,20 @@ def test_render_matches_oracle_room_small_k(K, alpha_bias):
     err = np.abs(out.rgb.cpu().numpy() - full.numpy()).max()
     dense = _dense_feat(out, view.raydir.shape[0], o.SR)[0]
     ferr = (np.abs(dense - fd.numpy()) / np.maximum(1.0, np.abs(fd.numpy()))).max()
-    print(f"room K={K} alpha_bias={alpha_bias} [f32]: max |rgb - oracle| = {err:.3e}, max feature error {ferr:.3e}")
-    assert err <= F32_TOL and ferr <= F32_TOL
+    print(f"room K={K} alpha_bias={alpha_bias} [{prec}]: max |rgb - oracle| = {err:.3e}, max feature error {ferr:.3e}")
+    assert err <= rgb_tol and ferr <= feat_tol
     assert int(mask.sum()) > 0.5 * mask.numel()
+    # blend weights per (sample, slot): the oracle's linear-kernel weights x clamped conf
+    dense_b = np.zeros((view.raydir.shape[0], o.SR, K), np.float32)
+    _, sr, slot, valid = _dense_feat(out, view.raydir.shape[0], o.SR)
+    dense_b[sr[valid], slot[valid]] = out.blend[:len(valid)].cpu().numpy()[valid]
+    pid = q["pidx"]
+    d = pid >= 0
+    lw = np.linalg.norm(pc.xyz[np.maximum(pid, 0)] - q["loc_w"][..., None, :], axis=-1)
+    w = np.where(d, 1.0 / np.maximum(lw, 1e-6), 0.0)
+    w = w / np.maximum(w.sum(-1, keepdims=True), 1e-8)
+    ref_b = w * np.clip(pc.conf.reshape(-1)[np.maximum(pid, 0)], 1e-4, 1.0)
+    np.testing.assert_allclose(dense_b[mask.numpy()], ref_b[mask.numpy()], atol=1e-5, rtol=1e-4)
 
 
 @pytest.mark.parametrize("theta,alpha_bias", [(30.0, 0.0), (200.0, 150.0)])

@@ -175,6 +175,41 @@ def test_f32_training_matches_fp32_autograd_on_same_query(cfg):
 
 
 @pytest.mark.parametrize("K", [4, 1])
+def test_f16_training_small_k_matches_fp32_autograd(K):
+    """precision "f16" with K < 8 neighbours per sample (rows k < K of a sample read pidx index
+    s * K + k, rows k >= K are empty in the forward and the backward): every gradient within the
+    f16 bars (GRAD_TOL_MLP / GRAD_TOL_POINTS) of train.Trainer's fp32 autograd on the very samples
+    the HIP query produced; colour within the north-star 1e-3."""
+    o = dataclasses_replace(O, K=K)
+    pc, view, _, mlp, gt = _setup(seed=5)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    tr = HipTrainer(points, mlp, o, DEV, precision="f16")
+    parts, full, ray_mask = tr.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV))
+    qd = {k: v.long() if v.dtype == torch.int32 else v for k, v in tr.last_query.items()}
+    assert qd["pidx"].shape[1] == K
+    ref_points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    ref = Trainer(ref_points, mlp, o, DEV)
+    parts_c, full_c, mask_c = ref.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV),
+                                           q=qd)
+    torch.cuda.synchronize()
+    assert torch.equal(ray_mask, mask_c)
+    assert float((full - full_c).abs().max()) <= 1e-3
+    assert abs(float(parts["total"]) - float(parts_c["total"])) <= 1e-3 * abs(float(parts_c["total"]))
+    g = grads_named(tr)
+    worst = {}
+    for name, *_ in LAYERS:
+        m = ref.mlp.lin[name.replace(".", "_")]
+        worst[name + ".weight"] = _rel(g[name + ".weight"], m.weight.grad)
+        worst[name + ".bias"] = _rel(g[name + ".bias"], m.bias.grad)
+    for k in ("points_embeding", "points_color", "points_dir", "points_conf"):
+        worst[k] = _rel(g[k].reshape(getattr(ref_points, k).grad.shape), getattr(ref_points, k).grad)
+    print(f"K={K} [f16]: relative L2 gradient errors (same query):", {k: f"{v:.2e}" for k, v in worst.items()})
+    bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("K", [4, 1])
 def test_f32_training_small_k_matches_fp32_autograd(K):
     """precision "f32" with K < 8 neighbours per sample (saved pre-activations at pidx index
     s * K + k): every gradient within GRAD_TOL_F32 of train.Trainer's fp32 autograd on the very
