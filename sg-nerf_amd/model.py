@@ -354,12 +354,17 @@ class HipPointsVolumetricModel:
         self.top_ray_miss_loss = torch.zeros([self.num_probe + 1], dtype=torch.float32, device=self.device)
         self.top_ray_miss_ids = torch.arange(self.num_probe + 1, dtype=torch.int32, device=self.device)
 
-    def set_bg(self, xyz_world_sect_plane, img_lst, c2ws_lst, w2cs_lst, intrinsics_all, HDWD_lst, plane_color=None,
+    def set_bg(self, xyz_world_sect_plane, img_lst, c2ws_lst, w2cs_lst, intrinsics_all, HDWD_lst, plane_color,
                fg_masks=None, **kwargs):
-        """mvs_points_volumetric_model.py:305-343 warps source images onto a background plane for
-        bgmodel '*plane'.  That background model is outside the per-ray hot path: refuse it."""
-        raise NotImplementedError("set_bg: bgmodel '*plane' (image-warped plane background) is not part of the "
-                                  "HIP hot path; use bgmodel 'no' with a bg_color")
+        """mvs_points_volumetric_model.py:276-315 (bgmodel '*plane'): the rays' background colours from
+        the source images warped onto the plane (sgnerf_amd.plane_bg).  Returns (bg_ray [1,R,3],
+        fg_masks); the drivers put bg_ray into the input dict as 'bg_ray' (run/train_ft.py:209-218),
+        which the renderer blends as T_bg * bg_ray."""
+        from .plane_bg import plane_bg
+        if self.neural_points is None:
+            raise RuntimeError("set_bg: no neural points (its foreground masks project them)")
+        return plane_bg(xyz_world_sect_plane, img_lst, w2cs_lst, intrinsics_all, HDWD_lst, plane_color,
+                        self.neural_points.xyz, fg_masks=fg_masks)
 
     # -- semantic dumps (neural_points_volumetric_model.py:337-362, 674-720) ------------------
     def _semantic_dir(self):

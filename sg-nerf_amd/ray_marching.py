@@ -214,7 +214,9 @@ class NeuralPointsRayMarching:
         raydir = inputs["raydir"].reshape(-1, 3)
         near = _scalar(inputs["near"]) if "near" in inputs else self.opts.near_plane
         far = _scalar(inputs["far"]) if "far" in inputs else self.opts.far_plane
-        bg = _bg_tuple(inputs.get("bg_color"), self.opts)
+        # a per-ray background (bgmodel '*plane', set_bg) replaces the constant one: the composite runs
+        # without background (ray_march with bg_color None, neural_points_volumetric_model.py:311-312)
+        bg = (0.0, 0.0, 0.0) if inputs.get("bg_ray") is not None else _bg_tuple(inputs.get("bg_color"), self.opts)
         pl = rl = None
         if self.opts.semantic_guidance == 1:  # neural_points.py:771-785: labels of the points and of the rays
             if self.neural_points.points_label is None or inputs.get("pixel_label") is None:
@@ -240,8 +242,12 @@ class NeuralPointsRayMarching:
         """Expanded outputs (what fill_invalid(forward(inputs)) gives), no host sync.
         Fresh tensors, as the reference returns (the renderer's buffers are reused)."""
         out, R = self._render(inputs, self.return_weights)
+        rgb = out.rgb[None].clone()
+        if inputs.get("bg_ray") is not None:   # T_bg * bg_ray + colour (neural_points_volumetric_model.py:114-116)
+            bg_ray = torch.as_tensor(inputs["bg_ray"]).to(self.device, torch.float32).reshape(1, R, 3)
+            rgb.addcmul_(out.bg_transmission[None, :, None], bg_ray)
         res = {
-            "coarse_raycolor": out.rgb[None].clone(),
+            "coarse_raycolor": rgb,
             "coarse_point_opacity": out.opacity[None].clone(),
             "coarse_is_background": out.bg_transmission[None, :, None].clone(),
             "queried_shading": (1 - out.ray_mask.float())[None, :, None].expand(1, R, 3).contiguous(),

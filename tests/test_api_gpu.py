@@ -84,6 +84,35 @@ def test_ray_marching_black_background():
     torch.testing.assert_close(black["coarse_raycolor"][0] + T, white, atol=1e-6, rtol=0)
 
 
+@pytest.mark.parametrize("name", ["patch", "opq_patch"])
+def test_ray_marching_plane_background(name):
+    """inputs['bg_ray'] (bgmodel '*plane', set_bg): the per-ray background replaces bg_color,
+    coarse_raycolor = T_bg * bg_ray + colour (neural_points_volumetric_model.py:114-116): against the
+    same render with a black background plus T_bg * bg_ray, and a constant bg_ray against bg_color."""
+    pts, mlp, case = _load(name)
+    o = HotPathOpts(SR=int(case["SR"]), K=int(case["K"]))
+    net = NeuralPointsRayMarching(NeuralPoints(pts["xyz"], pts["embedding"], pts["color"], pts["dir"], pts["conf"],
+                                               DEV), mlp, o, DEV)
+    R = case["raydir"].shape[0]
+    black = net.render(_inputs(case, bg=(0.0, 0.0, 0.0)))
+    T = black["coarse_is_background"][0]
+    bg_ray = torch.rand(1, R, 3, generator=torch.Generator().manual_seed(7)).to(DEV)
+    inp = _inputs(case)
+    inp["bg_ray"] = bg_ray
+    out = net.render(inp)
+    assert torch.equal(out["ray_mask"], black["ray_mask"])
+    torch.testing.assert_close(out["coarse_raycolor"][0], black["coarse_raycolor"][0] + T * bg_ray[0], atol=1e-6,
+                               rtol=0)
+    miss = ~out["ray_mask"][0].bool()
+    if miss.any():   # rays without a sample show the background ray colour itself
+        torch.testing.assert_close(out["coarse_raycolor"][0][miss], bg_ray[0][miss], atol=0, rtol=0)
+    c = (0.25, 0.5, 0.75)
+    inp = _inputs(case, bg=(1.0, 1.0, 1.0))
+    inp["bg_ray"] = torch.tensor(c, device=DEV).expand(1, R, 3)
+    ref = net.render(_inputs(case, bg=c))["coarse_raycolor"]
+    torch.testing.assert_close(net.render(inp)["coarse_raycolor"], ref, atol=1e-6, rtol=0)
+
+
 def _gathered(pts, case):
     """NeuralPoints.forward gather (neural_points.py:942-988), test-side numpy."""
     pidx = case["sample_pidx"]

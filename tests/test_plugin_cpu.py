@@ -1,6 +1,6 @@
 """The model plugin's host-side surface on the CPU (no kernels run): checkpoint keys the
 reference's NeuralPoints reads, the train_ft.py save block and probe guard, the ray-miss
-ranking, the semantic point dumps and set_bg's refusal.
+ranking, the semantic point dumps and set_bg's plane background.
 
   run/train_ft.py:1006-1020   save block (saveSemanticEmbedding + save_networks in try/except)
   run/train_ft.py:888-891     probe guard (top_ray_miss_loss[0] > 1e-5 ...)
@@ -178,10 +178,88 @@ def test_semantic_point_dumps(tmp_path):
         m.saveSemanticPoints(1)
 
 
-def test_set_bg_refuses_plane_background(tmp_path):
+def _plane_bg_loops(campos, raydir, pnt, nrm, imgs, w2cs, Ks, plane_color, pts, thresh=0.03):
+    """Independent float64 restatement of set_bg (mvs_points_volumetric_model.py:276-315 over
+    mvs_utils.py:299-420) with explicit loops: per ray and view the plane point's projection, the
+    foreground test at its ceil'd pixel, a hand-written bilinear tap (align_corners, zero padding).
+    Returns bg [R,3] and, per (ray, view), the sampled colour's distance to the fit boundary."""
+    R, V = raydir.shape[0], len(imgs)
+    bg = np.zeros((R, 3))
+    margin = np.full((R, V), np.inf)
+    for v in range(V):
+        _, C, H, W = imgs[v].shape
+        w2c, K = w2cs[v][0, 0], Ks[v][0]
+
+        def proj(x):
+            c = w2c @ np.append(x, 1.0)
+            with np.errstate(divide="ignore", invalid="ignore"):   # z = 0: nan / inf, outside the image
+                return (K @ (c[:3] / c[2]))[:2]
+        fg = np.zeros((H, W), bool)
+        for x in pts:
+            u = proj(x)
+            if 0 <= u[0] <= W - 1 and 0 <= u[1] <= H - 1:
+                fg[int(np.ceil(u[1])), int(np.ceil(u[0]))] = True
+        for r in range(R):
+            d = raydir[r]
+            dot = nrm @ d
+            hit = campos + d * (-(nrm @ (campos - pnt)) / dot) if dot >= 1e-3 else np.zeros(3)
+            u = proj(hit)
+            if not (0 <= u[0] <= W - 1 and 0 <= u[1] <= H - 1) or fg[int(np.ceil(u[1])), int(np.ceil(u[0]))]:
+                s = np.zeros(3)
+            else:
+                x0, y0 = int(np.floor(u[0])), int(np.floor(u[1]))
+                fx, fy = u[0] - x0, u[1] - y0
+                s = np.zeros(3)
+                for (yy, xx, wt) in ((y0, x0, (1 - fx) * (1 - fy)), (y0, x0 + 1, fx * (1 - fy)),
+                                     (y0 + 1, x0, (1 - fx) * fy), (y0 + 1, x0 + 1, fx * fy)):
+                    if 0 <= yy < H and 0 <= xx < W:
+                        s = s + wt * imgs[v][0, :, yy, xx]
+            dist = np.abs(np.abs(s - plane_color) - thresh).min()
+            margin[r, v] = dist
+            if np.all(np.abs(s - plane_color) <= thresh):
+                bg[r] = np.maximum(bg[r], s)
+    return bg, margin
+
+
+def test_set_bg_plane_background_matches_loops(tmp_path):
+    """set_bg (bgmodel '*plane'): the rays' plane points warped into two source views, foreground
+    pixels (where neural points project) excluded, colours within 0.03 of the plane colour kept, max
+    over views -- against the explicit-loop restatement above (rays whose sampled colour sits within
+    1e-4 of the fit boundary are skipped: float32 vs float64 may decide them either way)."""
+    from sgnerf_amd.plane_bg import gen_bg_points
     m = _model(tmp_path)
-    with pytest.raises(NotImplementedError, match="plane"):
-        m.set_bg(None, [], [], [], [], [], plane_color=None)
+    g = np.random.default_rng(3)
+    H, W, pc = 12, 16, np.array([0.5, 0.4, 0.3])
+    imgs = []
+    for v in range(2):
+        im = pc[None, :, None, None] + g.uniform(-0.02, 0.02, (1, 3, H, W))
+        far = g.random((H, W)) < 0.3
+        im[0][:, far] = g.uniform(0, 1, (3, int(far.sum())))
+        imgs.append(im.astype(np.float32))
+    Ks = [np.array([[[8.0, 0, 7.5], [0, 8.0, 5.5], [0, 0, 1]]], np.float32)] * 2
+    w2cs = []
+    for t in ([0.1, -0.05, 0.0], [-0.15, 0.1, 0.2]):
+        e = np.eye(4, dtype=np.float32)
+        e[:3, 3] = -np.array(t, np.float32)
+        w2cs.append(e[None, None])
+    campos = np.zeros(3, np.float32)
+    d = np.stack([g.uniform(-0.8, 0.8, 60), g.uniform(-0.6, 0.6, 60), np.ones(60)], -1).astype(np.float32)
+    d[:3] = [[0.2, 0.1, -1.0], [0.0, 0.0, 1e-4], [1.5, 0.0, 1.0]]   # away from the plane, parallel, off-image
+    pnt, nrm = np.array([0.0, 0.0, 2.0], np.float32), np.array([0.0, 0.0, 1.0], np.float32)
+    pts = np.concatenate([g.uniform(-0.5, 0.5, (12, 2)), np.full((12, 1), 2.0)], -1).astype(np.float32)
+    m.neural_points.xyz = torch.from_numpy(pts)
+    batch = {"campos": torch.from_numpy(campos)[None], "raydir": torch.from_numpy(d)[None],
+             "plane_pnt": torch.from_numpy(pnt)[None], "plane_normal": torch.from_numpy(nrm)[None]}
+    xyz = gen_bg_points(batch)
+    bg, fgm = m.set_bg(xyz, [torch.from_numpy(i) for i in imgs], None, [torch.from_numpy(w) for w in w2cs],
+                       [torch.from_numpy(k) for k in Ks], [(H, W)] * 2, torch.from_numpy(pc.astype(np.float32)))
+    assert bg.shape == (1, 60, 3) and fgm is None
+    ref, margin = _plane_bg_loops(campos.astype(np.float64), d.astype(np.float64), pnt, nrm, imgs, w2cs, Ks, pc,
+                                  pts.astype(np.float64))
+    ok = margin.min(1) > 1e-4
+    assert ok.sum() >= 40 and (ref[ok].sum(1) > 0).sum() >= 10   # enough rays decided, some with a background
+    np.testing.assert_allclose(bg[0].numpy()[ok], ref[ok], atol=1e-5)
+    np.testing.assert_array_equal(bg[0, :3].numpy(), 0.0)   # behind the camera, parallel, off both images
 
 
 def test_set_points_reference_signature(tmp_path):
