@@ -243,6 +243,50 @@ __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int
     for (int j = 0; j < 8; ++j) o[j] = (_Float16)__builtin_fmaf(l[j], inv, -(float)h[j]);
     return X3B{h8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]}, h8{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]}};
 }''')
+    elif p == "v_early3":
+        # block3.2's input converted during block3.0's last k-step (the VALU-free ext k-step), tiles 2J, 2J + 1
+        # after tile 2J + 3's MFMAs, so block3.2's pass 0 runs without conversion VALU
+        s = rep(s, '''        auto &in2 = pick<(KB > 0)>(accA, accB);
+        auto &acc2 = pick<(KB > 0)>(accB, accA);
+        const float inv_in2 = KB > 0 ? inv7 : inv1;''', '''        auto &in2 = pick<(KB > 0)>(accA, accB);
+        auto &acc2 = pick<(KB > 0)>(accB, accA);
+        const float inv_in2 = KB > 0 ? inv7 : inv1;
+        X3B in3[NS][8];
+        constexpr int LASTK = (Net::L[L2].ks - 1) * 16;''')
+        s = rep(s, '''                    nx[q].ray = nx[q].sval ? a.samp_ray[nx[q].s] : 0;
+                }
+            }
+        });''', '''                    nx[q].ray = nx[q].sval ? a.samp_ray[nx[q].s] : 0;
+                }
+            }
+        }, NoHook{}, [&](auto f) {
+            constexpr int F = decltype(f)::value;
+            if constexpr (F >= LASTK + 3 && ((F - LASTK) & 1) == 1) {
+                constexpr int J = (F - LASTK - 3) / 2;
+#pragma unroll
+                for (int q = 0; q < NS; ++q) in3[q][J] = chain_k(q, acc2[q], inv2, std::integral_constant<int, J>{}, a.z3);
+            }
+        });
+#pragma unroll
+        for (int q = 0; q < NS; ++q) in3[q][7] = chain_k(q, acc2[q], inv2, std::integral_constant<int, 7>{}, a.z3);''')
+        s = rep(s, '''            X3B in3[NS][8];
+            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0, !SAVE>(
+                wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
+                    constexpr int K = decltype(k)::value;
+                    X3S<NS> o;
+#pragma unroll
+                    for (int q = 0; q < NS; ++q) {
+                        in3[q][K] = chain_k(q, acc2[q], inv2, k, a.z3);
+                        o.b[q] = in3[q][K];
+                    }
+                    return o;
+                }, NoHook{}, first_chunk_loads);''', '''            run_layer_ns<Net, L3, true, std::conditional_t<SAVE, VmZero, VmL3P0<NS>>, 0, 0>(
+                wb, ldsi, slot, w, lane, lz, acc, [&](auto k) {
+                    X3S<NS> o;
+#pragma unroll
+                    for (int q = 0; q < NS; ++q) o.b[q] = in3[q][decltype(k)::value];
+                    return o;
+                }, NoHook{}, first_chunk_loads);''')
     elif p == "v_epic":
         # the epilogue's per-lane constants (block3.2 bias and alpha weight of unit 16 T + r, T = 0..15) read
         # into registers once per tile (8 ds_read_b128, one wait) instead of one LDS read + wait per step
