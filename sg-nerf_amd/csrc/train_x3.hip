@@ -1047,6 +1047,9 @@ __global__ __launch_bounds__(TPB) void k_colour_head(RowArgs a, const float *h3,
 }
 
 constexpr int HEAD_BLOCKS = 256;
+// k_row_head's workgroups (its partials: [ROW_HEAD_BLOCKS][257], summed in order by k_reduce_partials, one
+// thread per element): 1024 took the head 132 -> 101 us but the reduce 43 -> 128 us per config-5 step
+constexpr int ROW_HEAD_BLOCKS = 256;
 
 // backward of k_colour_head: dy4 = d rgb 1.002 sig (1 - sig); dy3 = (W6^T dy4) LReLU'(h3); the
 // weight / bias gradient of color_branch.6 as one fixed-order partial per workgroup
@@ -1542,7 +1545,7 @@ int sgn_train_colour_head(const sgn_query_out *q, const int32_t *d_counts, const
 }
 
 size_t sgn_train_head_partial_floats(int32_t which) {
-    return (size_t)sgn::tx::HEAD_BLOCKS * (which == 0 ? 3 * 129 : 257);
+    return which == 0 ? (size_t)sgn::tx::HEAD_BLOCKS * 3 * 129 : (size_t)sgn::tx::ROW_HEAD_BLOCKS * 257;
 }
 
 int sgn_train_colour_head_bwd(const sgn_query_out *q, const int32_t *d_counts, const float *d_h3, const float *d_w6,
@@ -1570,7 +1573,7 @@ int sgn_train_row_head(const sgn_point_tables *pt, const sgn_query_out *q, int32
                 "null argument");
     SGN_REQUIRE(K >= 1 && K <= 8, "K = 1 .. 8");
     const RowArgs a = row_args(pt, q, K, d_row_off, d_counts);
-    hipLaunchKernelGGL(k_row_head, dim3(HEAD_BLOCKS), dim3(TPB), 0, as_stream(stream), a, d_z4_delta4, d_dfs,
+    hipLaunchKernelGGL(k_row_head, dim3(ROW_HEAD_BLOCKS), dim3(TPB), 0, as_stream(stream), a, d_z4_delta4, d_dfs,
                        (const float4 *)d_dfeat, (const float2 *)d_rw, d_wa, d_ba, d_gconf, d_amax, d_part);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
