@@ -243,6 +243,77 @@ __device__ __forceinline__ void dma_piece(const WBlob &wb, char *dst, int w, int
     for (int j = 0; j < 8; ++j) o[j] = (_Float16)__builtin_fmaf(l[j], inv, -(float)h[j]);
     return X3B{h8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]}, h8{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]}};
 }''')
+    elif p == "v_early":
+        # chunk start before the barrier: every wave LDS-DMAs its own copy of the chunk's first fragment pair
+        # (pieces 0 and 1, identical bytes to the same LDS address), so after its own vmcnt wait it can read
+        # pair 0 and issue that pair's MFMAs; the workgroup barrier follows them (its wait overlaps the MFMAs)
+        s = rep(s, '''// LDS-DMA of stream chunk N into `dst`: 2 * pairs 1-KiB pieces, wave w (of NWv) moves pieces''', '''// piece p (0 or 1) of chunk N by any wave: the chunk's first fragment pair, duplicated per wave
+template <class Net, int N, int P>
+__device__ __forceinline__ void dma_dup(const WBlob &wb, char *dst, int lane) {
+    uint32_t soff = Sched<Net>::off(N) + (uint32_t)(P * 1024);
+    asm volatile("" : "+s"(soff));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wb.rsrc, (__attribute__((address_space(3))) void *)(dst + P * 1024), 16,
+                                             lane * 16, soff, 0, 0);
+}
+// LDS-DMA of stream chunk N into `dst`: 2 * pairs 1-KiB pieces, wave w (of NWv) moves pieces''')
+        s = rep(s, '''    static_assert(VM >= 0 && VM < 64, "vmcnt range");
+    if constexpr (VM == 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else  // vmcnt[3:0] | expcnt 7 | lgkmcnt 15 | vmcnt[5:4] << 14 (gfx9 encoding: wait on vmcnt only)
+        __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}''', '''    static_assert(VM >= 0 && VM < 64, "vmcnt range");
+    if constexpr (VM == 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else  // vmcnt[3:0] | expcnt 7 | lgkmcnt 15 | vmcnt[5:4] << 14 (gfx9 encoding: wait on vmcnt only)
+        __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}''')
+        # the prologue chunk: every wave also moves pieces 0 and 1
+        s = rep(s, '''            lds_dma_1k(wb, dst + NWv * J * 1024, w, lane, S::off(N) + (uint32_t)(NWv * J * 1024));
+    });
+}''', '''            lds_dma_1k(wb, dst + NWv * J * 1024, w, lane, S::off(N) + (uint32_t)(NWv * J * 1024));
+    });
+    dma_dup<Net, N, 0>(wb, dst, lane);
+    dma_dup<Net, N, 1>(wb, dst, lane);
+}''')
+        s = rep(s, '''        h8 fh[PD], fl[PD];
+#pragma unroll
+        for (int f = 0; f < PD; ++f) {
+            fh[f] = frag(f, 0);
+            fl[f] = frag(f, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * PD, 0);''', '''        h8 fh[PD], fl[PD];
+        fh[0] = frag(0, 0);   // pair 0: this wave's own copy, landed at its vmcnt wait
+        fl[0] = frag(0, 1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);''')
+        s = rep(s, '''                const h8 Ah = fh[F % PD], Al = fl[F % PD];
+                if constexpr (F + PD < NF) {
+                    fh[F % PD] = frag(F + PD, 0);
+                    fl[F % PD] = frag(F + PD, 1);
+                }''', '''                const h8 Ah = fh[F % PD], Al = fl[F % PD];
+                if constexpr (F > 0 && F + PD < NF) {
+                    fh[F % PD] = frag(F + PD, 0);
+                    fl[F % PD] = frag(F + PD, 1);
+                }''')
+        s = rep(s, '''                constexpr int NSP = NF / 2 > 0 ? NF / 2 : 1;
+                if constexpr (F < NSP) {''', '''                if constexpr (F == 0) {
+                    // the other waves' pieces: barrier after this wave's first MFMAs, then the queue
+                    __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_s_barrier();
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int f = 1; f <= PD; ++f)
+                        if (f < NF) {
+                            fh[f % PD] = frag(f, 0);
+                            fl[f % PD] = frag(f, 1);
+                        }
+                    dma_dup<Net, NN, 0>(wb, dnext, lane);
+                    dma_dup<Net, NN, 1>(wb, dnext, lane);
+                }
+                constexpr int NSP = NF / 2 > 0 ? NF / 2 : 1;
+                if constexpr (F < NSP) {''')
     elif p == "v_early3":
         # block3.2's input converted during block3.0's last k-step (the VALU-free ext k-step), tiles 2J, 2J + 1
         # after tile 2J + 3's MFMAs, so block3.2's pass 0 runs without conversion VALU
