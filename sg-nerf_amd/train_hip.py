@@ -734,9 +734,9 @@ class HipTrainer:
             torch.cuda.current_stream(dev).wait_stream(side)
             g = torch.cuda.CUDAGraph()
             # a garbage collection inside the capture would destroy dead objects that hold HIP resources (an
-            # earlier trainer's graphs, streams, events), which invalidates a global-mode capture: collect
-            # them first and keep the collector off until the capture ends
-            gc.collect()
+            # earlier trainer's graphs, streams, events), which invalidates a global-mode capture: keep the
+            # collector off until the capture ends (no gc.collect() first: a full collection costs tens of ms
+            # per capture, +0.3..0.9 ms per step over a 100-step run with one capture in it)
             gc_on = gc.isenabled()
             gc.disable()
             try:

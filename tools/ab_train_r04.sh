@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 OUT=gpurun_out/abtr_$TAG.txt
 : > $OUT
 for rep in $(seq 1 ${REPS:-3}); do
-  for prec in f32 f16; do
+  for prec in ${PRECS:-f32 f16}; do
     for v in r04 head; do
       f=gpurun_out/abtr_${TAG}_${v}_${prec}_$rep.json
       if [ $v = r04 ]; then
