@@ -17,6 +17,7 @@ every fp32 product as three fp16 MFMA products); the fp16-operand mode is an ext
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -124,6 +125,9 @@ def train_main(args, world, rank, dev, dist, steps=None, warmup=None, precision=
         c, r_, d, gt = batches[i]
         tr.step(c, r_, d, 0.1, 8.0, gt, **_lab(labels[i]))
     torch.cuda.synchronize()
+    # the garbage of the runs before this one (the render extras' renderers and tables) is collected here,
+    # untimed, not by an automatic full collection somewhere inside the timed steps
+    gc.collect()
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -368,6 +372,7 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
         e.record()
         events[-1][name] = e
 
+    gc.collect()   # untimed (see train_main)
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
