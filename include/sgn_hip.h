@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 15
+#define SGN_ABI_VERSION 16
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -627,6 +627,9 @@ typedef struct {
     float bg[3];
     float zero_one_weight;     /* 1e-4 (train_ft) */
     float zero_one_eps;        /* 1e-3 */
+    const float *bg_ray;       /* ABI 16: device float[R*3], the rays' background (inputs['bg_ray'] of the
+                                  plane background model, fill_invalid's T_bg * bg_ray,
+                                  neural_points_volumetric_model.py:175-177); NULL: bg[3] for every ray */
 } sgn_loss_params;
 
 size_t sgn_loss_workspace_bytes(int64_t R, int32_t SR);

@@ -12,7 +12,7 @@ import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds 
 
 # SGN_HIP_LIB: another build of the same ABI (same-box A/B of kernel variants, tools/ab_lib.sh)
 LIB_PATH = os.environ.get("SGN_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 COLSUM_SLABS = 512   # SGN_COLSUM_SLABS
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
@@ -66,7 +66,7 @@ class CompositeParams(ctypes.Structure):
 
 class LossParams(ctypes.Structure):
     _fields_ = [("SR", c_i32), ("K", c_i32), ("vsize_z", c_f32), ("raydist_mode_unit", c_i32), ("bg", c_f32 * 3),
-                ("zero_one_weight", c_f32), ("zero_one_eps", c_f32)]
+                ("zero_one_weight", c_f32), ("zero_one_eps", c_f32), ("bg_ray", c_vp)]
 
 
 class GradSegment(ctypes.Structure):

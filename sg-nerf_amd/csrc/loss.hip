@@ -34,6 +34,7 @@ struct LossArgs {
     int64_t R;
     int SR, K, unit;
     float vz, bg0, bg1, bg2, zo_w, zo_eps;
+    const float *bg_ray;  // [R][3] per-ray background (ABI 16, inputs['bg_ray']) or null: (bg0, bg1, bg2)
     float *slot_ws;   // [R][SR][3]: T (transmittance before the slot), e = exp(-sigma dist), dist
     float *partial;   // [blocks][LOSS_NSUM]
     float *sums;      // [8]: l_col, l_zo, l_miss, l_all, 2 / max(3 n, 1), zo_w / max(n SR K, 1), n
@@ -42,6 +43,16 @@ struct LossArgs {
     float *dfeat;     // [S][4]
     float *dconf;     // [N]
 };
+
+// the ray's background colour: inputs['bg_ray'] when given (fill_invalid blends T_bg * bg_ray,
+// neural_points_volumetric_model.py:175-177), else the constant bg
+__device__ __forceinline__ void ray_bg(const LossArgs &a, int64_t r, float (&bg)[3]) {
+    if (a.bg_ray) {
+        bg[0] = a.bg_ray[r * 3]; bg[1] = a.bg_ray[r * 3 + 1]; bg[2] = a.bg_ray[r * 3 + 2];
+    } else {
+        bg[0] = a.bg0; bg[1] = a.bg1; bg[2] = a.bg2;
+    }
+}
 
 __device__ __forceinline__ float pers_z(const float *campos, const float *rot, float x, float y, float z) {
     const float sx = __fsub_rn(x, campos[0]), sy = __fsub_rn(y, campos[1]), sz = __fsub_rn(z, campos[2]);
@@ -131,7 +142,8 @@ __global__ __launch_bounds__(LOSS_TPB) void k_loss_fwd(LossArgs a) {
         float col[3], T;
         bool any;
         ray_forward<true>(a, r, sub == 0, col, T, any);
-        const float bg[3] = {a.bg0, a.bg1, a.bg2};
+        float bg[3];
+        ray_bg(a, r, bg);
         float se = 0.f;
         for (int c = 0; c < 3; ++c) {
             const float full = any ? col[c] + bg[c] * T : bg[c];
@@ -220,7 +232,9 @@ __global__ __launch_bounds__(LOSS_TPB) void k_loss_bwd(LossArgs a) {
             Tend = Tl * (1.f - (1.f - el) + 1e-10f);
         }
         // U = sum over later slots of g . c_i o_i T_i + g . bg T_end (d L / d a_s times a_s), from the end
-        float U = (g[0] * a.bg0 + g[1] * a.bg1 + g[2] * a.bg2) * Tend;
+        float bg[3];
+        ray_bg(a, r, bg);
+        float U = (g[0] * bg[0] + g[1] * bg[1] + g[2] * bg[2]) * Tend;
         for (int s = nv - 1; s >= 0; --s) {
             const int64_t id = off + s;
             const float T = ws[3 * s], e = ws[3 * s + 1], dist = ws[3 * s + 2];
@@ -289,6 +303,7 @@ int sgn_loss_train(const sgn_loss_params *lp, const float *d_campos, const float
     a.samp_locw = q->samp_locw; a.feat = d_feat; a.gt = d_gt; a.conf = d_conf;
     a.R = R; a.SR = lp->SR; a.K = lp->K; a.unit = lp->raydist_mode_unit; a.vz = lp->vsize_z;
     a.bg0 = lp->bg[0]; a.bg1 = lp->bg[1]; a.bg2 = lp->bg[2];
+    a.bg_ray = lp->bg_ray;
     a.zo_w = lp->zero_one_weight; a.zo_eps = lp->zero_one_eps;
     a.slot_ws = (float *)d_workspace;
     a.partial = a.slot_ws + R * lp->SR * 3;

@@ -50,10 +50,10 @@ class LossStage:
         return self.ws
 
     def __call__(self, points, q_abi, feat, campos, rot, gt, opts: HotPathOpts, R, bg=(1.0, 1.0, 1.0),
-                 zero_one_weight=1e-4, zero_eps=1e-3):
+                 zero_one_weight=1e-4, zero_eps=1e-3, bg_ray=None):
         """feat [S_cap, 4] fp32 per sample (alpha, r, g, b; zeros for samples without neighbours),
-        q_abi: the query's sgn_query_out.  Returns (total, parts, full [R, 3], ray_mask [R] bool)
-        as train.composite_losses."""
+        q_abi: the query's sgn_query_out; bg_ray: the rays' background [R, 3] (device, replaces bg).
+        Returns (total, parts, full [R, 3], ray_mask [R] bool) as train.composite_losses."""
         dev = self.device
         conf = points.points_conf
         n_points = conf.shape[0]
@@ -70,6 +70,9 @@ class LossStage:
         for i in range(3):
             lp.bg[i] = float(bg[i])
         lp.zero_one_weight, lp.zero_one_eps = 1.0, float(zero_eps)   # dconf = d zero-one / d conf
+        if bg_ray is not None:
+            bg_ray = bg_ray.reshape(R, 3).to(dev, torch.float32).contiguous()
+            lp.bg_ray = bg_ray.data_ptr()
 
         def run(feat_t, conf_t):
             losses = torch.empty(_N_LOSS, dtype=torch.float32, device=dev)

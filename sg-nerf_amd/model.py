@@ -24,7 +24,8 @@ reset_ray_miss_ranking, top_ray_miss_loss / top_ray_miss_ids, mvs_points_volumet
 saveSemanticEmbedding / saveSemanticPoints / saveSemanticPoints_test
 (neural_points_volumetric_model.py:337-362, 674-720); checkpoints carry
 neural_points.points_feats / points_label / bpnet_points_embedding.  set_bg (plane background)
-is refused: that background model is not on the hot path.  Pruning keeps the semantic
+returns the rays' bg_ray, which test() blends as T_bg * bg_ray and optimize_parameters composites
+into the loss the same way.  Pruning keeps the semantic
 per-point arrays aligned with the points (the reference leaves them unpruned).
 """
 import dataclasses
@@ -299,11 +300,14 @@ class HipPointsVolumetricModel:
                       torch.as_tensor(inp["pixel_label"]).reshape(-1).to(self.device, torch.int32).contiguous(),
                       inp.get("seconds"))
         tr.step_count = int(total_steps)
+        # the plane background model's per-ray colour (set_bg -> inputs['bg_ray'], run/train_ft.py:209-218):
+        # the loss composites T_bg * bg_ray + colour (neural_points_volumetric_model.py:175-177)
+        bg_ray = inp.get("bg_ray")
         if backward:
-            parts, full, ray_mask = tr.step(*args, labels=labels)
+            parts, full, ray_mask = tr.step(*args, labels=labels, bg_ray=bg_ray)
             self._weights_dirty = True
         else:
-            parts, full, ray_mask = tr.backward(*args, labels=labels)
+            parts, full, ray_mask = tr.backward(*args, labels=labels, bg_ray=bg_ray)
         for k, v in parts.items():
             setattr(self, "loss_" + k, v)
         self.output = {"coarse_raycolor": full[None], "ray_mask": ray_mask[None].to(torch.int8)}

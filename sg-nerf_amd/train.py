@@ -277,7 +277,8 @@ class _CumprodPositive(torch.autograd.Function):
 def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotPathOpts, bg=(1.0, 1.0, 1.0),
                      zero_one_weight=1e-4, zero_eps=1e-3, s_count=None):
     """ray_dist + ray_march + the reference losses from per-sample features feat [S,4]
-    (alpha, r, g, b) and the per-sample validity (>= 1 neighbour).
+    (alpha, r, g, b) and the per-sample validity (>= 1 neighbour).  bg: a constant colour (3
+    floats) or the rays' background [R, 3] (the plane model's bg_ray: T_bg * bg_ray + colour).
 
     s_count (device scalar, optional): only the first s_count of the S sample entries are
     real; the rest (capacity padding, for a graph-captured step with static shapes) are routed
@@ -315,7 +316,10 @@ def composite_losses(points, q, feat, valid, campos, rot, raydir, gt, opts: HotP
     acc = _CumprodPositive.apply(1 - o + 1e-10)
     bg_t = acc[:, -1:]
     acc = torch.cat([torch.ones(R, 1, device=dev), acc[:, :-1]], dim=-1)
-    bgv = torch.cat([torch.full((1,), float(b), device=dev) for b in bg])  # no host copy (graph-safe)
+    if torch.is_tensor(bg):   # per-ray background [R, 3] (inputs['bg_ray'], neural_points_volumetric_model.py:175-177)
+        bgv = bg.reshape(R, 3).to(dev, torch.float32)
+    else:
+        bgv = torch.cat([torch.full((1,), float(b), device=dev) for b in bg])  # no host copy (graph-safe)
     color = torch.sum(fd[..., 1:4] * (o * acc)[..., None], dim=1) + bgv * bg_t
     ray_mask = vd.any(-1)
     full = torch.where(ray_mask[:, None], color, bgv.expand(R, 3))
@@ -501,13 +505,16 @@ class Trainer:
             for g in opt.param_groups:
                 g["lr"] = base * f
 
-    def backward(self, campos, rot, raydir, near, far, gt, q=None):
-        """Forward + backward + gradient all-reduce (no parameter update)."""
+    def backward(self, campos, rot, raydir, near, far, gt, q=None, bg_ray=None):
+        """Forward + backward + gradient all-reduce (no parameter update).  bg_ray: the rays'
+        background [R, 3] (plane model) or None (white)."""
         if q is None:
             q = self._query(campos.reshape(3).contiguous(), raydir.reshape(-1, 3).contiguous(), near, far)
         self.opt_net.zero_grad(set_to_none=True)
         self.opt_pts.zero_grad(set_to_none=True)
-        total, parts, full, ray_mask = loss_from_query(self.points, self.mlp, q, campos, rot, raydir, gt, self.opts)
+        bg = (1.0, 1.0, 1.0) if bg_ray is None else bg_ray
+        total, parts, full, ray_mask = loss_from_query(self.points, self.mlp, q, campos, rot, raydir, gt, self.opts,
+                                                       bg)
         total.backward()
         for p in self.point_params + self.net_params:
             if p.grad is None:

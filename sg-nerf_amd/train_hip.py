@@ -1,32 +1,41 @@
 """Training step on the HIP kernels.
 
 The reference trains through torch autograd (`optimize_parameters`,
-models/base_rendering_model.py:534-664; models/mvs_points_volumetric_model.py:47-141).  Here
-the per-neighbour part -- the NeuralPoints gather and the 4-layer per-row MLP + alpha +
-K-blend of PointAggregator (point_aggregators.py:868-959, :561-786), 95 % of the FLOPs --
-runs forward and backward in hand-written MFMA kernels (mlp.hip k_agg_rows<0, true>,
-agg_train.hip k_agg_bwd); the per-sample colour MLP, ray_dist / ray_march and the losses
-are differentiated by torch on the device (they are small, per sample / per ray):
+models/base_rendering_model.py:534-664; models/mvs_points_volumetric_model.py:47-141).  Here the
+whole step -- the NeuralPoints gather, the per-row MLP + alpha + K-blend of PointAggregator
+(point_aggregators.py:868-959, :561-786), the colour MLP, ray_dist / ray_march and the losses,
+and all their gradients -- runs as hand-written HIP launches; torch only allocates buffers and
+all-reduces gradients.  Two arithmetic modes, as the renderer has:
 
-  query        sgn_query (jittered depths, is_train), indices carry no gradient
-  forward      sgn_aggregate_train_fwd: blended features f_s (fp16) and alpha_s per sample,
-               per-row layer inputs saved for the backward
-  colour+loss  torch: colour MLP on [f_s | PE(v)] (autograd); the HIP loss stage (loss.hip via
-               loss_hip.LossStage): ray_dist + ray_march, ray-masked MSE + zero-one(conf) and their
-               gradients -> d f_s, d alpha_s, colour grads, d conf
-  backward     sgn_aggregate_backward: deltas of the 4 row layers, d alpha-logit, point grads
-               (embedding via PE(feat), colour, dir, conf through the straight-through clamp)
-               with a power-of-two loss scale; dW = delta^T x per layer as fp16 GEMMs with fp32
-               output (hipBLASLt), unpermuted into the flat parameter gradient
-  update       bucketed all-reduce (RCCL) of the flat MLP gradient and the point gradients,
-               two Adam groups (lr 5e-4 / plr 2e-3) with iter_exponential_decay
+precision "f32" (the reference's fp32 arithmetic; `_backward_f32`, train_f32.F32Step):
+  query        sgn_query (jittered depths, is_train) -> sgn_touched_points (the step's points)
+  projection   sgn_point_project_f32_subset: block1.0's per-point part for the touched points only
+  forward      k_rows16 in save mode (block1.0 / 1.2 / 3.0 pre-activations per row; SG: + block2_bpnet)
+  colour+loss  the colour MLP on k_x3rows (3 fp16 products per fp32 product), sgn_loss_train
+  backward     k_row_head / masked backward-data GEMMs / k_row_tail (point gradients), the split-K
+               weight gradients on k_x3dw / k_x3tn and one fixed-order sgn_reduce_partials
+  no host synchronisation on one GPU.
+
+precision "f16" (fp16-operand MFMA, fp32 accumulation; `backward`):
+  query        sgn_query, then the step's one host sync (sample / work-item counts)
+  forward      sgn_aggregate_train_fwd (k_agg_rows save mode): f_s (fp16) and alpha per sample,
+               the row layers' inputs saved
+  colour+loss  one captured HIP graph (ColourStep: sgn_colour_inputs, the colour MLP on k_x3rows,
+               sgn_loss_train, the colour backward and its weight gradients), or the same stage
+               eagerly (use_graph = False) through loss_hip.LossStage and torch autograd of the
+               colour MLP -- the graph's parity reference in the tests
+  backward     sgn_aggregate_backward (k_agg_bwd): deltas of the 4 row layers, d alpha-logit, point
+               gradients, under a power-of-two loss scale; dW = delta^T x per row layer on k_f16dw
+               (sgn_f16_weight_grad, split-K fp32 partials) and the alpha branch's weighted column
+               sums, all added into the flat gradient by one sgn_grad_accumulate
+
+Both: bucketed all-reduce (RCCL) of the flat MLP gradient and a sparse all-gather of the touched
+point rows under DP, then two Adam groups (lr 5e-4 / plr 2e-3, iter_exponential_decay) on
+sgn_adam_step_multi.  The plane background model's per-ray colour (inputs['bg_ray']) enters the
+loss stage as T_bg * bg_ray.
 
 MLP weights live in ONE flat fp32 parameter (LAYERS order), so the MFMA blobs are re-packed on
-the device every step by index gathers (sgn_mlp_pack_index / sgn_train_pack_index).
-
-precision "f32" (the reference's arithmetic): the fp32-faithful row kernel in save mode
-(k_rows16: block1.0 / 1.2 / 3.0 pre-activations per row) after re-projecting the touched points'
-P rows, then train.aggregate(saved=...) and fp32 autograd through the HIP loss stage.
+the device every step by index gathers (sgn_gather_segments / sgn_pack_scaled_f32).
 """
 import ctypes
 import gc
@@ -488,24 +497,64 @@ class HipTrainer:
         if self._tstep == 0:   # the stamp table outlived 2^31 steps: start it again
             self._stamp_n = -1
         K = self.opts.K
+        self._check_oob()
         _lib.check(_lib.lib().sgn_touched_points(_lib.ptr(q.pidx), _lib.ptr(q.counters), q.pidx.numel() // K, K, npts,
                                                  step, _lib.ptr(self._stamp), _lib.ptr(self._tlist),
                                                  _lib.ptr(self._tcount), _lib.stream_handle()), "sgn_touched_points")
+        # the out-of-range neighbour count goes to pinned host memory without a sync; the next step
+        # (or check_touched()) reads it once the copy has landed and fails loudly on a query / point
+        # table mismatch (those points would never be projected)
+        if not hasattr(self, "_oob_host"):
+            self._oob_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._oob_event = torch.cuda.Event()
+        self._oob_host.copy_(self._tcount[2:3], non_blocking=True)
+        self._oob_event.record()
+        self._oob_pending = True
         return self._tlist, self._tcount[step & 1]
 
+    def _check_oob(self, wait=False):
+        """Raise if an earlier step's query named a point index >= n_points (sgn_touched_points'
+        counter d_count2[2]); without wait only a copy that has already landed is read."""
+        if not getattr(self, "_oob_pending", False):
+            return
+        if not wait and not self._oob_event.query():
+            return
+        self._oob_event.synchronize()
+        self._oob_pending = False
+        n = int(self._oob_host[0])
+        if n:
+            raise RuntimeError(f"training step: {n} neighbour indices >= n_points (query and point tables disagree)")
+
+    def check_touched(self):
+        """Wait for and check the last step's out-of-range neighbour counter (see _check_oob)."""
+        self._check_oob(wait=True)
+
     # -- one step ------------------------------------------------------------------------
-    def backward(self, campos, rot, raydir, near, far, gt, labels=None):
+    def _bg_ray(self, bg_ray, R):
+        """inputs['bg_ray'] (the plane background model's per-ray colour, [1, R, 3]) as a contiguous
+        device [R, 3] fp32 tensor, or None (the constant white background)."""
+        if bg_ray is None:
+            return None
+        bg_ray = torch.as_tensor(bg_ray).to(self.device, torch.float32).reshape(-1, 3).contiguous()
+        if bg_ray.shape[0] != R:
+            raise ValueError(f"bg_ray has {bg_ray.shape[0]} rays, the batch {R}")
+        return bg_ray
+
+    def backward(self, campos, rot, raydir, near, far, gt, labels=None, bg_ray=None):
         """Forward + backward + gradient all-reduce (no parameter update).  labels: (point_labels,
-        ray_labels, seconds) for the semantic-guided query (semantic_guidance = 1).
+        ray_labels, seconds) for the semantic-guided query (semantic_guidance = 1).  bg_ray: the
+        rays' background [1, R, 3] of the plane background model (inputs['bg_ray']): the composite
+        and its gradient use T_bg * bg_ray per ray (neural_points_volumetric_model.py:175-177).
         Returns (loss parts, rendered colour [R,3], ray_mask [R])."""
         if self.precision == "f32":
-            return self._backward_f32(campos, rot, raydir, near, far, gt, labels)
+            return self._backward_f32(campos, rot, raydir, near, far, gt, labels, bg_ray)
         o = self.opts
         dev = self.device
         campos = campos.reshape(3).to(dev, torch.float32).contiguous()
         rot = rot.reshape(3, 3).to(dev, torch.float32).contiguous()
         raydir = raydir.reshape(-1, 3).to(dev, torch.float32).contiguous()
         R = raydir.shape[0]
+        bg_ray = self._bg_ray(bg_ray, R)
         q = self._query(campos, raydir, near, far, labels)
         # work that does not depend on the query is queued before the step's one host sync, so
         # the GPU runs it while the host waits
@@ -548,7 +597,7 @@ class HipTrainer:
                        "sgn_aggregate_train_fwd")
         # ---- colour MLP + composite + losses (torch autograd, per sample / per ray) ----------
         if graph:
-            out = self._graph_losses(q, campos, rot, raydir, gt, R, S, n)
+            out = self._graph_losses(q, campos, rot, raydir, gt, R, S, n, bg_ray)
             total, parts, full, ray_mask = out["total"], dict(out["parts"]), out["full"], out["ray_mask"]
             dfs, dal, scale = out["dfs"], out["dal"], out["scale"]
         else:
@@ -562,7 +611,7 @@ class HipTrainer:
             validS[samp] = True
             qd = {"ray_ns": q.ray_ns[:R], "ray_soff": q.ray_soff[:R], "samp_ray": q.samp_ray[:S],
                   "samp_locw": q.samp_locw[:S * 3].view(S, 3), "pidx": q.pidx[:S * o.K].view(S, o.K)}
-            total, parts, full, ray_mask = self.loss_stage(self.points, qo, featS, campos, rot, gt, o, R)
+            total, parts, full, ray_mask = self.loss_stage(self.points, qo, featS, campos, rot, gt, o, R, bg_ray=bg_ray)
             total.backward()
             if n > 0:
                 dfs = fs_t.grad.contiguous()
@@ -594,7 +643,7 @@ class HipTrainer:
         return parts, full.detach(), ray_mask
 
     # -- fp32-faithful step ---------------------------------------------------------------------
-    def _loss_params(self):
+    def _loss_params(self, bg_ray=None):
         o = self.opts
         lp = _lib.LossParams()
         lp.SR, lp.K = o.SR, o.K
@@ -602,9 +651,11 @@ class HipTrainer:
         for i in range(3):
             lp.bg[i] = 1.0
         lp.zero_one_weight, lp.zero_one_eps = 1e-4, 1e-3   # train_ft: zero_one weight 1e-4, epsilon 1e-3
+        if bg_ray is not None:   # per-ray background [R, 3] (device, contiguous)
+            lp.bg_ray = bg_ray.data_ptr()
         return lp
 
-    def _backward_f32(self, campos, rot, raydir, near, far, gt, labels=None):
+    def _backward_f32(self, campos, rot, raydir, near, far, gt, labels=None, bg_ray=None):
         """The reference's fp32 step on hand-written kernels (train_f32.F32Step): query, forward,
         colour MLP, losses and the whole backward as HIP launches with the counts on the device (no
         host sync on one GPU; under DP one for the touched-row counts).  The block1.0 projection P is
@@ -618,6 +669,7 @@ class HipTrainer:
         raydir = raydir.reshape(-1, 3).to(dev, torch.float32).contiguous()
         gt = gt.reshape(-1, 3).to(dev, torch.float32).contiguous()
         R = raydir.shape[0]
+        bg_ray = self._bg_ray(bg_ray, R)
         q = self._query(campos, raydir, near, far, labels)
         blob = self.packer32.pack(self.mlp.flat)
         for p in self.point_params + [self.mlp.flat]:
@@ -647,7 +699,7 @@ class HipTrainer:
         if step is None or step.key != key:
             step = self._f32step = F32Step(self, q, R)
             step.key = key
-        losses, full, mask = step.run(pt, self._proj32, blob, campos, rot, gt, self._loss_params())
+        losses, full, mask = step.run(pt, self._proj32, blob, campos, rot, gt, self._loss_params(bg_ray))
         self._last_q = q
         # the step's buffers are reused by the next step: the losses, the colour and the mask out into
         # one fresh allocation (one launch), as the f16 step's graph outputs
@@ -692,7 +744,7 @@ class HipTrainer:
                                                 _lib.ptr(st["col"].vpe),
                                                 _lib.stream_handle()), "sgn_colour_inputs")
         # hand-written colour MLP, losses and backward (train_f32.ColourStep)
-        losses, full, mask, dfs, dfeat = st["col"].run(st["campos"], st["rot"], st["gt"], self._loss_params())
+        losses, full, mask, dfs, dfeat = st["col"].run(st["campos"], st["rot"], st["gt"], self._loss_params(st["bg_ray"]))
         dal = dfeat[samp.long(), 0]          # per item (padding: the zero row Sc)
         scale = self._loss_scale(dfs, dal)
         total = losses[0] + 3e-6 + 1e-4 * losses[1]
@@ -700,17 +752,19 @@ class HipTrainer:
         return {"scalars": torch.stack([total, losses[0], losses[2], losses[3], losses[1]]), "names": names,
                 "full": full, "ray_mask": mask, "dfs": dfs, "dal": dal, "scale": scale}
 
-    def _graph_losses(self, q, campos, rot, raydir, gt, R, S, n):
+    def _graph_losses(self, q, campos, rot, raydir, gt, R, S, n, bg_ray=None):
         """Replay the captured loss stage for this step's capacity bucket (item / sample counts
         rounded up to GRAPH_BUCKET); captured on first use and again when a buffer it reads
-        moved.  At most GRAPH_CACHE graphs are kept."""
+        moved.  At most GRAPH_CACHE graphs are kept.  A step with a per-ray background (bg_ray)
+        replays a graph of its own whose static bg_ray buffer the step's colours are copied into."""
         dev = self.device
         P, fl = self.points, self.mlp.flat
         cap = R * self.opts.SR
         Sc = min(cap, -(-max(S, 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
         Nc = min(Sc, -(-max(n, 1) // GRAPH_BUCKET) * GRAPH_BUCKET)
         key = (R, Sc, Nc, q.work.data_ptr(), q.counters.data_ptr(), self.fs.data_ptr(), self.feat.data_ptr(),
-               fl.data_ptr(), fl.grad.data_ptr(), P.points_conf.data_ptr(), P.points_conf.grad.data_ptr())
+               fl.data_ptr(), fl.grad.data_ptr(), P.points_conf.data_ptr(), P.points_conf.grad.data_ptr(),
+               bg_ray is not None)
         st = self._graphs.pop(key, None)
         if st is not None:
             self._graphs[key] = st              # most recently used goes last (LRU eviction order)
@@ -721,6 +775,7 @@ class HipTrainer:
             st = {"key": key, "R": R, "Sc": Sc, "Nc": Nc, "q": q, "qabi": q.abi(),
                   "raydir": raydir.clone(), "gt": gt.reshape(-1, 3).to(dev, torch.float32).clone(),
                   "campos": campos.clone(), "rot": rot.clone(),
+                  "bg_ray": None if bg_ray is None else bg_ray.clone(),
                   "fs32": torch.zeros(Nc, 256, device=dev), "al32": torch.zeros(Nc, device=dev),
                   "v": torch.zeros(Nc, 3, device=dev), "samp": torch.zeros(Nc, dtype=torch.int32, device=dev)}
             from .train_f32 import ColourStep
@@ -753,7 +808,8 @@ class HipTrainer:
         if g3.dtype != torch.float32 or g3.device != dev or not g3.is_contiguous():
             g3 = g3.to(dev, torch.float32).contiguous()
         # the step's inputs into the graph's static buffers: one launch
-        _lib.copy_segments([(raydir, st["raydir"]), (g3, st["gt"]), (campos, st["campos"]), (rot, st["rot"])])
+        _lib.copy_segments([(raydir, st["raydir"]), (g3, st["gt"]), (campos, st["campos"]), (rot, st["rot"])] +
+                           ([] if bg_ray is None else [(bg_ray, st["bg_ray"])]))
         st["graph"].replay()
         out = st["out"]
         # the loss, its parts, the rendered colour and the ray mask out of the graph's buffers: one
@@ -831,10 +887,13 @@ class HipTrainer:
             # block2_bpnet.0: x = [h (chain order) | the row's BPNet embedding (natural order)]
             x = self.h2b[:rp]
             if self.variant[1]:
-                item = torch.arange(rp, device=self.device) // 8
-                ok = item < rows // 8
+                # row r = item * 8 + k: rows k < K read pidx index s * K + k, rows k >= K are empty
+                K = self.opts.K
+                r = torch.arange(rp, device=self.device)
+                item, k = r // 8, r % 8
+                ok = (item < rows // 8) & (k < K)
                 s_of = q.work[torch.where(ok, item, 0)].long()
-                pid = q.pidx[s_of * 8 + (torch.arange(rp, device=self.device) % 8)].long()
+                pid = torch.where(ok, q.pidx[s_of * K + torch.clamp(k, max=K - 1)].long(), -1)
                 bp = self.bpnet16[torch.clamp(pid, min=0)]
                 bp = torch.where((ok & (pid >= 0))[:, None], bp, torch.zeros((), dtype=bp.dtype, device=bp.device))
                 x = torch.cat([x, bp], dim=1)
@@ -881,8 +940,8 @@ class HipTrainer:
         self._grads_clean = all(isinstance(o, PointAdam) and o.zero_grad_in_step for o in (self.opt_net, self.opt_pts))
         self.step_count += 1
 
-    def step(self, campos, rot, raydir, near, far, gt, labels=None):
-        out = self.backward(campos, rot, raydir, near, far, gt, labels)
+    def step(self, campos, rot, raydir, near, far, gt, labels=None, bg_ray=None):
+        out = self.backward(campos, rot, raydir, near, far, gt, labels, bg_ray)
         self.apply()
         return out
 

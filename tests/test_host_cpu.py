@@ -44,6 +44,31 @@ def test_library_loads_and_exports_every_symbol():
     assert L.sgn_abi_version() == v == _lib.ABI_VERSION
 
 
+def test_integration_snippet_matches_binding():
+    """INTEGRATION.md §3's reference-side ctypes binding: its ABI constant and struct definitions,
+    executed, must equal sgnerf_amd._lib's (sizeof, field names, offsets, types) and the header's
+    SGN_ABI_VERSION -- a snippet a maintainer copies must not pass a struct of the wrong size."""
+    import ast
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = txt[txt.index("## 3. ctypes binding"):txt.index("## 4.")]
+    code = re.search(r"```python\n(.*?)```", sec, flags=re.S).group(1)
+    tree = ast.parse(code)
+    keep = [n for n in tree.body if isinstance(n, ast.ClassDef) or
+            (isinstance(n, ast.Assign) and any(getattr(t, "id", "") == "SGN_ABI_VERSION" for t in n.targets))]
+    ns = {"ctypes": ctypes}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), "INTEGRATION.md", "exec"), ns)
+    hdr = int(re.search(r"#define SGN_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert ns["SGN_ABI_VERSION"] == _lib.ABI_VERSION == hdr
+    classes = [n.name for n in keep if isinstance(n, ast.ClassDef)]
+    assert {"QueryParams", "LossParams"} <= set(classes)
+    for name in classes:
+        mine, ref = ns[name], getattr(_lib, name)
+        assert ctypes.sizeof(mine) == ctypes.sizeof(ref), name
+        fm = [(f[0], getattr(mine, f[0]).offset, ctypes.sizeof(f[1])) for f in mine._fields_]
+        fr = [(f[0], getattr(ref, f[0]).offset, ctypes.sizeof(f[1])) for f in ref._fields_]
+        assert fm == fr, name
+
+
 def test_sizing_functions():
     L = _lib.lib()
     assert L.sgn_mlp_packed_bytes() > 2 * N_PARAMS  # fp16 fragments (+ padding) + fp32 params

@@ -49,29 +49,37 @@ def _case(seed, SR, alpha_scale, conf_lo, conf_hi, h=24, w=32, n=60_000, unit=0)
     return o, points, q, qd, feat, valid, campos, rot, raydir, gt, R
 
 
-@pytest.mark.parametrize("seed,SR,alpha_scale,conf_lo,conf_hi,unit", [
-    (0, 24, 100.0, -0.1, 1.2, 0),    # config-5 shape, near-opaque samples, conf outside both clamps
-    (1, 24, 2.0, 0.0, 1.0, 0),       # translucent
-    (2, 64, 20.0, 0.0005, 0.9995, 1),  # SR 64, raydist_mode_unit, conf around the zero-one eps
+@pytest.mark.parametrize("seed,SR,alpha_scale,conf_lo,conf_hi,unit,bgr", [
+    (0, 24, 100.0, -0.1, 1.2, 0, False),    # config-5 shape, near-opaque samples, conf outside both clamps
+    (1, 24, 2.0, 0.0, 1.0, 0, False),       # translucent
+    (2, 64, 20.0, 0.0005, 0.9995, 1, False),  # SR 64, raydist_mode_unit, conf around the zero-one eps
+    (1, 24, 2.0, 0.0, 1.0, 0, True),        # translucent, per-ray background (the plane model's bg_ray)
+    (0, 24, 100.0, -0.1, 1.2, 0, True),
 ])
-def test_loss_stage_matches_torch_autograd(seed, SR, alpha_scale, conf_lo, conf_hi, unit):
+def test_loss_stage_matches_torch_autograd(seed, SR, alpha_scale, conf_lo, conf_hi, unit, bgr):
+    """bgr: the rays' background is inputs['bg_ray'] [R, 3] (set_bg), composited as T_bg * bg_ray
+    and taken by the rays without a valid sample (neural_points_volumetric_model.py:175-177)."""
     o, points, q, qd, feat, valid, campos, rot, raydir, gt, R = _case(seed, SR, alpha_scale, conf_lo, conf_hi,
                                                                      unit=unit)
+    bg_ray = torch.rand(R, 3, generator=torch.Generator().manual_seed(seed + 40)).to(DEV) if bgr else None
     # torch restatement
     f_t = feat.clone().requires_grad_(True)
     points.points_conf.grad = None
-    tot_t, parts_t, full_t, mask_t = composite_losses(points, qd, f_t, valid, campos, rot, raydir, gt, o)
+    tot_t, parts_t, full_t, mask_t = composite_losses(points, qd, f_t, valid, campos, rot, raydir, gt, o,
+                                                      bg=bg_ray if bgr else (1.0, 1.0, 1.0))
     tot_t.backward()
     dconf_t = points.points_conf.grad.clone()
     # HIP loss stage
     f_h = feat.clone().requires_grad_(True)
     points.points_conf.grad = None
-    tot_h, parts_h, full_h, mask_h = LossStage(DEV)(points, q.abi(), f_h, campos, rot, gt, o, R)
+    tot_h, parts_h, full_h, mask_h = LossStage(DEV)(points, q.abi(), f_h, campos, rot, gt, o, R, bg_ray=bg_ray)
     tot_h.backward()
     dconf_h = points.points_conf.grad.clone()
     torch.cuda.synchronize()
     assert int(mask_h.sum()) > 10 and int((~mask_h).sum()) > 0
     assert torch.equal(mask_h, mask_t)
+    if bgr:   # the rays without a valid sample take their own background
+        assert torch.equal(full_h[~mask_h], bg_ray[~mask_h])
     assert float((full_h - full_t.detach()).abs().max()) <= 1e-5
     assert abs(float(tot_h) - float(tot_t)) <= 1e-5 * abs(float(tot_t))
     for k in parts_t:

@@ -242,6 +242,53 @@ def test_f32_training_small_k_matches_fp32_autograd(K):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("precision,graph", [("f32", False), ("f16", True), ("f16", False)])
+def test_training_with_plane_background_matches_fp32_autograd(precision, graph):
+    """A step whose rays carry the plane background model's per-ray colour (inputs['bg_ray'] from
+    set_bg, run/train_ft.py:209-218): the loss composites T_bg * bg_ray + colour and its gradient
+    flows through T_bg (neural_points_volumetric_model.py:175-177).  Against train.Trainer's fp32
+    autograd with the same bg_ray on the very samples the HIP query produced: f32 within
+    GRAD_TOL_F32, f16 (captured loss graph and eager) within the f16 bars."""
+    pc, view, _, mlp, gt = _setup(seed=3)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    R = view.raydir.shape[0]
+    bg_ray = torch.rand(1, R, 3, generator=torch.Generator().manual_seed(21)).to(DEV)
+    points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    tr = HipTrainer(points, mlp, O, DEV, precision=precision)
+    tr.use_graph = graph
+    parts, full, ray_mask = tr.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV),
+                                        bg_ray=bg_ray)
+    qd = {k: v.long() if v.dtype == torch.int32 else v for k, v in tr.last_query.items()}
+    ref_points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+    ref = Trainer(ref_points, mlp, O, DEV)
+    parts_c, full_c, mask_c = ref.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV),
+                                           q=qd, bg_ray=bg_ray[0])
+    # the white-background loss differs: the plane colour reached the loss
+    ref_w = Trainer(PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV), mlp, O, DEV)
+    parts_w, _, _ = ref_w.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV), q=qd)
+    torch.cuda.synchronize()
+    assert torch.equal(ray_mask, mask_c)
+    assert torch.equal(full[~ray_mask], bg_ray[0][~ray_mask])
+    assert abs(float(parts_w["total"]) - float(parts_c["total"])) > 1e-3 * abs(float(parts_c["total"]))
+    tol_c = GRAD_TOL_F32 if precision == "f32" else 1e-3
+    assert float((full - full_c).abs().max()) <= tol_c
+    assert abs(float(parts["total"]) - float(parts_c["total"])) <= tol_c * abs(float(parts_c["total"]))
+    g = grads_named(tr)
+    worst = {}
+    for name, *_ in LAYERS:
+        m = ref.mlp.lin[name.replace(".", "_")]
+        worst[name + ".weight"] = _rel(g[name + ".weight"], m.weight.grad)
+        worst[name + ".bias"] = _rel(g[name + ".bias"], m.bias.grad)
+    for k in ("points_embeding", "points_color", "points_dir", "points_conf"):
+        worst[k] = _rel(g[k].reshape(getattr(ref_points, k).grad.shape), getattr(ref_points, k).grad)
+    print(f"bg_ray [{precision}, graph {graph}]: relative L2 gradient errors:", {k: f"{v:.2e}" for k, v in worst.items()})
+    if precision == "f32":
+        bad = {k: v for k, v in worst.items() if v > GRAD_TOL_F32}
+    else:
+        bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
+    assert not bad, bad
+
+
 def _config5():
     from sgnerf_amd import scene
     pc = scene.synth_room(1_200_000, seed=0)
@@ -837,13 +884,16 @@ def test_hip_sg_training_gradients_match_oracle(dim, seed):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("dim,seed", [(96, 3), (0, 5)])
-def test_hip_sg_f32_training_gradients_match_fp32_autograd(dim, seed):
+@pytest.mark.parametrize("precision,dim,seed,K", [("f32", 96, 3, 8), ("f32", 0, 5, 8), ("f16", 96, 3, 4),
+                                                  ("f32", 96, 3, 4)])
+def test_hip_sg_f32_training_gradients_match_fp32_autograd(precision, dim, seed, K):
     """SG-NeRF's block2_bpnet at precision "f32" (train_f32.F32Step with block2_bpnet.0 between
     block1.2 and block3.0): one backward against fp32 autograd through oracle/agg_ref.py's SG
     aggregator, on the GPU, over the very samples the HIP query produced (last_query): the
     colour, the loss and every gradient (block2_bpnet.0 and the points included) within
-    GRAD_TOL_F32."""
+    GRAD_TOL_F32.  K = 4 (rows k >= K of a sample empty): also at precision "f16", whose
+    block2_bpnet.0 weight gradient gathers each row's BPNet embedding at pidx index s * K + k
+    (ADVICE r5), held to the f16 bars (GRAD_TOL_MLP / GRAD_TOL_POINTS, colour 1e-3)."""
     import math
 
     import agg_ref
@@ -857,10 +907,10 @@ def test_hip_sg_f32_training_gradients_match_fp32_autograd(dim, seed):
     mlp["block2_bpnet.0.bias"] = torch.randn(256, generator=g) * 0.01
     bp = (torch.rand(n, dim, generator=g) - 0.5) if dim else None
     o = dataclasses_replace(O_BASE, shading_feature_mlp_layer2_bpnet=1, predict_semantic=1 if dim else 0,
-                            semantic_guidance=1 if dim else 0)
+                            semantic_guidance=1 if dim else 0, K=K)
     d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
     points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
-    tr = HipTrainer(points, mlp, o, DEV, bpnet=bp, precision="f32")
+    tr = HipTrainer(points, mlp, o, DEV, bpnet=bp, precision=precision)
     R = view.raydir.shape[0]
     labels = (torch.zeros(n, dtype=torch.int32), torch.ones(R, dtype=torch.int32), 10) if dim else None
     parts, full, mask = tr.backward(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gt.to(DEV), labels)
@@ -882,8 +932,9 @@ def test_hip_sg_f32_training_gradients_match_fp32_autograd(dim, seed):
     l_col = torch.mean((color[ray_mask] - gtd[ray_mask]) ** 2)
     S = qd["samp_ray"].shape[0]
     slot = torch.arange(S, device=DEV) - qd["ray_soff"][qd["samp_ray"]]
-    pd = torch.full((R, O_BASE.SR, O_BASE.K), -1, dtype=torch.long, device=DEV)
+    pd = torch.full((R, O_BASE.SR, K), -1, dtype=torch.long, device=DEV)
     pd[qd["samp_ray"], slot] = qd["pidx"]
+    assert qd["pidx"].shape[1] == K
     cd = pts["conf"][torch.clamp(pd[ray_mask], min=0).reshape(-1), 0]
     val = torch.clamp(torch.clamp(cd, 1e-4, 1.0), 1e-3, 1 - 1e-3)
     l_zo = torch.mean(torch.log(val) + torch.log(1 - val))
@@ -891,16 +942,24 @@ def test_hip_sg_f32_training_gradients_match_fp32_autograd(dim, seed):
     total.backward()
     torch.cuda.synchronize()
     assert torch.equal(mask, ray_mask)
-    assert _rel(full[ray_mask], color[ray_mask].detach()) <= GRAD_TOL_F32
-    assert abs(float(parts["total"]) - float(total)) <= GRAD_TOL_F32 * abs(float(total))
+    if precision == "f32":
+        assert _rel(full[ray_mask], color[ray_mask].detach()) <= GRAD_TOL_F32
+        assert abs(float(parts["total"]) - float(total)) <= GRAD_TOL_F32 * abs(float(total))
+    else:
+        assert float((full[ray_mask] - color[ray_mask].detach()).abs().max()) <= 1e-3
+        assert abs(float(parts["total"]) - float(total)) <= 1e-3 * abs(float(total))
     names = {"points_embeding": "embedding", "points_color": "color", "points_dir": "dir", "points_conf": "conf"}
     worst = {}
     for k, v in hg.items():
         ref = pts[names[k]].grad if k in names else m[k].grad
         worst[k] = _rel(v.reshape(ref.shape), ref)
-    print(f"SG f32 dim {dim} relative L2 gradient errors (same query):", {k: f"{v:.2e}" for k, v in worst.items()})
+    print(f"SG {precision} dim {dim} K {K} relative L2 gradient errors (same query):",
+          {k: f"{v:.2e}" for k, v in worst.items()})
     assert "block2_bpnet.0.weight" in worst
-    bad = {k: v for k, v in worst.items() if v > GRAD_TOL_F32}
+    if precision == "f32":
+        bad = {k: v for k, v in worst.items() if v > GRAD_TOL_F32}
+    else:
+        bad = {k: v for k, v in worst.items() if v > (GRAD_TOL_POINTS if k.startswith("points_") else GRAD_TOL_MLP)}
     assert not bad, bad
 
 
