@@ -251,6 +251,26 @@ int sgn_aggregate_check_f32(const void *d_workspace, size_t workspace_bytes, sgn
 size_t sgn_aggregate_flag_offset_f32(size_t workspace_bytes);
 int64_t sgn_aggregate_fs_offset_f32(size_t workspace_bytes, int64_t S_capacity);
 
+/* ---- plain-fp32 aggregator (ABI 16): the f32 mode's range fallback -----------------------
+ * The same operator as sgn_aggregate_f32 (stages 1 + 2: alpha and colour of every work item,
+ * optional blend / wnorm), every nn.Linear as v_mfma_f32_16x16x4_f32 on fp32 operands (exact fp32
+ * products, fp32 sums) with the weights as the checkpoint holds them: no fp16 operand, so no range
+ * limit below fp32's.  For frames whose activations leave fp16 range (sgn_aggregate_check_f32 /
+ * the flag at sgn_aggregate_flag_offset_f32): the host re-runs them here instead of failing.  About
+ * 1/5 of the split path's rate.  Needs no point projection (block1.0 is computed per row in full).
+ *   sgn_mlp_pack_exact      : the 9 (+ block2_bpnet.0) layers in sgn_mlp_pack_f32's order -> fp32 blob of
+ *                             sgn_mlp_packed_bytes_exact(bpnet_layers, bpnet_dim) bytes (W^T per layer)
+ *   sgn_aggregate_exact     : workspace >= 1 KiB (1 KiB per work item of a chunk; a workspace holding
+ *                             S_capacity items runs one chunk); d_bpnet fp32 [N, 96] when bpnet_dim = 96;
+ *                             pt->pers / samp_pers optional as for sgn_aggregate_f32 */
+size_t sgn_mlp_packed_bytes_exact(int32_t bpnet_layers, int32_t bpnet_dim);
+int sgn_mlp_pack_exact(int32_t bpnet_layers, int32_t bpnet_dim, const float *const *w, const float *const *b,
+                       void *d_packed, sgn_stream_t stream);
+int sgn_aggregate_exact(int32_t bpnet_layers, int32_t bpnet_dim, const float *d_bpnet, const sgn_point_tables *pt,
+                        const sgn_query_out *q, int64_t S_capacity, int32_t K, const void *d_packed_exact,
+                        float *d_out_feat, float *d_out_blend, float *d_out_wnorm, void *d_workspace,
+                        size_t workspace_bytes, sgn_stream_t stream);
+
 /* sgn_point_project_f32 for the points d_idx[0 .. *d_count) only (int32 indices < n_points; the
  * count is a device int64): a training step re-projects the rows its rays touch after each weight
  * update instead of all N.  The other points' P rows and records are left as they are. */

@@ -170,6 +170,10 @@ SIGNATURES = {
     "sgn_aggregate_f32": (c_i32, [c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
     "sgn_aggregate_check_f32": (c_i32, [c_vp, c_sz, c_vp]),
+    "sgn_mlp_packed_bytes_exact": (c_sz, [c_i32, c_i32]),
+    "sgn_mlp_pack_exact": (c_i32, [c_i32, c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_vp, c_vp]),
+    "sgn_aggregate_exact": (c_i32, [c_i32, c_i32, c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64,
+                                    c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "sgn_aggregate_flag_offset_f32": (c_sz, [c_sz]),
     "sgn_aggregate_fs_offset_f32": (c_i64, [c_sz, c_i64]),
     "sgn_aggregate_train_fwd_f32": (c_i32, [c_vp, ctypes.POINTER(PointTables), ctypes.POINTER(QueryOut), c_i64, c_i32,

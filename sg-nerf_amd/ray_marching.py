@@ -297,6 +297,8 @@ class PointAggregator:
         # fp32 arithmetic (the reference's) unless opts say f16
         self.f32 = self.opts.precision == "f32"
         self.packed = pack_mlp(state, self.device, self.opts.precision)
+        self.state = state              # fp32 weights for the range fallback's plain-fp32 pack
+        self.packed_exact = None
 
     def forward(self, sampled_color, sampled_label_embedding, sampled_Rw2c, sampled_dir, sampled_conf,
                 sampled_embedding, sampled_xyz_pers, sampled_xyz, sample_pnt_mask, sample_loc, sample_loc_w,
@@ -371,7 +373,15 @@ class PointAggregator:
             _lib.check(L.sgn_aggregate_f32(nl, dim, _lib.ptr(bp), _lib.ptr(proj), ctypes.byref(pt), ctypes.byref(qo), S, K,
                                            _lib.ptr(self.packed), _lib.ptr(feat), None, _lib.ptr(wnorm), _lib.ptr(ws),
                                            ws.numel(), 3, st), "sgn_aggregate_f32")
-            _lib.check(L.sgn_aggregate_check_f32(_lib.ptr(ws), ws.numel(), st), "sgn_aggregate_f32 (fp16 range)")
+            # an activation outside fp16 range (the split path's limit, mlp_x3.hip): the same operator on the
+            # plain-fp32 path instead (sgn_aggregate_exact; the fp32 reference has no such limit)
+            off = int(L.sgn_aggregate_flag_offset_f32(ws.numel()))
+            if int(ws[off:off + 4].view(torch.int32).item()) != 0:
+                if getattr(self, "packed_exact", None) is None:
+                    self.packed_exact = pack_mlp(self.state, dev, "exact")
+                _lib.check(L.sgn_aggregate_exact(nl, dim, _lib.ptr(bp), ctypes.byref(pt), ctypes.byref(qo), S, K,
+                                                 _lib.ptr(self.packed_exact), _lib.ptr(feat), None, _lib.ptr(wnorm),
+                                                 _lib.ptr(ws), ws.numel(), st), "sgn_aggregate_exact")
             wnorm = torch.zeros_like(wnorm).scatter_(1, order, wnorm)   # back to the caller's slot order
         else:
             ws = torch.empty(int(L.sgn_aggregate_workspace_bytes(S)), dtype=torch.uint8, device=dev)

@@ -84,6 +84,10 @@ class HipRenderer:
                              f"{self.opts.bpnet_variant} (shading_feature_mlp_layer2_bpnet / predict_semantic)")
         self.f32 = self.opts.precision == "f32"
         self.packed = pack_mlp(self.mlp_state, self.device, self.opts.precision)
+        # f32 mode's range fallback: plain fp32 weights for sgn_aggregate_exact, packed on first use; `exact`
+        # turns on (for these weights) once a frame's activations left fp16 range
+        self.packed_exact = None
+        self.exact = False
 
     def _buffers(self, R):
         SR = self.opts.SR
@@ -103,36 +107,47 @@ class HipRenderer:
             self.blendw = None
             self._cap = (R, cap)
 
-    def _range_check(self, mode):
+    def _flag(self):
+        off = int(_lib.lib().sgn_aggregate_flag_offset_f32(self.agg_ws.numel()))
+        return self.agg_ws[off:off + 4].view(torch.int32)
+
+    def _range_check(self, mode, redo):
         """f32 mode: the colour stage flags samples whose decoded features are not finite (an
-        activation outside fp16 range, mlp_x3.hip header).  "sync": check now (one stream sync);
-        "deferred": copy the flag to pinned memory and check it after the NEXT frame has been
-        enqueued (or at finish()), so frames stay pipelined; False: no check."""
-        if not self.f32 or not mode:
+        activation outside fp16 range, mlp_x3.hip header).  "sync": check now (one stream sync) and,
+        when flagged, re-run the frame's aggregation and composite on the plain-fp32 path (`redo`,
+        sgn_aggregate_exact), which later frames then take directly; "deferred": copy the flag to
+        pinned memory and check it after the NEXT frame has been enqueued (or at finish()), so frames
+        stay pipelined -- a flagged frame raises there (its output was handed out already) and switches
+        the renderer to the plain-fp32 path; False: no check."""
+        if not self.f32 or not mode or self.exact:
             return
-        L = _lib.lib()
         if mode == "sync":
-            _lib.check(L.sgn_aggregate_check_f32(_lib.ptr(self.agg_ws), self.agg_ws.numel(), _lib.stream_handle()),
-                       "sgn_aggregate_check_f32")
+            flag = self._flag()
+            if int(flag.item()) != 0:
+                self.exact = True
+                flag.zero_()
+                redo()
             return
-        off = int(L.sgn_aggregate_flag_offset_f32(self.agg_ws.numel()))
         if self._flag_host is None:
             self._flag_host = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
         prev = self._pending.pop(0) if self._pending else None   # at most one frame is pending
         buf = self._flag_host[1] if prev is not None and prev[0] is self._flag_host[0] else self._flag_host[0]
-        buf.copy_(self.agg_ws[off:off + 4].view(torch.int32), non_blocking=True)
+        buf.copy_(self._flag(), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._pending.append((buf, ev))
         if prev is not None:
             self._raise_if_flagged(*prev)
 
-    @staticmethod
-    def _raise_if_flagged(buf, ev):
+    def _raise_if_flagged(self, buf, ev):
         ev.synchronize()
         if int(buf.item()) != 0:
+            self.exact = True   # every later frame on the plain-fp32 path
+            self._flag().zero_()
             raise _lib.SgnError("sgn_aggregate_f32: fp16 range exceeded -- an aggregator activation or point "
-                                "feature reached |x| >= 65504, so the decoded features of a frame are not finite")
+                                "feature reached |x| >= 65504, so the decoded features of a frame rendered with "
+                                "check_range='deferred' are not finite; the renderer now uses the plain-fp32 path "
+                                "(sgn_aggregate_exact): render that frame again")
 
     def finish(self):
         """Wait for the deferred range checks of the frames rendered so far (raises if one failed)."""
@@ -148,7 +163,8 @@ class HipRenderer:
         weights and the per-slot alpha-blend weights (reference `weight`, `blend_weight`).
         `point_labels` [N] / `ray_labels` [R] int32 (+ `seconds`): the SG semantic-guided kNN
         (semantic_guidance = 1, worldcoords.py:839-938).  `check_range`: the f32 mode's fp16-range
-        guard ("sync" default, "deferred" for pipelined frame loops + finish(), False)."""
+        guard ("sync" default: a frame whose activations leave fp16 range is re-rendered on the
+        plain-fp32 path, sgn_aggregate_exact; "deferred" for pipelined frame loops + finish(), False)."""
         o = self.opts
         mark = marks or (lambda name: None)
         campos = campos.reshape(3).to(self.device, torch.float32).contiguous()
@@ -178,22 +194,35 @@ class HipRenderer:
         if dim and self.points.bpnet16 is None:
             raise ValueError("block2_bpnet with predict_semantic = 1 needs the points' BPNet embedding (set_bpnet)")
         bp = (_lib.ptr(self.points.bpnet32) if self.f32 else _lib.ptr(self.points.bpnet16)) if dim else None
+        def aggregate_exact():
+            # the f32 mode's range fallback: the whole aggregator and colour MLP in plain fp32
+            if self.packed_exact is None:
+                self.packed_exact = pack_mlp(self.mlp_state, self.device, "exact")
+            _lib.check(L.sgn_aggregate_exact(nl, dim, bp, ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
+                                             _lib.ptr(self.packed_exact), _lib.ptr(self.feat),
+                                             _lib.ptr(self.blend) if want_blend else None,
+                                             _lib.ptr(self.wnorm) if want_weights else None, _lib.ptr(self.agg_ws),
+                                             self.agg_ws.numel(), _lib.stream_handle()), "sgn_aggregate_exact")
+
         # split block1.0: P[point] = W0a [feat | PE(feat)] + b0 for every point, once per frame
         mark("proj")
         nproj = int(L.sgn_point_proj_bytes_f32(self.points.n) if self.f32 else L.sgn_point_proj_bytes(self.points.n))
         if self._proj is None or self._proj.numel() < nproj:
             self._proj = torch.empty(max(nproj, 16), dtype=torch.uint8, device=self.device)
-        if self.f32:
+        if self.f32 and not self.exact:
             _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
                        "sgn_point_project_f32")
-        else:
+        elif not self.f32:
             _lib.check(L.sgn_point_project(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
                        "sgn_point_project")
         for stage, name in ((1, "agg_rows"), (2, "agg_color")):
             mark(name)
             blend = _lib.ptr(self.blend) if want_blend else None
             wnorm = _lib.ptr(self.wnorm) if want_weights and stage == 1 else None
-            if self.f32:
+            if self.exact:
+                if stage == 1:
+                    aggregate_exact()
+            elif self.f32:
                 _lib.check(L.sgn_aggregate_f32(nl, dim, bp, _lib.ptr(self._proj), ctypes.byref(pt), ctypes.byref(qo), cap, o.K,
                                                _lib.ptr(self.packed), _lib.ptr(self.feat), blend, wnorm,
                                                _lib.ptr(self.agg_ws), self.agg_ws.numel(), stage, st), "sgn_aggregate_f32")
@@ -208,13 +237,17 @@ class HipRenderer:
             bg = (1.0, 1.0, 1.0) if o.bg_color == "white" else (0.0, 0.0, 0.0)
         for i in range(3):
             cp.bg[i] = bg[i]
-        _lib.check(L.sgn_composite(ctypes.byref(cp), _lib.ptr(campos), _lib.ptr(rot), _lib.ptr(raydir), R,
-                                   _lib.ptr(q.t_table), q.per_ray_t, q.t_table.shape[-1], ctypes.byref(qo),
-                                   _lib.ptr(self.feat), _lib.ptr(self.rgb), _lib.ptr(self.mask), _lib.ptr(self.bgT),
-                                   _lib.ptr(self.opacity) if want_opacity else None,
-                                   _lib.ptr(self.blendw) if want_weights else None, st), "sgn_composite")
+
+        def composite():
+            _lib.check(L.sgn_composite(ctypes.byref(cp), _lib.ptr(campos), _lib.ptr(rot), _lib.ptr(raydir), R,
+                                       _lib.ptr(q.t_table), q.per_ray_t, q.t_table.shape[-1], ctypes.byref(qo),
+                                       _lib.ptr(self.feat), _lib.ptr(self.rgb), _lib.ptr(self.mask), _lib.ptr(self.bgT),
+                                       _lib.ptr(self.opacity) if want_opacity else None,
+                                       _lib.ptr(self.blendw) if want_weights else None, _lib.stream_handle()),
+                       "sgn_composite")
+        composite()
         mark("end")
-        self._range_check(check_range)
+        self._range_check(check_range, lambda: (aggregate_exact(), composite()))
         return RenderOut(self.rgb[:R], self.mask[:R], self.bgT[:R], self.opacity[:R], q, self.feat, self.blend,
                          self.wnorm if want_weights else None, self.blendw[:R] if want_weights else None)
 

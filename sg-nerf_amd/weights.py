@@ -91,13 +91,15 @@ def check_shapes(state):
 def pack_mlp(state, device, precision="f16"):
     """fp32 state -> packed MFMA fragment blob on `device` (uint8 tensor).  precision "f16":
     fp16 fragments (mlp.hip); "f32": (hi, lo) fp16 fragment pairs of 2^s-scaled weights plus
-    fp32 biases (mlp_x3.hip, the reference's fp32 arithmetic)."""
+    fp32 biases (mlp_x3.hip, the reference's fp32 arithmetic); "exact": plain fp32 W^T per layer
+    (exact.hip, the f32 mode's range fallback)."""
     state = strip_prefix(state)
     check_shapes(state)
     nl, dim = mlp_variant(state)
     layers = layers_for(nl, dim)
     L = _lib.lib()
-    nbytes = int(L.sgn_mlp_packed_bytes_f32(nl, dim) if precision == "f32" else L.sgn_mlp_packed_bytes_sg(nl, dim))
+    nbytes = int(L.sgn_mlp_packed_bytes_f32(nl, dim) if precision == "f32" else
+                 L.sgn_mlp_packed_bytes_exact(nl, dim) if precision == "exact" else L.sgn_mlp_packed_bytes_sg(nl, dim))
     out = torch.empty(nbytes, dtype=torch.uint8, device=device)
     ws = [np.ascontiguousarray(torch.as_tensor(state[n + ".weight"]).detach().cpu().float().numpy()) for n, *_ in layers]
     bs = [np.ascontiguousarray(torch.as_tensor(state[n + ".bias"]).detach().cpu().float().numpy()) for n, *_ in layers]
@@ -111,6 +113,8 @@ def pack_mlp(state, device, precision="f16"):
     with torch.cuda.device(device):
         if precision == "f32":
             _lib.check(L.sgn_mlp_pack_f32(nl, dim, wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_f32")
+        elif precision == "exact":   # plain fp32 W^T for the range fallback (sgn_aggregate_exact)
+            _lib.check(L.sgn_mlp_pack_exact(nl, dim, wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_exact")
         else:
             _lib.check(L.sgn_mlp_pack_sg(nl, dim, wp, bp, _lib.ptr(out), _lib.stream_handle()), "sgn_mlp_pack_sg")
     return out

@@ -111,6 +111,18 @@ def test_argument_errors_are_reported_without_gpu():
     assert rc != 0 and b"K = 1 .. 8" in L.sgn_last_error()
     rc = L.sgn_point_project_f32_subset(ctypes.byref(pt), fake, None, fake, fake, None)
     assert rc != 0 and b"null" in L.sgn_last_error()
+    # plain-fp32 range fallback: K, the SG variant, the workspace
+    rc = L.sgn_aggregate_exact(0, 0, None, ctypes.byref(pt), ctypes.byref(qo), 64, 9, fake, fake, None, None, fake,
+                               1 << 20, None)
+    assert rc != 0 and b"K = 1 .. 8" in L.sgn_last_error()
+    rc = L.sgn_aggregate_exact(1, 64, None, ctypes.byref(pt), ctypes.byref(qo), 64, 8, fake, fake, None, None, fake,
+                               1 << 20, None)
+    assert rc != 0 and b"block2_bpnet" in L.sgn_last_error()
+    rc = L.sgn_aggregate_exact(0, 0, None, ctypes.byref(pt), ctypes.byref(qo), 64, 8, fake, fake, None, None, fake,
+                               512, None)
+    assert rc != 0 and b"workspace" in L.sgn_last_error()
+    assert L.sgn_mlp_packed_bytes_exact(0, 0) >= 4 * N_PARAMS and L.sgn_mlp_packed_bytes_exact(2, 0) == 0
+    assert L.sgn_mlp_packed_bytes_exact(1, 96) > L.sgn_mlp_packed_bytes_exact(1, 0) > L.sgn_mlp_packed_bytes_exact(0, 0)
     # training loss stage: null pointers, SR / K, the workspace size
     lp = _lib.LossParams()
     lp.SR, lp.K = 24, 8

@@ -427,6 +427,37 @@ struct EpiC {
         constexpr int T = decltype(tc)::value;''', '''    auto epi_step = [&](Epi16 &e, const char *ldsi, const f32x4 (&ac)[16], auto tc) {
         constexpr int T = decltype(tc)::value;
         if constexpr (KB == 0 && !SAVE) { e.fsv[T & 3] = ac[T][0]; if constexpr ((T & 3) == 3) { if (e.fs_have) e.fs_dst[16 * (T - 3)] = e.fsv[0] + e.fsv[1] + e.fsv[2] + e.fsv[3]; } return; }''')
+    elif p == "e_order":
+        # MFMA order of a (k-step, tile) across the row sets grouped by weight fragment: (lo, hi_s) for every
+        # row set, then (hi, lo_s), then (hi, hi_s) -- each accumulator sees the same three products in the
+        # same order as before (bit-identical), the weight operand changes twice per 3 NS MFMAs
+        s = rep(s, '''#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    f32x4 &c = acc[s][AOFF + t];
+                    if constexpr (TRANS) {
+                        c = mfma16(B.b[s].hi, Al, c);
+                        c = mfma16(B.b[s].lo, Ah, c);
+                        c = mfma16(B.b[s].hi, Ah, c);
+                    } else {
+                        c = mfma16(Al, B.b[s].hi, c);
+                        c = mfma16(Ah, B.b[s].lo, c);
+                        c = mfma16(Ah, B.b[s].hi, c);
+                    }
+                }''', '''if constexpr (TRANS) {
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) acc[s][AOFF + t] = mfma16(B.b[s].hi, Al, acc[s][AOFF + t]);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) acc[s][AOFF + t] = mfma16(B.b[s].lo, Ah, acc[s][AOFF + t]);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) acc[s][AOFF + t] = mfma16(B.b[s].hi, Ah, acc[s][AOFF + t]);
+                } else {
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) acc[s][AOFF + t] = mfma16(Al, B.b[s].hi, acc[s][AOFF + t]);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) acc[s][AOFF + t] = mfma16(Ah, B.b[s].lo, acc[s][AOFF + t]);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) acc[s][AOFF + t] = mfma16(Ah, B.b[s].hi, acc[s][AOFF + t]);
+                }''')
     elif p == "abl_pe":
         s = rep(s, '''                    for (int q = 0; q < NS; ++q) o.b[q] = pe_dists16_k<decltype(k)::value>(pr[q]);''',
                 '''                    for (int q = 0; q < NS; ++q) {
