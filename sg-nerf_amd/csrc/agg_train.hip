@@ -60,9 +60,35 @@ struct BwdArgs {
     _Float16 *db;              // SG: [rows][256] scaled block2_bpnet deltas (chain order)
 };
 
-__device__ __forceinline__ h8 load_frag(const _Float16 *base, int C, int64_t row0, int s, int lane, bool ok) {
-    if (!ok) return h8{};
-    return *(const h8 *)(base + (row0 + (lane & 31)) * C + s * 16 + (lane >> 5) * 8);
+// A wave's window onto rows [row0, row0 + 32) of a [rows][C] fp16 tile: the descriptor's range ends
+// at the last row of a work item (rows of items past the end read 0 and drop their stores), so the
+// epilogues load and store without a branch per fragment (a branch around each load made hipcc wait
+// vmcnt(0) per fragment: 8 dependent round trips per product).
+struct Tile {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t lo;  // lane offset (lane & 31) * C * 2 + (lane >> 5) * 16
+    __device__ __forceinline__ h8 load(int s) const {
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, lo, s * 32, 0));
+    }
+    __device__ __forceinline__ void store(int s, h8 v) const {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, lo, s * 32, 0);
+    }
+};
+// buffer descriptor of a wave-uniform range (readfirstlane keeps it in SGPRs: a VGPR descriptor
+// is a waterfall loop around every access)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_u(const void *ptr, int bytes) {
+    const uint64_t p = (uint64_t)ptr;
+    const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)p), phi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)phi << 32) | plo), (short)0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// nrow: rows of this wave's tile that belong to work items (a multiple of 8, wave-uniform)
+__device__ __forceinline__ Tile tile_of(const _Float16 *base, int C, int64_t row0, int nrow, int lane) {
+    Tile t;
+    t.r = rsrc_u(base + row0 * C, nrow * C * 2);
+    t.lo = (uint32_t)((lane & 31) * C * 2 + (lane >> 5) * 16);
+    return t;
 }
 
 // delta (fp32 accumulator registers 8 s2 .. 8 s2 + 7) * LReLU'(h) with h the saved fp16 fragment
@@ -84,9 +110,9 @@ __device__ __forceinline__ h8 plain_frag(const f32x16 &acc, int s2) {
 // The workgroup's 4 waves (one per SIMD) run the same sequence of 12 weight products per tile
 // on different rows.  Each product's NT x 16 fragments are staged once per workgroup in LDS by
 // LDS-DMA and read there by all four waves; two slots, the next product's DMA in flight while
-// the current one multiplies (the forward's ring protocol: boundary = vmcnt(0) + barrier, then
-// issue the next DMA into the slot read one product ago).  Read one by one from L2 instead, the
-// MFMAs waited on every fragment (one wave per SIMD, ~5 % of the MFMA rate).
+// the current one multiplies (boundary = counted vmcnt + raw barrier, then issue the next DMA
+// into the slot read one product ago).  Read one by one from L2 instead, the MFMAs waited on
+// every fragment (one wave per SIMD, ~5 % of the MFMA rate).
 constexpr int BWD_TPB = 256;
 constexpr int BWD_SLOT = 4 * 16 * (int)FRAG;  // the largest product: 4 tiles x 16 k-steps
 constexpr int BWD_LDS = 2 * BWD_SLOT;
@@ -120,31 +146,93 @@ __device__ __forceinline__ void prod_dma(char *lds, const WBlob &wb, const WBlob
     }
 }
 
-// acc[t] (+)= sum_ks W_I(t, ks) * in[ks]; `more`: the workgroup has another tile (the last
-// product's successor is the next tile's product 0)
-template <int I, int NT, bool SG = false>
+// LDS: the two weight slots, then one 8 KB region per wave (MR): at a tile's start this wave's
+// d f_s rows (4 items x 1 KB, rows MR_DFS apart so the items' lanes read different banks) and its
+// copy of block3.2's bias and the alpha weight; from product 2 on, the saved activations whose
+// LReLU' masks the current product's epilogue (8 fragments, LDS-DMA'd with the product's weights
+// instead of loaded to registers in the epilogue: hipcc waits vmcnt(0) -- the weight DMA in flight
+// included -- at every use of a global load while a DMA is outstanding).  One LDS array: a second
+// __shared__ object makes hipcc wait vmcnt(0) for the DMA before every LDS read.
+constexpr int MRW = 8192;
+constexpr int MR_DFS = 1040;
+constexpr int MR_F = 4 * MR_DFS;  // b3 [256] fp32, then wa [256]
+static_assert(MR_F + 2 * HID * 4 <= MRW, "per-wave region");
+constexpr int BWD_LDS_ALL = BWD_LDS + 4 * MRW;  // 160 KB: the CU's whole LDS
+
+// Product boundary: this wave's DMA pieces of product I have landed -- the VM vector-memory
+// operations it issued after them (the previous epilogue's stores) may stay in flight, vmcnt
+// retires in order -- and its LDS reads are done; then the barrier (every wave's pieces landed,
+// every wave done with the slot the next DMA overwrites).  Not __syncthreads(): its fence waits
+// vmcnt(0), draining the stores.
+template <int VM>
+__device__ __forceinline__ void boundary() {
+    static_assert(VM >= 0 && VM < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(VM) : "memory");
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *dst, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)dst, 16, voff, soff, 0, 0);
+}
+
+// the 8 saved fragments k0 .. k0 + 7 of this wave's tile -> its region, fragment k0 + i at i KB
+__device__ __forceinline__ void mask_dma(char *mr, const Tile &t, int k0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dma16(t.r, mr + i * 1024, t.lo, (uint32_t)(k0 + i) * 32);
+}
+
+// acc[t] (+)= sum_ks W_I(t, ks) * in[ks].  VM: boundary allowance (the stores of product I - 1's
+// epilogue); mask: the tile whose fragments k0 .. k0 + 7 product I's epilogue reads from the
+// region; `more`: the workgroup has another tile (the last product's successor is the next tile's
+// product 0)
+template <int I, int NT, bool SG, int VM>
 __device__ __forceinline__ void prod_mul(char *lds, const WBlob &wb, const WBlob &tb, const h8 (&in)[16],
-                                         f32x16 (&acc)[NT], int w, int lane, bool more) {
+                                         f32x16 (&acc)[NT], int w, int lane, bool more,
+                                         const Tile *mask = nullptr, int k0 = 0) {
     static_assert(NT == prod_nt(I, SG), "product width");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of product I landed
-    __syncthreads();  // everyone's, and everyone is done with product I - 1's slot
+    boundary<VM>();
+    if (mask) mask_dma(lds + BWD_LDS + w * MRW, *mask, k0);
+    asm volatile("" ::: "memory");  // the masks' pieces stay older than the weights' (mask_wait counts)
     if constexpr (I + 1 < n_prod(SG)) prod_dma<I + 1, SG>(lds, wb, tb, w, lane);
     else if (more) prod_dma<0, SG>(lds, wb, tb, w, lane);
-    const char *sl = lds + (I & 1) * BWD_SLOT;
+    asm volatile("" ::: "memory");  // and the epilogue's stores younger than both (boundary counts)
+    // opaque per product: hipcc hoisted every fragment's address out of the tile loop into its own
+    // VGPR (64 of them); one base VGPR + the read's 16-bit immediate offset instead
+    uint32_t voff = (uint32_t)((I & 1) * BWD_SLOT + lane * 16);
+    asm volatile("" : "+v"(voff));
+    const char *sl = lds + voff;
+    // fragment n = ks * NT + t read PF ahead of its MFMA: one read in flight per MFMA left the MFMAs
+    // waiting out the LDS latency one by one (the scheduler, short of registers, chose that)
+    constexpr int NF = 16 * NT, PF = 4;
+    h8 fr[NF];
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks)
+    for (int n = 0; n < PF; ++n) fr[n] = *(const h8 *)(sl + n * (int)FRAG);
+    // program order pinned (sched_barrier after each pair): the scheduler otherwise regrouped the
+    // MFMAs by accumulator -- a dependent chain -- each behind its own read
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-            acc[t] = mfma32(*(const h8 *)(sl + (ks * NT + t) * (int)FRAG + lane * 16), in[ks], acc[t]);
+    for (int n = 0; n < NF; ++n) {
+        if (n + PF < NF) fr[n + PF] = *(const h8 *)(sl + (n + PF) * (int)FRAG);
+        acc[n % NT] = mfma32(fr[n], in[n / NT], acc[n % NT]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 // acc[t] = sum_ks T[t0 + t][ks] * in[ks] for the NT row tiles of transposed product I
-template <int I, int NT, bool SG = false>
+template <int I, int NT, bool SG, int VM>
 __device__ __forceinline__ void tmul(char *lds, const WBlob &wb, const WBlob &tb, const h8 (&in)[16],
-                                     f32x16 (&acc)[NT], int w, int lane, bool more) {
+                                     f32x16 (&acc)[NT], int w, int lane, bool more, const Tile *mask = nullptr,
+                                     int k0 = 0) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
-    prod_mul<I, NT, SG>(lds, wb, tb, in, acc, w, lane, more);
+    prod_mul<I, NT, SG, VM>(lds, wb, tb, in, acc, w, lane, more, mask, k0);
+}
+
+// product I's epilogue reads its masks: the DMA pieces issued after them (product I + 1's
+// weights, 4 per row tile) may stay in flight
+template <int I, bool SG>
+__device__ __forceinline__ void mask_wait() {
+    static_assert(I + 1 < n_prod(SG), "a masked product has a successor in the tile");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * prod_nt(I + 1, SG)) : "memory");
 }
 
 // d feat[c] contribution of layer-0 local channel C (mlp_layout.h l0 order): PE(feat) chain rule
@@ -161,182 +249,205 @@ __device__ __forceinline__ void l0_backward(float d, const float (&feat)[16], fl
     // C >= 112: PE(dists) -> point xyz / sample positions (not trained)
 }
 
+// one masked product pair's epilogue: delta = acc * LReLU'(saved), kept for the next product and stored
+template <int P>
+__device__ __forceinline__ void masked_epilogue(const char *lds, int w, const f32x16 (&ac)[4], h8 (&out)[16],
+                                                const Tile &dst, int lane) {
+    uint32_t voff = (uint32_t)(BWD_LDS + w * MRW + lane * 16);
+    asm volatile("" : "+v"(voff));
+    const char *mr = lds + voff;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int i = 2 * tt + s2, k = 8 * P + i;
+            out[k] = mask_frag(ac[tt], s2, *(const h8 *)(mr + i * 1024));
+            dst.store(k, out[k]);
+        }
+}
+
 template <bool SG>
 __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
     constexpr int IW1 = prod_w1(SG), IW0 = prod_w0(SG);
-    __shared__ __attribute__((aligned(16))) char lds[BWD_LDS];
+    __shared__ __attribute__((aligned(16))) char lds[BWD_LDS_ALL];
     const AggArgs &a = b.a;
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, j = lane & 31, q = j >> 3;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    char *mr = lds + BWD_LDS + w * MRW;
     const Cam cam = load_cam(a.campos, a.rot);
     const WBlob wb = make_blob(a.blob, a.blob_bytes);
     const WBlob tb = make_blob(b.tblob, T_BYTES);
-    const float *F = (const float *)((const char *)a.blob + OFF_F32);
+    const float ba = ((const float *)((const char *)a.blob + OFF_F32))[F_BA];
     const float scale = *b.scale, inv = 1.f / scale;
     const int end = b.n_items;
     if (blockIdx.x * 16 < end) prod_dma<0, SG>(lds, wb, tb, w, lane);  // stream prologue
     // trip count uniform over the workgroup (its waves meet at the staging barriers); rows past
-    // the end are masked (ok = false)
+    // the end are masked (ok = false) and out of the tiles' range
     for (int bbase = blockIdx.x * 16; bbase < end; bbase += gridDim.x * 16) {
         const int base = bbase + w * 4;
         const bool more = bbase + (int)gridDim.x * 16 < end;
         const int item = base + q;
         const int64_t row0 = (int64_t)base * 8;
+        const int nrow = min(max(end - base, 0), 4) * 8;
+        // this wave's d f_s rows and the fp32 constants -> its region (landed at product 0's boundary;
+        // the region's last readers, the previous tile's block1.2 epilogue, are past 3 boundaries)
+        {
+            const __amdgpu_buffer_rsrc_t rd = rsrc_u(b.dfs + (int64_t)base * HID, nrow / 8 * HID * 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dma16(rd, mr + i * MR_DFS, lane * 16, i * HID * 4);
+            dma16(wb.rsrc, mr + MR_F, lane * 16, (uint32_t)(OFF_F32 + F_B3 * 4));
+            dma16(wb.rsrc, mr + MR_F + HID * 4, lane * 16, (uint32_t)(OFF_F32 + F_WA * 4));
+        }
         float feat[16], dist[3];
         h8 ext;
-        const RowIn ri = gather_row(a, cam, item, end, lane, feat, dist, ext);
+        const RowIdx ix = row_index(a, item, end, lane);
+        const RowIn ri = gather_row(a, cam, ix, lane, feat, dist, ext);
         const bool ok = ri.sval;
         const int it = ok ? item : 0;
+        // this row's ray direction (the dir gradient of product 6), loaded with the gather
+        const float vr[3] = {a.raydir[(int64_t)ix.ray * 3], a.raydir[(int64_t)ix.ray * 3 + 1],
+                             a.raydir[(int64_t)ix.ray * 3 + 2]};
+        const float dal = b.dalpha[it];
+        const Tile t3 = tile_of(b.sh3, 256, row0, nrow, lane);
         // ---- recompute block3.2: z4 = W3 h3 + b3 ------------------------------------------
         f32x16 acc[8];
         {
             h8 x3[16];
 #pragma unroll
-            for (int s = 0; s < 16; ++s) x3[s] = load_frag(b.sh3, 256, row0, s, lane, ok);
+            for (int s = 0; s < 16; ++s) x3[s] = t3.load(s);
 #pragma unroll
             for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
-            prod_mul<0, 4, SG>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[0], w, lane, more);
-            prod_mul<1, 4, SG>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[4], w, lane, more);
+            prod_mul<0, 4, SG, 0>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[0], w, lane, more);
+            prod_mul<1, 4, SG, 0>(lds, wb, tb, x3, *(f32x16(*)[4])&acc[4], w, lane, more);
         }
         // ---- pass 1: h4, alpha logit, <h4, d f_s> ------------------------------------------
-        const float *dfs = b.dfs + (int64_t)it * HID;
+        const float *dfl = (const float *)(mr + q * MR_DFS);
+        const float *Fb3 = (const float *)(mr + MR_F), *Fwa = Fb3 + HID;
         float za = 0.f, dwv = 0.f;
 #pragma unroll
         for (int t = 0; t < 8; ++t)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int u0 = 32 * t + 8 * g + 4 * h;
-                const f32x4 df4 = *(const f32x4 *)(dfs + u0);
+                const f32x4 df4 = *(const f32x4 *)(dfl + u0);
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const int r = 4 * g + c, u = u0 + c;
-                    const float z = acc[t][r] + F[F_B3 + u];
+                    const float z = acc[t][r] + Fb3[u];
                     const float hv = z > 0.f ? z : 0.01f * z;
                     acc[t][r] = hv;
-                    za = fmaf(F[F_WA + u], hv, za);
+                    za = fmaf(Fwa[u], hv, za);
                     dwv = fmaf(hv, df4[c], dwv);
                 }
             }
-        za += __shfl_xor(za, 32) + F[F_BA];
+        za += __shfl_xor(za, 32) + ba;
         dwv = (dwv + __shfl_xor(dwv, 32)) * scale;
         const float x1 = za - 1.f;
         const float alpha_row = softplus(x1);
         const float sig = 1.f / (1.f + expf(-x1));
-        const float das = ok ? b.dalpha[it] * scale : 0.f;
+        const float das = ok ? dal * scale : 0.f;
         const float wgt = ri.wgt;  // 0 for masked neighbours and padding rows
         const float dz = wgt * das * sig;
         const float dwgt = dwv + alpha_row * das;  // scaled d loss / d (weight * conf) of this row
-        // ---- pass 2: delta4 = (w d f_s + dz wa) * LReLU'(z4); save h4 / delta4 ---------------
+        // ---- pass 2: delta4 = (w d f_s + dz wa) * LReLU'(z4); save h4 / delta4 (33 stores) ----
         h8 dl[16];
+        {
+            const Tile th4 = tile_of(b.h4, 256, row0, nrow, lane), td4 = tile_of(b.d4, 256, row0, nrow, lane);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            f32x16 dv;
+            for (int t = 0; t < 8; ++t) {
+                f32x16 dv;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int u0 = 32 * t + 8 * g + 4 * h;
-                const f32x4 df4 = *(const f32x4 *)(dfs + u0);
+                for (int g = 0; g < 4; ++g) {
+                    const int u0 = 32 * t + 8 * g + 4 * h;
+                    const f32x4 df4 = *(const f32x4 *)(dfl + u0);
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int r = 4 * g + c, u = u0 + c;
-                    const float hv = acc[t][r];
-                    const float d = fmaf(wgt * scale, df4[c], dz * F[F_WA + u]);
-                    dv[r] = hv > 0.f ? d : 0.01f * d;
+                    for (int c = 0; c < 4; ++c) {
+                        const int r = 4 * g + c, u = u0 + c;
+                        const float hv = acc[t][r];
+                        const float d = fmaf(wgt * scale, df4[c], dz * Fwa[u]);
+                        dv[r] = hv > 0.f ? d : 0.01f * d;
+                    }
                 }
-            }
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                dl[2 * t + s2] = plain_frag(dv, s2);
-                save_frag(b.h4, 256, row0, 2 * t + s2, plain_frag(acc[t], s2), lane, ok);
-                save_frag(b.d4, 256, row0, 2 * t + s2, dl[2 * t + s2], lane, ok);
-            }
-        }
-        if (ok && h == 0) b.dza[row0 + j] = dz;
-        // ---- block3.2 backward: delta3 = (W3^T delta4) * LReLU'(h3) ----------------------
-        h8 dn[16];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-            f32x16 ac[4];
-            if (p == 0) tmul<2, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
-            else tmul<3, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
-                    const int k = 2 * (4 * p + tt) + s2;
-                    dn[k] = mask_frag(ac[tt], s2, load_frag(b.sh3, 256, row0, k, lane, ok));
-                    save_frag(b.d3, 256, row0, k, dn[k], lane, ok);
+                    dl[2 * t + s2] = plain_frag(dv, s2);
+                    th4.store(2 * t + s2, plain_frag(acc[t], s2));
+                    td4.store(2 * t + s2, dl[2 * t + s2]);
                 }
+            }
+            // lane-half 1 stores out of range (dropped): one store instruction either way
+            const __amdgpu_buffer_rsrc_t rz = rsrc_u(b.dza + row0, nrow * 4);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dz), rz, h ? 0x40000000u : j * 4u, 0, 0);
+        }
+        // ---- block3.2 backward: delta3 = (W3^T delta4) * LReLU'(h3) ----------------------
+        h8 dn[16];
+        {
+            const Tile td3 = tile_of(b.d3, 256, row0, nrow, lane);
+            f32x16 ac[4];
+            tmul<2, 4, SG, 33>(lds, wb, tb, dl, ac, w, lane, more, &t3, 0);
+            mask_wait<2, SG>();
+            masked_epilogue<0>(lds, w, ac, dn, td3, lane);
+            tmul<3, 4, SG, 8>(lds, wb, tb, dl, ac, w, lane, more, &t3, 8);
+            mask_wait<3, SG>();
+            masked_epilogue<1>(lds, w, ac, dn, td3, lane);
         }
         // ---- block3.0 backward: delta2 = (W2^T delta3)[:256] * LReLU'(h2); ext grads -------
         // (SG: h2 is the block2_bpnet output, so this is block2_bpnet's delta, saved to db)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
+        {
+            const Tile t2 = tile_of(b.sh2, KS_L2 * 16, row0, nrow, lane);
+            const Tile td2 = tile_of(SG ? b.db : b.d2, 256, row0, nrow, lane);
             f32x16 ac[4];
-            if (p == 0) tmul<4, 4, SG>(lds, wb, tb, dn, ac, w, lane, more);
-            else tmul<5, 4, SG>(lds, wb, tb, dn, ac, w, lane, more);
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    const int k = 2 * (4 * p + tt) + s2;
-                    dl[k] = mask_frag(ac[tt], s2, load_frag(b.sh2, KS_L2 * 16, row0, k, lane, ok));
-                    save_frag(SG ? b.db : b.d2, 256, row0, k, dl[k], lane, ok);
-                }
+            tmul<4, 4, SG, 8>(lds, wb, tb, dn, ac, w, lane, more, &t2, 0);
+            mask_wait<4, SG>();
+            masked_epilogue<0>(lds, w, ac, dl, td2, lane);
+            tmul<5, 4, SG, 8>(lds, wb, tb, dn, ac, w, lane, more, &t2, 8);
+            mask_wait<5, SG>();
+            masked_epilogue<1>(lds, w, ac, dl, td2, lane);
         }
         {
             f32x16 ae[1];
-            tmul<6, 1, SG>(lds, wb, tb, dn, ae, w, lane, more);
+            tmul<6, 1, SG, 8>(lds, wb, tb, dn, ae, w, lane, more);
             // tile 8 = inputs 256..262: half 0 regs 0..3 -> colour 0..2, (dir - v)_0;
             // half 1 regs 0..2 -> (dir - v)_1, (dir - v)_2, <dir, v>   (:639-652)
             const float o0 = __shfl_xor(ae[0][0], 32), o1 = __shfl_xor(ae[0][1], 32), o2 = __shfl_xor(ae[0][2], 32);
             if (ok && ri.pid >= 0 && h == 0) {
-                const int ray = a.samp_ray[ri.s];
-                const float v[3] = {a.raydir[(int64_t)ray * 3], a.raydir[(int64_t)ray * 3 + 1],
-                                    a.raydir[(int64_t)ray * 3 + 2]};
                 const float ddiff[3] = {ae[0][3], o0, o1};
                 const int64_t pb = (int64_t)ri.pid * 3;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     atomicAdd(b.g_color + pb + c, ae[0][c] * inv);
-                    atomicAdd(b.g_dir + pb + c, fmaf(o2, v[c], ddiff[c]) * inv);
+                    atomicAdd(b.g_dir + pb + c, fmaf(o2, vr[c], ddiff[c]) * inv);
                 }
                 atomicAdd(b.g_conf + ri.pid, dwgt * ri.wn * inv);  // straight-through clamp (:863-865)
             }
         }
+        // (the atomics are conditional: the next boundary drains vmcnt)
         // ---- SG block2_bpnet backward: delta2 = (W_B[:, :256]^T delta_B) * LReLU'(h) ------
         if constexpr (SG) {
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                f32x16 ac[4];
-                if (p == 0) tmul<7, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
-                else tmul<8, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
-#pragma unroll
-                for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) {
-                        const int k = 2 * (4 * p + tt) + s2;
-                        dn[k] = mask_frag(ac[tt], s2, load_frag(b.sh2b, 256, row0, k, lane, ok));
-                        save_frag(b.d2, 256, row0, k, dn[k], lane, ok);
-                    }
-            }
+            const Tile tb2 = tile_of(b.sh2b, 256, row0, nrow, lane);
+            const Tile td2 = tile_of(b.d2, 256, row0, nrow, lane);
+            f32x16 ac[4];
+            tmul<7, 4, SG, 0>(lds, wb, tb, dl, ac, w, lane, more, &tb2, 0);
+            mask_wait<7, SG>();
+            masked_epilogue<0>(lds, w, ac, dn, td2, lane);
+            tmul<8, 4, SG, 8>(lds, wb, tb, dl, ac, w, lane, more, &tb2, 8);
+            mask_wait<8, SG>();
+            masked_epilogue<1>(lds, w, ac, dn, td2, lane);
 #pragma unroll
             for (int k = 0; k < 16; ++k) dl[k] = dn[k];
         }
         // ---- block1.2 backward: delta1 = (W1^T delta2) * LReLU'(h1) ----------------------
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
+        {
+            const Tile t1 = tile_of(b.sh1, 256, row0, nrow, lane);
+            const Tile td1 = tile_of(b.d1, 256, row0, nrow, lane);
             f32x16 ac[4];
-            if (p == 0) tmul<IW1, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
-            else tmul<IW1 + 1, 4, SG>(lds, wb, tb, dl, ac, w, lane, more);
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    const int k = 2 * (4 * p + tt) + s2;
-                    dn[k] = mask_frag(ac[tt], s2, load_frag(b.sh1, 256, row0, k, lane, ok));
-                    save_frag(b.d1, 256, row0, k, dn[k], lane, ok);
-                }
+            tmul<IW1, 4, SG, SG ? 8 : 0>(lds, wb, tb, dl, ac, w, lane, more, &t1, 0);
+            mask_wait<IW1, SG>();
+            masked_epilogue<0>(lds, w, ac, dn, td1, lane);
+            tmul<IW1 + 1, 4, SG, 8>(lds, wb, tb, dl, ac, w, lane, more, &t1, 8);
+            mask_wait<IW1 + 1, SG>();
+            masked_epilogue<1>(lds, w, ac, dn, td1, lane);
         }
         // ---- block1.0 backward: d x0 = W0^T delta1 -> d feat through PE(feat) --------------
         float dfe[16];
@@ -345,7 +456,7 @@ __global__ __launch_bounds__(BWD_TPB) void k_agg_bwd(BwdArgs b) {
         static_for<3>([&](auto pp) {
             constexpr int P = decltype(pp)::value;
             f32x16 ac[3];
-            tmul<IW0 + P, 3, SG>(lds, wb, tb, dn, ac, w, lane, more);
+            tmul<IW0 + P, 3, SG, P == 0 ? 8 : 0>(lds, wb, tb, dn, ac, w, lane, more);
             static_for<3>([&](auto ttc) {
                 constexpr int T = 3 * P + decltype(ttc)::value;
                 static_for<16>([&](auto rr) {
