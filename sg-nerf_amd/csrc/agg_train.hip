@@ -132,18 +132,28 @@ __host__ __device__ constexpr uint32_t prod_off(int I, int ks, int t, bool sg = 
                                       : OFF_T0 + ((size_t)((I - prod_w0(sg)) * 3 + t) * 16 + ks) * FRAG);
 }
 
+// A product's NT x 16 fragments are contiguous in their blob (prod_off(I, 0, 0) on), W3 k-step-major,
+// the transposed layers row-tile-major; the slot mirrors that order, so fragment (ks, t) sits at
+// slot index prod_m(I, ks, t) and the DMA piece i of wave w moves index w + 4 i.
+template <int I, bool SG = false>
+__host__ __device__ constexpr int prod_m(int ks, int t) { return I < 2 ? ks * prod_nt(I, SG) + t : t * 16 + ks; }
+
 template <int I, bool SG = false>
 __device__ __forceinline__ void prod_dma(char *lds, const WBlob &wb, const WBlob &tb, int w, int lane) {
     constexpr int NT = prod_nt(I, SG), NF = 16 * NT;
     static_assert(NF % 4 == 0 && NF * (int)FRAG <= BWD_SLOT, "staging slot");
     const WBlob &src = I < 2 ? wb : tb;
-    char *dst = lds + (I & 1) * BWD_SLOT;
+    // wo: this wave's first index in bytes, opaque per product, so each piece's LDS address and blob
+    // offset are one SALU add here (hoisted out of the tile loop, the pieces' addresses were spilled to
+    // VGPR lanes and read back with a readlane and hazard nops each)
+    uint32_t wo = (uint32_t)w * (uint32_t)FRAG;
+    asm volatile("" : "+s"(wo));
+    char *dst = lds + (I & 1) * BWD_SLOT + wo;
+    const uint32_t src0 = (uint32_t)prod_off(I, 0, 0, SG) + wo;
 #pragma unroll
-    for (int i = 0; i < NF / 4; ++i) {
-        const int n = w + 4 * i;  // fragment n = (ks, t) = (n / NT, n % NT)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rsrc, (__attribute__((address_space(3))) void *)(dst + n * (int)FRAG),
-                                                 16, lane * 16, prod_off(I, n / NT, n % NT, SG), 0, 0);
-    }
+    for (int i = 0; i < NF / 4; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src.rsrc, (__attribute__((address_space(3))) void *)(dst + 4 * i * (int)FRAG),
+                                                 16, lane * 16, src0 + 4 * i * (uint32_t)FRAG, 0, 0);
 }
 
 // LDS: the two weight slots, then one 8 KB region per wave (MR): at a tile's start this wave's
@@ -205,13 +215,16 @@ __device__ __forceinline__ void prod_mul(char *lds, const WBlob &wb, const WBlob
     constexpr int NF = 16 * NT, PF = 4;
     h8 fr[NF];
 #pragma unroll
-    for (int n = 0; n < PF; ++n) fr[n] = *(const h8 *)(sl + n * (int)FRAG);
+    for (int n = 0; n < PF; ++n) fr[n] = *(const h8 *)(sl + prod_m<I, SG>(n / NT, n % NT) * (int)FRAG);
     // program order pinned (sched_barrier after each pair): the scheduler otherwise regrouped the
     // MFMAs by accumulator -- a dependent chain -- each behind its own read
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int n = 0; n < NF; ++n) {
-        if (n + PF < NF) fr[n + PF] = *(const h8 *)(sl + (n + PF) * (int)FRAG);
+        if (n + PF < NF) {
+            const int m = n + PF;
+            fr[m] = *(const h8 *)(sl + prod_m<I, SG>(m / NT, m % NT) * (int)FRAG);
+        }
         acc[n % NT] = mfma32(fr[n], in[n / NT], acc[n % NT]);
         __builtin_amdgcn_sched_barrier(0);
     }
