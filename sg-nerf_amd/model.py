@@ -199,8 +199,11 @@ class HipPointsVolumetricModel:
         self.setup_optimizer(opt)
 
     def _sync_weights(self):
-        """Trained aggregator weights -> the renderer's packed blob (once per change)."""
+        """Trained aggregator weights -> the renderer's packed blob (once per change); every point
+        row brought to the optimizer's step (the row-sparse point Adam defers untouched rows)."""
         tr = getattr(self, "trainer", None)
+        if tr is not None:
+            tr.sync_points()
         if tr is not None and getattr(self, "_weights_dirty", False):
             self.net_ray_marching.set_aggregator_state(tr.mlp_state())
         self._weights_dirty = False

@@ -428,7 +428,7 @@ def _allreduce_point_rows(grads, idx=None, counts=None):
     non-zero gradient rows here, at the cost of two host syncs.  Every row outside idx must
     hold a zero gradient (true of both sources)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return
+        return None
     n = dist.get_world_size()
     dev = grads[0].device
     N = grads[0].shape[0]
@@ -463,6 +463,7 @@ def _allreduce_point_rows(grads, idx=None, counts=None):
         for r in range(n):
             g2.index_add_(0, all_idx[r * m:(r + 1) * m], all_rows[r * m:(r + 1) * m, off:off + wdt])
         off += wdt
+    return all_idx   # every rank's rows (duplicates, and padding clamped to N - 1): the rows the step changed
 
 
 class Trainer:

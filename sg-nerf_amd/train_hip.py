@@ -294,14 +294,136 @@ class PointAdam(torch.optim.Adam):
     gradients, so the next step skips their fill pass.  For the dense ~47 M-element point group
     and the MLP's flat parameter."""
 
-    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, zero_grad=True):
+    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, zero_grad=True, rows=False, flush_every=256):
+        """rows: row-sparse exact mode (one group of <= 4 tensors sharing their first dimension, the
+        points): a step updates the rows its list names (sgn_adam_rows), each first replaying the
+        zero-gradient steps it missed, so every row equals the dense update bit for bit once brought
+        forward -- before a step reads it (catch_up) and, for all rows, before anything else does
+        (flush(): state_dict, the model's renders; every flush_every steps, which bounds the replay)."""
         super().__init__(params, lr=lr, betas=betas, eps=eps)
         self.zero_grad_in_step = zero_grad
+        self.rows_mode = rows
+        if rows:
+            ps = self.param_groups[0]["params"]
+            if len(self.param_groups) != 1 or not 1 <= len(ps) <= 4:
+                raise ValueError("PointAdam(rows=True): one parameter group of 1 .. 4 tensors")
+            n = ps[0].shape[0]
+            if any(p.shape[0] != n or not p.is_contiguous() or p.dtype != torch.float32 for p in ps):
+                raise ValueError("PointAdam(rows=True): contiguous fp32 tensors sharing the first dimension")
+            dev = ps[0].device
+            self.n_rows = n
+            self._width = (ctypes.c_int32 * len(ps))(*[p.numel() // n for p in ps])
+            self._last = torch.zeros(n, dtype=torch.int32, device=dev)   # the step each row holds
+            self._claim = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            self._sched = torch.zeros(2 * 1024, dtype=torch.float32, device=dev)
+            self._tag = 0
+            self._rows = None        # the step's row list (set_rows), consumed by step()
+            self._flushed = 0        # every row holds at least this step
+            self.flush_every = flush_every
+
+    # -- row-sparse mode ------------------------------------------------------------------------
+    def _state_step(self):
+        """The group's step count (0 before the first step); creates the state tensors."""
+        for p in self.param_groups[0]["params"]:
+            s = self.state[p]
+            if not s:
+                s["step"] = torch.tensor(0.0)
+                s["exp_avg"] = torch.zeros_like(p)
+                s["exp_avg_sq"] = torch.zeros_like(p)
+        return int(self.state[self.param_groups[0]["params"][0]]["step"].item())
+
+    def _launch(self, step, apply, rows=None, count=None, count_is64=False, count_mul=1, n_max=None, row0=True,
+                reuse=False):
+        g = self.param_groups[0]
+        ps = g["params"]
+        n = len(ps)
+        arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() if t is not None else None for t in ts])  # noqa: E731
+        if step >= self._sched.numel() // 2:   # grow the per-step constant table (entries kept)
+            grown = torch.zeros(max(2 * self._sched.numel(), 2 * (step + 1)), dtype=torch.float32,
+                                device=self._sched.device)
+            grown[:self._sched.numel()] = self._sched
+            self._sched = grown
+        b1, b2 = g["betas"]
+        self._tag = (self._tag + 1) & 0x7fffffff
+        n_max = self.n_rows if n_max is None else n_max
+        L = _lib.lib()
+        need = int(L.sgn_adam_rows_workspace_bytes(n_max + 1))
+        if getattr(self, "_ws", None) is None or self._ws.numel() < need:
+            assert not reuse
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self._last.device)
+        _lib.check(L.sgn_adam_rows(
+            n, arr(ps), arr([p.grad if apply else None for p in ps]), arr([self.state[p]["exp_avg"] for p in ps]),
+            arr([self.state[p]["exp_avg_sq"] for p in ps]), self._width, self.n_rows,
+            _lib.ptr(rows) if rows is not None else None, _lib.ptr(count) if count is not None else None,
+            int(count_is64), count_mul, n_max, int(row0), _lib.ptr(self._last),
+            _lib.ptr(self._claim), self._tag, _lib.ptr(self._ws), self._ws.numel(), int(reuse), _lib.ptr(self._sched),
+            float(g["lr"]), b1, b2, float(g["eps"]), step, int(apply), int(self.zero_grad_in_step),
+            _lib.stream_handle()), "sgn_adam_rows")
+
+    def set_rows(self, rows, count=None, count_is64=False, count_mul=1, n_max=None):
+        """The rows the coming step reads and changes: an int32 device list (-1 / duplicates allowed)
+        with its device count (int32 or int64, times count_mul) or host length n_max.  Brings those
+        rows (and row 0) to the current step now, before the forward reads them, and keeps the list
+        for step()."""
+        assert self.rows_mode and rows.dtype == torch.int32 and rows.is_contiguous()
+        n_max = rows.numel() if n_max is None else n_max
+        t = self._state_step()
+        caught = t > 0
+        if caught:
+            self._launch(t, apply=False, rows=rows, count=count, count_is64=count_is64, count_mul=count_mul,
+                         n_max=n_max)
+        # the step reuses the catch-up's compact list when there was one (then every listed row is at t)
+        self._rows = (rows, count, count_is64, count_mul, n_max, caught)
+
+    def set_update_rows(self, rows):
+        """Replace the step's update list (int32 device, host length), keeping the catch-up done."""
+        assert self.rows_mode and rows.dtype == torch.int32 and rows.is_contiguous()
+        self._rows = (rows, None, False, 1, rows.numel(), False)
+
+    @torch.no_grad()
+    def flush(self):
+        """Bring every row to the current step (before anything outside the step reads the tensors)."""
+        if not self.rows_mode:
+            return
+        t = self._state_step()
+        if t > self._flushed:
+            self._launch(t, apply=False)
+            self._flushed = t
+
+    def state_dict(self):
+        self.flush()
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        if self.rows_mode:   # the loaded tensors are a dense state: every row holds its step
+            t = self._state_step()
+            self._last.fill_(t)
+            self._flushed = t
+            # the constants of the steps before t are not needed: no row holds an earlier step
 
     @torch.no_grad()
     def step(self, closure=None):
-        """One sgn_adam_step_multi launch per parameter group (tensors sharing a step count)."""
+        """One sgn_adam_step_multi launch per parameter group (tensors sharing a step count); in the
+        row-sparse mode one sgn_adam_rows launch over the list set_rows gave (every row without one)."""
         assert closure is None
+        if self.rows_mode:
+            t = self._state_step() + 1
+            for p in self.param_groups[0]["params"]:
+                self.state[p]["step"] += 1
+            r = self._rows
+            self._rows = None
+            if r is None:
+                self._launch(t, apply=True)
+                self._flushed = t
+            else:
+                rows, count, is64, mul, n_max, caught = r
+                self._launch(t, apply=True, rows=rows, count=count, count_is64=is64, count_mul=mul, n_max=n_max,
+                             reuse=caught)
+                if t - self._flushed >= self.flush_every:
+                    self._launch(t, apply=False)
+                    self._flushed = t
+            return None
         L = _lib.lib()
         st = _lib.stream_handle()
         for g in self.param_groups:
@@ -370,7 +492,10 @@ class HipTrainer:
         fused = self.device.type == "cuda"
         if fused:
             self.opt_net = PointAdam([self.mlp.flat], lr=lr, betas=(0.9, 0.999))
-            self.opt_pts = PointAdam(self.point_params, lr=plr, betas=(0.9, 0.999))
+            # row-sparse exact mode: a step updates the ~50 k rows it touches (each first replaying the
+            # zero-gradient steps it missed) instead of streaming all 47 M elements; flushed before
+            # anything else reads the points (sync_points)
+            self.opt_pts = PointAdam(self.point_params, lr=plr, betas=(0.9, 0.999), rows=True)
         else:
             self.opt_net = torch.optim.Adam([self.mlp.flat], lr=lr, betas=(0.9, 0.999))
             self.opt_pts = torch.optim.Adam(self.point_params, lr=plr, betas=(0.9, 0.999))
@@ -529,6 +654,24 @@ class HipTrainer:
         """Wait for and check the last step's out-of-range neighbour counter (see _check_oob)."""
         self._check_oob(wait=True)
 
+    # -- row-sparse point Adam --------------------------------------------------------------
+    def _adam_rows(self, rows, count, count_is64, count_mul):
+        """The step's point rows (a device list and count) to the row-sparse Adam: brought to the
+        current step before the forward reads them; the step's update takes the same list."""
+        if isinstance(self.opt_pts, PointAdam) and self.opt_pts.rows_mode:
+            self.opt_pts.set_rows(rows, count, count_is64, count_mul)
+
+    def _adam_union(self, all_idx):
+        """Under DP the exchanged gradient covers every rank's rows: the update takes all of them."""
+        if all_idx is not None and isinstance(self.opt_pts, PointAdam) and self.opt_pts.rows_mode:
+            self.opt_pts.set_update_rows(all_idx.to(torch.int32))
+
+    def sync_points(self):
+        """Bring every point row to the optimizer's current step (the row-sparse Adam updates a row
+        when a step touches it): call before reading the point tensors outside a step."""
+        if isinstance(self.opt_pts, PointAdam):
+            self.opt_pts.flush()
+
     # -- one step ------------------------------------------------------------------------
     def _bg_ray(self, bg_ray, R):
         """inputs['bg_ray'] (the plane background model's per-ray colour, [1, R, 3]) as a contiguous
@@ -556,6 +699,7 @@ class HipTrainer:
         R = raydir.shape[0]
         bg_ray = self._bg_ray(bg_ray, R)
         q = self._query(campos, raydir, near, far, labels)
+        self._adam_rows(q.pidx, q.counters, False, o.K)
         # work that does not depend on the query is queued before the step's one host sync, so
         # the GPU runs it while the host waits
         blob, tblob = self.packer.pack(self.mlp.flat)
@@ -638,7 +782,7 @@ class HipTrainer:
             self._weight_grads(n * 8, scale, q)
         self.allreduce_grads([self.mlp.flat])
         if dp:
-            _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
+            self._adam_union(_allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts))
         parts["total"] = total.detach()
         return parts, full.detach(), ray_mask
 
@@ -691,6 +835,7 @@ class HipTrainer:
         if dp:
             t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, npts)
         idx32, cnt = self._touched(q, npts) if not dp else (t_idx.to(torch.int32), t_cnt)
+        self._adam_rows(idx32, cnt, True, 1)   # before the projection subset reads those points
         _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(idx32),
                                                   _lib.ptr(cnt), _lib.ptr(self._proj32), st),
                    "sgn_point_project_f32_subset")
@@ -714,7 +859,7 @@ class HipTrainer:
         self.allreduce_grads([self.mlp.flat])
         if dp:
             t_counts = [int(x) for x in gather_counts(t_cnt).tolist()]
-            _allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts)
+            self._adam_union(_allreduce_point_rows([p.grad for p in self.point_params], t_idx, t_counts))
         parts["total"] = total
         return parts, full_o, mask_o.bool()
 

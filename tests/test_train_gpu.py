@@ -442,6 +442,58 @@ def test_point_adam_matches_torch_adam(sizes):
     assert all(float(oa.state[x]["step"]) == 3.0 for x in a)
 
 
+@pytest.mark.parametrize("n_rows,steps,flush_every", [(5_003, 12, 256), (20_000, 9, 4), (7, 5, 256)])
+def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every):
+    """PointAdam(rows=True) (sgn_adam_rows: a step updates the rows its list names, each first
+    replaying the zero-gradient steps it missed) against the dense PointAdam on the point group's
+    shapes [N, 32] [N, 3] [N, 3] [N, 1]: every step's gradient lives on a random row subset plus
+    row 0 (the loss stage's conf read), the list holds those rows as a neighbour table would (-1
+    slots, duplicates, a device int32 count times K), lr decays per step.  Rows a step reads equal
+    the dense state at its start, and after flush() every parameter and moment equals the dense
+    one exactly (the same fp32 operations in the same order); state_dict() flushes."""
+    from sgnerf_amd.train_hip import PointAdam
+    g = torch.Generator().manual_seed(n_rows + steps)
+    widths = (32, 3, 3, 1)
+    p0 = [torch.randn(n_rows, w, generator=g) for w in widths]
+    a = [torch.nn.Parameter(x.clone().to(DEV)) for x in p0]
+    b = [torch.nn.Parameter(x.clone().to(DEV)) for x in p0]
+    od = PointAdam(a, lr=2e-3)
+    orow = PointAdam(b, lr=2e-3, rows=True, flush_every=flush_every)
+    K = 8
+    for it in range(steps):
+        n_s = max(1, n_rows // 40)
+        table = torch.randint(0, n_rows, (n_s, K), generator=g, dtype=torch.int32)
+        table[torch.rand(n_s, K, generator=g) < 0.3] = -1          # empty neighbour slots
+        table[: n_s // 4, 1] = table[: n_s // 4, 0]                  # duplicates
+        used = torch.unique(table[table >= 0].long())
+        cap = torch.full((n_s + 5, K), n_rows - 1, dtype=torch.int32)   # entries past the count: ignored
+        cap[:n_s] = table
+        rows = cap.reshape(-1).to(DEV)
+        count = torch.tensor([n_s, 0], dtype=torch.int32, device=DEV)
+        orow.set_rows(rows, count, False, K)
+        read = torch.cat([used, torch.zeros(1, dtype=torch.long)]).to(DEV)   # the rows the step may read
+        for x, y in zip(a, b):                                       # caught up: the dense state
+            assert torch.equal(x.detach()[read], y.detach()[read])
+        for x, y, w in zip(a, b, widths):
+            gr = torch.zeros(n_rows, w)
+            gr[used] = torch.randn(used.numel(), w, generator=g) * 10 ** (it % 3 - 1)
+            gr[0] = torch.randn(w, generator=g)
+            x.grad = gr.to(DEV)
+            y.grad = gr.to(DEV)
+        for o in (od, orow):
+            o.param_groups[0]["lr"] = 2e-3 * 0.97 ** it
+        od.step()
+        orow.step()
+        for y in b:
+            assert torch.count_nonzero(y.grad) == 0
+    sd = orow.state_dict()                                           # flushes
+    for x, y in zip(a, b):
+        assert torch.equal(x.detach(), y.detach())
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(od.state[x][k], orow.state[y][k])
+    assert all(float(v["step"]) == steps for v in sd["state"].values())
+
+
 @pytest.mark.parametrize("rows", [0, 1, 777, 165_000])
 def test_colsum_matches_torch_sum(rows):
     """sgn_colsum_f16 (bias gradients) against a float64 column sum of the same fp16 tiles,
