@@ -938,8 +938,11 @@ __device__ __forceinline__ void row_geometry(const RowArgs &a, const Cam &cam, i
 constexpr int X0_QUADS = 72, ROW_QUADS = 74;
 
 __global__ __launch_bounds__(TPB) void k_row_inputs(RowArgs a, float *x0, float *ext, float2 *rw, float *vpe) {
-    const int lane = threadIdx.x & 63;
-    const int wv = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6), nw = gridDim.x * (TPB / 64);
+    // the item's rows' embeddings, staged once per item: the PE tasks read them here instead of
+    // issuing a dependent global load per task (the loop waited out the latency task by task)
+    __shared__ __attribute__((aligned(16))) float se[TPB / 64][8 * 32];  // K <= 8 rows
+    const int lane = threadIdx.x & 63, wl = threadIdx.x >> 6;
+    const int wv = blockIdx.x * (TPB / 64) + wl, nw = gridDim.x * (TPB / 64);
     const Cam cam = load_cam(a.campos, a.rot);
     const int n = n_items(a);
     for (int it = wv; it < n; it += nw) {
@@ -969,6 +972,14 @@ __global__ __launch_bounds__(TPB) void k_row_inputs(RowArgs a, float *x0, float 
             }
             vpe[(int64_t)it * 32 + lane] = v;
         }
+        {   // lane l: floats 4 (l & 7) .. + 3 of row l >> 3
+            const int k = lane >> 3;
+            const int pk = __shfl(pidl, k);
+            f32x4 e4 = {0.f, 0.f, 0.f, 0.f};
+            if (k < nnb && pk >= 0) e4 = *(const f32x4 *)(a.emb + (int64_t)pk * 32 + 4 * (lane & 7));
+            *(f32x4 *)&se[wl][32 * k + 4 * (lane & 7)] = e4;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own writes are every lane's
+        }
         const int ntask = nnb * ROW_QUADS;
         for (int t0 = 0; t0 < ntask; t0 += 64) {  // wave-uniform trip count: the shuffles see every lane
             const int t = t0 + lane;
@@ -982,7 +993,7 @@ __global__ __launch_bounds__(TPB) void k_row_inputs(RowArgs a, float *x0, float 
             const int64_t row = ro + k;
             const int64_t pb = (int64_t)pid * 3;
             if (q < X0_QUADS) {
-                *(f32x4 *)(x0 + row * 288 + 4 * q) = x0_quad(4 * q, a.emb + (int64_t)pid * 32, d);
+                *(f32x4 *)(x0 + row * 288 + 4 * q) = x0_quad(4 * q, &se[wl][32 * k], d);
             } else if (q == X0_QUADS) {  // block3.0's extra channels (:639-652): colour, dir - v
                 f32x4 u;
                 u[0] = a.color[pb]; u[1] = a.color[pb + 1]; u[2] = a.color[pb + 2];
@@ -1047,9 +1058,9 @@ __global__ __launch_bounds__(TPB) void k_colour_head(RowArgs a, const float *h3,
 }
 
 constexpr int HEAD_BLOCKS = 256;
-// k_row_head's workgroups (its partials: [ROW_HEAD_BLOCKS][257], summed in order by k_reduce_partials, one
-// thread per element): 1024 took the head 132 -> 101 us but the reduce 43 -> 128 us per config-5 step
-constexpr int ROW_HEAD_BLOCKS = 256;
+// k_row_head's workgroups (its partials: [ROW_HEAD_BLOCKS][257], summed in a fixed order by k_reduce_wide):
+// 1024 took the head 132 -> 101 us per config-5 step (one wave walks ~4 items instead of ~15)
+constexpr int ROW_HEAD_BLOCKS = 1024;
 
 // backward of k_colour_head: dy4 = d rgb 1.002 sig (1 - sig); dy3 = (W6^T dy4) LReLU'(h3); the
 // weight / bias gradient of color_branch.6 as one fixed-order partial per workgroup
@@ -1295,6 +1306,30 @@ __global__ __launch_bounds__(TPB) void k_reduce_partials(RedArgs r) {
     const float v = (v0 + v1) + (v2 + v3);
     if (c < s.n_in) s.dst_w[(int64_t)m * s.ldw + c] += v;
     else if (c == s.bias_col) s.dst_b[m] += v;
+}
+
+// segments with many splits and few outputs (k_row_head's [ROW_HEAD_BLOCKS][257]): one workgroup per
+// output, thread i sums splits i, i + TPB, .. in order, then a fixed LDS tree (deterministic); one
+// thread per output walked the splits serially (128 us for 1024 splits)
+constexpr int WIDE_SPLITS = 512;
+__global__ __launch_bounds__(TPB) void k_reduce_wide(RedSeg s) {
+    __shared__ float red[TPB];
+    const int64_t e = blockIdx.x;
+    const int m = (int)(e / s.N), c = (int)(e % s.N);
+    const int64_t stride = (int64_t)s.M * s.N;
+    float v = 0.f;
+    for (int i = threadIdx.x; i < s.splits; i += TPB) v += s.part[e + i * stride];
+    red[threadIdx.x] = v;
+    __syncthreads();
+#pragma unroll
+    for (int o = TPB / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (c < s.n_in) s.dst_w[(int64_t)m * s.ldw + c] += red[0];
+        else if (c == s.bias_col) s.dst_b[m] += red[0];
+    }
 }
 
 }  // namespace tx
@@ -1599,16 +1634,24 @@ int sgn_reduce_partials(int32_t n_seg, const sgn_partial_segment *segs, sgn_stre
     using namespace sgn::tx;
     SGN_REQUIRE(segs && n_seg >= 1 && n_seg <= MAX_RED, "1..16 segments");
     RedArgs r{};
-    r.n_seg = n_seg;
+    r.n_seg = 0;
     r.start[0] = 0;
     for (int i = 0; i < n_seg; ++i) {
         const sgn_partial_segment &s = segs[i];
         SGN_REQUIRE(s.part && s.splits >= 1 && s.M >= 1 && s.N >= 1 && s.dst_w, "bad segment");
         SGN_REQUIRE(s.n_in <= s.N && (s.bias_col < 0 || (s.bias_col < s.N && s.dst_b)), "bad segment columns");
-        r.s[i] = RedSeg{s.part, s.splits, s.M, s.N, s.n_in, s.bias_col, s.ldw, s.dst_w, s.dst_b};
-        r.start[i + 1] = r.start[i] + (int64_t)s.M * s.N;
+        const RedSeg g{s.part, s.splits, s.M, s.N, s.n_in, s.bias_col, s.ldw, s.dst_w, s.dst_b};
+        if (s.splits >= WIDE_SPLITS && (int64_t)s.M * s.N <= 4096) {
+            hipLaunchKernelGGL(k_reduce_wide, dim3((unsigned)(s.M * s.N)), dim3(TPB), 0, as_stream(stream), g);
+            SGN_CHECK_HIP(hipGetLastError());
+            continue;
+        }
+        r.s[r.n_seg] = g;
+        r.start[r.n_seg + 1] = r.start[r.n_seg] + (int64_t)s.M * s.N;
+        ++r.n_seg;
     }
-    const int64_t blocks = (r.start[n_seg] + TPB - 1) / TPB;
+    if (r.n_seg == 0) return 0;
+    const int64_t blocks = (r.start[r.n_seg] + TPB - 1) / TPB;
     hipLaunchKernelGGL(k_reduce_partials, dim3((unsigned)blocks), dim3(TPB), 0, as_stream(stream), r);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;

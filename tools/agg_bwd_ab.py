@@ -1,6 +1,6 @@
 """Same-box A/B of k_agg_bwd builds (NOT product).  A few config-5 training steps (bench.py's
 train_main, f16) on the in-tree library record the last sgn_aggregate_backward[_sg] call; every
-library named on the command line (tools/agg_bwd_variant.sh builds) then replays that call between
+library named on the command line (tools/src_variant.sh builds) then replays that call between
 HIP events on the same stream, interleaved over rounds.  Before timing, each library's outputs of
 one replay (deltas, h4, dza bit for bit; point gradients to 1e-5 relative, atomics reorder) are
 compared with the in-tree library's.  Prints one JSON line per library.
