@@ -392,26 +392,31 @@ int sgn_adam_step_multi(int32_t n_t, float *const *d_param, float *const *d_grad
 /* Row-sparse exact Adam for n_t <= 4 tensors sharing a row index (the point group: embedding,
  * colour, dir, conf; row_width[t] elements per row, <= 64 in all; n_rows rows).  Dense Adam
  * updates every row every step; a step's gradient touches few, and an untouched row's update is
- * the zero-gradient recurrence.  d_last[r] (int32, n_rows, zero at step 0) is the step row r holds;
- * a launch brings each listed row from d_last[r] to `step`, replaying the missed steps at zero
+ * the zero-gradient recurrence.  d_last[r] (int32, n_rows, zero at step 0) is the step row r holds.
+ * A launch brings each listed row from d_last[r] to `step`: it replays the missed steps at zero
  * gradient with their constants from d_sched ([step][2] fp32, (lr_k / bc1_k, sqrt(bc2_k)), written
- * by each apply launch for its step), then (apply != 0) takes step `step` itself with the gradient
- * (and clears it with zero_grad).  The same fp32 operations as sgn_adam_step_multi, so a row
- * equals the dense update's bit for bit once brought forward; read a row only then (d_rows null:
- * every row, n_max = n_rows).  List: d_rows[0 .. n) with n = min(n_max, count_mul * *d_count)
- * (d_count int32 or int64 on the device, or null: n = n_max), -1 and duplicate entries allowed
- * (d_claim, int32 n_rows initialised to -1, takes each row once per launch under a tag unique to
- * the launch), row0 != 0: row 0 as one more entry (the loss stage reads point 0's conf).
- * d_ws: sgn_adam_rows_workspace_bytes(n_max + 1) bytes, the launch's compact row list; reuse != 0
- * (an apply launch straight after a catch-up launch of the same list and workspace) skips the
- * claim and updates that list's rows, all then at step - 1. */
-size_t sgn_adam_rows_workspace_bytes(int64_t n_max);
+ * by each apply launch for its step), and with apply != 0 takes step `step` itself with the
+ * gradient buffer's value (zero on rows the step did not touch: that step's zero-gradient update;
+ * zero_grad clears it).  The same fp32 operations as sgn_adam_step_multi, so a row equals the
+ * dense update's bit for bit once brought forward: read a row only then (d_rows null: every row,
+ * n_max = n_rows).  List 1: d_rows[0 .. n) with n = min(n_max, count_mul * *d_count) (d_count int32
+ * or int64 on the device, or null: n = n_max), -1 and duplicate entries allowed; row0 != 0 adds row
+ * 0 (the loss stage reads point 0's conf for empty slots); list 2 (optional): d_rows2[0 ..
+ * min(n_max2, *d_count2)) (int64 device count), e.g. a previous launch's pend list.  d_claim (int32
+ * n_rows, -1 initialised) takes each row once per launch under `tag` (unique per launch);
+ * d_ws: sgn_adam_rows_workspace_bytes(min(entries, n_rows)) bytes of scratch (entries = n_max +
+ * n_max2 + row0).  d_pend (optional, with d_claim2 like d_claim): sgn_adam_rows_pend_bytes(min(n_max
+ * + 1, n_rows)) bytes receiving list 1's distinct valid rows and row 0 -- int64 count at [0], the
+ * number of list-1 ids >= n_rows at [1] (a query / table mismatch), int32 rows from byte 16. */
+size_t sgn_adam_rows_workspace_bytes(int64_t n_entries);
+size_t sgn_adam_rows_pend_bytes(int64_t n_entries);
 int sgn_adam_rows(int32_t n_t, float *const *d_param, float *const *d_grad, float *const *d_exp_avg,
                   float *const *d_exp_avg_sq, const int32_t *row_width, int64_t n_rows, const int32_t *d_rows,
                   const void *d_count, int32_t count_is64, int32_t count_mul, int64_t n_max, int32_t row0,
-                  int32_t *d_last, int32_t *d_claim, int32_t tag, void *d_ws, size_t ws_bytes, int32_t reuse,
-                  float *d_sched, double lr, double beta1, double beta2, double eps, int64_t step, int32_t apply,
-                  int32_t zero_grad, sgn_stream_t stream);
+                  const int32_t *d_rows2, const int64_t *d_count2, int64_t n_max2, int32_t *d_last,
+                  int32_t *d_claim, int32_t *d_claim2, int32_t tag, void *d_ws, size_t ws_bytes, void *d_pend,
+                  size_t pend_bytes, float *d_sched, double lr, double beta1, double beta2, double eps, int64_t step,
+                  int32_t apply, int32_t zero_grad, sgn_stream_t stream);
 /* d_out[i][c] = sum over r < rows of d_x[i][r][c] (fp16 in, fp32 out, deterministic order),
  * for count <= 8 matrices [rows][256] (the bias gradients db = sum of the deltas,
  * torch.sum(d, 0) in the reference's autograd of nn.Linear).  d_x: host array of device

@@ -144,10 +144,12 @@ SIGNATURES = {
                                      ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), ctypes.c_double, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_double, c_i64, c_i32, c_vp]),
     "sgn_adam_rows_workspace_bytes": (c_sz, [c_i64]),
+    "sgn_adam_rows_pend_bytes": (c_sz, [c_i64]),
     "sgn_adam_rows": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                               ctypes.POINTER(c_vp), ctypes.POINTER(c_i32), c_i64, c_vp, c_vp, c_i32, c_i32, c_i64,
-                              c_i32, c_vp, c_vp, c_i32, c_vp, c_sz, c_i32, c_vp, ctypes.c_double, ctypes.c_double,
-                              ctypes.c_double, ctypes.c_double, c_i64, c_i32, c_i32, c_vp]),
+                              c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_sz, c_vp, c_sz, c_vp,
+                              ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_i32, c_i32,
+                              c_vp]),
     "sgn_colsum_workspace_bytes": (c_sz, [c_i32]),
     "sgn_colsum_f16": (c_i32, [c_i32, ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp, c_vp]),
     "sgn_colsum_f16_weighted": (c_i32, [c_i32, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i64, c_i32, c_vp, c_vp,

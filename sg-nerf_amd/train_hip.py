@@ -296,10 +296,12 @@ class PointAdam(torch.optim.Adam):
 
     def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, zero_grad=True, rows=False, flush_every=256):
         """rows: row-sparse exact mode (one group of <= 4 tensors sharing their first dimension, the
-        points): a step updates the rows its list names (sgn_adam_rows), each first replaying the
-        zero-gradient steps it missed, so every row equals the dense update bit for bit once brought
-        forward -- before a step reads it (catch_up) and, for all rows, before anything else does
-        (flush(): state_dict, the model's renders; every flush_every steps, which bounds the replay)."""
+        points; sgn_adam_rows).  A row is brought forward only when something reads it, replaying the
+        zero-gradient steps it missed, so it equals the dense update bit for bit whenever read.  The
+        step's own update is deferred to the next step's first launch: set_rows(list) applies the
+        pending step to the previous step's rows and brings the new list's rows to the current step in
+        one pass; flush() (state_dict, the model's renders; every flush_every steps, which bounds the
+        replay) brings every row."""
         super().__init__(params, lr=lr, betas=betas, eps=eps)
         self.zero_grad_in_step = zero_grad
         self.rows_mode = rows
@@ -315,10 +317,15 @@ class PointAdam(torch.optim.Adam):
             self._width = (ctypes.c_int32 * len(ps))(*[p.numel() // n for p in ps])
             self._last = torch.zeros(n, dtype=torch.int32, device=dev)   # the step each row holds
             self._claim = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            self._claim2 = torch.full((n,), -1, dtype=torch.int32, device=dev)
             self._sched = torch.zeros(2 * 1024, dtype=torch.float32, device=dev)
+            self._ws = None
+            self._pend = [None, None]   # two pend lists: the previous step's is read while the next is written
+            self._pi = 0
             self._tag = 0
-            self._rows = None        # the step's row list (set_rows), consumed by step()
-            self._flushed = 0        # every row holds at least this step
+            self._rows = None           # the step's list (set_rows) once its rows are brought forward
+            self._pending = None        # (pend buffer, length bound): the rows of the step not yet applied
+            self._flushed = 0           # every row holds at least this step
             self.flush_every = flush_every
 
     # -- row-sparse mode ------------------------------------------------------------------------
@@ -332,8 +339,15 @@ class PointAdam(torch.optim.Adam):
                 s["exp_avg_sq"] = torch.zeros_like(p)
         return int(self.state[self.param_groups[0]["params"][0]]["step"].item())
 
-    def _launch(self, step, apply, rows=None, count=None, count_is64=False, count_mul=1, n_max=None, row0=True,
-                reuse=False):
+    def _buf(self, t, nbytes):
+        if t is None or t.numel() < nbytes:
+            t = torch.empty(nbytes, dtype=torch.uint8, device=self._last.device)
+        return t
+
+    def _launch(self, step, apply, rows=None, count=None, count_is64=False, count_mul=1, n_max=None, pend=False,
+                lr=None):
+        """One sgn_adam_rows call: list 1 (rows, or every row), the pending list as list 2 when applying a
+        deferred step, row 0; with pend, list 1's distinct rows go to the next pend buffer."""
         g = self.param_groups[0]
         ps = g["params"]
         n = len(ps)
@@ -347,38 +361,50 @@ class PointAdam(torch.optim.Adam):
         self._tag = (self._tag + 1) & 0x7fffffff
         n_max = self.n_rows if n_max is None else n_max
         L = _lib.lib()
-        need = int(L.sgn_adam_rows_workspace_bytes(n_max + 1))
-        if getattr(self, "_ws", None) is None or self._ws.numel() < need:
-            assert not reuse
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self._last.device)
+        prev = self._pending if apply and rows is not None else None
+        lr = float(g["lr"]) if lr is None else lr
+        n2 = prev[1] if prev is not None else 0
+        self._ws = self._buf(self._ws, int(L.sgn_adam_rows_workspace_bytes(min(n_max + n2 + 1, self.n_rows))))
+        pb = None
+        if pend:
+            self._pi ^= 1
+            pb = self._pend[self._pi] = self._buf(self._pend[self._pi],
+                                                  int(L.sgn_adam_rows_pend_bytes(min(n_max + 1, self.n_rows))))
         _lib.check(L.sgn_adam_rows(
             n, arr(ps), arr([p.grad if apply else None for p in ps]), arr([self.state[p]["exp_avg"] for p in ps]),
             arr([self.state[p]["exp_avg_sq"] for p in ps]), self._width, self.n_rows,
             _lib.ptr(rows) if rows is not None else None, _lib.ptr(count) if count is not None else None,
-            int(count_is64), count_mul, n_max, int(row0), _lib.ptr(self._last),
-            _lib.ptr(self._claim), self._tag, _lib.ptr(self._ws), self._ws.numel(), int(reuse), _lib.ptr(self._sched),
-            float(g["lr"]), b1, b2, float(g["eps"]), step, int(apply), int(self.zero_grad_in_step),
-            _lib.stream_handle()), "sgn_adam_rows")
+            int(count_is64), count_mul, n_max, 1,
+            prev[0].data_ptr() + 16 if prev is not None else None, prev[0].data_ptr() if prev is not None else None,
+            n2, _lib.ptr(self._last), _lib.ptr(self._claim), _lib.ptr(self._claim2), self._tag,
+            _lib.ptr(self._ws), self._ws.numel(), _lib.ptr(pb) if pb is not None else None,
+            pb.numel() if pb is not None else 0, _lib.ptr(self._sched), lr, b1, b2, float(g["eps"]),
+            step, int(apply), int(self.zero_grad_in_step), _lib.stream_handle()), "sgn_adam_rows")
+        return pb
 
     def set_rows(self, rows, count=None, count_is64=False, count_mul=1, n_max=None):
         """The rows the coming step reads and changes: an int32 device list (-1 / duplicates allowed)
-        with its device count (int32 or int64, times count_mul) or host length n_max.  Brings those
-        rows (and row 0) to the current step now, before the forward reads them, and keeps the list
-        for step()."""
+        with its device count (int32 or int64, times count_mul) or host length n_max.  One launch
+        applies the deferred previous step to its rows and brings these rows (and row 0) to the current
+        step; returns the step's distinct rows (int32 from byte 16 of the returned buffer, int64 count
+        at byte 0, list-1 ids >= n_rows at byte 8)."""
         assert self.rows_mode and rows.dtype == torch.int32 and rows.is_contiguous()
         n_max = rows.numel() if n_max is None else n_max
         t = self._state_step()
-        caught = t > 0
-        if caught:
-            self._launch(t, apply=False, rows=rows, count=count, count_is64=count_is64, count_mul=count_mul,
-                         n_max=n_max)
-        # the step reuses the catch-up's compact list when there was one (then every listed row is at t)
-        self._rows = (rows, count, count_is64, count_mul, n_max, caught)
+        pd = self._pending
+        pb = self._launch(t, apply=pd is not None, rows=rows, count=count, count_is64=count_is64,
+                          count_mul=count_mul, n_max=n_max, pend=True, lr=pd[2] if pd is not None else None)
+        self._pending = None
+        self._rows = (pb, min(n_max + 1, self.n_rows))
+        return pb
 
     def set_update_rows(self, rows):
-        """Replace the step's update list (int32 device, host length), keeping the catch-up done."""
+        """Under DP: the rows the step's update changes (every rank's, int32 device, host length) --
+        they replace the step's pend list (a launch gathers their distinct rows now)."""
         assert self.rows_mode and rows.dtype == torch.int32 and rows.is_contiguous()
-        self._rows = (rows, None, False, 1, rows.numel(), False)
+        t = self._state_step()
+        pb = self._launch(t, apply=False, rows=rows, n_max=rows.numel(), pend=True)
+        self._rows = (pb, min(rows.numel() + 1, self.n_rows))
 
     @torch.no_grad()
     def flush(self):
@@ -386,8 +412,10 @@ class PointAdam(torch.optim.Adam):
         if not self.rows_mode:
             return
         t = self._state_step()
-        if t > self._flushed:
-            self._launch(t, apply=False)
+        pd = self._pending
+        if pd is not None or t > self._flushed:
+            self._launch(t, apply=pd is not None, lr=pd[2] if pd is not None else None)
+            self._pending = None
             self._flushed = t
 
     def state_dict(self):
@@ -400,14 +428,18 @@ class PointAdam(torch.optim.Adam):
             t = self._state_step()
             self._last.fill_(t)
             self._flushed = t
-            # the constants of the steps before t are not needed: no row holds an earlier step
+            self._pending = None
+            self._rows = None
 
     @torch.no_grad()
     def step(self, closure=None):
         """One sgn_adam_step_multi launch per parameter group (tensors sharing a step count); in the
-        row-sparse mode one sgn_adam_rows launch over the list set_rows gave (every row without one)."""
+        row-sparse mode the step is recorded as pending on the rows set_rows listed (applied by the next
+        set_rows or flush), or applied to every row at once without such a list."""
         assert closure is None
         if self.rows_mode:
+            if self._pending is not None:   # the previous step was never applied: its gradient is this one
+                self.flush()
             t = self._state_step() + 1
             for p in self.param_groups[0]["params"]:
                 self.state[p]["step"] += 1
@@ -416,13 +448,10 @@ class PointAdam(torch.optim.Adam):
             if r is None:
                 self._launch(t, apply=True)
                 self._flushed = t
-            else:
-                rows, count, is64, mul, n_max, caught = r
-                self._launch(t, apply=True, rows=rows, count=count, count_is64=is64, count_mul=mul, n_max=n_max,
-                             reuse=caught)
+            else:   # the step's lr travels with it: the update runs at the next set_rows / flush
+                self._pending = (r[0], r[1], float(self.param_groups[0]["lr"]))
                 if t - self._flushed >= self.flush_every:
-                    self._launch(t, apply=False)
-                    self._flushed = t
+                    self.flush()
             return None
         L = _lib.lib()
         st = _lib.stream_handle()
@@ -626,16 +655,20 @@ class HipTrainer:
         _lib.check(_lib.lib().sgn_touched_points(_lib.ptr(q.pidx), _lib.ptr(q.counters), q.pidx.numel() // K, K, npts,
                                                  step, _lib.ptr(self._stamp), _lib.ptr(self._tlist),
                                                  _lib.ptr(self._tcount), _lib.stream_handle()), "sgn_touched_points")
-        # the out-of-range neighbour count goes to pinned host memory without a sync; the next step
-        # (or check_touched()) reads it once the copy has landed and fails loudly on a query / point
-        # table mismatch (those points would never be projected)
+        self._watch_oob(self._tcount[2:3])
+        return self._tlist, self._tcount[step & 1]
+
+    def _watch_oob(self, count):
+        """The out-of-range neighbour count (a device int64) goes to pinned host memory without a sync;
+        the next step (or check_touched()) reads it once the copy has landed and fails loudly on a
+        query / point table mismatch (those points would never be projected or updated)."""
+        self._check_oob()
         if not hasattr(self, "_oob_host"):
             self._oob_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
             self._oob_event = torch.cuda.Event()
-        self._oob_host.copy_(self._tcount[2:3], non_blocking=True)
+        self._oob_host.copy_(count.reshape(1), non_blocking=True)
         self._oob_event.record()
         self._oob_pending = True
-        return self._tlist, self._tcount[step & 1]
 
     def _check_oob(self, wait=False):
         """Raise if an earlier step's query named a point index >= n_points (sgn_touched_points'
@@ -655,11 +688,19 @@ class HipTrainer:
         self._check_oob(wait=True)
 
     # -- row-sparse point Adam --------------------------------------------------------------
+    def _rows_adam(self):
+        return isinstance(self.opt_pts, PointAdam) and self.opt_pts.rows_mode
+
     def _adam_rows(self, rows, count, count_is64, count_mul):
-        """The step's point rows (a device list and count) to the row-sparse Adam: brought to the
-        current step before the forward reads them; the step's update takes the same list."""
-        if isinstance(self.opt_pts, PointAdam) and self.opt_pts.rows_mode:
-            self.opt_pts.set_rows(rows, count, count_is64, count_mul)
+        """The step's point rows (a device list and count) to the row-sparse Adam: the deferred previous
+        step applied and these rows brought to the current step before the forward reads them.  Returns
+        the step's distinct rows (int32 list, int64 device count) or None (dense Adam); a list id >=
+        n_points is reported at the next step (_watch_oob)."""
+        if not self._rows_adam():
+            return None
+        pb = self.opt_pts.set_rows(rows, count, count_is64, count_mul)
+        self._watch_oob(pb[8:16].view(torch.int64))
+        return pb[16:].view(torch.int32), pb[:8].view(torch.int64)
 
     def _adam_union(self, all_idx):
         """Under DP the exchanged gradient covers every rank's rows: the update takes all of them."""
@@ -834,8 +875,12 @@ class HipTrainer:
         t_idx = t_cnt = None
         if dp:
             t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, npts)
-        idx32, cnt = self._touched(q, npts) if not dp else (t_idx.to(torch.int32), t_cnt)
-        self._adam_rows(idx32, cnt, True, 1)   # before the projection subset reads those points
+        if dp:   # every rank's touched rows ride the step's one sync (the point-row exchange)
+            idx32, cnt = t_idx.to(torch.int32), t_cnt
+            self._adam_rows(idx32, cnt, True, 1)
+        else:    # the Adam's distinct-row list is the step's touched list (row 0 included)
+            lst = self._adam_rows(q.pidx, q.counters, False, o.K)
+            idx32, cnt = lst if lst is not None else self._touched(q, npts)
         _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(blob), _lib.ptr(idx32),
                                                   _lib.ptr(cnt), _lib.ptr(self._proj32), st),
                    "sgn_point_project_f32_subset")

@@ -444,8 +444,9 @@ def test_point_adam_matches_torch_adam(sizes):
 
 @pytest.mark.parametrize("n_rows,steps,flush_every", [(5_003, 12, 256), (20_000, 9, 4), (7, 5, 256)])
 def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every):
-    """PointAdam(rows=True) (sgn_adam_rows: a step updates the rows its list names, each first
-    replaying the zero-gradient steps it missed) against the dense PointAdam on the point group's
+    """PointAdam(rows=True) (sgn_adam_rows: a step's update deferred to the next step's launch, which
+    brings the rows it lists forward, each first replaying the zero-gradient steps it missed) against
+    the dense PointAdam on the point group's
     shapes [N, 32] [N, 3] [N, 3] [N, 1]: every step's gradient lives on a random row subset plus
     row 0 (the loss stage's conf read), the list holds those rows as a neighbour table would (-1
     slots, duplicates, a device int32 count times K), lr decays per step.  Rows a step reads equal
@@ -470,10 +471,13 @@ def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every):
         cap[:n_s] = table
         rows = cap.reshape(-1).to(DEV)
         count = torch.tensor([n_s, 0], dtype=torch.int32, device=DEV)
-        orow.set_rows(rows, count, False, K)
+        pb = orow.set_rows(rows, count, False, K)   # applies the previous step, brings these rows forward
         read = torch.cat([used, torch.zeros(1, dtype=torch.long)]).to(DEV)   # the rows the step may read
         for x, y in zip(a, b):                                       # caught up: the dense state
             assert torch.equal(x.detach()[read], y.detach()[read])
+        n_pb = int(pb[:8].view(torch.int64).item())                  # the step's distinct rows, row 0 too
+        assert n_pb == torch.unique(read).numel() and int(pb[8:16].view(torch.int64).item()) == 0
+        assert torch.equal(torch.sort(pb[16:].view(torch.int32)[:n_pb].long()).values, torch.unique(read))
         for x, y, w in zip(a, b, widths):
             gr = torch.zeros(n_rows, w)
             gr[used] = torch.randn(used.numel(), w, generator=g) * 10 ** (it % 3 - 1)
@@ -483,11 +487,10 @@ def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every):
         for o in (od, orow):
             o.param_groups[0]["lr"] = 2e-3 * 0.97 ** it
         od.step()
-        orow.step()
-        for y in b:
-            assert torch.count_nonzero(y.grad) == 0
-    sd = orow.state_dict()                                           # flushes
+        orow.step()                                                  # deferred to the next set_rows
+    sd = orow.state_dict()                                           # flushes: the last step applied
     for x, y in zip(a, b):
+        assert torch.count_nonzero(y.grad) == 0
         assert torch.equal(x.detach(), y.detach())
         for k in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(od.state[x][k], orow.state[y][k])
