@@ -127,67 +127,95 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 // ---- row-sparse exact Adam (the point group) -------------------------------------------------
 // A step's gradient touches ~50 k of the 1.2 M points; the dense update of the other rows is the
 // zero-gradient recurrence m = b1 m, v = b2 v, p -= step_size_k m / (sqrt(v) / bc2_sqrt_k + eps),
-// deterministic per element.  Each row records the step it holds (last[r]); a touched row replays
-// the steps it missed with adam_el at g = 0 and each step's constants (sched[k - 1] = (step_size_k,
-// bc2_sqrt_k)), then (apply) takes the current step with its gradient: the same operations in the
-// same order as the dense kernel, so a row equals the dense update bit for bit once brought forward.
-// Two launches: k_rows_claim takes each listed row once (a claim tag per launch; the list may repeat
-// rows and hold -1) into a compact list of (row, step it held); k_rows_update then runs one thread
-// per (row, element) of that list -- every row's elements in flight at once, no per-row chain.
+// deterministic per element.  Each row records the step it holds (last[r]); a listed row replays the
+// steps it missed with adam_el at g = 0 and each step's constants (sched[k - 1] = (step_size_k,
+// bc2_sqrt_k)), then (apply) takes step `target` with the gradient buffer's value (zero for a row the
+// step did not touch, which is that step's zero-gradient update): the same operations in the same
+// order as the dense kernel, so a row equals the dense update bit for bit once brought forward.
+// Two launches: k_rows_claim takes each listed row once (a claim tag per launch; the lists may repeat
+// rows and hold -1) into a compact (row, step held) list -- and, for list 1 and row 0, once more into
+// the `pend` list of distinct rows (the rows whose gradient the coming step writes, also the f32
+// step's projection subset); k_rows_update then runs one thread per (row, element) of the compact list.
 constexpr int kMaxRowTensors = 4;
 struct AdamRowsArgs {
     float *p[kMaxRowTensors], *g[kMaxRowTensors], *m[kMaxRowTensors], *v[kMaxRowTensors];
     int32_t w[kMaxRowTensors];     // elements per row
     int32_t nt, wsum;              // tensors, elements per row in all
-    const int32_t *rows;           // row list (duplicates and -1 allowed), or null: rows 0 .. n_max - 1
-    const void *d_count;           // device count of the list (int32 or int64, times count_mul; null: n_max)
-    int32_t count_is64, count_mul, row0;   // row0: row 0 as one more entry after the list
+    const int32_t *rows;           // list 1 (duplicates and -1 allowed), or null: rows 0 .. n_max - 1
+    const void *d_count;           // device count of list 1 (int32 or int64, times count_mul; null: n_max)
+    int32_t count_is64, count_mul, row0;   // row0: row 0 as one more list-1 entry
     int64_t n_max, n_rows;
-    int32_t *last, *claim;         // [n_rows]: step the row holds; this launch's claim tag
+    const int32_t *rows2;          // list 2 (a previous pend list), device int64 count at d_count2
+    const int64_t *d_count2;
+    int64_t n_max2;
+    int32_t *last, *claim, *claim2;   // [n_rows]: step the row holds; this launch's claim tags
     int32_t tag;
-    int32_t *ws;                   // [0]: compact count, then (row, step held) pairs
+    int32_t *ws;                   // [0] count, rows at ws + 4, steps held at ws + 4 + cap
+    int64_t cap;
+    int64_t *pend;                 // [0] count, [1] list-1 ids >= n_rows met; rows (int32) at pend + 2
     float2 *sched;                 // [k - 1] = (step_size_k, bc2_sqrt_k), k = 1 .. target
-    int32_t target, apply, reuse;  // reuse: the list of the previous launch, its rows all at target - 1
+    int32_t target, apply;         // bring rows to step `target`; apply: that step with the gradient
     float b1, b2, omb1, omb2, eps, ss_t, bs_t;   // ss_t, bs_t: step `target`'s constants
     int32_t zero_grad;
 };
 
+__device__ __forceinline__ int wave_append(int *ctr, bool take, int lane) {
+    const uint64_t bal = __ballot(take);
+    int base = 0;
+    if (bal && lane == 0) base = atomicAdd(ctr, __popcll(bal));
+    base = __shfl(base, 0);
+    return base + __popcll(bal & ((1ull << lane) - 1));
+}
+
 // one lane per list entry: the row's first claimant appends (row, last[row]) and sets last[row]
 __global__ __launch_bounds__(256) void k_rows_claim(AdamRowsArgs a) {
-    int64_t n = a.n_max;
+    int64_t n1 = a.n_max;
     if (a.d_count) {
         const int64_t c = a.count_is64 ? *(const int64_t *)a.d_count : (int64_t)*(const int32_t *)a.d_count;
-        n = min(n, c * a.count_mul);
+        n1 = min(n1, c * a.count_mul);
     }
+    const int64_t n2 = a.rows2 ? min(a.n_max2, *a.d_count2) : 0;
+    const int64_t n = n1 + n2 + a.row0;
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    // wave-uniform trip count: the ballot below sees every lane
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n + a.row0; i0 += stride) {
+    int32_t *prow = a.pend ? (int32_t *)(a.pend + 2) : nullptr;
+    // wave-uniform trip count: the ballots below see every lane
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n; i0 += stride) {
         const int64_t i = i0 + lane;
         int r = -1;
-        if (i < n + a.row0) r = i == n ? 0 : a.rows ? a.rows[i] : (int)i;
+        bool l1 = false;
+        if (i < n1) r = a.rows ? a.rows[i] : (int)i, l1 = true;
+        else if (i < n1 + n2) r = a.rows2[i - n1];
+        else if (i < n) r = 0, l1 = true;
+        const bool valid = r >= 0 && r < a.n_rows;
+        if (a.pend && l1 && r >= a.n_rows) atomicAdd((unsigned long long *)(a.pend + 1), 1ull);
         bool win = false;
         int from = 0;
-        if (r >= 0 && r < a.n_rows && atomicExch(a.claim + r, a.tag) != a.tag) {
-            // rows already at the target stay in the list (no replay): a reuse launch updates them
-            win = true;
+        // test, then test-and-set: a point is the neighbour of many samples, and its repeats would
+        // otherwise serialise on one address's atomics
+        if (valid && __builtin_nontemporal_load(a.claim + r) != a.tag && atomicExch(a.claim + r, a.tag) != a.tag) {
+            win = true;   // rows already at the target stay in the list: the update rewrites them unchanged
             from = a.last[r];
             a.last[r] = a.target;
         }
-        const uint64_t bal = __ballot(win);
-        if (!bal) continue;
-        int base = 0;
-        if (lane == 0) base = atomicAdd(a.ws, __popcll(bal));
-        base = __shfl(base, 0);
+        const bool pd = a.pend && l1 && valid && __builtin_nontemporal_load(a.claim2 + r) != a.tag &&
+                        atomicExch(a.claim2 + r, a.tag) != a.tag;
+        const int slot = wave_append(a.ws, win, lane);
         if (win) {
-            const int slot = base + __popcll(bal & ((1ull << lane) - 1));
-            a.ws[2 + 2 * slot] = r;
-            a.ws[3 + 2 * slot] = from;
+            a.ws[4 + slot] = r;
+            a.ws[4 + a.cap + slot] = from;
+        }
+        if (a.pend) {
+            const uint64_t bal = __ballot(pd);
+            unsigned long long base = 0;
+            if (bal && lane == 0) base = atomicAdd((unsigned long long *)a.pend, (unsigned long long)__popcll(bal));
+            base = __shfl(base, 0);
+            if (pd) prow[base + __popcll(bal & ((1ull << lane) - 1))] = r;
         }
     }
 }
 
-// one thread per (compact row, element): replay the missed steps, then (apply) the current one.
+// one thread per (compact row, element): replay the missed steps, then (apply) step `target`.
 // The constants of the last kSchedWin steps are staged in LDS (a row lags at most the flush
 // interval); older steps are read from the table itself.
 constexpr int kSchedWin = 1024;
@@ -205,15 +233,15 @@ __global__ __launch_bounds__(256) void k_rows_update(AdamRowsArgs a) {
         const int w = j / a.wsum;
         int c = j - w * a.wsum, t = 0;
         while (t + 1 < a.nt && c >= a.w[t]) c -= a.w[t++];
-        const int r = a.ws[2 + 2 * w];
-        const int from = a.reuse ? a.target - 1 : a.ws[3 + 2 * w];
+        const int r = a.ws[4 + w];
+        const int from = a.ws[4 + a.cap + w];
         const int64_t e = (int64_t)r * a.w[t] + c;
         float p = a.p[t][e], m = a.m[t][e], v = a.v[t][e];
         for (int k = from + 1; k <= upto; ++k) {
             const float2 sc = k > lo ? win[k - 1 - lo] : a.sched[k - 1];
             adam_el(p, 0.f, m, v, a.b1, a.b2, a.omb1, a.omb2, sc.x, sc.y, a.eps);
         }
-        if (a.apply) {
+        if (a.apply && from < a.target) {
             const float g = a.g[t][e];
             adam_el(p, g, m, v, a.b1, a.b2, a.omb1, a.omb2, a.ss_t, a.bs_t, a.eps);
             if (a.zero_grad && g != 0.f) a.g[t][e] = 0.f;
@@ -221,7 +249,6 @@ __global__ __launch_bounds__(256) void k_rows_update(AdamRowsArgs a) {
         a.p[t][e] = p;
         a.m[t][e] = m;
         a.v[t][e] = v;
-        if (a.reuse && c == 0 && t == 0) a.last[r] = a.target;
     }
 }
 
@@ -685,22 +712,32 @@ int sgn_adam_step_multi(int32_t n_t, float *const *d_param, float *const *d_grad
     return 0;
 }
 
-size_t sgn_adam_rows_workspace_bytes(int64_t n_max) { return (size_t)(2 * std::max<int64_t>(n_max, 0) + 4) * 4; }
+size_t sgn_adam_rows_workspace_bytes(int64_t n_entries) {
+    return (size_t)(2 * std::max<int64_t>(n_entries, 0) + 4) * 4;
+}
+size_t sgn_adam_rows_pend_bytes(int64_t n_entries) { return (size_t)(std::max<int64_t>(n_entries, 0) + 4) * 4; }
 
 int sgn_adam_rows(int32_t n_t, float *const *d_param, float *const *d_grad, float *const *d_exp_avg,
                   float *const *d_exp_avg_sq, const int32_t *row_width, int64_t n_rows, const int32_t *d_rows,
                   const void *d_count, int32_t count_is64, int32_t count_mul, int64_t n_max, int32_t row0,
-                  int32_t *d_last, int32_t *d_claim, int32_t tag, void *d_ws, size_t ws_bytes, int32_t reuse,
-                  float *d_sched, double lr, double beta1, double beta2, double eps, int64_t step, int32_t apply,
-                  int32_t zero_grad, sgn_stream_t stream) {
+                  const int32_t *d_rows2, const int64_t *d_count2, int64_t n_max2, int32_t *d_last,
+                  int32_t *d_claim, int32_t *d_claim2, int32_t tag, void *d_ws, size_t ws_bytes, void *d_pend,
+                  size_t pend_bytes, float *d_sched, double lr, double beta1, double beta2, double eps, int64_t step,
+                  int32_t apply, int32_t zero_grad, sgn_stream_t stream) {
     SGN_REQUIRE(n_t >= 1 && n_t <= kMaxRowTensors, "sgn_adam_rows: 1 <= n_t <= 4");
-    SGN_REQUIRE(step >= 1 && step < (1ll << 31), "sgn_adam_rows: 1 <= step < 2^31");
+    SGN_REQUIRE(step >= (apply ? 1 : 0) && step < (1ll << 31), "sgn_adam_rows: 0 <= step < 2^31 (apply: >= 1)");
     SGN_REQUIRE(d_param && d_exp_avg && d_exp_avg_sq && row_width && d_last && d_claim && d_sched && d_ws,
                 "sgn_adam_rows: null argument");
     SGN_REQUIRE(!apply || d_grad, "sgn_adam_rows: apply needs the gradients");
-    SGN_REQUIRE(!reuse || apply, "sgn_adam_rows: reuse is the step after a catch-up of the same list");
-    SGN_REQUIRE(n_max >= 0 && (d_rows || n_max <= n_rows), "sgn_adam_rows: n_max");
-    SGN_REQUIRE(ws_bytes >= sgn_adam_rows_workspace_bytes(n_max + 1), "sgn_adam_rows: workspace too small");
+    SGN_REQUIRE(n_max >= 0 && n_max2 >= 0 && (d_rows || n_max <= n_rows), "sgn_adam_rows: n_max");
+    SGN_REQUIRE(!d_rows2 || d_count2, "sgn_adam_rows: list 2 needs its device count");
+    SGN_REQUIRE(!d_pend || d_claim2, "sgn_adam_rows: the pend list needs the second claim array");
+    const int64_t entries = n_max + (d_rows2 ? n_max2 : 0) + (row0 ? 1 : 0);
+    SGN_REQUIRE(ws_bytes >= sgn_adam_rows_workspace_bytes(std::min<int64_t>(entries, n_rows)),
+                "sgn_adam_rows: workspace too small");
+    SGN_REQUIRE(!d_pend || pend_bytes >= sgn_adam_rows_pend_bytes(std::min<int64_t>(n_max + 1, n_rows)),
+                "sgn_adam_rows: pend list too small");
+    SGN_REQUIRE(!d_count || count_mul >= 1, "sgn_adam_rows: count_mul >= 1");
     AdamRowsArgs a{};
     a.nt = n_t;
     a.wsum = 0;
@@ -721,36 +758,37 @@ int sgn_adam_rows(int32_t n_t, float *const *d_param, float *const *d_grad, floa
     a.row0 = row0 ? 1 : 0;
     a.n_max = n_max;
     a.n_rows = n_rows;
-    SGN_REQUIRE(!d_count || count_mul >= 1, "sgn_adam_rows: count_mul >= 1");
+    a.rows2 = d_rows2;
+    a.d_count2 = d_count2;
+    a.n_max2 = n_max2;
     a.last = d_last;
     a.claim = d_claim;
+    a.claim2 = d_claim2;
     a.tag = tag;
     a.ws = static_cast<int32_t *>(d_ws);
+    a.cap = std::min<int64_t>(entries, n_rows);
+    a.pend = static_cast<int64_t *>(d_pend);
     a.sched = reinterpret_cast<float2 *>(d_sched);
     a.target = (int32_t)step;
     a.apply = apply ? 1 : 0;
-    a.reuse = reuse ? 1 : 0;
     // the scalars exactly as sgn_adam_step_multi forms them
     a.b1 = (float)beta1;
     a.b2 = (float)beta2;
     a.omb1 = (float)(1.0 - beta1);
     a.omb2 = (float)(1.0 - beta2);
-    a.ss_t = (float)(lr / (1.0 - std::pow(beta1, (double)step)));
-    a.bs_t = (float)std::sqrt(1.0 - std::pow(beta2, (double)step));
+    a.ss_t = apply ? (float)(lr / (1.0 - std::pow(beta1, (double)step))) : 0.f;
+    a.bs_t = apply ? (float)std::sqrt(1.0 - std::pow(beta2, (double)step)) : 0.f;
     a.eps = (float)eps;
     a.zero_grad = zero_grad ? 1 : 0;
+    SGN_REQUIRE(a.cap * a.wsum < (1ll << 31), "sgn_adam_rows: rows x elements < 2^31");
     hipStream_t st = as_stream(stream);
-    const int64_t entries = n_max + 1;
-    if (!reuse) {
-        SGN_CHECK_HIP(hipMemsetAsync(d_ws, 0, 4, st));
-        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((entries + 255) / 256, 256 * 16));
-        hipLaunchKernelGGL(k_rows_claim, dim3((unsigned)blocks), dim3(256), 0, st, a);
-        SGN_CHECK_HIP(hipGetLastError());
-    }
-    const int64_t pairs = std::min<int64_t>(entries, n_rows) * a.wsum;
-    SGN_REQUIRE(pairs < (1ll << 31), "sgn_adam_rows: rows x elements < 2^31");
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((pairs + 255) / 256, 256 * 64));
-    hipLaunchKernelGGL(k_rows_update, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    SGN_CHECK_HIP(hipMemsetAsync(d_ws, 0, 4, st));
+    if (d_pend) SGN_CHECK_HIP(hipMemsetAsync(d_pend, 0, 16, st));
+    const int64_t cblocks = std::max<int64_t>(1, std::min<int64_t>((entries + 255) / 256, 256 * 16));
+    hipLaunchKernelGGL(k_rows_claim, dim3((unsigned)cblocks), dim3(256), 0, st, a);
+    SGN_CHECK_HIP(hipGetLastError());
+    const int64_t ublocks = std::max<int64_t>(1, std::min<int64_t>((a.cap * a.wsum + 255) / 256, 256 * 64));
+    hipLaunchKernelGGL(k_rows_update, dim3((unsigned)ublocks), dim3(256), 0, st, a);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }
