@@ -159,16 +159,31 @@ struct AdamRowsArgs {
     int32_t zero_grad;
 };
 
-__device__ __forceinline__ int wave_append(int *ctr, bool take, int lane) {
-    const uint64_t bal = __ballot(take);
-    int base = 0;
-    if (bal && lane == 0) base = atomicAdd(ctr, __popcll(bal));
-    base = __shfl(base, 0);
-    return base + __popcll(bal & ((1ull << lane) - 1));
+// exclusive prefix sum of v over the workgroup's 256 threads and the total (LDS scratch [256])
+__device__ __forceinline__ int block_scan(int v, int *sc, int &total) {
+    const int t = threadIdx.x;
+    sc[t] = v;
+    __syncthreads();
+#pragma unroll
+    for (int o = 1; o < 256; o <<= 1) {
+        const int x = t >= o ? sc[t - o] : 0;
+        __syncthreads();
+        sc[t] += x;
+        __syncthreads();
+    }
+    total = sc[255];
+    const int ex = sc[t] - v;
+    __syncthreads();
+    return ex;
 }
 
-// one lane per list entry: the row's first claimant appends (row, last[row]) and sets last[row]
+// A workgroup takes CLAIM_PER entries (CLAIM_PER / 256 per thread): the row's first claimant records
+// (row, last[row]) and sets last[row]; the winners are appended with one counter atomic per workgroup
+// and list (one per wave serialised ~3.6 k atomics on each counter: 60 us)
+constexpr int CLAIM_EPT = 2, CLAIM_PER = 256 * CLAIM_EPT;
 __global__ __launch_bounds__(256) void k_rows_claim(AdamRowsArgs a) {
+    __shared__ int sc[256];
+    __shared__ int base_s[2];
     int64_t n1 = a.n_max;
     if (a.d_count) {
         const int64_t c = a.count_is64 ? *(const int64_t *)a.d_count : (int64_t)*(const int32_t *)a.d_count;
@@ -176,41 +191,52 @@ __global__ __launch_bounds__(256) void k_rows_claim(AdamRowsArgs a) {
     }
     const int64_t n2 = a.rows2 ? min(a.n_max2, *a.d_count2) : 0;
     const int64_t n = n1 + n2 + a.row0;
-    const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int32_t *prow = a.pend ? (int32_t *)(a.pend + 2) : nullptr;
-    // wave-uniform trip count: the ballots below see every lane
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < n; i0 += stride) {
-        const int64_t i = i0 + lane;
-        int r = -1;
-        bool l1 = false;
-        if (i < n1) r = a.rows ? a.rows[i] : (int)i, l1 = true;
-        else if (i < n1 + n2) r = a.rows2[i - n1];
-        else if (i < n) r = 0, l1 = true;
-        const bool valid = r >= 0 && r < a.n_rows;
-        if (a.pend && l1 && r >= a.n_rows) atomicAdd((unsigned long long *)(a.pend + 1), 1ull);
-        bool win = false;
-        int from = 0;
-        // test, then test-and-set: a point is the neighbour of many samples, and its repeats would
-        // otherwise serialise on one address's atomics
-        if (valid && __builtin_nontemporal_load(a.claim + r) != a.tag && atomicExch(a.claim + r, a.tag) != a.tag) {
-            win = true;   // rows already at the target stay in the list: the update rewrites them unchanged
-            from = a.last[r];
-            a.last[r] = a.target;
+    for (int64_t b0 = (int64_t)blockIdx.x * CLAIM_PER; b0 < n; b0 += (int64_t)gridDim.x * CLAIM_PER) {
+        int rr[CLAIM_EPT], fr[CLAIM_EPT];
+        uint32_t wm = 0, pm = 0;   // this thread's winners / pend entries (bit e)
+        int oob = 0;
+#pragma unroll
+        for (int e = 0; e < CLAIM_EPT; ++e) {
+            const int64_t i = b0 + e * 256 + threadIdx.x;
+            int r = -1;
+            bool l1 = false;
+            if (i < n1) r = a.rows ? a.rows[i] : (int)i, l1 = true;
+            else if (i < n1 + n2) r = a.rows2[i - n1];
+            else if (i < n) r = 0, l1 = true;
+            const bool valid = r >= 0 && r < a.n_rows;
+            oob += l1 && r >= a.n_rows;
+            rr[e] = r;
+            fr[e] = 0;
+            // test, then test-and-set (a point repeats across many samples' neighbour lists)
+            if (valid && __builtin_nontemporal_load(a.claim + r) != a.tag && atomicExch(a.claim + r, a.tag) != a.tag) {
+                fr[e] = a.last[r];
+                a.last[r] = a.target;
+                wm |= 1u << e;
+            }
+            if (a.pend && l1 && valid && __builtin_nontemporal_load(a.claim2 + r) != a.tag &&
+                atomicExch(a.claim2 + r, a.tag) != a.tag)
+                pm |= 1u << e;
         }
-        const bool pd = a.pend && l1 && valid && __builtin_nontemporal_load(a.claim2 + r) != a.tag &&
-                        atomicExch(a.claim2 + r, a.tag) != a.tag;
-        const int slot = wave_append(a.ws, win, lane);
-        if (win) {
-            a.ws[4 + slot] = r;
-            a.ws[4 + a.cap + slot] = from;
+        if (a.pend && oob) atomicAdd((unsigned long long *)(a.pend + 1), (unsigned long long)oob);
+        int tw, tp;
+        const int ew = block_scan(__popc(wm), sc, tw);
+        const int ep = a.pend ? block_scan(__popc(pm), sc, tp) : 0;
+        if (threadIdx.x == 0) {
+            base_s[0] = tw ? atomicAdd(a.ws, tw) : 0;
+            base_s[1] = a.pend && tp ? (int)atomicAdd((unsigned long long *)a.pend, (unsigned long long)tp) : 0;
         }
-        if (a.pend) {
-            const uint64_t bal = __ballot(pd);
-            unsigned long long base = 0;
-            if (bal && lane == 0) base = atomicAdd((unsigned long long *)a.pend, (unsigned long long)__popcll(bal));
-            base = __shfl(base, 0);
-            if (pd) prow[base + __popcll(bal & ((1ull << lane) - 1))] = r;
+        __syncthreads();
+        int sw = base_s[0] + ew, sp = base_s[1] + ep;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < CLAIM_EPT; ++e) {
+            if (wm >> e & 1) {
+                a.ws[4 + sw] = rr[e];
+                a.ws[4 + a.cap + sw] = fr[e];
+                ++sw;
+            }
+            if (pm >> e & 1) prow[sp++] = rr[e];
         }
     }
 }
@@ -237,8 +263,15 @@ __global__ __launch_bounds__(256) void k_rows_update(AdamRowsArgs a) {
         const int from = a.ws[4 + a.cap + w];
         const int64_t e = (int64_t)r * a.w[t] + c;
         float p = a.p[t][e], m = a.m[t][e], v = a.v[t][e];
-        for (int k = from + 1; k <= upto; ++k) {
-            const float2 sc = k > lo ? win[k - 1 - lo] : a.sched[k - 1];
+        // two loops, so the common one reads LDS only (one loop selecting between LDS and the table
+        // compiled to a flat load and a full wait per step)
+        int k = from + 1;
+        for (; k <= min(upto, lo); ++k) {
+            const float2 sc = a.sched[k - 1];
+            adam_el(p, 0.f, m, v, a.b1, a.b2, a.omb1, a.omb2, sc.x, sc.y, a.eps);
+        }
+        for (; k <= upto; ++k) {
+            const float2 sc = win[k - 1 - lo];
             adam_el(p, 0.f, m, v, a.b1, a.b2, a.omb1, a.omb2, sc.x, sc.y, a.eps);
         }
         if (a.apply && from < a.target) {
@@ -784,7 +817,7 @@ int sgn_adam_rows(int32_t n_t, float *const *d_param, float *const *d_grad, floa
     hipStream_t st = as_stream(stream);
     SGN_CHECK_HIP(hipMemsetAsync(d_ws, 0, 4, st));
     if (d_pend) SGN_CHECK_HIP(hipMemsetAsync(d_pend, 0, 16, st));
-    const int64_t cblocks = std::max<int64_t>(1, std::min<int64_t>((entries + 255) / 256, 256 * 16));
+    const int64_t cblocks = std::max<int64_t>(1, std::min<int64_t>((entries + CLAIM_PER - 1) / CLAIM_PER, 256 * 4));
     hipLaunchKernelGGL(k_rows_claim, dim3((unsigned)cblocks), dim3(256), 0, st, a);
     SGN_CHECK_HIP(hipGetLastError());
     const int64_t ublocks = std::max<int64_t>(1, std::min<int64_t>((a.cap * a.wsum + 255) / 256, 256 * 64));
