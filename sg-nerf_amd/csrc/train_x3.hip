@@ -938,62 +938,72 @@ __device__ __forceinline__ void row_geometry(const RowArgs &a, const Cam &cam, i
 constexpr int X0_QUADS = 72, ROW_QUADS = 74;
 
 __global__ __launch_bounds__(TPB) void k_row_inputs(RowArgs a, float *x0, float *ext, float2 *rw, float *vpe) {
-    // the item's rows' embeddings, staged once per item: the PE tasks read them here instead of
-    // issuing a dependent global load per task (the loop waited out the latency task by task)
-    __shared__ __attribute__((aligned(16))) float se[TPB / 64][8 * 32];  // K <= 8 rows
-    const int lane = threadIdx.x & 63, wl = threadIdx.x >> 6;
+    // Two items per wave, one per half-wave (lanes 32 h .. 32 h + 31): the items' dependent index chains
+    // (work -> sample -> neighbours -> point records) are in flight together, so a wave pays that
+    // latency once per two items.  The items' rows' embeddings are staged in LDS once (the PE tasks
+    // read them there instead of issuing a dependent global load per task).
+    __shared__ __attribute__((aligned(16))) float se[TPB / 64][2][8 * 32];  // K <= 8 rows per item
+    const int lane = threadIdx.x & 63, wl = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
     const int wv = blockIdx.x * (TPB / 64) + wl, nw = gridDim.x * (TPB / 64);
     const Cam cam = load_cam(a.campos, a.rot);
     const int n = n_items(a);
-    for (int it = wv; it < n; it += nw) {
-        const int s = a.work[it];
-        const int nnb = a.samp_nnb[s], ro = a.row_off[s];
-        const int ray = a.samp_ray[s];
-        // lanes k < K: row k's geometry and weight; normalised over the sample's rows
-        const int kl = lane < a.K ? lane : 0;
-        const int pidl = lane < nnb ? a.pidx[(int64_t)s * a.K + kl] : -1;
+    for (int i2 = wv; 2 * i2 < n; i2 += nw) {
+        const int it = 2 * i2 + h;
+        const bool iv = it < n;
+        const int s = iv ? a.work[it] : 0;
+        const int nnb = iv ? a.samp_nnb[s] : 0, ro = iv ? a.row_off[s] : 0;
+        const int ray = iv ? a.samp_ray[s] : 0;
+        // lanes k < K of each half: row k's geometry and weight; normalised over the sample's rows
+        const int kl = l32 < a.K ? l32 : 0;
+        const int pidl = l32 < nnb ? a.pidx[(int64_t)s * a.K + kl] : -1;
         float dl[6], w, cf;
         row_geometry(a, cam, s, pidl, dl, w, cf);
         float wsum = w;
 #pragma unroll
-        for (int o = 1; o < 8; o <<= 1) wsum += __shfl_xor(wsum, o);  // lanes 0..7 (K <= 8)
-        wsum = __shfl(wsum, 0);
+        for (int o = 1; o < 8; o <<= 1) wsum += __shfl_xor(wsum, o);  // lanes 32 h .. 32 h + 7 (K <= 8)
+        wsum = __shfl(wsum, 32 * h);
         const float wn = w / fmaxf(wsum, 1e-8f);
         const float wgt = wn * fminf(fmaxf(cf, 1e-4f), 1.f);
-        if (lane < nnb) rw[ro + lane] = make_float2(wgt, wn);
+        if (l32 < nnb) rw[ro + l32] = make_float2(wgt, wn);
         const float vx = a.raydir[(int64_t)ray * 3], vy = a.raydir[(int64_t)ray * 3 + 1], vz = a.raydir[(int64_t)ray * 3 + 2];
-        if (lane < 32) {  // the item's PE(viewdir) for the colour MLP (:772-780), ones column 24
-            float v = lane == 24 ? 1.f : 0.f;
-            if (lane < 24) {
-                const int jj = lane < 12 ? lane : lane - 12, c = jj >> 2, f = jj & 3;
+        if (iv) {  // the item's PE(viewdir) for the colour MLP (:772-780), ones column 24
+            float v = l32 == 24 ? 1.f : 0.f;
+            if (l32 < 24) {
+                const int jj = l32 < 12 ? l32 : l32 - 12, c = jj >> 2, f = jj & 3;
                 float sn, cs;
                 sincos_acc((c == 0 ? vx : c == 1 ? vy : vz) * (float)(1 << f), sn, cs);
-                v = lane < 12 ? sn : cs;
+                v = l32 < 12 ? sn : cs;
             }
-            vpe[(int64_t)it * 32 + lane] = v;
+            vpe[(int64_t)it * 32 + l32] = v;
         }
-        {   // lane l: floats 4 (l & 7) .. + 3 of row l >> 3
-            const int k = lane >> 3;
-            const int pk = __shfl(pidl, k);
-            f32x4 e4 = {0.f, 0.f, 0.f, 0.f};
-            if (k < nnb && pk >= 0) e4 = *(const f32x4 *)(a.emb + (int64_t)pk * 32 + 4 * (lane & 7));
-            *(f32x4 *)&se[wl][32 * k + 4 * (lane & 7)] = e4;
+        {   // half-lane l: floats 8 (l & 3) .. + 7 of row l >> 2
+            const int k = l32 >> 2;
+            const int pk = __shfl(pidl, 32 * h + k);
+            f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = e0;
+            if (k < nnb && pk >= 0) {
+                const f32x4 *src = (const f32x4 *)(a.emb + (int64_t)pk * 32 + 8 * (l32 & 3));
+                e0 = src[0];
+                e1 = src[1];
+            }
+            *(f32x4 *)&se[wl][h][32 * k + 8 * (l32 & 3)] = e0;
+            *(f32x4 *)&se[wl][h][32 * k + 8 * (l32 & 3) + 4] = e1;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its own writes are every lane's
         }
         const int ntask = nnb * ROW_QUADS;
-        for (int t0 = 0; t0 < ntask; t0 += 64) {  // wave-uniform trip count: the shuffles see every lane
-            const int t = t0 + lane;
+        const int nmax = max(ntask, __shfl_xor(ntask, 32));
+        for (int t0 = 0; t0 < nmax; t0 += 32) {  // wave-uniform trip count: the shuffles see every lane
+            const int t = t0 + l32;
             const bool act = t < ntask;
             const int k = act ? t / ROW_QUADS : 0, q = t - k * ROW_QUADS;
-            const int pid = __shfl(pidl, k);
+            const int pid = __shfl(pidl, 32 * h + k);
             float d[6];
 #pragma unroll
-            for (int c = 0; c < 6; ++c) d[c] = __shfl(dl[c], k);
+            for (int c = 0; c < 6; ++c) d[c] = __shfl(dl[c], 32 * h + k);
             if (!act) continue;
             const int64_t row = ro + k;
             const int64_t pb = (int64_t)pid * 3;
             if (q < X0_QUADS) {
-                *(f32x4 *)(x0 + row * 288 + 4 * q) = x0_quad(4 * q, &se[wl][32 * k], d);
+                *(f32x4 *)(x0 + row * 288 + 4 * q) = x0_quad(4 * q, &se[wl][h][32 * k], d);
             } else if (q == X0_QUADS) {  // block3.0's extra channels (:639-652): colour, dir - v
                 f32x4 u;
                 u[0] = a.color[pb]; u[1] = a.color[pb + 1]; u[2] = a.color[pb + 2];
