@@ -740,9 +740,16 @@ class HipTrainer:
         R = raydir.shape[0]
         bg_ray = self._bg_ray(bg_ray, R)
         q = self._query(campos, raydir, near, far, labels)
+        dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if not dp:   # the counts leave right after the query: the host waits for the query only
+            if not hasattr(self, "_cnt_host"):
+                self._cnt_host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+                self._cnt_event = torch.cuda.Event()
+            self._cnt_host.copy_(q.counters[:2], non_blocking=True)
+            self._cnt_event.record()
         self._adam_rows(q.pidx, q.counters, False, o.K)
-        # work that does not depend on the query is queued before the step's one host sync, so
-        # the GPU runs it while the host waits
+        # work that does not depend on the counts is queued before the step's one host sync, so the
+        # GPU runs it while the host waits, and still has it queued when the host issues the rest
         blob, tblob = self.packer.pack(self.mlp.flat)
         for p in self.point_params + [self.mlp.flat]:
             if p.grad is None:
@@ -750,13 +757,13 @@ class HipTrainer:
             elif not self._grads_clean:
                 p.grad.zero_()
         self._grads_clean = False
-        dp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         if dp:   # the point rows this rank's step can touch, and every rank's count, ride the same sync
             t_idx, t_cnt = touched_rows(q.pidx, q.counters[0], o.K, self.points.xyz.shape[0])
             sync = torch.cat([q.counters[:2].to(torch.int64), gather_counts(t_cnt)])
+            S, n, *t_counts = (int(x) for x in sync.tolist())  # one host sync per step
         else:
-            sync = q.counters[:2]
-        S, n, *t_counts = (int(x) for x in sync.tolist())  # one host sync per step
+            self._cnt_event.synchronize()   # one host sync per step, on the query's counts
+            S, n = (int(x) for x in self._cnt_host.tolist())
         self._last_q = q
         graph = self.use_graph and dev.type == "cuda"
         if graph:
