@@ -5,7 +5,6 @@
 set -u
 TAG=$1
 bash tools/gpu_full.sh $TAG || exit 1
-bash tools/prof_train.sh ${TAG}_f32 --steps 20 --warmup 5 > /dev/null || exit 1
-bash tools/prof_train.sh ${TAG}_f16 --train-precision f16 --steps 20 --warmup 5 > /dev/null || exit 1
+bash tools/gpu_train_trace.sh $TAG || exit 1
 bash tools/gpu_pmc_final.sh $TAG || exit 1
 echo ROUND_END_DONE
