@@ -12,6 +12,8 @@ patches:
   abl_dma  no weight LDS-DMA (wrong results)          abl_bar  no chunk-boundary waits / barrier
   abl_conv no hi/lo conversion of the chained layers   abl_epi  no block3.2 epilogue
   abl_pe   no PE(dists) sin/cos (block1.0's input constant)
+  cabl_dma / cabl_bar / cabl_fs / cabl_out: the colour kernel (k_color16) without its weight DMA, its
+           chunk-boundary waits and barriers, its f_s row loads, its output layer
 The ablations compute wrong results by design: timing only."""
 import os
 import shutil
@@ -391,6 +393,41 @@ struct EpiC {
         s = rep(s, '''            for (int q = 0; q < NS; ++q) epi_begin(e[q], ldsi, rw[q].wgt, nA[q], nB[q], ce[q], eslot[q] < nslots);''',
                 '''            for (int q = 0; q < NS; ++q) epi_begin(e[q], ldsi, rw[q].wgt, nA[q], nB[q], ce[q], eslot[q] < nslots);
             epi_consts(ldsi);''')
+    elif p == "cabl_dma":   # colour kernel: no weight LDS-DMA
+        s = rep(s, """    using S = Sched<Net>;
+    constexpr int nf = 2 * S::pairs(N);
+    static_for<(nf + NWv - 1) / NWv>([&](auto jj) {""", """    using S = Sched<Net>;
+    constexpr int nf = 2 * S::pairs(N);
+    if constexpr (Net::NL == 3) return;
+    static_for<(nf + NWv - 1) / NWv>([&](auto jj) {""")
+        s = rep(s, """    constexpr int PW = (nf + NWv - 1) / NWv;
+    const int i = w * PW + J;""", """    constexpr int PW = (nf + NWv - 1) / NWv;
+    if constexpr (Net::NL == 3) return;
+    const int i = w * PW + J;""")
+    elif p == "cabl_bar":   # colour kernel: no chunk-boundary waits / barrier
+        s = rep(s, """    static_assert(VM >= 0 && VM < 64, "vmcnt range");
+    if constexpr (VM == 0)""", """    static_assert(VM >= 0 && VM < 64, "vmcnt range");
+    if constexpr (Net::NL == 3) return;
+    if constexpr (VM == 0)""")
+    elif p == "cabl_fs":    # colour kernel: no f_s row loads
+        s = rep(s, """#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            fr[2 * k] = row[8 * k];
+            fr[2 * k + 1] = row[8 * k + 1];
+        }""", """        (void)row;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            fr[2 * k] = f32x4{0.25f, 0.5f, 0.125f, 1.f};
+            fr[2 * k + 1] = f32x4{0.25f, 0.5f, 0.125f, 1.f};
+        }""")
+    elif p == "cabl_out":   # colour kernel: no output layer
+        s = rep(s, """        float o[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            f32x4 wc[3];""", """        float o[3] = {c0[0][0], c0[1][1], c0[2][2]};
+#pragma unroll
+        for (int t = 0; t < 0; ++t) {
+            f32x4 wc[3];""")
     elif p == "abl_dma":
         s = rep(s, '''    asm volatile("" : "+s"(soff));
     __builtin_amdgcn_raw_ptr_buffer_load_lds(''', '''    return;
