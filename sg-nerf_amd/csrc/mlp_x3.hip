@@ -1368,29 +1368,49 @@ __global__ __launch_bounds__(TPBC, 8 / NWC) void k_color16(ColorArgs a) {
     __syncthreads();
     int slot = 0;
     dma_chunk<NetColor16, 0, NWC>(wb, lds, w, lane, 0);
-    // The tile's f_s rows and sample ids, then its ray ids, then its ray directions: the next tile's
-    // rows and sample ids go out in colour 1, its ray ids in colour 2 and its directions in its own
-    // colour 0 (needed by colour 0's last k-step), each step one chunk after the load it depends on,
-    // so no hook waits on a dependent load
+    // The tile's f_s rows go out in four quarters (k-steps 2 q, 2 q + 1 of colour 0), each at a chunk
+    // boundary after its registers were consumed and a chunk before they are needed: the next tile's
+    // quarter 0 in colour 0's second chunk, quarter 1 (and the sample ids) in colour 1, quarter 2 (and
+    // the ray ids) in colour 2, quarter 3 in the tile's own first chunk with its ray directions.  The
+    // rows as one 16 KiB-per-wave burst had to land within one chunk (vmcnt retires in order: the next
+    // boundary's wait for its weight pieces waits for them too), and did not (colour stage -23 % without
+    // them, tools/x3_variant.py cabl_fs).
     f32x4 fr[16];
     float vd[3];
     int sn = 0, rn = 0;
-    auto load_rows = [&](int item) {
+    // The quarters are asm loads, outside the compiler's wait tracking: with an LDS-DMA outstanding it
+    // waits vmcnt(0) at the first use of any load result, which would drain a quarter right after it
+    // was issued.  A quarter issued in a chunk's hook is older than the next chunk's weight pieces, so
+    // that chunk's boundary wait has retired it; its first use re-reads the registers through an empty
+    // asm after that boundary (in order with the boundary's asm), so no read moves above it.
+    auto load_q = [&](auto qc, int item) {
+        constexpr int Q = decltype(qc)::value;
         const bool ok = item < end;
-        sn = ok ? a.work[item] : 0;
-        const f32x4 *row = (const f32x4 *)(a.fs + (int64_t)(ok ? item - a.item0 : 0) * HID + 8 * g);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            fr[2 * k] = row[8 * k];
-            fr[2 * k + 1] = row[8 * k + 1];
-        }
+        const f32x4 *row = (const f32x4 *)(a.fs + (int64_t)(ok ? item - a.item0 : 0) * HID + 8 * g) + 16 * Q;
+        f32x4 t0, t1, t2, t3;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(t0) : "v"(row));
+        asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(t1) : "v"(row));
+        asm volatile("global_load_dwordx4 %0, %1, off offset:128" : "=v"(t2) : "v"(row));
+        asm volatile("global_load_dwordx4 %0, %1, off offset:144" : "=v"(t3) : "v"(row));
+        fr[4 * Q] = t0;
+        fr[4 * Q + 1] = t1;
+        fr[4 * Q + 2] = t2;
+        fr[4 * Q + 3] = t3;
     };
+    auto load_sid = [&](int item) { sn = item < end ? a.work[item] : 0; };
     auto load_ray = [&]() { rn = a.samp_ray[sn]; };
     auto load_dir = [&]() {
 #pragma unroll
         for (int c = 0; c < 3; ++c) vd[c] = a.raydir[(int64_t)rn * 3 + c];
     };
-    load_rows(a.item0 + blockIdx.x * (16 * NWC) + w * 16 + r);
+    {
+        const int item = a.item0 + blockIdx.x * (16 * NWC) + w * 16 + r;
+        load_sid(item);
+        load_q(std::integral_constant<int, 0>{}, item);
+        load_q(std::integral_constant<int, 1>{}, item);
+        load_q(std::integral_constant<int, 2>{}, item);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the first tile's quarters (no boundary between)
+    }
     load_ray();
     for (int base = a.item0 + blockIdx.x * (16 * NWC); base < end; base += gridDim.x * (16 * NWC)) {
         int lz = 0;
@@ -1417,7 +1437,8 @@ __global__ __launch_bounds__(TPBC, 8 / NWC) void k_color16(ColorArgs a) {
             constexpr int K = decltype(k)::value;
             float v[8];
             if constexpr (K < 8) {
-                const f32x4 u0 = fr[2 * K], u1 = fr[2 * K + 1];
+                f32x4 u0 = fr[2 * K], u1 = fr[2 * K + 1];
+                asm volatile("" : "+v"(u0), "+v"(u1));   // after the boundary that retired them
                 v[0] = u0[0]; v[1] = u0[1]; v[2] = u0[2]; v[3] = u0[3];
                 v[4] = u1[0]; v[5] = u1[1]; v[6] = u1[2]; v[7] = u1[3];
             } else {
@@ -1441,19 +1462,30 @@ __global__ __launch_bounds__(TPBC, 8 / NWC) void k_color16(ColorArgs a) {
             }
             return split8(v);
         }, [&](auto c) {
-            if constexpr (decltype(c)::value == 0) load_dir();  // this tile's directions (k-step 8)
+            constexpr int C = decltype(c)::value;
+            if constexpr (C == 0) {
+                load_q(std::integral_constant<int, 3>{}, item);   // this tile's k-steps 6, 7 (next chunk)
+                load_dir();                                        // this tile's directions (k-step 8)
+            }
+            if constexpr (C == 1) load_q(std::integral_constant<int, 0>{}, item + gridDim.x * (16 * NWC));
         });
         bias(c1, Y_CB1);
         const float inv4 = Yl[Y_INV + 4], inv5 = Yl[Y_INV + 5], inv6 = Yl[Y_INV + 6];
-        // colour 0 consumed fr: the next tile's rows go out after colour 1's boundary (land under it)
+        // colour 0 consumed fr: the next tile's quarters 1, 2 go out at colour 1's and colour 2's boundaries
         run_layer16<NetColor16, 1>(wb, ldsi, slot, w, lane, lz, c1, [&](auto k) { return chain(c0, inv4, k); },
                                    [&](auto c) {
-                                       if constexpr (decltype(c)::value == 0) load_rows(item + gridDim.x * (16 * NWC));
+                                       if constexpr (decltype(c)::value == 0) {
+                                           load_q(std::integral_constant<int, 1>{}, item + gridDim.x * (16 * NWC));
+                                           load_sid(item + gridDim.x * (16 * NWC));
+                                       }
                                    });
         bias(c0, Y_CB2);
         run_layer16<NetColor16, 2>(wb, ldsi, slot, w, lane, lz, c0, [&](auto k) { return chain(c1, inv5, k); },
                                    [&](auto c) {
-                                       if constexpr (decltype(c)::value == 0) load_ray();  // the next tile's ray ids
+                                       if constexpr (decltype(c)::value == 0) {
+                                           load_q(std::integral_constant<int, 2>{}, item + gridDim.x * (16 * NWC));
+                                           load_ray();  // the next tile's ray ids
+                                       }
                                    });
         // output layer: units 16 t + 4 g + i of this lane, summed over the 4 lane groups (the four
         // weights of a (t, c) as one 16-B LDS read: this file is built without SLP vectorisation)
