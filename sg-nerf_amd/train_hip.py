@@ -422,6 +422,12 @@ class PointAdam(torch.optim.Adam):
         self.flush()
         return super().state_dict()
 
+    def zero_grad(self, set_to_none=True):
+        """A deferred step reads its gradient at the next launch: apply it before the gradient goes."""
+        if self.rows_mode and self._pending is not None:
+            self.flush()
+        super().zero_grad(set_to_none)
+
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         if self.rows_mode:   # the loaded tensors are a dense state: every row holds its step

@@ -442,8 +442,10 @@ def test_point_adam_matches_torch_adam(sizes):
     assert all(float(oa.state[x]["step"]) == 3.0 for x in a)
 
 
-@pytest.mark.parametrize("n_rows,steps,flush_every", [(5_003, 12, 256), (20_000, 9, 4), (7, 5, 256)])
-def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every):
+@pytest.mark.parametrize("n_rows,steps,flush_every,dp", [(5_003, 12, 256, False), (20_000, 9, 4, False),
+                                                         (7, 5, 256, False), (5_003, 12, 256, True),
+                                                         (20_000, 9, 4, True)])
+def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every, dp):
     """PointAdam(rows=True) (sgn_adam_rows: a step's update deferred to the next step's launch, which
     brings the rows it lists forward, each first replaying the zero-gradient steps it missed) against
     the dense PointAdam on the point group's
@@ -451,7 +453,10 @@ def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every):
     row 0 (the loss stage's conf read), the list holds those rows as a neighbour table would (-1
     slots, duplicates, a device int32 count times K), lr decays per step.  Rows a step reads equal
     the dense state at its start, and after flush() every parameter and moment equals the dense
-    one exactly (the same fp32 operations in the same order); state_dict() flushes."""
+    one exactly (the same fp32 operations in the same order); state_dict() flushes, and so does
+    zero_grad() while a step is pending.  dp: the data-parallel sequence of HipTrainer (the exchanged
+    gradient also holds other ranks' rows, which this rank's step never read; set_update_rows gets
+    every rank's list as _allreduce_point_rows returns it: padded slices, duplicates, pad row N-1)."""
     from sgnerf_amd.train_hip import PointAdam
     g = torch.Generator().manual_seed(n_rows + steps)
     widths = (32, 3, 3, 1)
@@ -478,16 +483,30 @@ def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every):
         n_pb = int(pb[:8].view(torch.int64).item())                  # the step's distinct rows, row 0 too
         assert n_pb == torch.unique(read).numel() and int(pb[8:16].view(torch.int64).item()) == 0
         assert torch.equal(torch.sort(pb[16:].view(torch.int32)[:n_pb].long()).values, torch.unique(read))
+        upd = read
+        if dp:   # two other ranks' rows (most of them never read here), as all_gather lays them out
+            other = [torch.unique(torch.randint(0, n_rows, (n_s * 3,), generator=g)) for _ in range(2)]
+            slices = [read.cpu()] + [torch.cat([o, torch.zeros(1, dtype=torch.long)]) for o in other]
+            m = max(s.numel() for s in slices)
+            all_idx = torch.full((3, m), n_rows - 1, dtype=torch.long)
+            for r, s in enumerate(slices):
+                all_idx[r, :s.numel()] = s
+            upd = torch.unique(all_idx).to(DEV)
         for x, y, w in zip(a, b, widths):
             gr = torch.zeros(n_rows, w)
-            gr[used] = torch.randn(used.numel(), w, generator=g) * 10 ** (it % 3 - 1)
+            gr[upd.cpu()] = torch.randn(upd.numel(), w, generator=g) * 10 ** (it % 3 - 1)
             gr[0] = torch.randn(w, generator=g)
             x.grad = gr.to(DEV)
             y.grad = gr.to(DEV)
+        if dp:
+            orow.set_update_rows(all_idx.reshape(-1).to(DEV).to(torch.int32))
         for o in (od, orow):
             o.param_groups[0]["lr"] = 2e-3 * 0.97 ** it
         od.step()
         orow.step()                                                  # deferred to the next set_rows
+        if it == 1:
+            orow.zero_grad(set_to_none=False)                        # applies the pending step first
+            assert all(torch.count_nonzero(y.grad) == 0 for y in b)
     sd = orow.state_dict()                                           # flushes: the last step applied
     for x, y in zip(a, b):
         assert torch.count_nonzero(y.grad) == 0
@@ -495,6 +514,65 @@ def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every):
         for k in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(od.state[x][k], orow.state[y][k])
     assert all(float(v["step"]) == steps for v in sd["state"].values())
+
+
+def _fake_two_ranks(monkeypatch):
+    """torch.distributed as two ranks holding the same batch: all_reduce sums two equal copies,
+    all_gather_into_tensor lays out two equal slices (the driver's multi-GPU runs are the only real
+    N > 1 runs; this drives HipTrainer's data-parallel branches on one GPU)."""
+    import torch.distributed as dist
+    monkeypatch.setattr(dist, "is_available", lambda: True)
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_world_size", lambda group=None: 2)
+    monkeypatch.setattr(dist, "all_reduce", lambda t, *a, **k: t.mul_(2))
+
+    def gather(out, inp, *a, **k):
+        assert out.numel() == 2 * inp.numel()
+        out.view(2, -1).copy_(inp.reshape(1, -1).expand(2, -1))
+    monkeypatch.setattr(dist, "all_gather_into_tensor", gather)
+
+
+@pytest.mark.parametrize("precision", ["f16", "f32"])
+def test_data_parallel_step_matches_single_rank(precision, monkeypatch):
+    """HipTrainer's data-parallel step (touched rows and counts gathered, the sparse point-row
+    exchange, the row-sparse Adam over every rank's rows: _adam_union / set_update_rows) with two
+    ranks holding the same batch equals the one-rank step: the exchanged means are exact (x/2 + x/2),
+    so the parameters after three steps differ only by the atomic accumulation order of the point
+    gradients, bounded here by the one-rank run's own spread."""
+    pc, view, qd, mlp, gt = _setup(seed=7)
+    d = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    names = ("points_embeding", "points_color", "points_dir", "points_conf")
+    runs = {}
+    for mode in ("one", "one_again", "dp"):
+        if mode == "dp":
+            _fake_two_ranks(monkeypatch)
+        points = PointParams(pc.xyz, pc.embedding, pc.color, pc.dir, pc.conf, DEV)
+        tr = HipTrainer(points, mlp, dataclasses_replace(O), DEV, precision=precision)
+        p0 = {k: getattr(points, k).detach().clone() for k in names}
+        p0["mlp"] = tr.mlp.flat.detach().clone()
+        losses = []
+        for it in range(3):
+            torch.manual_seed(100 + it)
+            gti = torch.rand(gt.shape, generator=torch.Generator().manual_seed(it)).to(DEV)
+            parts, _, _ = tr.step(d(view.campos), d(view.camrotc2w), d(view.raydir), 0.1, 8.0, gti)
+            losses.append(float(parts["total"]))
+        tr.sync_points()
+        upd = {k: getattr(points, k).detach() - p0[k] for k in names}
+        upd["mlp"] = tr.mlp.flat.detach() - p0["mlp"]
+        runs[mode] = (losses, upd)
+        monkeypatch.undo()
+    rel = lambda x, y: {k: float(torch.linalg.vector_norm((x[k] - y[k]).double())  # noqa: E731
+                                 / torch.linalg.vector_norm(y[k].double())) for k in y}
+    spread = rel(runs["one_again"][1], runs["one"][1])
+    err = rel(runs["dp"][1], runs["one"][1])
+    print("one-rank spread", {k: f"{v:.1e}" for k, v in spread.items()})
+    print("dp vs one-rank", {k: f"{v:.1e}" for k, v in err.items()})
+    assert abs(runs["dp"][0][0] - runs["one"][0][0]) <= 1e-5 * abs(runs["one"][0][0])
+    for a, b in zip(runs["dp"][0], runs["one"][0]):
+        assert abs(a - b) <= 1e-3 * abs(b)
+    for k in err:   # every point and MLP tensor moved, by the one-rank update
+        assert float(torch.linalg.vector_norm(runs["dp"][1][k])) > 0
+        assert err[k] <= max(UPDATE_TOL if precision == "f16" else 1e-2, 3 * spread[k]), (k, err, spread)
 
 
 @pytest.mark.parametrize("rows", [0, 1, 777, 165_000])
