@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 17
+#define SGN_ABI_VERSION 18
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -403,17 +403,20 @@ int sgn_adam_step_multi(int32_t n_t, float *const *d_param, float *const *d_grad
  * or int64 on the device, or null: n = n_max), -1 and duplicate entries allowed; row0 != 0 adds row
  * 0 (the loss stage reads point 0's conf for empty slots); list 2 (optional): d_rows2[0 ..
  * min(n_max2, *d_count2)) (int64 device count), e.g. a previous launch's pend list.  d_claim (int32
- * n_rows, -1 initialised) takes each row once per launch under `tag` (unique per launch);
+ * n_rows, initialised to a value no launch uses as its tag, e.g. 0) takes each row once per launch
+ * under `tag` (unique per launch, != 0);
  * d_ws: sgn_adam_rows_workspace_bytes(min(entries, n_rows)) bytes of scratch (entries = n_max +
  * n_max2 + row0).  d_pend (optional, with d_claim2 like d_claim): sgn_adam_rows_pend_bytes(min(n_max
  * + 1, n_rows)) bytes receiving list 1's distinct valid rows and row 0 -- int64 count at [0], the
- * number of list-1 ids >= n_rows at [1] (a query / table mismatch), int32 rows from byte 16. */
+ * number of list-1 ids >= n_rows at [1] (a query / table mismatch), int32 rows from byte 16.
+ * mv_stride (host, optional): row stride in floats of d_exp_avg[t] / d_exp_avg_sq[t] (>= row_width[t];
+ * null: row_width) -- the narrow tensors' moments may share one packed [n_rows][16] buffer (ABI 18). */
 size_t sgn_adam_rows_workspace_bytes(int64_t n_entries);
 size_t sgn_adam_rows_pend_bytes(int64_t n_entries);
 int sgn_adam_rows(int32_t n_t, float *const *d_param, float *const *d_grad, float *const *d_exp_avg,
-                  float *const *d_exp_avg_sq, const int32_t *row_width, int64_t n_rows, const int32_t *d_rows,
-                  const void *d_count, int32_t count_is64, int32_t count_mul, int64_t n_max, int32_t row0,
-                  const int32_t *d_rows2, const int64_t *d_count2, int64_t n_max2, int32_t *d_last,
+                  float *const *d_exp_avg_sq, const int32_t *row_width, const int32_t *mv_stride, int64_t n_rows,
+                  const int32_t *d_rows, const void *d_count, int32_t count_is64, int32_t count_mul, int64_t n_max,
+                  int32_t row0, const int32_t *d_rows2, const int64_t *d_count2, int64_t n_max2, int32_t *d_last,
                   int32_t *d_claim, int32_t *d_claim2, int32_t tag, void *d_ws, size_t ws_bytes, void *d_pend,
                   size_t pend_bytes, float *d_sched, double lr, double beta1, double beta2, double eps, int64_t step,
                   int32_t apply, int32_t zero_grad, sgn_stream_t stream);

@@ -140,6 +140,7 @@ constexpr int kMaxRowTensors = 4;
 struct AdamRowsArgs {
     float *p[kMaxRowTensors], *g[kMaxRowTensors], *m[kMaxRowTensors], *v[kMaxRowTensors];
     int32_t w[kMaxRowTensors];     // elements per row
+    int32_t ms[kMaxRowTensors];    // row stride of exp_avg / exp_avg_sq (>= w: narrow tensors' moments packed)
     int32_t nt, wsum;              // tensors, elements per row in all
     const int32_t *rows;           // list 1 (duplicates and -1 allowed), or null: rows 0 .. n_max - 1
     const void *d_count;           // device count of list 1 (int32 or int64, times count_mul; null: n_max)
@@ -159,22 +160,29 @@ struct AdamRowsArgs {
     int32_t zero_grad;
 };
 
-// exclusive prefix sum of v over the workgroup's 256 threads and the total (LDS scratch [256])
-__device__ __forceinline__ int block_scan(int v, int *sc, int &total) {
-    const int t = threadIdx.x;
-    sc[t] = v;
-    __syncthreads();
+// exclusive prefix over the workgroup (256 threads, 4 waves, lane-major) of two per-thread bit sets'
+// popcounts, and their totals: ballots within a wave, one barrier across the four
+__device__ __forceinline__ void wg_scan2(uint32_t wm, uint32_t pm, int *sc, int &ew, int &ep, int &tw, int &tp) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t lt = (1ull << lane) - 1;
+    int xw = 0, xp = 0, sw = 0, sp = 0;
 #pragma unroll
-    for (int o = 1; o < 256; o <<= 1) {
-        const int x = t >= o ? sc[t - o] : 0;
-        __syncthreads();
-        sc[t] += x;
-        __syncthreads();
+    for (int e = 0; e < 2; ++e) {
+        const uint64_t bw = __ballot(wm >> e & 1), bp = __ballot(pm >> e & 1);
+        xw += __popcll(bw & lt), sw += __popcll(bw);
+        xp += __popcll(bp & lt), sp += __popcll(bp);
     }
-    total = sc[255];
-    const int ex = sc[t] - v;
+    if (lane == 0) sc[wv] = sw, sc[4 + wv] = sp;
     __syncthreads();
-    return ex;
+    int ow = 0, op = 0;
+    tw = tp = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int cw = sc[w], cp = sc[4 + w];
+        ow += w < wv ? cw : 0, op += w < wv ? cp : 0;
+        tw += cw, tp += cp;
+    }
+    ew = ow + xw, ep = op + xp;
 }
 
 // A workgroup takes CLAIM_PER entries (CLAIM_PER / 256 per thread): the row's first claimant records
@@ -182,7 +190,7 @@ __device__ __forceinline__ int block_scan(int v, int *sc, int &total) {
 // and list (one per wave serialised ~3.6 k atomics on each counter: 60 us)
 constexpr int CLAIM_EPT = 2, CLAIM_PER = 256 * CLAIM_EPT;
 __global__ __launch_bounds__(256) void k_rows_claim(AdamRowsArgs a) {
-    __shared__ int sc[256];
+    __shared__ int sc[8];
     __shared__ int base_s[2];
     int64_t n1 = a.n_max;
     if (a.d_count) {
@@ -219,9 +227,8 @@ __global__ __launch_bounds__(256) void k_rows_claim(AdamRowsArgs a) {
                 pm |= 1u << e;
         }
         if (a.pend && oob) atomicAdd((unsigned long long *)(a.pend + 1), (unsigned long long)oob);
-        int tw, tp;
-        const int ew = block_scan(__popc(wm), sc, tw);
-        const int ep = a.pend ? block_scan(__popc(pm), sc, tp) : 0;
+        int tw, tp, ew, ep;
+        wg_scan2(wm, pm, sc, ew, ep, tw, tp);
         if (threadIdx.x == 0) {
             base_s[0] = tw ? atomicAdd(a.ws, tw) : 0;
             base_s[1] = a.pend && tp ? (int)atomicAdd((unsigned long long *)a.pend, (unsigned long long)tp) : 0;
@@ -261,8 +268,10 @@ __global__ __launch_bounds__(256) void k_rows_update(AdamRowsArgs a) {
         while (t + 1 < a.nt && c >= a.w[t]) c -= a.w[t++];
         const int r = a.ws[4 + w];
         const int from = a.ws[4 + a.cap + w];
-        const int64_t e = (int64_t)r * a.w[t] + c;
-        float p = a.p[t][e], m = a.m[t][e], v = a.v[t][e];
+        const int64_t e = (int64_t)r * a.w[t] + c, em = (int64_t)r * a.ms[t] + c;
+        const bool app = a.apply && from < a.target;
+        float p = a.p[t][e], m = a.m[t][em], v = a.v[t][em];
+        const float g = app ? a.g[t][e] : 0.f;   // with p, m, v: one memory round trip, not two
         // two loops, so the common one reads LDS only (one loop selecting between LDS and the table
         // compiled to a flat load and a full wait per step)
         int k = from + 1;
@@ -274,14 +283,13 @@ __global__ __launch_bounds__(256) void k_rows_update(AdamRowsArgs a) {
             const float2 sc = win[k - 1 - lo];
             adam_el(p, 0.f, m, v, a.b1, a.b2, a.omb1, a.omb2, sc.x, sc.y, a.eps);
         }
-        if (a.apply && from < a.target) {
-            const float g = a.g[t][e];
+        if (app) {
             adam_el(p, g, m, v, a.b1, a.b2, a.omb1, a.omb2, a.ss_t, a.bs_t, a.eps);
             if (a.zero_grad && g != 0.f) a.g[t][e] = 0.f;
         }
         a.p[t][e] = p;
-        a.m[t][e] = m;
-        a.v[t][e] = v;
+        a.m[t][em] = m;
+        a.v[t][em] = v;
     }
 }
 
@@ -751,7 +759,8 @@ size_t sgn_adam_rows_workspace_bytes(int64_t n_entries) {
 size_t sgn_adam_rows_pend_bytes(int64_t n_entries) { return (size_t)(std::max<int64_t>(n_entries, 0) + 4) * 4; }
 
 int sgn_adam_rows(int32_t n_t, float *const *d_param, float *const *d_grad, float *const *d_exp_avg,
-                  float *const *d_exp_avg_sq, const int32_t *row_width, int64_t n_rows, const int32_t *d_rows,
+                  float *const *d_exp_avg_sq, const int32_t *row_width, const int32_t *mv_stride, int64_t n_rows,
+                  const int32_t *d_rows,
                   const void *d_count, int32_t count_is64, int32_t count_mul, int64_t n_max, int32_t row0,
                   const int32_t *d_rows2, const int64_t *d_count2, int64_t n_max2, int32_t *d_last,
                   int32_t *d_claim, int32_t *d_claim2, int32_t tag, void *d_ws, size_t ws_bytes, void *d_pend,
@@ -781,7 +790,9 @@ int sgn_adam_rows(int32_t n_t, float *const *d_param, float *const *d_grad, floa
         a.g[t] = apply ? d_grad[t] : nullptr;
         a.m[t] = d_exp_avg[t];
         a.v[t] = d_exp_avg_sq[t];
+        SGN_REQUIRE(!mv_stride || mv_stride[t] >= row_width[t], "sgn_adam_rows: mv_stride[t] >= row_width[t]");
         a.w[t] = row_width[t];
+        a.ms[t] = mv_stride ? mv_stride[t] : row_width[t];
         a.wsum += row_width[t];
     }
     a.rows = d_rows;

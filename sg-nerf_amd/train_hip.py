@@ -301,7 +301,9 @@ class PointAdam(torch.optim.Adam):
         step's own update is deferred to the next step's first launch: set_rows(list) applies the
         pending step to the previous step's rows and brings the new list's rows to the current step in
         one pass; flush() (state_dict, the model's renders; every flush_every steps, which bounds the
-        replay) brings every row."""
+        replay) brings every row.  The narrow tensors' moments (widths <= 8, e.g. colour, dir, conf: 7
+        floats a row) share one [N, 16] buffer, m in columns 0-7 and v in 8-15, and the state holds views
+        of it: a row's moments are one 64-byte access instead of six scattered 4-12 byte ones."""
         super().__init__(params, lr=lr, betas=betas, eps=eps)
         self.zero_grad_in_step = zero_grad
         self.rows_mode = rows
@@ -314,10 +316,18 @@ class PointAdam(torch.optim.Adam):
                 raise ValueError("PointAdam(rows=True): contiguous fp32 tensors sharing the first dimension")
             dev = ps[0].device
             self.n_rows = n
-            self._width = (ctypes.c_int32 * len(ps))(*[p.numel() // n for p in ps])
+            widths = [p.numel() // n for p in ps]
+            self._width = (ctypes.c_int32 * len(ps))(*widths)
+            self._narrow, off = {}, 0   # tensor index -> its columns' offset in the packed moments
+            for i, w in enumerate(widths):
+                if w <= 8 and off + w <= 8:
+                    self._narrow[i] = (off, w)
+                    off += w
+            self._mv = torch.zeros(n, 16, dtype=torch.float32, device=dev) if self._narrow else None
+            self._mstride = (ctypes.c_int32 * len(ps))(*[16 if i in self._narrow else w for i, w in enumerate(widths)])
             self._last = torch.zeros(n, dtype=torch.int32, device=dev)   # the step each row holds
-            self._claim = torch.full((n,), -1, dtype=torch.int32, device=dev)
-            self._claim2 = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            self._claim = torch.zeros(n, dtype=torch.int32, device=dev)   # claim tags (launch tags start at 1)
+            self._claim2 = torch.zeros(n, dtype=torch.int32, device=dev)
             self._sched = torch.zeros(2 * 1024, dtype=torch.float32, device=dev)
             self._ws = None
             self._pend = [None, None]   # two pend lists: the previous step's is read while the next is written
@@ -331,13 +341,21 @@ class PointAdam(torch.optim.Adam):
     # -- row-sparse mode ------------------------------------------------------------------------
     def _state_step(self):
         """The group's step count (0 before the first step); creates the state tensors."""
-        for p in self.param_groups[0]["params"]:
+        for i, p in enumerate(self.param_groups[0]["params"]):
             s = self.state[p]
             if not s:
                 s["step"] = torch.tensor(0.0)
-                s["exp_avg"] = torch.zeros_like(p)
-                s["exp_avg_sq"] = torch.zeros_like(p)
+                if i in self._narrow:
+                    s["exp_avg"], s["exp_avg_sq"] = self._mv_views(i)
+                else:
+                    s["exp_avg"] = torch.zeros_like(p)
+                    s["exp_avg_sq"] = torch.zeros_like(p)
         return int(self.state[self.param_groups[0]["params"][0]]["step"].item())
+
+    def _mv_views(self, i):
+        """Tensor i's exp_avg / exp_avg_sq as views of the packed narrow moments (zero at creation)."""
+        o, w = self._narrow[i]
+        return self._mv[:, o:o + w], self._mv[:, 8 + o:8 + o + w]
 
     def _buf(self, t, nbytes):
         if t is None or t.numel() < nbytes:
@@ -372,7 +390,7 @@ class PointAdam(torch.optim.Adam):
                                                   int(L.sgn_adam_rows_pend_bytes(min(n_max + 1, self.n_rows))))
         _lib.check(L.sgn_adam_rows(
             n, arr(ps), arr([p.grad if apply else None for p in ps]), arr([self.state[p]["exp_avg"] for p in ps]),
-            arr([self.state[p]["exp_avg_sq"] for p in ps]), self._width, self.n_rows,
+            arr([self.state[p]["exp_avg_sq"] for p in ps]), self._width, self._mstride, self.n_rows,
             _lib.ptr(rows) if rows is not None else None, _lib.ptr(count) if count is not None else None,
             int(count_is64), count_mul, n_max, 1,
             prev[0].data_ptr() + 16 if prev is not None else None, prev[0].data_ptr() if prev is not None else None,
@@ -431,6 +449,12 @@ class PointAdam(torch.optim.Adam):
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         if self.rows_mode:   # the loaded tensors are a dense state: every row holds its step
+            for i, p in enumerate(self.param_groups[0]["params"]):
+                s = self.state[p]
+                if i in self._narrow and s:   # back into the packed moments
+                    for key, view in zip(("exp_avg", "exp_avg_sq"), self._mv_views(i)):
+                        view.copy_(s[key].reshape(view.shape))
+                        s[key] = view
             t = self._state_step()
             self._last.fill_(t)
             self._flushed = t

@@ -514,6 +514,21 @@ def test_row_sparse_adam_matches_dense_bit_for_bit(n_rows, steps, flush_every, d
         for k in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(od.state[x][k], orow.state[y][k])
     assert all(float(v["step"]) == steps for v in sd["state"].values())
+    # a fresh optimizer loads the state (the narrow tensors' moments back into its packed buffer) and
+    # steps on as the dense one does
+    o2 = PointAdam(b, lr=2e-3, rows=True, flush_every=flush_every)
+    o2.load_state_dict(sd)
+    assert o2._mv is not None and o2.state[b[1]]["exp_avg"].data_ptr() == o2._mv.data_ptr() + 4 * o2._narrow[1][0]
+    for x, y, w in zip(a, b, widths):
+        gr = torch.randn(n_rows, w, generator=g)
+        x.grad = gr.to(DEV)
+        y.grad = gr.to(DEV)
+    od.step()
+    o2.step()                                                        # no row list: every row at once
+    for x, y in zip(a, b):
+        assert torch.equal(x.detach(), y.detach())
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(od.state[x][k], o2.state[y][k])
 
 
 def _fake_two_ranks(monkeypatch):
