@@ -8,8 +8,9 @@ and all their gradients -- runs as hand-written HIP launches; torch only allocat
 all-reduces gradients.  Two arithmetic modes, as the renderer has:
 
 precision "f32" (the reference's fp32 arithmetic; `_backward_f32`, train_f32.F32Step):
-  query        sgn_query (jittered depths, is_train) -> sgn_touched_points (the step's points)
-  projection   sgn_point_project_f32_subset: block1.0's per-point part for the touched points only
+  query        sgn_query (jittered depths, is_train) -> the point Adam's launch (sgn_adam_rows: the
+               previous step's deferred update, this step's rows brought forward, their distinct list)
+  projection   sgn_point_project_f32_subset: block1.0's per-point part for that list's points only
   forward      k_rows16 in save mode (block1.0 / 1.2 / 3.0 pre-activations per row; SG: + block2_bpnet)
   colour+loss  the colour MLP on k_x3rows (3 fp16 products per fp32 product), sgn_loss_train
   backward     k_row_head / masked backward-data GEMMs / k_row_tail (point gradients), the split-K
@@ -17,7 +18,8 @@ precision "f32" (the reference's fp32 arithmetic; `_backward_f32`, train_f32.F32
   no host synchronisation on one GPU.
 
 precision "f16" (fp16-operand MFMA, fp32 accumulation; `backward`):
-  query        sgn_query, then the step's one host sync (sample / work-item counts)
+  query        sgn_query -> the point Adam's launch, then the step's one host sync (sample /
+               work-item counts, read after an event on the query's pinned copy)
   forward      sgn_aggregate_train_fwd (k_agg_rows save mode): f_s (fp16) and alpha per sample,
                the row layers' inputs saved
   colour+loss  one captured HIP graph (ColourStep: sgn_colour_inputs, the colour MLP on k_x3rows,
@@ -30,8 +32,9 @@ precision "f16" (fp16-operand MFMA, fp32 accumulation; `backward`):
                sums, all added into the flat gradient by one sgn_grad_accumulate
 
 Both: bucketed all-reduce (RCCL) of the flat MLP gradient and a sparse all-gather of the touched
-point rows under DP, then two Adam groups (lr 5e-4 / plr 2e-3, iter_exponential_decay) on
-sgn_adam_step_multi.  The plane background model's per-ray colour (inputs['bg_ray']) enters the
+point rows under DP, then two Adam groups (lr 5e-4 / plr 2e-3, iter_exponential_decay): the MLP's
+on sgn_adam_step_multi, the points' on the row-sparse exact sgn_adam_rows (PointAdam(rows=True):
+bit-identical to the dense update, applied at the next step's launch or at a flush).  The plane background model's per-ray colour (inputs['bg_ray']) enters the
 loss stage as T_bg * bg_ray.
 
 MLP weights live in ONE flat fp32 parameter (LAYERS order), so the MFMA blobs are re-packed on
