@@ -411,12 +411,14 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
     g2.close()
     res["grid_rebuild_ms"] = {"hip_events": e0.elapsed_time(e1), "wall": (time.perf_counter() - t1) * 1e3}
     # occupancy / algorithmic work of the timed frames (deterministic re-render, untimed)
-    n_nb, n_smp, n_samples, q_bytes = [], [], [], []
+    n_nb, n_smp, n_samples, q_bytes, n_proj = [], [], [], [], []
     for i in range(warmup, n_frames):
         out = frame(i, count=True)
         drain()
         q = out.query
         S = q.n_samples()
+        pp = r.points_projected()   # the f32 mode projects the frame's points only (sgn_frame_points)
+        n_proj.append(pp[0] if pp is not None else r.points.n)
         cnt = [c & 0xFFFFFFFF for c in q.counters.tolist()]  # [3] is uint32
         W = cnt[1]
         n_samples.append(S)
@@ -428,7 +430,7 @@ def render_run(args, precision, world, rank, dev, dist, steps, warmup, lego, wan
                        + 4 * W)
     torch.cuda.synchronize()
     res.update(n_nb=float(np.mean(n_nb)), n_smp=float(np.mean(n_smp)), n_samples=float(np.mean(n_samples)),
-               q_bytes=float(np.mean(q_bytes)))
+               q_bytes=float(np.mean(q_bytes)), n_proj=float(np.mean(n_proj)))
     return res
 
 
@@ -580,9 +582,11 @@ def main():
             "counter": _query_counter(stage_ms["query"], f"{args.h}x{args.w}x{args.sr}"),
         },
         "roofline_proj": {
-            "kernel": ("k_point_proj16" if x3 else "k_point_proj") + " (block1.0 point inputs, all points, once per frame)",
-            "bound": "mfma", "achieved": FLOP_PER_POINT_PROJ * args.points / (stage_ms["proj"] * 1e-3) / 1e12,
-            "peak": peak, "unit": "TFLOP/s", "avg_launch_ms": stage_ms["proj"],
+            "kernel": ("k_point_proj16 (block1.0 point inputs of the points the frame's samples name, "
+                       "sgn_frame_points + subset projection, once per frame)" if x3 else
+                       "k_point_proj (block1.0 point inputs, all points, once per frame)"),
+            "bound": "mfma", "achieved": FLOP_PER_POINT_PROJ * h["n_proj"] / (stage_ms["proj"] * 1e-3) / 1e12,
+            "peak": peak, "unit": "TFLOP/s", "avg_launch_ms": stage_ms["proj"], "points_projected": h["n_proj"],
         },
         "stages_ms": stage_ms,
         "grid_build_ms": h["grid_build_ms"],

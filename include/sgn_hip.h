@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 18
+#define SGN_ABI_VERSION 19
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -519,6 +519,17 @@ int sgn_pow2_scale(const float *d_a, int64_t na, const float *d_b, int64_t nb, v
  * the neighbours come from the reference's query (neural_points.py:942-988). */
 int sgn_touched_points(const int32_t *d_pidx, const int32_t *d_counters, int64_t s_cap, int32_t K, int64_t n_points,
                        int32_t step, int32_t *d_stamp, int32_t *d_idx, int64_t *d_count2, sgn_stream_t stream);
+
+/* The distinct points a render frame's samples name (ABI 19), for sgn_point_project_f32_subset: the
+ * block1.0 projection then runs over those points only (~19 % of the 1.2 M points of a config-2
+ * frame) instead of all of them.  Point 0 and every neighbour d_pidx[e] >= 0, e < min(d_counters[0]
+ * * K, s_cap * K), go to d_idx (int32 [n_points], no particular order) with their count at
+ * d_count[0] (int64, device); d_count[1] accumulates neighbour indices >= n_points (a query / table
+ * mismatch: never projected; the caller zeroes it once).  d_mark: sgn_frame_points_mark_bytes(
+ * n_points) bytes, zero at allocation and left zero by every call.  d_pidx 16-B aligned. */
+size_t sgn_frame_points_mark_bytes(int64_t n_points);
+int sgn_frame_points(const int32_t *d_pidx, const int32_t *d_counters, int64_t s_cap, int32_t K, int64_t n_points,
+                     uint8_t *d_mark, int32_t *d_idx, int64_t *d_count, sgn_stream_t stream);
 
 /* ---- fp32 training step on hand-written kernels (ABI 9; SG entries ABI 10) -----------------------------------
  * The reference's fp32 autograd through PointAggregator / viewmlp and the NeuralPoints gather

@@ -703,6 +703,78 @@ __global__ void __launch_bounds__(256) k_touched_points(const int32_t *__restric
     }
 }
 
+// The distinct points a render frame's samples name (sgn_frame_points): a frame's ~28 M neighbour
+// slots name ~0.2 M points ~100 times each, so they are byte marks by plain stores (idempotent, no
+// atomics, no read before the store), then one thread per 4-byte word of marks compacts and clears them.
+__device__ __forceinline__ void mark_point(int32_t p, int64_t n_points, uint8_t *mark, unsigned &bad) {
+    if (p >= 0 && p < n_points) mark[p] = 1;
+    else if (p >= n_points) ++bad;
+}
+
+__global__ void __launch_bounds__(256) k_mark_points(const int32_t *__restrict__ pidx,
+                                                     const int32_t *__restrict__ counters, int64_t cap_slots,
+                                                     int32_t K, int64_t n_points, uint8_t *mark,
+                                                     unsigned long long *cnt) {
+    int64_t n = (int64_t)counters[0] * K;
+    n = n < cap_slots ? n : cap_slots;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        mark[0] = 1;   // point 0, as sgn_touched_points has it
+        cnt[0] = 0;    // the compaction's counter (it runs after this kernel on the stream)
+    }
+    unsigned bad = 0;
+    const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+    const int4 *p4 = reinterpret_cast<const int4 *>(pidx);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const int4 v = p4[i];
+        mark_point(v.x, n_points, mark, bad);
+        mark_point(v.y, n_points, mark, bad);
+        mark_point(v.z, n_points, mark, bad);
+        mark_point(v.w, n_points, mark, bad);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) mark_point(pidx[4 * n4 + threadIdx.x], n_points, mark, bad);
+    if (bad) atomicAdd(cnt + 1, (unsigned long long)bad);
+}
+
+__global__ void __launch_bounds__(256) k_compact_points(uint8_t *mark, int64_t n_points, int32_t *__restrict__ idx,
+                                                        unsigned long long *cnt) {
+    __shared__ int sc[4];
+    __shared__ int base_s;
+    const int64_t nw = (n_points + 3) >> 2;
+    uint32_t *mw = reinterpret_cast<uint32_t *>(mark);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int64_t w0 = (int64_t)blockIdx.x * blockDim.x; w0 < nw; w0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t w = w0 + threadIdx.x;
+        uint32_t m = w < nw ? mw[w] : 0u;
+        if (m) mw[w] = 0u;
+        const uint32_t bits = (uint32_t)((m & 0xffu) != 0) | (uint32_t)((m & 0xff00u) != 0) << 1 |
+                              (uint32_t)((m & 0xff0000u) != 0) << 2 | (uint32_t)((m & 0xff000000u) != 0) << 3;
+        const int c = __popc(bits);
+        int x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) sc[wv] = x;
+        __syncthreads();
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            off += k < wv ? sc[k] : 0;
+            tot += sc[k];
+        }
+        if (threadIdx.x == 0) base_s = tot ? (int)atomicAdd(cnt, (unsigned long long)tot) : 0;
+        __syncthreads();
+        int pos = base_s + off + x - c;
+        __syncthreads();
+        uint32_t b = bits;
+        while (b) {
+            idx[pos++] = (int32_t)(4 * w + __ffs(b) - 1);
+            b &= b - 1;
+        }
+    }
+}
+
 }  // namespace
 }  // namespace sgn
 
@@ -1063,6 +1135,30 @@ int sgn_touched_points(const int32_t *d_pidx, const int32_t *d_counters, int64_t
     auto *c = reinterpret_cast<unsigned long long *>(d_count2);
     hipLaunchKernelGGL(k_touched_points, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), d_pidx, d_counters,
                        s_cap * K, K, n_points, step, d_stamp, d_idx, c + (step & 1), c + ((step + 1) & 1), c + 2);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+size_t sgn_frame_points_mark_bytes(int64_t n_points) {
+    return (size_t)((std::max<int64_t>(n_points, 1) + 15) / 16 * 16);
+}
+
+int sgn_frame_points(const int32_t *d_pidx, const int32_t *d_counters, int64_t s_cap, int32_t K, int64_t n_points,
+                     uint8_t *d_mark, int32_t *d_idx, int64_t *d_count, sgn_stream_t stream) {
+    SGN_REQUIRE(s_cap >= 0 && K >= 1 && n_points >= 1 && n_points < (1ll << 31), "sgn_frame_points: bad size");
+    SGN_REQUIRE(d_pidx && d_counters && d_mark && d_idx && d_count, "sgn_frame_points: null buffer");
+    SGN_REQUIRE(!(reinterpret_cast<uintptr_t>(d_pidx) & 15) && !(reinterpret_cast<uintptr_t>(d_mark) & 3),
+                "sgn_frame_points: d_pidx 16-B and d_mark 4-B aligned");
+    const int64_t slots4 = (s_cap * K + 3) / 4;
+    const int64_t mblocks = std::max<int64_t>(1, std::min<int64_t>((slots4 + 255) / 256, 256 * 16));
+    auto *c = reinterpret_cast<unsigned long long *>(d_count);
+    hipLaunchKernelGGL(k_mark_points, dim3((unsigned)mblocks), dim3(256), 0, as_stream(stream), d_pidx, d_counters,
+                       s_cap * K, K, n_points, d_mark, c);
+    SGN_CHECK_HIP(hipGetLastError());
+    const int64_t nw = (n_points + 3) / 4;
+    const int64_t kblocks = std::max<int64_t>(1, std::min<int64_t>((nw + 255) / 256, 256 * 4));
+    hipLaunchKernelGGL(k_compact_points, dim3((unsigned)kblocks), dim3(256), 0, as_stream(stream), d_mark, n_points,
+                       d_idx, c);
     SGN_CHECK_HIP(hipGetLastError());
     return 0;
 }

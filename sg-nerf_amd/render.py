@@ -72,6 +72,7 @@ class HipRenderer:
         self.set_mlp(mlp_state)
         self._cap = None
         self._proj = None
+        self._fp = None        # sgn_frame_points buffers (marks, list, counts) for the projection subset
         self._pending = []   # deferred fp16-range checks: (pinned flag copy, event)
         self._flag_host = None
 
@@ -204,14 +205,24 @@ class HipRenderer:
                                              _lib.ptr(self.wnorm) if want_weights else None, _lib.ptr(self.agg_ws),
                                              self.agg_ws.numel(), _lib.stream_handle()), "sgn_aggregate_exact")
 
-        # split block1.0: P[point] = W0a [feat | PE(feat)] + b0 for every point, once per frame
+        # split block1.0: P[point] = W0a [feat | PE(feat)] + b0, once per frame; the f32 mode projects
+        # only the points the frame's samples name (sgn_frame_points: ~19 % of a config-2 frame's)
         mark("proj")
         nproj = int(L.sgn_point_proj_bytes_f32(self.points.n) if self.f32 else L.sgn_point_proj_bytes(self.points.n))
         if self._proj is None or self._proj.numel() < nproj:
             self._proj = torch.empty(max(nproj, 16), dtype=torch.uint8, device=self.device)
         if self.f32 and not self.exact:
-            _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
-                       "sgn_point_project_f32")
+            n = self.points.n
+            if self._fp is None or self._fp[0] != n:
+                self._fp = (n, torch.zeros(int(L.sgn_frame_points_mark_bytes(n)), dtype=torch.uint8, device=self.device),
+                            torch.empty(n, dtype=torch.int32, device=self.device),
+                            torch.zeros(2, dtype=torch.int64, device=self.device))
+            _, marks, plist, pcount = self._fp
+            _lib.check(L.sgn_frame_points(_lib.ptr(q.pidx), _lib.ptr(q.counters), q.pidx.numel() // o.K, o.K, n,
+                                          _lib.ptr(marks), _lib.ptr(plist), _lib.ptr(pcount), st), "sgn_frame_points")
+            _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(plist),
+                                                      _lib.ptr(pcount), _lib.ptr(self._proj), st),
+                       "sgn_point_project_f32_subset")
         elif not self.f32:
             _lib.check(L.sgn_point_project(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
                        "sgn_point_project")
@@ -250,6 +261,14 @@ class HipRenderer:
         self._range_check(check_range, lambda: (aggregate_exact(), composite()))
         return RenderOut(self.rgb[:R], self.mask[:R], self.bgT[:R], self.opacity[:R], q, self.feat, self.blend,
                          self.wnorm if want_weights else None, self.blendw[:R] if want_weights else None)
+
+    def points_projected(self):
+        """The last f32 frame's projected point count and the neighbour indices >= n_points met so far
+        (host sync), or None before any f32 frame."""
+        if self._fp is None:
+            return None
+        c, bad = (int(x) for x in self._fp[3].tolist())
+        return c, bad
 
     def grid_info(self):
         return self.querier.grid_for(self.points.xyz).info()

@@ -643,3 +643,36 @@ def test_f32_fp16_range_falls_back_to_plain_fp32():
     print(f"x30000 block1.2, PointAggregator: max feature error {aerr:.3e}")
     assert aerr <= max(F32_TOL, 4.0 * floor)
 
+
+
+@pytest.mark.parametrize("n_points,S,K", [(1_200_000, 300_000, 8), (5, 3, 1), (1_001, 7, 3)])
+def test_frame_points_lists_the_named_points(n_points, S, K):
+    """sgn_frame_points (the f32 renderer's projection subset): point 0 and every neighbour slot >= 0 of
+    the first S samples, once each (slots past S * K ignored, ids >= n_points counted, not listed);
+    the marks are left zero, so a second frame on the same buffers lists its own points only."""
+    import ctypes
+    from sgnerf_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(n_points + S)
+    marks = torch.zeros(int(L.sgn_frame_points_mark_bytes(n_points)), dtype=torch.uint8, device=DEV)
+    lst = torch.empty(n_points, dtype=torch.int32, device=DEV)
+    cnt = torch.zeros(2, dtype=torch.int64, device=DEV)
+    for frame in range(2):
+        pidx = torch.randint(-1, min(n_points, 50_000 * (frame + 1)), ((S + 9) * K,), generator=g, dtype=torch.int32)
+        pidx[S * K:] = n_points - 1                       # past the sample count: never read
+        if n_points > 10:
+            pidx[5] = n_points + 3                        # a query / table mismatch: counted only
+        counters = torch.tensor([S, 0, 0, 0], dtype=torch.int32)
+        pidx_d, counters_d = pidx.to(DEV), counters.to(DEV)   # alive until the launch has run
+        _lib.check(L.sgn_frame_points(_lib.ptr(pidx_d), _lib.ptr(counters_d), S + 9, K, n_points,
+                                      _lib.ptr(marks), _lib.ptr(lst), _lib.ptr(cnt), _lib.stream_handle()),
+                   "sgn_frame_points")
+        torch.cuda.synchronize()
+        used = pidx[:S * K]
+        used = used[(used >= 0) & (used < n_points)].long()
+        want = torch.unique(torch.cat([used, torch.zeros(1, dtype=torch.long)]))
+        n = int(cnt[0].item())
+        assert n == want.numel()
+        assert torch.equal(torch.sort(lst[:n].long().cpu()).values, want)
+        assert int(cnt[1].item()) == (frame + 1 if n_points > 10 else 0)
+        assert int(marks.count_nonzero().item()) == 0
