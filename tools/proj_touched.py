@@ -1,7 +1,7 @@
 """Timing probe (not product): config-2 frames (tools/agg_time.py's setup, f32); for each frame the
 fraction of the 1.2 M points its samples touch, and HIP-event times of the full block1.0 point
-projection (sgn_point_project_f32) against the touched list (sgn_touched_points) + the subset
-projection (sgn_point_project_f32_subset).   python tools/proj_touched.py [frames]"""
+projection (sgn_point_project_f32) against the frame's point list (sgn_frame_points, the renderer's
+path) + the subset projection (sgn_point_project_f32_subset).   python tools/proj_touched.py [frames]"""
 import ctypes
 import json
 import os
@@ -26,9 +26,9 @@ mlp["alpha_branch.0.bias"] = mlp["alpha_branch.0.bias"] + 50.0
 r = HipRenderer(PointTables.from_cloud(pc, dev), mlp, HotPathOpts(SR=64, precision="f32"), dev)
 L = _lib.lib()
 N = r.points.n
-stamp = torch.full((N,), -1, dtype=torch.int32, device=dev)
+marks = torch.zeros(int(L.sgn_frame_points_mark_bytes(N)), dtype=torch.uint8, device=dev)
 idx = torch.empty(N, dtype=torch.int32, device=dev)
-cnt = torch.zeros(3, dtype=torch.int64, device=dev)
+cnt = torch.zeros(2, dtype=torch.int64, device=dev)
 out = []
 for i in range(2 + nf):
     yaw, pitch = scene.spiral_yaw_pitch(i % 120, 120)
@@ -50,16 +50,14 @@ for i in range(2 + nf):
     e[0].record()
     _lib.check(L.sgn_point_project_f32(ctypes.byref(pt), _lib.ptr(r.packed), _lib.ptr(r._proj), st), "full")
     e[1].record()
-    _lib.check(L.sgn_touched_points(_lib.ptr(q.pidx), _lib.ptr(q.counters), q.pidx.numel() // 8, 8, N, i,
-                                    _lib.ptr(stamp), _lib.ptr(idx), _lib.ptr(cnt), st), "touched")
+    _lib.check(L.sgn_frame_points(_lib.ptr(q.pidx), _lib.ptr(q.counters), q.pidx.numel() // 8, 8, N,
+                                  _lib.ptr(marks), _lib.ptr(idx), _lib.ptr(cnt), st), "frame points")
     e[2].record()
     _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(r.packed), _lib.ptr(idx),
-                                              _lib.ptr(cnt[i & 1:]), _lib.ptr(r._proj), st), "subset")
+                                              _lib.ptr(cnt), _lib.ptr(r._proj), st), "subset")
     e[3].record()
     torch.cuda.synchronize()
     if i >= 2:
-        out.append({"touched_frac": frac, "full_ms": e[0].elapsed_time(e[1]), "touched_ms": e[1].elapsed_time(e[2]),
-                    "subset_ms": e[2].elapsed_time(e[3]), "list_n": int(cnt[i & 1].item())})
-for o in out:
-    print(json.dumps(o))
-print(json.dumps({k: float(np.median([o[k] for o in out])) for k in out[0]}))
+        out.append({"touched_frac": frac, "full_ms": e[0].elapsed_time(e[1]), "list_ms": e[1].elapsed_time(e[2]),
+                    "subset_ms": e[2].elapsed_time(e[3]), "list_n": int(cnt[0].item())})
+print(json.dumps({"lib": os.path.basename(os.environ.get("SGN_HIP_LIB", "intree")), **{k: float(np.median([o[k] for o in out])) for k in out[0]}}))
