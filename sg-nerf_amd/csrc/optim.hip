@@ -735,6 +735,39 @@ __global__ void __launch_bounds__(256) k_mark_points(const int32_t *__restrict__
     if (bad) atomicAdd(cnt + 1, (unsigned long long)bad);
 }
 
+// K = 8 (the configs' neighbour count): one thread per sample, whose slots are stored unless the
+// previous sample (the thread before it) holds the same point -- consecutive samples along a ray share
+// most of their neighbours, and a point that sample holds is marked by that thread.
+__global__ void __launch_bounds__(256) k_mark_points8(const int32_t *__restrict__ pidx,
+                                                      const int32_t *__restrict__ counters, int64_t cap_samples,
+                                                      int64_t n_points, uint8_t *mark, unsigned long long *cnt) {
+    int64_t S = counters[0];
+    S = S < cap_samples ? S : cap_samples;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        mark[0] = 1;
+        cnt[0] = 0;
+    }
+    unsigned bad = 0;
+    const int4 *p4 = reinterpret_cast<const int4 *>(pidx);
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += (int64_t)gridDim.x * blockDim.x) {
+        const int4 a = p4[2 * s], b = p4[2 * s + 1];
+        int4 pa = make_int4(-1, -1, -1, -1), pb = pa;
+        if (s > 0) pa = p4[2 * s - 2], pb = p4[2 * s - 1];
+        const int cur[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        const int prv[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int p = cur[k];
+            bool dup = false;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dup |= p == prv[j];
+            if (p >= n_points) ++bad;
+            else if (p >= 0 && !dup) mark[p] = 1;
+        }
+    }
+    if (bad) atomicAdd(cnt + 1, (unsigned long long)bad);
+}
+
 __global__ void __launch_bounds__(256) k_compact_points(uint8_t *mark, int64_t n_points, int32_t *__restrict__ idx,
                                                         unsigned long long *cnt) {
     __shared__ int sc[4];
@@ -1150,10 +1183,16 @@ int sgn_frame_points(const int32_t *d_pidx, const int32_t *d_counters, int64_t s
     SGN_REQUIRE(!(reinterpret_cast<uintptr_t>(d_pidx) & 15) && !(reinterpret_cast<uintptr_t>(d_mark) & 3),
                 "sgn_frame_points: d_pidx 16-B and d_mark 4-B aligned");
     const int64_t slots4 = (s_cap * K + 3) / 4;
-    const int64_t mblocks = std::max<int64_t>(1, std::min<int64_t>((slots4 + 255) / 256, 256 * 16));
     auto *c = reinterpret_cast<unsigned long long *>(d_count);
-    hipLaunchKernelGGL(k_mark_points, dim3((unsigned)mblocks), dim3(256), 0, as_stream(stream), d_pidx, d_counters,
-                       s_cap * K, K, n_points, d_mark, c);
+    if (K == 8) {
+        const int64_t mblocks = std::max<int64_t>(1, std::min<int64_t>((s_cap + 255) / 256, 256 * 16));
+        hipLaunchKernelGGL(k_mark_points8, dim3((unsigned)mblocks), dim3(256), 0, as_stream(stream), d_pidx, d_counters,
+                           s_cap, n_points, d_mark, c);
+    } else {
+        const int64_t mblocks = std::max<int64_t>(1, std::min<int64_t>((slots4 + 255) / 256, 256 * 16));
+        hipLaunchKernelGGL(k_mark_points, dim3((unsigned)mblocks), dim3(256), 0, as_stream(stream), d_pidx,
+                           d_counters, s_cap * K, K, n_points, d_mark, c);
+    }
     SGN_CHECK_HIP(hipGetLastError());
     const int64_t nw = (n_points + 3) / 4;
     const int64_t kblocks = std::max<int64_t>(1, std::min<int64_t>((nw + 255) / 256, 256 * 4));
