@@ -582,9 +582,9 @@ def main():
             "counter": _query_counter(stage_ms["query"], f"{args.h}x{args.w}x{args.sr}"),
         },
         "roofline_proj": {
-            "kernel": ("k_point_proj16 (block1.0 point inputs of the points the frame's samples name, "
-                       "sgn_frame_points + subset projection, once per frame)" if x3 else
-                       "k_point_proj (block1.0 point inputs, all points, once per frame)"),
+            "kernel": ("k_point_proj16" if x3 else "k_point_proj") + (
+                " (block1.0 point inputs of the points the frame's samples name, sgn_frame_points + subset "
+                "projection, once per frame)"),
             "bound": "mfma", "achieved": FLOP_PER_POINT_PROJ * h["n_proj"] / (stage_ms["proj"] * 1e-3) / 1e12,
             "peak": peak, "unit": "TFLOP/s", "avg_launch_ms": stage_ms["proj"], "points_projected": h["n_proj"],
         },

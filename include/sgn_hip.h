@@ -41,7 +41,7 @@ extern "C" {
 typedef void *sgn_stream_t; /* hipStream_t (torch.cuda.current_stream().cuda_stream) */
 typedef struct sgn_grid sgn_grid; /* opaque, device-resident voxel grid of one point cloud */
 
-#define SGN_ABI_VERSION 19
+#define SGN_ABI_VERSION 20
 
 /* ---- grid ------------------------------------------------------------- */
 
@@ -175,6 +175,11 @@ int sgn_aggregate(const sgn_point_tables *pt, const sgn_query_out *q, int64_t S_
 size_t sgn_point_proj_bytes(int64_t n_points);
 int sgn_point_project(const sgn_point_tables *pt, const void *d_packed_mlp, void *d_proj,
                       sgn_stream_t stream);
+/* sgn_point_project for the points d_idx[0 .. *d_count) only (ABI 20; int32 indices < n_points, int64
+ * device count, e.g. sgn_frame_points' list): the f16 renderer projects the points a frame's
+ * samples name.  The other points' P rows are left as they are. */
+int sgn_point_project_subset(const sgn_point_tables *pt, const void *d_packed, const int32_t *d_idx,
+                             const int64_t *d_count, void *d_proj, sgn_stream_t stream);
 /* Byte offsets inside the packed blob: 0 = fp32 section, 1 = split block1.0 sections,
  * 2 = end of the base blob (sgn_mlp_packed_bytes). */
 size_t sgn_mlp_section(int32_t which);

@@ -12,7 +12,7 @@ import torch  # noqa: F401  -- loads torch's libamdhip64 first so the .so binds 
 
 # SGN_HIP_LIB: another build of the same ABI (same-box A/B of kernel variants, tools/ab_lib.sh)
 LIB_PATH = os.environ.get("SGN_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsgn_hip.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 COLSUM_SLABS = 512   # SGN_COLSUM_SLABS
 
 c_i32, c_i64, c_u64, c_f32, c_vp, c_sz = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
@@ -151,6 +151,7 @@ SIGNATURES = {
                               c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_sz, c_vp, c_sz, c_vp,
                               ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_i32, c_i32,
                               c_vp]),
+    "sgn_point_project_subset": (c_i32, [ctypes.POINTER(PointTables), c_vp, c_vp, c_vp, c_vp, c_vp]),
     "sgn_frame_points_mark_bytes": (c_sz, [c_i64]),
     "sgn_frame_points": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "sgn_colsum_workspace_bytes": (c_sz, [c_i32]),

@@ -697,6 +697,8 @@ struct ProjArgs {
     int64_t n;
     const void *blob;
     _Float16 *proj;
+    const int32_t *idx = nullptr;    // subset: the points idx[0 .. *count) only
+    const int64_t *count = nullptr;
 };
 
 __global__ __launch_bounds__(PROJ_TPB, 1) void k_point_proj(ProjArgs a) {
@@ -717,14 +719,16 @@ __global__ __launch_bounds__(PROJ_TPB, 1) void k_point_proj(ProjArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int64_t nt = (a.n + 31) / 32;
+    const int64_t n = a.idx ? (*a.count < a.n ? *a.count : a.n) : a.n;
+    const int64_t nt = (n + 31) / 32;
     for (int64_t tile = (int64_t)blockIdx.x * (PROJ_TPB / 64) + w; tile < nt; tile += (int64_t)gridDim.x * (PROJ_TPB / 64)) {
         int lz = 0;
         asm volatile("" : "+s"(lz));
         const char *W = lds + lz;
         const float *B = (const float *)(lds + lz + PROJ_FRAGS * (int)FRAG);
-        const int64_t p = tile * 32 + (lane & 31);
-        const bool ok = p < a.n;
+        const int64_t q = tile * 32 + (lane & 31);
+        const bool ok = q < n;
+        const int64_t p = a.idx ? (ok ? (int64_t)a.idx[q] : 0) : q;
         float feat[16], dist[3] = {0.f, 0.f, 0.f};
         {
             const f32x4 *e4 = (const f32x4 *)(a.emb + (ok ? p : 0) * 32 + 16 * h);
@@ -856,6 +860,22 @@ size_t sgn_mlp_section(int32_t which) {
 }
 
 size_t sgn_point_proj_bytes(int64_t n_points) { return (size_t)(n_points > 0 ? n_points : 0) * sgn::mlp::PROJ_BYTES_PER_POINT; }
+
+int sgn_point_project_subset(const sgn_point_tables *pt, const void *d_packed, const int32_t *d_idx,
+                             const int64_t *d_count, void *d_proj, sgn_stream_t stream) {
+    using namespace sgn;
+    using namespace sgn::mlp;
+    SGN_REQUIRE(pt && d_packed && d_proj && d_idx && d_count, "null argument");
+    SGN_REQUIRE(pt->n_points >= 0 && (pt->n_points == 0 || pt->embedding), "embedding required");
+    if (pt->n_points == 0) return 0;
+    ProjArgs a{pt->embedding, pt->n_points, d_packed, (_Float16 *)d_proj, d_idx, d_count};
+    // persistent grid over the device count (a frame names ~19 % of the points)
+    const int64_t waves = (pt->n_points + 31) / 32;
+    const int64_t wg = (waves + PROJ_TPB / 64 - 1) / (PROJ_TPB / 64);
+    hipLaunchKernelGGL(k_point_proj, dim3((unsigned)(wg < 256 ? wg : 256)), dim3(PROJ_TPB), 0, as_stream(stream), a);
+    SGN_CHECK_HIP(hipGetLastError());
+    return 0;
+}
 
 int sgn_point_project(const sgn_point_tables *pt, const void *d_packed, void *d_proj, sgn_stream_t stream) {
     using namespace sgn;

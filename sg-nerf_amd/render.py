@@ -205,13 +205,13 @@ class HipRenderer:
                                              _lib.ptr(self.wnorm) if want_weights else None, _lib.ptr(self.agg_ws),
                                              self.agg_ws.numel(), _lib.stream_handle()), "sgn_aggregate_exact")
 
-        # split block1.0: P[point] = W0a [feat | PE(feat)] + b0, once per frame; the f32 mode projects
-        # only the points the frame's samples name (sgn_frame_points: ~19 % of a config-2 frame's)
+        # split block1.0: P[point] = W0a [feat | PE(feat)] + b0, once per frame, for the points the
+        # frame's samples name only (sgn_frame_points: ~19 % of a config-2 frame's)
         mark("proj")
         nproj = int(L.sgn_point_proj_bytes_f32(self.points.n) if self.f32 else L.sgn_point_proj_bytes(self.points.n))
         if self._proj is None or self._proj.numel() < nproj:
             self._proj = torch.empty(max(nproj, 16), dtype=torch.uint8, device=self.device)
-        if self.f32 and not self.exact:
+        if not self.exact:
             n = self.points.n
             if self._fp is None or self._fp[0] != n:
                 self._fp = (n, torch.zeros(int(L.sgn_frame_points_mark_bytes(n)), dtype=torch.uint8, device=self.device),
@@ -220,12 +220,9 @@ class HipRenderer:
             _, marks, plist, pcount = self._fp
             _lib.check(L.sgn_frame_points(_lib.ptr(q.pidx), _lib.ptr(q.counters), q.pidx.numel() // o.K, o.K, n,
                                           _lib.ptr(marks), _lib.ptr(plist), _lib.ptr(pcount), st), "sgn_frame_points")
-            _lib.check(L.sgn_point_project_f32_subset(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(plist),
-                                                      _lib.ptr(pcount), _lib.ptr(self._proj), st),
-                       "sgn_point_project_f32_subset")
-        elif not self.f32:
-            _lib.check(L.sgn_point_project(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(self._proj), st),
-                       "sgn_point_project")
+            project = L.sgn_point_project_f32_subset if self.f32 else L.sgn_point_project_subset
+            _lib.check(project(ctypes.byref(pt), _lib.ptr(self.packed), _lib.ptr(plist), _lib.ptr(pcount),
+                               _lib.ptr(self._proj), st), "point projection (subset)")
         for stage, name in ((1, "agg_rows"), (2, "agg_color")):
             mark(name)
             blend = _lib.ptr(self.blend) if want_blend else None
@@ -263,8 +260,8 @@ class HipRenderer:
                          self.wnorm if want_weights else None, self.blendw[:R] if want_weights else None)
 
     def points_projected(self):
-        """The last f32 frame's projected point count and the neighbour indices >= n_points met so far
-        (host sync), or None before any f32 frame."""
+        """The last frame's projected point count and the neighbour indices >= n_points met so far
+        (host sync), or None before any frame (or on the plain-fp32 fallback path only)."""
         if self._fp is None:
             return None
         c, bad = (int(x) for x in self._fp[3].tolist())
